@@ -1,0 +1,56 @@
+# Builds the MI355X scan library, the `speq` CLI and the oracle (test-only) for gfx950.
+#   make            -> speq_amd/libspeq_scan.so, bin/speq, oracle/build/libkmer_oracle.so
+# No cmake/ninja: plain hipcc/gcc lines.
+HIPCC    ?= /opt/rocm/bin/hipcc
+CXX      ?= g++
+CC       ?= gcc
+ARCH     ?= gfx950
+JOBS     ?= 8
+
+INC      := -Iinclude -Ispeq_amd/csrc
+HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -Wall -Wextra -munsafe-fp-atomics $(INC)
+HOSTFLAGS:= -O3 -std=c++17 -fPIC -Wall -Wextra $(INC)
+
+LIB      := speq_amd/libspeq_scan.so
+CLI      := bin/speq
+OBJDIR   := build/obj
+
+LIB_HIP  := speq_amd/csrc/scan_kernels.hip
+LIB_CPP  := speq_amd/csrc/sais.cpp speq_amd/csrc/fm_index.cpp speq_amd/csrc/capi.cpp speq_amd/csrc/comm.cpp \
+            speq_amd/csrc/host_io.cpp
+CLI_CPP  := speq_amd/cli/speq_main.cpp
+
+LIB_OBJS := $(patsubst speq_amd/csrc/%.hip,$(OBJDIR)/%.o,$(LIB_HIP)) \
+            $(patsubst speq_amd/csrc/%.cpp,$(OBJDIR)/%.o,$(LIB_CPP))
+HDRS     := include/speq_scan.h $(wildcard speq_amd/csrc/*.hpp)
+
+all: $(LIB) $(CLI) oracle
+
+$(OBJDIR)/%.o: speq_amd/csrc/%.hip $(HDRS)
+	@mkdir -p $(OBJDIR)
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(OBJDIR)/comm.o: speq_amd/csrc/comm.cpp $(HDRS)
+	@mkdir -p $(OBJDIR)
+	$(CXX) $(HOSTFLAGS) -I/opt/rocm/include -D__HIP_PLATFORM_AMD__ -c $< -o $@
+
+$(OBJDIR)/%.o: speq_amd/csrc/%.cpp $(HDRS)
+	@mkdir -p $(OBJDIR)
+	$(CXX) $(HOSTFLAGS) -c $< -o $@
+
+$(LIB): $(LIB_OBJS)
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $^ -L/opt/rocm/lib -lrccl -lamdhip64 -lpthread \
+	    -Wl,-rpath,/opt/rocm/lib
+
+$(CLI): $(CLI_CPP) $(LIB) $(HDRS) speq_amd/cli/*.hpp
+	@mkdir -p bin
+	$(CXX) $(HOSTFLAGS) -Ispeq_amd/cli -o $@ $(CLI_CPP) -Lspeq_amd -lspeq_scan -Wl,-rpath,'$$ORIGIN/../speq_amd' -lpthread
+
+oracle:
+	$(MAKE) -C oracle
+
+clean:
+	rm -rf build bin $(LIB)
+	$(MAKE) -C oracle clean
+
+.PHONY: all oracle clean

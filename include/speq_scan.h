@@ -1,0 +1,172 @@
+/*
+ * speq_scan.h — C ABI of libspeq_scan.so, the MI355X-native SPeQ scan path.
+ *
+ * This is the drop-in boundary for the reference's hot path.
+ * The reference has no FFI; its seam is the SeqAn3 library call pair
+ *
+ *   seqan3::fm_index{collection}            /root/reference/src/fm_indexer.cpp:36
+ *   search(windows, fm_index, cfg)          /root/reference/src/fm_scanner.cpp:208 (+12 more sites)
+ *
+ * followed by the per-window tally `do_a_count` (fm_scanner.cpp:153-196, :426-471, :665-708, :916-962),
+ * the per-thread reduction (fm_scanner.cpp:224-233 …) and the reference-uniqueness pass
+ * `_async_count_unique_kmers_per_group` (fm_scanner.cpp:1476-1576).  The functions below replace that
+ * seam AND the tally, so per-window hit lists never materialise: the GPU returns the counters directly.
+ *
+ * Conventions
+ *  - Every function returns 0 on success, a negative SPEQ_E_* code on failure; the message of the last
+ *    failure on the calling thread is returned by speq_last_error() (mirrors the reference's exceptions,
+ *    e.g. std::logic_error at fm_scanner.cpp:69, which the C++ CLI re-raises).
+ *  - Plain pointers and sizes only.  "d_" pointers are device (HBM) pointers of the device the handle was
+ *    opened on; "stream" is a hipStream_t passed as void* (NULL = the default stream).
+ *  - An index is immutable after build/load; a device replica may be used concurrently from many host
+ *    threads (the reference copies the index per worker thread, fm_scanner.cpp:145 — we do not need to).
+ *  - Product paths run on the GPU only.  There is no CPU fallback: a call that needs a device fails
+ *    with SPEQ_E_DEVICE when none is present.
+ */
+#ifndef SPEQ_SCAN_H
+#define SPEQ_SCAN_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SPEQ_ABI_VERSION 1
+
+enum {
+    SPEQ_OK = 0,
+    SPEQ_E_ARG = -1,      /* invalid argument (shape, range, null pointer) */
+    SPEQ_E_IO = -2,       /* file could not be read / written / has a bad format */
+    SPEQ_E_DEVICE = -3,   /* no GPU, HIP runtime failure, or kernel launch failure */
+    SPEQ_E_GROUPS = -4,   /* groupings do not cover every reference record */
+    SPEQ_E_NOMEM = -5
+};
+
+/* Scan modes: fm_scanner.cpp:5-32 picks "local" (Phred-weighted) when --fixed-accuracy == 0. */
+enum { SPEQ_MODE_GLOBAL = 0, SPEQ_MODE_LOCAL = 1 };
+
+typedef struct speq_index speq_index;            /* host-side FM-index (immutable) */
+typedef struct speq_device_index speq_device_index; /* replica of an index in one GPU's HBM */
+
+typedef struct {
+    uint32_t prefix_q;   /* length of the q-mer interval lookup table (0 = none, max 13) */
+    uint32_t threads;    /* host threads for the build (0 = all) */
+} speq_build_opts;
+
+/* Per-scan parameters (reference: cmd_arguments in include/arg_parse.h:10-28). */
+typedef struct {
+    uint32_t k;              /* --kmer (reference default 70)                               */
+    uint32_t phred_cutoff;   /* --phred-cutoff; a window passes iff min(Q) > cutoff (:162) */
+    uint32_t paired;         /* 1: records 2i and 2i+1 are mates; ambiguity per pair (:709-729) */
+    uint32_t mode;           /* SPEQ_MODE_GLOBAL (integer U[g]) or SPEQ_MODE_LOCAL (also fp64 W[g]) */
+} speq_scan_params;
+
+/* Counter vector layout (u64): [0] = T (passing windows, fm_scanner.cpp:164),
+ *                              [1] = ambiguous reads/pairs (:183-190, :213),
+ *                              [2 .. 2+G) = U[g] (windows unique to group g, :180).
+ * Local mode additionally fills a fp64 vector W[G] (:454-455). */
+#define SPEQ_COUNTS_LEN(G) ((size_t)(G) + 2u)
+
+/* ---- library ---- */
+const char* speq_last_error(void);
+int speq_abi_version(void);
+/* Number of visible GPUs (0 when none); never fails. */
+int speq_device_count(void);
+
+/* ---- index build / persistence (replaces seqan3::fm_index{…}, fm_indexer.cpp:8-52) ----
+ * seq          : concatenated ASCII sequences of the R reference records (FASTA order)
+ * rec_offsets  : R+1 offsets into seq
+ * group_of_rec : group id of each record (file_to_map's group_scaffolds, file_to_map.cpp:20-119);
+ *                n_group_entries may exceed R (extra entries are ignored like the zip at
+ *                fm_scanner.cpp:1494) but every record r < R must have 0 <= group < n_groups.
+ * The indexed collection is [fwd_0, rc_0, fwd_1, rc_1, …] as built at fm_indexer.cpp:25-33. */
+int speq_index_build(const char* seq, const uint64_t* rec_offsets, uint32_t n_records,
+                     const int32_t* group_of_rec, uint32_t n_group_entries, uint32_t n_groups,
+                     const speq_build_opts* opts, speq_index** out);
+/* user_header: opaque bytes stored in front of the index (the CLI stores the reference's
+ * {ref path, ref mtime, groups mtime, names, group_scaffolds, counts}, fm_indexer.cpp:39-50). */
+int speq_index_save(const speq_index* idx, const char* path, const void* user_header, uint64_t header_len);
+/* Loads an index; *user_header (may be NULL) receives a malloc'ed copy of the stored header that the
+ * caller frees with speq_free(). */
+int speq_index_load(const char* path, speq_index** out, void** user_header, uint64_t* header_len);
+/* Reads only the user header of an index file (for the staleness check at fm_indexer.cpp:68-97). */
+int speq_index_read_header(const char* path, void** user_header, uint64_t* header_len);
+void speq_index_free(speq_index* idx);
+void speq_free(void* p);
+
+typedef struct {
+    uint64_t n;            /* FM text length (all texts + separators + terminator) */
+    uint32_t n_texts;      /* 2R */
+    uint32_t n_records;    /* R */
+    uint32_t n_groups;     /* G */
+    uint32_t prefix_q;
+    uint64_t n_runs;       /* runs of equal group label along the suffix array */
+    uint64_t device_bytes; /* bytes a device replica occupies in HBM */
+} speq_index_info;
+int speq_index_get_info(const speq_index* idx, speq_index_info* info);
+
+/* Read-only views of the host arrays (for tests and tools; layout documented in DESIGN.md §3).
+ * name: "text", "sa", "occ", "occn", "runs", "run_label", "prefix", "C", "text_start", "text_group". */
+int speq_index_array(const speq_index* idx, const char* name, const void** ptr, uint64_t* bytes);
+
+/* ---- device replica ---- */
+int speq_device_open(const speq_index* idx, int device, speq_device_index** out);
+int speq_device_close(speq_device_index* d);
+
+/* ---- the hot path: scan reads already resident in HBM ----
+ * Replaces search() + do_a_count() for every window of every read (fm_scanner.cpp:149-214 and the
+ * paired/local variants).  Counters are ADDED to d_counts (u64[G+2]) and, in local mode, to d_weights
+ * (f64[G]); the caller zeroes them.  d_seq/d_qual: ASCII bases and Phred+33 qualities, d_offsets:
+ * n_reads+1 u64 offsets into both.  With params->paired the records are mate pairs (2i, 2i+1) and
+ * n_reads must be even.  Asynchronous on `stream`. */
+int speq_scan_reads_device(speq_device_index* d, const uint8_t* d_seq, const uint8_t* d_qual,
+                           const uint64_t* d_offsets, uint64_t n_reads, const speq_scan_params* params,
+                           uint64_t* d_counts, double* d_weights, void* stream);
+
+/* Host-buffer convenience used by the CLI: stages the reads to HBM in batches, runs the kernel and
+ * returns the totals (counts: u64[G+2]; weights: f64[G] or NULL). Synchronous. */
+int speq_scan_reads(speq_device_index* d, const uint8_t* seq, const uint8_t* qual, const uint64_t* offsets,
+                    uint64_t n_reads, const speq_scan_params* params, uint64_t* counts, double* weights);
+
+/* ---- reference-uniqueness pass (replaces _async_count_unique_kmers_per_group, fm_scanner.cpp:1476-1576)
+ * For every window of every text (fwd and rc of each record): Tot_ref[g] += 1, and U_ref[g] += 1 iff
+ * every occurrence lies in a text of group g.  Outputs are host arrays of G u64 (overwritten). */
+int speq_ref_unique(speq_device_index* d, uint32_t k, uint64_t* u_ref, uint64_t* tot_ref);
+/* Same on device buffers (added to d_u_ref/d_tot_ref), asynchronous. */
+int speq_ref_unique_device(speq_device_index* d, uint32_t k, uint64_t* d_u_ref, uint64_t* d_tot_ref,
+                           void* stream);
+
+/* ---- multi-GPU: one RCCL all-reduce of the counter vector (replaces the future.get() sums,
+ * fm_scanner.cpp:224-233).  comm is an ncclComm_t created with speq_comm_init. ---- */
+int speq_comm_unique_id(void* id_out /* 128 bytes */);
+int speq_comm_init(int nranks, int rank, const void* id /* 128 bytes */, void** comm_out);
+int speq_comm_destroy(void* comm);
+int speq_allreduce_u64(void* comm, uint64_t* d_buf, uint64_t count, void* stream);
+int speq_allreduce_f64(void* comm, double* d_buf, uint64_t count, void* stream);
+
+/* ---- groupings file (speq::file_to_map, /root/reference/src/file_to_map.cpp:20-119) ----
+ * Same grammar "Name(count): i, j-k, …"; parse errors of single tokens are collected (the reference prints
+ * them to std::cerr) and returned by speq_groupings_errors(). A missing "(count)" fails with SPEQ_E_ARG
+ * (std::invalid_argument from std::stoi at file_to_map.cpp:43). */
+typedef struct speq_groupings speq_groupings;
+int speq_groupings_parse(const char* path, speq_groupings** out);
+uint32_t speq_groupings_n_groups(const speq_groupings* g);
+const char* speq_groupings_name(const speq_groupings* g, uint32_t i);
+int32_t speq_groupings_count(const speq_groupings* g, uint32_t i);
+uint32_t speq_groupings_n_entries(const speq_groupings* g);
+const int32_t* speq_groupings_scaffolds(const speq_groupings* g);
+const char* speq_groupings_errors(const speq_groupings* g);
+void speq_groupings_free(speq_groupings* g);
+
+/* ---- kernel timing (HIP events on the launch stream; bench/roofline support) ----
+ * Returns the summed elapsed milliseconds of the scan kernels launched by speq_scan_reads_device on
+ * this handle since the last reset, and the number of launches.  Enabled by speq_timing_enable(d, 1). */
+int speq_timing_enable(speq_device_index* d, int on);
+int speq_timing_read(speq_device_index* d, double* total_ms, uint64_t* launches);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SPEQ_SCAN_H */

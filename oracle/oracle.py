@@ -1,0 +1,103 @@
+"""ctypes wrapper of the CPU oracle (oracle/build/libkmer_oracle.so). TEST INFRASTRUCTURE ONLY.
+
+Importable by tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg — never by speq_amd/.
+See kmer_oracle.c for what it restates (and "parity unpinned" at the SeqAn3 boundary).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+import time
+from typing import Optional, Sequence
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "build", "libkmer_oracle.so")
+_lib = None
+
+
+def build() -> None:
+    subprocess.run(["make", "-s", "-C", _HERE], check=True)
+
+
+def lib() -> C.CDLL:
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            build()
+        L = C.CDLL(LIB_PATH)
+        P = C.c_void_p
+        U64P = C.POINTER(C.c_uint64)
+        L.oracle_build.restype = P
+        L.oracle_build.argtypes = [C.c_char_p, U64P, C.c_uint32, C.POINTER(C.c_int32), C.c_uint32, C.c_uint32]
+        L.oracle_free.argtypes = [P]
+        L.oracle_lookup_ascii.restype = C.c_int32
+        L.oracle_lookup_ascii.argtypes = [P, C.c_char_p]
+        L.oracle_scan.restype = C.c_int
+        L.oracle_scan.argtypes = [P, C.c_char_p, C.c_char_p, U64P, C.c_uint64, C.c_int, C.c_uint32, C.c_int, U64P,
+                                  C.POINTER(C.c_double), C.c_int]
+        L.oracle_ref_unique.restype = C.c_int
+        L.oracle_ref_unique.argtypes = [P, U64P, U64P]
+        _lib = L
+    return _lib
+
+
+def _u64p(a):
+    return a.ctypes.data_as(C.POINTER(C.c_uint64))
+
+
+class Oracle:
+    """k-mer -> group-label hash map over [fwd_r, rc_r] of every record."""
+
+    def __init__(self, records: Sequence[bytes], groups: Sequence[int], n_groups: int, k: int):
+        bs = [bytes(r) for r in records]
+        off = np.zeros(len(bs) + 1, dtype=np.uint64)
+        off[1:] = np.cumsum([len(b) for b in bs])
+        g = np.asarray(groups, dtype=np.int32)
+        self.k, self.G = k, n_groups
+        self._h = lib().oracle_build(b"".join(bs), _u64p(off), len(bs), g.ctypes.data_as(C.POINTER(C.c_int32)),
+                                     n_groups, k)
+        if not self._h:
+            raise ValueError("oracle_build failed")
+
+    def lookup(self, kmer: bytes) -> int:
+        assert len(kmer) == self.k
+        return int(lib().oracle_lookup_ascii(self._h, kmer))
+
+    def scan(self, seq, qual, offsets, phred_cutoff: int = 30, paired: bool = False, local: bool = False,
+             threads: int = 0):
+        """Returns (T, ambiguous, U[G] u64, W[G] f64 or None)."""
+        seq_b = seq.tobytes() if isinstance(seq, np.ndarray) else bytes(seq)
+        qual_b = qual.tobytes() if isinstance(qual, np.ndarray) else bytes(qual)
+        off = np.ascontiguousarray(offsets, dtype=np.uint64)
+        counts = np.zeros(self.G + 2, dtype=np.uint64)
+        w = np.zeros(self.G, dtype=np.float64) if local else None
+        rc = lib().oracle_scan(self._h, seq_b, qual_b, _u64p(off), len(off) - 1, int(paired), phred_cutoff,
+                               1 if local else 0, _u64p(counts),
+                               w.ctypes.data_as(C.POINTER(C.c_double)) if w is not None else None, threads)
+        if rc != 0:
+            raise ValueError("oracle_scan: bad arguments")
+        return int(counts[0]), int(counts[1]), counts[2:].copy(), w
+
+    def ref_unique(self):
+        u = np.zeros(self.G, dtype=np.uint64)
+        t = np.zeros(self.G, dtype=np.uint64)
+        lib().oracle_ref_unique(self._h, _u64p(u), _u64p(t))
+        return u, t
+
+    def __del__(self):
+        try:
+            if self._h:
+                lib().oracle_free(self._h)
+                self._h = None
+        except Exception:
+            pass
+
+
+def time_scan(oracle: Oracle, seq, qual, offsets, threads: int = 0, min_seconds: float = 0.0):
+    """Times oracle.scan (the CPU baseline leg of bench.py). Returns (seconds, result)."""
+    t0 = time.perf_counter()
+    res = oracle.scan(seq, qual, offsets, threads=threads)
+    return time.perf_counter() - t0, res

@@ -1,0 +1,207 @@
+"""Python host mirror of the SPeQ scan path (thin layer over the C ABI in include/speq_scan.h).
+
+Names follow the reference (``/root/reference``):
+
+* :func:`file_to_map`       — ``speq::file_to_map``                      src/file_to_map.cpp:20-119
+* :class:`FmIndex`          — ``seqan3::fm_index`` built by ``speq::fm::generate_fm_index``
+                              src/fm_indexer.cpp:8-52 (texts [fwd_r, rc_r], :25-33)
+* :meth:`DeviceIndex.scan`  — ``search`` + ``do_a_count`` over all reads  src/fm_scanner.cpp:137-236
+* :meth:`DeviceIndex.count_unique_kmers_per_group`
+                            — ``_async_count_unique_kmers_per_group``     src/fm_scanner.cpp:1476-1576
+* :func:`unique_to_percent` — ``speq::scan::unique_to_percent``          src/fm_scanner.cpp:1455-1474
+
+Every compute call runs on the GPU through libspeq_scan.so; nothing here computes counts on the CPU.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass
+from typing import Optional, Sequence
+
+import numpy as np
+
+from ._lib import (SPEQ_MODE_GLOBAL, SPEQ_MODE_LOCAL, BuildOpts, IndexInfo, ScanParams, SpeqError, check, lib)
+
+__all__ = ["FmIndex", "DeviceIndex", "ScanResult", "Groupings", "file_to_map", "unique_to_percent",
+           "pack_records", "SpeqError", "SPEQ_MODE_GLOBAL", "SPEQ_MODE_LOCAL"]
+
+
+def _u64p(a: np.ndarray):
+    return a.ctypes.data_as(C.POINTER(C.c_uint64))
+
+
+def pack_records(records: Sequence[bytes | str]) -> tuple[bytes, np.ndarray]:
+    """Concatenates sequences into one byte buffer + (n+1) u64 offsets."""
+    bs = [r.encode() if isinstance(r, str) else bytes(r) for r in records]
+    off = np.zeros(len(bs) + 1, dtype=np.uint64)
+    if bs:
+        off[1:] = np.cumsum([len(b) for b in bs], dtype=np.uint64)
+    return b"".join(bs), off
+
+
+@dataclass
+class Groupings:
+    names: list[str]
+    scaffolds: list[int]
+    counts: list[int]
+    errors: str
+
+
+def file_to_map(path: str) -> Groupings:
+    """Parses a genome_groupings file exactly as speq::file_to_map does (file_to_map.cpp:20-119)."""
+    L = lib()
+    h = C.c_void_p()
+    check(L.speq_groupings_parse(path.encode(), C.byref(h)))
+    try:
+        n = L.speq_groupings_n_groups(h)
+        names = [L.speq_groupings_name(h, i).decode() for i in range(n)]
+        counts = [int(L.speq_groupings_count(h, i)) for i in range(n)]
+        m = L.speq_groupings_n_entries(h)
+        p = L.speq_groupings_scaffolds(h)
+        scaff = [int(p[i]) for i in range(m)] if m else []
+        errs = L.speq_groupings_errors(h).decode()
+    finally:
+        L.speq_groupings_free(h)
+    return Groupings(names, scaff, counts, errs)
+
+
+def unique_to_percent(unique_in_reads, total_in_reads, unique_in_refs, total_in_refs) -> list[float]:
+    """P_i = 100 * u_i / T / (U_ref_i / Tot_ref_i) when Tot_ref_i > 0, else 0 (fm_scanner.cpp:1455-1474)."""
+    out = []
+    for u, ur, tr in zip(unique_in_reads, unique_in_refs, total_in_refs):
+        if float(tr) > 0.0:
+            pu = float(ur) / float(tr)
+            with np.errstate(all="ignore"):
+                out.append(float(np.float64(100.0) * np.float64(u) / np.float64(total_in_reads) / np.float64(pu)))
+        else:
+            out.append(0.0)
+    return out
+
+
+class FmIndex:
+    """Immutable FM-index of the grouped reference collection (host side)."""
+
+    def __init__(self, handle: C.c_void_p, header: bytes = b""):
+        self._h = handle
+        self.header = header
+
+    @classmethod
+    def build(cls, records: Sequence[bytes | str], group_of_record: Sequence[int], n_groups: int,
+              prefix_q: int = 0, threads: int = 0) -> "FmIndex":
+        seq, off = pack_records(records)
+        grp = np.asarray(group_of_record, dtype=np.int32)
+        h = C.c_void_p()
+        opts = BuildOpts(prefix_q, threads)
+        check(lib().speq_index_build(seq, _u64p(off), len(records), grp.ctypes.data_as(C.POINTER(C.c_int32)),
+                                     len(grp), n_groups, C.byref(opts), C.byref(h)))
+        return cls(h)
+
+    @classmethod
+    def load(cls, path: str) -> "FmIndex":
+        h, hdr, hl = C.c_void_p(), C.c_void_p(), C.c_uint64()
+        check(lib().speq_index_load(path.encode(), C.byref(h), C.byref(hdr), C.byref(hl)))
+        header = C.string_at(hdr, hl.value) if hl.value else b""
+        lib().speq_free(hdr)
+        return cls(h, header)
+
+    def save(self, path: str, header: bytes = b"") -> None:
+        check(lib().speq_index_save(self._h, path.encode(), header if header else None, len(header)))
+
+    def info(self) -> IndexInfo:
+        info = IndexInfo()
+        check(lib().speq_index_get_info(self._h, C.byref(info)))
+        return info
+
+    def array(self, name: str, dtype) -> np.ndarray:
+        """Copy of a host array of the index (layout: DESIGN.md §3)."""
+        p, nb = C.c_void_p(), C.c_uint64()
+        check(lib().speq_index_array(self._h, name.encode(), C.byref(p), C.byref(nb)))
+        if nb.value == 0:
+            return np.zeros(0, dtype=dtype)
+        return np.frombuffer(C.string_at(p, nb.value), dtype=dtype).copy()
+
+    @property
+    def handle(self):
+        return self._h
+
+    def close(self):
+        if self._h:
+            lib().speq_index_free(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+@dataclass
+class ScanResult:
+    total: int               # T: passing windows
+    ambiguous: int           # reads (or pairs) whose counted windows name >= 2 groups
+    unique: np.ndarray       # U[g] (u64)
+    weights: Optional[np.ndarray]  # W[g] (f64, local mode only)
+
+
+class DeviceIndex:
+    """A replica of an FmIndex in one GPU's HBM."""
+
+    def __init__(self, index: FmIndex, device: int = 0):
+        self.index = index
+        self.n_groups = index.info().n_groups
+        h = C.c_void_p()
+        check(lib().speq_device_open(index.handle, device, C.byref(h)))
+        self._h = h
+
+    @property
+    def handle(self):
+        return self._h
+
+    def scan(self, seq: bytes, qual: bytes, offsets: np.ndarray, k: int, phred_cutoff: int = 30,
+             paired: bool = False, local: bool = False) -> ScanResult:
+        """Scans host reads (staged to HBM in batches)."""
+        off = np.ascontiguousarray(offsets, dtype=np.uint64)
+        n = len(off) - 1
+        G = self.n_groups
+        counts = np.zeros(G + 2, dtype=np.uint64)
+        w = np.zeros(G, dtype=np.float64) if local else None
+        p = ScanParams(k, phred_cutoff, int(paired), SPEQ_MODE_LOCAL if local else SPEQ_MODE_GLOBAL)
+        check(lib().speq_scan_reads(self._h, seq, qual, _u64p(off), n, C.byref(p), _u64p(counts),
+                                    w.ctypes.data_as(C.POINTER(C.c_double)) if w is not None else None))
+        return ScanResult(int(counts[0]), int(counts[1]), counts[2:].copy(), w)
+
+    def scan_device(self, d_seq: int, d_qual: int, d_offsets: int, n_reads: int, k: int, d_counts: int,
+                    d_weights: int = 0, phred_cutoff: int = 30, paired: bool = False, local: bool = False,
+                    stream: int = 0) -> None:
+        """Hot path on HBM-resident buffers (raw device pointers, e.g. torch tensor.data_ptr())."""
+        p = ScanParams(k, phred_cutoff, int(paired), SPEQ_MODE_LOCAL if local else SPEQ_MODE_GLOBAL)
+        check(lib().speq_scan_reads_device(self._h, d_seq, d_qual, d_offsets, n_reads, C.byref(p), d_counts,
+                                           d_weights or None, stream or None))
+
+    def count_unique_kmers_per_group(self, k: int) -> tuple[np.ndarray, np.ndarray]:
+        """(U_ref[G], Tot_ref[G]) of the reference-uniqueness pass."""
+        G = self.n_groups
+        u = np.zeros(G, dtype=np.uint64)
+        t = np.zeros(G, dtype=np.uint64)
+        check(lib().speq_ref_unique(self._h, k, _u64p(u), _u64p(t)))
+        return u, t
+
+    def timing(self, on: bool) -> None:
+        check(lib().speq_timing_enable(self._h, int(on)))
+
+    def timing_read(self) -> tuple[float, int]:
+        ms, n = C.c_double(), C.c_uint64()
+        check(lib().speq_timing_read(self._h, C.byref(ms), C.byref(n)))
+        return ms.value, n.value
+
+    def close(self):
+        if self._h:
+            lib().speq_device_close(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

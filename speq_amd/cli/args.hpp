@@ -1,0 +1,47 @@
+// Command line of `speq [index|scan|all] [options]`.
+// Mirrors speq::args (/root/reference/include/arg_parse.h:10-37, src/arg_parse.cpp:3-203): the same
+// sub-commands, option letters/names and defaults. seqan3::argument_parser is replaced by a small parser.
+#pragma once
+#include <cstdint>
+#include <filesystem>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+namespace speq::args {
+
+struct CmdArguments {  // include/arg_parse.h:10-28
+    std::filesystem::path in_file_reads_path_1{};
+    std::filesystem::path in_file_reads_path_2{};
+    std::filesystem::path in_file_references{};
+    std::filesystem::path in_file_references_groups{};
+    std::filesystem::path io_file_index{"output.idx"};
+    std::filesystem::path out_file_path{"output.txt"};
+    bool is_force{};
+    unsigned int threads{2};
+    unsigned int kmer{70};
+    unsigned int phred_cutoff{30};
+    double fixed_accuracy{0.0};
+    double precision{1e-6};
+    bool is_indexer{false};
+    bool is_scanner{false};
+    bool is_parsed{false};
+    // MI355X build extensions (not in the reference)
+    unsigned int prefix_q{10};   // --prefix-q: q-mer interval table of the FM-index
+    int device{-1};              // --device: GPU ordinal (default: $LOCAL_RANK or 0)
+    unsigned int max_em_iterations{1000};
+};
+
+struct ParseError : std::runtime_error {
+    explicit ParseError(const std::string& m) : std::runtime_error(m) {}
+};
+
+// Parses argv; prints help and returns is_parsed=false for -h/--help; throws ParseError on bad input
+// (the reference prints "speq <sub> | argument parsing error: …", src/arg_parse.cpp:41-45).
+CmdArguments parse(int argc, char** argv);
+
+// src/arg_parse.cpp:167-202
+void check_in_file(std::filesystem::path& p);
+void check_out_file(std::filesystem::path& p, bool is_force);
+
+}  // namespace speq::args

@@ -1,0 +1,473 @@
+// `speq` command line: index | scan | all. Host C++ (reference layers L5/L4/L3) calling the
+// MI355X scan path only through the C ABI of libspeq_scan.so (include/speq_scan.h).
+//
+//   main                        /root/reference/src/main.cpp:15-40
+//   speq::fm::index             /root/reference/src/fm_indexer.cpp:55-111
+//   speq::scan::async_one/two   /root/reference/src/fm_scanner.cpp:5-32 and the four mode variants
+//   .dat cache                  /root/reference/src/fm_scanner.cpp:79-135, :1561-1571
+#include <chrono>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <filesystem>
+#include <fstream>
+#include <iostream>
+#include <memory>
+#include <sstream>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "args.hpp"
+#include "host_io.hpp"
+#include "speq_scan.h"
+
+namespace fs = std::filesystem;
+
+namespace speq::args {
+
+namespace {
+const char* HELP =
+    "speq - Species PErcent Quantifier (MI355X build)\n"
+    "usage: speq [index|scan|all] [options]\n"
+    "  -1, --forward FILE        FASTQ of (forward) reads\n"
+    "  -2, --reverse FILE        FASTQ of reverse mates (paired mode)\n"
+    "  -r, --reference FILE      reference sequences (FASTA)\n"
+    "  -g, --groups FILE         groupings of reference sequences\n"
+    "  -x, --index FILE          index file (default output.idx)\n"
+    "  -o, --output FILE         output file of percentages (default output.txt)\n"
+    "  -f, --force               overwrite existing output files\n"
+    "  -k, --kmer N              k-mer size (default 70)\n"
+    "  -t, --threads N           host threads (default 2)\n"
+    "      --precision-cutoff X  EM convergence threshold (default 1e-6)\n"
+    "      --phred-cutoff N      a window passes iff min(Q) > N (default 30)\n"
+    "      --fixed-accuracy X    fixed per-base accuracy in [0,1]; 0 = Phred-weighted (default)\n"
+    "      --prefix-q N          q-mer lookup table of the FM-index (default 10, 0 = off)\n"
+    "      --device N            GPU ordinal (default $LOCAL_RANK or 0)\n";
+
+template <typename T>
+T to_number(const std::string& opt, const std::string& v) {
+    try {
+        size_t used = 0;
+        if constexpr (std::is_same_v<T, double>) {
+            double x = std::stod(v, &used);
+            if (used != v.size()) throw std::invalid_argument("");
+            return x;
+        } else if constexpr (std::is_same_v<T, int>) {
+            long x = std::stol(v, &used);
+            if (used != v.size()) throw std::invalid_argument("");
+            return (int)x;
+        } else {
+            if (!v.empty() && v[0] == '-') throw std::invalid_argument("");
+            unsigned long x = std::stoul(v, &used);
+            if (used != v.size()) throw std::invalid_argument("");
+            return (T)x;
+        }
+    } catch (const std::exception&) {
+        throw ParseError("Value parse failed for " + opt + ": " + v);
+    }
+}
+}  // namespace
+
+CmdArguments parse(int argc, char** argv) {
+    CmdArguments a;
+    if (argc < 2) throw ParseError("missing sub-command (index, scan or all)");
+    const std::string sub = argv[1];
+    if (sub == "-h" || sub == "--help") {
+        std::cout << HELP;
+        return a;
+    }
+    if (sub == "index") a.is_indexer = true;
+    else if (sub == "scan") a.is_scanner = true;
+    else if (sub == "all") a.is_indexer = a.is_scanner = true;
+    else throw ParseError("You specified an unknown subcommand! Available subcommands are: [index, scan, all]");
+    const bool allow_reads = a.is_scanner, allow_refs = a.is_indexer;
+    for (int i = 2; i < argc; ++i) {
+        std::string opt = argv[i], val;
+        const size_t eq = opt.find('=');
+        bool has_inline = opt.rfind("--", 0) == 0 && eq != std::string::npos;
+        if (has_inline) {
+            val = opt.substr(eq + 1);
+            opt = opt.substr(0, eq);
+        }
+        auto value = [&]() -> std::string {
+            if (has_inline) return val;
+            if (i + 1 >= argc) throw ParseError("Missing value for option " + opt);
+            return argv[++i];
+        };
+        if (opt == "-h" || opt == "--help") { std::cout << HELP; a.is_parsed = false; return a; }
+        else if (opt == "-f" || opt == "--force") a.is_force = true;
+        else if (allow_reads && (opt == "-1" || opt == "--forward")) a.in_file_reads_path_1 = value();
+        else if (allow_reads && (opt == "-2" || opt == "--reverse")) a.in_file_reads_path_2 = value();
+        else if (allow_refs && (opt == "-r" || opt == "--reference")) a.in_file_references = value();
+        else if (allow_refs && (opt == "-g" || opt == "--groups")) a.in_file_references_groups = value();
+        else if (opt == "-x" || opt == "--index") a.io_file_index = value();
+        else if (opt == "-o" || opt == "--output") a.out_file_path = value();
+        else if (allow_reads && (opt == "-k" || opt == "--kmer")) a.kmer = to_number<unsigned>(opt, value());
+        else if (opt == "-t" || opt == "--threads") a.threads = to_number<unsigned>(opt, value());
+        else if (allow_reads && opt == "--precision-cutoff") a.precision = to_number<double>(opt, value());
+        else if (allow_reads && opt == "--phred-cutoff") a.phred_cutoff = to_number<unsigned>(opt, value());
+        else if (allow_reads && opt == "--fixed-accuracy") a.fixed_accuracy = to_number<double>(opt, value());
+        else if (allow_refs && opt == "--prefix-q") a.prefix_q = to_number<unsigned>(opt, value());
+        else if (opt == "--device") a.device = to_number<int>(opt, value());
+        else if (allow_reads && opt == "--max-em-iterations") a.max_em_iterations = to_number<unsigned>(opt, value());
+        else throw ParseError("Unknown option " + opt + ". In case this is meant to be a non-option/argument/parameter, "
+                              "please specify the start of non-options with '--'.");
+    }
+    // validators (src/arg_parse.cpp:33-34, :62-63, :101)
+    if (a.fixed_accuracy < 0.0 || a.fixed_accuracy > 1.0)
+        throw ParseError("Validation failed for option --fixed-accuracy: Value " + std::to_string(a.fixed_accuracy) +
+                         " is not in range [0.000000,1.000000].");
+    const unsigned hw = std::max(2u, std::thread::hardware_concurrency());
+    if (a.threads < 2 || a.threads > hw)
+        throw ParseError("Validation failed for option -t/--threads: Value " + std::to_string(a.threads) +
+                         " is not in range [2," + std::to_string(hw) + "].");
+    if (a.kmer < 1) throw ParseError("Validation failed for option -k/--kmer: must be >= 1");
+    if (a.prefix_q > 13) throw ParseError("Validation failed for option --prefix-q: must be <= 13");
+    if (a.is_scanner) {
+        check_in_file(a.in_file_reads_path_1);
+        check_in_file(a.in_file_reads_path_2);
+        if (a.in_file_reads_path_1.empty()) throw ParseError("Option -1/--forward is required.");
+    }
+    if (a.is_indexer) {
+        check_in_file(a.in_file_references);
+        check_in_file(a.in_file_references_groups);
+        if (a.in_file_references.empty() || a.in_file_references_groups.empty())
+            throw ParseError("Options -r/--reference and -g/--groups are required.");
+    }
+    if (a.is_scanner && !a.is_indexer) {
+        fs::path idx = a.io_file_index;
+        idx.replace_extension(".idx");
+        check_in_file(idx);
+        a.io_file_index = idx;
+    }
+    check_out_file(a.out_file_path, a.is_force);
+    a.is_parsed = true;
+    return a;
+}
+
+void check_in_file(fs::path& p) {
+    if (p.empty()) return;
+    if (p.is_relative()) {
+        if (fs::exists(fs::current_path() / p)) p = fs::current_path() / p;
+        else throw ParseError("Validation failed: The relative-path file " + p.string() + " was not found.");
+    } else if (!fs::exists(p)) {
+        throw ParseError("Validation failed: The full-path file " + p.string() + " was not found.");
+    }
+}
+
+void check_out_file(fs::path& p, bool is_force) {
+    if (p.is_relative()) {
+        p = fs::current_path() / p;
+        if (fs::exists(p) && !is_force)
+            throw ParseError("Validation failed: Cowardly refusing to use an existing output file. Use '-f' to overwrite.");
+    }
+}
+
+}  // namespace speq::args
+
+// ------------------------------------------------------------------------------------------------------------
+namespace {
+
+using speq::args::CmdArguments;
+
+struct CApiError : std::runtime_error {
+    explicit CApiError(const std::string& m) : std::runtime_error(m) {}
+};
+
+void ok(int rc, const char* what) {
+    if (rc != SPEQ_OK) throw CApiError(std::string(what) + ": " + speq_last_error());
+}
+
+int64_t mtime_ns(const fs::path& p) {
+    return (int64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(fs::last_write_time(p).time_since_epoch()).count();
+}
+
+// ---- index header (stored in front of the FM-index; reference: fm_indexer.cpp:39-50) ----
+struct IndexHeader {
+    std::string ref_path;
+    int64_t ref_mtime = 0, groups_mtime = 0;
+    std::vector<std::string> names;
+    std::vector<int32_t> scaffolds;
+    std::vector<int32_t> counts;
+};
+
+void put_u64(std::string& s, uint64_t v) { s.append(reinterpret_cast<const char*>(&v), 8); }
+void put_str(std::string& s, const std::string& v) { put_u64(s, v.size()); s += v; }
+template <typename T>
+void put_vec(std::string& s, const std::vector<T>& v) {
+    put_u64(s, v.size());
+    s.append(reinterpret_cast<const char*>(v.data()), v.size() * sizeof(T));
+}
+
+struct Reader {
+    const uint8_t* p;
+    size_t n, i = 0;
+    void need(size_t k) { if (i + k > n) throw CApiError("corrupt index header"); }
+    uint64_t u64() { need(8); uint64_t v; std::memcpy(&v, p + i, 8); i += 8; return v; }
+    std::string str() { uint64_t l = u64(); need(l); std::string s(reinterpret_cast<const char*>(p + i), l); i += l; return s; }
+    template <typename T>
+    std::vector<T> vec() {
+        uint64_t l = u64();
+        need(l * sizeof(T));
+        std::vector<T> v(l);
+        if (l) std::memcpy(v.data(), p + i, l * sizeof(T));
+        i += l * sizeof(T);
+        return v;
+    }
+};
+
+std::string encode_header(const IndexHeader& h) {
+    std::string s;
+    put_str(s, h.ref_path);
+    put_u64(s, (uint64_t)h.ref_mtime);
+    put_u64(s, (uint64_t)h.groups_mtime);
+    put_u64(s, h.names.size());
+    for (auto& n : h.names) put_str(s, n);
+    put_vec(s, h.scaffolds);
+    put_vec(s, h.counts);
+    return s;
+}
+
+IndexHeader decode_header(const void* data, uint64_t len) {
+    Reader r{static_cast<const uint8_t*>(data), (size_t)len};
+    IndexHeader h;
+    h.ref_path = r.str();
+    h.ref_mtime = (int64_t)r.u64();
+    h.groups_mtime = (int64_t)r.u64();
+    uint64_t ng = r.u64();
+    for (uint64_t i = 0; i < ng; ++i) h.names.push_back(r.str());
+    h.scaffolds = r.vec<int32_t>();
+    h.counts = r.vec<int32_t>();
+    return h;
+}
+
+bool read_index_header(const fs::path& p, IndexHeader& h) {
+    void* data = nullptr;
+    uint64_t len = 0;
+    if (speq_index_read_header(p.c_str(), &data, &len) != SPEQ_OK) return false;
+    try {
+        h = decode_header(data, len);
+    } catch (...) {
+        speq_free(data);
+        return false;
+    }
+    speq_free(data);
+    return true;
+}
+
+// ---- speq index (fm_indexer.cpp:55-111) ----
+void generate_fm_index(const CmdArguments& a, const fs::path& idx_path, const IndexHeader& h) {
+    speq::SeqBatch refs = speq::read_sequences(a.in_file_references.string(), false);
+    if (refs.size() == 0) throw CApiError("no sequences in reference file " + a.in_file_references.string());
+    speq_build_opts opts{a.prefix_q, a.threads};
+    speq_index* idx = nullptr;
+    ok(speq_index_build(refs.seq.data(), refs.offsets.data(), (uint32_t)refs.size(), h.scaffolds.data(),
+                        (uint32_t)h.scaffolds.size(), (uint32_t)h.names.size(), &opts, &idx),
+       "building the FM-index");
+    const std::string hdr = encode_header(h);
+    int rc = speq_index_save(idx, idx_path.c_str(), hdr.data(), hdr.size());
+    speq_index_free(idx);
+    ok(rc, "writing the index");
+}
+
+int run_index(CmdArguments& a) {
+    IndexHeader h;
+    h.ref_path = a.in_file_references.string();
+    h.ref_mtime = mtime_ns(a.in_file_references);
+    h.groups_mtime = mtime_ns(a.in_file_references_groups);
+    std::string perr;
+    speq::Groupings g = speq::parse_groupings(a.in_file_references_groups.string(), &perr);
+    if (!perr.empty()) std::cerr << perr;
+    h.names = g.names;
+    h.scaffolds.assign(g.scaffolds.begin(), g.scaffolds.end());
+    h.counts.assign(g.counts.begin(), g.counts.end());
+    fs::path idx_path = a.io_file_index;
+    idx_path.replace_extension(".idx");  // the reference tests exists() before this (fm_indexer.cpp:68 vs :72)
+    IndexHeader old;
+    if (fs::exists(idx_path) && !a.is_force && read_index_header(idx_path, old) && old.ref_path == h.ref_path &&
+        old.ref_mtime == h.ref_mtime && old.groups_mtime == h.groups_mtime) {
+        a.io_file_index = idx_path;
+        return 0;  // up to date (fm_indexer.cpp:81-85)
+    }
+    generate_fm_index(a, idx_path, h);
+    a.io_file_index = idx_path;
+    return 0;
+}
+
+// ---- .dat cache: cereal binary of {file_time_type idx mtime, vector<size_t> unique, vector<size_t> total} ----
+fs::path dat_path(const fs::path& idx, unsigned k) {
+    fs::path p = idx;
+    p.replace_filename(idx.stem().string() + "_" + std::to_string(k) + "mer.dat");
+    return p;
+}
+
+bool read_dat(const fs::path& p, int64_t idx_mtime, size_t G, std::vector<uint64_t>& u, std::vector<uint64_t>& t) {
+    std::ifstream is(p, std::ios::binary);
+    if (!is) return false;
+    int64_t stamp = 0;
+    uint64_t n1 = 0, n2 = 0;
+    is.read(reinterpret_cast<char*>(&stamp), 8);
+    if (!is || stamp != idx_mtime) return false;
+    is.read(reinterpret_cast<char*>(&n1), 8);
+    if (!is || n1 != G) return false;
+    u.resize(G);
+    is.read(reinterpret_cast<char*>(u.data()), (std::streamsize)(8 * G));
+    is.read(reinterpret_cast<char*>(&n2), 8);
+    if (!is || n2 != G) return false;
+    t.resize(G);
+    is.read(reinterpret_cast<char*>(t.data()), (std::streamsize)(8 * G));
+    return (bool)is;
+}
+
+void write_dat(const fs::path& p, int64_t idx_mtime, const std::vector<uint64_t>& u, const std::vector<uint64_t>& t) {
+    std::ofstream os(p, std::ios::binary | std::ios::trunc);
+    if (!os) throw CApiError("cannot write " + p.string());
+    uint64_t G = u.size();
+    os.write(reinterpret_cast<const char*>(&idx_mtime), 8);
+    os.write(reinterpret_cast<const char*>(&G), 8);
+    os.write(reinterpret_cast<const char*>(u.data()), (std::streamsize)(8 * G));
+    os.write(reinterpret_cast<const char*>(&G), 8);
+    os.write(reinterpret_cast<const char*>(t.data()), (std::streamsize)(8 * G));
+}
+
+// unique_to_percent (fm_scanner.cpp:1455-1474)
+std::vector<double> unique_to_percent(const std::vector<double>& ur, uint64_t total, const std::vector<double>& uref,
+                                      const std::vector<double>& tref) {
+    std::vector<double> out(uref.size(), 0.0);
+    for (size_t i = 0; i < uref.size(); ++i) {
+        if (tref[i] > 0.0) {
+            const double pu = uref[i] / tref[i];
+            out[i] = 100.0 * ur[i] / static_cast<double>(total) / pu;
+        }
+    }
+    return out;
+}
+
+std::vector<double> to_double(const std::vector<uint64_t>& v) { return std::vector<double>(v.begin(), v.end()); }
+
+// ---- speq scan (fm_scanner.cpp:5-32 and the four mode variants) ----
+int run_scan(CmdArguments& a) {
+    fs::path idx_path = a.io_file_index;
+    idx_path.replace_extension(".idx");
+    speq_index* idx = nullptr;
+    void* hdr_data = nullptr;
+    uint64_t hdr_len = 0;
+    ok(speq_index_load(idx_path.c_str(), &idx, &hdr_data, &hdr_len), "loading the index");
+    IndexHeader h = decode_header(hdr_data, hdr_len);
+    speq_free(hdr_data);
+    const size_t G = h.names.size();
+
+    int dev = a.device;
+    if (dev < 0) {
+        const char* lr = std::getenv("LOCAL_RANK");
+        dev = lr ? std::atoi(lr) : 0;
+    }
+    speq_device_index* d = nullptr;
+    ok(speq_device_open(idx, dev, &d), "opening the GPU");
+
+    // Reference uniqueness per group, cached in <stem>_<k>mer.dat keyed by the index mtime.
+    const int64_t idx_mtime = mtime_ns(idx_path);
+    const fs::path dat = dat_path(idx_path, a.kmer);
+    std::vector<uint64_t> u_ref, tot_ref;
+    if (!read_dat(dat, idx_mtime, G, u_ref, tot_ref)) {
+        u_ref.assign(G, 0);
+        tot_ref.assign(G, 0);
+        ok(speq_ref_unique(d, a.kmer, u_ref.data(), tot_ref.data()), "reference-uniqueness pass");
+        write_dat(dat, idx_mtime, u_ref, tot_ref);
+        std::cerr << speq::format_vector(u_ref) << "\n" << speq::format_vector(tot_ref) << "\n";  // :1572-1573
+    }
+
+    const bool paired = !a.in_file_reads_path_2.empty();
+    const bool local = a.fixed_accuracy == 0.0;
+    speq_scan_params prm{a.kmer, a.phred_cutoff, paired ? 1u : 0u, local ? (uint32_t)SPEQ_MODE_LOCAL : (uint32_t)SPEQ_MODE_GLOBAL};
+    std::vector<uint64_t> counts(G + 2, 0), part(G + 2);
+    std::vector<double> weights(G, 0.0), wpart(G);
+    const uint64_t BATCH_RECORDS = 1u << 21, BATCH_BYTES = 512ull << 20;
+    speq::FastqReader r1(a.in_file_reads_path_1.string());
+    std::unique_ptr<speq::FastqReader> r2;
+    if (paired) r2 = std::make_unique<speq::FastqReader>(a.in_file_reads_path_2.string());
+    for (;;) {
+        speq::SeqBatch b1;
+        uint64_t n1 = r1.next(b1, BATCH_RECORDS, BATCH_BYTES);
+        speq::SeqBatch batch;
+        if (paired) {
+            speq::SeqBatch b2;
+            uint64_t n2 = r2->next(b2, n1, ~0ull);
+            if (n2 != n1) throw CApiError("paired read files have different numbers of records");
+            // interleave mates (2i, 2i+1): both mates share one read state (fm_scanner.cpp:709-729)
+            batch.seq.reserve(b1.seq.size() + b2.seq.size());
+            batch.qual.reserve(b1.seq.size() + b2.seq.size());
+            for (uint64_t i = 0; i < n1; ++i) {
+                for (const speq::SeqBatch* b : {&b1, &b2}) {
+                    uint64_t s = b->offsets[i], e = b->offsets[i + 1];
+                    batch.seq.insert(batch.seq.end(), b->seq.begin() + s, b->seq.begin() + e);
+                    batch.qual.insert(batch.qual.end(), b->qual.begin() + s, b->qual.begin() + e);
+                    batch.offsets.push_back(batch.seq.size());
+                }
+            }
+        } else {
+            batch = std::move(b1);
+        }
+        const uint64_t n = batch.size();
+        if (n == 0) break;
+        ok(speq_scan_reads(d, reinterpret_cast<const uint8_t*>(batch.seq.data()),
+                           reinterpret_cast<const uint8_t*>(batch.qual.data()), batch.offsets.data(), n, &prm,
+                           part.data(), local ? wpart.data() : nullptr),
+           "scanning reads");
+        for (size_t i = 0; i < G + 2; ++i) counts[i] += part[i];
+        if (local)
+            for (size_t i = 0; i < G; ++i) weights[i] += wpart[i];
+    }
+    const uint64_t total = counts[0], ambiguous = counts[1];
+    std::vector<double> unique_totals(G, 0.0);
+    if (local) {
+        unique_totals = weights;
+    } else {
+        const double percent_perfect = std::pow(a.fixed_accuracy, (double)a.kmer);  // fm_scanner.cpp:15
+        for (size_t i = 0; i < G; ++i) unique_totals[i] = static_cast<double>(counts[2 + i]) / percent_perfect;
+    }
+    std::vector<double> percent = unique_to_percent(unique_totals, total, to_double(u_ref), to_double(tot_ref));
+
+    // stderr output of the reference (fm_scanner.cpp:245-247, :513-514, :757-759, :1030-1033)
+    std::cerr << speq::format_vector(percent) << "\n";
+    if (!(local && !paired)) std::cerr << speq::format_vector(unique_totals) << "\n";
+    std::cerr << total << "\t" << ambiguous << "\n";
+    if (local && paired) std::cerr << "[({}," << ambiguous << ")]\n";  // fusion map: key always {} (:916)
+
+    // The reference writes nothing to -o (quirk B1); we write the percentage vector there.
+    {
+        std::ofstream of(a.out_file_path);
+        if (!of) throw CApiError("cannot write " + a.out_file_path.string());
+        for (size_t i = 0; i < G; ++i) of << h.names[i] << "\t" << percent[i] << "\n";
+    }
+    speq_device_close(d);
+    speq_index_free(idx);
+    return 1;  // the reference's scan returns 1 (fm_scanner.cpp:280); main ignores it
+}
+
+}  // namespace
+
+int main(int argc, char** argv) {
+    CmdArguments a;
+    try {
+        a = speq::args::parse(argc, argv);
+    } catch (const speq::args::ParseError& e) {
+        std::string sub = argc > 1 ? argv[1] : "";
+        if (sub == "index" || sub == "scan" || sub == "all")
+            std::cerr << "speq " << sub << " | argument parsing error:  " << e.what() << "\n";
+        else
+            std::cerr << "SPeQ Error: " << e.what() << "\n";
+        return 1;
+    }
+    if (!a.is_parsed) return 0;
+    try {
+        if (a.is_indexer) run_index(a);
+        if (a.is_scanner) run_scan(a);
+    } catch (const std::exception& e) {
+        std::cerr << "speq: error: " << e.what() << "\n";
+        return 2;
+    }
+    return 0;
+}

@@ -1,0 +1,89 @@
+// Host-side FM-index of the reference collection, laid out for the HIP scan kernels.
+//
+// Replaces seqan3::fm_index<dna5, collection> built at /root/reference/src/fm_indexer.cpp:36 over the texts
+// [fwd_0, rc_0, fwd_1, rc_1, …] (fm_indexer.cpp:25-33). The layout:
+//
+//   text   : SA alphabet codes, texts separated by SEP and closed by TERM:
+//            T = t_0 SEP t_1 SEP … t_{2R-1} SEP TERM          (TERM=0 < SEP=1 < A=2 < C=3 < G=4 < T=5 < N=6)
+//   occ    : one 64-B block per 96 BWT positions; for each of A,C,G,T a 16-B entry
+//            {u32 rank of that symbol before the block, u32 x3 bitmap of the 96 positions}
+//   occn   : the same 16-B entry for N (only touched by windows that contain N: the .dat pass)
+//   runs   : 16-B entries over the label-change bitvector B[i] = [label(SA[i]) != label(SA[i-1])],
+//            label = group of the text holding suffix SA[i]
+//   run_label : group id of every run (u16)
+//   prefix : for every q-mer over ACGT its SA interval (u32 lo, u32 hi)
+//
+// "All occurrences of a window lie in ONE group" <=> the window's SA interval [lo,hi) holds no label change,
+// i.e. run(lo) == run(hi-1). That replaces SeqAn3's locate of every occurrence.
+#pragma once
+#include <cstdint>
+#include <string>
+#include <vector>
+
+namespace speq {
+
+enum : uint8_t { SYM_TERM = 0, SYM_SEP = 1, SYM_A = 2, SYM_C = 3, SYM_G = 4, SYM_T = 5, SYM_N = 6, SYM_COUNT = 7 };
+constexpr uint32_t OCC_BLOCK = 96;   // BWT positions per occ block
+constexpr uint32_t MAX_PREFIX_Q = 13;
+
+// dna5 conversion of an ASCII base (seqan3 dna5 assign_char: ACGT/acgt, U/u -> T, anything else -> N).
+inline uint8_t ascii_to_sym(unsigned char ch) {
+    switch (ch) {
+        case 'A': case 'a': return SYM_A;
+        case 'C': case 'c': return SYM_C;
+        case 'G': case 'g': return SYM_G;
+        case 'T': case 't': case 'U': case 'u': return SYM_T;
+        default: return SYM_N;
+    }
+}
+inline uint8_t complement_sym(uint8_t s) {
+    switch (s) {
+        case SYM_A: return SYM_T;
+        case SYM_C: return SYM_G;
+        case SYM_G: return SYM_C;
+        case SYM_T: return SYM_A;
+        default: return s;
+    }
+}
+
+struct OccEntry {  // 16 B
+    uint32_t count;
+    uint32_t bits[3];
+};
+
+struct FmIndex {
+    uint64_t n = 0;               // length of text (incl. separators and terminator)
+    uint32_t n_records = 0;
+    uint32_t n_texts = 0;
+    uint32_t n_groups = 0;
+    uint32_t prefix_q = 0;
+    std::vector<uint8_t> text;            // n
+    std::vector<uint64_t> text_start;     // n_texts + 1 (text t occupies [start[t], start[t+1]-1), SEP at start[t+1]-1)
+    std::vector<int32_t> text_group;      // n_texts
+    std::vector<int32_t> group_of_rec;    // as given (length >= n_records)
+    uint32_t C[SYM_COUNT + 1] = {0};      // C[c] = #symbols < c
+    std::vector<OccEntry> occ;            // n_blocks * 4
+    std::vector<OccEntry> occn;           // n_blocks
+    std::vector<OccEntry> runs;           // n_blocks
+    std::vector<uint16_t> run_label;      // n_runs
+    std::vector<uint32_t> prefix;         // 2 * 4^q
+    std::vector<int32_t> sa;              // n (host only, not persisted; empty after load)
+
+    uint64_t n_blocks() const { return n / OCC_BLOCK + 1; }
+    uint64_t device_bytes() const;
+
+    // Host rank used by the builder and by tests: # of symbol `sym` (SYM_A..SYM_N) in BWT[0, i).
+    uint32_t rank(uint8_t sym, uint64_t i) const;
+    uint32_t run_of(uint64_t i) const;   // index of the label run holding SA position i
+};
+
+// Builds the index (throws std::invalid_argument / std::runtime_error).
+void fm_build(FmIndex& idx, const char* seq, const uint64_t* rec_offsets, uint32_t n_records,
+              const int32_t* group_of_rec, uint32_t n_group_entries, uint32_t n_groups, uint32_t prefix_q,
+              uint32_t threads);
+
+void fm_save(const FmIndex& idx, const std::string& path, const void* header, uint64_t header_len);
+void fm_load(FmIndex& idx, const std::string& path, std::vector<uint8_t>* header);
+void fm_read_header(const std::string& path, std::vector<uint8_t>& header);
+
+}  // namespace speq

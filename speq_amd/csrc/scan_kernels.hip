@@ -1,0 +1,669 @@
+// HIP kernels of the SPeQ scan path for gfx950 (MI355X), plus the device half of the C ABI.
+//
+// One kernel template serves the three reference loops that call seqan3::search:
+//   KM_GLOBAL : read scan, integer tallies        /root/reference/src/fm_scanner.cpp:145-216 (paired :662-732)
+//   KM_LOCAL  : read scan, Phred-weighted tallies /root/reference/src/fm_scanner.cpp:418-491 (paired :911-998)
+//   KM_REF    : reference-uniqueness (.dat) pass  /root/reference/src/fm_scanner.cpp:1499-1542
+//
+// Work decomposition: a wavefront owns a contiguous range of units (reads, mate pairs, or a
+// slice of reference windows) and walks the FLATTENED stream of their k-mer windows 64 at a time, one
+// window per lane, so short tails of one read are packed with the head of the next (130 windows per
+// 150-bp read at k=21 would waste a third of the lanes with one-read-per-wave). The bases of those 64
+// windows are staged once into a per-wave LDS buffer as 3-bit symbols + a "bad" bit (Phred <= cutoff or
+// N, fm_scanner.cpp:162). Each lane then runs exact LF-mapping backward search over the window (two
+// 16-byte occ-entry loads per step), classifies the final SA interval with the label-run bitvector, and
+// tallies into an LDS histogram that is flushed with one global atomic per group per workgroup. Read
+// ambiguity (fm_scanner.cpp:183-190, :709-729) is a segmented min/max scan across lanes by unit.
+#include <hip/hip_runtime.h>
+
+#include <climits>
+#include <cmath>
+#include <cstdint>
+#include <cstring>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "capi_internal.hpp"
+#include "fm_index.hpp"
+
+namespace {
+
+constexpr uint32_t WAVES_PER_BLOCK = 4;
+constexpr uint32_t BLOCK_THREADS = 64 * WAVES_PER_BLOCK;
+constexpr uint32_t MAX_K = 4096;
+constexpr uint32_t LDS_HIST_MAX_G = 2048;
+constexpr uint32_t QLUT_LEN = 42;  // phred42 ranks 0..41
+
+enum { KM_GLOBAL = 0, KM_LOCAL = 1, KM_REF = 2 };
+
+struct DevView {
+    const uint4* occ;        // n_blocks * 4 entries {count, bits[3]} for A,C,G,T
+    const uint4* occn;       // n_blocks entries for N
+    const uint4* runs;       // n_blocks entries over the label-change bitvector
+    const uint16_t* run_label;
+    const uint2* prefix;     // 4^q intervals (or null)
+    uint32_t n, q, G, pad;
+    uint32_t c0, c1, c2, c3, c4;  // C[] of A,C,G,T,N
+};
+
+struct UnitSrc {
+    const uint8_t* seq;       // reads: ASCII bases; ref: SA-alphabet text codes
+    const uint8_t* qual;      // reads: Phred+33; ref: null
+    const uint64_t* off;      // unit u spans [off[u], off[u+1] - end_adj)
+    const uint64_t* cum_win;  // ref only: prefix sums of windows per text
+    const int32_t* unit_group;  // ref only: group of each text
+    const double* qlut;       // local only: 1 - 10^(-q/10), q = 0..41
+    uint64_t n_units;         // reads (not pairs) or texts
+    uint64_t total_windows;   // ref only
+    uint32_t end_adj;
+    uint32_t k;
+    uint32_t cutoff;
+    uint32_t buf_bytes;       // per-wave staging buffer
+};
+
+__host__ __device__ inline uint32_t staging_bytes(uint32_t k) { return ((2u * (64u + k)) + 15u) & ~15u; }
+
+__device__ __forceinline__ void wave_sync() {
+    // Lanes of one wave exchange data through their wave-private LDS buffer: order the LDS writes
+    // before the reads of other lanes (workgroup-scope fences emit the lgkmcnt wait).
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+}
+
+__device__ __forceinline__ uint32_t rank_entry(uint4 v, uint32_t r) {  // v.x + #bits set among the first r (0..96)
+    const uint64_t a = (uint64_t)v.y | ((uint64_t)v.z << 32);
+    const uint64_t ma = (r >= 64u) ? ~0ull : ((1ull << r) - 1ull);
+    const uint32_t mb = (r <= 64u) ? 0u : ((r >= 96u) ? ~0u : ((1u << (r - 64u)) - 1u));
+    return v.x + (uint32_t)__popcll(a & ma) + (uint32_t)__popc(v.w & mb);
+}
+
+__device__ __forceinline__ uint32_t lf(const DevView& I, uint32_t c, uint32_t i, uint32_t Cc) {
+    const uint32_t b = i / 96u, r = i - b * 96u;
+    const uint4* p = (c < 4u) ? (I.occ + (size_t)b * 4u + c) : (I.occn + b);
+    return Cc + rank_entry(*p, r);
+}
+
+__device__ __forceinline__ uint32_t run_of(const DevView& I, uint32_t i) {
+    const uint32_t b = i / 96u, r = i - b * 96u;
+    return rank_entry(I.runs[b], r + 1u);
+}
+
+// Exact backward search of the k symbols at w[0..k) (symbols 0..3 = ACGT, 4 = N in the low 3 bits).
+// Returns -1 (no occurrence), -2 (occurrences in >= 2 groups) or the single group id — the outcome of
+// the first-hit rule at fm_scanner.cpp:165-177 when every record is assigned.
+__device__ __forceinline__ int search_classify(const DevView& I, const unsigned char* w, uint32_t k) {
+    uint32_t lo = 0, hi = I.n;
+    int32_t s = (int32_t)k;
+    if (I.q != 0u && k >= I.q) {
+        uint32_t code = 0, bad = 0;
+        for (uint32_t i = k - I.q; i < k; ++i) {
+            const uint32_t c = w[i] & 7u;
+            bad |= c >> 2;
+            code = (code << 2) | (c & 3u);
+        }
+        if (!bad) {
+            const uint2 e = I.prefix[code];
+            lo = e.x;
+            hi = e.y;
+            s -= (int32_t)I.q;
+        }
+    }
+    while (s > 0 && lo < hi) {
+        const uint32_t c = w[s - 1] & 7u;
+        const uint32_t Cc = c == 0u ? I.c0 : c == 1u ? I.c1 : c == 2u ? I.c2 : c == 3u ? I.c3 : I.c4;
+        lo = lf(I, c, lo, Cc);
+        hi = lf(I, c, hi, Cc);
+        --s;
+    }
+    if (lo >= hi) return -1;
+    const uint32_t rl = run_of(I, lo);
+    const uint32_t rh = (hi - lo == 1u) ? rl : run_of(I, hi - 1u);
+    if (rl != rh) return -2;
+    return (int)I.run_label[rl];
+}
+
+__device__ __forceinline__ uint32_t ascii_sym(uint32_t ch) {  // dna5: A C G T/U -> 0..3, else N (4)
+    ch |= 0x20u;
+    return ch == 'a' ? 0u : ch == 'c' ? 1u : ch == 'g' ? 2u : (ch == 't' || ch == 'u') ? 3u : 4u;
+}
+
+template <typename T>
+__device__ __forceinline__ T wave_sum(T v) {
+    for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d);
+    return v;
+}
+
+template <int MODE, bool PAIRED, bool LDS_HIST>
+__global__ __launch_bounds__(BLOCK_THREADS) void k_scan(DevView I, UnitSrc src, unsigned long long* __restrict__ out_a,
+                                                        unsigned long long* __restrict__ out_b,
+                                                        double* __restrict__ out_w) {
+    // out_a: reads -> counts[G+2] (T, ambiguous, U[g]); ref -> U_ref[G]
+    // out_b: ref -> Tot_ref[G];  out_w: local -> W[G]
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const uint32_t lane = threadIdx.x & 63u, wid = threadIdx.x >> 6;
+    const uint32_t G = I.G, k = src.k;
+    const uint32_t hist_words = LDS_HIST ? ((MODE == KM_GLOBAL) ? G : 2u * G) : 0u;
+    const uint32_t hist_bytes = (hist_words * 8u + 15u) & ~15u;
+    unsigned long long* hA = reinterpret_cast<unsigned long long*>(smem);
+    unsigned long long* hB = hA + G;              // KM_REF: Tot_ref
+    double* hW = reinterpret_cast<double*>(hA + G);  // KM_LOCAL: W
+    unsigned char* sbuf = smem + hist_bytes + wid * src.buf_bytes * (MODE == KM_LOCAL ? 2u : 1u);
+    unsigned char* qbuf = sbuf + src.buf_bytes;
+
+    if (LDS_HIST) {
+        for (uint32_t i = threadIdx.x; i < hist_words; i += BLOCK_THREADS) hA[i] = 0ull;
+        __syncthreads();
+    }
+    unsigned long long* gU = (MODE == KM_REF) ? out_a : out_a + 2;
+
+    const uint64_t NW = (uint64_t)gridDim.x * WAVES_PER_BLOCK;
+    const uint64_t gw = (uint64_t)blockIdx.x * WAVES_PER_BLOCK + wid;
+    uint64_t r, r_end, o = 0, remaining;
+    if (MODE == KM_REF) {
+        const uint64_t F0 = src.total_windows * gw / NW, F1 = src.total_windows * (gw + 1) / NW;
+        remaining = F1 - F0;
+        uint64_t lo = 0, hi = src.n_units;  // largest t with cum_win[t] <= F0
+        while (hi - lo > 1) {
+            const uint64_t mid = (lo + hi) >> 1;
+            if (src.cum_win[mid] <= F0) lo = mid; else hi = mid;
+        }
+        r = lo;
+        o = F0 - src.cum_win[lo];
+        r_end = src.n_units;
+    } else {
+        const uint64_t nu = PAIRED ? src.n_units / 2 : src.n_units;
+        const uint64_t u0 = nu * gw / NW, u1 = nu * (gw + 1) / NW;
+        r = PAIRED ? 2 * u0 : u0;
+        r_end = PAIRED ? 2 * u1 : u1;
+        remaining = ~0ull;
+    }
+
+    uint32_t t_cnt = 0;       // passing windows seen by this lane
+    uint32_t amb = 0;         // ambiguous units finished by this wave (wave-uniform)
+    int cmin = INT_MAX, cmax = -1;
+    uint64_t cunit = ~0ull;   // unit whose windows continue past the previous pass
+
+    while (r < r_end && remaining > 0) {
+        // ---- locate this lane's window: the lane-th window after the cursor (r, o)
+        uint64_t rr = r, oo = o + lane, rb = 0;
+        bool has = false;
+        while (rr < r_end) {
+            const uint64_t b = src.off[rr], e = src.off[rr + 1] - src.end_adj;
+            const uint64_t L = e - b;
+            const uint64_t Wr = L >= k ? L - k + 1 : 0;
+            if (oo < Wr) { has = true; rb = b; break; }
+            oo -= Wr;
+            ++rr;
+        }
+        if (!(__ballot(has) & 1ull)) break;  // lane 0 found nothing: range exhausted
+        const uint64_t pos = rb + oo;
+        const uint64_t s0 = __shfl(pos, 0);
+        has = has && (pos + k - s0 <= src.buf_bytes) && ((uint64_t)lane < remaining);
+        const uint64_t taken = __ballot(has);   // a prefix of the lanes (positions are monotone)
+        const uint32_t n_taken = (uint32_t)__popcll(taken);
+        const uint32_t last = n_taken - 1u;
+        const uint64_t pos_last = __shfl(pos, (int)last);
+        const uint32_t span = (uint32_t)(pos_last + k - s0);
+
+        // ---- stage bases [s0, s0 + span) into the wave's LDS buffer
+        for (uint32_t p = lane; p < span; p += 64u) {
+            const uint32_t ch = src.seq[s0 + p];
+            uint32_t sym, bad;
+            if (MODE == KM_REF) {
+                sym = ch - 2u;         // SA alphabet A..N = 2..6
+                bad = ch < 2u ? 1u : 0u;  // separator / terminator
+            } else {
+                sym = ascii_sym(ch);
+                int q = (int)src.qual[s0 + p] - 33;
+                q = q < 0 ? 0 : (q > 41 ? 41 : q);
+                bad = ((uint32_t)q <= src.cutoff || sym == 4u) ? 1u : 0u;
+                if (MODE == KM_LOCAL) qbuf[p] = (unsigned char)q;
+            }
+            sbuf[p] = (unsigned char)(sym | (bad << 3));
+        }
+        wave_sync();
+
+        // ---- search + classify
+        int which = -1;
+        bool valid = false;
+        double wgt = 0.0;
+        if (has) {
+            const unsigned char* w = sbuf + (uint32_t)(pos - s0);
+            uint32_t acc = 0;
+            for (uint32_t i = 0; i < k; ++i) acc |= w[i];
+            valid = !(acc & 8u);
+            if (valid) which = search_classify(I, w, k);
+            if (MODE == KM_LOCAL && valid && which >= 0) {
+                // w = 1.0; for q in window: w = w / (1 - 1/10^(q/10))   (fm_scanner.cpp:454, left to right)
+                const unsigned char* qw = qbuf + (uint32_t)(pos - s0);
+                double x = 1.0;
+                for (uint32_t i = 0; i < k; ++i) x = x / src.qlut[qw[i]];
+                wgt = x;
+            }
+        }
+
+        // ---- tallies
+        if (MODE == KM_REF) {
+            if (has && valid) {
+                const int g = src.unit_group[rr];
+                if (LDS_HIST) {
+                    atomicAdd(&hB[g], 1ull);
+                    if (which == g) atomicAdd(&hA[g], 1ull);
+                } else {
+                    atomicAdd(&out_b[g], 1ull);
+                    if (which == g) atomicAdd(&out_a[g], 1ull);
+                }
+            }
+            remaining -= n_taken;
+        } else {
+            if (valid) {
+                ++t_cnt;
+                if (which >= 0) {
+                    if (LDS_HIST) {
+                        atomicAdd(&hA[which], 1ull);
+                        if (MODE == KM_LOCAL) atomicAdd(&hW[which], wgt);
+                    } else {
+                        atomicAdd(&gU[which], 1ull);
+                        if (MODE == KM_LOCAL) atomicAdd(&out_w[which], wgt);
+                    }
+                }
+            }
+            // Ambiguity: a unit is ambiguous iff its counted windows name >= 2 groups (min != max).
+            const uint64_t unit = PAIRED ? (rr >> 1) : rr;
+            int vmin = (valid && which >= 0) ? which : INT_MAX;
+            int vmax = (valid && which >= 0) ? which : -1;
+            const uint64_t unit0 = __shfl(unit, 0);
+            if (cunit != ~0ull && unit0 != cunit) {  // the carried unit is complete
+                amb += (cmax >= 0 && cmin != cmax) ? 1u : 0u;
+                cunit = ~0ull;
+            }
+            if (lane == 0 && unit == cunit) {
+                vmin = min(vmin, cmin);
+                vmax = max(vmax, cmax);
+            }
+            const uint64_t uprev = __shfl_up(unit, 1);
+            const bool head = has && (lane == 0 || unit != uprev);
+            const uint64_t heads = __ballot(head);
+            const uint64_t below = heads & ((lane == 63u) ? ~0ull : ((2ull << lane) - 1ull));
+            const uint32_t seg_start = 63u - (uint32_t)__clzll(below);
+            for (uint32_t d = 1; d < 64u; d <<= 1) {
+                const int om = __shfl_up(vmin, d), oM = __shfl_up(vmax, d);
+                if (lane >= d && lane - d >= seg_start) {
+                    vmin = min(vmin, om);
+                    vmax = max(vmax, oM);
+                }
+            }
+            const bool tail = has && (lane == last || ((heads >> (lane + 1u)) & 1ull));
+            const bool amb_lane = tail && lane != last && vmax >= 0 && vmin != vmax;
+            amb += (uint32_t)__popcll(__ballot(amb_lane));
+            cmin = __shfl(vmin, (int)last);
+            cmax = __shfl(vmax, (int)last);
+            cunit = __shfl(unit, (int)last);
+        }
+        wave_sync();
+        // ---- advance the cursor past the last window taken
+        r = __shfl(rr, (int)last);
+        o = __shfl(oo, (int)last) + 1;
+    }
+
+    if (MODE != KM_REF) {
+        if (cunit != ~0ull) amb += (cmax >= 0 && cmin != cmax) ? 1u : 0u;
+        const unsigned long long tsum = wave_sum<unsigned long long>((unsigned long long)t_cnt);
+        if (lane == 0) {
+            if (tsum) atomicAdd(&out_a[0], tsum);
+            if (amb) atomicAdd(&out_a[1], (unsigned long long)amb);
+        }
+    }
+    if (LDS_HIST) {
+        __syncthreads();
+        for (uint32_t g = threadIdx.x; g < G; g += BLOCK_THREADS) {
+            const unsigned long long a = hA[g];
+            if (a) atomicAdd(&gU[g], a);
+            if (MODE == KM_REF) {
+                const unsigned long long b = hB[g];
+                if (b) atomicAdd(&out_b[g], b);
+            }
+            if (MODE == KM_LOCAL) {
+                const double x = hW[g];
+                if (x != 0.0) atomicAdd(&out_w[g], x);
+            }
+        }
+    }
+}
+
+#define HIP_OK(expr)                                                                                         \
+    do {                                                                                                     \
+        hipError_t _e = (expr);                                                                              \
+        if (_e != hipSuccess)                                                                                \
+            throw speq::DeviceError(std::string(#expr) + ": " + hipGetErrorString(_e));                      \
+    } while (0)
+
+template <typename T>
+T* dev_upload(const std::vector<T>& v) {
+    if (v.empty()) return nullptr;
+    void* p = nullptr;
+    HIP_OK(hipMalloc(&p, v.size() * sizeof(T)));
+    HIP_OK(hipMemcpy(p, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice));
+    return static_cast<T*>(p);
+}
+
+}  // namespace
+
+struct speq_device_index {
+    int device = 0;
+    DevView view{};
+    std::vector<void*> allocs;
+    uint8_t* d_text = nullptr;
+    uint64_t* d_text_start = nullptr;
+    int32_t* d_text_group = nullptr;
+    double* d_qlut = nullptr;
+    std::vector<uint64_t> text_start;  // host copy (ref pass window sums)
+    uint32_t n_texts = 0;
+    uint32_t G = 0;
+    hipStream_t stream = nullptr;
+    bool timing = false;
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> events;
+    double timed_ms = 0.0;
+    uint64_t timed_launches = 0;
+};
+
+namespace {
+
+struct DeviceGuard {
+    int prev = -1;
+    explicit DeviceGuard(int dev) {
+        HIP_OK(hipGetDevice(&prev));
+        if (prev != dev) HIP_OK(hipSetDevice(dev));
+    }
+    ~DeviceGuard() {
+        int cur = -1;
+        if (hipGetDevice(&cur) == hipSuccess && cur != prev && prev >= 0) (void)hipSetDevice(prev);
+    }
+};
+
+template <int MODE, bool PAIRED, bool LDS>
+void launch_t(const speq_device_index* d, const UnitSrc& src, uint32_t grid, size_t lds, hipStream_t st,
+              unsigned long long* a, unsigned long long* b, double* w) {
+    hipLaunchKernelGGL((k_scan<MODE, PAIRED, LDS>), dim3(grid), dim3(BLOCK_THREADS), lds, st, d->view, src, a, b, w);
+}
+
+void launch_scan(const speq_device_index* d, int mode, bool paired, const UnitSrc& src, uint64_t work_units,
+                 hipStream_t st, unsigned long long* a, unsigned long long* b, double* w) {
+    const bool lds_hist = d->G <= LDS_HIST_MAX_G;
+    const uint32_t hist_words = lds_hist ? ((mode == KM_GLOBAL) ? d->G : 2u * d->G) : 0u;
+    const size_t lds = ((hist_words * 8u + 15u) & ~15u) +
+                       (size_t)WAVES_PER_BLOCK * src.buf_bytes * (mode == KM_LOCAL ? 2u : 1u);
+    // >= 4 units (or 256 windows) per wave; at most 8 resident 256-thread blocks on each of the 256 CUs, x2.
+    uint64_t blocks = (work_units + 4 * WAVES_PER_BLOCK - 1) / (4 * WAVES_PER_BLOCK);
+    if (blocks < 1) blocks = 1;
+    if (blocks > 4096) blocks = 4096;
+    const uint32_t grid = (uint32_t)blocks;
+#define SPEQ_DISPATCH(M, P)                                                        \
+    do {                                                                           \
+        if (lds_hist) launch_t<M, P, true>(d, src, grid, lds, st, a, b, w);       \
+        else launch_t<M, P, false>(d, src, grid, lds, st, a, b, w);               \
+    } while (0)
+    if (mode == KM_REF) SPEQ_DISPATCH(KM_REF, false);
+    else if (mode == KM_GLOBAL) { if (paired) SPEQ_DISPATCH(KM_GLOBAL, true); else SPEQ_DISPATCH(KM_GLOBAL, false); }
+    else { if (paired) SPEQ_DISPATCH(KM_LOCAL, true); else SPEQ_DISPATCH(KM_LOCAL, false); }
+#undef SPEQ_DISPATCH
+    HIP_OK(hipGetLastError());
+}
+
+}  // namespace
+
+extern "C" {
+
+int speq_device_count(void) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+}
+
+int speq_device_open(const speq_index* idx, int device, speq_device_index** out) {
+    return speq::guarded([&] {
+        if (!idx || !out) throw std::invalid_argument("speq_device_open: null argument");
+        int ndev = speq_device_count();
+        if (ndev <= 0) throw speq::DeviceError("no GPU visible (the scan path has no CPU fallback)");
+        if (device < 0 || device >= ndev) throw std::invalid_argument("speq_device_open: bad device ordinal");
+        DeviceGuard g(device);
+        const speq::FmIndex& fm = idx->fm;
+        auto d = std::make_unique<speq_device_index>();
+        d->device = device;
+        d->G = fm.n_groups;
+        d->n_texts = fm.n_texts;
+        d->text_start = fm.text_start;
+        DevView& v = d->view;
+        v.occ = reinterpret_cast<const uint4*>(dev_upload(fm.occ));
+        v.occn = reinterpret_cast<const uint4*>(dev_upload(fm.occn));
+        v.runs = reinterpret_cast<const uint4*>(dev_upload(fm.runs));
+        v.run_label = dev_upload(fm.run_label);
+        v.prefix = reinterpret_cast<const uint2*>(dev_upload(fm.prefix));
+        v.n = (uint32_t)fm.n;
+        v.q = fm.prefix_q;
+        v.G = fm.n_groups;
+        v.c0 = fm.C[speq::SYM_A];
+        v.c1 = fm.C[speq::SYM_C];
+        v.c2 = fm.C[speq::SYM_G];
+        v.c3 = fm.C[speq::SYM_T];
+        v.c4 = fm.C[speq::SYM_N];
+        d->allocs = {(void*)v.occ, (void*)v.occn, (void*)v.runs, (void*)v.run_label, (void*)v.prefix};
+        d->d_text = dev_upload(fm.text);
+        d->d_text_start = dev_upload(fm.text_start);
+        d->d_text_group = dev_upload(fm.text_group);
+        std::vector<double> lut(QLUT_LEN);
+        for (uint32_t q = 0; q < QLUT_LEN; ++q) lut[q] = 1.0 - 1.0 / std::pow(10.0, (double)q / 10.0);
+        d->d_qlut = dev_upload(lut);
+        d->allocs.push_back(d->d_text);
+        d->allocs.push_back(d->d_text_start);
+        d->allocs.push_back(d->d_text_group);
+        d->allocs.push_back(d->d_qlut);
+        HIP_OK(hipStreamCreateWithFlags(&d->stream, hipStreamNonBlocking));
+        *out = d.release();
+    });
+}
+
+int speq_device_close(speq_device_index* d) {
+    return speq::guarded([&] {
+        if (!d) return;
+        DeviceGuard g(d->device);
+        for (auto& e : d->events) {
+            (void)hipEventDestroy(e.first);
+            (void)hipEventDestroy(e.second);
+        }
+        for (void* p : d->allocs)
+            if (p) (void)hipFree(p);
+        if (d->stream) (void)hipStreamDestroy(d->stream);
+        delete d;
+    });
+}
+
+int speq_scan_reads_device(speq_device_index* d, const uint8_t* d_seq, const uint8_t* d_qual,
+                           const uint64_t* d_offsets, uint64_t n_reads, const speq_scan_params* p,
+                           uint64_t* d_counts, double* d_weights, void* stream) {
+    return speq::guarded([&] {
+        if (!d || !p || !d_counts) throw std::invalid_argument("speq_scan_reads_device: null argument");
+        if (p->k < 1 || p->k > MAX_K) throw std::invalid_argument("speq_scan_reads_device: k must be in [1, 4096]");
+        if (p->mode != SPEQ_MODE_GLOBAL && p->mode != SPEQ_MODE_LOCAL)
+            throw std::invalid_argument("speq_scan_reads_device: bad mode");
+        if (p->mode == SPEQ_MODE_LOCAL && !d_weights)
+            throw std::invalid_argument("speq_scan_reads_device: local mode needs a weights buffer");
+        if (p->paired && (n_reads & 1)) throw std::invalid_argument("speq_scan_reads_device: paired scan needs an even record count");
+        if (n_reads == 0) return;
+        if (!d_seq || !d_qual || !d_offsets) throw std::invalid_argument("speq_scan_reads_device: null read buffer");
+        DeviceGuard g(d->device);
+        hipStream_t st = stream ? static_cast<hipStream_t>(stream) : d->stream;
+        UnitSrc src{};
+        src.seq = d_seq;
+        src.qual = d_qual;
+        src.off = d_offsets;
+        src.qlut = d->d_qlut;
+        src.n_units = n_reads;
+        src.end_adj = 0;
+        src.k = p->k;
+        src.cutoff = p->phred_cutoff;
+        src.buf_bytes = staging_bytes(p->k);
+        const int mode = p->mode == SPEQ_MODE_LOCAL ? KM_LOCAL : KM_GLOBAL;
+        hipEvent_t e0 = nullptr, e1 = nullptr;
+        if (d->timing) {
+            HIP_OK(hipEventCreate(&e0));
+            HIP_OK(hipEventCreate(&e1));
+            HIP_OK(hipEventRecord(e0, st));
+        }
+        launch_scan(d, mode, p->paired != 0, src, p->paired ? n_reads / 2 : n_reads, st,
+                    reinterpret_cast<unsigned long long*>(d_counts), nullptr, d_weights);
+        if (d->timing) {
+            HIP_OK(hipEventRecord(e1, st));
+            d->events.emplace_back(e0, e1);
+        }
+    });
+}
+
+int speq_scan_reads(speq_device_index* d, const uint8_t* seq, const uint8_t* qual, const uint64_t* offsets,
+                    uint64_t n_reads, const speq_scan_params* p, uint64_t* counts, double* weights) {
+    return speq::guarded([&] {
+        if (!d || !p || !counts || (!offsets && n_reads)) throw std::invalid_argument("speq_scan_reads: null argument");
+        if (p->mode == SPEQ_MODE_LOCAL && !weights) throw std::invalid_argument("speq_scan_reads: local mode needs weights");
+        if (p->paired && (n_reads & 1)) throw std::invalid_argument("speq_scan_reads: paired scan needs an even record count");
+        const uint32_t G = d->G;
+        std::fill(counts, counts + SPEQ_COUNTS_LEN(G), 0ull);
+        if (weights) std::fill(weights, weights + G, 0.0);
+        if (n_reads == 0) return;
+        for (uint64_t i = 0; i < n_reads; ++i)
+            if (offsets[i + 1] < offsets[i]) throw std::invalid_argument("speq_scan_reads: offsets must be non-decreasing");
+        DeviceGuard g(d->device);
+        hipStream_t st = d->stream;
+        // Batches [r0, r1) of whole units holding at most BATCH_BYTES of bases (or a single larger unit).
+        const uint64_t BATCH_BYTES = 256ull << 20;
+        const uint64_t step = p->paired ? 2 : 1;
+        std::vector<std::pair<uint64_t, uint64_t>> batches;
+        uint64_t max_bytes = 1, max_reads = 1;
+        for (uint64_t r0 = 0; r0 < n_reads;) {
+            uint64_t r1 = r0 + step;
+            while (r1 < n_reads && offsets[r1 + step] - offsets[r0] <= BATCH_BYTES) r1 += step;
+            batches.emplace_back(r0, r1);
+            max_bytes = std::max(max_bytes, offsets[r1] - offsets[r0]);
+            max_reads = std::max(max_reads, r1 - r0);
+            r0 = r1;
+        }
+        struct Free {
+            std::vector<void*> p;
+            ~Free() { for (void* x : p) if (x) (void)hipFree(x); }
+        } fr;
+        auto alloc = [&](size_t bytes) {
+            void* x = nullptr;
+            HIP_OK(hipMalloc(&x, bytes));
+            fr.p.push_back(x);
+            return x;
+        };
+        auto* d_counts = static_cast<uint64_t*>(alloc(SPEQ_COUNTS_LEN(G) * 8));
+        double* d_w = p->mode == SPEQ_MODE_LOCAL ? static_cast<double*>(alloc(G * 8)) : nullptr;
+        auto* d_seq = static_cast<uint8_t*>(alloc(max_bytes));
+        auto* d_qual = static_cast<uint8_t*>(alloc(max_bytes));
+        auto* d_off = static_cast<uint64_t*>(alloc((max_reads + 1) * 8));
+        HIP_OK(hipMemsetAsync(d_counts, 0, SPEQ_COUNTS_LEN(G) * 8, st));
+        if (d_w) HIP_OK(hipMemsetAsync(d_w, 0, G * 8, st));
+        std::vector<uint64_t> rel;
+        for (const auto& bt : batches) {
+            const uint64_t r0 = bt.first, r1 = bt.second;
+            const uint64_t nb = offsets[r1] - offsets[r0], nr = r1 - r0;
+            rel.resize(nr + 1);
+            for (uint64_t i = 0; i <= nr; ++i) rel[i] = offsets[r0 + i] - offsets[r0];
+            if (nb) {
+                HIP_OK(hipMemcpyAsync(d_seq, seq + offsets[r0], nb, hipMemcpyHostToDevice, st));
+                HIP_OK(hipMemcpyAsync(d_qual, qual + offsets[r0], nb, hipMemcpyHostToDevice, st));
+            }
+            HIP_OK(hipMemcpyAsync(d_off, rel.data(), (nr + 1) * 8, hipMemcpyHostToDevice, st));
+            if (speq_scan_reads_device(d, d_seq, d_qual, d_off, nr, p, d_counts, d_w, st) != SPEQ_OK)
+                throw speq::DeviceError(speq_last_error());
+            HIP_OK(hipStreamSynchronize(st));  // `rel` and the device staging buffers are reused next batch
+        }
+        HIP_OK(hipMemcpyAsync(counts, d_counts, SPEQ_COUNTS_LEN(G) * 8, hipMemcpyDeviceToHost, st));
+        if (d_w) HIP_OK(hipMemcpyAsync(weights, d_w, G * 8, hipMemcpyDeviceToHost, st));
+        HIP_OK(hipStreamSynchronize(st));
+    });
+}
+
+int speq_ref_unique_device(speq_device_index* d, uint32_t k, uint64_t* d_u_ref, uint64_t* d_tot_ref, void* stream) {
+    return speq::guarded([&] {
+        if (!d || !d_u_ref || !d_tot_ref) throw std::invalid_argument("speq_ref_unique_device: null argument");
+        if (k < 1 || k > MAX_K) throw std::invalid_argument("speq_ref_unique_device: k must be in [1, 4096]");
+        DeviceGuard g(d->device);
+        hipStream_t st = stream ? static_cast<hipStream_t>(stream) : d->stream;
+        std::vector<uint64_t> cum(d->n_texts + 1, 0);
+        for (uint32_t t = 0; t < d->n_texts; ++t) {
+            const uint64_t L = d->text_start[t + 1] - d->text_start[t] - 1;  // minus separator
+            cum[t + 1] = cum[t] + (L >= k ? L - k + 1 : 0);
+        }
+        const uint64_t total = cum[d->n_texts];
+        if (total == 0) return;
+        uint64_t* d_cum = nullptr;
+        HIP_OK(hipMalloc(&d_cum, cum.size() * 8));
+        HIP_OK(hipMemcpyAsync(d_cum, cum.data(), cum.size() * 8, hipMemcpyHostToDevice, st));
+        UnitSrc src{};
+        src.seq = d->d_text;
+        src.off = d->d_text_start;
+        src.cum_win = d_cum;
+        src.unit_group = d->d_text_group;
+        src.n_units = d->n_texts;
+        src.total_windows = total;
+        src.end_adj = 1;
+        src.k = k;
+        src.buf_bytes = staging_bytes(k);
+        launch_scan(d, KM_REF, false, src, (total + 255) / 256, st, reinterpret_cast<unsigned long long*>(d_u_ref),
+                    reinterpret_cast<unsigned long long*>(d_tot_ref), nullptr);
+        HIP_OK(hipStreamSynchronize(st));  // d_cum is freed below
+        HIP_OK(hipFree(d_cum));
+    });
+}
+
+int speq_ref_unique(speq_device_index* d, uint32_t k, uint64_t* u_ref, uint64_t* tot_ref) {
+    return speq::guarded([&] {
+        if (!d || !u_ref || !tot_ref) throw std::invalid_argument("speq_ref_unique: null argument");
+        DeviceGuard g(d->device);
+        const uint32_t G = d->G;
+        uint64_t* buf = nullptr;
+        HIP_OK(hipMalloc(&buf, 2ull * G * 8));
+        HIP_OK(hipMemsetAsync(buf, 0, 2ull * G * 8, d->stream));
+        int rc = speq_ref_unique_device(d, k, buf, buf + G, d->stream);
+        if (rc != SPEQ_OK) {
+            std::string msg = speq_last_error();
+            (void)hipFree(buf);
+            throw speq::DeviceError(msg);
+        }
+        HIP_OK(hipMemcpyAsync(u_ref, buf, G * 8, hipMemcpyDeviceToHost, d->stream));
+        HIP_OK(hipMemcpyAsync(tot_ref, buf + G, G * 8, hipMemcpyDeviceToHost, d->stream));
+        HIP_OK(hipStreamSynchronize(d->stream));
+        HIP_OK(hipFree(buf));
+    });
+}
+
+int speq_timing_enable(speq_device_index* d, int on) {
+    return speq::guarded([&] {
+        if (!d) throw std::invalid_argument("speq_timing_enable: null handle");
+        d->timing = on != 0;
+    });
+}
+
+int speq_timing_read(speq_device_index* d, double* total_ms, uint64_t* launches) {
+    return speq::guarded([&] {
+        if (!d || !total_ms || !launches) throw std::invalid_argument("speq_timing_read: null argument");
+        DeviceGuard g(d->device);
+        double ms = 0.0;
+        for (auto& e : d->events) {
+            HIP_OK(hipEventSynchronize(e.second));
+            float t = 0.f;
+            HIP_OK(hipEventElapsedTime(&t, e.first, e.second));
+            ms += t;
+            (void)hipEventDestroy(e.first);
+            (void)hipEventDestroy(e.second);
+        }
+        *total_ms = ms;
+        *launches = d->events.size();
+        d->events.clear();
+    });
+}
+
+}  // extern "C"

@@ -1,0 +1,98 @@
+"""Test helper: vectorised numpy backward search over the HOST arrays of an FmIndex.
+
+Used only by the CPU tests to check the index layout (occ/runs/prefix) against the oracle without a
+GPU. It reads the arrays through the C ABI accessor ``speq_index_array``; it is not part of the product path.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+SYM = {ord("A"): 0, ord("C"): 1, ord("G"): 2, ord("T"): 3}
+BLOCK = 96
+
+
+def _popc32(x: np.ndarray) -> np.ndarray:
+    return np.bitwise_count(x.astype(np.uint32)).astype(np.int64)
+
+
+def entry_rank(entries: np.ndarray, idx: np.ndarray, r: np.ndarray) -> np.ndarray:
+    """entries: (m, 4) u32 {count, bits0, bits1, bits2}; rank = count + popcount of the first r bits (0..96)."""
+    e = entries[idx]
+    out = e[:, 0].astype(np.int64)
+    for w in range(3):
+        lo = 32 * w
+        full = r >= lo + 32
+        part = (r > lo) & ~full
+        bits = e[:, 1 + w].astype(np.uint64)
+        sh = np.clip(r - lo, 0, 31).astype(np.uint64)
+        mask = ((np.uint64(1) << sh) - np.uint64(1)).astype(np.uint64)
+        out += np.where(full, _popc32(bits), 0) + np.where(part, _popc32(bits & mask), 0)
+    return out
+
+
+class NumpyFm:
+    def __init__(self, index):
+        self.occ = index.array("occ", np.uint32).reshape(-1, 4)       # (nb*4, 4)
+        self.occn = index.array("occn", np.uint32).reshape(-1, 4)
+        self.runs = index.array("runs", np.uint32).reshape(-1, 4)
+        self.run_label = index.array("run_label", np.uint16)
+        self.C = index.array("C", np.uint32).astype(np.int64)
+        self.n = int(index.info().n)
+        self.q = int(index.info().prefix_q)
+        self.prefix = index.array("prefix", np.uint32).reshape(-1, 2) if self.q else None
+
+    def rank(self, sym: np.ndarray, i: np.ndarray) -> np.ndarray:
+        """sym: 0..3 ACGT, 4 N."""
+        b, r = i // BLOCK, i % BLOCK
+        out = np.empty(len(i), dtype=np.int64)
+        acgt = sym < 4
+        if acgt.any():
+            out[acgt] = entry_rank(self.occ, b[acgt] * 4 + sym[acgt], r[acgt])
+        if (~acgt).any():
+            out[~acgt] = entry_rank(self.occn, b[~acgt], r[~acgt])
+        return out
+
+    def run_of(self, i: np.ndarray) -> np.ndarray:
+        return entry_rank(self.runs, i // BLOCK, i % BLOCK + 1)
+
+    def classify(self, kmers: np.ndarray, use_prefix: bool = True) -> np.ndarray:
+        """kmers: (m, k) symbols 0..4. Returns -1 / -2 / group per row (same contract as the kernel)."""
+        m, k = kmers.shape
+        lo = np.zeros(m, dtype=np.int64)
+        hi = np.full(m, self.n, dtype=np.int64)
+        start = k
+        if use_prefix and self.q and k >= self.q:
+            tail = kmers[:, k - self.q:]
+            okq = (tail < 4).all(axis=1)
+            code = np.zeros(m, dtype=np.int64)
+            for j in range(self.q):
+                code = code * 4 + (tail[:, j] & 3)
+            lo = np.where(okq, self.prefix[code, 0].astype(np.int64), lo)
+            hi = np.where(okq, self.prefix[code, 1].astype(np.int64), hi)
+            steps = np.where(okq, k - self.q, k)
+        else:
+            steps = np.full(m, k)
+        for s in range(start, 0, -1):
+            act = (s <= steps) & (lo < hi)
+            if not act.any():
+                continue
+            c = kmers[act, s - 1].astype(np.int64)
+            Cc = self.C[c + 2]
+            lo[act] = Cc + self.rank(c, lo[act])
+            hi[act] = Cc + self.rank(c, hi[act])
+        out = np.full(m, -1, dtype=np.int64)
+        hit = lo < hi
+        if hit.any():
+            rl = self.run_of(lo[hit])
+            rh = self.run_of(hi[hit] - 1)
+            out[hit] = np.where(rl == rh, self.run_label[rl].astype(np.int64), -2)
+        return out
+
+
+def ascii_to_syms(b: bytes | np.ndarray) -> np.ndarray:
+    a = np.frombuffer(bytes(b), dtype=np.uint8) if not isinstance(b, np.ndarray) else b
+    lut = np.full(256, 4, dtype=np.int64)
+    for ch, v in ((b"A", 0), (b"C", 1), (b"G", 2), (b"T", 3), (b"U", 3)):
+        lut[ch[0]] = v
+        lut[ch.lower()[0]] = v
+    return lut[a]

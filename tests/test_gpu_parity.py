@@ -1,0 +1,179 @@
+"""GPU parity: the HIP scan path (through the C ABI) against the CPU oracle on the same seeded inputs.
+
+Integer counters (T, ambiguous, U[g], U_ref[g], Tot_ref[g]) must be bit-exact. Phred-weighted W[g] is fp64: per
+window it is computed with the same left-to-right divisions as the reference (fm_scanner.cpp:454), but windows
+are summed in a different order, so W is compared with rtol = 1e-12.
+"""
+import numpy as np
+import pytest
+
+from oracle.oracle import Oracle
+from speq_amd import DeviceIndex, FmIndex, synth
+
+pytestmark = pytest.mark.gpu
+W_RTOL = 1e-12
+
+
+def _check(dev, orc, reads, k, cutoff=30, paired=False, local=False):
+    got = dev.scan(reads.seq.tobytes(), reads.qual.tobytes(), reads.offsets, k=k, phred_cutoff=cutoff,
+                   paired=paired, local=local)
+    T, amb, U, W = orc.scan(reads.seq, reads.qual, reads.offsets, phred_cutoff=cutoff, paired=paired, local=local)
+    assert got.total == T
+    assert got.ambiguous == amb
+    assert np.array_equal(got.unique, U), (got.unique, U)
+    if local:
+        np.testing.assert_allclose(got.weights, W, rtol=W_RTOL, atol=0)
+    return got
+
+
+@pytest.fixture(scope="module")
+def cfg1():
+    ref = synth.make_reference(3, 1, 10_000)
+    reads = synth.make_reads(ref, 10_000)
+    return ref, reads
+
+
+@pytest.mark.parametrize("q", [0, 10])
+@pytest.mark.parametrize("local", [False, True])
+def test_config1_single(cfg1, q, local):
+    ref, reads = cfg1
+    idx = FmIndex.build(ref.records, ref.groups, 3, prefix_q=q)
+    dev = DeviceIndex(idx)
+    orc = Oracle(ref.records, ref.groups, 3, 21)
+    got = _check(dev, orc, reads, 21, local=local)
+    assert got.total == 10_000 * 130  # all-Q40, no N: every window passes
+    u, t = dev.count_unique_kmers_per_group(21)
+    ou, ot = orc.ref_unique()
+    assert np.array_equal(u, ou) and np.array_equal(t, ot)
+
+
+@pytest.fixture(scope="module")
+def edge():
+    ref = synth.make_reference(4, 2, 3_000, ref_n_rate=0.003)
+    reads = synth.make_reads(ref, 3_000, n_rate=0.005, lowq_rate=0.02, short_frac=0.05)
+    return ref, reads
+
+
+@pytest.mark.parametrize("k", [1, 2, 5, 16, 21, 31, 32, 33, 70, 150, 151])
+def test_edge_reads_all_k(edge, k):
+    ref, reads = edge
+    idx = FmIndex.build(ref.records, ref.groups, 4, prefix_q=6)
+    dev = DeviceIndex(idx)
+    orc = Oracle(ref.records, ref.groups, 4, k)
+    _check(dev, orc, reads, k)
+    _check(dev, orc, reads, k, local=True)
+    _check(dev, orc, reads, k, cutoff=5)
+    u, t = dev.count_unique_kmers_per_group(k)
+    ou, ot = orc.ref_unique()
+    assert np.array_equal(u, ou) and np.array_equal(t, ot), (k, u, ou, t, ot)
+
+
+@pytest.mark.parametrize("local", [False, True])
+def test_paired(edge, local):
+    ref, _ = edge
+    reads = synth.make_reads(ref, 2_000, paired=True, n_rate=0.003, lowq_rate=0.01)
+    idx = FmIndex.build(ref.records, ref.groups, 4, prefix_q=8)
+    dev = DeviceIndex(idx)
+    for k in (21, 31, 64):
+        orc = Oracle(ref.records, ref.groups, 4, k)
+        _check(dev, orc, reads, k, paired=True, local=local)
+
+
+def test_empty_and_short_inputs(edge):
+    ref, _ = edge
+    idx = FmIndex.build(ref.records, ref.groups, 4)
+    dev = DeviceIndex(idx)
+    got = dev.scan(b"", b"", np.zeros(1, np.uint64), k=21)
+    assert got.total == 0 and got.ambiguous == 0 and not got.unique.any()
+    seq = b"ACGT" * 5
+    off = np.array([0, 4, 4, 20], dtype=np.uint64)  # 3 reads: 4 bp, empty, 16 bp (< k)
+    got = dev.scan(seq, b"I" * 20, off, k=21)
+    assert got.total == 0 and not got.unique.any()
+
+
+def test_many_groups_global_atomics():
+    """G > 2048 takes the global-atomic tally path of the kernel."""
+    G = 2500
+    ref = synth.make_reference(G, 1, 300)
+    reads = synth.make_reads(ref, 4_000, read_len=100)
+    idx = FmIndex.build(ref.records, ref.groups, G, prefix_q=5)
+    dev = DeviceIndex(idx)
+    orc = Oracle(ref.records, ref.groups, G, 25)
+    _check(dev, orc, reads, 25)
+    _check(dev, orc, reads, 25, local=True)
+    u, t = dev.count_unique_kmers_per_group(25)
+    ou, ot = orc.ref_unique()
+    assert np.array_equal(u, ou) and np.array_equal(t, ot)
+
+
+def test_irregular_groupings():
+    """Records assigned to groups out of order, one group spanning scattered records, single group."""
+    ref = synth.make_reference(6, 1, 4_000)
+    reads = synth.make_reads(ref, 2_000)
+    for groups, G in (([2, 0, 1, 2, 0, 1], 3), ([0] * 6, 1), ([5, 4, 3, 2, 1, 0], 6)):
+        idx = FmIndex.build(ref.records, groups, G, prefix_q=7)
+        dev = DeviceIndex(idx)
+        orc = Oracle(ref.records, groups, G, 19)
+        _check(dev, orc, reads, 19)
+        u, t = dev.count_unique_kmers_per_group(19)
+        ou, ot = orc.ref_unique()
+        assert np.array_equal(u, ou) and np.array_equal(t, ot)
+
+
+def test_device_buffers_match_host_path(cfg1):
+    """The hot-path entry (speq_scan_reads_device on HBM-resident torch tensors) equals the host path."""
+    torch = pytest.importorskip("torch")
+    ref, reads = cfg1
+    idx = FmIndex.build(ref.records, ref.groups, 3, prefix_q=10)
+    dev = DeviceIndex(idx)
+    host = dev.scan(reads.seq.tobytes(), reads.qual.tobytes(), reads.offsets, k=21, local=True)
+    cuda = torch.device("cuda:0")
+    d_seq = torch.from_numpy(reads.seq).to(cuda)
+    d_qual = torch.from_numpy(reads.qual).to(cuda)
+    d_off = torch.from_numpy(reads.offsets.astype(np.int64)).to(cuda)
+    d_counts = torch.zeros(3 + 2, dtype=torch.int64, device=cuda)
+    d_w = torch.zeros(3, dtype=torch.float64, device=cuda)
+    stream = torch.cuda.current_stream().cuda_stream
+    dev.scan_device(d_seq.data_ptr(), d_qual.data_ptr(), d_off.data_ptr(), reads.n, 21, d_counts.data_ptr(),
+                    d_w.data_ptr(), local=True, stream=stream)
+    torch.cuda.synchronize()
+    c = d_counts.cpu().numpy().astype(np.uint64)
+    assert c[0] == host.total and c[1] == host.ambiguous and np.array_equal(c[2:], host.unique)
+    np.testing.assert_allclose(d_w.cpu().numpy(), host.weights, rtol=W_RTOL)
+
+
+def test_config2_full_size_vs_oracle():
+    """BASELINE config 2 at full size (10 x 50 kb, 1M x 150 bp, k = 21): bit-exact vs the oracle, plus
+    size-independent properties (shard additivity, read-order invariance, run-to-run determinism)."""
+    c = synth.CONFIGS[2]
+    ref = synth.make_reference(c["n_variants"], c["n_isolates"], c["length"])
+    reads = synth.make_reads(ref, c["n_reads"])
+    G, k = c["n_variants"], c["k"]
+    idx = FmIndex.build(ref.records, ref.groups, G, prefix_q=10)
+    dev = DeviceIndex(idx)
+    orc = Oracle(ref.records, ref.groups, G, k)
+    full = _check(dev, orc, reads, k)
+    assert full.total == c["n_reads"] * (150 - k + 1)
+    again = dev.scan(reads.seq.tobytes(), reads.qual.tobytes(), reads.offsets, k=k)
+    assert again.total == full.total and np.array_equal(again.unique, full.unique)
+    # shards: [0, h) + [h, n) == whole
+    h = reads.n // 3
+    parts = []
+    for lo, hi in ((0, h), (h, reads.n)):
+        a, b = int(reads.offsets[lo]), int(reads.offsets[hi])
+        parts.append(dev.scan(reads.seq[a:b].tobytes(), reads.qual[a:b].tobytes(),
+                              reads.offsets[lo:hi + 1] - reads.offsets[lo], k=k))
+    assert sum(p.total for p in parts) == full.total
+    assert sum(p.ambiguous for p in parts) == full.ambiguous
+    assert np.array_equal(parts[0].unique + parts[1].unique, full.unique)
+    # read order
+    perm = np.random.default_rng(7).permutation(reads.n)[:200_000]
+    segs = [reads.seq[int(reads.offsets[i]):int(reads.offsets[i + 1])] for i in perm]
+    qs = [reads.qual[int(reads.offsets[i]):int(reads.offsets[i + 1])] for i in perm]
+    off = np.zeros(len(perm) + 1, np.uint64)
+    off[1:] = np.cumsum([len(s) for s in segs])
+    sub = synth.Reads(np.concatenate(segs), np.concatenate(qs), off, reads.variant[perm])
+    _check(dev, orc, sub, k)
+    u, t = dev.count_unique_kmers_per_group(k)
+    ou, ot = orc.ref_unique()
+    assert np.array_equal(u, ou) and np.array_equal(t, ot)
