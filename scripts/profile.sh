@@ -1,0 +1,21 @@
+#!/bin/bash
+# rocprofv3 passes over the default bench command (run on the GPU box). Kernel trace + stats in one pass, then one
+# PMC pass per counter group (FETCH_SIZE and WRITE_SIZE cannot share a pass on gfx950; MI355X_MICROARCH.md).
+# Output: gpurun_out/prof/<pass>/...; copy the summaries you want judged into profiles/.
+set -o pipefail
+cd "$GRAFT_REPO_ROOT"
+export TMPDIR=/tmp
+OUT=gpurun_out/prof
+mkdir -p $OUT
+BENCH="bench.py --steps 5 --warmup 1 --no-cpu-baseline $*"
+run() {  # name, rocprof args...
+    local name=$1; shift
+    echo "== $name" >&2
+    timeout -k 10 420 rocprofv3 "$@" -d $OUT/$name -o $name --output-format csv -- python3 $BENCH > $OUT/$name.log 2>&1
+}
+run trace --kernel-trace --stats && \
+run fetch --pmc FETCH_SIZE && \
+run write --pmc WRITE_SIZE && \
+run tcc --pmc TCC_HIT_sum TCC_MISS_sum TCC_EA0_RDREQ_sum && \
+run sq --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_INSTS_LDS SQ_WAIT_INST_ANY SQ_WAVE_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE
+echo "profile rc=$?" >&2

@@ -1,0 +1,60 @@
+#!/usr/bin/env python3
+"""Summarises a scripts/profile.sh output directory into profiles/<round>/ (kernel stats + per-launch PMC means).
+
+Usage: python scripts/summarize_profile.py gpurun_out/prof profiles/r01 [--tag cfg2_k21_q10_global]
+HBM/fabric bytes follow MI355X_MICROARCH.md §HBM: FETCH_SIZE and WRITE_SIZE are in KiB and derive from the L2's
+memory-side request counters (TCC_EA0_RDREQ x 64 B); Infinity-Cache hits are counted, not excluded, so they are an
+upper bound on HBM bytes for an index that stays MALL-resident. (The documented x2 correction applies to wide
+coalesced 16 B/lane streams; this kernel's traffic is 16-B random gathers, for which FETCH_SIZE == RDREQ x 64 B
+exactly — checked below — so no correction is applied.)
+"""
+import collections
+import csv
+import json
+import os
+import shutil
+import sys
+
+
+def main():
+    src, dst = sys.argv[1], sys.argv[2]
+    tag = sys.argv[4] if len(sys.argv) > 4 and sys.argv[3] == "--tag" else "default"
+    os.makedirs(dst, exist_ok=True)
+    out = {"tag": tag}
+    st = os.path.join(src, "trace", "trace_kernel_stats.csv")
+    if os.path.exists(st):
+        shutil.copy(st, os.path.join(dst, f"kernel_stats_{tag}.csv"))
+        rows = list(csv.DictReader(open(st)))
+        out["kernel_stats"] = [{k: r[k] for k in ("Name", "Calls", "AverageNs", "MinNs", "MaxNs", "Percentage")}
+                               for r in rows]
+    pmc = collections.defaultdict(list)
+    meta = {}
+    for p in ("fetch", "write", "tcc", "sq"):
+        f = os.path.join(src, p, f"{p}_counter_collection.csv")
+        if not os.path.exists(f):
+            continue
+        for r in csv.DictReader(open(f)):
+            if "k_scan" not in r["Kernel_Name"]:
+                continue
+            pmc[r["Counter_Name"]].append(float(r["Counter_Value"]))
+            meta = {k: r[k] for k in ("Grid_Size", "Workgroup_Size", "LDS_Block_Size", "VGPR_Count", "SGPR_Count",
+                                      "Scratch_Size")}
+    means = {k: sum(v) / len(v) for k, v in pmc.items()}
+    out["k_scan_pmc_mean_per_launch"] = means
+    out["k_scan_dispatch"] = meta
+    if "FETCH_SIZE" in means:
+        out["fabric_read_bytes_per_launch"] = means["FETCH_SIZE"] * 1024
+    if "WRITE_SIZE" in means:
+        out["fabric_write_bytes_per_launch"] = means["WRITE_SIZE"] * 1024
+    if "TCC_EA0_RDREQ_sum" in means and "FETCH_SIZE" in means:
+        out["check_fetch_equals_rdreq_x64"] = abs(means["TCC_EA0_RDREQ_sum"] * 64 - means["FETCH_SIZE"] * 1024) \
+            / max(1.0, means["FETCH_SIZE"] * 1024)
+    if "TCC_HIT_sum" in means:
+        h, m = means["TCC_HIT_sum"], means.get("TCC_MISS_sum", 0.0)
+        out["l2_hit_rate"] = h / max(1.0, h + m)
+    json.dump(out, open(os.path.join(dst, f"pmc_{tag}.json"), "w"), indent=1)
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main()

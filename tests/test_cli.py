@@ -1,0 +1,116 @@
+"""The `speq` CLI (index|scan|all): options, defaults, cache files and stderr output of the reference.
+
+CPU tests cover argument handling and `speq index`; `speq scan` needs the GPU (marked gpu)."""
+import json
+import os
+import shutil
+import subprocess
+
+import numpy as np
+import pytest
+
+from golden_io import CASES, Case
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+SPEQ = os.path.join(ROOT, "bin", "speq")
+
+
+def run(args, cwd):
+    return subprocess.run([SPEQ] + args, cwd=cwd, capture_output=True, text=True, timeout=300)
+
+
+@pytest.fixture
+def work(tmp_path):
+    c = Case("tiny_single")
+    for f in ("refs.fa", "groups.txt", "reads_1.fq"):
+        shutil.copy(os.path.join(c.dir, f), tmp_path / f)
+    return tmp_path
+
+
+def test_help_and_unknown_subcommand(work):
+    r = run(["--help"], work)
+    assert r.returncode == 0 and "speq [index|scan|all]" in r.stdout
+    r = run(["frobnicate"], work)
+    assert r.returncode == 1 and "SPeQ Error" in r.stderr
+
+
+def test_index_builds_and_is_cached(work):
+    r = run(["index", "-r", "refs.fa", "-g", "groups.txt", "-x", "ref", "-o", "out.txt"], work)
+    assert r.returncode == 0, r.stderr
+    idx = work / "ref.idx"
+    assert idx.exists()
+    m1 = idx.stat().st_mtime_ns
+    # unchanged inputs: not rebuilt (fm_indexer.cpp:68-97)
+    r = run(["index", "-r", "refs.fa", "-g", "groups.txt", "-x", "ref.idx", "-o", "out2.txt"], work)
+    assert r.returncode == 0 and idx.stat().st_mtime_ns == m1
+    # -f forces a rebuild
+    r = run(["index", "-r", "refs.fa", "-g", "groups.txt", "-x", "ref.idx", "-o", "out2.txt", "-f"], work)
+    assert r.returncode == 0 and idx.stat().st_mtime_ns != m1
+
+
+def test_index_rebuilds_when_groupings_change(work):
+    assert run(["index", "-r", "refs.fa", "-g", "groups.txt", "-x", "ref", "-o", "o.txt"], work).returncode == 0
+    m1 = (work / "ref.idx").stat().st_mtime_ns
+    os.utime(work / "groups.txt", ns=(m1 + 10**9, m1 + 10**9))
+    assert run(["index", "-r", "refs.fa", "-g", "groups.txt", "-x", "ref", "-o", "o2.txt"], work).returncode == 0
+    assert (work / "ref.idx").stat().st_mtime_ns != m1
+
+
+def test_argument_errors(work):
+    r = run(["index", "-r", "missing.fa", "-g", "groups.txt"], work)
+    assert r.returncode == 1 and "argument parsing error" in r.stderr and "was not found" in r.stderr
+    (work / "output.txt").write_text("x")
+    r = run(["index", "-r", "refs.fa", "-g", "groups.txt"], work)  # default -o output.txt exists
+    assert r.returncode == 1 and "Cowardly refusing" in r.stderr
+    r = run(["scan", "-1", "reads_1.fq", "-x", "nope", "-o", "s.txt"], work)
+    assert r.returncode == 1 and "was not found" in r.stderr
+    r = run(["scan", "-1", "reads_1.fq", "-t", "1", "-o", "s.txt"], work)
+    assert r.returncode == 1 and "threads" in r.stderr
+    r = run(["scan", "-1", "reads_1.fq", "--fixed-accuracy", "1.5", "-o", "s.txt"], work)
+    assert r.returncode == 1 and "fixed-accuracy" in r.stderr
+
+
+def test_groupings_without_counts_fail_index(work):
+    shutil.copy(os.path.join(ROOT, "tests", "golden", "genome_groupings.txt"), work / "g0.txt")
+    r = run(["index", "-r", "refs.fa", "-g", "g0.txt", "-x", "bad", "-o", "o.txt"], work)
+    assert r.returncode == 2 and "(count)" in r.stderr
+
+
+def _parse_vec(line):
+    assert line.startswith("[") and line.endswith("]"), line
+    body = line[1:-1]
+    return [float(x) for x in body.split(",")] if body else []
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", CASES)
+@pytest.mark.parametrize("mode", ["global", "local"])
+def test_scan_end_to_end(tmp_path, name, mode):
+    c = Case(name)
+    for f in os.listdir(c.dir):
+        shutil.copy(os.path.join(c.dir, f), tmp_path / f)
+    k = c.ks[0]
+    e = c.exp["by_k"][str(k)]
+    r = run(["index", "-r", "refs.fa", "-g", "groups.txt", "-x", "ref", "-o", "i.txt", "--prefix-q", "4"], tmp_path)
+    assert r.returncode == 0, r.stderr
+    args = ["scan", "-1", "reads_1.fq", "-x", "ref", "-k", str(k), "--phred-cutoff", str(c.cutoff)]
+    if c.paired:
+        args += ["-2", "reads_2.fq"]
+    if mode == "global":
+        args += ["--fixed-accuracy", str(c.exp["fixed_accuracy"])]
+    r = run(args + ["-o", "p.txt"], tmp_path)
+    assert r.returncode == 0, r.stderr
+    lines = r.stderr.strip().split("\n")
+    # first scan computes the .dat pass and prints U_ref / Tot_ref (fm_scanner.cpp:1572-1573)
+    assert _parse_vec(lines[0]) == e["u_ref"] and _parse_vec(lines[1]) == e["tot_ref"]
+    assert (tmp_path / f"ref_{k}mer.dat").exists()
+    g = e[mode]
+    np.testing.assert_allclose(_parse_vec(lines[2]), g["percent"], rtol=1e-5)
+    tl = [ln for ln in lines if "\t" in ln]
+    assert tl[0] == f"{g['T']}\t{g['ambiguous']}"
+    # second scan reuses the .dat (no U_ref/Tot_ref lines) and writes the percentages to -o
+    r2 = run(args + ["-o", "p2.txt"], tmp_path)
+    assert r2.returncode == 0
+    assert r2.stderr.strip().split("\n")[0] == lines[2]
+    out = (tmp_path / "p2.txt").read_text().strip().split("\n")
+    assert len(out) == c.G
