@@ -108,7 +108,7 @@ typedef struct {
 int speq_index_get_info(const speq_index* idx, speq_index_info* info);
 
 /* Read-only views of the host arrays (for tests and tools; layout documented in DESIGN.md §3).
- * name: "text", "sa", "occ", "occn", "runs", "run_label", "prefix", "C", "text_start", "text_group". */
+ * name: "text", "sa", "occ", "runs", "run_label", "prefix", "C", "text_start", "text_group". */
 int speq_index_array(const speq_index* idx, const char* name, const void** ptr, uint64_t* bytes);
 
 /* ---- device replica ---- */

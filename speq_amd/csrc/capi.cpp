@@ -97,7 +97,6 @@ int speq_index_array(const speq_index* idx, const char* name, const void** ptr, 
         if (n == "text") set(f.text.data(), f.text.size());
         else if (n == "sa") set(f.sa.data(), f.sa.size() * 4);
         else if (n == "occ") set(f.occ.data(), f.occ.size() * sizeof(speq::OccEntry));
-        else if (n == "occn") set(f.occn.data(), f.occn.size() * sizeof(speq::OccEntry));
         else if (n == "runs") set(f.runs.data(), f.runs.size() * sizeof(speq::OccEntry));
         else if (n == "run_label") set(f.run_label.data(), f.run_label.size() * 2);
         else if (n == "prefix") set(f.prefix.data(), f.prefix.size() * 4);

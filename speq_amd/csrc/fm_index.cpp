@@ -74,16 +74,18 @@ void fill_bitvector(OccEntry* entries, size_t stride, uint64_t n, uint64_t n_blo
 }  // namespace
 
 uint64_t FmIndex::device_bytes() const {
-    return occ.size() * sizeof(OccEntry) + occn.size() * sizeof(OccEntry) + runs.size() * sizeof(OccEntry) +
+    return occ.size() * sizeof(OccEntry) + runs.size() * sizeof(OccEntry) +
            run_label.size() * 2 + prefix.size() * 4 + text.size() + text_start.size() * 8 + text_group.size() * 4;
 }
 
-uint32_t FmIndex::rank(uint8_t sym, uint64_t i) const {
+uint32_t FmIndex::lf(uint8_t sym, uint64_t i) const {
     uint64_t b = i / OCC_BLOCK;
     uint32_t r = (uint32_t)(i - b * OCC_BLOCK);
-    const OccEntry& e = (sym == SYM_N) ? occn[b] : occ[b * 4 + (sym - SYM_A)];
+    const OccEntry& e = occ[(uint64_t)(sym - SYM_A) * n_blocks() + b];
     return entry_rank(e, r);
 }
+
+uint32_t FmIndex::rank(uint8_t sym, uint64_t i) const { return lf(sym, i) - C[sym]; }
 
 uint32_t FmIndex::run_of(uint64_t i) const {
     uint64_t b = i / OCC_BLOCK;
@@ -153,12 +155,16 @@ void fm_build(FmIndex& idx, const char* seq, const uint64_t* rec_offsets, uint32
     const int32_t* SA = idx.sa.data();
     auto bwt = [&](uint64_t i) -> uint8_t { return SA[i] == 0 ? (uint8_t)SYM_TERM : T[SA[i] - 1]; };
 
-    idx.occ.assign(nb * 4, OccEntry{});
-    for (uint8_t s = SYM_A; s <= SYM_T; ++s) {
-        fill_bitvector(idx.occ.data() + (s - SYM_A), 4, n, nb, [&](uint64_t i) { return bwt(i) == s; }, threads);
+    idx.occ.assign(nb * 5, OccEntry{});
+    for (uint8_t s = SYM_A; s <= SYM_N; ++s) {
+        OccEntry* plane = idx.occ.data() + (uint64_t)(s - SYM_A) * nb;
+        fill_bitvector(plane, 1, n, nb, [&](uint64_t i) { return bwt(i) == s; }, threads);
+        // Fold C[s] into the block counts: an LF step is then entry.count + popcount, with no C[] lookup.
+        for (uint64_t b = 0; b < nb; ++b) {
+            if ((uint64_t)plane[b].count + idx.C[s] > 0xFFFFFFFFull) throw std::runtime_error("fm_build: LF overflows 32 bits");
+            plane[b].count += idx.C[s];
+        }
     }
-    idx.occn.assign(nb, OccEntry{});
-    fill_bitvector(idx.occn.data(), 1, n, nb, [&](uint64_t i) { return bwt(i) == SYM_N; }, threads);
 
     // Label of every SA position: group of the text that holds the suffix start.
     std::vector<uint16_t> label(n);
@@ -198,8 +204,8 @@ void fm_build(FmIndex& idx, const char* seq, const uint64_t* rec_offsets, uint32
                     uint32_t lo = cur[2 * y], hi = cur[2 * y + 1];
                     uint8_t s = (uint8_t)(SYM_A + c);
                     if (lo < hi) {
-                        lo = idx.C[s] + idx.rank(s, lo);
-                        hi = idx.C[s] + idx.rank(s, hi);
+                        lo = idx.lf(s, lo);
+                        hi = idx.lf(s, hi);
                     } else {
                         lo = hi = 0;
                     }
@@ -217,8 +223,8 @@ void fm_build(FmIndex& idx, const char* seq, const uint64_t* rec_offsets, uint32
 // ---------------------------------------------------------------------------------------------
 // Persistence: "SPEQIDX1" | u32 version | u32 0 | u64 header_len | header | fields | arrays
 namespace {
-constexpr char MAGIC[8] = {'S', 'P', 'E', 'Q', 'I', 'D', 'X', '1'};
-constexpr uint32_t FILE_VERSION = 1;
+constexpr char MAGIC[8] = {'S', 'P', 'E', 'Q', 'I', 'D', 'X', '1'};  // + FILE_VERSION
+constexpr uint32_t FILE_VERSION = 3;
 
 template <typename T>
 void put(std::ofstream& os, const T& v) { os.write(reinterpret_cast<const char*>(&v), sizeof(T)); }
@@ -280,7 +286,6 @@ void fm_save(const FmIndex& idx, const std::string& path, const void* header, ui
     put_vec(os, idx.text_group);
     put_vec(os, idx.group_of_rec);
     put_vec(os, idx.occ);
-    put_vec(os, idx.occn);
     put_vec(os, idx.runs);
     put_vec(os, idx.run_label);
     put_vec(os, idx.prefix);
@@ -310,13 +315,12 @@ void fm_load(FmIndex& idx, const std::string& path, std::vector<uint8_t>* header
     get_vec(is, idx.text_group, lim);
     get_vec(is, idx.group_of_rec, lim);
     get_vec(is, idx.occ, lim);
-    get_vec(is, idx.occn, lim);
     get_vec(is, idx.runs, lim);
     get_vec(is, idx.run_label, lim);
     get_vec(is, idx.prefix, lim);
     const uint64_t nb = idx.n_blocks();
     if (idx.text.size() != idx.n || idx.text_start.size() != (uint64_t)idx.n_texts + 1 ||
-        idx.text_group.size() != idx.n_texts || idx.occ.size() != nb * 4 || idx.occn.size() != nb ||
+        idx.text_group.size() != idx.n_texts || idx.occ.size() != nb * 5 ||
         idx.runs.size() != nb || idx.prefix_q > MAX_PREFIX_Q ||
         idx.prefix.size() != (idx.prefix_q ? 2 * (uint64_t(1) << (2 * idx.prefix_q)) : 0) || idx.n_groups == 0)
         throw IoError("inconsistent index file " + path);

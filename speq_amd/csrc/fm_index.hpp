@@ -5,9 +5,12 @@
 //
 //   text   : SA alphabet codes, texts separated by SEP and closed by TERM:
 //            T = t_0 SEP t_1 SEP … t_{2R-1} SEP TERM          (TERM=0 < SEP=1 < A=2 < C=3 < G=4 < T=5 < N=6)
-//   occ    : one 64-B block per 96 BWT positions; for each of A,C,G,T a 16-B entry
-//            {u32 rank of that symbol before the block, u32 x3 bitmap of the 96 positions}
-//   occn   : the same 16-B entry for N (only touched by windows that contain N: the .dat pass)
+//   occ    : five planes (A, C, G, T, N), plane-major [symbol][block]; one 16-B entry per 96 BWT positions
+//            {u32 C[s] + rank of s before the block, u32 x3 bitmap of the 96 positions}, so LF(s, i) is that count
+//            plus a popcount (C[] is folded in: no per-step table lookup). Plane-major keeps
+//            the entries of one symbol for 768 consecutive positions in one 128-B line, so the lo and hi loads of
+//            a narrow SA interval hit the same line. The N plane is only touched by windows that contain N
+//            (the .dat pass).
 //   runs   : 16-B entries over the label-change bitvector B[i] = [label(SA[i]) != label(SA[i-1])],
 //            label = group of the text holding suffix SA[i]
 //   run_label : group id of every run (u16)
@@ -62,8 +65,7 @@ struct FmIndex {
     std::vector<int32_t> text_group;      // n_texts
     std::vector<int32_t> group_of_rec;    // as given (length >= n_records)
     uint32_t C[SYM_COUNT + 1] = {0};      // C[c] = #symbols < c
-    std::vector<OccEntry> occ;            // n_blocks * 4
-    std::vector<OccEntry> occn;           // n_blocks
+    std::vector<OccEntry> occ;            // 5 * n_blocks, entry (s, b) at s * n_blocks + b
     std::vector<OccEntry> runs;           // n_blocks
     std::vector<uint16_t> run_label;      // n_runs
     std::vector<uint32_t> prefix;         // 2 * 4^q
@@ -72,7 +74,8 @@ struct FmIndex {
     uint64_t n_blocks() const { return n / OCC_BLOCK + 1; }
     uint64_t device_bytes() const;
 
-    // Host rank used by the builder and by tests: # of symbol `sym` (SYM_A..SYM_N) in BWT[0, i).
+    // Host LF / rank used by the builder and by tests: LF(sym, i) = C[sym] + #sym in BWT[0, i).
+    uint32_t lf(uint8_t sym, uint64_t i) const;
     uint32_t rank(uint8_t sym, uint64_t i) const;
     uint32_t run_of(uint64_t i) const;   // index of the label run holding SA position i
 };

@@ -7,13 +7,19 @@
 //
 // Work decomposition: a wavefront owns a contiguous range of units (reads, mate pairs, or a
 // slice of reference windows) and walks the FLATTENED stream of their k-mer windows 64 at a time, one
-// window per lane, so short tails of one read are packed with the head of the next (130 windows per
-// 150-bp read at k=21 would waste a third of the lanes with one-read-per-wave). The bases of those 64
-// windows are staged once into a per-wave LDS buffer as 3-bit symbols + a "bad" bit (Phred <= cutoff or
-// N, fm_scanner.cpp:162). Each lane then runs exact LF-mapping backward search over the window (two
-// 16-byte occ-entry loads per step), classifies the final SA interval with the label-run bitvector, and
-// tallies into an LDS histogram that is flushed with one global atomic per group per workgroup. Read
-// ambiguity (fm_scanner.cpp:183-190, :709-729) is a segmented min/max scan across lanes by unit.
+// window per lane, so the short tail of one read is packed with the head of the next (130 windows per
+// 150-bp read at k=21 would waste a third of the lanes with one read per pass). Per pass:
+//   1. cursor: every lane loads the window count of read (r + lane) — one coalesced load — and a wave
+//      prefix sum assigns lanes to (read, offset);
+//   2. staging: the bases of the pass are loaded once (coalesced bytes) into a wave-private LDS buffer as
+//      3-bit symbols; a ballot per 64 bases builds the "bad" bitmask (Phred <= cutoff or N, fm_scanner.cpp:162),
+//      so a window's filter is one or two masked 64-bit tests;
+//   3. search: exact LF-mapping backward search, one 16-B occ entry per rank, with the lo and hi ranks of a
+//      step sharing ONE load whenever both fall in the same 96-position block;
+//   4. classify: the SA interval holds one group iff it holds no label-run boundary (two rank loads, again
+//      shared when in one block, and one run-label load);
+//   5. tally into an LDS histogram (flushed with one global atomic per group per workgroup); read ambiguity
+//      (fm_scanner.cpp:183-190, :709-729) is a segmented min/max scan across the lanes of each unit.
 #include <hip/hip_runtime.h>
 
 #include <climits>
@@ -38,13 +44,11 @@ constexpr uint32_t QLUT_LEN = 42;  // phred42 ranks 0..41
 enum { KM_GLOBAL = 0, KM_LOCAL = 1, KM_REF = 2 };
 
 struct DevView {
-    const uint4* occ;        // n_blocks * 4 entries {count, bits[3]} for A,C,G,T
-    const uint4* occn;       // n_blocks entries for N
+    const uint4* occ;        // 5 planes x n_blocks entries {C[s] + count, bits[3]}: A, C, G, T, N (plane-major)
     const uint4* runs;       // n_blocks entries over the label-change bitvector
     const uint16_t* run_label;
     const uint2* prefix;     // 4^q intervals (or null)
-    uint32_t n, q, G, pad;
-    uint32_t c0, c1, c2, c3, c4;  // C[] of A,C,G,T,N
+    uint32_t n, q, G, nb;
 };
 
 struct UnitSrc {
@@ -59,47 +63,108 @@ struct UnitSrc {
     uint32_t end_adj;
     uint32_t k;
     uint32_t cutoff;
-    uint32_t buf_bytes;       // per-wave staging buffer
+    uint32_t buf_bytes;       // per-wave staging buffer (bases)
 };
 
-__host__ __device__ inline uint32_t staging_bytes(uint32_t k) { return ((2u * (64u + k)) + 15u) & ~15u; }
+// Per-wave LDS: bases [buf_bytes] | qualities [buf_bytes] (local mode) | bad-mask words | N-mask words.
+__host__ __device__ inline uint32_t staging_bytes(uint32_t k) { return ((2u * (64u + k)) + 63u) & ~63u; }
+__host__ __device__ inline uint32_t mask_words(uint32_t buf) { return buf / 64u + 1u; }
+__host__ __device__ inline uint32_t wave_lds_bytes(uint32_t buf, bool local) {
+    return buf * (local ? 2u : 1u) + 16u * mask_words(buf);
+}
 
 __device__ __forceinline__ void wave_sync() {
-    // Lanes of one wave exchange data through their wave-private LDS buffer: order the LDS writes
-    // before the reads of other lanes (workgroup-scope fences emit the lgkmcnt wait).
+    // Lanes of one wave exchange data through their wave-private LDS region: order the LDS writes before
+    // the reads of other lanes (workgroup-scope fences emit the lgkmcnt wait).
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
 }
 
-__device__ __forceinline__ uint32_t rank_entry(uint4 v, uint32_t r) {  // v.x + #bits set among the first r (0..96)
-    const uint64_t a = (uint64_t)v.y | ((uint64_t)v.z << 32);
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ uint32_t rank_entry(u32x4 v, uint32_t r) {  // v.x + #bits set among the first r (0..96)
+    const uint64_t a = (uint64_t)v[1] | ((uint64_t)v[2] << 32);
     const uint64_t ma = (r >= 64u) ? ~0ull : ((1ull << r) - 1ull);
     const uint32_t mb = (r <= 64u) ? 0u : ((r >= 96u) ? ~0u : ((1u << (r - 64u)) - 1u));
-    return v.x + (uint32_t)__popcll(a & ma) + (uint32_t)__popc(v.w & mb);
+    return v[0] + (uint32_t)__popcll(a & ma) + (uint32_t)__popc(v[3] & mb);
 }
 
-__device__ __forceinline__ uint32_t lf(const DevView& I, uint32_t c, uint32_t i, uint32_t Cc) {
-    const uint32_t b = i / 96u, r = i - b * 96u;
-    const uint4* p = (c < 4u) ? (I.occ + (size_t)b * 4u + c) : (I.occn + b);
-    return Cc + rank_entry(*p, r);
+// Buffer descriptors of the occ planes and of the run bitvector. A lane that does not need its second load of
+// a step gets an out-of-range offset: the buffer range check drops that load (no memory request, returns 0), so
+// both loads issue back to back with no branch and no wait on the first (a conditional plain load made hipcc
+// wait for the first load before issuing the second).
+struct Rsrc {
+    __amdgpu_buffer_rsrc_t occ, runs;
+};
+constexpr uint32_t OOB = 0xFFFFFFF0u;
+
+__device__ __forceinline__ Rsrc make_rsrc(const DevView& I) {
+    Rsrc R;
+    R.occ = __builtin_amdgcn_make_buffer_rsrc((void*)I.occ, (short)0, (int)(5u * I.nb * 16u), 0x00020000);
+    R.runs = __builtin_amdgcn_make_buffer_rsrc((void*)I.runs, (short)0, (int)(I.nb * 16u), 0x00020000);
+    return R;
 }
 
-__device__ __forceinline__ uint32_t run_of(const DevView& I, uint32_t i) {
-    const uint32_t b = i / 96u, r = i - b * 96u;
-    return rank_entry(I.runs[b], r + 1u);
+// One backward-search step for both ends of [lo, hi): the two ranks share one 16-B load when they fall in the
+// same 96-position block (narrow intervals, i.e. almost every step after the q-mer table).
+__device__ __forceinline__ void lf2(const DevView& I, const Rsrc& R, uint32_t c, uint32_t& lo, uint32_t& hi) {
+    const uint32_t plane = c * I.nb * 16u;
+    const uint32_t bl = lo / 96u, bh = hi / 96u;
+    const bool two = bh != bl;
+    const u32x4 vl = __builtin_amdgcn_raw_buffer_load_b128(R.occ, plane + bl * 16u, 0, 0);
+    const u32x4 vx = __builtin_amdgcn_raw_buffer_load_b128(R.occ, two ? plane + bh * 16u : OOB, 0, 0);
+    const u32x4 vh = two ? vx : vl;
+    lo = rank_entry(vl, lo - bl * 96u);  // entry counts include C[c]
+    hi = rank_entry(vh, hi - bh * 96u);
 }
 
-// Exact backward search of the k symbols at w[0..k) (symbols 0..3 = ACGT, 4 = N in the low 3 bits).
-// Returns -1 (no occurrence), -2 (occurrences in >= 2 groups) or the single group id — the outcome of
-// the first-hit rule at fm_scanner.cpp:165-177 when every record is assigned.
-__device__ __forceinline__ int search_classify(const DevView& I, const unsigned char* w, uint32_t k) {
+// Classifies a non-empty SA interval: run(i) = #label boundaries in [1, i]; one group <=> run(lo) == run(hi-1).
+__device__ __forceinline__ int classify(const DevView& I, const Rsrc& R, uint32_t lo, uint32_t hi) {
+    const uint32_t last = hi - 1u;
+    const uint32_t bl = lo / 96u, bh = last / 96u;
+    const bool two = bh != bl;
+    const u32x4 vl = __builtin_amdgcn_raw_buffer_load_b128(R.runs, bl * 16u, 0, 0);
+    const u32x4 vx = __builtin_amdgcn_raw_buffer_load_b128(R.runs, two ? bh * 16u : OOB, 0, 0);
+    const u32x4 vh = two ? vx : vl;
+    const uint32_t rl = rank_entry(vl, lo - bl * 96u + 1u);
+    const uint32_t rh = rank_entry(vh, last - bh * 96u + 1u);
+    if (rl != rh) return -2;
+    return (int)I.run_label[rl];
+}
+
+// Exact backward search of the k symbols at w[0..k) (0..3 = ACGT, 4 = N). Returns -1 (no occurrence),
+// -2 (occurrences in >= 2 groups) or the single group id: the outcome of the first-hit rule at
+// fm_scanner.cpp:165-177 when every record is assigned.
+// Packed form (k <= 32, no N): the window is folded into a register, R = sum sym[i] * 4^(k-1-i), so the
+// q-mer table index is R's low 2q bits and each step shifts two bits out (no LDS read per step).
+__device__ __forceinline__ int search_packed(const DevView& I, const Rsrc& R, const unsigned char* w, uint32_t k) {
+    uint64_t P = 0;
+    for (uint32_t i = 0; i < k; ++i) P = (P << 2) | (uint64_t)(w[i] & 3u);
+    uint32_t lo = 0, hi = I.n;
+    int32_t s = (int32_t)k;
+    if (I.q != 0u && k >= I.q) {
+        const uint2 e = I.prefix[(uint32_t)(P & ((1ull << (2u * I.q)) - 1ull))];
+        lo = e.x;
+        hi = e.y;
+        P >>= 2u * I.q;
+        s -= (int32_t)I.q;
+    }
+    while (s > 0 && lo < hi) {
+        lf2(I, R, (uint32_t)(P & 3u), lo, hi);
+        P >>= 2;
+        --s;
+    }
+    return lo < hi ? classify(I, R, lo, hi) : -1;
+}
+
+__device__ __forceinline__ int search_lds(const DevView& I, const Rsrc& R, const unsigned char* w, uint32_t k) {
     uint32_t lo = 0, hi = I.n;
     int32_t s = (int32_t)k;
     if (I.q != 0u && k >= I.q) {
         uint32_t code = 0, bad = 0;
         for (uint32_t i = k - I.q; i < k; ++i) {
-            const uint32_t c = w[i] & 7u;
+            const uint32_t c = w[i];
             bad |= c >> 2;
             code = (code << 2) | (c & 3u);
         }
@@ -110,18 +175,14 @@ __device__ __forceinline__ int search_classify(const DevView& I, const unsigned 
             s -= (int32_t)I.q;
         }
     }
+    uint32_t c = s > 0 ? w[s - 1] : 0u;
     while (s > 0 && lo < hi) {
-        const uint32_t c = w[s - 1] & 7u;
-        const uint32_t Cc = c == 0u ? I.c0 : c == 1u ? I.c1 : c == 2u ? I.c2 : c == 3u ? I.c3 : I.c4;
-        lo = lf(I, c, lo, Cc);
-        hi = lf(I, c, hi, Cc);
+        const uint32_t cn = s > 1 ? w[s - 2] : 0u;  // next symbol, read under this step's gathers
+        lf2(I, R, c, lo, hi);
+        c = cn;
         --s;
     }
-    if (lo >= hi) return -1;
-    const uint32_t rl = run_of(I, lo);
-    const uint32_t rh = (hi - lo == 1u) ? rl : run_of(I, hi - 1u);
-    if (rl != rh) return -2;
-    return (int)I.run_label[rl];
+    return lo < hi ? classify(I, R, lo, hi) : -1;
 }
 
 __device__ __forceinline__ uint32_t ascii_sym(uint32_t ch) {  // dna5: A C G T/U -> 0..3, else N (4)
@@ -149,8 +210,13 @@ __global__ __launch_bounds__(BLOCK_THREADS) void k_scan(DevView I, UnitSrc src, 
     unsigned long long* hA = reinterpret_cast<unsigned long long*>(smem);
     unsigned long long* hB = hA + G;              // KM_REF: Tot_ref
     double* hW = reinterpret_cast<double*>(hA + G);  // KM_LOCAL: W
-    unsigned char* sbuf = smem + hist_bytes + wid * src.buf_bytes * (MODE == KM_LOCAL ? 2u : 1u);
-    unsigned char* qbuf = sbuf + src.buf_bytes;
+    const uint32_t buf = src.buf_bytes;
+    unsigned char* sbuf = smem + hist_bytes + wid * wave_lds_bytes(buf, MODE == KM_LOCAL);
+    unsigned char* qbuf = sbuf + buf;
+    unsigned long long* mbuf =
+        reinterpret_cast<unsigned long long*>(sbuf + buf * (MODE == KM_LOCAL ? 2u : 1u));
+    unsigned long long* nbuf = mbuf + mask_words(buf);  // KM_REF: N positions (windows with N search via LDS)
+    const Rsrc R = make_rsrc(I);
 
     if (LDS_HIST) {
         for (uint32_t i = threadIdx.x; i < hist_words; i += BLOCK_THREADS) hA[i] = 0ull;
@@ -186,65 +252,103 @@ __global__ __launch_bounds__(BLOCK_THREADS) void k_scan(DevView I, UnitSrc src, 
     uint64_t cunit = ~0ull;   // unit whose windows continue past the previous pass
 
     while (r < r_end && remaining > 0) {
-        // ---- locate this lane's window: the lane-th window after the cursor (r, o)
-        uint64_t rr = r, oo = o + lane, rb = 0;
-        bool has = false;
-        while (rr < r_end) {
-            const uint64_t b = src.off[rr], e = src.off[rr + 1] - src.end_adj;
-            const uint64_t L = e - b;
-            const uint64_t Wr = L >= k ? L - k + 1 : 0;
-            if (oo < Wr) { has = true; rb = b; break; }
-            oo -= Wr;
-            ++rr;
+        // ---- 1. cursor: lane i holds the windows of read r+i still to scan (read r starts at window o)
+        uint64_t wl = 0, bl_ = 0;
+        if (r + lane < r_end) {
+            bl_ = src.off[r + lane];
+            const uint64_t L = src.off[r + lane + 1] - src.end_adj - bl_;
+            wl = L >= k ? L - k + 1 : 0;
+            if (lane == 0) wl = wl > o ? wl - o : 0;
         }
-        if (!(__ballot(has) & 1ull)) break;  // lane 0 found nothing: range exhausted
-        const uint64_t pos = rb + oo;
+        uint64_t incl = wl;  // inclusive prefix sum across lanes
+        for (uint32_t d = 1; d < 64u; d <<= 1) {
+            const uint64_t y = __shfl_up(incl, d);
+            if (lane >= d) incl += y;
+        }
+        const uint64_t total = __shfl(incl, 63);
+        if (total == 0) {  // the next 64 reads hold no window
+            r = (r + 64 < r_end) ? r + 64 : r_end;
+            o = 0;
+            continue;
+        }
+        // lane j belongs to read i = #{reads whose windows end at or before j} (binary search over lanes)
+        uint32_t i_lo = 0;
+        for (uint32_t step = 32; step >= 1; step >>= 1) {
+            const uint64_t v = __shfl(incl, (int)(i_lo + step - 1u));
+            if (v <= (uint64_t)lane) i_lo += step;
+        }
+        const uint32_t ri = i_lo > 63u ? 63u : i_lo;
+        const uint64_t excl_i = __shfl(incl, (int)ri) - __shfl(wl, (int)ri);
+        const uint64_t base_i = __shfl(bl_, (int)ri);
+        const uint64_t rr = r + ri;
+        const uint64_t oo = (uint64_t)lane - excl_i + (ri == 0 ? o : 0);
+        bool has = (uint64_t)lane < total;
+        const uint64_t pos = base_i + oo;  // global byte position of the window start
         const uint64_t s0 = __shfl(pos, 0);
-        has = has && (pos + k - s0 <= src.buf_bytes) && ((uint64_t)lane < remaining);
-        const uint64_t taken = __ballot(has);   // a prefix of the lanes (positions are monotone)
+        has = has && (pos + k - s0 <= buf) && ((uint64_t)lane < remaining);
+        const uint64_t taken = __ballot(has);  // a prefix of the lanes (positions are monotone)
         const uint32_t n_taken = (uint32_t)__popcll(taken);
         const uint32_t last = n_taken - 1u;
         const uint64_t pos_last = __shfl(pos, (int)last);
         const uint32_t span = (uint32_t)(pos_last + k - s0);
 
-        // ---- stage bases [s0, s0 + span) into the wave's LDS buffer
-        for (uint32_t p = lane; p < span; p += 64u) {
-            const uint32_t ch = src.seq[s0 + p];
-            uint32_t sym, bad;
-            if (MODE == KM_REF) {
-                sym = ch - 2u;         // SA alphabet A..N = 2..6
-                bad = ch < 2u ? 1u : 0u;  // separator / terminator
-            } else {
-                sym = ascii_sym(ch);
-                int q = (int)src.qual[s0 + p] - 33;
-                q = q < 0 ? 0 : (q > 41 ? 41 : q);
-                bad = ((uint32_t)q <= src.cutoff || sym == 4u) ? 1u : 0u;
-                if (MODE == KM_LOCAL) qbuf[p] = (unsigned char)q;
+        // ---- 2. stage bases [s0, s0 + span) into LDS; ballot the "bad" mask 64 bases at a time
+        for (uint32_t p0 = 0; p0 < span; p0 += 64u) {
+            const uint32_t p = p0 + lane;
+            uint32_t bad = 1, isn = 0;
+            if (p < span) {
+                const uint32_t ch = src.seq[s0 + p];
+                uint32_t sym;
+                if (MODE == KM_REF) {
+                    sym = ch - 2u;            // SA alphabet A..N = 2..6
+                    bad = ch < 2u ? 1u : 0u;  // separator / terminator
+                    isn = sym == 4u ? 1u : 0u;
+                } else {
+                    sym = ascii_sym(ch);
+                    int q = (int)src.qual[s0 + p] - 33;
+                    q = q < 0 ? 0 : (q > 41 ? 41 : q);
+                    bad = ((uint32_t)q <= src.cutoff || sym == 4u) ? 1u : 0u;
+                    if (MODE == KM_LOCAL) qbuf[p] = (unsigned char)q;
+                }
+                sbuf[p] = (unsigned char)sym;
             }
-            sbuf[p] = (unsigned char)(sym | (bad << 3));
+            const uint64_t m = __ballot(bad != 0u);
+            if (lane == 0) mbuf[p0 >> 6] = m;
+            if (MODE == KM_REF) {
+                const uint64_t nm = __ballot(isn != 0u);
+                if (lane == 0) nbuf[p0 >> 6] = nm;
+            }
         }
         wave_sync();
 
-        // ---- search + classify
+        // ---- 3./4. filter, search, classify
         int which = -1;
         bool valid = false;
         double wgt = 0.0;
         if (has) {
-            const unsigned char* w = sbuf + (uint32_t)(pos - s0);
-            uint32_t acc = 0;
-            for (uint32_t i = 0; i < k; ++i) acc |= w[i];
-            valid = !(acc & 8u);
-            if (valid) which = search_classify(I, w, k);
+            const uint32_t off = (uint32_t)(pos - s0);
+            const uint32_t w0 = off >> 6, w1 = (off + k - 1u) >> 6;
+            uint64_t badbits = 0, nbits = 0;
+            for (uint32_t wi = w0; wi <= w1; ++wi) {
+                uint64_t sel = ~0ull;
+                if (wi == w0) sel &= ~0ull << (off & 63u);
+                if (wi == w1) sel &= ~0ull >> (63u - ((off + k - 1u) & 63u));
+                badbits |= mbuf[wi] & sel;
+                if (MODE == KM_REF) nbits |= nbuf[wi] & sel;
+            }
+            valid = badbits == 0;
+            const unsigned char* w = sbuf + off;
+            if (valid) which = (k <= 32u && nbits == 0) ? search_packed(I, R, w, k) : search_lds(I, R, w, k);
             if (MODE == KM_LOCAL && valid && which >= 0) {
                 // w = 1.0; for q in window: w = w / (1 - 1/10^(q/10))   (fm_scanner.cpp:454, left to right)
-                const unsigned char* qw = qbuf + (uint32_t)(pos - s0);
+                const unsigned char* qw = qbuf + off;
                 double x = 1.0;
                 for (uint32_t i = 0; i < k; ++i) x = x / src.qlut[qw[i]];
                 wgt = x;
             }
         }
 
-        // ---- tallies
+        // ---- 5. tallies
         if (MODE == KM_REF) {
             if (has && valid) {
                 const int g = src.unit_group[rr];
@@ -394,7 +498,7 @@ void launch_scan(const speq_device_index* d, int mode, bool paired, const UnitSr
     const bool lds_hist = d->G <= LDS_HIST_MAX_G;
     const uint32_t hist_words = lds_hist ? ((mode == KM_GLOBAL) ? d->G : 2u * d->G) : 0u;
     const size_t lds = ((hist_words * 8u + 15u) & ~15u) +
-                       (size_t)WAVES_PER_BLOCK * src.buf_bytes * (mode == KM_LOCAL ? 2u : 1u);
+                       (size_t)WAVES_PER_BLOCK * wave_lds_bytes(src.buf_bytes, mode == KM_LOCAL);
     // >= 4 units (or 256 windows) per wave; at most 8 resident 256-thread blocks on each of the 256 CUs, x2.
     uint64_t blocks = (work_units + 4 * WAVES_PER_BLOCK - 1) / (4 * WAVES_PER_BLOCK);
     if (blocks < 1) blocks = 1;
@@ -437,19 +541,14 @@ int speq_device_open(const speq_index* idx, int device, speq_device_index** out)
         d->text_start = fm.text_start;
         DevView& v = d->view;
         v.occ = reinterpret_cast<const uint4*>(dev_upload(fm.occ));
-        v.occn = reinterpret_cast<const uint4*>(dev_upload(fm.occn));
+        v.nb = (uint32_t)fm.n_blocks();
         v.runs = reinterpret_cast<const uint4*>(dev_upload(fm.runs));
         v.run_label = dev_upload(fm.run_label);
         v.prefix = reinterpret_cast<const uint2*>(dev_upload(fm.prefix));
         v.n = (uint32_t)fm.n;
         v.q = fm.prefix_q;
         v.G = fm.n_groups;
-        v.c0 = fm.C[speq::SYM_A];
-        v.c1 = fm.C[speq::SYM_C];
-        v.c2 = fm.C[speq::SYM_G];
-        v.c3 = fm.C[speq::SYM_T];
-        v.c4 = fm.C[speq::SYM_N];
-        d->allocs = {(void*)v.occ, (void*)v.occn, (void*)v.runs, (void*)v.run_label, (void*)v.prefix};
+        d->allocs = {(void*)v.occ, (void*)v.runs, (void*)v.run_label, (void*)v.prefix};
         d->d_text = dev_upload(fm.text);
         d->d_text_start = dev_upload(fm.text_start);
         d->d_text_group = dev_upload(fm.text_group);

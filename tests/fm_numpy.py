@@ -32,8 +32,8 @@ def entry_rank(entries: np.ndarray, idx: np.ndarray, r: np.ndarray) -> np.ndarra
 
 class NumpyFm:
     def __init__(self, index):
-        self.occ = index.array("occ", np.uint32).reshape(-1, 4)       # (nb*4, 4)
-        self.occn = index.array("occn", np.uint32).reshape(-1, 4)
+        self.occ = index.array("occ", np.uint32).reshape(-1, 4)       # (5*nb, 4): plane-major [symbol][block]
+        self.nb = self.occ.shape[0] // 5
         self.runs = index.array("runs", np.uint32).reshape(-1, 4)
         self.run_label = index.array("run_label", np.uint16)
         self.C = index.array("C", np.uint32).astype(np.int64)
@@ -41,16 +41,13 @@ class NumpyFm:
         self.q = int(index.info().prefix_q)
         self.prefix = index.array("prefix", np.uint32).reshape(-1, 2) if self.q else None
 
-    def rank(self, sym: np.ndarray, i: np.ndarray) -> np.ndarray:
-        """sym: 0..3 ACGT, 4 N."""
+    def lf(self, sym: np.ndarray, i: np.ndarray) -> np.ndarray:
+        """LF(sym, i) = C[sym] + rank; sym: 0..3 ACGT, 4 N (entry counts include C)."""
         b, r = i // BLOCK, i % BLOCK
-        out = np.empty(len(i), dtype=np.int64)
-        acgt = sym < 4
-        if acgt.any():
-            out[acgt] = entry_rank(self.occ, b[acgt] * 4 + sym[acgt], r[acgt])
-        if (~acgt).any():
-            out[~acgt] = entry_rank(self.occn, b[~acgt], r[~acgt])
-        return out
+        return entry_rank(self.occ, sym * self.nb + b, r)
+
+    def rank(self, sym: np.ndarray, i: np.ndarray) -> np.ndarray:
+        return self.lf(sym, i) - self.C[np.asarray(sym) + 2]
 
     def run_of(self, i: np.ndarray) -> np.ndarray:
         return entry_rank(self.runs, i // BLOCK, i % BLOCK + 1)
@@ -77,9 +74,8 @@ class NumpyFm:
             if not act.any():
                 continue
             c = kmers[act, s - 1].astype(np.int64)
-            Cc = self.C[c + 2]
-            lo[act] = Cc + self.rank(c, lo[act])
-            hi[act] = Cc + self.rank(c, hi[act])
+            lo[act] = self.lf(c, lo[act])
+            hi[act] = self.lf(c, hi[act])
         out = np.full(m, -1, dtype=np.int64)
         hit = lo < hi
         if hit.any():

@@ -84,7 +84,7 @@ def test_save_load_roundtrip(tmp_path):
     idx.save(p, b"hello header")
     back = FmIndex.load(p)
     assert back.header == b"hello header"
-    for name, dt in (("text", np.uint8), ("occ", np.uint32), ("occn", np.uint32), ("runs", np.uint32),
+    for name, dt in (("text", np.uint8), ("occ", np.uint32), ("runs", np.uint32),
                      ("run_label", np.uint16), ("prefix", np.uint32), ("C", np.uint32), ("text_start", np.uint64),
                      ("text_group", np.int32)):
         assert np.array_equal(idx.array(name, dt), back.array(name, dt)), name
