@@ -25,7 +25,7 @@ SPEQ_MODE_GLOBAL, SPEQ_MODE_LOCAL = 0, 1
 
 
 class BuildOpts(C.Structure):
-    _fields_ = [("prefix_q", C.c_uint32), ("threads", C.c_uint32)]
+    _fields_ = [("prefix_q", C.c_uint32), ("threads", C.c_uint32), ("pair_steps", C.c_uint32)]
 
 
 class ScanParams(C.Structure):
@@ -34,7 +34,8 @@ class ScanParams(C.Structure):
 
 class IndexInfo(C.Structure):
     _fields_ = [("n", C.c_uint64), ("n_texts", C.c_uint32), ("n_records", C.c_uint32), ("n_groups", C.c_uint32),
-                ("prefix_q", C.c_uint32), ("n_runs", C.c_uint64), ("device_bytes", C.c_uint64)]
+                ("prefix_q", C.c_uint32), ("pair_steps", C.c_uint32), ("n_runs", C.c_uint64),
+                ("device_bytes", C.c_uint64)]
 
 
 # name -> (restype, argtypes); every symbol declared in include/speq_scan.h
@@ -73,6 +74,7 @@ SIGNATURES = {
     "speq_groupings_scaffolds": (_I32P, [_P]),
     "speq_groupings_errors": (C.c_char_p, [_P]),
     "speq_groupings_free": (None, [_P]),
+    "speq_device_set_tuning": (C.c_int, [_P, C.c_char_p, C.c_int64]),
     "speq_timing_enable": (C.c_int, [_P, C.c_int]),
     "speq_timing_read": (C.c_int, [_P, _F64P, _U64P]),
 }

@@ -87,11 +87,11 @@ class FmIndex:
 
     @classmethod
     def build(cls, records: Sequence[bytes | str], group_of_record: Sequence[int], n_groups: int,
-              prefix_q: int = 0, threads: int = 0) -> "FmIndex":
+              prefix_q: int = 0, threads: int = 0, pair_steps: bool = False) -> "FmIndex":
         seq, off = pack_records(records)
         grp = np.asarray(group_of_record, dtype=np.int32)
         h = C.c_void_p()
-        opts = BuildOpts(prefix_q, threads)
+        opts = BuildOpts(prefix_q, threads, int(pair_steps))
         check(lib().speq_index_build(seq, _u64p(off), len(records), grp.ctypes.data_as(C.POINTER(C.c_int32)),
                                      len(grp), n_groups, C.byref(opts), C.byref(h)))
         return cls(h)
@@ -174,7 +174,9 @@ class DeviceIndex:
     def scan_device(self, d_seq: int, d_qual: int, d_offsets: int, n_reads: int, k: int, d_counts: int,
                     d_weights: int = 0, phred_cutoff: int = 30, paired: bool = False, local: bool = False,
                     stream: int = 0) -> None:
-        """Hot path on HBM-resident buffers (raw device pointers, e.g. torch tensor.data_ptr())."""
+        """Hot path on HBM-resident buffers (raw device pointers, e.g. torch tensor.data_ptr()).
+
+        `stream` is a raw hipStream_t (e.g. torch.cuda.current_stream().cuda_stream); 0 = the null stream."""
         p = ScanParams(k, phred_cutoff, int(paired), SPEQ_MODE_LOCAL if local else SPEQ_MODE_GLOBAL)
         check(lib().speq_scan_reads_device(self._h, d_seq, d_qual, d_offsets, n_reads, C.byref(p), d_counts,
                                            d_weights or None, stream or None))
@@ -186,6 +188,11 @@ class DeviceIndex:
         t = np.zeros(G, dtype=np.uint64)
         check(lib().speq_ref_unique(self._h, k, _u64p(u), _u64p(t)))
         return u, t
+
+    def tune(self, **kw) -> None:
+        """Launch tuning (blocks_per_cu=..., grid_blocks=...); never changes results."""
+        for k, v in kw.items():
+            check(lib().speq_device_set_tuning(self._h, k.encode(), int(v)))
 
     def timing(self, on: bool) -> None:
         check(lib().speq_timing_enable(self._h, int(on)))

@@ -27,7 +27,8 @@ struct CmdArguments {  // include/arg_parse.h:10-28
     bool is_scanner{false};
     bool is_parsed{false};
     // MI355X build extensions (not in the reference)
-    unsigned int prefix_q{10};   // --prefix-q: q-mer interval table of the FM-index
+    unsigned int prefix_q{11};   // --prefix-q: q-mer interval table of the FM-index
+    bool pair_steps{true};       // --pair-steps: two-symbol occ planes
     int device{-1};              // --device: GPU ordinal (default: $LOCAL_RANK or 0)
     unsigned int max_em_iterations{1000};
 };

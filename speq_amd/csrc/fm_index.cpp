@@ -74,7 +74,7 @@ void fill_bitvector(OccEntry* entries, size_t stride, uint64_t n, uint64_t n_blo
 }  // namespace
 
 uint64_t FmIndex::device_bytes() const {
-    return occ.size() * sizeof(OccEntry) + runs.size() * sizeof(OccEntry) +
+    return occ.size() * sizeof(OccEntry) + occ2.size() * sizeof(OccEntry) + runs.size() * sizeof(OccEntry) +
            run_label.size() * 2 + prefix.size() * 4 + text.size() + text_start.size() * 8 + text_group.size() * 4;
 }
 
@@ -87,6 +87,12 @@ uint32_t FmIndex::lf(uint8_t sym, uint64_t i) const {
 
 uint32_t FmIndex::rank(uint8_t sym, uint64_t i) const { return lf(sym, i) - C[sym]; }
 
+uint32_t FmIndex::lf2(uint8_t a, uint8_t b, uint64_t i) const {
+    uint64_t blk = i / OCC_BLOCK;
+    uint32_t r = (uint32_t)(i - blk * OCC_BLOCK);
+    return entry_rank(occ2[(uint64_t)((a - SYM_A) * 4 + (b - SYM_A)) * n_blocks() + blk], r);
+}
+
 uint32_t FmIndex::run_of(uint64_t i) const {
     uint64_t b = i / OCC_BLOCK;
     uint32_t r = (uint32_t)(i - b * OCC_BLOCK);
@@ -95,7 +101,7 @@ uint32_t FmIndex::run_of(uint64_t i) const {
 
 void fm_build(FmIndex& idx, const char* seq, const uint64_t* rec_offsets, uint32_t n_records,
               const int32_t* group_of_rec, uint32_t n_group_entries, uint32_t n_groups, uint32_t prefix_q,
-              uint32_t threads) {
+              uint32_t threads, bool pair_steps) {
     if (n_records == 0) throw std::invalid_argument("fm_build: no reference records");
     if (n_groups == 0 || n_groups > 65535) throw std::invalid_argument("fm_build: n_groups must be in [1, 65535]");
     if (prefix_q > MAX_PREFIX_Q) throw std::invalid_argument("fm_build: prefix_q > 13");
@@ -166,6 +172,27 @@ void fm_build(FmIndex& idx, const char* seq, const uint64_t* rec_offsets, uint32
         }
     }
 
+    if (pair_steps) {
+        // C2[ab] = #suffixes < "ab" = #positions p with T[p] < a, or T[p] == a and T[p+1] < b.
+        uint64_t pc[SYM_COUNT][SYM_COUNT] = {{0}};
+        for (uint64_t p = 0; p + 1 < n; ++p) pc[T[p]][T[p + 1]]++;
+        idx.occ2.assign(nb * 16, OccEntry{});
+        for (uint8_t a = SYM_A; a <= SYM_T; ++a) {
+            for (uint8_t b = SYM_A; b <= SYM_T; ++b) {
+                uint64_t c2 = idx.C[a];
+                for (uint8_t c = 0; c < b; ++c) c2 += pc[a][c];
+                OccEntry* plane = idx.occ2.data() + (uint64_t)((a - SYM_A) * 4 + (b - SYM_A)) * nb;
+                fill_bitvector(plane, 1, n, nb, [&](uint64_t i) {
+                    return SA[i] >= 2 && T[SA[i] - 2] == a && T[SA[i] - 1] == b;
+                }, threads);
+                for (uint64_t blk = 0; blk < nb; ++blk) {
+                    if ((uint64_t)plane[blk].count + c2 > 0xFFFFFFFFull) throw std::runtime_error("fm_build: LF2 overflows");
+                    plane[blk].count += (uint32_t)c2;
+                }
+            }
+        }
+    }
+
     // Label of every SA position: group of the text that holds the suffix start.
     std::vector<uint16_t> label(n);
     const uint64_t* ts = idx.text_start.data();
@@ -224,7 +251,7 @@ void fm_build(FmIndex& idx, const char* seq, const uint64_t* rec_offsets, uint32
 // Persistence: "SPEQIDX1" | u32 version | u32 0 | u64 header_len | header | fields | arrays
 namespace {
 constexpr char MAGIC[8] = {'S', 'P', 'E', 'Q', 'I', 'D', 'X', '1'};  // + FILE_VERSION
-constexpr uint32_t FILE_VERSION = 3;
+constexpr uint32_t FILE_VERSION = 4;
 
 template <typename T>
 void put(std::ofstream& os, const T& v) { os.write(reinterpret_cast<const char*>(&v), sizeof(T)); }
@@ -286,6 +313,7 @@ void fm_save(const FmIndex& idx, const std::string& path, const void* header, ui
     put_vec(os, idx.text_group);
     put_vec(os, idx.group_of_rec);
     put_vec(os, idx.occ);
+    put_vec(os, idx.occ2);
     put_vec(os, idx.runs);
     put_vec(os, idx.run_label);
     put_vec(os, idx.prefix);
@@ -315,12 +343,13 @@ void fm_load(FmIndex& idx, const std::string& path, std::vector<uint8_t>* header
     get_vec(is, idx.text_group, lim);
     get_vec(is, idx.group_of_rec, lim);
     get_vec(is, idx.occ, lim);
+    get_vec(is, idx.occ2, lim);
     get_vec(is, idx.runs, lim);
     get_vec(is, idx.run_label, lim);
     get_vec(is, idx.prefix, lim);
     const uint64_t nb = idx.n_blocks();
     if (idx.text.size() != idx.n || idx.text_start.size() != (uint64_t)idx.n_texts + 1 ||
-        idx.text_group.size() != idx.n_texts || idx.occ.size() != nb * 5 ||
+        idx.text_group.size() != idx.n_texts || idx.occ.size() != nb * 5 || (!idx.occ2.empty() && idx.occ2.size() != nb * 16) ||
         idx.runs.size() != nb || idx.prefix_q > MAX_PREFIX_Q ||
         idx.prefix.size() != (idx.prefix_q ? 2 * (uint64_t(1) << (2 * idx.prefix_q)) : 0) || idx.n_groups == 0)
         throw IoError("inconsistent index file " + path);

@@ -11,6 +11,9 @@
 //            the entries of one symbol for 768 consecutive positions in one 128-B line, so the lo and hi loads of
 //            a narrow SA interval hit the same line. The N plane is only touched by windows that contain N
 //            (the .dat pass).
+//   occ2   : optional 16 two-symbol planes (pairs ab over ACGT, plane 4a+b), same entry format: bit j set iff
+//            T[SA[j]-2] T[SA[j]-1] == ab, count = C2[ab] + rank, with C2[ab] = #suffixes < "ab". One gather pair
+//            then extends the pattern by TWO bases: interval(abP) = (LF2(ab, lo), LF2(ab, hi)).
 //   runs   : 16-B entries over the label-change bitvector B[i] = [label(SA[i]) != label(SA[i-1])],
 //            label = group of the text holding suffix SA[i]
 //   run_label : group id of every run (u16)
@@ -66,6 +69,7 @@ struct FmIndex {
     std::vector<int32_t> group_of_rec;    // as given (length >= n_records)
     uint32_t C[SYM_COUNT + 1] = {0};      // C[c] = #symbols < c
     std::vector<OccEntry> occ;            // 5 * n_blocks, entry (s, b) at s * n_blocks + b
+    std::vector<OccEntry> occ2;           // 16 * n_blocks or empty
     std::vector<OccEntry> runs;           // n_blocks
     std::vector<uint16_t> run_label;      // n_runs
     std::vector<uint32_t> prefix;         // 2 * 4^q
@@ -76,6 +80,7 @@ struct FmIndex {
 
     // Host LF / rank used by the builder and by tests: LF(sym, i) = C[sym] + #sym in BWT[0, i).
     uint32_t lf(uint8_t sym, uint64_t i) const;
+    uint32_t lf2(uint8_t a, uint8_t b, uint64_t i) const;  // two-symbol LF (requires occ2)
     uint32_t rank(uint8_t sym, uint64_t i) const;
     uint32_t run_of(uint64_t i) const;   // index of the label run holding SA position i
 };
@@ -83,7 +88,7 @@ struct FmIndex {
 // Builds the index (throws std::invalid_argument / std::runtime_error).
 void fm_build(FmIndex& idx, const char* seq, const uint64_t* rec_offsets, uint32_t n_records,
               const int32_t* group_of_rec, uint32_t n_group_entries, uint32_t n_groups, uint32_t prefix_q,
-              uint32_t threads);
+              uint32_t threads, bool pair_steps = false);
 
 void fm_save(const FmIndex& idx, const std::string& path, const void* header, uint64_t header_len);
 void fm_load(FmIndex& idx, const std::string& path, std::vector<uint8_t>* header);

@@ -45,6 +45,7 @@ enum { KM_GLOBAL = 0, KM_LOCAL = 1, KM_REF = 2 };
 
 struct DevView {
     const uint4* occ;        // 5 planes x n_blocks entries {C[s] + count, bits[3]}: A, C, G, T, N (plane-major)
+    const uint4* occ2;       // 16 two-symbol planes x n_blocks (plane 4a+b), or null
     const uint4* runs;       // n_blocks entries over the label-change bitvector
     const uint16_t* run_label;
     const uint2* prefix;     // 4^q intervals (or null)
@@ -95,7 +96,7 @@ __device__ __forceinline__ uint32_t rank_entry(u32x4 v, uint32_t r) {  // v.x + 
 // both loads issue back to back with no branch and no wait on the first (a conditional plain load made hipcc
 // wait for the first load before issuing the second).
 struct Rsrc {
-    __amdgpu_buffer_rsrc_t occ, runs;
+    __amdgpu_buffer_rsrc_t occ, occ2, runs;
 };
 constexpr uint32_t OOB = 0xFFFFFFF0u;
 
@@ -103,17 +104,21 @@ __device__ __forceinline__ Rsrc make_rsrc(const DevView& I) {
     Rsrc R;
     R.occ = __builtin_amdgcn_make_buffer_rsrc((void*)I.occ, (short)0, (int)(5u * I.nb * 16u), 0x00020000);
     R.runs = __builtin_amdgcn_make_buffer_rsrc((void*)I.runs, (short)0, (int)(I.nb * 16u), 0x00020000);
+    R.occ2 = __builtin_amdgcn_make_buffer_rsrc((void*)I.occ2, (short)0, I.occ2 ? (int)(16u * I.nb * 16u) : 0,
+                                               0x00020000);
     return R;
 }
 
 // One backward-search step for both ends of [lo, hi): the two ranks share one 16-B load when they fall in the
-// same 96-position block (narrow intervals, i.e. almost every step after the q-mer table).
-__device__ __forceinline__ void lf2(const DevView& I, const Rsrc& R, uint32_t c, uint32_t& lo, uint32_t& hi) {
-    const uint32_t plane = c * I.nb * 16u;
+// same 96-position block (narrow intervals, i.e. almost every step after the q-mer table). `rs` selects the
+// one-symbol planes (plane = symbol) or the two-symbol planes (plane = 4a + b: extends by two bases).
+__device__ __forceinline__ void lf_step(const DevView& I, __amdgpu_buffer_rsrc_t rs, uint32_t plane_id, uint32_t& lo,
+                                        uint32_t& hi) {
+    const uint32_t plane = plane_id * I.nb * 16u;
     const uint32_t bl = lo / 96u, bh = hi / 96u;
     const bool two = bh != bl;
-    const u32x4 vl = __builtin_amdgcn_raw_buffer_load_b128(R.occ, plane + bl * 16u, 0, 0);
-    const u32x4 vx = __builtin_amdgcn_raw_buffer_load_b128(R.occ, two ? plane + bh * 16u : OOB, 0, 0);
+    const u32x4 vl = __builtin_amdgcn_raw_buffer_load_b128(rs, plane + bl * 16u, 0, 0);
+    const u32x4 vx = __builtin_amdgcn_raw_buffer_load_b128(rs, two ? plane + bh * 16u : OOB, 0, 0);
     const u32x4 vh = two ? vx : vl;
     lo = rank_entry(vl, lo - bl * 96u);  // entry counts include C[c]
     hi = rank_entry(vh, hi - bh * 96u);
@@ -150,15 +155,29 @@ __device__ __forceinline__ int search_packed(const DevView& I, const Rsrc& R, co
         P >>= 2u * I.q;
         s -= (int32_t)I.q;
     }
-    while (s > 0 && lo < hi) {
-        lf2(I, R, (uint32_t)(P & 3u), lo, hi);
-        P >>= 2;
-        --s;
+    if (I.occ2 != nullptr) {
+        if ((s & 1) && lo < hi) {  // odd remainder: one single-base step first (the rightmost base)
+            lf_step(I, R.occ, (uint32_t)(P & 3u), lo, hi);
+            P >>= 2;
+            --s;
+        }
+        while (s > 0 && lo < hi) {  // P's low digit is w[s-1] (b), the next is w[s-2] (a): plane 4a + b
+            lf_step(I, R.occ2, (uint32_t)(((P >> 2) & 3u) * 4u + (P & 3u)), lo, hi);
+            P >>= 4;
+            s -= 2;
+        }
+    } else {
+        while (s > 0 && lo < hi) {
+            lf_step(I, R.occ, (uint32_t)(P & 3u), lo, hi);
+            P >>= 2;
+            --s;
+        }
     }
     return lo < hi ? classify(I, R, lo, hi) : -1;
 }
 
-__device__ __forceinline__ int search_lds(const DevView& I, const Rsrc& R, const unsigned char* w, uint32_t k) {
+__device__ __forceinline__ int search_lds(const DevView& I, const Rsrc& R, const unsigned char* w, uint32_t k,
+                                          bool no_n) {
     uint32_t lo = 0, hi = I.n;
     int32_t s = (int32_t)k;
     if (I.q != 0u && k >= I.q) {
@@ -175,12 +194,23 @@ __device__ __forceinline__ int search_lds(const DevView& I, const Rsrc& R, const
             s -= (int32_t)I.q;
         }
     }
-    uint32_t c = s > 0 ? w[s - 1] : 0u;
-    while (s > 0 && lo < hi) {
-        const uint32_t cn = s > 1 ? w[s - 2] : 0u;  // next symbol, read under this step's gathers
-        lf2(I, R, c, lo, hi);
-        c = cn;
-        --s;
+    if (I.occ2 != nullptr && no_n) {
+        if ((s & 1) && lo < hi) {
+            lf_step(I, R.occ, w[s - 1], lo, hi);
+            --s;
+        }
+        while (s > 0 && lo < hi) {
+            lf_step(I, R.occ2, (uint32_t)w[s - 2] * 4u + w[s - 1], lo, hi);
+            s -= 2;
+        }
+    } else {
+        uint32_t c = s > 0 ? w[s - 1] : 0u;
+        while (s > 0 && lo < hi) {
+            const uint32_t cn = s > 1 ? w[s - 2] : 0u;  // next symbol, read under this step's gathers
+            lf_step(I, R.occ, c, lo, hi);
+            c = cn;
+            --s;
+        }
     }
     return lo < hi ? classify(I, R, lo, hi) : -1;
 }
@@ -338,7 +368,7 @@ __global__ __launch_bounds__(BLOCK_THREADS) void k_scan(DevView I, UnitSrc src, 
             }
             valid = badbits == 0;
             const unsigned char* w = sbuf + off;
-            if (valid) which = (k <= 32u && nbits == 0) ? search_packed(I, R, w, k) : search_lds(I, R, w, k);
+            if (valid) which = (k <= 32u && nbits == 0) ? search_packed(I, R, w, k) : search_lds(I, R, w, k, nbits == 0);
             if (MODE == KM_LOCAL && valid && which >= 0) {
                 // w = 1.0; for q in window: w = w / (1 - 1/10^(q/10))   (fm_scanner.cpp:454, left to right)
                 const unsigned char* qw = qbuf + off;
@@ -468,6 +498,9 @@ struct speq_device_index {
     uint32_t G = 0;
     hipStream_t stream = nullptr;
     bool timing = false;
+    uint32_t blocks_per_cu = 0;   // tuning: 0 = as many as registers/LDS allow; else pad LDS to cap occupancy
+    uint32_t grid_blocks = 8192;  // tuning: upper bound of the grid
+    uint32_t n_cus = 256;
     std::vector<std::pair<hipEvent_t, hipEvent_t>> events;
     double timed_ms = 0.0;
     uint64_t timed_launches = 0;
@@ -488,6 +521,25 @@ struct DeviceGuard {
 };
 
 template <int MODE, bool PAIRED, bool LDS>
+void allow_big_lds() {
+    HIP_OK(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_scan<MODE, PAIRED, LDS>),
+                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+}
+
+void allow_big_lds_all() {
+    allow_big_lds<KM_GLOBAL, false, true>();
+    allow_big_lds<KM_GLOBAL, false, false>();
+    allow_big_lds<KM_GLOBAL, true, true>();
+    allow_big_lds<KM_GLOBAL, true, false>();
+    allow_big_lds<KM_LOCAL, false, true>();
+    allow_big_lds<KM_LOCAL, false, false>();
+    allow_big_lds<KM_LOCAL, true, true>();
+    allow_big_lds<KM_LOCAL, true, false>();
+    allow_big_lds<KM_REF, false, true>();
+    allow_big_lds<KM_REF, false, false>();
+}
+
+template <int MODE, bool PAIRED, bool LDS>
 void launch_t(const speq_device_index* d, const UnitSrc& src, uint32_t grid, size_t lds, hipStream_t st,
               unsigned long long* a, unsigned long long* b, double* w) {
     hipLaunchKernelGGL((k_scan<MODE, PAIRED, LDS>), dim3(grid), dim3(BLOCK_THREADS), lds, st, d->view, src, a, b, w);
@@ -499,15 +551,20 @@ void launch_scan(const speq_device_index* d, int mode, bool paired, const UnitSr
     const uint32_t hist_words = lds_hist ? ((mode == KM_GLOBAL) ? d->G : 2u * d->G) : 0u;
     const size_t lds = ((hist_words * 8u + 15u) & ~15u) +
                        (size_t)WAVES_PER_BLOCK * wave_lds_bytes(src.buf_bytes, mode == KM_LOCAL);
-    // >= 4 units (or 256 windows) per wave; at most 8 resident 256-thread blocks on each of the 256 CUs, x2.
+    // >= 4 units (or 256 windows) per wave; grid capped (default 4096 = 2x the 8 resident blocks x 256 CUs).
     uint64_t blocks = (work_units + 4 * WAVES_PER_BLOCK - 1) / (4 * WAVES_PER_BLOCK);
     if (blocks < 1) blocks = 1;
-    if (blocks > 4096) blocks = 4096;
+    if (blocks > d->grid_blocks) blocks = d->grid_blocks;
+    size_t lds_launch = lds;
+    if (d->blocks_per_cu > 0) {  // occupancy cap: pad dynamic LDS so only blocks_per_cu blocks fit a CU
+        const size_t pad = (160u * 1024u) / d->blocks_per_cu;
+        if (pad > lds_launch) lds_launch = pad & ~(size_t)15;
+    }
     const uint32_t grid = (uint32_t)blocks;
-#define SPEQ_DISPATCH(M, P)                                                        \
-    do {                                                                           \
-        if (lds_hist) launch_t<M, P, true>(d, src, grid, lds, st, a, b, w);       \
-        else launch_t<M, P, false>(d, src, grid, lds, st, a, b, w);               \
+#define SPEQ_DISPATCH(M, P)                                                            \
+    do {                                                                               \
+        if (lds_hist) launch_t<M, P, true>(d, src, grid, lds_launch, st, a, b, w);    \
+        else launch_t<M, P, false>(d, src, grid, lds_launch, st, a, b, w);            \
     } while (0)
     if (mode == KM_REF) SPEQ_DISPATCH(KM_REF, false);
     else if (mode == KM_GLOBAL) { if (paired) SPEQ_DISPATCH(KM_GLOBAL, true); else SPEQ_DISPATCH(KM_GLOBAL, false); }
@@ -542,13 +599,14 @@ int speq_device_open(const speq_index* idx, int device, speq_device_index** out)
         DevView& v = d->view;
         v.occ = reinterpret_cast<const uint4*>(dev_upload(fm.occ));
         v.nb = (uint32_t)fm.n_blocks();
+        v.occ2 = reinterpret_cast<const uint4*>(dev_upload(fm.occ2));
         v.runs = reinterpret_cast<const uint4*>(dev_upload(fm.runs));
         v.run_label = dev_upload(fm.run_label);
         v.prefix = reinterpret_cast<const uint2*>(dev_upload(fm.prefix));
         v.n = (uint32_t)fm.n;
         v.q = fm.prefix_q;
         v.G = fm.n_groups;
-        d->allocs = {(void*)v.occ, (void*)v.runs, (void*)v.run_label, (void*)v.prefix};
+        d->allocs = {(void*)v.occ, (void*)v.occ2, (void*)v.runs, (void*)v.run_label, (void*)v.prefix};
         d->d_text = dev_upload(fm.text);
         d->d_text_start = dev_upload(fm.text_start);
         d->d_text_group = dev_upload(fm.text_group);
@@ -560,6 +618,17 @@ int speq_device_open(const speq_index* idx, int device, speq_device_index** out)
         d->allocs.push_back(d->d_text_group);
         d->allocs.push_back(d->d_qlut);
         HIP_OK(hipStreamCreateWithFlags(&d->stream, hipStreamNonBlocking));
+        hipDeviceProp_t prop;
+        HIP_OK(hipGetDeviceProperties(&prop, device));
+        d->n_cus = (uint32_t)prop.multiProcessorCount;
+        // Default launch shape (measured, profiles/r01/sweep_tuning.jsonl): an index whose ACGT occ planes exceed
+        // one XCD's 4 MiB L2 is served from the Infinity Cache, where 3 resident blocks per CU beat full occupancy
+        // (fewer concurrent gathers thrashing L1/L2); an L2-resident index wants every wave it can get.
+        // (With the two-symbol planes the gather chain is half as long and full occupancy wins again.)
+        const uint64_t acgt_bytes = 4ull * fm.n_blocks() * sizeof(speq::OccEntry);
+        d->blocks_per_cu = (fm.occ2.empty() && acgt_bytes > (4ull << 20)) ? 3u : 0u;
+        d->grid_blocks = 8192;
+        allow_big_lds_all();
         *out = d.release();
     });
 }
@@ -593,7 +662,7 @@ int speq_scan_reads_device(speq_device_index* d, const uint8_t* d_seq, const uin
         if (n_reads == 0) return;
         if (!d_seq || !d_qual || !d_offsets) throw std::invalid_argument("speq_scan_reads_device: null read buffer");
         DeviceGuard g(d->device);
-        hipStream_t st = stream ? static_cast<hipStream_t>(stream) : d->stream;
+        hipStream_t st = static_cast<hipStream_t>(stream);  // NULL = the null (default) stream
         UnitSrc src{};
         src.seq = d_seq;
         src.qual = d_qual;
@@ -690,7 +759,7 @@ int speq_ref_unique_device(speq_device_index* d, uint32_t k, uint64_t* d_u_ref, 
         if (!d || !d_u_ref || !d_tot_ref) throw std::invalid_argument("speq_ref_unique_device: null argument");
         if (k < 1 || k > MAX_K) throw std::invalid_argument("speq_ref_unique_device: k must be in [1, 4096]");
         DeviceGuard g(d->device);
-        hipStream_t st = stream ? static_cast<hipStream_t>(stream) : d->stream;
+        hipStream_t st = static_cast<hipStream_t>(stream);  // NULL = the null (default) stream
         std::vector<uint64_t> cum(d->n_texts + 1, 0);
         for (uint32_t t = 0; t < d->n_texts; ++t) {
             const uint64_t L = d->text_start[t + 1] - d->text_start[t] - 1;  // minus separator
@@ -736,6 +805,22 @@ int speq_ref_unique(speq_device_index* d, uint32_t k, uint64_t* u_ref, uint64_t*
         HIP_OK(hipMemcpyAsync(tot_ref, buf + G, G * 8, hipMemcpyDeviceToHost, d->stream));
         HIP_OK(hipStreamSynchronize(d->stream));
         HIP_OK(hipFree(buf));
+    });
+}
+
+int speq_device_set_tuning(speq_device_index* d, const char* key, int64_t value) {
+    return speq::guarded([&] {
+        if (!d || !key) throw std::invalid_argument("speq_device_set_tuning: null argument");
+        const std::string k(key);
+        if (k == "blocks_per_cu") {
+            if (value < 0 || value > 8) throw std::invalid_argument("blocks_per_cu must be in [0, 8]");
+            d->blocks_per_cu = (uint32_t)value;
+        } else if (k == "grid_blocks") {
+            if (value < 1 || value > (1 << 20)) throw std::invalid_argument("grid_blocks must be in [1, 2^20]");
+            d->grid_blocks = (uint32_t)value;
+        } else {
+            throw std::invalid_argument("speq_device_set_tuning: unknown key " + k);
+        }
     });
 }
 

@@ -40,11 +40,18 @@ class NumpyFm:
         self.n = int(index.info().n)
         self.q = int(index.info().prefix_q)
         self.prefix = index.array("prefix", np.uint32).reshape(-1, 2) if self.q else None
+        occ2 = index.array("occ2", np.uint32)
+        self.occ2 = occ2.reshape(-1, 4) if occ2.size else None
 
     def lf(self, sym: np.ndarray, i: np.ndarray) -> np.ndarray:
         """LF(sym, i) = C[sym] + rank; sym: 0..3 ACGT, 4 N (entry counts include C)."""
         b, r = i // BLOCK, i % BLOCK
         return entry_rank(self.occ, sym * self.nb + b, r)
+
+    def lf2(self, a: np.ndarray, b: np.ndarray, i: np.ndarray) -> np.ndarray:
+        """Two-symbol LF: interval of abP from that of P (plane 4a+b)."""
+        blk, r = i // BLOCK, i % BLOCK
+        return entry_rank(self.occ2, (a * 4 + b) * self.nb + blk, r)
 
     def rank(self, sym: np.ndarray, i: np.ndarray) -> np.ndarray:
         return self.lf(sym, i) - self.C[np.asarray(sym) + 2]
@@ -52,7 +59,7 @@ class NumpyFm:
     def run_of(self, i: np.ndarray) -> np.ndarray:
         return entry_rank(self.runs, i // BLOCK, i % BLOCK + 1)
 
-    def classify(self, kmers: np.ndarray, use_prefix: bool = True) -> np.ndarray:
+    def classify(self, kmers: np.ndarray, use_prefix: bool = True, use_pairs: bool = True) -> np.ndarray:
         """kmers: (m, k) symbols 0..4. Returns -1 / -2 / group per row (same contract as the kernel)."""
         m, k = kmers.shape
         lo = np.zeros(m, dtype=np.int64)
@@ -69,6 +76,30 @@ class NumpyFm:
             steps = np.where(okq, k - self.q, k)
         else:
             steps = np.full(m, k)
+        if self.occ2 is not None and use_pairs:
+            # odd remainder: one single step first, then pairs (same order as the kernel)
+            pair_ok = ~(kmers == 4).any(axis=1)
+            odd = (steps % 2 == 1) & (lo < hi) & pair_ok
+            rows = np.nonzero(odd)[0]
+            if rows.size:
+                c = kmers[rows, steps[rows] - 1].astype(np.int64)
+                lo[rows] = self.lf(c, lo[rows])
+                hi[rows] = self.lf(c, hi[rows])
+                steps = steps.copy()
+                steps[rows] -= 1
+            single_steps = np.where(pair_ok, 0, steps)
+            steps = np.where(pair_ok, steps, 0)
+            while True:
+                act = (steps > 0) & (lo < hi)
+                if not act.any():
+                    break
+                rows = np.nonzero(act)[0]
+                a = kmers[rows, steps[rows] - 2].astype(np.int64)
+                b = kmers[rows, steps[rows] - 1].astype(np.int64)
+                lo[rows] = self.lf2(a, b, lo[rows])
+                hi[rows] = self.lf2(a, b, hi[rows])
+                steps[rows] -= 2
+            steps = single_steps
         for s in range(start, 0, -1):
             act = (s <= steps) & (lo < hi)
             if not act.any():

@@ -15,9 +15,10 @@ pytestmark = pytest.mark.gpu
 
 @pytest.mark.parametrize("name", CASES)
 @pytest.mark.parametrize("q", [0, 4, 8])
-def test_gpu_matches_golden(name, q):
+@pytest.mark.parametrize("pairs", [False, True])
+def test_gpu_matches_golden(name, q, pairs):
     c = Case(name)
-    dev = DeviceIndex(FmIndex.build(c.records, c.groups, c.G, prefix_q=q))
+    dev = DeviceIndex(FmIndex.build(c.records, c.groups, c.G, prefix_q=q, pair_steps=pairs))
     for k in c.ks:
         e = c.exp["by_k"][str(k)]
         u, t = dev.count_unique_kmers_per_group(k)

@@ -35,9 +35,10 @@ def cfg1():
 
 @pytest.mark.parametrize("q", [0, 10])
 @pytest.mark.parametrize("local", [False, True])
-def test_config1_single(cfg1, q, local):
+@pytest.mark.parametrize("pairs", [False, True])
+def test_config1_single(cfg1, q, local, pairs):
     ref, reads = cfg1
-    idx = FmIndex.build(ref.records, ref.groups, 3, prefix_q=q)
+    idx = FmIndex.build(ref.records, ref.groups, 3, prefix_q=q, pair_steps=pairs)
     dev = DeviceIndex(idx)
     orc = Oracle(ref.records, ref.groups, 3, 21)
     got = _check(dev, orc, reads, 21, local=local)
@@ -55,9 +56,10 @@ def edge():
 
 
 @pytest.mark.parametrize("k", [1, 2, 5, 16, 21, 31, 32, 33, 70, 150, 151])
-def test_edge_reads_all_k(edge, k):
+@pytest.mark.parametrize("pairs", [False, True])
+def test_edge_reads_all_k(edge, k, pairs):
     ref, reads = edge
-    idx = FmIndex.build(ref.records, ref.groups, 4, prefix_q=6)
+    idx = FmIndex.build(ref.records, ref.groups, 4, prefix_q=6, pair_steps=pairs)
     dev = DeviceIndex(idx)
     orc = Oracle(ref.records, ref.groups, 4, k)
     _check(dev, orc, reads, k)
@@ -72,7 +74,7 @@ def test_edge_reads_all_k(edge, k):
 def test_paired(edge, local):
     ref, _ = edge
     reads = synth.make_reads(ref, 2_000, paired=True, n_rate=0.003, lowq_rate=0.01)
-    idx = FmIndex.build(ref.records, ref.groups, 4, prefix_q=8)
+    idx = FmIndex.build(ref.records, ref.groups, 4, prefix_q=8, pair_steps=True)
     dev = DeviceIndex(idx)
     for k in (21, 31, 64):
         orc = Oracle(ref.records, ref.groups, 4, k)
@@ -96,7 +98,7 @@ def test_many_groups_global_atomics():
     G = 2500
     ref = synth.make_reference(G, 1, 300)
     reads = synth.make_reads(ref, 4_000, read_len=100)
-    idx = FmIndex.build(ref.records, ref.groups, G, prefix_q=5)
+    idx = FmIndex.build(ref.records, ref.groups, G, prefix_q=5, pair_steps=True)
     dev = DeviceIndex(idx)
     orc = Oracle(ref.records, ref.groups, G, 25)
     _check(dev, orc, reads, 25)
@@ -133,9 +135,12 @@ def test_device_buffers_match_host_path(cfg1):
     d_off = torch.from_numpy(reads.offsets.astype(np.int64)).to(cuda)
     d_counts = torch.zeros(3 + 2, dtype=torch.int64, device=cuda)
     d_w = torch.zeros(3, dtype=torch.float64, device=cuda)
-    stream = torch.cuda.current_stream().cuda_stream
-    dev.scan_device(d_seq.data_ptr(), d_qual.data_ptr(), d_off.data_ptr(), reads.n, 21, d_counts.data_ptr(),
-                    d_w.data_ptr(), local=True, stream=stream)
+    stream = torch.cuda.current_stream().cuda_stream  # 0 = the null stream: torch's ops and ours are ordered
+    for _ in range(3):  # zero -> scan, repeated: the counters must hold ONE pass (stream ordering regression)
+        d_counts.zero_()
+        d_w.zero_()
+        dev.scan_device(d_seq.data_ptr(), d_qual.data_ptr(), d_off.data_ptr(), reads.n, 21, d_counts.data_ptr(),
+                        d_w.data_ptr(), local=True, stream=stream)
     torch.cuda.synchronize()
     c = d_counts.cpu().numpy().astype(np.uint64)
     assert c[0] == host.total and c[1] == host.ambiguous and np.array_equal(c[2:], host.unique)
@@ -149,7 +154,7 @@ def test_config2_full_size_vs_oracle():
     ref = synth.make_reference(c["n_variants"], c["n_isolates"], c["length"])
     reads = synth.make_reads(ref, c["n_reads"])
     G, k = c["n_variants"], c["k"]
-    idx = FmIndex.build(ref.records, ref.groups, G, prefix_q=10)
+    idx = FmIndex.build(ref.records, ref.groups, G, prefix_q=12, pair_steps=True)
     dev = DeviceIndex(idx)
     orc = Oracle(ref.records, ref.groups, G, k)
     full = _check(dev, orc, reads, k)
