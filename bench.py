@@ -122,13 +122,15 @@ def main():
     achieved_gbs = algo_bytes_per_launch / avg_kernel_s / 1e9
 
     traffic = None
+    traffic_src = None
     prof = os.path.join(ROOT, "profiles", "traffic.json")
     if os.path.exists(prof):
         try:
             tj = json.load(open(prof))
-            key = f"cfg{a.config}_k{k}_q{a.prefix_q}_{a.mode}"
+            key = f"cfg{a.config}_k{k}_q{a.prefix_q}_pairs{a.pair_steps}_{a.mode}_reads{n_reads}"
             if key in tj:
                 traffic = tj[key]["hbm_bytes_per_launch"]
+                traffic_src = tj[key]["source"]
         except Exception:
             traffic = None
 
@@ -163,6 +165,11 @@ def main():
                 "kernel": "k_scan (speq_amd/csrc/scan_kernels.hip)",
                 "algorithmic_bytes_per_kmer": 2 * k * OCC_ENTRY_BYTES,
                 "avg_kernel_ms": avg_kernel_s * 1e3, "launches_timed": launches,
+                "traffic_source": traffic_src,
+                "note": "achieved uses SURVEY.md 8(d)'s algorithmic 2*k*64 B per k-mer (k LF steps x 2 uncached "
+                        "64-B occ loads); the kernel issues ~0.3 of those gathers (q-mer table, two-base steps, "
+                        "shared lo/hi loads) and they hit L2/Infinity Cache, so frac > 1 means HBM does not bound "
+                        "this kernel; traffic = measured L2->fabric bytes per launch (DESIGN.md 6)",
             },
             "cpu_baseline": cpu,
             "check": {"T": int(counts[0]), "ambiguous": int(counts[1]), "U": [int(x) for x in counts[2:]]},
