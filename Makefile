@@ -49,8 +49,16 @@ $(CLI): $(CLI_CPP) $(LIB) $(HDRS) speq_amd/cli/*.hpp
 oracle:
 	$(MAKE) -C oracle
 
+# A/B kernel variants for scripts/sweep.py (SPEQ_LIB_PATH=build/variants/<NAME>/libspeq_scan.so):
+#   make variant NAME=hibranch VFLAGS=-DSPEQ_HI_BRANCH=1
+variant: $(filter-out $(OBJDIR)/scan_kernels.o,$(LIB_OBJS))
+	@mkdir -p build/variants/$(NAME)
+	$(HIPCC) $(HIPFLAGS) $(VFLAGS) -c $(LIB_HIP) -o build/variants/$(NAME)/scan_kernels.o
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o build/variants/$(NAME)/libspeq_scan.so \
+	    build/variants/$(NAME)/scan_kernels.o $^ -L/opt/rocm/lib -lrccl -lamdhip64 -lpthread -Wl,-rpath,/opt/rocm/lib
+
 clean:
 	rm -rf build bin $(LIB)
 	$(MAKE) -C oracle clean
 
-.PHONY: all oracle clean
+.PHONY: all oracle clean variant

@@ -36,6 +36,7 @@ def parse_args():
     p.add_argument("--k", type=int, default=0, help="override k")
     p.add_argument("--prefix-q", type=int, default=11)
     p.add_argument("--pair-steps", type=int, default=1)
+    p.add_argument("--label-table", type=int, default=1)
     p.add_argument("--mode", choices=["global", "local"], default="global")
     p.add_argument("--cpu-seconds", type=float, default=15.0, help="target CPU-baseline sample duration")
     p.add_argument("--no-cpu-baseline", action="store_true")
@@ -65,7 +66,8 @@ def main():
 
     ref = synth.make_reference(c["n_variants"], c["n_isolates"], c["length"])
     t0 = time.time()
-    idx = FmIndex.build(ref.records, ref.groups, G, prefix_q=a.prefix_q, pair_steps=bool(a.pair_steps))
+    idx = FmIndex.build(ref.records, ref.groups, G, prefix_q=a.prefix_q, pair_steps=bool(a.pair_steps),
+                        label_table=bool(a.label_table))
     build_s = time.time() - t0
     dev = DeviceIndex(idx, local_rank)
 
@@ -155,7 +157,7 @@ def main():
             "config": {
                 "workload": f"BASELINE config {a.config}: {c['n_variants']} variants x {c['n_isolates']} isolates x "
                             f"{c['length']} bp, {n_reads} x 150 bp {'pairs' if paired else 'reads'} per GPU, k={k}",
-                "k": k, "reads_per_gpu": n_reads, "paired": paired, "mode": a.mode, "prefix_q": a.prefix_q, "pair_steps": a.pair_steps,
+                "k": k, "reads_per_gpu": n_reads, "paired": paired, "mode": a.mode, "prefix_q": a.prefix_q, "pair_steps": a.pair_steps, "label_table": a.label_table,
                 "kmers_per_step_per_gpu": kmers_per_step, "parallelism": f"dp{world} (reads sharded, index replicated)",
                 "index_build_s": round(build_s, 3), "fm_text_len": int(idx.info().n),
             },

@@ -54,6 +54,7 @@ typedef struct {
     uint32_t prefix_q;   /* length of the q-mer interval lookup table (0 = none, max 13) */
     uint32_t threads;    /* host threads for the build (0 = all) */
     uint32_t pair_steps; /* 1: add the 16 two-symbol occ planes (LF over two bases per gather pair) */
+    uint32_t label_table;/* 1: add the per-SA-position {group, run distance} table (one-load classification) */
 } speq_build_opts;
 
 /* Per-scan parameters (reference: cmd_arguments in include/arg_parse.h:10-28). */
@@ -104,13 +105,14 @@ typedef struct {
     uint32_t n_groups;     /* G */
     uint32_t prefix_q;
     uint32_t pair_steps;   /* 1 when the two-symbol occ planes are present */
+    uint32_t label_table;  /* 1 when the per-position label table is present */
     uint64_t n_runs;       /* runs of equal group label along the suffix array */
     uint64_t device_bytes; /* bytes a device replica occupies in HBM */
 } speq_index_info;
 int speq_index_get_info(const speq_index* idx, speq_index_info* info);
 
 /* Read-only views of the host arrays (for tests and tools; layout documented in DESIGN.md §3).
- * name: "text", "sa", "occ", "occ2", "runs", "run_label", "prefix", "C", "text_start", "text_group". */
+ * name: "text", "sa", "occ", "occ2", "runs", "run_label", "lab", "prefix", "C", "text_start", "text_group". */
 int speq_index_array(const speq_index* idx, const char* name, const void** ptr, uint64_t* bytes);
 
 /* ---- device replica ---- */
@@ -165,7 +167,8 @@ void speq_groupings_free(speq_groupings* g);
 /* ---- launch tuning (performance only; results never depend on it) ----
  * "blocks_per_cu": cap resident 256-thread workgroups per CU (0 = no cap; the kernel's LDS is padded);
  *                  default 3 when the index's occ planes exceed one XCD's L2, else 0;
- * "grid_blocks"  : upper bound of the grid (default 8192). */
+ * "grid_blocks"  : upper bound of the grid (default 8192);
+ * "ilp"          : k-mer windows each lane searches concurrently, 1 or 2 (default 1). */
 int speq_device_set_tuning(speq_device_index* d, const char* key, int64_t value);
 
 /* ---- kernel timing (HIP events on the launch stream; bench/roofline support) ----

@@ -9,7 +9,7 @@ cat gpurun_out/sweep.jsonl | python -c "
 import sys, json
 for l in sys.stdin:
     d = json.loads(l)
-    if 'kmers_per_s' in d: print(d['config'], d['k'], d['prefix_q'], d.get('pairs'), d['mode'], d.get('blocks_per_cu'), d.get('grid_blocks'), round(d['kernel_ms_median'],3), '%.3g' % d['kmers_per_s'], d['counts_match_first'])
+    if 'kmers_per_s' in d: print(d['config'], d['k'], d['prefix_q'], d.get('pairs'), d.get('lab'), d['mode'], d.get('blocks_per_cu'), d.get('ilp'), d.get('grid_blocks'), round(d['kernel_ms_median'],3), '%.3g' % d['kmers_per_s'], d['counts_match_first'])
     else: print(d)
 "
 exit $rc

@@ -30,6 +30,8 @@ def main():
     ap.add_argument("--bpc", default="0", help="blocks-per-CU caps to sweep (0 = none)")
     ap.add_argument("--grids", default="8192", help="grid caps to sweep")
     ap.add_argument("--pairs", default="0,1", help="pair_steps values to sweep")
+    ap.add_argument("--labs", default="1", help="label_table values to sweep")
+    ap.add_argument("--ilps", default="1", help="windows per lane to sweep (1, 2)")
     a = ap.parse_args()
     import torch
 
@@ -51,17 +53,20 @@ def main():
         devs = {}
         for q in [int(x) for x in a.qs.split(",")]:
             for pr in [int(x) for x in a.pairs.split(",")]:
-                t0 = time.time()
-                idx = FmIndex.build(ref.records, ref.groups, G, prefix_q=q, pair_steps=bool(pr))
-                info = idx.info()
-                devs[(q, pr)] = (DeviceIndex(idx), time.time() - t0, info)
-        times = {(q, m, b, g): [] for q in devs for m in a.modes.split(",")
-                 for b in [int(x) for x in a.bpc.split(",")] for g in [int(x) for x in a.grids.split(",")]}
+                for lb in [int(x) for x in a.labs.split(",")]:
+                    t0 = time.time()
+                    idx = FmIndex.build(ref.records, ref.groups, G, prefix_q=q, pair_steps=bool(pr),
+                                        label_table=bool(lb))
+                    info = idx.info()
+                    devs[(q, pr, lb)] = (DeviceIndex(idx), time.time() - t0, info)
+        times = {(q, m, b, g, il): [] for q in devs for m in a.modes.split(",")
+                 for b in [int(x) for x in a.bpc.split(",")] for g in [int(x) for x in a.grids.split(",")]
+                 for il in [int(x) for x in a.ilps.split(",")]}
         checks = {}
         for r in range(a.rounds):
-            for (q, m, b, g) in times:
+            for (q, m, b, g, il) in times:
                 dev = devs[q][0]
-                dev.tune(blocks_per_cu=b, grid_blocks=g)
+                dev.tune(blocks_per_cu=b, grid_blocks=g, ilp=il)
                 d_counts.zero_()
                 d_w.zero_()
                 dev.timing(True)
@@ -71,19 +76,19 @@ def main():
                                 stream=stream)
                 torch.cuda.synchronize()
                 ms, n = dev.timing_read()
-                times[(q, m, b, g)].append(ms)
-                checks[(q, m, b, g)] = d_counts.cpu().numpy().tolist()
+                times[(q, m, b, g, il)].append(ms)
+                checks[(q, m, b, g, il)] = d_counts.cpu().numpy().tolist()
         ref_check = None
-        for (q, m, b, g), ts in times.items():
+        for (q, m, b, g, il), ts in times.items():
             med = statistics.median(ts)
             if ref_check is None:
-                ref_check = checks[(q, m, b, g)]
-            out = {"config": cfg, "k": k, "reads": reads.n, "prefix_q": q[0], "pairs": q[1], "mode": m, "blocks_per_cu": b,
-                   "grid_blocks": g, "kernel_ms_median": med,
+                ref_check = checks[(q, m, b, g, il)]
+            out = {"config": cfg, "k": k, "reads": reads.n, "prefix_q": q[0], "pairs": q[1], "lab": q[2], "mode": m, "blocks_per_cu": b,
+                   "grid_blocks": g, "ilp": il, "kernel_ms_median": med,
                    "kernel_ms_min": min(ts), "kmers_per_s": kmers / (med / 1e3),
                    "algo_GBps": kmers * 2 * k * 64 / (med / 1e3) / 1e9,
                    "index_build_s": round(devs[q][1], 3), "n": int(devs[q][2].n), "n_runs": int(devs[q][2].n_runs),
-                   "device_MB": devs[q][2].device_bytes / 1e6, "counts_match_first": checks[(q, m, b, g)] == ref_check}
+                   "device_MB": devs[q][2].device_bytes / 1e6, "counts_match_first": checks[(q, m, b, g, il)] == ref_check}
             print(json.dumps(out), flush=True)
         if a.ref_pass:
             for q, (dev, _, info) in devs.items():
@@ -91,7 +96,7 @@ def main():
                 t0 = time.perf_counter()
                 u, t = dev.count_unique_kmers_per_group(k)
                 el = time.perf_counter() - t0
-                print(json.dumps({"config": cfg, "ref_pass": True, "prefix_q": q[0], "pairs": q[1], "seconds": el,
+                print(json.dumps({"config": cfg, "ref_pass": True, "prefix_q": q[0], "pairs": q[1], "lab": q[2], "seconds": el,
                                   "windows": int(t.sum()), "windows_per_s": int(t.sum()) / el}), flush=True)
 
 

@@ -9,7 +9,8 @@ import ctypes as C
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libspeq_scan.so")
+# SPEQ_LIB_PATH selects an alternative build of the same library (A/B kernel variants in scripts/).
+LIB_PATH = os.environ.get("SPEQ_LIB_PATH") or os.path.join(_HERE, "libspeq_scan.so")
 
 
 class SpeqError(RuntimeError):
@@ -25,7 +26,8 @@ SPEQ_MODE_GLOBAL, SPEQ_MODE_LOCAL = 0, 1
 
 
 class BuildOpts(C.Structure):
-    _fields_ = [("prefix_q", C.c_uint32), ("threads", C.c_uint32), ("pair_steps", C.c_uint32)]
+    _fields_ = [("prefix_q", C.c_uint32), ("threads", C.c_uint32), ("pair_steps", C.c_uint32),
+                ("label_table", C.c_uint32)]
 
 
 class ScanParams(C.Structure):
@@ -34,7 +36,8 @@ class ScanParams(C.Structure):
 
 class IndexInfo(C.Structure):
     _fields_ = [("n", C.c_uint64), ("n_texts", C.c_uint32), ("n_records", C.c_uint32), ("n_groups", C.c_uint32),
-                ("prefix_q", C.c_uint32), ("pair_steps", C.c_uint32), ("n_runs", C.c_uint64),
+                ("prefix_q", C.c_uint32), ("pair_steps", C.c_uint32), ("label_table", C.c_uint32),
+                ("n_runs", C.c_uint64),
                 ("device_bytes", C.c_uint64)]
 
 

@@ -87,11 +87,12 @@ class FmIndex:
 
     @classmethod
     def build(cls, records: Sequence[bytes | str], group_of_record: Sequence[int], n_groups: int,
-              prefix_q: int = 0, threads: int = 0, pair_steps: bool = False) -> "FmIndex":
+              prefix_q: int = 0, threads: int = 0, pair_steps: bool = False,
+              label_table: bool = False) -> "FmIndex":
         seq, off = pack_records(records)
         grp = np.asarray(group_of_record, dtype=np.int32)
         h = C.c_void_p()
-        opts = BuildOpts(prefix_q, threads, int(pair_steps))
+        opts = BuildOpts(prefix_q, threads, int(pair_steps), int(label_table))
         check(lib().speq_index_build(seq, _u64p(off), len(records), grp.ctypes.data_as(C.POINTER(C.c_int32)),
                                      len(grp), n_groups, C.byref(opts), C.byref(h)))
         return cls(h)

@@ -75,7 +75,7 @@ void fill_bitvector(OccEntry* entries, size_t stride, uint64_t n, uint64_t n_blo
 
 uint64_t FmIndex::device_bytes() const {
     return occ.size() * sizeof(OccEntry) + occ2.size() * sizeof(OccEntry) + runs.size() * sizeof(OccEntry) +
-           run_label.size() * 2 + prefix.size() * 4 + text.size() + text_start.size() * 8 + text_group.size() * 4;
+           run_label.size() * 2 + lab.size() * 4 + prefix.size() * 4 + text.size() + text_start.size() * 8 + text_group.size() * 4;
 }
 
 uint32_t FmIndex::lf(uint8_t sym, uint64_t i) const {
@@ -101,7 +101,7 @@ uint32_t FmIndex::run_of(uint64_t i) const {
 
 void fm_build(FmIndex& idx, const char* seq, const uint64_t* rec_offsets, uint32_t n_records,
               const int32_t* group_of_rec, uint32_t n_group_entries, uint32_t n_groups, uint32_t prefix_q,
-              uint32_t threads, bool pair_steps) {
+              uint32_t threads, bool pair_steps, bool label_table) {
     if (n_records == 0) throw std::invalid_argument("fm_build: no reference records");
     if (n_groups == 0 || n_groups > 65535) throw std::invalid_argument("fm_build: n_groups must be in [1, 65535]");
     if (prefix_q > MAX_PREFIX_Q) throw std::invalid_argument("fm_build: prefix_q > 13");
@@ -211,6 +211,15 @@ void fm_build(FmIndex& idx, const char* seq, const uint64_t* rec_offsets, uint32
     idx.run_label.push_back(label[0]);
     for (uint64_t i = 1; i < n; ++i)
         if (label[i] != label[i - 1]) idx.run_label.push_back(label[i]);
+    if (label_table) {
+        idx.lab.resize(n);
+        uint64_t run_end = n;
+        for (uint64_t i = n; i-- > 0;) {
+            if (i + 1 < n && label[i] != label[i + 1]) run_end = i + 1;
+            const uint64_t rem = std::min<uint64_t>(run_end - i, 0xFFFF);
+            idx.lab[i] = (uint32_t)label[i] | ((uint32_t)rem << 16);
+        }
+    }
 
     // q-mer interval table, built level by level by backward extension.
     if (prefix_q > 0) {
@@ -251,7 +260,7 @@ void fm_build(FmIndex& idx, const char* seq, const uint64_t* rec_offsets, uint32
 // Persistence: "SPEQIDX1" | u32 version | u32 0 | u64 header_len | header | fields | arrays
 namespace {
 constexpr char MAGIC[8] = {'S', 'P', 'E', 'Q', 'I', 'D', 'X', '1'};  // + FILE_VERSION
-constexpr uint32_t FILE_VERSION = 4;
+constexpr uint32_t FILE_VERSION = 5;
 
 template <typename T>
 void put(std::ofstream& os, const T& v) { os.write(reinterpret_cast<const char*>(&v), sizeof(T)); }
@@ -316,6 +325,7 @@ void fm_save(const FmIndex& idx, const std::string& path, const void* header, ui
     put_vec(os, idx.occ2);
     put_vec(os, idx.runs);
     put_vec(os, idx.run_label);
+    put_vec(os, idx.lab);
     put_vec(os, idx.prefix);
     if (!os) throw IoError("failed writing index file " + path);
 }
@@ -346,10 +356,11 @@ void fm_load(FmIndex& idx, const std::string& path, std::vector<uint8_t>* header
     get_vec(is, idx.occ2, lim);
     get_vec(is, idx.runs, lim);
     get_vec(is, idx.run_label, lim);
+    get_vec(is, idx.lab, lim);
     get_vec(is, idx.prefix, lim);
     const uint64_t nb = idx.n_blocks();
     if (idx.text.size() != idx.n || idx.text_start.size() != (uint64_t)idx.n_texts + 1 ||
-        idx.text_group.size() != idx.n_texts || idx.occ.size() != nb * 5 || (!idx.occ2.empty() && idx.occ2.size() != nb * 16) ||
+        idx.text_group.size() != idx.n_texts || idx.occ.size() != nb * 5 || (!idx.occ2.empty() && idx.occ2.size() != nb * 16) || (!idx.lab.empty() && idx.lab.size() != idx.n) ||
         idx.runs.size() != nb || idx.prefix_q > MAX_PREFIX_Q ||
         idx.prefix.size() != (idx.prefix_q ? 2 * (uint64_t(1) << (2 * idx.prefix_q)) : 0) || idx.n_groups == 0)
         throw IoError("inconsistent index file " + path);

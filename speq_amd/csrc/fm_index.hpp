@@ -17,6 +17,9 @@
 //   runs   : 16-B entries over the label-change bitvector B[i] = [label(SA[i]) != label(SA[i-1])],
 //            label = group of the text holding suffix SA[i]
 //   run_label : group id of every run (u16)
+//   lab    : optional u32 per SA position: group (low 16 bits) | min(run_end - i, 65535) (high 16 bits), where
+//            run_end is one past the label run holding i. [lo,hi) is single-group iff hi - lo <= that distance, so
+//            the classification is one 4-B load (the runs/run_label rank path remains for saturated distances).
 //   prefix : for every q-mer over ACGT its SA interval (u32 lo, u32 hi)
 //
 // "All occurrences of a window lie in ONE group" <=> the window's SA interval [lo,hi) holds no label change,
@@ -72,6 +75,7 @@ struct FmIndex {
     std::vector<OccEntry> occ2;           // 16 * n_blocks or empty
     std::vector<OccEntry> runs;           // n_blocks
     std::vector<uint16_t> run_label;      // n_runs
+    std::vector<uint32_t> lab;            // n or empty
     std::vector<uint32_t> prefix;         // 2 * 4^q
     std::vector<int32_t> sa;              // n (host only, not persisted; empty after load)
 
@@ -88,7 +92,7 @@ struct FmIndex {
 // Builds the index (throws std::invalid_argument / std::runtime_error).
 void fm_build(FmIndex& idx, const char* seq, const uint64_t* rec_offsets, uint32_t n_records,
               const int32_t* group_of_rec, uint32_t n_group_entries, uint32_t n_groups, uint32_t prefix_q,
-              uint32_t threads, bool pair_steps = false);
+              uint32_t threads, bool pair_steps = false, bool label_table = false);
 
 void fm_save(const FmIndex& idx, const std::string& path, const void* header, uint64_t header_len);
 void fm_load(FmIndex& idx, const std::string& path, std::vector<uint8_t>* header);

@@ -48,6 +48,7 @@ struct DevView {
     const uint4* occ2;       // 16 two-symbol planes x n_blocks (plane 4a+b), or null
     const uint4* runs;       // n_blocks entries over the label-change bitvector
     const uint16_t* run_label;
+    const uint32_t* lab;     // per SA position {group | min(run_end - i, 65535) << 16}, or null
     const uint2* prefix;     // 4^q intervals (or null)
     uint32_t n, q, G, nb;
 };
@@ -68,7 +69,9 @@ struct UnitSrc {
 };
 
 // Per-wave LDS: bases [buf_bytes] | qualities [buf_bytes] (local mode) | bad-mask words | N-mask words.
-__host__ __device__ inline uint32_t staging_bytes(uint32_t k) { return ((2u * (64u + k)) + 63u) & ~63u; }
+__host__ __device__ inline uint32_t staging_bytes(uint32_t k, uint32_t nwin) {
+    return ((2u * (64u * nwin + k)) + 63u) & ~63u;
+}
 __host__ __device__ inline uint32_t mask_words(uint32_t buf) { return buf / 64u + 1u; }
 __host__ __device__ inline uint32_t wave_lds_bytes(uint32_t buf, bool local) {
     return buf * (local ? 2u : 1u) + 16u * mask_words(buf);
@@ -99,6 +102,9 @@ struct Rsrc {
     __amdgpu_buffer_rsrc_t occ, occ2, runs;
 };
 constexpr uint32_t OOB = 0xFFFFFFF0u;
+#ifndef SPEQ_HI_BRANCH
+#define SPEQ_HI_BRANCH 0
+#endif
 
 __device__ __forceinline__ Rsrc make_rsrc(const DevView& I) {
     Rsrc R;
@@ -117,15 +123,36 @@ __device__ __forceinline__ void lf_step(const DevView& I, __amdgpu_buffer_rsrc_t
     const uint32_t plane = plane_id * I.nb * 16u;
     const uint32_t bl = lo / 96u, bh = hi / 96u;
     const bool two = bh != bl;
+#if SPEQ_HI_BRANCH  // A/B variant: exec-masked second load instead of the out-of-range offset
+    u32x4 vx = {0u, 0u, 0u, 0u};
+    if (two) vx = __builtin_amdgcn_raw_buffer_load_b128(rs, plane + bh * 16u, 0, 0);
+    const u32x4 vl = __builtin_amdgcn_raw_buffer_load_b128(rs, plane + bl * 16u, 0, 0);
+#else
     const u32x4 vl = __builtin_amdgcn_raw_buffer_load_b128(rs, plane + bl * 16u, 0, 0);
     const u32x4 vx = __builtin_amdgcn_raw_buffer_load_b128(rs, two ? plane + bh * 16u : OOB, 0, 0);
+#endif
     const u32x4 vh = two ? vx : vl;
     lo = rank_entry(vl, lo - bl * 96u);  // entry counts include C[c]
     hi = rank_entry(vh, hi - bh * 96u);
 }
 
+// lf_step for a window that may be finished (lo >= hi): such a window issues no load and keeps its interval.
+__device__ __forceinline__ void lf_step_pred(const DevView& I, __amdgpu_buffer_rsrc_t rs, uint32_t plane_id,
+                                             uint32_t& lo, uint32_t& hi) {
+    const bool act = lo < hi;
+    const uint32_t plane = plane_id * I.nb * 16u;
+    const uint32_t bl = lo / 96u, bh = hi / 96u;
+    const bool two = bh != bl;
+    const u32x4 vl = __builtin_amdgcn_raw_buffer_load_b128(rs, act ? plane + bl * 16u : OOB, 0, 0);
+    const u32x4 vx = __builtin_amdgcn_raw_buffer_load_b128(rs, (act && two) ? plane + bh * 16u : OOB, 0, 0);
+    const u32x4 vh = two ? vx : vl;
+    const uint32_t nlo = rank_entry(vl, lo - bl * 96u), nhi = rank_entry(vh, hi - bh * 96u);
+    lo = act ? nlo : lo;
+    hi = act ? nhi : hi;
+}
+
 // Classifies a non-empty SA interval: run(i) = #label boundaries in [1, i]; one group <=> run(lo) == run(hi-1).
-__device__ __forceinline__ int classify(const DevView& I, const Rsrc& R, uint32_t lo, uint32_t hi) {
+__device__ __forceinline__ int classify_runs(const DevView& I, const Rsrc& R, uint32_t lo, uint32_t hi) {
     const uint32_t last = hi - 1u;
     const uint32_t bl = lo / 96u, bh = last / 96u;
     const bool two = bh != bl;
@@ -138,44 +165,20 @@ __device__ __forceinline__ int classify(const DevView& I, const Rsrc& R, uint32_
     return (int)I.run_label[rl];
 }
 
-// Exact backward search of the k symbols at w[0..k) (0..3 = ACGT, 4 = N). Returns -1 (no occurrence),
-// -2 (occurrences in >= 2 groups) or the single group id: the outcome of the first-hit rule at
-// fm_scanner.cpp:165-177 when every record is assigned.
-// Packed form (k <= 32, no N): the window is folded into a register, R = sum sym[i] * 4^(k-1-i), so the
-// q-mer table index is R's low 2q bits and each step shifts two bits out (no LDS read per step).
-__device__ __forceinline__ int search_packed(const DevView& I, const Rsrc& R, const unsigned char* w, uint32_t k) {
-    uint64_t P = 0;
-    for (uint32_t i = 0; i < k; ++i) P = (P << 2) | (uint64_t)(w[i] & 3u);
-    uint32_t lo = 0, hi = I.n;
-    int32_t s = (int32_t)k;
-    if (I.q != 0u && k >= I.q) {
-        const uint2 e = I.prefix[(uint32_t)(P & ((1ull << (2u * I.q)) - 1ull))];
-        lo = e.x;
-        hi = e.y;
-        P >>= 2u * I.q;
-        s -= (int32_t)I.q;
-    }
-    if (I.occ2 != nullptr) {
-        if ((s & 1) && lo < hi) {  // odd remainder: one single-base step first (the rightmost base)
-            lf_step(I, R.occ, (uint32_t)(P & 3u), lo, hi);
-            P >>= 2;
-            --s;
-        }
-        while (s > 0 && lo < hi) {  // P's low digit is w[s-1] (b), the next is w[s-2] (a): plane 4a + b
-            lf_step(I, R.occ2, (uint32_t)(((P >> 2) & 3u) * 4u + (P & 3u)), lo, hi);
-            P >>= 4;
-            s -= 2;
-        }
-    } else {
-        while (s > 0 && lo < hi) {
-            lf_step(I, R.occ, (uint32_t)(P & 3u), lo, hi);
-            P >>= 2;
-            --s;
-        }
-    }
-    return lo < hi ? classify(I, R, lo, hi) : -1;
+// One 4-B load when the label table is present: the run holding lo reaches hi-1 iff hi - lo <= its distance.
+__device__ __forceinline__ int classify(const DevView& I, const Rsrc& R, uint32_t lo, uint32_t hi) {
+    if (I.lab == nullptr) return classify_runs(I, R, lo, hi);
+    const uint32_t x = I.lab[lo];
+    const uint32_t dist = x >> 16, width = hi - lo;
+    if (width <= dist) return (int)(x & 0xFFFFu);
+    if (dist < 0xFFFFu) return -2;
+    return classify_runs(I, R, lo, hi);  // saturated distance and a wider interval: exact rank path
 }
 
+// Exact backward search of the k symbols at w[0..k) (0..3 = ACGT, 4 = N) read from LDS (k > 32, or N in a
+// reference window). Returns -1 (no occurrence), -2 (occurrences in >= 2 groups) or the single group id: the
+// outcome of the first-hit rule at fm_scanner.cpp:165-177 when every record is assigned.
+// The packed register form for k <= 32 is search_packed_n below.
 __device__ __forceinline__ int search_lds(const DevView& I, const Rsrc& R, const unsigned char* w, uint32_t k,
                                           bool no_n) {
     uint32_t lo = 0, hi = I.n;
@@ -226,12 +229,78 @@ __device__ __forceinline__ T wave_sum(T v) {
     return v;
 }
 
-template <int MODE, bool PAIRED, bool LDS_HIST>
+// Backward search of NW windows per lane, interleaved so each lane keeps NW independent gather chains in flight
+// (the kernel is bound by gather latency, not by L2 or fabric bandwidth: profiles/r01). Packed form only (k <= 32,
+// no N). A window with an empty interval issues no further loads (out-of-range offsets).
+template <int NW>
+__device__ __forceinline__ void search_packed_n(const DevView& I, const Rsrc& R, const uint64_t (&P0)[NW],
+                                                const bool (&act)[NW], uint32_t k, int (&out)[NW]) {
+    uint64_t P[NW];
+    uint32_t lo[NW], hi[NW];
+    int32_t s = (int32_t)k;
+#pragma unroll
+    for (int w = 0; w < NW; ++w) {
+        P[w] = P0[w];
+        lo[w] = 0;
+        hi[w] = act[w] ? I.n : 0u;
+    }
+    if (I.q != 0u && k >= I.q) {
+        const uint64_t qmask = (1ull << (2u * I.q)) - 1ull;
+#pragma unroll
+        for (int w = 0; w < NW; ++w) {
+            if (act[w]) {
+                const uint2 e = I.prefix[(uint32_t)(P[w] & qmask)];
+                lo[w] = e.x;
+                hi[w] = e.y;
+            }
+            P[w] >>= 2u * I.q;
+        }
+        s -= (int32_t)I.q;
+    }
+    if (I.occ2 != nullptr) {
+        if (s & 1) {
+#pragma unroll
+            for (int w = 0; w < NW; ++w) {
+                lf_step_pred(I, R.occ, (uint32_t)(P[w] & 3u), lo[w], hi[w]);
+                P[w] >>= 2;
+            }
+            --s;
+        }
+        for (; s > 0; s -= 2) {
+            bool any = false;
+#pragma unroll
+            for (int w = 0; w < NW; ++w) any |= lo[w] < hi[w];
+            if (!any) break;
+#pragma unroll
+            for (int w = 0; w < NW; ++w) {
+                lf_step_pred(I, R.occ2, (uint32_t)(((P[w] >> 2) & 3u) * 4u + (P[w] & 3u)), lo[w], hi[w]);
+                P[w] >>= 4;
+            }
+        }
+    } else {
+        for (; s > 0; --s) {
+            bool any = false;
+#pragma unroll
+            for (int w = 0; w < NW; ++w) any |= lo[w] < hi[w];
+            if (!any) break;
+#pragma unroll
+            for (int w = 0; w < NW; ++w) {
+                lf_step_pred(I, R.occ, (uint32_t)(P[w] & 3u), lo[w], hi[w]);
+                P[w] >>= 2;
+            }
+        }
+    }
+#pragma unroll
+    for (int w = 0; w < NW; ++w) out[w] = (act[w] && lo[w] < hi[w]) ? classify(I, R, lo[w], hi[w]) : -1;
+}
+
+template <int MODE, bool PAIRED, bool LDS_HIST, int NWIN>
 __global__ __launch_bounds__(BLOCK_THREADS) void k_scan(DevView I, UnitSrc src, unsigned long long* __restrict__ out_a,
                                                         unsigned long long* __restrict__ out_b,
                                                         double* __restrict__ out_w) {
     // out_a: reads -> counts[G+2] (T, ambiguous, U[g]); ref -> U_ref[G]
     // out_b: ref -> Tot_ref[G];  out_w: local -> W[G]
+    // A pass covers 64 * NWIN consecutive windows of the wave's stream: slot j = lane + 64 * w.
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const uint32_t lane = threadIdx.x & 63u, wid = threadIdx.x >> 6;
     const uint32_t G = I.G, k = src.k;
@@ -279,48 +348,64 @@ __global__ __launch_bounds__(BLOCK_THREADS) void k_scan(DevView I, UnitSrc src, 
     uint32_t t_cnt = 0;       // passing windows seen by this lane
     uint32_t amb = 0;         // ambiguous units finished by this wave (wave-uniform)
     int cmin = INT_MAX, cmax = -1;
-    uint64_t cunit = ~0ull;   // unit whose windows continue past the previous pass
+    uint64_t cunit = ~0ull;   // unit whose windows continue past the previous (sub-)pass
 
     while (r < r_end && remaining > 0) {
-        // ---- 1. cursor: lane i holds the windows of read r+i still to scan (read r starts at window o)
-        uint64_t wl = 0, bl_ = 0;
+        // ---- 1. cursor: lane i holds the windows of read r+i still to scan (read r starts at window o).
+        // Window counts are clamped to 64*NWIN+1: only the first 64*NWIN windows of the pass matter, and the
+        // clamp keeps the lane prefix sums in 32 bits.
+        uint32_t wl = 0;
+        uint64_t bl_ = 0;
         if (r + lane < r_end) {
             bl_ = src.off[r + lane];
             const uint64_t L = src.off[r + lane + 1] - src.end_adj - bl_;
-            wl = L >= k ? L - k + 1 : 0;
-            if (lane == 0) wl = wl > o ? wl - o : 0;
+            uint64_t W = L >= k ? L - k + 1 : 0;
+            if (lane == 0) W = W > o ? W - o : 0;
+            wl = (uint32_t)(W < 64u * NWIN + 1u ? W : 64u * NWIN + 1u);
         }
-        uint64_t incl = wl;  // inclusive prefix sum across lanes
+        uint32_t incl = wl;  // inclusive prefix sum across lanes
         for (uint32_t d = 1; d < 64u; d <<= 1) {
-            const uint64_t y = __shfl_up(incl, d);
+            const uint32_t y = __shfl_up(incl, d);
             if (lane >= d) incl += y;
         }
-        const uint64_t total = __shfl(incl, 63);
+        const uint32_t total = __shfl(incl, 63);
         if (total == 0) {  // the next 64 reads hold no window
             r = (r + 64 < r_end) ? r + 64 : r_end;
             o = 0;
             continue;
         }
-        // lane j belongs to read i = #{reads whose windows end at or before j} (binary search over lanes)
-        uint32_t i_lo = 0;
-        for (uint32_t step = 32; step >= 1; step >>= 1) {
-            const uint64_t v = __shfl(incl, (int)(i_lo + step - 1u));
-            if (v <= (uint64_t)lane) i_lo += step;
+        // slot j belongs to read r + ri, ri = #{reads whose windows end at or before j} (binary search over lanes)
+        uint32_t ri[NWIN], oo[NWIN], off[NWIN];
+        bool has[NWIN];
+        uint64_t s0 = 0;
+#pragma unroll
+        for (int w = 0; w < NWIN; ++w) {
+            const uint32_t slot = lane + 64u * (uint32_t)w;
+            uint32_t i_lo = 0;
+            for (uint32_t step = 32; step >= 1; step >>= 1) {
+                const uint32_t v = __shfl(incl, (int)(i_lo + step - 1u));
+                if (v <= slot) i_lo += step;
+            }
+            ri[w] = i_lo > 63u ? 63u : i_lo;
+            const uint32_t excl_i = __shfl(incl, (int)ri[w]) - __shfl(wl, (int)ri[w]);
+            oo[w] = slot - excl_i;  // window offset in the read, relative to o for read r (ri == 0)
+            const uint64_t pos = __shfl(bl_, (int)ri[w]) + oo[w] + (ri[w] == 0 ? o : 0);
+            if (w == 0) s0 = __shfl(pos, 0);
+            off[w] = (uint32_t)(pos - s0);  // < buf for every slot that is taken
+            has[w] = slot < total && pos + k - s0 <= buf && (uint64_t)slot < remaining;
         }
-        const uint32_t ri = i_lo > 63u ? 63u : i_lo;
-        const uint64_t excl_i = __shfl(incl, (int)ri) - __shfl(wl, (int)ri);
-        const uint64_t base_i = __shfl(bl_, (int)ri);
-        const uint64_t rr = r + ri;
-        const uint64_t oo = (uint64_t)lane - excl_i + (ri == 0 ? o : 0);
-        bool has = (uint64_t)lane < total;
-        const uint64_t pos = base_i + oo;  // global byte position of the window start
-        const uint64_t s0 = __shfl(pos, 0);
-        has = has && (pos + k - s0 <= buf) && ((uint64_t)lane < remaining);
-        const uint64_t taken = __ballot(has);  // a prefix of the lanes (positions are monotone)
-        const uint32_t n_taken = (uint32_t)__popcll(taken);
-        const uint32_t last = n_taken - 1u;
-        const uint64_t pos_last = __shfl(pos, (int)last);
-        const uint32_t span = (uint32_t)(pos_last + k - s0);
+        uint32_t n_taken = 0, off_last = 0, ri_last = 0, oo_last = 0;
+#pragma unroll
+        for (int w = 0; w < NWIN; ++w) {
+            const uint32_t c = (uint32_t)__popcll(__ballot(has[w]));  // valid slots are a prefix in slot order
+            if (c > 0) {
+                off_last = __shfl(off[w], (int)(c - 1u));
+                ri_last = __shfl(ri[w], (int)(c - 1u));
+                oo_last = __shfl(oo[w], (int)(c - 1u));
+            }
+            n_taken += c;
+        }
+        const uint32_t span = off_last + k;
 
         // ---- 2. stage bases [s0, s0 + span) into LDS; ballot the "bad" mask 64 bases at a time
         for (uint32_t p0 = 0; p0 < span; p0 += 64u) {
@@ -352,94 +437,126 @@ __global__ __launch_bounds__(BLOCK_THREADS) void k_scan(DevView I, UnitSrc src, 
         wave_sync();
 
         // ---- 3./4. filter, search, classify
-        int which = -1;
-        bool valid = false;
-        double wgt = 0.0;
-        if (has) {
-            const uint32_t off = (uint32_t)(pos - s0);
-            const uint32_t w0 = off >> 6, w1 = (off + k - 1u) >> 6;
-            uint64_t badbits = 0, nbits = 0;
-            for (uint32_t wi = w0; wi <= w1; ++wi) {
-                uint64_t sel = ~0ull;
-                if (wi == w0) sel &= ~0ull << (off & 63u);
-                if (wi == w1) sel &= ~0ull >> (63u - ((off + k - 1u) & 63u));
-                badbits |= mbuf[wi] & sel;
-                if (MODE == KM_REF) nbits |= nbuf[wi] & sel;
+        int which[NWIN];
+        bool valid[NWIN], packed[NWIN];
+        uint64_t P[NWIN];
+#pragma unroll
+        for (int w = 0; w < NWIN; ++w) {
+            which[w] = -1;
+            valid[w] = false;
+            packed[w] = false;
+            P[w] = 0;
+            if (has[w]) {
+                const uint32_t w0 = off[w] >> 6, w1 = (off[w] + k - 1u) >> 6;
+                uint64_t badbits = 0, nbits = 0;
+                for (uint32_t wi = w0; wi <= w1; ++wi) {
+                    uint64_t sel = ~0ull;
+                    if (wi == w0) sel &= ~0ull << (off[w] & 63u);
+                    if (wi == w1) sel &= ~0ull >> (63u - ((off[w] + k - 1u) & 63u));
+                    badbits |= mbuf[wi] & sel;
+                    if (MODE == KM_REF) nbits |= nbuf[wi] & sel;
+                }
+                valid[w] = badbits == 0;
+                packed[w] = valid[w] && k <= 32u && nbits == 0;
+                if (packed[w]) {
+                    const unsigned char* ws = sbuf + off[w];
+                    uint64_t x = 0;
+                    for (uint32_t i = 0; i < k; ++i) x = (x << 2) | (uint64_t)(ws[i] & 3u);
+                    P[w] = x;
+                } else if (valid[w]) {
+                    which[w] = search_lds(I, R, sbuf + off[w], k, nbits == 0);
+                }
             }
-            valid = badbits == 0;
-            const unsigned char* w = sbuf + off;
-            if (valid) which = (k <= 32u && nbits == 0) ? search_packed(I, R, w, k) : search_lds(I, R, w, k, nbits == 0);
-            if (MODE == KM_LOCAL && valid && which >= 0) {
-                // w = 1.0; for q in window: w = w / (1 - 1/10^(q/10))   (fm_scanner.cpp:454, left to right)
-                const unsigned char* qw = qbuf + off;
-                double x = 1.0;
-                for (uint32_t i = 0; i < k; ++i) x = x / src.qlut[qw[i]];
-                wgt = x;
-            }
+        }
+        {
+            int wp[NWIN];
+            search_packed_n<NWIN>(I, R, P, packed, k, wp);
+#pragma unroll
+            for (int w = 0; w < NWIN; ++w)
+                if (packed[w]) which[w] = wp[w];
         }
 
         // ---- 5. tallies
-        if (MODE == KM_REF) {
-            if (has && valid) {
-                const int g = src.unit_group[rr];
-                if (LDS_HIST) {
-                    atomicAdd(&hB[g], 1ull);
-                    if (which == g) atomicAdd(&hA[g], 1ull);
-                } else {
-                    atomicAdd(&out_b[g], 1ull);
-                    if (which == g) atomicAdd(&out_a[g], 1ull);
-                }
-            }
-            remaining -= n_taken;
-        } else {
-            if (valid) {
-                ++t_cnt;
-                if (which >= 0) {
+#pragma unroll
+        for (int w = 0; w < NWIN; ++w) {
+            if (MODE == KM_REF) {
+                if (has[w] && valid[w]) {
+                    const int g = src.unit_group[r + ri[w]];
                     if (LDS_HIST) {
-                        atomicAdd(&hA[which], 1ull);
-                        if (MODE == KM_LOCAL) atomicAdd(&hW[which], wgt);
+                        atomicAdd(&hB[g], 1ull);
+                        if (which[w] == g) atomicAdd(&hA[g], 1ull);
                     } else {
-                        atomicAdd(&gU[which], 1ull);
-                        if (MODE == KM_LOCAL) atomicAdd(&out_w[which], wgt);
+                        atomicAdd(&out_b[g], 1ull);
+                        if (which[w] == g) atomicAdd(&out_a[g], 1ull);
+                    }
+                }
+            } else if (valid[w]) {
+                ++t_cnt;
+                if (which[w] >= 0) {
+                    double wgt = 0.0;
+                    if (MODE == KM_LOCAL) {
+                        // w = 1.0; for q in window: w = w / (1 - 1/10^(q/10))   (fm_scanner.cpp:454, left to right)
+                        const unsigned char* qw = qbuf + off[w];
+                        double x = 1.0;
+                        for (uint32_t i = 0; i < k; ++i) x = x / src.qlut[qw[i]];
+                        wgt = x;
+                    }
+                    if (LDS_HIST) {
+                        atomicAdd(&hA[which[w]], 1ull);
+                        if (MODE == KM_LOCAL) atomicAdd(&hW[which[w]], wgt);
+                    } else {
+                        atomicAdd(&gU[which[w]], 1ull);
+                        if (MODE == KM_LOCAL) atomicAdd(&out_w[which[w]], wgt);
                     }
                 }
             }
-            // Ambiguity: a unit is ambiguous iff its counted windows name >= 2 groups (min != max).
-            const uint64_t unit = PAIRED ? (rr >> 1) : rr;
-            int vmin = (valid && which >= 0) ? which : INT_MAX;
-            int vmax = (valid && which >= 0) ? which : -1;
-            const uint64_t unit0 = __shfl(unit, 0);
-            if (cunit != ~0ull && unit0 != cunit) {  // the carried unit is complete
-                amb += (cmax >= 0 && cmin != cmax) ? 1u : 0u;
-                cunit = ~0ull;
-            }
-            if (lane == 0 && unit == cunit) {
-                vmin = min(vmin, cmin);
-                vmax = max(vmax, cmax);
-            }
-            const uint64_t uprev = __shfl_up(unit, 1);
-            const bool head = has && (lane == 0 || unit != uprev);
-            const uint64_t heads = __ballot(head);
-            const uint64_t below = heads & ((lane == 63u) ? ~0ull : ((2ull << lane) - 1ull));
-            const uint32_t seg_start = 63u - (uint32_t)__clzll(below);
-            for (uint32_t d = 1; d < 64u; d <<= 1) {
-                const int om = __shfl_up(vmin, d), oM = __shfl_up(vmax, d);
-                if (lane >= d && lane - d >= seg_start) {
-                    vmin = min(vmin, om);
-                    vmax = max(vmax, oM);
+        }
+        if (MODE == KM_REF) remaining -= n_taken;
+
+        // ---- 6. ambiguity: a unit is ambiguous iff its counted windows name >= 2 groups (min != max).
+        // Sub-pass w covers slots [64w, 64w + 64) in stream order; the last unit of a sub-pass is carried.
+        if (MODE != KM_REF) {
+#pragma unroll
+            for (int w = 0; w < NWIN; ++w) {
+                const uint64_t hm = __ballot(has[w]);
+                if (hm == 0) continue;
+                const uint32_t last = (uint32_t)__popcll(hm) - 1u;
+                const uint64_t unit = PAIRED ? ((r + ri[w]) >> 1) : (r + ri[w]);
+                int vmin = (valid[w] && which[w] >= 0) ? which[w] : INT_MAX;
+                int vmax = (valid[w] && which[w] >= 0) ? which[w] : -1;
+                const uint64_t unit0 = __shfl(unit, 0);
+                if (cunit != ~0ull && unit0 != cunit) {  // the carried unit is complete
+                    amb += (cmax >= 0 && cmin != cmax) ? 1u : 0u;
+                    cunit = ~0ull;
                 }
+                if (lane == 0 && unit == cunit) {
+                    vmin = min(vmin, cmin);
+                    vmax = max(vmax, cmax);
+                }
+                const uint64_t uprev = __shfl_up(unit, 1);
+                const bool head = has[w] && (lane == 0 || unit != uprev);
+                const uint64_t heads = __ballot(head);
+                const uint64_t below = heads & ((lane == 63u) ? ~0ull : ((2ull << lane) - 1ull));
+                const uint32_t seg_start = 63u - (uint32_t)__clzll(below);
+                for (uint32_t d = 1; d < 64u; d <<= 1) {
+                    const int om = __shfl_up(vmin, d), oM = __shfl_up(vmax, d);
+                    if (lane >= d && lane - d >= seg_start) {
+                        vmin = min(vmin, om);
+                        vmax = max(vmax, oM);
+                    }
+                }
+                const bool tail = has[w] && (lane == last || ((heads >> (lane + 1u)) & 1ull));
+                const bool amb_lane = tail && lane != last && vmax >= 0 && vmin != vmax;
+                amb += (uint32_t)__popcll(__ballot(amb_lane));
+                cmin = __shfl(vmin, (int)last);
+                cmax = __shfl(vmax, (int)last);
+                cunit = __shfl(unit, (int)last);
             }
-            const bool tail = has && (lane == last || ((heads >> (lane + 1u)) & 1ull));
-            const bool amb_lane = tail && lane != last && vmax >= 0 && vmin != vmax;
-            amb += (uint32_t)__popcll(__ballot(amb_lane));
-            cmin = __shfl(vmin, (int)last);
-            cmax = __shfl(vmax, (int)last);
-            cunit = __shfl(unit, (int)last);
         }
         wave_sync();
         // ---- advance the cursor past the last window taken
-        r = __shfl(rr, (int)last);
-        o = __shfl(oo, (int)last) + 1;
+        o = (ri_last == 0 ? o : 0) + oo_last + 1;
+        r = r + ri_last;
     }
 
     if (MODE != KM_REF) {
@@ -500,6 +617,7 @@ struct speq_device_index {
     bool timing = false;
     uint32_t blocks_per_cu = 0;   // tuning: 0 = as many as registers/LDS allow; else pad LDS to cap occupancy
     uint32_t grid_blocks = 8192;  // tuning: upper bound of the grid
+    uint32_t ilp = 1;             // tuning: windows per lane searched concurrently (1 or 2; profiles/r01/sweep_ilp)
     uint32_t n_cus = 256;
     std::vector<std::pair<hipEvent_t, hipEvent_t>> events;
     double timed_ms = 0.0;
@@ -522,7 +640,9 @@ struct DeviceGuard {
 
 template <int MODE, bool PAIRED, bool LDS>
 void allow_big_lds() {
-    HIP_OK(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_scan<MODE, PAIRED, LDS>),
+    HIP_OK(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_scan<MODE, PAIRED, LDS, 1>),
+                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    HIP_OK(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_scan<MODE, PAIRED, LDS, 2>),
                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
 }
 
@@ -542,7 +662,10 @@ void allow_big_lds_all() {
 template <int MODE, bool PAIRED, bool LDS>
 void launch_t(const speq_device_index* d, const UnitSrc& src, uint32_t grid, size_t lds, hipStream_t st,
               unsigned long long* a, unsigned long long* b, double* w) {
-    hipLaunchKernelGGL((k_scan<MODE, PAIRED, LDS>), dim3(grid), dim3(BLOCK_THREADS), lds, st, d->view, src, a, b, w);
+    if (d->ilp == 2)
+        hipLaunchKernelGGL((k_scan<MODE, PAIRED, LDS, 2>), dim3(grid), dim3(BLOCK_THREADS), lds, st, d->view, src, a, b, w);
+    else
+        hipLaunchKernelGGL((k_scan<MODE, PAIRED, LDS, 1>), dim3(grid), dim3(BLOCK_THREADS), lds, st, d->view, src, a, b, w);
 }
 
 void launch_scan(const speq_device_index* d, int mode, bool paired, const UnitSrc& src, uint64_t work_units,
@@ -602,11 +725,12 @@ int speq_device_open(const speq_index* idx, int device, speq_device_index** out)
         v.occ2 = reinterpret_cast<const uint4*>(dev_upload(fm.occ2));
         v.runs = reinterpret_cast<const uint4*>(dev_upload(fm.runs));
         v.run_label = dev_upload(fm.run_label);
+        v.lab = dev_upload(fm.lab);
         v.prefix = reinterpret_cast<const uint2*>(dev_upload(fm.prefix));
         v.n = (uint32_t)fm.n;
         v.q = fm.prefix_q;
         v.G = fm.n_groups;
-        d->allocs = {(void*)v.occ, (void*)v.occ2, (void*)v.runs, (void*)v.run_label, (void*)v.prefix};
+        d->allocs = {(void*)v.occ, (void*)v.occ2, (void*)v.runs, (void*)v.run_label, (void*)v.lab, (void*)v.prefix};
         d->d_text = dev_upload(fm.text);
         d->d_text_start = dev_upload(fm.text_start);
         d->d_text_group = dev_upload(fm.text_group);
@@ -672,7 +796,7 @@ int speq_scan_reads_device(speq_device_index* d, const uint8_t* d_seq, const uin
         src.end_adj = 0;
         src.k = p->k;
         src.cutoff = p->phred_cutoff;
-        src.buf_bytes = staging_bytes(p->k);
+        src.buf_bytes = staging_bytes(p->k, d->ilp);
         const int mode = p->mode == SPEQ_MODE_LOCAL ? KM_LOCAL : KM_GLOBAL;
         hipEvent_t e0 = nullptr, e1 = nullptr;
         if (d->timing) {
@@ -779,7 +903,7 @@ int speq_ref_unique_device(speq_device_index* d, uint32_t k, uint64_t* d_u_ref, 
         src.total_windows = total;
         src.end_adj = 1;
         src.k = k;
-        src.buf_bytes = staging_bytes(k);
+        src.buf_bytes = staging_bytes(k, d->ilp);
         launch_scan(d, KM_REF, false, src, (total + 255) / 256, st, reinterpret_cast<unsigned long long*>(d_u_ref),
                     reinterpret_cast<unsigned long long*>(d_tot_ref), nullptr);
         HIP_OK(hipStreamSynchronize(st));  // d_cum is freed below
@@ -815,6 +939,9 @@ int speq_device_set_tuning(speq_device_index* d, const char* key, int64_t value)
         if (k == "blocks_per_cu") {
             if (value < 0 || value > 8) throw std::invalid_argument("blocks_per_cu must be in [0, 8]");
             d->blocks_per_cu = (uint32_t)value;
+        } else if (k == "ilp") {
+            if (value != 1 && value != 2) throw std::invalid_argument("ilp must be 1 or 2");
+            d->ilp = (uint32_t)value;
         } else if (k == "grid_blocks") {
             if (value < 1 || value > (1 << 20)) throw std::invalid_argument("grid_blocks must be in [1, 2^20]");
             d->grid_blocks = (uint32_t)value;

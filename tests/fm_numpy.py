@@ -40,6 +40,8 @@ class NumpyFm:
         self.n = int(index.info().n)
         self.q = int(index.info().prefix_q)
         self.prefix = index.array("prefix", np.uint32).reshape(-1, 2) if self.q else None
+        lab = index.array("lab", np.uint32)
+        self.lab = lab if lab.size else None
         occ2 = index.array("occ2", np.uint32)
         self.occ2 = occ2.reshape(-1, 4) if occ2.size else None
 
@@ -59,7 +61,8 @@ class NumpyFm:
     def run_of(self, i: np.ndarray) -> np.ndarray:
         return entry_rank(self.runs, i // BLOCK, i % BLOCK + 1)
 
-    def classify(self, kmers: np.ndarray, use_prefix: bool = True, use_pairs: bool = True) -> np.ndarray:
+    def classify(self, kmers: np.ndarray, use_prefix: bool = True, use_pairs: bool = True,
+                 use_lab: bool = True) -> np.ndarray:
         """kmers: (m, k) symbols 0..4. Returns -1 / -2 / group per row (same contract as the kernel)."""
         m, k = kmers.shape
         lo = np.zeros(m, dtype=np.int64)
@@ -112,7 +115,13 @@ class NumpyFm:
         if hit.any():
             rl = self.run_of(lo[hit])
             rh = self.run_of(hi[hit] - 1)
-            out[hit] = np.where(rl == rh, self.run_label[rl].astype(np.int64), -2)
+            by_runs = np.where(rl == rh, self.run_label[rl].astype(np.int64), -2)
+            if self.lab is not None and use_lab:  # the kernel's one-load path must agree with the rank path
+                x = self.lab[lo[hit]].astype(np.int64)
+                dist, width = x >> 16, hi[hit] - lo[hit]
+                by_lab = np.where(width <= dist, x & 0xFFFF, np.where(dist < 0xFFFF, -2, by_runs))
+                assert np.array_equal(by_lab, by_runs)
+            out[hit] = by_runs
         return out
 
 

@@ -18,8 +18,9 @@ pytestmark = pytest.mark.gpu
 @pytest.mark.parametrize("pairs", [False, True])
 def test_gpu_matches_golden(name, q, pairs):
     c = Case(name)
-    dev = DeviceIndex(FmIndex.build(c.records, c.groups, c.G, prefix_q=q, pair_steps=pairs))
-    for k in c.ks:
+    dev = DeviceIndex(FmIndex.build(c.records, c.groups, c.G, prefix_q=q, pair_steps=pairs, label_table=pairs))
+    for k, ilp in [(k, ilp) for k in c.ks for ilp in (1, 2)]:
+        dev.tune(ilp=ilp)
         e = c.exp["by_k"][str(k)]
         u, t = dev.count_unique_kmers_per_group(k)
         assert u.tolist() == e["u_ref"] and t.tolist() == e["tot_ref"], (name, k)

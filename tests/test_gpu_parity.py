@@ -14,7 +14,16 @@ pytestmark = pytest.mark.gpu
 W_RTOL = 1e-12
 
 
-def _check(dev, orc, reads, k, cutoff=30, paired=False, local=False):
+def _check(dev, orc, reads, k, cutoff=30, paired=False, local=False, ilps=(1, 2)):
+    """Every kernel variant (windows per lane = 1 and 2) must give the oracle's counts."""
+    for ilp in ilps:
+        dev.tune(ilp=ilp)
+        got = _check_one(dev, orc, reads, k, cutoff, paired, local)
+    dev.tune(ilp=1)
+    return got
+
+
+def _check_one(dev, orc, reads, k, cutoff, paired, local):
     got = dev.scan(reads.seq.tobytes(), reads.qual.tobytes(), reads.offsets, k=k, phred_cutoff=cutoff,
                    paired=paired, local=local)
     T, amb, U, W = orc.scan(reads.seq, reads.qual, reads.offsets, phred_cutoff=cutoff, paired=paired, local=local)
@@ -38,7 +47,7 @@ def cfg1():
 @pytest.mark.parametrize("pairs", [False, True])
 def test_config1_single(cfg1, q, local, pairs):
     ref, reads = cfg1
-    idx = FmIndex.build(ref.records, ref.groups, 3, prefix_q=q, pair_steps=pairs)
+    idx = FmIndex.build(ref.records, ref.groups, 3, prefix_q=q, pair_steps=pairs, label_table=pairs)
     dev = DeviceIndex(idx)
     orc = Oracle(ref.records, ref.groups, 3, 21)
     got = _check(dev, orc, reads, 21, local=local)
@@ -59,7 +68,7 @@ def edge():
 @pytest.mark.parametrize("pairs", [False, True])
 def test_edge_reads_all_k(edge, k, pairs):
     ref, reads = edge
-    idx = FmIndex.build(ref.records, ref.groups, 4, prefix_q=6, pair_steps=pairs)
+    idx = FmIndex.build(ref.records, ref.groups, 4, prefix_q=6, pair_steps=pairs, label_table=not pairs)
     dev = DeviceIndex(idx)
     orc = Oracle(ref.records, ref.groups, 4, k)
     _check(dev, orc, reads, k)
@@ -74,7 +83,7 @@ def test_edge_reads_all_k(edge, k, pairs):
 def test_paired(edge, local):
     ref, _ = edge
     reads = synth.make_reads(ref, 2_000, paired=True, n_rate=0.003, lowq_rate=0.01)
-    idx = FmIndex.build(ref.records, ref.groups, 4, prefix_q=8, pair_steps=True)
+    idx = FmIndex.build(ref.records, ref.groups, 4, prefix_q=8, pair_steps=True, label_table=True)
     dev = DeviceIndex(idx)
     for k in (21, 31, 64):
         orc = Oracle(ref.records, ref.groups, 4, k)
@@ -98,7 +107,7 @@ def test_many_groups_global_atomics():
     G = 2500
     ref = synth.make_reference(G, 1, 300)
     reads = synth.make_reads(ref, 4_000, read_len=100)
-    idx = FmIndex.build(ref.records, ref.groups, G, prefix_q=5, pair_steps=True)
+    idx = FmIndex.build(ref.records, ref.groups, G, prefix_q=5, pair_steps=True, label_table=True)
     dev = DeviceIndex(idx)
     orc = Oracle(ref.records, ref.groups, G, 25)
     _check(dev, orc, reads, 25)
@@ -113,7 +122,7 @@ def test_irregular_groupings():
     ref = synth.make_reference(6, 1, 4_000)
     reads = synth.make_reads(ref, 2_000)
     for groups, G in (([2, 0, 1, 2, 0, 1], 3), ([0] * 6, 1), ([5, 4, 3, 2, 1, 0], 6)):
-        idx = FmIndex.build(ref.records, groups, G, prefix_q=7)
+        idx = FmIndex.build(ref.records, groups, G, prefix_q=7, pair_steps=True, label_table=True)
         dev = DeviceIndex(idx)
         orc = Oracle(ref.records, groups, G, 19)
         _check(dev, orc, reads, 19)
@@ -154,7 +163,7 @@ def test_config2_full_size_vs_oracle():
     ref = synth.make_reference(c["n_variants"], c["n_isolates"], c["length"])
     reads = synth.make_reads(ref, c["n_reads"])
     G, k = c["n_variants"], c["k"]
-    idx = FmIndex.build(ref.records, ref.groups, G, prefix_q=12, pair_steps=True)
+    idx = FmIndex.build(ref.records, ref.groups, G, prefix_q=11, pair_steps=True, label_table=True)
     dev = DeviceIndex(idx)
     orc = Oracle(ref.records, ref.groups, G, k)
     full = _check(dev, orc, reads, k)
@@ -182,3 +191,15 @@ def test_config2_full_size_vs_oracle():
     u, t = dev.count_unique_kmers_per_group(k)
     ou, ot = orc.ref_unique()
     assert np.array_equal(u, ou) and np.array_equal(t, ot)
+
+
+def test_label_table_saturation_gpu():
+    """Single-group runs longer than 65535 SA positions: wide intervals take the rank fallback of classify()."""
+    ref = synth.make_reference(2, 2, 120_000)
+    reads = synth.make_reads(ref, 3_000, read_len=40)
+    for groups, G in (([0, 0, 0, 0], 1), ([0, 0, 0, 1], 2)):
+        idx = FmIndex.build(ref.records, groups, G, prefix_q=0, pair_steps=True, label_table=True)
+        dev = DeviceIndex(idx)
+        for k in (1, 3, 12):
+            orc = Oracle(ref.records, groups, G, k)
+            _check(dev, orc, reads, k)

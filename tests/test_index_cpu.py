@@ -140,3 +140,17 @@ def test_load_rejects_garbage(tmp_path):
     assert e.value.code == SPEQ_E_IO
     with pytest.raises(SpeqError):
         FmIndex.load(str(tmp_path / "missing.idx"))
+
+
+def test_label_table_saturated_runs():
+    """Label runs longer than 65535 positions saturate the table's distance; wide intervals (k = 1, 2) must then
+    fall back to the rank path and still classify exactly (NumpyFm asserts table == rank path)."""
+    ref = synth.make_reference(1, 2, 150_000)
+    groups = [0, 0]
+    idx = FmIndex.build(ref.records, groups, 2, prefix_q=0, label_table=True)  # group 1 is empty
+    fm = NumpyFm(idx)
+    assert fm.lab is not None and (fm.lab >> 16).max() == 0xFFFF
+    for k in (1, 2, 9):
+        kmers = np.array([[s % 4 for s in range(j, j + k)] for j in range(16)])
+        got = fm.classify(kmers)
+        assert set(got.tolist()) <= {0, -1}
