@@ -17,7 +17,7 @@ OBJDIR   := build/obj
 
 LIB_HIP  := speq_amd/csrc/scan_kernels.hip
 LIB_CPP  := speq_amd/csrc/sais.cpp speq_amd/csrc/fm_index.cpp speq_amd/csrc/capi.cpp speq_amd/csrc/comm.cpp \
-            speq_amd/csrc/host_io.cpp
+            speq_amd/csrc/host_io.cpp speq_amd/csrc/em.cpp
 CLI_CPP  := speq_amd/cli/speq_main.cpp
 
 LIB_OBJS := $(patsubst speq_amd/csrc/%.hip,$(OBJDIR)/%.o,$(LIB_HIP)) \

@@ -150,6 +150,31 @@ int speq_comm_destroy(void* comm);
 int speq_allreduce_u64(void* comm, uint64_t* d_buf, uint64_t count, void* stream);
 int speq_allreduce_f64(void* comm, double* d_buf, uint64_t count, void* stream);
 
+/* ---- EM refinement (reference: fm_scanner.cpp:1069-1453 and the loops at :248-279) ----
+ * The reference re-reads and re-searches all reads in every EM iteration. Here ONE scan records, for every passing
+ * window whose occurrences span >= 2 groups, its SA interval (a window's EM weight depends only on the per-group
+ * occurrence counts of its k-mer; the per-window factor temp_acc/qavg cancels), and every iteration is a sweep
+ * over that histogram:
+ *   speq_em_create -> speq_em_scan_reads[_device] (any number of batches; also returns the normal counters)
+ *   -> speq_em_finalize -> speq_em_step per iteration.
+ * The speq_index and the device replica must outlive the histogram. */
+typedef struct speq_em speq_em;
+int speq_em_create(const speq_index* idx, speq_device_index* d, speq_em** out);
+int speq_em_scan_reads(speq_em* em, const uint8_t* seq, const uint8_t* qual, const uint64_t* offsets,
+                       uint64_t n_reads, const speq_scan_params* params, uint64_t* counts, double* weights);
+int speq_em_scan_reads_device(speq_em* em, const uint8_t* d_seq, const uint8_t* d_qual, const uint64_t* d_offsets,
+                              uint64_t n_reads, const speq_scan_params* params, uint64_t* d_counts,
+                              double* d_weights, void* stream);
+/* Downloads the histogram and builds one row per distinct interval {multiplicity, (group, count)...}. */
+int speq_em_finalize(speq_em* em, uint32_t threads);
+int speq_em_info(const speq_em* em, uint64_t* n_intervals, uint64_t* n_entries, uint64_t* n_windows);
+/* next[g] = sum over passing windows with hits of (c_g p_g / n_g) / sum_j (c_j p_j / n_j) (windows with a
+ * non-positive sum skipped), given percent[G], group_counts[G] (the "(count)" of each groupings line) and
+ * unique[G] (the U[g] counters of the same scan, i.e. its single-group windows). */
+int speq_em_step(const speq_em* em, const double* percent, const int32_t* group_counts, const uint64_t* unique,
+                 double* next);
+void speq_em_free(speq_em* em);
+
 /* ---- groupings file (speq::file_to_map, /root/reference/src/file_to_map.cpp:20-119) ----
  * Same grammar "Name(count): i, j-k, …"; parse errors of single tokens are collected (the reference prints
  * them to std::cerr) and returned by speq_groupings_errors(). A missing "(count)" fails with SPEQ_E_ARG

@@ -20,6 +20,8 @@
  *   Phred weight w = fold(w / (1 - 1/10^(q/10)))         src/fm_scanner.cpp:454
  *   paired: both mates share one read state               src/fm_scanner.cpp:709-729 (global), :963-995 (local)
  *   reference-uniqueness (.dat) pass                      src/fm_scanner.cpp:1503-1539
+ *   EM estimator pass (global temp_acc / local qavg)      src/fm_scanner.cpp:1087-1125, :1175-1219, :1273-1311,
+ *                                                         :1370-1415
  * dna5 conversion (ACGT/acgt, U->T, other->N) and phred42 clamping [0,41] follow SeqAn 3.0.1 (upstream,
  * believed).
  */
@@ -41,6 +43,10 @@ typedef struct {
     uint64_t cap;           /* hash table capacity (power of two) */
     uint64_t* slot_pos;     /* window start + 1 (0 = empty) */
     int32_t* slot_label;    /* group, or -2 when the k-mer occurs in >= 2 groups */
+    int64_t* slot_first;    /* head of the k-mer's occurrence list (index into occ_*), -1 = none */
+    uint32_t* occ_text;     /* text id of an occurrence */
+    int64_t* occ_next;      /* next occurrence of the same k-mer */
+    uint64_t n_occ;
 } oracle_t;
 
 static uint8_t dna5(unsigned char c) {
@@ -80,6 +86,7 @@ static int32_t lookup(const oracle_t* o, const uint8_t* q) {
 void oracle_free(oracle_t* o) {
     if (!o) return;
     free(o->text); free(o->text_start); free(o->text_group); free(o->slot_pos); free(o->slot_label);
+    free(o->slot_first); free(o->occ_text); free(o->occ_next);
     free(o);
 }
 
@@ -115,6 +122,9 @@ oracle_t* oracle_build(const char* seq, const uint64_t* rec_off, uint32_t n_reco
     o->cap = cap;
     o->slot_pos = (uint64_t*)calloc(cap, sizeof(uint64_t));
     o->slot_label = (int32_t*)malloc(sizeof(int32_t) * cap);
+    o->slot_first = (int64_t*)malloc(sizeof(int64_t) * cap);
+    o->occ_text = (uint32_t*)malloc(sizeof(uint32_t) * (n_windows + 1));
+    o->occ_next = (int64_t*)malloc(sizeof(int64_t) * (n_windows + 1));
     for (uint32_t t = 0; t < 2 * n_records; ++t) {
         uint64_t s = o->text_start[t], e = o->text_start[t + 1] - 1;
         if (e - s < k) continue;
@@ -123,9 +133,16 @@ oracle_t* oracle_build(const char* seq, const uint64_t* rec_off, uint32_t n_reco
             uint64_t m = cap - 1, i = hash_kmer(kp, k) & m;
             for (;;) {
                 uint64_t sp = o->slot_pos[i];
-                if (!sp) { o->slot_pos[i] = w + 1; o->slot_label[i] = o->text_group[t]; break; }
-                if (memcmp(o->text + (sp - 1), kp, k) == 0) {
-                    if (o->slot_label[i] != o->text_group[t]) o->slot_label[i] = -2;
+                if (!sp) {
+                    o->slot_pos[i] = w + 1;
+                    o->slot_label[i] = o->text_group[t];
+                    o->slot_first[i] = -1;
+                }
+                if (!sp || memcmp(o->text + (sp - 1), kp, k) == 0) {
+                    if (sp && o->slot_label[i] != o->text_group[t]) o->slot_label[i] = -2;
+                    o->occ_text[o->n_occ] = t;
+                    o->occ_next[o->n_occ] = o->slot_first[i];
+                    o->slot_first[i] = (int64_t)o->n_occ++;
                     break;
                 }
                 i = (i + 1) & m;
@@ -133,6 +150,16 @@ oracle_t* oracle_build(const char* seq, const uint64_t* rec_off, uint32_t n_reco
         }
     }
     return o;
+}
+
+static int64_t find_slot(const oracle_t* o, const uint8_t* q) {
+    uint64_t m = o->cap - 1, i = hash_kmer(q, o->k) & m;
+    for (;;) {
+        uint64_t p = o->slot_pos[i];
+        if (!p) return -1;
+        if (memcmp(o->text + (p - 1), q, o->k) == 0) return (int64_t)i;
+        i = (i + 1) & m;
+    }
 }
 
 /* Label of an arbitrary ASCII k-mer (for tests). */
@@ -231,5 +258,63 @@ int oracle_ref_unique(const oracle_t* o, uint64_t* u_ref, uint64_t* tot_ref) {
             if (lookup(o, o->text + w) == g) ++u_ref[g];
         }
     }
+    return 0;
+}
+
+/*
+ * One EM estimator pass, literally as the reference runs it (single-end global src/fm_scanner.cpp:1087-1125, local
+ * :1175-1219, paired :1273-1311 / :1370-1415): for every passing window, hits_per_group_int[g] += f for each
+ * occurrence in a text of group g (f = 1/pp - (1 - pp) in global mode, qavg = fold(a / (1 - 10^(-b/10))) -
+ * (1 - fold(a * (1 - 10^(-b/10)))) in local mode), a[i] = hits_per_group_int[i] * percent[i] / counts[i],
+ * norm = sum a[i] (i in order), and if norm > 0, next[i] += a[i] / norm. Single-threaded. next is overwritten.
+ */
+int oracle_em_pass(const oracle_t* o, const char* seq, const char* qual, const uint64_t* off, uint64_t n_reads,
+                   int paired, uint32_t cutoff, int mode, double percent_perfect, const double* percent,
+                   const int32_t* group_counts, double* next) {
+    const uint32_t G = o->n_groups, k = o->k;
+    if (paired && (n_reads & 1)) return -1;
+    memset(next, 0, sizeof(double) * G);
+    double* h = (double*)malloc(sizeof(double) * G);
+    double* a = (double*)malloc(sizeof(double) * G);
+    size_t cap = 1 << 16;
+    uint8_t* sb = (uint8_t*)malloc(cap);
+    uint8_t* qb = (uint8_t*)malloc(cap);
+    for (uint64_t r = 0; r < n_reads; ++r) {
+        uint64_t b = off[r], L = off[r + 1] - b;
+        if (L > cap) { cap = L; sb = (uint8_t*)realloc(sb, cap); qb = (uint8_t*)realloc(qb, cap); }
+        for (uint64_t i = 0; i < L; ++i) {
+            sb[i] = dna5((unsigned char)seq[b + i]);
+            int q = (int)(unsigned char)qual[b + i] - 33;
+            qb[i] = (uint8_t)(q < 0 ? 0 : (q > 41 ? 41 : q));
+        }
+        if (L < k) continue;
+        for (uint64_t j = 0; j + k <= L; ++j) {
+            int pass = 1;
+            for (uint32_t i = 0; i < k; ++i)
+                if (qb[j + i] <= cutoff || sb[j + i] == 'N') { pass = 0; break; }
+            if (!pass) continue;
+            double f;
+            if (mode == 0) {
+                f = 1.0 / percent_perfect - (1 - percent_perfect);
+            } else {
+                double x = 1.0, y = 1.0;
+                for (uint32_t i = 0; i < k; ++i) x = x / (1.0 - 1.0 / pow(10.0, (double)qb[j + i] / 10.0));
+                for (uint32_t i = 0; i < k; ++i) y = y * (1.0 - 1.0 / pow(10.0, (double)qb[j + i] / 10.0));
+                f = x - (1.0 - y);
+            }
+            for (uint32_t g = 0; g < G; ++g) h[g] = 0.0;
+            int64_t s = find_slot(o, sb + j);
+            if (s >= 0)
+                for (int64_t x = o->slot_first[s]; x >= 0; x = o->occ_next[x]) h[o->text_group[o->occ_text[x]]] += f;
+            double norm = 0.0;
+            for (uint32_t g = 0; g < G; ++g) {
+                a[g] = h[g] * percent[g] / group_counts[g];
+                norm += a[g];
+            }
+            if (norm > 0.0)
+                for (uint32_t g = 0; g < G; ++g) next[g] += a[g] / norm;
+        }
+    }
+    free(h); free(a); free(sb); free(qb);
     return 0;
 }

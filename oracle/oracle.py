@@ -38,6 +38,9 @@ def lib() -> C.CDLL:
         L.oracle_scan.restype = C.c_int
         L.oracle_scan.argtypes = [P, C.c_char_p, C.c_char_p, U64P, C.c_uint64, C.c_int, C.c_uint32, C.c_int, U64P,
                                   C.POINTER(C.c_double), C.c_int]
+        L.oracle_em_pass.restype = C.c_int
+        L.oracle_em_pass.argtypes = [P, C.c_char_p, C.c_char_p, U64P, C.c_uint64, C.c_int, C.c_uint32, C.c_int,
+                                     C.c_double, C.POINTER(C.c_double), C.POINTER(C.c_int32), C.POINTER(C.c_double)]
         L.oracle_ref_unique.restype = C.c_int
         L.oracle_ref_unique.argtypes = [P, U64P, U64P]
         _lib = L
@@ -80,6 +83,23 @@ class Oracle:
         if rc != 0:
             raise ValueError("oracle_scan: bad arguments")
         return int(counts[0]), int(counts[1]), counts[2:].copy(), w
+
+    def em_pass(self, seq, qual, offsets, percent, group_counts, phred_cutoff: int = 30, paired: bool = False,
+                local: bool = False, percent_perfect: float = 1.0):
+        """One literal EM estimator pass of the reference; returns next_tkpg[G]."""
+        seq_b = seq.tobytes() if isinstance(seq, np.ndarray) else bytes(seq)
+        qual_b = qual.tobytes() if isinstance(qual, np.ndarray) else bytes(qual)
+        off = np.ascontiguousarray(offsets, dtype=np.uint64)
+        p = np.ascontiguousarray(percent, dtype=np.float64)
+        gc = np.ascontiguousarray(group_counts, dtype=np.int32)
+        nxt = np.zeros(self.G, dtype=np.float64)
+        dp = C.POINTER(C.c_double)
+        rc = lib().oracle_em_pass(self._h, seq_b, qual_b, _u64p(off), len(off) - 1, int(paired), phred_cutoff,
+                                  1 if local else 0, percent_perfect, p.ctypes.data_as(dp),
+                                  gc.ctypes.data_as(C.POINTER(C.c_int32)), nxt.ctypes.data_as(dp))
+        if rc != 0:
+            raise ValueError("oracle_em_pass: bad arguments")
+        return nxt
 
     def ref_unique(self):
         u = np.zeros(self.G, dtype=np.uint64)

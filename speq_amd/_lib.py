@@ -69,6 +69,14 @@ SIGNATURES = {
     "speq_comm_destroy": (C.c_int, [_P]),
     "speq_allreduce_u64": (C.c_int, [_P, _P, C.c_uint64, _P]),
     "speq_allreduce_f64": (C.c_int, [_P, _P, C.c_uint64, _P]),
+    "speq_em_create": (C.c_int, [_P, _P, C.POINTER(_P)]),
+    "speq_em_scan_reads": (C.c_int, [_P, C.c_char_p, C.c_char_p, _U64P, C.c_uint64, C.POINTER(ScanParams),
+                                     _U64P, _F64P]),
+    "speq_em_scan_reads_device": (C.c_int, [_P, _P, _P, _P, C.c_uint64, C.POINTER(ScanParams), _P, _P, _P]),
+    "speq_em_finalize": (C.c_int, [_P, C.c_uint32]),
+    "speq_em_info": (C.c_int, [_P, _U64P, _U64P, _U64P]),
+    "speq_em_step": (C.c_int, [_P, _F64P, _I32P, _U64P, _F64P]),
+    "speq_em_free": (None, [_P]),
     "speq_groupings_parse": (C.c_int, [C.c_char_p, C.POINTER(_P)]),
     "speq_groupings_n_groups": (C.c_uint32, [_P]),
     "speq_groupings_name": (C.c_char_p, [_P, C.c_uint32]),

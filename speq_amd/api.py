@@ -22,8 +22,8 @@ import numpy as np
 
 from ._lib import (SPEQ_MODE_GLOBAL, SPEQ_MODE_LOCAL, BuildOpts, IndexInfo, ScanParams, SpeqError, check, lib)
 
-__all__ = ["FmIndex", "DeviceIndex", "ScanResult", "Groupings", "file_to_map", "unique_to_percent",
-           "pack_records", "SpeqError", "SPEQ_MODE_GLOBAL", "SPEQ_MODE_LOCAL"]
+__all__ = ["FmIndex", "DeviceIndex", "ScanResult", "Groupings", "EmHistogram", "file_to_map", "unique_to_percent",
+           "em_refine", "pack_records", "SpeqError", "SPEQ_MODE_GLOBAL", "SPEQ_MODE_LOCAL"]
 
 
 def _u64p(a: np.ndarray):
@@ -213,3 +213,82 @@ class DeviceIndex:
             self.close()
         except Exception:
             pass
+
+
+class EmHistogram:
+    """{multi-group SA interval -> multiplicity} of the passing windows of a read set (include/speq_scan.h, EM).
+
+    Replaces the reference's re-scan of every read in every EM iteration (fm_scanner.cpp:1069-1453): one GPU scan
+    fills the histogram, then every iteration is a host sweep over it (step)."""
+
+    def __init__(self, dev: "DeviceIndex"):
+        self.dev = dev
+        self.n_groups = dev.n_groups
+        h = C.c_void_p()
+        check(lib().speq_em_create(dev.index.handle, dev.handle, C.byref(h)))
+        self._h = h
+
+    def scan(self, seq: bytes, qual: bytes, offsets: np.ndarray, k: int, phred_cutoff: int = 30,
+             paired: bool = False, local: bool = False) -> ScanResult:
+        off = np.ascontiguousarray(offsets, dtype=np.uint64)
+        G = self.n_groups
+        counts = np.zeros(G + 2, dtype=np.uint64)
+        w = np.zeros(G, dtype=np.float64) if local else None
+        p = ScanParams(k, phred_cutoff, int(paired), SPEQ_MODE_LOCAL if local else SPEQ_MODE_GLOBAL)
+        check(lib().speq_em_scan_reads(self._h, seq, qual, _u64p(off), len(off) - 1, C.byref(p), _u64p(counts),
+                                       w.ctypes.data_as(C.POINTER(C.c_double)) if w is not None else None))
+        return ScanResult(int(counts[0]), int(counts[1]), counts[2:].copy(), w)
+
+    def finalize(self, threads: int = 0) -> None:
+        check(lib().speq_em_finalize(self._h, threads))
+
+    def info(self) -> tuple[int, int, int]:
+        a, b, c = C.c_uint64(), C.c_uint64(), C.c_uint64()
+        check(lib().speq_em_info(self._h, C.byref(a), C.byref(b), C.byref(c)))
+        return a.value, b.value, c.value
+
+    def step(self, percent, group_counts, unique) -> np.ndarray:
+        p = np.ascontiguousarray(percent, dtype=np.float64)
+        gc = np.ascontiguousarray(group_counts, dtype=np.int32)
+        u = np.ascontiguousarray(unique, dtype=np.uint64)
+        nxt = np.zeros(self.n_groups, dtype=np.float64)
+        dp = C.POINTER(C.c_double)
+        check(lib().speq_em_step(self._h, p.ctypes.data_as(dp), gc.ctypes.data_as(C.POINTER(C.c_int32)), _u64p(u),
+                                 nxt.ctypes.data_as(dp)))
+        return nxt
+
+    def close(self):
+        if self._h:
+            lib().speq_em_free(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def em_refine(step, unique_totals, total, percent0, precision: float = 1e-6, max_iterations: int = 1000):
+    """The reference's refinement loop (fm_scanner.cpp:248-279): starting from diff = 1.0 per group, while
+    max(diff) > precision: next_tkpg = step(percent); percent' = unique_to_percent(unique_totals, total,
+    unique_totals, next_tkpg); diff = |percent' - percent|. Returns [(percent', next_tkpg), ...] per iteration."""
+    percent = list(percent0)
+    out = []
+    diff = [1.0] * len(percent)
+    while _max_element(diff) > precision and len(out) < max_iterations:
+        nxt = step(np.asarray(percent, dtype=np.float64))
+        new = unique_to_percent(unique_totals, total, unique_totals, nxt)
+        diff = [abs(x - y) for x, y in zip(new, percent)]
+        percent = new
+        out.append((list(new), [float(x) for x in nxt]))
+    return out
+
+
+def _max_element(v):
+    """std::max_element with operator< (NaN never compares greater, so a leading NaN wins)."""
+    best = v[0]
+    for x in v[1:]:
+        if best < x:
+            best = x
+    return best

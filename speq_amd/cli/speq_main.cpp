@@ -5,6 +5,7 @@
 //   speq::fm::index             /root/reference/src/fm_indexer.cpp:55-111
 //   speq::scan::async_one/two   /root/reference/src/fm_scanner.cpp:5-32 and the four mode variants
 //   .dat cache                  /root/reference/src/fm_scanner.cpp:79-135, :1561-1571
+#include <algorithm>
 #include <chrono>
 #include <cmath>
 #include <cstdio>
@@ -388,6 +389,9 @@ int run_scan(CmdArguments& a) {
     speq_scan_params prm{a.kmer, a.phred_cutoff, paired ? 1u : 0u, local ? (uint32_t)SPEQ_MODE_LOCAL : (uint32_t)SPEQ_MODE_GLOBAL};
     std::vector<uint64_t> counts(G + 2, 0), part(G + 2);
     std::vector<double> weights(G, 0.0), wpart(G);
+    // One scan also fills the EM histogram (the reference re-scans every read per EM iteration instead).
+    speq_em* em = nullptr;
+    ok(speq_em_create(idx, d, &em), "allocating the EM histogram");
     const uint64_t BATCH_RECORDS = 1u << 21, BATCH_BYTES = 512ull << 20;
     speq::FastqReader r1(a.in_file_reads_path_1.string());
     std::unique_ptr<speq::FastqReader> r2;
@@ -416,9 +420,9 @@ int run_scan(CmdArguments& a) {
         }
         const uint64_t n = batch.size();
         if (n == 0) break;
-        ok(speq_scan_reads(d, reinterpret_cast<const uint8_t*>(batch.seq.data()),
-                           reinterpret_cast<const uint8_t*>(batch.qual.data()), batch.offsets.data(), n, &prm,
-                           part.data(), local ? wpart.data() : nullptr),
+        ok(speq_em_scan_reads(em, reinterpret_cast<const uint8_t*>(batch.seq.data()),
+                              reinterpret_cast<const uint8_t*>(batch.qual.data()), batch.offsets.data(), n, &prm,
+                              part.data(), local ? wpart.data() : nullptr),
            "scanning reads");
         for (size_t i = 0; i < G + 2; ++i) counts[i] += part[i];
         if (local)
@@ -440,7 +444,32 @@ int run_scan(CmdArguments& a) {
     std::cerr << total << "\t" << ambiguous << "\n";
     if (local && paired) std::cerr << "[({}," << ambiguous << ")]\n";  // fusion map: key always {} (:916)
 
-    // The reference writes nothing to -o (quirk B1); we write the percentage vector there.
+    // EM refinement (fm_scanner.cpp:248-279, :515-545, :761-792, :1035-1065) over the histogram.
+    ok(speq_em_finalize(em, a.threads), "building the EM histogram");
+    std::vector<uint64_t> unique(counts.begin() + 2, counts.end());
+    std::vector<double> diff(G, 1.0), next(G);
+    for (unsigned it = 0; G > 0 && *std::max_element(diff.begin(), diff.end()) > a.precision; ++it) {
+        if (it >= a.max_em_iterations) {
+            std::cerr << "speq: EM stopped after " << it << " iterations (--max-em-iterations)\n";
+            break;
+        }
+        ok(speq_em_step(em, percent.data(), h.counts.data(), unique.data(), next.data()), "EM step");
+        if (local && !paired)
+            std::cerr << "1: " << speq::format_vector(unique_totals) << "\n2: " << total << "\n3: "
+                      << speq::format_vector(next) << "\n";
+        std::vector<double> np = unique_to_percent(unique_totals, total, unique_totals, next);
+        for (size_t i = 0; i < G; ++i) diff[i] = std::fabs(np[i] - percent[i]);
+        percent = np;
+        if (local && !paired) {
+            std::cerr << "Percent of each group: " << speq::format_vector(percent) << "\n";
+            std::cerr << "Total Kmers per group: " << speq::format_vector(next) << "\n\n";
+        } else {
+            std::cerr << speq::format_vector(percent) << "\n" << speq::format_vector(next) << "\n\n";
+        }
+    }
+    speq_em_free(em);
+
+    // The reference writes nothing to -o (quirk B1); we write the (refined) percentage vector there.
     {
         std::ofstream of(a.out_file_path);
         if (!of) throw CApiError("cannot write " + a.out_file_path.string());

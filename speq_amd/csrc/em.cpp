@@ -1,0 +1,149 @@
+// Host half of the EM refinement: histogram rows and the EM step (see em.hpp).
+#include "em.hpp"
+
+#include <algorithm>
+#include <cmath>
+#include <limits>
+#include <thread>
+
+namespace speq {
+
+void em_build_rows(speq_em& em, const std::vector<uint32_t>& mult, const std::vector<uint32_t>& hi, uint32_t threads) {
+    const FmIndex& fm = em.idx->fm;
+    const uint64_t n = em.n;
+    if (threads == 0) threads = std::max(1u, std::thread::hardware_concurrency());
+    threads = std::max<uint32_t>(1, std::min<uint64_t>(threads, n / 65536 + 1));
+    struct Part {
+        std::vector<uint64_t> mult, nnz;
+        std::vector<uint32_t> grp, cnt;
+    };
+    std::vector<Part> parts(threads);
+    std::vector<std::thread> pool;
+    const uint64_t chunk = (n + threads - 1) / threads;
+    for (uint32_t t = 0; t < threads; ++t) {
+        pool.emplace_back([&, t] {
+            Part& P = parts[t];
+            std::vector<uint32_t> dense(em.G, 0);
+            std::vector<uint32_t> touched;
+            const uint64_t b = t * chunk, e = std::min(n, b + chunk);
+            for (uint64_t lo = b; lo < e; ++lo) {
+                if (!mult[lo]) continue;
+                const uint64_t h = hi[lo];
+                // per-group occurrence counts c_g = overlap of [lo, h) with the label runs of group g
+                for (uint64_t i = lo; i < h;) {
+                    const uint64_t j = std::min<uint64_t>(fm.run_end(i), h);
+                    const uint16_t g = fm.label_at(i);
+                    if (!dense[g]) touched.push_back(g);
+                    dense[g] += (uint32_t)(j - i);
+                    i = j;
+                }
+                std::sort(touched.begin(), touched.end());  // the reference sums groups in index order
+                P.mult.push_back(mult[lo]);
+                P.nnz.push_back(touched.size());
+                for (uint32_t g : touched) {
+                    P.grp.push_back(g);
+                    P.cnt.push_back(dense[g]);
+                    dense[g] = 0;
+                }
+                touched.clear();
+            }
+        });
+    }
+    for (auto& th : pool) th.join();
+    em.row_mult.clear();
+    em.row_ptr.assign(1, 0);
+    em.col_group.clear();
+    em.col_count.clear();
+    for (auto& P : parts) {
+        em.row_mult.insert(em.row_mult.end(), P.mult.begin(), P.mult.end());
+        for (uint64_t z : P.nnz) em.row_ptr.push_back(em.row_ptr.back() + z);
+        em.col_group.insert(em.col_group.end(), P.grp.begin(), P.grp.end());
+        em.col_count.insert(em.col_count.end(), P.cnt.begin(), P.cnt.end());
+    }
+    em.finalized = true;
+}
+
+}  // namespace speq
+
+extern "C" {
+
+int speq_em_info(const speq_em* em, uint64_t* n_intervals, uint64_t* n_entries, uint64_t* n_windows) {
+    return speq::guarded([&] {
+        if (!em || !em->finalized) throw std::invalid_argument("speq_em_info: histogram not finalized");
+        if (n_intervals) *n_intervals = em->row_mult.size();
+        if (n_entries) *n_entries = em->col_group.size();
+        if (n_windows) {
+            uint64_t s = 0;
+            for (uint64_t m : em->row_mult) s += m;
+            *n_windows = s;
+        }
+    });
+}
+
+// One EM step (fm_scanner.cpp:1098-1120 global, :1186-1214 local): for every passing window with hits,
+// a_i = c_i p_i / n_i, norm = sum_i a_i (group order), and if norm > 0, next_i += a_i / norm.
+int speq_em_step(const speq_em* em, const double* percent, const int32_t* group_counts, const uint64_t* unique,
+                 double* next) {
+    return speq::guarded([&] {
+        if (!em || !percent || !group_counts || !unique || !next) throw std::invalid_argument("speq_em_step: null argument");
+        if (!em->finalized) throw std::invalid_argument("speq_em_step: histogram not finalized");
+        const uint32_t G = em->G;
+        std::vector<double> coef(G);  // p_i / n_i, evaluated as (c * p) / n below
+        bool clean = true;            // every "0 * p_i / n_i" term is exactly 0 (no n_i == 0, finite p_i)
+        for (uint32_t g = 0; g < G; ++g) {
+            const double z = 0.0 * percent[g] / (double)group_counts[g];
+            if (!(z == 0.0)) clean = false;
+        }
+        std::fill(next, next + G, 0.0);
+        const uint64_t R = em->row_mult.size();
+        if (clean) {
+            // single-group windows: a / a = 1 when a = c p_g / n_g > 0 (c >= 1), else norm == 0 and they are skipped
+            for (uint32_t g = 0; g < G; ++g) {
+                const double a = percent[g] / (double)group_counts[g];
+                if (a > 0.0) next[g] += (double)unique[g];
+            }
+            std::vector<double> a;
+            for (uint64_t r = 0; r < R; ++r) {
+                const uint64_t b = em->row_ptr[r], e = em->row_ptr[r + 1];
+                a.resize(e - b);
+                double norm = 0.0;
+                for (uint64_t x = b; x < e; ++x) {
+                    const uint32_t g = em->col_group[x];
+                    a[x - b] = (double)em->col_count[x] * percent[g] / (double)group_counts[g];
+                    norm += a[x - b];
+                }
+                if (norm > 0.0) {
+                    const double m = (double)em->row_mult[r];
+                    for (uint64_t x = b; x < e; ++x) next[em->col_group[x]] += m * (a[x - b] / norm);
+                }
+            }
+        } else {
+            // IEEE edge cases (a group count of 0, non-finite percentages): evaluate every group of every row
+            // exactly as the reference does, zero terms included.
+            std::vector<double> a(G);
+            auto window = [&](const uint32_t* grp, const uint32_t* cnt, uint64_t nnz, double m) {
+                std::vector<double> h(G, 0.0);
+                for (uint64_t x = 0; x < nnz; ++x) h[grp[x]] = (double)cnt[x];
+                double norm = 0.0;
+                for (uint32_t g = 0; g < G; ++g) {
+                    a[g] = h[g] * percent[g] / (double)group_counts[g];
+                    norm += a[g];
+                }
+                if (norm > 0.0)
+                    for (uint32_t g = 0; g < G; ++g) next[g] += m * (a[g] / norm);
+            };
+            for (uint32_t g = 0; g < G; ++g) {
+                if (!unique[g]) continue;
+                const uint32_t one = 1;
+                window(&g, &one, 1, (double)unique[g]);
+            }
+            for (uint64_t r = 0; r < R; ++r) {
+                const uint64_t b = em->row_ptr[r];
+                window(em->col_group.data() + b, em->col_count.data() + b, em->row_ptr[r + 1] - b,
+                       (double)em->row_mult[r]);
+            }
+        }
+    });
+}
+
+}  // extern "C"

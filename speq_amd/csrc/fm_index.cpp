@@ -93,6 +93,22 @@ uint32_t FmIndex::lf2(uint8_t a, uint8_t b, uint64_t i) const {
     return entry_rank(occ2[(uint64_t)((a - SYM_A) * 4 + (b - SYM_A)) * n_blocks() + blk], r);
 }
 
+uint64_t FmIndex::run_end(uint64_t i) const {
+    // first j > i with B[j] = 1 (a label boundary), scanning the run bitvector entry by entry
+    for (uint64_t j = i + 1; j < n;) {
+        const uint64_t b = j / OCC_BLOCK;
+        const uint32_t r = (uint32_t)(j - b * OCC_BLOCK);
+        const OccEntry& e = runs[b];
+        for (uint32_t w = r / 32; w < 3; ++w) {
+            uint32_t bits = e.bits[w];
+            if (w == r / 32) bits &= ~0u << (r % 32);
+            if (bits) return std::min<uint64_t>(n, b * OCC_BLOCK + w * 32 + (uint64_t)__builtin_ctz(bits));
+        }
+        j = (b + 1) * OCC_BLOCK;
+    }
+    return n;
+}
+
 uint32_t FmIndex::run_of(uint64_t i) const {
     uint64_t b = i / OCC_BLOCK;
     uint32_t r = (uint32_t)(i - b * OCC_BLOCK);

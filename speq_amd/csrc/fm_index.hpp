@@ -87,6 +87,8 @@ struct FmIndex {
     uint32_t lf2(uint8_t a, uint8_t b, uint64_t i) const;  // two-symbol LF (requires occ2)
     uint32_t rank(uint8_t sym, uint64_t i) const;
     uint32_t run_of(uint64_t i) const;   // index of the label run holding SA position i
+    uint64_t run_end(uint64_t i) const;  // one past the last position of the label run holding i
+    uint16_t label_at(uint64_t i) const { return run_label[run_of(i)]; }
 };
 
 // Builds the index (throws std::invalid_argument / std::runtime_error).

@@ -31,6 +31,7 @@
 #include <vector>
 
 #include "capi_internal.hpp"
+#include "em.hpp"
 #include "fm_index.hpp"
 
 namespace {
@@ -60,6 +61,8 @@ struct UnitSrc {
     const uint64_t* cum_win;  // ref only: prefix sums of windows per text
     const int32_t* unit_group;  // ref only: group of each text
     const double* qlut;       // local only: 1 - 10^(-q/10), q = 0..41
+    uint32_t* em_mult;        // optional: per SA position, # passing multi-group windows whose interval starts there
+    uint32_t* em_hi;          // optional: the end of that interval
     uint64_t n_units;         // reads (not pairs) or texts
     uint64_t total_windows;   // ref only
     uint32_t end_adj;
@@ -180,7 +183,7 @@ __device__ __forceinline__ int classify(const DevView& I, const Rsrc& R, uint32_
 // outcome of the first-hit rule at fm_scanner.cpp:165-177 when every record is assigned.
 // The packed register form for k <= 32 is search_packed_n below.
 __device__ __forceinline__ int search_lds(const DevView& I, const Rsrc& R, const unsigned char* w, uint32_t k,
-                                          bool no_n) {
+                                          bool no_n, uint32_t& lo_out, uint32_t& hi_out) {
     uint32_t lo = 0, hi = I.n;
     int32_t s = (int32_t)k;
     if (I.q != 0u && k >= I.q) {
@@ -215,6 +218,8 @@ __device__ __forceinline__ int search_lds(const DevView& I, const Rsrc& R, const
             --s;
         }
     }
+    lo_out = lo;
+    hi_out = hi;
     return lo < hi ? classify(I, R, lo, hi) : -1;
 }
 
@@ -234,7 +239,8 @@ __device__ __forceinline__ T wave_sum(T v) {
 // no N). A window with an empty interval issues no further loads (out-of-range offsets).
 template <int NW>
 __device__ __forceinline__ void search_packed_n(const DevView& I, const Rsrc& R, const uint64_t (&P0)[NW],
-                                                const bool (&act)[NW], uint32_t k, int (&out)[NW]) {
+                                                const bool (&act)[NW], uint32_t k, int (&out)[NW],
+                                                uint32_t (&lo_out)[NW], uint32_t (&hi_out)[NW]) {
     uint64_t P[NW];
     uint32_t lo[NW], hi[NW];
     int32_t s = (int32_t)k;
@@ -291,7 +297,11 @@ __device__ __forceinline__ void search_packed_n(const DevView& I, const Rsrc& R,
         }
     }
 #pragma unroll
-    for (int w = 0; w < NW; ++w) out[w] = (act[w] && lo[w] < hi[w]) ? classify(I, R, lo[w], hi[w]) : -1;
+    for (int w = 0; w < NW; ++w) {
+        out[w] = (act[w] && lo[w] < hi[w]) ? classify(I, R, lo[w], hi[w]) : -1;
+        lo_out[w] = lo[w];
+        hi_out[w] = hi[w];
+    }
 }
 
 template <int MODE, bool PAIRED, bool LDS_HIST, int NWIN>
@@ -438,11 +448,13 @@ __global__ __launch_bounds__(BLOCK_THREADS) void k_scan(DevView I, UnitSrc src, 
 
         // ---- 3./4. filter, search, classify
         int which[NWIN];
+        uint32_t ilo[NWIN], ihi[NWIN];  // final SA interval (EM histogram)
         bool valid[NWIN], packed[NWIN];
         uint64_t P[NWIN];
 #pragma unroll
         for (int w = 0; w < NWIN; ++w) {
             which[w] = -1;
+            ilo[w] = ihi[w] = 0;
             valid[w] = false;
             packed[w] = false;
             P[w] = 0;
@@ -464,16 +476,21 @@ __global__ __launch_bounds__(BLOCK_THREADS) void k_scan(DevView I, UnitSrc src, 
                     for (uint32_t i = 0; i < k; ++i) x = (x << 2) | (uint64_t)(ws[i] & 3u);
                     P[w] = x;
                 } else if (valid[w]) {
-                    which[w] = search_lds(I, R, sbuf + off[w], k, nbits == 0);
+                    which[w] = search_lds(I, R, sbuf + off[w], k, nbits == 0, ilo[w], ihi[w]);
                 }
             }
         }
         {
             int wp[NWIN];
-            search_packed_n<NWIN>(I, R, P, packed, k, wp);
+            uint32_t plo[NWIN], phi[NWIN];
+            search_packed_n<NWIN>(I, R, P, packed, k, wp, plo, phi);
 #pragma unroll
             for (int w = 0; w < NWIN; ++w)
-                if (packed[w]) which[w] = wp[w];
+                if (packed[w]) {
+                    which[w] = wp[w];
+                    ilo[w] = plo[w];
+                    ihi[w] = phi[w];
+                }
         }
 
         // ---- 5. tallies
@@ -492,6 +509,12 @@ __global__ __launch_bounds__(BLOCK_THREADS) void k_scan(DevView I, UnitSrc src, 
                 }
             } else if (valid[w]) {
                 ++t_cnt;
+                if (src.em_mult != nullptr && which[w] == -2) {
+                    // EM histogram: distinct k-mers have disjoint SA intervals, so lo
+                    // identifies the interval; hi is the same for every window that hits it.
+                    atomicAdd(&src.em_mult[ilo[w]], 1u);
+                    src.em_hi[ilo[w]] = ihi[w];
+                }
                 if (which[w] >= 0) {
                     double wgt = 0.0;
                     if (MODE == KM_LOCAL) {
@@ -698,6 +721,110 @@ void launch_scan(const speq_device_index* d, int mode, bool paired, const UnitSr
 
 }  // namespace
 
+// ---- scan implementations shared by the plain and the EM-histogram entry points ----
+static void scan_device_impl(speq_device_index* d, const uint8_t* d_seq, const uint8_t* d_qual, const uint64_t* d_offsets,
+                      uint64_t n_reads, const speq_scan_params* p, uint64_t* d_counts, double* d_weights,
+                      uint32_t* em_mult, uint32_t* em_hi, hipStream_t st) {
+    if (!d || !p || !d_counts) throw std::invalid_argument("speq_scan_reads_device: null argument");
+    if (p->k < 1 || p->k > MAX_K) throw std::invalid_argument("speq_scan_reads_device: k must be in [1, 4096]");
+    if (p->mode != SPEQ_MODE_GLOBAL && p->mode != SPEQ_MODE_LOCAL)
+        throw std::invalid_argument("speq_scan_reads_device: bad mode");
+    if (p->mode == SPEQ_MODE_LOCAL && !d_weights)
+        throw std::invalid_argument("speq_scan_reads_device: local mode needs a weights buffer");
+    if (p->paired && (n_reads & 1)) throw std::invalid_argument("speq_scan_reads_device: paired scan needs an even record count");
+    if (n_reads == 0) return;
+    if (!d_seq || !d_qual || !d_offsets) throw std::invalid_argument("speq_scan_reads_device: null read buffer");
+    DeviceGuard g(d->device);
+    UnitSrc src{};
+    src.seq = d_seq;
+    src.qual = d_qual;
+    src.off = d_offsets;
+    src.qlut = d->d_qlut;
+    src.em_mult = em_mult;
+    src.em_hi = em_hi;
+    src.n_units = n_reads;
+    src.end_adj = 0;
+    src.k = p->k;
+    src.cutoff = p->phred_cutoff;
+    src.buf_bytes = staging_bytes(p->k, d->ilp);
+    const int mode = p->mode == SPEQ_MODE_LOCAL ? KM_LOCAL : KM_GLOBAL;
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    if (d->timing) {
+        HIP_OK(hipEventCreate(&e0));
+        HIP_OK(hipEventCreate(&e1));
+        HIP_OK(hipEventRecord(e0, st));
+    }
+    launch_scan(d, mode, p->paired != 0, src, p->paired ? n_reads / 2 : n_reads, st,
+                reinterpret_cast<unsigned long long*>(d_counts), nullptr, d_weights);
+    if (d->timing) {
+        HIP_OK(hipEventRecord(e1, st));
+        d->events.emplace_back(e0, e1);
+    }
+}
+
+static void scan_host_impl(speq_device_index* d, const uint8_t* seq, const uint8_t* qual, const uint64_t* offsets,
+                    uint64_t n_reads, const speq_scan_params* p, uint64_t* counts, double* weights,
+                    uint32_t* em_mult, uint32_t* em_hi) {
+    if (!d || !p || !counts || (!offsets && n_reads)) throw std::invalid_argument("speq_scan_reads: null argument");
+    if (p->mode == SPEQ_MODE_LOCAL && !weights) throw std::invalid_argument("speq_scan_reads: local mode needs weights");
+    if (p->paired && (n_reads & 1)) throw std::invalid_argument("speq_scan_reads: paired scan needs an even record count");
+    const uint32_t G = d->G;
+    std::fill(counts, counts + SPEQ_COUNTS_LEN(G), 0ull);
+    if (weights) std::fill(weights, weights + G, 0.0);
+    if (n_reads == 0) return;
+    for (uint64_t i = 0; i < n_reads; ++i)
+        if (offsets[i + 1] < offsets[i]) throw std::invalid_argument("speq_scan_reads: offsets must be non-decreasing");
+    DeviceGuard g(d->device);
+    hipStream_t st = d->stream;
+    // Batches [r0, r1) of whole units holding at most BATCH_BYTES of bases (or a single larger unit).
+    const uint64_t BATCH_BYTES = 256ull << 20;
+    const uint64_t step = p->paired ? 2 : 1;
+    std::vector<std::pair<uint64_t, uint64_t>> batches;
+    uint64_t max_bytes = 1, max_reads = 1;
+    for (uint64_t r0 = 0; r0 < n_reads;) {
+        uint64_t r1 = r0 + step;
+        while (r1 < n_reads && offsets[r1 + step] - offsets[r0] <= BATCH_BYTES) r1 += step;
+        batches.emplace_back(r0, r1);
+        max_bytes = std::max(max_bytes, offsets[r1] - offsets[r0]);
+        max_reads = std::max(max_reads, r1 - r0);
+        r0 = r1;
+    }
+    struct Free {
+        std::vector<void*> p;
+        ~Free() { for (void* x : p) if (x) (void)hipFree(x); }
+    } fr;
+    auto alloc = [&](size_t bytes) {
+        void* x = nullptr;
+        HIP_OK(hipMalloc(&x, bytes));
+        fr.p.push_back(x);
+        return x;
+    };
+    auto* d_counts = static_cast<uint64_t*>(alloc(SPEQ_COUNTS_LEN(G) * 8));
+    double* d_w = p->mode == SPEQ_MODE_LOCAL ? static_cast<double*>(alloc(G * 8)) : nullptr;
+    auto* d_seq = static_cast<uint8_t*>(alloc(max_bytes));
+    auto* d_qual = static_cast<uint8_t*>(alloc(max_bytes));
+    auto* d_off = static_cast<uint64_t*>(alloc((max_reads + 1) * 8));
+    HIP_OK(hipMemsetAsync(d_counts, 0, SPEQ_COUNTS_LEN(G) * 8, st));
+    if (d_w) HIP_OK(hipMemsetAsync(d_w, 0, G * 8, st));
+    std::vector<uint64_t> rel;
+    for (const auto& bt : batches) {
+        const uint64_t r0 = bt.first, r1 = bt.second;
+        const uint64_t nb = offsets[r1] - offsets[r0], nr = r1 - r0;
+        rel.resize(nr + 1);
+        for (uint64_t i = 0; i <= nr; ++i) rel[i] = offsets[r0 + i] - offsets[r0];
+        if (nb) {
+            HIP_OK(hipMemcpyAsync(d_seq, seq + offsets[r0], nb, hipMemcpyHostToDevice, st));
+            HIP_OK(hipMemcpyAsync(d_qual, qual + offsets[r0], nb, hipMemcpyHostToDevice, st));
+        }
+        HIP_OK(hipMemcpyAsync(d_off, rel.data(), (nr + 1) * 8, hipMemcpyHostToDevice, st));
+        scan_device_impl(d, d_seq, d_qual, d_off, nr, p, d_counts, d_w, em_mult, em_hi, st);
+        HIP_OK(hipStreamSynchronize(st));  // `rel` and the device staging buffers are reused next batch
+    }
+    HIP_OK(hipMemcpyAsync(counts, d_counts, SPEQ_COUNTS_LEN(G) * 8, hipMemcpyDeviceToHost, st));
+    if (d_w) HIP_OK(hipMemcpyAsync(weights, d_w, G * 8, hipMemcpyDeviceToHost, st));
+    HIP_OK(hipStreamSynchronize(st));
+}
+
 extern "C" {
 
 int speq_device_count(void) {
@@ -776,106 +903,73 @@ int speq_scan_reads_device(speq_device_index* d, const uint8_t* d_seq, const uin
                            const uint64_t* d_offsets, uint64_t n_reads, const speq_scan_params* p,
                            uint64_t* d_counts, double* d_weights, void* stream) {
     return speq::guarded([&] {
-        if (!d || !p || !d_counts) throw std::invalid_argument("speq_scan_reads_device: null argument");
-        if (p->k < 1 || p->k > MAX_K) throw std::invalid_argument("speq_scan_reads_device: k must be in [1, 4096]");
-        if (p->mode != SPEQ_MODE_GLOBAL && p->mode != SPEQ_MODE_LOCAL)
-            throw std::invalid_argument("speq_scan_reads_device: bad mode");
-        if (p->mode == SPEQ_MODE_LOCAL && !d_weights)
-            throw std::invalid_argument("speq_scan_reads_device: local mode needs a weights buffer");
-        if (p->paired && (n_reads & 1)) throw std::invalid_argument("speq_scan_reads_device: paired scan needs an even record count");
-        if (n_reads == 0) return;
-        if (!d_seq || !d_qual || !d_offsets) throw std::invalid_argument("speq_scan_reads_device: null read buffer");
-        DeviceGuard g(d->device);
-        hipStream_t st = static_cast<hipStream_t>(stream);  // NULL = the null (default) stream
-        UnitSrc src{};
-        src.seq = d_seq;
-        src.qual = d_qual;
-        src.off = d_offsets;
-        src.qlut = d->d_qlut;
-        src.n_units = n_reads;
-        src.end_adj = 0;
-        src.k = p->k;
-        src.cutoff = p->phred_cutoff;
-        src.buf_bytes = staging_bytes(p->k, d->ilp);
-        const int mode = p->mode == SPEQ_MODE_LOCAL ? KM_LOCAL : KM_GLOBAL;
-        hipEvent_t e0 = nullptr, e1 = nullptr;
-        if (d->timing) {
-            HIP_OK(hipEventCreate(&e0));
-            HIP_OK(hipEventCreate(&e1));
-            HIP_OK(hipEventRecord(e0, st));
-        }
-        launch_scan(d, mode, p->paired != 0, src, p->paired ? n_reads / 2 : n_reads, st,
-                    reinterpret_cast<unsigned long long*>(d_counts), nullptr, d_weights);
-        if (d->timing) {
-            HIP_OK(hipEventRecord(e1, st));
-            d->events.emplace_back(e0, e1);
-        }
+        scan_device_impl(d, d_seq, d_qual, d_offsets, n_reads, p, d_counts, d_weights, nullptr, nullptr,
+                         static_cast<hipStream_t>(stream));
     });
 }
 
 int speq_scan_reads(speq_device_index* d, const uint8_t* seq, const uint8_t* qual, const uint64_t* offsets,
                     uint64_t n_reads, const speq_scan_params* p, uint64_t* counts, double* weights) {
+    return speq::guarded([&] { scan_host_impl(d, seq, qual, offsets, n_reads, p, counts, weights, nullptr, nullptr); });
+}
+
+// ---- EM histogram (see em.hpp) ----
+int speq_em_create(const speq_index* idx, speq_device_index* d, speq_em** out) {
     return speq::guarded([&] {
-        if (!d || !p || !counts || (!offsets && n_reads)) throw std::invalid_argument("speq_scan_reads: null argument");
-        if (p->mode == SPEQ_MODE_LOCAL && !weights) throw std::invalid_argument("speq_scan_reads: local mode needs weights");
-        if (p->paired && (n_reads & 1)) throw std::invalid_argument("speq_scan_reads: paired scan needs an even record count");
-        const uint32_t G = d->G;
-        std::fill(counts, counts + SPEQ_COUNTS_LEN(G), 0ull);
-        if (weights) std::fill(weights, weights + G, 0.0);
-        if (n_reads == 0) return;
-        for (uint64_t i = 0; i < n_reads; ++i)
-            if (offsets[i + 1] < offsets[i]) throw std::invalid_argument("speq_scan_reads: offsets must be non-decreasing");
+        if (!idx || !d || !out) throw std::invalid_argument("speq_em_create: null argument");
+        if (idx->fm.n != d->view.n) throw std::invalid_argument("speq_em_create: index and device replica differ");
         DeviceGuard g(d->device);
-        hipStream_t st = d->stream;
-        // Batches [r0, r1) of whole units holding at most BATCH_BYTES of bases (or a single larger unit).
-        const uint64_t BATCH_BYTES = 256ull << 20;
-        const uint64_t step = p->paired ? 2 : 1;
-        std::vector<std::pair<uint64_t, uint64_t>> batches;
-        uint64_t max_bytes = 1, max_reads = 1;
-        for (uint64_t r0 = 0; r0 < n_reads;) {
-            uint64_t r1 = r0 + step;
-            while (r1 < n_reads && offsets[r1 + step] - offsets[r0] <= BATCH_BYTES) r1 += step;
-            batches.emplace_back(r0, r1);
-            max_bytes = std::max(max_bytes, offsets[r1] - offsets[r0]);
-            max_reads = std::max(max_reads, r1 - r0);
-            r0 = r1;
-        }
-        struct Free {
-            std::vector<void*> p;
-            ~Free() { for (void* x : p) if (x) (void)hipFree(x); }
-        } fr;
-        auto alloc = [&](size_t bytes) {
-            void* x = nullptr;
-            HIP_OK(hipMalloc(&x, bytes));
-            fr.p.push_back(x);
-            return x;
-        };
-        auto* d_counts = static_cast<uint64_t*>(alloc(SPEQ_COUNTS_LEN(G) * 8));
-        double* d_w = p->mode == SPEQ_MODE_LOCAL ? static_cast<double*>(alloc(G * 8)) : nullptr;
-        auto* d_seq = static_cast<uint8_t*>(alloc(max_bytes));
-        auto* d_qual = static_cast<uint8_t*>(alloc(max_bytes));
-        auto* d_off = static_cast<uint64_t*>(alloc((max_reads + 1) * 8));
-        HIP_OK(hipMemsetAsync(d_counts, 0, SPEQ_COUNTS_LEN(G) * 8, st));
-        if (d_w) HIP_OK(hipMemsetAsync(d_w, 0, G * 8, st));
-        std::vector<uint64_t> rel;
-        for (const auto& bt : batches) {
-            const uint64_t r0 = bt.first, r1 = bt.second;
-            const uint64_t nb = offsets[r1] - offsets[r0], nr = r1 - r0;
-            rel.resize(nr + 1);
-            for (uint64_t i = 0; i <= nr; ++i) rel[i] = offsets[r0 + i] - offsets[r0];
-            if (nb) {
-                HIP_OK(hipMemcpyAsync(d_seq, seq + offsets[r0], nb, hipMemcpyHostToDevice, st));
-                HIP_OK(hipMemcpyAsync(d_qual, qual + offsets[r0], nb, hipMemcpyHostToDevice, st));
-            }
-            HIP_OK(hipMemcpyAsync(d_off, rel.data(), (nr + 1) * 8, hipMemcpyHostToDevice, st));
-            if (speq_scan_reads_device(d, d_seq, d_qual, d_off, nr, p, d_counts, d_w, st) != SPEQ_OK)
-                throw speq::DeviceError(speq_last_error());
-            HIP_OK(hipStreamSynchronize(st));  // `rel` and the device staging buffers are reused next batch
-        }
-        HIP_OK(hipMemcpyAsync(counts, d_counts, SPEQ_COUNTS_LEN(G) * 8, hipMemcpyDeviceToHost, st));
-        if (d_w) HIP_OK(hipMemcpyAsync(weights, d_w, G * 8, hipMemcpyDeviceToHost, st));
-        HIP_OK(hipStreamSynchronize(st));
+        auto em = std::make_unique<speq_em>();
+        em->idx = idx;
+        em->dev = d;
+        em->n = idx->fm.n;
+        em->G = idx->fm.n_groups;
+        HIP_OK(hipMalloc(&em->d_mult, em->n * 4));
+        HIP_OK(hipMalloc(&em->d_hi, em->n * 4));
+        HIP_OK(hipMemset(em->d_mult, 0, em->n * 4));
+        *out = em.release();
     });
+}
+
+int speq_em_scan_reads(speq_em* em, const uint8_t* seq, const uint8_t* qual, const uint64_t* offsets, uint64_t n_reads,
+                       const speq_scan_params* p, uint64_t* counts, double* weights) {
+    return speq::guarded([&] {
+        if (!em || em->finalized) throw std::invalid_argument("speq_em_scan_reads: bad or finalized histogram");
+        scan_host_impl(em->dev, seq, qual, offsets, n_reads, p, counts, weights, em->d_mult, em->d_hi);
+    });
+}
+
+int speq_em_scan_reads_device(speq_em* em, const uint8_t* d_seq, const uint8_t* d_qual, const uint64_t* d_offsets,
+                              uint64_t n_reads, const speq_scan_params* p, uint64_t* d_counts, double* d_weights,
+                              void* stream) {
+    return speq::guarded([&] {
+        if (!em || em->finalized) throw std::invalid_argument("speq_em_scan_reads_device: bad or finalized histogram");
+        scan_device_impl(em->dev, d_seq, d_qual, d_offsets, n_reads, p, d_counts, d_weights, em->d_mult, em->d_hi,
+                         static_cast<hipStream_t>(stream));
+    });
+}
+
+int speq_em_finalize(speq_em* em, uint32_t threads) {
+    return speq::guarded([&] {
+        if (!em) throw std::invalid_argument("speq_em_finalize: null argument");
+        if (em->finalized) return;
+        DeviceGuard g(em->dev->device);
+        HIP_OK(hipDeviceSynchronize());
+        std::vector<uint32_t> mult(em->n), hi(em->n);
+        HIP_OK(hipMemcpy(mult.data(), em->d_mult, em->n * 4, hipMemcpyDeviceToHost));
+        HIP_OK(hipMemcpy(hi.data(), em->d_hi, em->n * 4, hipMemcpyDeviceToHost));
+        speq::em_build_rows(*em, mult, hi, threads);
+        (void)hipFree(em->d_mult);
+        (void)hipFree(em->d_hi);
+        em->d_mult = em->d_hi = nullptr;
+    });
+}
+
+void speq_em_free(speq_em* em) {
+    if (!em) return;
+    if (em->d_mult) (void)hipFree(em->d_mult);
+    if (em->d_hi) (void)hipFree(em->d_hi);
+    delete em;
 }
 
 int speq_ref_unique_device(speq_device_index* d, uint32_t k, uint64_t* d_u_ref, uint64_t* d_tot_ref, void* stream) {

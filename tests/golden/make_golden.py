@@ -113,6 +113,51 @@ def scan(texts, dgs, G, reads, quals, k, cutoff, local, paired):
     return T, amb, U, W
 
 
+def em_pass(texts, dgs, G, reads, quals, k, cutoff, local, pp, percent, counts):
+    """One EM estimator pass, literally (/root/reference/src/fm_scanner.cpp:1087-1125 global, :1175-1219 local)."""
+    nxt = [0.0] * G
+    for s_raw, q_raw in zip(reads, quals):
+        s, q = dna5(s_raw), [phred(c) for c in q_raw]
+        for j in range(len(s) - k + 1):
+            km, qm = s[j:j + k], q[j:j + k]
+            if not (min(qm) > cutoff and "N" not in km):
+                continue
+            if local:
+                x = 1.0
+                for b in qm:
+                    x = x / (1.0 - 1.0 / math.pow(10.0, b / 10.0))
+                y = 1.0
+                for b in qm:
+                    y = y * (1.0 - 1.0 / math.pow(10.0, b / 10.0))
+                f = x - (1.0 - y)
+            else:
+                f = 1.0 / pp - (1 - pp)
+            h = [0.0] * G
+            for tid, _ in hits(texts, km):
+                h[dgs[tid]] += f
+            a = [h[i] * percent[i] / counts[i] for i in range(G)]
+            norm = 0.0
+            for x in a:
+                norm += x
+            if norm > 0.0:
+                for i in range(G):
+                    nxt[i] += a[i] / norm
+    return nxt
+
+
+def em_loop(step, unique_totals, total, percent, precision=1e-6, max_iter=200):
+    """The refinement loop of /root/reference/src/fm_scanner.cpp:248-279."""
+    out = []
+    diff = [1.0] * len(percent)
+    while max(diff) > precision and len(out) < max_iter:
+        nxt = step(percent)
+        new = unique_to_percent(unique_totals, total, unique_totals, nxt)
+        diff = [abs(x - y) for x, y in zip(new, percent)]
+        percent = new
+        out.append({"percent": new, "next_tkpg": nxt})
+    return out
+
+
 def ref_unique(records, texts, dgs, group_scaffolds, G, k):
     u, t = [0] * G, [0] * G
     for r, (g, rec) in enumerate(zip(group_scaffolds, records)):
@@ -140,7 +185,7 @@ def unique_to_percent(ur, total, uref, tref):
 
 
 def write_case(name, records, groups_text, group_scaffolds, n_groups, reads1, quals1, reads2, quals2, ks, cutoff,
-               fixed_accuracy):
+               fixed_accuracy, group_counts):
     d = os.path.join(HERE, name)
     os.makedirs(d, exist_ok=True)
     with open(os.path.join(d, "refs.fa"), "w") as f:
@@ -164,8 +209,8 @@ def write_case(name, records, groups_text, group_scaffolds, n_groups, reads1, qu
         quals = [x for pair in zip(quals1, quals2) for x in pair]
     else:
         reads, quals = reads1, quals1
-    exp = {"n_groups": n_groups, "group_scaffolds": group_scaffolds, "paired": paired, "phred_cutoff": cutoff,
-           "fixed_accuracy": fixed_accuracy, "by_k": {}}
+    exp = {"n_groups": n_groups, "group_scaffolds": group_scaffolds, "group_counts": group_counts, "paired": paired,
+           "phred_cutoff": cutoff, "fixed_accuracy": fixed_accuracy, "by_k": {}}
     for k in ks:
         e = {}
         u_ref, t_ref = ref_unique(records, texts, dgs, group_scaffolds, n_groups, k)
@@ -177,13 +222,17 @@ def write_case(name, records, groups_text, group_scaffolds, n_groups, reads1, qu
             else:
                 pp = math.pow(fixed_accuracy, k)
                 ut = [u / pp for u in U]
+            pct = unique_to_percent(ut, T, u_ref, t_ref)
+            pp = math.pow(fixed_accuracy, k)
+            em = em_loop(lambda p: em_pass(texts, dgs, n_groups, reads, quals, k, cutoff, local, pp, p, group_counts),
+                         ut, T, pct) if k == ks[0] else None
             e["local" if local else "global"] = {"T": T, "ambiguous": amb, "U": U, "W": W if local else None,
-                                                  "unique_totals": ut,
-                                                  "percent": unique_to_percent(ut, T, u_ref, t_ref)}
+                                                  "unique_totals": ut, "percent": pct, "em": em}
         exp["by_k"][str(k)] = e
     with open(os.path.join(d, "expected.json"), "w") as f:
         json.dump(exp, f, indent=1)
-    print(name, {k: (v["global"]["T"], v["global"]["U"], v["u_ref"]) for k, v in exp["by_k"].items()})
+    print(name, {k: (v["global"]["T"], v["global"]["U"], v["u_ref"]) for k, v in exp["by_k"].items()},
+          "em iterations", [len(exp["by_k"][str(ks[0])][m]["em"]) for m in ("global", "local")])
 
 
 def reads_lists(reads):
@@ -202,14 +251,15 @@ def main():
     recs[1] = recs[1][:300] + recs[1][300:].lower()   # lowercase input is dna5-converted
     rd = synth.make_reads(ref, 80, read_len=60, n_rate=0.01, lowq_rate=0.02, short_frac=0.1)
     rs, qs = reads_lists(rd)
-    write_case("tiny_single", recs, ref.groupings_text(), [0, 1, 2], 3, rs, qs, None, None, [7, 11, 16], 30, 0.99)
+    write_case("tiny_single", recs, ref.groupings_text(), [0, 1, 2], 3, rs, qs, None, None, [11, 7, 16], 30, 0.99,
+               [1, 1, 1])
 
     # case 2: paired mates over 2 variants x 2 isolates
     ref2 = synth.make_reference(2, 2, 500)
     rp = synth.make_reads(ref2, 30, read_len=50, fragment=120, paired=True, n_rate=0.005, lowq_rate=0.02)
     rs, qs = reads_lists(rp)
     write_case("tiny_paired", [r.decode() for r in ref2.records], ref2.groupings_text(), [0, 0, 1, 1], 2,
-               rs[0::2], qs[0::2], rs[1::2], qs[1::2], [9, 13], 30, 0.995)
+               rs[0::2], qs[0::2], rs[1::2], qs[1::2], [13, 9], 30, 0.995, [2, 2])
 
     # case 3: scattered groupings written with ranges, singletons, comments and a bad token
     ref3 = synth.make_reference(5, 1, 300)
@@ -221,7 +271,7 @@ def main():
     rd3 = synth.make_reads(ref3, 40, read_len=40, lowq_rate=0.01)
     rs, qs = reads_lists(rd3)
     write_case("scattered_groups", [r.decode() for r in ref3.records], groups_text, [1, 0, 2, 2, 0], 3, rs, qs,
-               None, None, [8, 12], 20, 0.98)
+               None, None, [12, 8], 20, 0.98, [2, 1, 3])
 
 
 if __name__ == "__main__":

@@ -114,3 +114,15 @@ def test_scan_end_to_end(tmp_path, name, mode):
     assert r2.stderr.strip().split("\n")[0] == lines[2]
     out = (tmp_path / "p2.txt").read_text().strip().split("\n")
     assert len(out) == c.G
+    # EM refinement: one stderr block per iteration, and -o holds the refined percentages
+    em = g["em"]
+    blocks = r.stderr.strip().split("\n\n")
+    assert len(blocks) == len(em)  # the first iteration follows the initial lines directly
+    last = blocks[-1].split("\n")
+    if mode == "local" and not c.paired:
+        assert last[0].startswith("1: ") and last[3].startswith("Percent of each group: ")
+        np.testing.assert_allclose(_parse_vec(last[2][3:]), em[-1]["next_tkpg"], rtol=1e-5)
+    else:
+        np.testing.assert_allclose(_parse_vec(last[1]), em[-1]["next_tkpg"], rtol=1e-5)
+    got = [float(ln.split("\t")[1]) for ln in out]
+    np.testing.assert_allclose(got, em[-1]["percent"], rtol=1e-5, atol=1e-9)
