@@ -43,6 +43,18 @@ def lib() -> C.CDLL:
                                      C.c_double, C.POINTER(C.c_double), C.POINTER(C.c_int32), C.POINTER(C.c_double)]
         L.oracle_ref_unique.restype = C.c_int
         L.oracle_ref_unique.argtypes = [P, U64P, U64P]
+        L.sl_build.restype = P
+        L.sl_build.argtypes = [C.c_char_p, U64P, C.c_uint32, C.POINTER(C.c_int32), C.c_uint32]
+        L.sl_free.argtypes = [P]
+        L.sl_count.restype = C.c_int64
+        L.sl_count.argtypes = [P, C.c_char_p, C.c_uint32]
+        L.sl_which.restype = C.c_int32
+        L.sl_which.argtypes = [P, C.c_char_p, C.c_uint32]
+        L.sl_scan.restype = C.c_int
+        L.sl_scan.argtypes = [P, C.c_char_p, C.c_char_p, U64P, C.c_uint64, C.c_int, C.c_uint32, C.c_uint32, C.c_int,
+                              U64P, C.POINTER(C.c_double), C.c_int]
+        L.sl_text_len.restype = C.c_uint32
+        L.sl_text_len.argtypes = [P]
         _lib = L
     return _lib
 
@@ -111,6 +123,55 @@ class Oracle:
         try:
             if self._h:
                 lib().oracle_free(self._h)
+                self._h = None
+        except Exception:
+            pass
+
+
+class SeqanLike:
+    """CPU stand-in for the reference's algorithm (seqan_like.c): backward search on a wavelet structure, locate of
+    every hit through SA samples (every 16 rows), sorted hit list, first-hit group rule. k is chosen per scan, as
+    with the reference's index."""
+
+    def __init__(self, records: Sequence[bytes], groups: Sequence[int], n_groups: int):
+        bs = [bytes(r) for r in records]
+        off = np.zeros(len(bs) + 1, dtype=np.uint64)
+        off[1:] = np.cumsum([len(b) for b in bs])
+        g = np.asarray(groups, dtype=np.int32)
+        self.G = n_groups
+        self._h = lib().sl_build(b"".join(bs), _u64p(off), len(bs), g.ctypes.data_as(C.POINTER(C.c_int32)), n_groups)
+        if not self._h:
+            raise ValueError("sl_build failed")
+
+    @property
+    def n(self) -> int:
+        return int(lib().sl_text_len(self._h))
+
+    def count(self, kmer: bytes) -> int:
+        return int(lib().sl_count(self._h, kmer, len(kmer)))
+
+    def which(self, kmer: bytes) -> int:
+        return int(lib().sl_which(self._h, kmer, len(kmer)))
+
+    def scan(self, seq, qual, offsets, k: int, phred_cutoff: int = 30, paired: bool = False, local: bool = False,
+             threads: int = 0):
+        """Returns (T, ambiguous, U[G] u64, W[G] f64 or None)."""
+        seq_b = seq.tobytes() if isinstance(seq, np.ndarray) else bytes(seq)
+        qual_b = qual.tobytes() if isinstance(qual, np.ndarray) else bytes(qual)
+        off = np.ascontiguousarray(offsets, dtype=np.uint64)
+        counts = np.zeros(self.G + 2, dtype=np.uint64)
+        w = np.zeros(self.G, dtype=np.float64) if local else None
+        rc = lib().sl_scan(self._h, seq_b, qual_b, _u64p(off), len(off) - 1, int(paired), k, phred_cutoff,
+                           1 if local else 0, _u64p(counts),
+                           w.ctypes.data_as(C.POINTER(C.c_double)) if w is not None else None, threads)
+        if rc != 0:
+            raise ValueError("sl_scan: bad arguments")
+        return int(counts[0]), int(counts[1]), counts[2:].copy(), w
+
+    def __del__(self):
+        try:
+            if self._h:
+                lib().sl_free(self._h)
                 self._h = None
         except Exception:
             pass
