@@ -17,7 +17,8 @@ OBJDIR   := build/obj
 
 LIB_HIP  := speq_amd/csrc/scan_kernels.hip
 LIB_CPP  := speq_amd/csrc/sais.cpp speq_amd/csrc/fm_index.cpp speq_amd/csrc/capi.cpp speq_amd/csrc/comm.cpp \
-            speq_amd/csrc/host_io.cpp speq_amd/csrc/em.cpp
+            speq_amd/csrc/host_io.cpp speq_amd/csrc/em.cpp speq_amd/csrc/pipeline.cpp \
+            speq_amd/csrc/fastq_stream.cpp
 CLI_CPP  := speq_amd/cli/speq_main.cpp
 
 LIB_OBJS := $(patsubst speq_amd/csrc/%.hip,$(OBJDIR)/%.o,$(LIB_HIP)) \
@@ -30,7 +31,8 @@ $(OBJDIR)/%.o: speq_amd/csrc/%.hip $(HDRS)
 	@mkdir -p $(OBJDIR)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
-$(OBJDIR)/comm.o: speq_amd/csrc/comm.cpp $(HDRS)
+# host-only translation units that call the HIP runtime / RCCL API (no kernels): g++ with the ROCm headers
+$(OBJDIR)/comm.o $(OBJDIR)/pipeline.o: $(OBJDIR)/%.o: speq_amd/csrc/%.cpp $(HDRS)
 	@mkdir -p $(OBJDIR)
 	$(CXX) $(HOSTFLAGS) -I/opt/rocm/include -D__HIP_PLATFORM_AMD__ -c $< -o $@
 
@@ -39,7 +41,7 @@ $(OBJDIR)/%.o: speq_amd/csrc/%.cpp $(HDRS)
 	$(CXX) $(HOSTFLAGS) -c $< -o $@
 
 $(LIB): $(LIB_OBJS)
-	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $^ -L/opt/rocm/lib -lrccl -lamdhip64 -lpthread \
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $^ -L/opt/rocm/lib -lrccl -lamdhip64 -lz -lpthread \
 	    -Wl,-rpath,/opt/rocm/lib
 
 $(CLI): $(CLI_CPP) $(LIB) $(HDRS) speq_amd/cli/*.hpp
@@ -55,7 +57,7 @@ variant: $(filter-out $(OBJDIR)/scan_kernels.o,$(LIB_OBJS))
 	@mkdir -p build/variants/$(NAME)
 	$(HIPCC) $(HIPFLAGS) $(VFLAGS) -c $(LIB_HIP) -o build/variants/$(NAME)/scan_kernels.o
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o build/variants/$(NAME)/libspeq_scan.so \
-	    build/variants/$(NAME)/scan_kernels.o $^ -L/opt/rocm/lib -lrccl -lamdhip64 -lpthread -Wl,-rpath,/opt/rocm/lib
+	    build/variants/$(NAME)/scan_kernels.o $^ -L/opt/rocm/lib -lrccl -lamdhip64 -lz -lpthread -Wl,-rpath,/opt/rocm/lib
 
 clean:
 	rm -rf build bin $(LIB)

@@ -175,6 +175,53 @@ int speq_em_step(const speq_em* em, const double* percent, const int32_t* group_
                  double* next);
 void speq_em_free(speq_em* em);
 
+/* ---- streaming scan: pinned host slots, H2D on a copy stream overlapped with the kernel ----
+ * Replaces the reference's single-producer async_input_buffer feeding T-1 search workers
+ * (fm_scanner.cpp:138-141, :219-222; paired :651-655). A pipeline owns n_slots pinned host buffers, each with a
+ * device twin; a producer thread acquires a free slot, writes whole records into it (ASCII bases, Phred+33
+ * qualities, offsets[0] = 0 .. offsets[n]), and submits it: the slot is copied to HBM on a copy stream while the
+ * kernel of the previous slot runs on a compute stream. Any number of producer threads may acquire/submit
+ * concurrently. Counters accumulate on the device; finish returns them (and resets them to zero).
+ * em may be NULL; when given, the scan also records its EM histogram (the pipeline must use em's device). */
+typedef struct speq_pipeline speq_pipeline;
+typedef struct {
+    uint8_t* seq;          /* capacity cap_bytes */
+    uint8_t* qual;         /* capacity cap_bytes */
+    uint64_t* offsets;     /* capacity cap_records + 1 */
+    uint64_t cap_bytes;
+    uint64_t cap_records;
+    int32_t slot;          /* pass back to speq_pipeline_submit */
+} speq_slot;
+int speq_pipeline_create(speq_device_index* d, const speq_scan_params* params, speq_em* em, uint64_t slot_bytes,
+                         uint64_t slot_records, uint32_t n_slots, speq_pipeline** out);
+/* Blocks until a slot is free (its previous copy and kernel have completed). */
+int speq_pipeline_acquire(speq_pipeline* pl, speq_slot* out);
+/* Grows a slot's capacity (host and device) before it is filled; contents are not preserved. */
+int speq_pipeline_reserve(speq_pipeline* pl, speq_slot* slot, uint64_t bytes, uint64_t records);
+/* Enqueues the copy + scan of n_records records of an acquired slot (n_records may be 0: releases the slot). */
+int speq_pipeline_submit(speq_pipeline* pl, int32_t slot, uint64_t n_records);
+/* Waits for every submitted slot; counts u64[G+2] (and weights f64[G] in local mode) receive the totals since
+ * the last finish. */
+int speq_pipeline_finish(speq_pipeline* pl, uint64_t* counts, double* weights);
+void speq_pipeline_free(speq_pipeline* pl);
+
+/* Scan of FASTQ files (plain or gzip; paired when path2 != NULL: records i of both files are mates) through a
+ * pipeline: one reader thread per file decompresses and cuts record-aligned blocks, `threads` parser threads fill
+ * pinned slots. FASTQ grammar of the reference's reader (multi-line sequence/quality accepted; a FASTA file is
+ * rejected: qualities are required). counts/weights as speq_scan_reads; stats may be NULL. */
+typedef struct {
+    uint64_t records;      /* records scanned (both mates) */
+    uint64_t bases;
+    uint64_t batches;      /* slots submitted */
+    double seconds;        /* wall time of the call */
+} speq_stream_stats;
+int speq_scan_fastq(speq_device_index* d, const char* path1, const char* path2, const speq_scan_params* params,
+                    speq_em* em, uint32_t threads, uint64_t* counts, double* weights, speq_stream_stats* stats);
+/* The same reader and parsers without a device (host only; for tests and tools): record and base counts, and an
+ * order-independent digest = sum over records of mix64(FNV-1a-64 over (len, (base << 8 | qual) per position)). */
+int speq_fastq_checksum(const char* path1, const char* path2, uint32_t threads, uint64_t* records, uint64_t* bases,
+                        uint64_t* digest);
+
 /* ---- groupings file (speq::file_to_map, /root/reference/src/file_to_map.cpp:20-119) ----
  * Same grammar "Name(count): i, j-k, …"; parse errors of single tokens are collected (the reference prints
  * them to std::cerr) and returned by speq_groupings_errors(). A missing "(count)" fails with SPEQ_E_ARG

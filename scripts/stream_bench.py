@@ -1,0 +1,98 @@
+#!/usr/bin/env python3
+"""Streaming / PCIe-inclusive throughput of the scan (SURVEY 8(d) secondary metrics).
+
+  host  : speq_scan_reads on pageable host arrays (memcpy into pinned slots -> H2D on a copy stream -> k_scan)
+  fastq : speq_scan_fastq on a FASTQ file in the page cache (reader thread -> parser threads -> pinned slots)
+  gz    : the same on a gzip file (zlib inflate on the reader thread)
+Prints one JSON line per measurement (and appends them to --out)."""
+import argparse
+import gzip
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--config", type=int, default=2)
+    ap.add_argument("--reads", type=int, default=1_000_000)
+    ap.add_argument("--threads", default="1,4,8,16")
+    ap.add_argument("--gz", type=int, default=1)
+    ap.add_argument("--dir", default=os.environ.get("TMPDIR", "/tmp"))
+    ap.add_argument("--out", default="")
+    a = ap.parse_args()
+    import torch  # noqa: F401  (one HIP runtime per process: torch first)
+    from speq_amd import DeviceIndex, FmIndex, synth
+
+    c = synth.CONFIGS[a.config]
+    k = c["k"]
+    ref = synth.make_reference(c["n_variants"], c["n_isolates"], c["length"])
+    dev = DeviceIndex(FmIndex.build(ref.records, ref.groups, c["n_variants"], prefix_q=11))
+    reads = synth.make_reads(ref, a.reads, paired=c["paired"])
+    lens = np.diff(reads.offsets).astype(np.int64)
+    kmers = int(np.maximum(lens - k + 1, 0).sum())
+    out = open(a.out, "a") if a.out else None
+
+    def emit(d):
+        d.update({"config": a.config, "reads": reads.n, "kmers": kmers})
+        line = json.dumps(d)
+        print(line, flush=True)
+        if out:
+            out.write(line + "\n")
+            out.flush()
+
+    seq, qual = reads.seq.tobytes(), reads.qual.tobytes()
+    dev.scan(seq, qual, reads.offsets[:1001], k=k)  # warm-up
+    for _ in range(3):
+        t0 = time.perf_counter()
+        r = dev.scan(seq, qual, reads.offsets, k=k, paired=c["paired"])
+        dt = time.perf_counter() - t0
+    emit({"path": "host (speq_scan_reads, pageable arrays)", "seconds": dt, "kmers_per_s": kmers / dt,
+          "GB_per_s_host": 2 * len(seq) / dt / 1e9, "T": r.total})
+
+    path = os.path.join(a.dir, "speq_stream_bench.fq")
+    t0 = time.perf_counter()
+    with open(path, "wb") as f:
+        for i in range(0, reads.n, 100_000):
+            parts = []
+            for j in range(i, min(reads.n, i + 100_000)):
+                s0, s1 = int(reads.offsets[j]), int(reads.offsets[j + 1])
+                parts.append(b"@r%d\n%s\n+\n%s\n" % (j, seq[s0:s1], qual[s0:s1]))
+            f.write(b"".join(parts))
+    size = os.path.getsize(path)
+    print(f"# wrote {size / 1e6:.0f} MB FASTQ in {time.perf_counter() - t0:.1f} s", flush=True)
+    for th in [int(x) for x in a.threads.split(",")]:
+        best = None
+        for _ in range(2):
+            r2, st = dev.scan_fastq(path, None, k=k, threads=th)
+            best = st if best is None or st["seconds"] < best["seconds"] else best
+        assert r2.total == r.total and r2.unique.tolist() == r.unique.tolist()
+        emit({"path": "fastq (speq_scan_fastq, plain, page cache)", "threads": th, "seconds": best["seconds"],
+              "kmers_per_s": kmers / best["seconds"], "MB_per_s_file": size / best["seconds"] / 1e6,
+              "batches": best["batches"]})
+    if a.gz:
+        gpath = path + ".gz"
+        with open(path, "rb") as f, gzip.open(gpath, "wb", compresslevel=1) as g:
+            while True:
+                b = f.read(64 << 20)
+                if not b:
+                    break
+                g.write(b)
+        th = max(int(x) for x in a.threads.split(","))
+        r3, st = dev.scan_fastq(gpath, None, k=k, threads=th)
+        assert r3.total == r.total
+        emit({"path": "fastq.gz (speq_scan_fastq, zlib level 1)", "threads": th, "seconds": st["seconds"],
+              "kmers_per_s": kmers / st["seconds"], "MB_per_s_file": size / st["seconds"] / 1e6,
+              "gz_bytes": os.path.getsize(gpath)})
+        os.remove(gpath)
+    os.remove(path)
+
+
+if __name__ == "__main__":
+    main()

@@ -44,6 +44,15 @@ class IndexInfo(C.Structure):
 # name -> (restype, argtypes); every symbol declared in include/speq_scan.h
 _P, _U8P, _U64P, _I32P, _F64P = C.c_void_p, C.POINTER(C.c_uint8), C.POINTER(C.c_uint64), C.POINTER(C.c_int32), \
     C.POINTER(C.c_double)
+class Slot(C.Structure):
+    _fields_ = [("seq", C.POINTER(C.c_uint8)), ("qual", C.POINTER(C.c_uint8)), ("offsets", C.POINTER(C.c_uint64)),
+                ("cap_bytes", C.c_uint64), ("cap_records", C.c_uint64), ("slot", C.c_int32)]
+
+
+class StreamStats(C.Structure):
+    _fields_ = [("records", C.c_uint64), ("bases", C.c_uint64), ("batches", C.c_uint64), ("seconds", C.c_double)]
+
+
 SIGNATURES = {
     "speq_last_error": (C.c_char_p, []),
     "speq_abi_version": (C.c_int, []),
@@ -77,6 +86,16 @@ SIGNATURES = {
     "speq_em_info": (C.c_int, [_P, _U64P, _U64P, _U64P]),
     "speq_em_step": (C.c_int, [_P, _F64P, _I32P, _U64P, _F64P]),
     "speq_em_free": (None, [_P]),
+    "speq_pipeline_create": (C.c_int, [_P, C.POINTER(ScanParams), _P, C.c_uint64, C.c_uint64, C.c_uint32,
+                                       C.POINTER(_P)]),
+    "speq_pipeline_acquire": (C.c_int, [_P, C.POINTER(Slot)]),
+    "speq_pipeline_reserve": (C.c_int, [_P, C.POINTER(Slot), C.c_uint64, C.c_uint64]),
+    "speq_pipeline_submit": (C.c_int, [_P, C.c_int32, C.c_uint64]),
+    "speq_pipeline_finish": (C.c_int, [_P, _U64P, _F64P]),
+    "speq_pipeline_free": (None, [_P]),
+    "speq_scan_fastq": (C.c_int, [_P, C.c_char_p, C.c_char_p, C.POINTER(ScanParams), _P, C.c_uint32, _U64P, _F64P,
+                                  C.POINTER(StreamStats)]),
+    "speq_fastq_checksum": (C.c_int, [C.c_char_p, C.c_char_p, C.c_uint32, _U64P, _U64P, _U64P]),
     "speq_groupings_parse": (C.c_int, [C.c_char_p, C.POINTER(_P)]),
     "speq_groupings_n_groups": (C.c_uint32, [_P]),
     "speq_groupings_name": (C.c_char_p, [_P, C.c_uint32]),

@@ -20,9 +20,10 @@ from typing import Optional, Sequence
 
 import numpy as np
 
-from ._lib import (SPEQ_MODE_GLOBAL, SPEQ_MODE_LOCAL, BuildOpts, IndexInfo, ScanParams, SpeqError, check, lib)
+from ._lib import (SPEQ_MODE_GLOBAL, SPEQ_MODE_LOCAL, BuildOpts, IndexInfo, ScanParams, Slot, SpeqError,  # noqa: F401
+                   StreamStats, check, lib)
 
-__all__ = ["FmIndex", "DeviceIndex", "ScanResult", "Groupings", "EmHistogram", "file_to_map", "unique_to_percent",
+__all__ = ["FmIndex", "DeviceIndex", "Pipeline", "ScanResult", "Groupings", "EmHistogram", "file_to_map", "unique_to_percent",
            "em_refine", "pack_records", "SpeqError", "SPEQ_MODE_GLOBAL", "SPEQ_MODE_LOCAL"]
 
 
@@ -182,6 +183,22 @@ class DeviceIndex:
         check(lib().speq_scan_reads_device(self._h, d_seq, d_qual, d_offsets, n_reads, C.byref(p), d_counts,
                                            d_weights or None, stream or None))
 
+    def scan_fastq(self, path1: str, path2: Optional[str] = None, k: int = 21, phred_cutoff: int = 30,
+                   local: bool = False, threads: int = 4, em: Optional["EmHistogram"] = None):
+        """Streams FASTQ(.gz) file(s) through pinned slots to the GPU (speq_scan_fastq). Paired when path2 is given.
+        Returns (ScanResult, stats dict)."""
+        G = self.n_groups
+        counts = np.zeros(G + 2, dtype=np.uint64)
+        w = np.zeros(G, dtype=np.float64) if local else None
+        p = ScanParams(k, phred_cutoff, int(path2 is not None), SPEQ_MODE_LOCAL if local else SPEQ_MODE_GLOBAL)
+        st = StreamStats()
+        check(lib().speq_scan_fastq(self._h, path1.encode(), path2.encode() if path2 else None, C.byref(p),
+                                    em._h if em is not None else None, threads, _u64p(counts),
+                                    w.ctypes.data_as(C.POINTER(C.c_double)) if w is not None else None,
+                                    C.byref(st)))
+        stats = {"records": st.records, "bases": st.bases, "batches": st.batches, "seconds": st.seconds}
+        return ScanResult(int(counts[0]), int(counts[1]), counts[2:].copy(), w), stats
+
     def count_unique_kmers_per_group(self, k: int) -> tuple[np.ndarray, np.ndarray]:
         """(U_ref[G], Tot_ref[G]) of the reference-uniqueness pass."""
         G = self.n_groups
@@ -206,6 +223,61 @@ class DeviceIndex:
     def close(self):
         if self._h:
             lib().speq_device_close(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class Pipeline:
+    """Pinned-slot streaming scan (include/speq_scan.h, speq_pipeline_*): fill a slot on the host, submit it, and
+    its copy to HBM overlaps the previous slot's kernel."""
+
+    def __init__(self, dev: DeviceIndex, k: int, phred_cutoff: int = 30, paired: bool = False, local: bool = False,
+                 slot_bytes: int = 8 << 20, slot_records: int = 1 << 15, n_slots: int = 3,
+                 em: Optional["EmHistogram"] = None):
+        self.dev, self.local, self.paired = dev, local, paired
+        self.n_groups = dev.n_groups
+        p = ScanParams(k, phred_cutoff, int(paired), SPEQ_MODE_LOCAL if local else SPEQ_MODE_GLOBAL)
+        h = C.c_void_p()
+        check(lib().speq_pipeline_create(dev.handle, C.byref(p), em._h if em is not None else None, slot_bytes,
+                                         slot_records, n_slots, C.byref(h)))
+        self._h = h
+
+    def put(self, seq: bytes, qual: bytes, offsets: np.ndarray) -> None:
+        """Copies whole records into a free slot (growing it if needed) and submits it."""
+        off = np.ascontiguousarray(offsets, dtype=np.uint64)
+        n = len(off) - 1
+        nb = int(off[-1] - off[0])
+        s = Slot()
+        check(lib().speq_pipeline_acquire(self._h, C.byref(s)))
+        try:
+            if nb > s.cap_bytes or n > s.cap_records:
+                check(lib().speq_pipeline_reserve(self._h, C.byref(s), nb, n))
+            base = int(off[0])
+            C.memmove(s.seq, bytes(seq[base:base + nb]), nb)
+            C.memmove(s.qual, bytes(qual[base:base + nb]), nb)
+            rel = (off - off[0]).astype(np.uint64)
+            C.memmove(s.offsets, rel.ctypes.data, (n + 1) * 8)
+        except BaseException:
+            lib().speq_pipeline_submit(self._h, s.slot, 0)
+            raise
+        check(lib().speq_pipeline_submit(self._h, s.slot, n))
+
+    def finish(self) -> ScanResult:
+        G = self.n_groups
+        counts = np.zeros(G + 2, dtype=np.uint64)
+        w = np.zeros(G, dtype=np.float64) if self.local else None
+        check(lib().speq_pipeline_finish(self._h, _u64p(counts),
+                                         w.ctypes.data_as(C.POINTER(C.c_double)) if w is not None else None))
+        return ScanResult(int(counts[0]), int(counts[1]), counts[2:].copy(), w)
+
+    def close(self):
+        if self._h:
+            lib().speq_pipeline_free(self._h)
             self._h = None
 
     def __del__(self):

@@ -387,51 +387,25 @@ int run_scan(CmdArguments& a) {
     const bool paired = !a.in_file_reads_path_2.empty();
     const bool local = a.fixed_accuracy == 0.0;
     speq_scan_params prm{a.kmer, a.phred_cutoff, paired ? 1u : 0u, local ? (uint32_t)SPEQ_MODE_LOCAL : (uint32_t)SPEQ_MODE_GLOBAL};
-    std::vector<uint64_t> counts(G + 2, 0), part(G + 2);
-    std::vector<double> weights(G, 0.0), wpart(G);
+    std::vector<uint64_t> counts(G + 2, 0);
+    std::vector<double> weights(std::max<size_t>(G, 1), 0.0);
     // One scan also fills the EM histogram (the reference re-scans every read per EM iteration instead).
     speq_em* em = nullptr;
     ok(speq_em_create(idx, d, &em), "allocating the EM histogram");
-    const uint64_t BATCH_RECORDS = 1u << 21, BATCH_BYTES = 512ull << 20;
-    speq::FastqReader r1(a.in_file_reads_path_1.string());
-    std::unique_ptr<speq::FastqReader> r2;
-    if (paired) r2 = std::make_unique<speq::FastqReader>(a.in_file_reads_path_2.string());
-    for (;;) {
-        speq::SeqBatch b1;
-        uint64_t n1 = r1.next(b1, BATCH_RECORDS, BATCH_BYTES);
-        speq::SeqBatch batch;
-        if (paired) {
-            speq::SeqBatch b2;
-            uint64_t n2 = r2->next(b2, n1, ~0ull);
-            if (n2 != n1) throw CApiError("paired read files have different numbers of records");
-            // interleave mates (2i, 2i+1): both mates share one read state (fm_scanner.cpp:709-729)
-            batch.seq.reserve(b1.seq.size() + b2.seq.size());
-            batch.qual.reserve(b1.seq.size() + b2.seq.size());
-            for (uint64_t i = 0; i < n1; ++i) {
-                for (const speq::SeqBatch* b : {&b1, &b2}) {
-                    uint64_t s = b->offsets[i], e = b->offsets[i + 1];
-                    batch.seq.insert(batch.seq.end(), b->seq.begin() + s, b->seq.begin() + e);
-                    batch.qual.insert(batch.qual.end(), b->qual.begin() + s, b->qual.begin() + e);
-                    batch.offsets.push_back(batch.seq.size());
-                }
-            }
-        } else {
-            batch = std::move(b1);
-        }
-        const uint64_t n = batch.size();
-        if (n == 0) break;
-        ok(speq_em_scan_reads(em, reinterpret_cast<const uint8_t*>(batch.seq.data()),
-                              reinterpret_cast<const uint8_t*>(batch.qual.data()), batch.offsets.data(), n, &prm,
-                              part.data(), local ? wpart.data() : nullptr),
-           "scanning reads");
-        for (size_t i = 0; i < G + 2; ++i) counts[i] += part[i];
-        if (local)
-            for (size_t i = 0; i < G; ++i) weights[i] += wpart[i];
-    }
+    // FASTQ(.gz) streamed through pinned slots: -t parser threads, H2D overlapped with the kernel (fm_scanner.cpp:
+    // 138-141 / :651-655 read through an async_input_buffer; paired files are zipped, stopping at the shorter one).
+    speq_stream_stats st{};
+    ok(speq_scan_fastq(d, a.in_file_reads_path_1.c_str(), paired ? a.in_file_reads_path_2.c_str() : nullptr, &prm,
+                       em, a.threads, counts.data(), local ? weights.data() : nullptr, &st),
+       "scanning reads");
+    if (const char* v = std::getenv("SPEQ_STREAM_STATS"); v && *v && *v != '0')
+        std::fprintf(stderr, "speq: streamed %llu records, %llu bases in %llu batches, %.3f s (%.1f M records/s)\n",
+                     (unsigned long long)st.records, (unsigned long long)st.bases, (unsigned long long)st.batches,
+                     st.seconds, st.seconds > 0 ? st.records / st.seconds / 1e6 : 0.0);
     const uint64_t total = counts[0], ambiguous = counts[1];
     std::vector<double> unique_totals(G, 0.0);
     if (local) {
-        unique_totals = weights;
+        unique_totals.assign(weights.begin(), weights.begin() + G);
     } else {
         const double percent_perfect = std::pow(a.fixed_accuracy, (double)a.kmer);  // fm_scanner.cpp:15
         for (size_t i = 0; i < G; ++i) unique_totals[i] = static_cast<double>(counts[2 + i]) / percent_perfect;

@@ -1,0 +1,563 @@
+// FASTQ (plain or gzip) -> pinned slots -> GPU scan: the streaming front end of speq_scan_fastq.
+//
+// Replaces seqan3::sequence_file_input + views::async_input_buffer (/root/reference/src/fm_scanner.cpp:138-141;
+// paired: views::zip(fin1, fin2), :651-655, which stops at the shorter file). One reader thread decompresses (zlib
+// gzread, transparent for plain files) and cuts record-aligned text blocks; parser threads turn blocks into
+// {bases, qualities, offsets} directly inside pinned pipeline slots and submit them (pipeline.cpp), so parsing,
+// PCIe copies and the kernel overlap.
+//
+// FASTQ grammar (same as FastqReader in host_io.cpp): blank lines between records are skipped; a record is
+// '@' header, sequence lines up to a line starting with '+', then quality lines until as many quality characters
+// as bases have been read; whitespace and digits inside sequence lines are dropped, whitespace inside quality
+// lines is dropped; a FASTA file is rejected (qualities are required).
+#include <fcntl.h>
+#include <unistd.h>
+#include <zlib.h>
+
+#include <cerrno>
+
+#include <algorithm>
+#include <atomic>
+#include <chrono>
+#include <condition_variable>
+#include <cstring>
+#include <deque>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "capi_internal.hpp"
+#include "scan_internal.hpp"
+
+namespace {
+
+using speq::IoError;
+
+// Decompressed byte source: plain files through read(2), gzip (magic 1f 8b) through zlib.
+class Source {
+public:
+    explicit Source(const std::string& path) : path_(path) {
+        fd_ = ::open(path.c_str(), O_RDONLY);
+        if (fd_ < 0) throw IoError("cannot open reads file " + path);
+        unsigned char magic[2] = {0, 0};
+        const ssize_t m = ::pread(fd_, magic, 2, 0);
+        if (m == 2 && magic[0] == 0x1f && magic[1] == 0x8b) {
+            gz_ = gzdopen(fd_, "rb");
+            if (!gz_) throw IoError("cannot open gzip stream " + path);
+            fd_ = -1;  // owned by gz_
+            gzbuffer(gz_, 1u << 20);
+        } else {
+            (void)::posix_fadvise(fd_, 0, 0, POSIX_FADV_SEQUENTIAL);
+        }
+    }
+    ~Source() {
+        if (gz_) gzclose(gz_);
+        if (fd_ >= 0) ::close(fd_);
+    }
+    size_t read(char* dst, size_t n) {
+        size_t got = 0;
+        while (got < n) {
+            const size_t want = std::min<size_t>(n - got, 1u << 30);
+            if (gz_) {
+                const int r = gzread(gz_, dst + got, (unsigned)want);
+                if (r < 0) {
+                    int err = 0;
+                    const char* msg = gzerror(gz_, &err);
+                    throw IoError("error reading " + path_ + ": " + (msg ? msg : "zlib error"));
+                }
+                if (r == 0) break;
+                got += (size_t)r;
+            } else {
+                const ssize_t r = ::read(fd_, dst + got, want);
+                if (r < 0) {
+                    if (errno == EINTR) continue;
+                    throw IoError("error reading " + path_ + ": " + std::strerror(errno));
+                }
+                if (r == 0) break;
+                got += (size_t)r;
+            }
+        }
+        return got;
+    }
+    const std::string& path() const { return path_; }
+
+private:
+    int fd_ = -1;
+    gzFile gz_ = nullptr;
+    std::string path_;
+};
+
+inline bool is_space(unsigned char c) { return c == ' ' || (c >= '\t' && c <= '\r'); }
+inline bool is_seq_char(unsigned char c) { return !is_space(c) && !(c >= '0' && c <= '9'); }
+
+// Line [b, e) of data starting at pos, '\n' excluded; trailing '\r's excluded from e. Returns false if no complete
+// line is available (a final unterminated line counts as complete only at end of input).
+inline bool get_line(const char* data, size_t len, size_t& pos, bool eof, size_t& b, size_t& e) {
+    if (pos >= len) return false;
+    const char* nl = static_cast<const char*>(std::memchr(data + pos, '\n', len - pos));
+    size_t stop, next;
+    if (nl) {
+        stop = (size_t)(nl - data);
+        next = stop + 1;
+    } else {
+        if (!eof) return false;
+        stop = len;
+        next = len;
+    }
+    b = pos;
+    e = stop;
+    while (e > b && data[e - 1] == '\r') --e;
+    pos = next;
+    return true;
+}
+
+size_t count_seq(const char* p, size_t n) {
+    size_t c = 0;
+    for (size_t i = 0; i < n; ++i) c += is_seq_char((unsigned char)p[i]);
+    return c;
+}
+size_t count_nonspace(const char* p, size_t n) {
+    size_t c = 0;
+    for (size_t i = 0; i < n; ++i) c += !is_space((unsigned char)p[i]);
+    return c;
+}
+
+enum ScanResult { REC_COMPLETE, REC_NEED_MORE, REC_NONE };
+
+// Finds the end of the record starting at pos (blank lines first), validating the general grammar.
+ScanResult scan_record(const char* data, size_t len, size_t pos, bool eof, size_t& end, const std::string& path) {
+    size_t b = 0, e = 0;
+    for (;;) {
+        if (!get_line(data, len, pos, eof, b, e)) return eof ? REC_NONE : REC_NEED_MORE;
+        if (e > b) break;
+    }
+    if (data[b] != '@') {
+        if (data[b] == '>') throw IoError("reads must be FASTQ (qualities are required): " + path);
+        throw IoError("malformed FASTQ record header in " + path + ": " + std::string(data + b, std::min<size_t>(e - b, 80)));
+    }
+    size_t seq = 0, qual = 0;
+    for (;;) {
+        if (!get_line(data, len, pos, eof, b, e)) {
+            if (eof) throw IoError("truncated FASTQ record (no '+' line) in " + path);
+            return REC_NEED_MORE;
+        }
+        if (e > b && data[b] == '+') break;
+        seq += count_seq(data + b, e - b);
+    }
+    while (qual < seq) {
+        if (!get_line(data, len, pos, eof, b, e)) {
+            if (eof) break;
+            return REC_NEED_MORE;
+        }
+        qual += count_nonspace(data + b, e - b);
+    }
+    if (qual != seq) throw IoError("FASTQ record with sequence/quality length mismatch in " + path);
+    end = pos;
+    return REC_COMPLETE;
+}
+
+// Four-line record (@header / bases / '+' / qualities of the same raw length) found with four memchr and no
+// per-byte work; anything else (blank lines, wrapped records, CR-only oddities) goes through scan_record. The
+// parser re-checks every record against the general grammar (parse_record), so a fast cut never changes results.
+inline bool fast_record(const char* data, size_t len, size_t pos, bool eof, size_t& end) {
+    if (pos >= len || data[pos] != '@') return false;
+    size_t nl[4];
+    size_t p = pos;
+    for (int i = 0; i < 4; ++i) {
+        const char* q = p < len ? static_cast<const char*>(std::memchr(data + p, '\n', len - p)) : nullptr;
+        if (!q) {
+            if (i < 3 || !eof || p >= len) return false;
+            nl[i] = len;  // last line unterminated at end of input
+            p = len;
+            break;
+        }
+        nl[i] = (size_t)(q - data);
+        p = nl[i] + 1;
+        if (i == 1 && (p >= len || data[p] != '+')) return false;
+    }
+    auto trimmed = [&](size_t b, size_t e) {
+        while (e > b && data[e - 1] == '\r') --e;
+        return e - b;
+    };
+    const size_t l2 = trimmed(nl[0] + 1, nl[1]), l4 = trimmed(nl[2] + 1, nl[3]);
+    if (l2 != l4 || trimmed(pos, nl[0]) == 0) return false;
+    end = p;
+    return true;
+}
+
+// A decompressed buffer; blocks keep it alive until parsed. Bytes [0, len) are immutable once written.
+struct Buf {
+    std::unique_ptr<char[]> data;
+    size_t cap = 0, len = 0;
+};
+
+struct Block {
+    std::shared_ptr<Buf> buf;
+    size_t begin = 0, end = 0;
+    uint64_t n = 0;
+    const char* data() const { return buf ? buf->data.get() + begin : nullptr; }
+    size_t size() const { return end - begin; }
+};
+
+// Cuts record-aligned blocks out of one decompressed stream without copying them.
+class Cutter {
+public:
+    explicit Cutter(const std::string& path) : src_(path) {}
+    // Up to max_records complete records, stopping after the record that reaches max_bytes.
+    Block next(uint64_t max_records, uint64_t max_bytes) {
+        uint64_t n = 0;
+        if (!cur_) grow(0);
+        size_t pos = pos_;
+        while (n < max_records && (n == 0 || pos - pos_ < max_bytes)) {
+            const char* data = cur_->data.get();
+            size_t end = 0;
+            if (fast_record(data, cur_->len, pos, eof_, end)) {
+                pos = end;
+                ++n;
+                continue;
+            }
+            const ScanResult r = scan_record(data, cur_->len, pos, eof_, end, src_.path());
+            if (r == REC_COMPLETE) {
+                pos = end;
+                ++n;
+            } else if (r == REC_NONE) {
+                break;
+            } else {
+                pos = refill(pos);
+            }
+        }
+        Block blk{cur_, pos_, pos, n};
+        pos_ = pos;
+        return blk;
+    }
+
+private:
+    static constexpr size_t BUF_BYTES = 64u << 20, READ_BYTES = 16u << 20;
+    // Makes room for READ_BYTES more input; moves the unconsumed tail [pos_, len) into a fresh buffer when the
+    // current one is full (blocks still reference the old one). Returns `pos` translated into the new buffer.
+    size_t refill(size_t pos) {
+        if (cur_->cap - cur_->len < READ_BYTES) pos = grow(pos);
+        const size_t r = src_.read(cur_->data.get() + cur_->len, std::min(READ_BYTES, cur_->cap - cur_->len));
+        cur_->len += r;
+        if (r == 0) eof_ = true;
+        return pos;
+    }
+    size_t grow(size_t pos) {
+        auto nb = std::make_shared<Buf>();
+        const size_t tail = cur_ ? cur_->len - pos_ : 0;
+        nb->cap = std::max(BUF_BYTES, 2 * tail + READ_BYTES);
+        nb->data.reset(new char[nb->cap]);
+        if (tail) std::memcpy(nb->data.get(), cur_->data.get() + pos_, tail);
+        nb->len = tail;
+        const size_t shift = pos_;
+        cur_ = std::move(nb);
+        pos_ = 0;
+        return pos - shift;
+    }
+    Source src_;
+    std::shared_ptr<Buf> cur_;
+    size_t pos_ = 0;
+    bool eof_ = false;
+};
+
+// Parses the record at pos of a block into (seq, qual) at `out` with the general grammar; returns the new out.
+// Throws when the record is not what the cutter saw (only possible for pathological files; see fast_record).
+uint64_t parse_record(const char* data, size_t len, size_t& pos, uint8_t* seq, uint8_t* qual, uint64_t out,
+                      const char* path) {
+    auto line = [&](size_t& b, size_t& e) {
+        if (!get_line(data, len, pos, true, b, e))
+            throw IoError(std::string("irregular FASTQ record (sequence/quality line layout) in ") + path);
+    };
+    size_t b = 0, e = 0;
+    do {
+        line(b, e);
+    } while (e == b);
+    uint64_t s = out;
+    for (;;) {
+        line(b, e);
+        if (e > b && data[b] == '+') break;
+        const size_t n = e - b;
+        std::memcpy(seq + s, data + b, n);  // fast path: no blanks/digits inside the line
+        if (count_seq(data + b, n) == n) {
+            s += n;
+        } else {
+            for (size_t i = b; i < e; ++i)
+                if (is_seq_char((unsigned char)data[i])) seq[s++] = (uint8_t)data[i];
+        }
+    }
+    uint64_t q = out;
+    while (q < s) {  // every non-blank character of a quality line counts, as in scan_record
+        line(b, e);
+        const size_t n = e - b, c = count_nonspace(data + b, n);
+        if (q + c > s) throw IoError(std::string("FASTQ record with sequence/quality length mismatch in ") + path);
+        if (c == n) {
+            std::memcpy(qual + q, data + b, n);
+        } else {
+            uint64_t w = q;
+            for (size_t i = b; i < e; ++i)
+                if (!is_space((unsigned char)data[i])) qual[w++] = (uint8_t)data[i];
+        }
+        q += c;
+    }
+    return s;
+}
+
+struct Work {
+    Block b1, b2;
+    uint64_t n = 0;  // records (pairs when paired) to parse
+};
+
+struct Shared {
+    std::mutex mu;
+    std::condition_variable cv_put, cv_get;
+    std::deque<Work> q;
+    size_t max_q = 4;
+    bool done = false;
+    std::atomic<bool> failed{false};
+    std::string error;
+    bool io_error = false;
+    std::atomic<uint64_t> records{0}, bases{0}, batches{0};
+    void fail(const std::string& msg, bool io) {
+        std::lock_guard<std::mutex> lk(mu);
+        if (!failed.exchange(true)) {
+            error = msg;
+            io_error = io;
+        }
+        done = true;
+        cv_put.notify_all();
+        cv_get.notify_all();
+    }
+};
+
+void check_rc(int rc) {
+    if (rc != SPEQ_OK) throw speq::DeviceError(speq_last_error());
+}
+
+
+// Where parsed blocks go: pinned pipeline slots (speq_scan_fastq) or host memory (speq_fastq_checksum, CPU tests).
+struct Sink {
+    virtual ~Sink() = default;
+    virtual void acquire(speq_slot& s, uint64_t bytes, uint64_t records) = 0;
+    virtual void submit(const speq_slot& s, uint64_t records) = 0;  // records == 0 releases the slot
+};
+
+struct PipelineSink final : Sink {
+    speq_pipeline* pl;
+    explicit PipelineSink(speq_pipeline* p) : pl(p) {}
+    void acquire(speq_slot& s, uint64_t bytes, uint64_t records) override {
+        check_rc(speq_pipeline_acquire(pl, &s));
+        if (bytes > s.cap_bytes || records > s.cap_records) {
+            const int rc = speq_pipeline_reserve(pl, &s, bytes, records);
+            if (rc != SPEQ_OK) {
+                (void)speq_pipeline_submit(pl, s.slot, 0);
+                check_rc(rc);
+            }
+        }
+    }
+    void submit(const speq_slot& s, uint64_t records) override { check_rc(speq_pipeline_submit(pl, s.slot, records)); }
+};
+
+// Order-independent digest of the parsed records (sum over records of a 64-bit hash of length, bases and
+// qualities), so CPU tests can check the reader/parser without a GPU.
+struct ChecksumSink final : Sink {
+    std::mutex mu;
+    std::atomic<uint64_t> digest{0};
+    struct Held {
+        std::vector<uint8_t> seq, qual;
+        std::vector<uint64_t> off;
+    };
+    std::vector<std::unique_ptr<Held>> held;
+    std::vector<int> free_ids;
+    void acquire(speq_slot& s, uint64_t bytes, uint64_t records) override {
+        std::lock_guard<std::mutex> lk(mu);
+        int id;
+        if (free_ids.empty()) {
+            id = (int)held.size();
+            held.push_back(std::make_unique<Held>());
+        } else {
+            id = free_ids.back();
+            free_ids.pop_back();
+        }
+        Held& h = *held[(size_t)id];
+        h.seq.resize(std::max<uint64_t>(bytes, 1));
+        h.qual.resize(std::max<uint64_t>(bytes, 1));
+        h.off.resize(records + 1);
+        s.seq = h.seq.data();
+        s.qual = h.qual.data();
+        s.offsets = h.off.data();
+        s.cap_bytes = bytes;
+        s.cap_records = records;
+        s.slot = id;
+    }
+    static uint64_t mix(uint64_t z) {
+        z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ULL;
+        z = (z ^ (z >> 27)) * 0x94d049bb133111ebULL;
+        return z ^ (z >> 31);
+    }
+    void submit(const speq_slot& s, uint64_t records) override {
+        uint64_t acc = 0;
+        for (uint64_t r = 0; r < records; ++r) {
+            uint64_t h = 0x9e3779b97f4a7c15ULL ^ (s.offsets[r + 1] - s.offsets[r]);
+            for (uint64_t i = s.offsets[r]; i < s.offsets[r + 1]; ++i)
+                h = (h ^ ((uint64_t)s.seq[i] << 8 | s.qual[i])) * 0x100000001b3ULL;
+            acc += mix(h);
+        }
+        digest += acc;
+        std::lock_guard<std::mutex> lk(mu);
+        free_ids.push_back(s.slot);
+    }
+};
+
+struct StreamTotals {
+    uint64_t records = 0, bases = 0, batches = 0;
+};
+
+// Reader thread (cutting blocks of both files in step) + n_parsers parser threads feeding `sink`.
+StreamTotals run_stream(const char* path1, const char* path2, uint32_t threads, Sink& sink) {
+    const bool paired = path2 != nullptr;
+    const uint32_t n_parsers = std::max<uint32_t>(1, std::min<uint32_t>(threads ? threads : 1, 64));
+    const uint64_t BLOCK_RECORDS = 1u << 17, BLOCK_BYTES = 48ull << 20;
+    // opened here so that a missing file fails before any thread starts
+    Cutter c1(path1);
+    std::unique_ptr<Cutter> c2;
+    if (paired) c2 = std::make_unique<Cutter>(path2);
+    Shared sh;
+    sh.max_q = n_parsers + 1;
+    auto reader = [&] {
+        try {
+            for (;;) {
+                Work w;
+                w.b1 = c1.next(BLOCK_RECORDS, BLOCK_BYTES);
+                w.n = w.b1.n;
+                if (paired && w.n) {
+                    w.b2 = c2->next(w.n, ~0ull);
+                    w.n = std::min(w.n, w.b2.n);  // views::zip stops at the shorter file
+                }
+                const bool last = w.n == 0 || (paired && w.b2.n < w.b1.n);
+                if (w.n) {
+                    std::unique_lock<std::mutex> lk(sh.mu);
+                    sh.cv_put.wait(lk, [&] { return sh.q.size() < sh.max_q || sh.failed; });
+                    if (sh.failed) return;
+                    sh.q.push_back(std::move(w));
+                    sh.cv_get.notify_one();
+                }
+                if (last) break;
+            }
+            std::lock_guard<std::mutex> lk(sh.mu);
+            sh.done = true;
+            sh.cv_get.notify_all();
+        } catch (const IoError& e) {
+            sh.fail(e.what(), true);
+        } catch (const std::exception& e) {
+            sh.fail(e.what(), false);
+        }
+    };
+    auto parser = [&] {
+        try {
+            for (;;) {
+                Work w;
+                {
+                    std::unique_lock<std::mutex> lk(sh.mu);
+                    sh.cv_get.wait(lk, [&] { return !sh.q.empty() || sh.done; });
+                    if (sh.failed || sh.q.empty()) return;
+                    w = std::move(sh.q.front());
+                    sh.q.pop_front();
+                    sh.cv_put.notify_one();
+                }
+                speq_slot s;
+                const uint64_t recs = paired ? 2 * w.n : w.n;
+                sink.acquire(s, w.b1.size() + w.b2.size(), recs);
+                uint64_t out = 0;
+                size_t p1 = 0, p2 = 0;
+                s.offsets[0] = 0;
+                try {
+                    for (uint64_t i = 0; i < w.n; ++i) {
+                        out = parse_record(w.b1.data(), w.b1.size(), p1, s.seq, s.qual, out, path1);
+                        if (paired) {
+                            s.offsets[2 * i + 1] = out;
+                            out = parse_record(w.b2.data(), w.b2.size(), p2, s.seq, s.qual, out, path2);
+                            s.offsets[2 * i + 2] = out;
+                        } else {
+                            s.offsets[i + 1] = out;
+                        }
+                    }
+                    // the general grammar must end exactly where the cutter did
+                    if ((w.n == w.b1.n && p1 != w.b1.size()) || (paired && p2 != w.b2.size()))
+                        throw IoError(std::string("irregular FASTQ record layout in ") +
+                                      (p1 != w.b1.size() ? path1 : path2));
+                } catch (...) {
+                    sink.submit(s, 0);
+                    throw;
+                }
+                sink.submit(s, recs);
+                sh.records += recs;
+                sh.bases += out;
+                sh.batches += 1;
+                if (sh.failed) return;
+            }
+        } catch (const IoError& e) {
+            sh.fail(e.what(), true);
+        } catch (const std::exception& e) {
+            sh.fail(e.what(), false);
+        }
+    };
+    std::vector<std::thread> ts;
+    ts.emplace_back(reader);
+    for (uint32_t i = 0; i < n_parsers; ++i) ts.emplace_back(parser);
+    for (auto& t : ts) t.join();
+    if (sh.failed) {
+        if (sh.io_error) throw IoError(sh.error);
+        throw speq::DeviceError(sh.error);
+    }
+    return {sh.records.load(), sh.bases.load(), sh.batches.load()};
+}
+
+}  // namespace
+
+extern "C" int speq_scan_fastq(speq_device_index* d, const char* path1, const char* path2,
+                               const speq_scan_params* params, speq_em* em, uint32_t threads, uint64_t* counts,
+                               double* weights, speq_stream_stats* stats) {
+    return speq::guarded([&] {
+        if (!d || !path1 || !params || !counts) throw std::invalid_argument("speq_scan_fastq: null argument");
+        if (params->mode == SPEQ_MODE_LOCAL && !weights)
+            throw std::invalid_argument("speq_scan_fastq: local mode needs weights");
+        const bool paired = path2 != nullptr;
+        if ((params->paired != 0) != paired)
+            throw std::invalid_argument("speq_scan_fastq: params->paired must match the presence of path2");
+        const auto t0 = std::chrono::steady_clock::now();
+        const uint32_t n_parsers = std::max<uint32_t>(1, std::min<uint32_t>(threads ? threads : 1, 64));
+        speq_pipeline* pl = nullptr;
+        check_rc(speq_pipeline_create(d, params, em, 24ull << 20, paired ? 2u << 17 : 1u << 17, n_parsers + 2, &pl));
+        std::unique_ptr<speq_pipeline, void (*)(speq_pipeline*)> pl_guard(pl, speq_pipeline_free);
+        PipelineSink sink(pl);
+        StreamTotals tot;
+        try {
+            tot = run_stream(path1, path2, threads, sink);
+        } catch (...) {
+            std::vector<uint64_t> scratch(SPEQ_COUNTS_LEN(speq::device_groups(d)));
+            std::vector<double> wscratch(std::max<uint32_t>(speq::device_groups(d), 1));
+            (void)speq_pipeline_finish(pl, scratch.data(), wscratch.data());
+            throw;
+        }
+        check_rc(speq_pipeline_finish(pl, counts, weights));
+        if (stats) {
+            stats->records = tot.records;
+            stats->bases = tot.bases;
+            stats->batches = tot.batches;
+            stats->seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+        }
+    });
+}
+
+extern "C" int speq_fastq_checksum(const char* path1, const char* path2, uint32_t threads, uint64_t* records,
+                                   uint64_t* bases, uint64_t* digest) {
+    return speq::guarded([&] {
+        if (!path1 || !records || !bases || !digest) throw std::invalid_argument("speq_fastq_checksum: null argument");
+        ChecksumSink sink;
+        const StreamTotals tot = run_stream(path1, path2, threads, sink);
+        *records = tot.records;
+        *bases = tot.bases;
+        *digest = sink.digest.load();
+    });
+}

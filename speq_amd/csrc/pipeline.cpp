@@ -1,0 +1,374 @@
+// Streaming scan pipeline: pinned host slots -> H2D on a copy stream -> k_scan on a compute stream.
+//
+// Replaces the reference's producer/consumer read path: one async_input_buffer thread parsing FASTQ for T-1 search
+// workers (/root/reference/src/fm_scanner.cpp:138-141, :219-222; paired :651-655). Here producers fill page-locked
+// slots; a submit enqueues three async copies on the copy stream, an event, and the kernel on the compute stream
+// behind that event, so the PCIe copy of slot i+1 overlaps the scan of slot i. A slot is handed out again only after
+// the event recorded behind its kernel has completed (its host and device buffers are then free).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <atomic>
+#include <condition_variable>
+#include <cstring>
+#include <deque>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "capi_internal.hpp"
+#include "em.hpp"
+#include "scan_internal.hpp"
+
+namespace {
+
+void hip_ok(hipError_t e, const char* what) {
+    if (e != hipSuccess) throw speq::DeviceError(std::string(what) + ": " + hipGetErrorString(e));
+}
+
+struct DevScope {
+    int prev = -1;
+    explicit DevScope(int dev) {
+        hip_ok(hipGetDevice(&prev), "hipGetDevice");
+        if (prev != dev) hip_ok(hipSetDevice(dev), "hipSetDevice");
+    }
+    ~DevScope() {
+        int cur = -1;
+        if (hipGetDevice(&cur) == hipSuccess && cur != prev && prev >= 0) (void)hipSetDevice(prev);
+    }
+};
+
+struct Slot {
+    uint8_t* h_seq = nullptr;
+    uint8_t* h_qual = nullptr;
+    uint64_t* h_off = nullptr;
+    uint8_t* d_seq = nullptr;
+    uint8_t* d_qual = nullptr;
+    uint64_t* d_off = nullptr;
+    uint64_t cap_bytes = 0, cap_records = 0;
+    hipEvent_t copied = nullptr, done = nullptr;
+    bool pending = false;  // `done` recorded and not yet waited for
+};
+
+void free_buffers(Slot& s) {
+    if (s.h_seq) (void)hipHostFree(s.h_seq);
+    if (s.h_qual) (void)hipHostFree(s.h_qual);
+    if (s.h_off) (void)hipHostFree(s.h_off);
+    if (s.d_seq) (void)hipFree(s.d_seq);
+    if (s.d_qual) (void)hipFree(s.d_qual);
+    if (s.d_off) (void)hipFree(s.d_off);
+    s.h_seq = s.h_qual = s.d_seq = s.d_qual = nullptr;
+    s.h_off = s.d_off = nullptr;
+    s.cap_bytes = s.cap_records = 0;
+}
+
+void alloc_buffers(Slot& s, uint64_t bytes, uint64_t records) {
+    free_buffers(s);
+    bytes = std::max<uint64_t>(bytes, 64);
+    records = std::max<uint64_t>(records, 2);
+    hip_ok(hipHostMalloc(reinterpret_cast<void**>(&s.h_seq), bytes, hipHostMallocDefault), "hipHostMalloc");
+    hip_ok(hipHostMalloc(reinterpret_cast<void**>(&s.h_qual), bytes, hipHostMallocDefault), "hipHostMalloc");
+    hip_ok(hipHostMalloc(reinterpret_cast<void**>(&s.h_off), (records + 1) * 8, hipHostMallocDefault),
+           "hipHostMalloc");
+    hip_ok(hipMalloc(reinterpret_cast<void**>(&s.d_seq), bytes), "hipMalloc");
+    hip_ok(hipMalloc(reinterpret_cast<void**>(&s.d_qual), bytes), "hipMalloc");
+    hip_ok(hipMalloc(reinterpret_cast<void**>(&s.d_off), (records + 1) * 8), "hipMalloc");
+    s.cap_bytes = bytes;
+    s.cap_records = records;
+}
+
+}  // namespace
+
+struct speq_pipeline {
+    speq_device_index* d = nullptr;
+    speq_scan_params p{};
+    speq_em* em = nullptr;
+    int device = 0;
+    uint32_t G = 0;
+    hipStream_t copy = nullptr, compute = nullptr;
+    uint64_t* d_counts = nullptr;
+    double* d_w = nullptr;
+    std::vector<Slot> slots;
+    std::mutex mu;              // free list
+    std::condition_variable cv;
+    std::deque<int> free_slots;
+    std::mutex submit_mu;       // stream order of copies and launches
+
+    ~speq_pipeline() {
+        if (compute) (void)hipStreamSynchronize(compute);
+        if (copy) (void)hipStreamSynchronize(copy);
+        for (Slot& s : slots) {
+            free_buffers(s);
+            if (s.copied) (void)hipEventDestroy(s.copied);
+            if (s.done) (void)hipEventDestroy(s.done);
+        }
+        if (d_counts) (void)hipFree(d_counts);
+        if (d_w) (void)hipFree(d_w);
+        if (copy) (void)hipStreamDestroy(copy);
+        if (compute) (void)hipStreamDestroy(compute);
+    }
+};
+
+extern "C" {
+
+int speq_pipeline_create(speq_device_index* d, const speq_scan_params* params, speq_em* em, uint64_t slot_bytes,
+                         uint64_t slot_records, uint32_t n_slots, speq_pipeline** out) {
+    return speq::guarded([&] {
+        if (!d || !params || !out) throw std::invalid_argument("speq_pipeline_create: null argument");
+        if (n_slots < 2 || n_slots > 64) throw std::invalid_argument("speq_pipeline_create: n_slots must be in [2, 64]");
+        if (params->paired && (slot_records & 1))
+            throw std::invalid_argument("speq_pipeline_create: paired scans need an even slot_records");
+        if (em && (em->dev != d || em->finalized))
+            throw std::invalid_argument("speq_pipeline_create: EM histogram of another device, or finalized");
+        if (params->mode != SPEQ_MODE_GLOBAL && params->mode != SPEQ_MODE_LOCAL)
+            throw std::invalid_argument("speq_pipeline_create: bad mode");
+        auto pl = std::make_unique<speq_pipeline>();
+        pl->d = d;
+        pl->p = *params;
+        pl->em = em;
+        pl->device = speq::device_ordinal(d);
+        pl->G = speq::device_groups(d);
+        DevScope g(pl->device);
+        hip_ok(hipStreamCreateWithFlags(&pl->copy, hipStreamNonBlocking), "hipStreamCreate");
+        hip_ok(hipStreamCreateWithFlags(&pl->compute, hipStreamNonBlocking), "hipStreamCreate");
+        hip_ok(hipMalloc(reinterpret_cast<void**>(&pl->d_counts), SPEQ_COUNTS_LEN(pl->G) * 8), "hipMalloc");
+        hip_ok(hipMemsetAsync(pl->d_counts, 0, SPEQ_COUNTS_LEN(pl->G) * 8, pl->compute), "hipMemset");
+        hip_ok(hipMalloc(reinterpret_cast<void**>(&pl->d_w), std::max<uint32_t>(pl->G, 1) * 8), "hipMalloc");
+        hip_ok(hipMemsetAsync(pl->d_w, 0, std::max<uint32_t>(pl->G, 1) * 8, pl->compute), "hipMemset");
+        pl->slots.resize(n_slots);
+        for (uint32_t i = 0; i < n_slots; ++i) {
+            Slot& s = pl->slots[i];
+            hip_ok(hipEventCreateWithFlags(&s.copied, hipEventDisableTiming), "hipEventCreate");
+            hip_ok(hipEventCreateWithFlags(&s.done, hipEventDisableTiming), "hipEventCreate");
+            alloc_buffers(s, slot_bytes, slot_records);
+            pl->free_slots.push_back((int)i);
+        }
+        hip_ok(hipStreamSynchronize(pl->compute), "hipStreamSynchronize");
+        *out = pl.release();
+    });
+}
+
+int speq_pipeline_acquire(speq_pipeline* pl, speq_slot* out) {
+    return speq::guarded([&] {
+        if (!pl || !out) throw std::invalid_argument("speq_pipeline_acquire: null argument");
+        int i;
+        {
+            std::unique_lock<std::mutex> lk(pl->mu);
+            pl->cv.wait(lk, [&] { return !pl->free_slots.empty(); });
+            i = pl->free_slots.front();
+            pl->free_slots.pop_front();
+        }
+        Slot& s = pl->slots[(size_t)i];
+        if (s.pending) {
+            hip_ok(hipEventSynchronize(s.done), "hipEventSynchronize");
+            s.pending = false;
+        }
+        out->seq = s.h_seq;
+        out->qual = s.h_qual;
+        out->offsets = s.h_off;
+        out->cap_bytes = s.cap_bytes;
+        out->cap_records = s.cap_records;
+        out->slot = i;
+    });
+}
+
+int speq_pipeline_reserve(speq_pipeline* pl, speq_slot* slot, uint64_t bytes, uint64_t records) {
+    return speq::guarded([&] {
+        if (!pl || !slot || slot->slot < 0 || (size_t)slot->slot >= pl->slots.size())
+            throw std::invalid_argument("speq_pipeline_reserve: bad slot");
+        Slot& s = pl->slots[(size_t)slot->slot];
+        if (bytes > s.cap_bytes || records > s.cap_records) {
+            DevScope g(pl->device);
+            alloc_buffers(s, std::max(bytes, s.cap_bytes), std::max(records, s.cap_records));
+        }
+        slot->seq = s.h_seq;
+        slot->qual = s.h_qual;
+        slot->offsets = s.h_off;
+        slot->cap_bytes = s.cap_bytes;
+        slot->cap_records = s.cap_records;
+    });
+}
+
+int speq_pipeline_submit(speq_pipeline* pl, int32_t slot, uint64_t n_records) {
+    auto release = [&] {
+        {
+            std::lock_guard<std::mutex> lk(pl->mu);
+            pl->free_slots.push_back(slot);
+        }
+        pl->cv.notify_one();
+    };
+    if (!pl || slot < 0 || (size_t)slot >= pl->slots.size())
+        return speq::guarded([] { throw std::invalid_argument("speq_pipeline_submit: bad slot"); });
+    const int rc = speq::guarded([&] {
+        Slot& s = pl->slots[(size_t)slot];
+        if (n_records == 0) return;
+        if (n_records > s.cap_records) throw std::invalid_argument("speq_pipeline_submit: more records than capacity");
+        if (pl->p.paired && (n_records & 1))
+            throw std::invalid_argument("speq_pipeline_submit: paired scan needs an even record count");
+        const uint64_t* off = s.h_off;
+        if (off[0] != 0) throw std::invalid_argument("speq_pipeline_submit: offsets[0] must be 0");
+        for (uint64_t i = 0; i < n_records; ++i)
+            if (off[i + 1] < off[i]) throw std::invalid_argument("speq_pipeline_submit: offsets must be non-decreasing");
+        const uint64_t bytes = off[n_records];
+        if (bytes > s.cap_bytes) throw std::invalid_argument("speq_pipeline_submit: offsets exceed the slot capacity");
+        DevScope g(pl->device);
+        std::lock_guard<std::mutex> lk(pl->submit_mu);
+        if (bytes) {
+            hip_ok(hipMemcpyAsync(s.d_seq, s.h_seq, bytes, hipMemcpyHostToDevice, pl->copy), "hipMemcpyAsync");
+            hip_ok(hipMemcpyAsync(s.d_qual, s.h_qual, bytes, hipMemcpyHostToDevice, pl->copy), "hipMemcpyAsync");
+        }
+        hip_ok(hipMemcpyAsync(s.d_off, s.h_off, (n_records + 1) * 8, hipMemcpyHostToDevice, pl->copy),
+               "hipMemcpyAsync");
+        hip_ok(hipEventRecord(s.copied, pl->copy), "hipEventRecord");
+        hip_ok(hipStreamWaitEvent(pl->compute, s.copied, 0), "hipStreamWaitEvent");
+        speq::launch_reads_scan(pl->d, s.d_seq, s.d_qual, s.d_off, n_records, &pl->p, pl->d_counts, pl->d_w,
+                                pl->em ? pl->em->d_mult : nullptr, pl->em ? pl->em->d_hi : nullptr, pl->compute);
+        hip_ok(hipEventRecord(s.done, pl->compute), "hipEventRecord");
+        s.pending = true;
+    });
+    release();
+    return rc;
+}
+
+int speq_pipeline_finish(speq_pipeline* pl, uint64_t* counts, double* weights) {
+    return speq::guarded([&] {
+        if (!pl || !counts) throw std::invalid_argument("speq_pipeline_finish: null argument");
+        if (pl->p.mode == SPEQ_MODE_LOCAL && !weights)
+            throw std::invalid_argument("speq_pipeline_finish: local mode needs weights");
+        DevScope g(pl->device);
+        std::lock_guard<std::mutex> lk(pl->submit_mu);
+        const size_t nc = SPEQ_COUNTS_LEN(pl->G);
+        hip_ok(hipMemcpyAsync(counts, pl->d_counts, nc * 8, hipMemcpyDeviceToHost, pl->compute), "hipMemcpyAsync");
+        if (weights && pl->p.mode == SPEQ_MODE_LOCAL)
+            hip_ok(hipMemcpyAsync(weights, pl->d_w, pl->G * 8, hipMemcpyDeviceToHost, pl->compute), "hipMemcpyAsync");
+        hip_ok(hipMemsetAsync(pl->d_counts, 0, nc * 8, pl->compute), "hipMemsetAsync");
+        if (pl->d_w) hip_ok(hipMemsetAsync(pl->d_w, 0, pl->G * 8, pl->compute), "hipMemsetAsync");
+        hip_ok(hipStreamSynchronize(pl->compute), "hipStreamSynchronize");
+    });
+}
+
+void speq_pipeline_free(speq_pipeline* pl) { delete pl; }
+
+}  // extern "C"
+
+// ---- host-buffer scans (speq_scan_reads / speq_em_scan_reads) over the pipeline ----
+// Whole units are cut into batches of <= 32 MiB of bases; up to four filler threads copy batches into pinned slots
+// (pageable -> pinned memcpy) and submit them, so the PCIe copy and the kernel of different batches overlap.
+namespace {
+// Idle host-scan pipelines per device (pinned allocation costs more than a typical scan); never destroyed at exit.
+std::mutex g_cache_mu;
+auto* g_cache = new std::multimap<const speq_device_index*, speq_pipeline*>();
+
+speq_pipeline* take_pipeline(speq_device_index* d, const speq_scan_params* p, speq_em* em, uint64_t bytes,
+                             uint64_t recs) {
+    {
+        std::lock_guard<std::mutex> lk(g_cache_mu);
+        auto it = g_cache->find(d);
+        if (it != g_cache->end()) {
+            speq_pipeline* pl = it->second;
+            g_cache->erase(it);
+            pl->p = *p;
+            pl->em = em;
+            return pl;
+        }
+    }
+    speq_pipeline* pl = nullptr;
+    if (speq_pipeline_create(d, p, em, bytes, recs + (recs & 1), 6, &pl) != SPEQ_OK)
+        throw speq::DeviceError(speq_last_error());
+    return pl;
+}
+
+void put_pipeline(speq_device_index* d, speq_pipeline* pl) {
+    pl->em = nullptr;
+    std::lock_guard<std::mutex> lk(g_cache_mu);
+    g_cache->emplace(d, pl);
+}
+}  // namespace
+
+namespace speq {
+void release_host_pipelines(const speq_device_index* d) {
+    std::vector<speq_pipeline*> v;
+    {
+        std::lock_guard<std::mutex> lk(g_cache_mu);
+        auto r = g_cache->equal_range(d);
+        for (auto it = r.first; it != r.second; ++it) v.push_back(it->second);
+        g_cache->erase(d);
+    }
+    for (speq_pipeline* pl : v) delete pl;
+}
+
+void scan_host_pipelined(speq_device_index* d, const uint8_t* seq, const uint8_t* qual, const uint64_t* offsets,
+                         uint64_t n_reads, const speq_scan_params* p, speq_em* em, uint64_t* counts,
+                         double* weights) {
+    if (!d || !p || !counts || (!offsets && n_reads)) throw std::invalid_argument("speq_scan_reads: null argument");
+    if (p->mode == SPEQ_MODE_LOCAL && !weights) throw std::invalid_argument("speq_scan_reads: local mode needs weights");
+    if (p->paired && (n_reads & 1)) throw std::invalid_argument("speq_scan_reads: paired scan needs an even record count");
+    const uint32_t G = device_groups(d);
+    std::fill(counts, counts + SPEQ_COUNTS_LEN(G), 0ull);
+    if (weights) std::fill(weights, weights + G, 0.0);
+    if (n_reads == 0) return;
+    for (uint64_t i = 0; i < n_reads; ++i)
+        if (offsets[i + 1] < offsets[i]) throw std::invalid_argument("speq_scan_reads: offsets must be non-decreasing");
+    if (offsets[n_reads] > offsets[0] && (!seq || !qual)) throw std::invalid_argument("speq_scan_reads: null read buffer");
+    const uint64_t BATCH_BYTES = 32ull << 20, BATCH_RECORDS = 1u << 17;
+    const uint64_t step = p->paired ? 2 : 1;
+    std::vector<std::pair<uint64_t, uint64_t>> batches;
+    uint64_t max_bytes = 1, max_recs = step;
+    for (uint64_t r0 = 0; r0 < n_reads;) {
+        uint64_t r1 = r0 + step;
+        while (r1 < n_reads && r1 - r0 < BATCH_RECORDS && offsets[r1 + step] - offsets[r0] <= BATCH_BYTES) r1 += step;
+        batches.emplace_back(r0, r1);
+        max_bytes = std::max(max_bytes, offsets[r1] - offsets[r0]);
+        max_recs = std::max(max_recs, r1 - r0);
+        r0 = r1;
+    }
+    const uint32_t fillers = (uint32_t)std::min<size_t>(4, batches.size());
+    std::unique_ptr<speq_pipeline, void (*)(speq_pipeline*)> guard(take_pipeline(d, p, em, max_bytes, max_recs),
+                                                                   speq_pipeline_free);
+    speq_pipeline* pl = guard.get();
+    std::atomic<size_t> next{0};
+    std::mutex err_mu;
+    std::string err;
+    auto fill = [&] {
+        for (;;) {
+            const size_t b = next++;
+            if (b >= batches.size()) return;
+            speq_slot s;
+            if (speq_pipeline_acquire(pl, &s) != SPEQ_OK) {
+                std::lock_guard<std::mutex> lk(err_mu);
+                if (err.empty()) err = speq_last_error();
+                return;
+            }
+            const uint64_t r0 = batches[b].first, r1 = batches[b].second, base = offsets[r0];
+            const uint64_t nb = offsets[r1] - base;
+            if ((nb > s.cap_bytes || r1 - r0 > s.cap_records) &&
+                speq_pipeline_reserve(pl, &s, nb, r1 - r0) != SPEQ_OK) {
+                std::lock_guard<std::mutex> lk(err_mu);
+                if (err.empty()) err = speq_last_error();
+                (void)speq_pipeline_submit(pl, s.slot, 0);
+                return;
+            }
+            if (nb) {
+                std::memcpy(s.seq, seq + base, nb);
+                std::memcpy(s.qual, qual + base, nb);
+            }
+            for (uint64_t i = r0; i <= r1; ++i) s.offsets[i - r0] = offsets[i] - base;
+            if (speq_pipeline_submit(pl, s.slot, r1 - r0) != SPEQ_OK) {
+                std::lock_guard<std::mutex> lk(err_mu);
+                if (err.empty()) err = speq_last_error();
+                return;
+            }
+        }
+    };
+    std::vector<std::thread> ts;
+    for (uint32_t i = 1; i < fillers; ++i) ts.emplace_back(fill);
+    fill();
+    for (auto& t : ts) t.join();
+    if (speq_pipeline_finish(pl, counts, weights) != SPEQ_OK) throw DeviceError(speq_last_error());
+    if (!err.empty()) throw DeviceError(err);
+    put_pipeline(d, guard.release());  // counters are zero again after finish
+}
+}  // namespace speq

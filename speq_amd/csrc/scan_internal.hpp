@@ -1,0 +1,21 @@
+// Internal entry points of the device half (scan_kernels.hip) used by the host-side streaming pipeline.
+#pragma once
+#include <cstdint>
+
+#include "speq_scan.h"
+
+namespace speq {
+// Enqueues one k_scan launch over reads already in device memory on `stream`; counters accumulate into d_counts
+// (and d_weights in local mode); em_mult/em_hi record multi-group intervals when non-null (EM scans).
+void launch_reads_scan(speq_device_index* d, const uint8_t* d_seq, const uint8_t* d_qual, const uint64_t* d_offsets,
+                       uint64_t n_reads, const speq_scan_params* p, uint64_t* d_counts, double* d_weights,
+                       uint32_t* em_mult, uint32_t* em_hi, void* stream);
+// Host-buffer scan through a pinned-slot pipeline (pipeline.cpp); counts/weights overwritten with the totals.
+void scan_host_pipelined(speq_device_index* d, const uint8_t* seq, const uint8_t* qual, const uint64_t* offsets,
+                         uint64_t n_reads, const speq_scan_params* p, speq_em* em, uint64_t* counts,
+                         double* weights);
+// Frees the idle host-scan pipelines cached for a device (called by speq_device_close).
+void release_host_pipelines(const speq_device_index* d);
+int device_ordinal(const speq_device_index* d);
+uint32_t device_groups(const speq_device_index* d);
+}  // namespace speq

@@ -32,6 +32,7 @@
 
 #include "capi_internal.hpp"
 #include "em.hpp"
+#include "scan_internal.hpp"
 #include "fm_index.hpp"
 
 namespace {
@@ -762,68 +763,6 @@ static void scan_device_impl(speq_device_index* d, const uint8_t* d_seq, const u
     }
 }
 
-static void scan_host_impl(speq_device_index* d, const uint8_t* seq, const uint8_t* qual, const uint64_t* offsets,
-                    uint64_t n_reads, const speq_scan_params* p, uint64_t* counts, double* weights,
-                    uint32_t* em_mult, uint32_t* em_hi) {
-    if (!d || !p || !counts || (!offsets && n_reads)) throw std::invalid_argument("speq_scan_reads: null argument");
-    if (p->mode == SPEQ_MODE_LOCAL && !weights) throw std::invalid_argument("speq_scan_reads: local mode needs weights");
-    if (p->paired && (n_reads & 1)) throw std::invalid_argument("speq_scan_reads: paired scan needs an even record count");
-    const uint32_t G = d->G;
-    std::fill(counts, counts + SPEQ_COUNTS_LEN(G), 0ull);
-    if (weights) std::fill(weights, weights + G, 0.0);
-    if (n_reads == 0) return;
-    for (uint64_t i = 0; i < n_reads; ++i)
-        if (offsets[i + 1] < offsets[i]) throw std::invalid_argument("speq_scan_reads: offsets must be non-decreasing");
-    DeviceGuard g(d->device);
-    hipStream_t st = d->stream;
-    // Batches [r0, r1) of whole units holding at most BATCH_BYTES of bases (or a single larger unit).
-    const uint64_t BATCH_BYTES = 256ull << 20;
-    const uint64_t step = p->paired ? 2 : 1;
-    std::vector<std::pair<uint64_t, uint64_t>> batches;
-    uint64_t max_bytes = 1, max_reads = 1;
-    for (uint64_t r0 = 0; r0 < n_reads;) {
-        uint64_t r1 = r0 + step;
-        while (r1 < n_reads && offsets[r1 + step] - offsets[r0] <= BATCH_BYTES) r1 += step;
-        batches.emplace_back(r0, r1);
-        max_bytes = std::max(max_bytes, offsets[r1] - offsets[r0]);
-        max_reads = std::max(max_reads, r1 - r0);
-        r0 = r1;
-    }
-    struct Free {
-        std::vector<void*> p;
-        ~Free() { for (void* x : p) if (x) (void)hipFree(x); }
-    } fr;
-    auto alloc = [&](size_t bytes) {
-        void* x = nullptr;
-        HIP_OK(hipMalloc(&x, bytes));
-        fr.p.push_back(x);
-        return x;
-    };
-    auto* d_counts = static_cast<uint64_t*>(alloc(SPEQ_COUNTS_LEN(G) * 8));
-    double* d_w = p->mode == SPEQ_MODE_LOCAL ? static_cast<double*>(alloc(G * 8)) : nullptr;
-    auto* d_seq = static_cast<uint8_t*>(alloc(max_bytes));
-    auto* d_qual = static_cast<uint8_t*>(alloc(max_bytes));
-    auto* d_off = static_cast<uint64_t*>(alloc((max_reads + 1) * 8));
-    HIP_OK(hipMemsetAsync(d_counts, 0, SPEQ_COUNTS_LEN(G) * 8, st));
-    if (d_w) HIP_OK(hipMemsetAsync(d_w, 0, G * 8, st));
-    std::vector<uint64_t> rel;
-    for (const auto& bt : batches) {
-        const uint64_t r0 = bt.first, r1 = bt.second;
-        const uint64_t nb = offsets[r1] - offsets[r0], nr = r1 - r0;
-        rel.resize(nr + 1);
-        for (uint64_t i = 0; i <= nr; ++i) rel[i] = offsets[r0 + i] - offsets[r0];
-        if (nb) {
-            HIP_OK(hipMemcpyAsync(d_seq, seq + offsets[r0], nb, hipMemcpyHostToDevice, st));
-            HIP_OK(hipMemcpyAsync(d_qual, qual + offsets[r0], nb, hipMemcpyHostToDevice, st));
-        }
-        HIP_OK(hipMemcpyAsync(d_off, rel.data(), (nr + 1) * 8, hipMemcpyHostToDevice, st));
-        scan_device_impl(d, d_seq, d_qual, d_off, nr, p, d_counts, d_w, em_mult, em_hi, st);
-        HIP_OK(hipStreamSynchronize(st));  // `rel` and the device staging buffers are reused next batch
-    }
-    HIP_OK(hipMemcpyAsync(counts, d_counts, SPEQ_COUNTS_LEN(G) * 8, hipMemcpyDeviceToHost, st));
-    if (d_w) HIP_OK(hipMemcpyAsync(weights, d_w, G * 8, hipMemcpyDeviceToHost, st));
-    HIP_OK(hipStreamSynchronize(st));
-}
 
 extern "C" {
 
@@ -887,6 +826,7 @@ int speq_device_open(const speq_index* idx, int device, speq_device_index** out)
 int speq_device_close(speq_device_index* d) {
     return speq::guarded([&] {
         if (!d) return;
+        speq::release_host_pipelines(d);
         DeviceGuard g(d->device);
         for (auto& e : d->events) {
             (void)hipEventDestroy(e.first);
@@ -910,7 +850,7 @@ int speq_scan_reads_device(speq_device_index* d, const uint8_t* d_seq, const uin
 
 int speq_scan_reads(speq_device_index* d, const uint8_t* seq, const uint8_t* qual, const uint64_t* offsets,
                     uint64_t n_reads, const speq_scan_params* p, uint64_t* counts, double* weights) {
-    return speq::guarded([&] { scan_host_impl(d, seq, qual, offsets, n_reads, p, counts, weights, nullptr, nullptr); });
+    return speq::guarded([&] { speq::scan_host_pipelined(d, seq, qual, offsets, n_reads, p, nullptr, counts, weights); });
 }
 
 // ---- EM histogram (see em.hpp) ----
@@ -935,7 +875,7 @@ int speq_em_scan_reads(speq_em* em, const uint8_t* seq, const uint8_t* qual, con
                        const speq_scan_params* p, uint64_t* counts, double* weights) {
     return speq::guarded([&] {
         if (!em || em->finalized) throw std::invalid_argument("speq_em_scan_reads: bad or finalized histogram");
-        scan_host_impl(em->dev, seq, qual, offsets, n_reads, p, counts, weights, em->d_mult, em->d_hi);
+        speq::scan_host_pipelined(em->dev, seq, qual, offsets, n_reads, p, em, counts, weights);
     });
 }
 
@@ -1072,3 +1012,15 @@ int speq_timing_read(speq_device_index* d, double* total_ms, uint64_t* launches)
 }
 
 }  // extern "C"
+
+// ---- internal entry points for the streaming pipeline (pipeline.cpp; scan_internal.hpp) ----
+namespace speq {
+void launch_reads_scan(speq_device_index* d, const uint8_t* d_seq, const uint8_t* d_qual, const uint64_t* d_offsets,
+                       uint64_t n_reads, const speq_scan_params* p, uint64_t* d_counts, double* d_weights,
+                       uint32_t* em_mult, uint32_t* em_hi, void* stream) {
+    scan_device_impl(d, d_seq, d_qual, d_offsets, n_reads, p, d_counts, d_weights, em_mult, em_hi,
+                     static_cast<hipStream_t>(stream));
+}
+int device_ordinal(const speq_device_index* d) { return d->device; }
+uint32_t device_groups(const speq_device_index* d) { return d->G; }
+}  // namespace speq

@@ -1,0 +1,172 @@
+"""GPU: the streaming front end (speq_scan_fastq: FASTQ/.gz reader thread -> parser threads -> pinned slots -> H2D on
+a copy stream overlapped with k_scan) and the speq_pipeline_* slot API give exactly the counters of the in-memory
+scan (and of the golden vectors). Integer counters bit-exact; W rtol 1e-12 (block order changes the fp64 sum order)."""
+import gzip
+import os
+
+import numpy as np
+import pytest
+
+from golden_io import CASES, Case
+from speq_amd import DeviceIndex, EmHistogram, FmIndex, Pipeline, SpeqError, synth
+
+pytestmark = pytest.mark.gpu
+
+
+def write_fastq(path, seqs, quals, wrap=0, crlf=False, blank=False, gz=False):
+    nl = "\r\n" if crlf else "\n"
+    out = []
+    for i, (s, q) in enumerate(zip(seqs, quals)):
+        s, q = s.decode(), q.decode()
+        out.append(f"@read{i} extra words{nl}")
+        if wrap:
+            out += [s[j:j + wrap] + nl for j in range(0, max(len(s), 1), wrap)] if s else [nl]
+            out.append("+" + nl)
+            out += [q[j:j + wrap] + nl for j in range(0, len(q), wrap)]
+        else:
+            out += [s + nl, "+read" + nl, q + nl]
+        if blank and i % 7 == 3:
+            out.append(nl)
+    data = "".join(out).encode()
+    with (gzip.open(path, "wb", compresslevel=1) if gz else open(path, "wb")) as f:
+        f.write(data)
+
+
+def split(reads):
+    seqs, quals = [], []
+    for i in range(len(reads.offsets) - 1):
+        a, b = int(reads.offsets[i]), int(reads.offsets[i + 1])
+        seqs.append(reads.seq[a:b].tobytes())
+        quals.append(reads.qual[a:b].tobytes())
+    return seqs, quals
+
+
+def same(a, b, local):
+    assert (a.total, a.ambiguous, a.unique.tolist()) == (b.total, b.ambiguous, b.unique.tolist())
+    if local:
+        np.testing.assert_allclose(a.weights, b.weights, rtol=1e-12)
+
+
+@pytest.mark.parametrize("name", CASES)
+@pytest.mark.parametrize("gz", [False, True])
+def test_scan_fastq_matches_golden(tmp_path, name, gz):
+    c = Case(name)
+    dev = DeviceIndex(FmIndex.build(c.records, c.groups, c.G, prefix_q=4))
+    p1 = os.path.join(c.dir, "reads_1.fq")
+    p2 = os.path.join(c.dir, "reads_2.fq") if c.paired else None
+    if gz:
+        for src in filter(None, [p1, p2]):
+            with open(src, "rb") as f, gzip.open(tmp_path / (os.path.basename(src) + ".gz"), "wb") as g:
+                g.write(f.read())
+        p1 = str(tmp_path / "reads_1.fq.gz")
+        p2 = str(tmp_path / "reads_2.fq.gz") if c.paired else None
+    for k in c.ks:
+        for mode in ("global", "local"):
+            g = c.exp["by_k"][str(k)][mode]
+            r, st = dev.scan_fastq(p1, p2, k=k, phred_cutoff=c.cutoff, local=mode == "local", threads=3)
+            assert (r.total, r.ambiguous, r.unique.tolist()) == (g["T"], g["ambiguous"], g["U"])
+            if mode == "local":
+                np.testing.assert_allclose(r.weights, g["W"], rtol=1e-12)
+            assert st["records"] == len(c.offsets) - 1
+
+
+@pytest.mark.parametrize("fmt", [dict(), dict(wrap=37, crlf=True, blank=True), dict(gz=True, wrap=60)])
+@pytest.mark.parametrize("paired", [False, True])
+def test_scan_fastq_formats_match_in_memory(tmp_path, fmt, paired):
+    ref = synth.make_reference(4, 2, 20_000, ref_n_rate=0.0005)
+    n = 150_000 if not fmt else 40_000  # > one 131072-record block for the plain case
+    reads = synth.make_reads(ref, n // (2 if paired else 1), paired=paired, n_rate=0.001, lowq_rate=0.005,
+                             short_frac=0.0 if paired else 0.02)
+    dev = DeviceIndex(FmIndex.build(ref.records, ref.groups, 4, prefix_q=10))
+    seqs, quals = split(reads)
+    if paired:
+        write_fastq(tmp_path / "r1.fq", seqs[0::2], quals[0::2], **fmt)
+        write_fastq(tmp_path / "r2.fq", seqs[1::2], quals[1::2], **fmt)
+        p1, p2 = str(tmp_path / "r1.fq"), str(tmp_path / "r2.fq")
+    else:
+        write_fastq(tmp_path / "r1.fq", seqs, quals, **fmt)
+        p1, p2 = str(tmp_path / "r1.fq"), None
+    for local in (False, True):
+        exp = dev.scan(reads.seq.tobytes(), reads.qual.tobytes(), reads.offsets, k=21, paired=paired, local=local)
+        for threads in (1, 6):
+            got, st = dev.scan_fastq(p1, p2, k=21, local=local, threads=threads)
+            same(got, exp, local)
+            assert st["records"] == reads.n and st["bases"] == int(reads.offsets[-1])
+
+
+def test_paired_files_of_unequal_length_zip_to_the_shorter(tmp_path):
+    ref = synth.make_reference(3, 1, 5_000)
+    reads = synth.make_reads(ref, 500, paired=True)
+    seqs, quals = split(reads)
+    write_fastq(tmp_path / "r1.fq", seqs[0::2], quals[0::2])
+    write_fastq(tmp_path / "r2.fq", seqs[1:401:2], quals[1:401:2])  # 200 mates only
+    dev = DeviceIndex(FmIndex.build(ref.records, ref.groups, 3, prefix_q=6))
+    got, st = dev.scan_fastq(str(tmp_path / "r1.fq"), str(tmp_path / "r2.fq"), k=21)
+    exp = dev.scan(reads.seq.tobytes(), reads.qual.tobytes(), reads.offsets[:401], k=21, paired=True)
+    same(got, exp, False)
+    assert st["records"] == 400
+
+
+def test_scan_fastq_errors(tmp_path):
+    ref = synth.make_reference(2, 1, 2_000)
+    dev = DeviceIndex(FmIndex.build(ref.records, ref.groups, 2, prefix_q=4))
+    (tmp_path / "a.fa").write_text(">r\nACGT\n")
+    (tmp_path / "trunc.fq").write_text("@r\nACGTACGT\n")
+    (tmp_path / "mismatch.fq").write_text("@r\nACGTACGT\n+\nIIII\n")
+    (tmp_path / "bad.fq").write_text("@r\nACGT\n+\nIIII\nxyz\n")
+    for f, msg in (("a.fa", "qualities are required"), ("trunc.fq", "truncated"), ("missing.fq", "cannot open"),
+                   ("bad.fq", "malformed")):
+        with pytest.raises(SpeqError, match=msg):
+            dev.scan_fastq(str(tmp_path / f), k=3)
+    with pytest.raises(SpeqError, match="mismatch"):
+        dev.scan_fastq(str(tmp_path / "mismatch.fq"), k=3)
+    (tmp_path / "empty.fq").write_text("")
+    r, st = dev.scan_fastq(str(tmp_path / "empty.fq"), k=3)
+    assert r.total == 0 and st["records"] == 0
+
+
+@pytest.mark.parametrize("local", [False, True])
+def test_pipeline_slots_equal_one_scan(local):
+    ref = synth.make_reference(5, 1, 8_000)
+    reads = synth.make_reads(ref, 6_000, n_rate=0.001, short_frac=0.05)
+    dev = DeviceIndex(FmIndex.build(ref.records, ref.groups, 5, prefix_q=8))
+    exp = dev.scan(reads.seq.tobytes(), reads.qual.tobytes(), reads.offsets, k=25, local=local)
+    pl = Pipeline(dev, k=25, local=local, slot_bytes=64 << 10, slot_records=256, n_slots=3)
+    seq, qual = reads.seq.tobytes(), reads.qual.tobytes()
+    cuts = [0, 1, 700, 701, 3000, 5999, 6000]  # includes 1-record slots and one larger than the slot (grows)
+    for a, b in zip(cuts, cuts[1:]):
+        pl.put(seq, qual, reads.offsets[a:b + 1])
+    same(pl.finish(), exp, local)
+    # finish resets the counters
+    pl.put(seq, qual, reads.offsets[:11])
+    part = dev.scan(seq, qual, reads.offsets[:11], k=25, local=local)
+    same(pl.finish(), part, local)
+    pl.close()
+
+
+def test_em_histogram_through_stream(tmp_path):
+    ref = synth.make_reference(4, 2, 6_000)
+    reads = synth.make_reads(ref, 3_000)
+    seqs, quals = split(reads)
+    write_fastq(tmp_path / "r.fq.gz", seqs, quals, gz=True)
+    dev = DeviceIndex(FmIndex.build(ref.records, ref.groups, 4, prefix_q=8))
+    em1, em2 = EmHistogram(dev), EmHistogram(dev)
+    r1 = em1.scan(reads.seq.tobytes(), reads.qual.tobytes(), reads.offsets, k=21)
+    r2, _ = dev.scan_fastq(str(tmp_path / "r.fq.gz"), k=21, em=em2, threads=4)
+    same(r1, r2, False)
+    em1.finalize()
+    em2.finalize()
+    assert em1.info() == em2.info()
+    p = np.array([10.0, 20.0, 30.0, 40.0])
+    np.testing.assert_array_equal(em1.step(p, [2, 2, 2, 2], r1.unique), em2.step(p, [2, 2, 2, 2], r2.unique))
+
+
+def test_pipeline_rejects_bad_input():
+    ref = synth.make_reference(2, 1, 2_000)
+    dev = DeviceIndex(FmIndex.build(ref.records, ref.groups, 2, prefix_q=4))
+    with pytest.raises(SpeqError):
+        Pipeline(dev, k=21, paired=True, slot_records=3)
+    pl = Pipeline(dev, k=21, paired=True, slot_records=4)
+    with pytest.raises(SpeqError, match="even"):
+        pl.put(b"ACGT" * 3, b"IIII" * 3, np.array([0, 4, 8, 12], dtype=np.uint64))
+    pl.close()
