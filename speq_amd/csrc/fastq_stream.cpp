@@ -11,6 +11,8 @@
 // as bases have been read; whitespace and digits inside sequence lines are dropped, whitespace inside quality
 // lines is dropped; a FASTA file is rejected (qualities are required).
 #include <fcntl.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
 #include <unistd.h>
 #include <zlib.h>
 
@@ -81,6 +83,8 @@ public:
         return got;
     }
     const std::string& path() const { return path_; }
+    bool plain() const { return gz_ == nullptr; }
+    int fd() const { return fd_; }
 
 private:
     int fd_ = -1;
@@ -186,31 +190,57 @@ inline bool fast_record(const char* data, size_t len, size_t pos, bool eof, size
     return true;
 }
 
-// A decompressed buffer; blocks keep it alive until parsed. Bytes [0, len) are immutable once written.
+// A decompressed buffer, or the whole mapping of a plain file; blocks keep it alive until parsed. Bytes [0, len)
+// are immutable once written.
 struct Buf {
-    std::unique_ptr<char[]> data;
+    std::unique_ptr<char[]> own;
+    char* ptr = nullptr;
     size_t cap = 0, len = 0;
+    void* map = nullptr;
+    size_t map_len = 0;
+    ~Buf() {
+        if (map) ::munmap(map, map_len);
+    }
+    char* data() const { return ptr; }
 };
 
 struct Block {
     std::shared_ptr<Buf> buf;
     size_t begin = 0, end = 0;
     uint64_t n = 0;
-    const char* data() const { return buf ? buf->data.get() + begin : nullptr; }
+    const char* data() const { return buf ? buf->data() + begin : nullptr; }
     size_t size() const { return end - begin; }
 };
 
 // Cuts record-aligned blocks out of one decompressed stream without copying them.
 class Cutter {
 public:
-    explicit Cutter(const std::string& path) : src_(path) {}
+    // Plain files are mapped whole (no read copies; parsers read the page cache directly); gzip is inflated into
+    // 64 MiB buffers.
+    explicit Cutter(const std::string& path) : src_(path) {
+        if (!src_.plain()) return;
+        struct stat st {};
+        if (::fstat(src_.fd(), &st) != 0 || !S_ISREG(st.st_mode)) return;  // pipes etc.: read path
+        auto b = std::make_shared<Buf>();
+        if (st.st_size > 0) {
+            void* m = ::mmap(nullptr, (size_t)st.st_size, PROT_READ, MAP_PRIVATE | MAP_POPULATE, src_.fd(), 0);
+            if (m == MAP_FAILED) return;
+            (void)::madvise(m, (size_t)st.st_size, MADV_SEQUENTIAL);
+            b->map = m;
+            b->map_len = (size_t)st.st_size;
+            b->ptr = static_cast<char*>(m);
+            b->cap = b->len = (size_t)st.st_size;
+        }
+        cur_ = std::move(b);
+        eof_ = true;
+    }
     // Up to max_records complete records, stopping after the record that reaches max_bytes.
     Block next(uint64_t max_records, uint64_t max_bytes) {
         uint64_t n = 0;
         if (!cur_) grow(0);
         size_t pos = pos_;
         while (n < max_records && (n == 0 || pos - pos_ < max_bytes)) {
-            const char* data = cur_->data.get();
+            const char* data = cur_->data();
             size_t end = 0;
             if (fast_record(data, cur_->len, pos, eof_, end)) {
                 pos = end;
@@ -238,7 +268,7 @@ private:
     // current one is full (blocks still reference the old one). Returns `pos` translated into the new buffer.
     size_t refill(size_t pos) {
         if (cur_->cap - cur_->len < READ_BYTES) pos = grow(pos);
-        const size_t r = src_.read(cur_->data.get() + cur_->len, std::min(READ_BYTES, cur_->cap - cur_->len));
+        const size_t r = src_.read(cur_->data() + cur_->len, std::min(READ_BYTES, cur_->cap - cur_->len));
         cur_->len += r;
         if (r == 0) eof_ = true;
         return pos;
@@ -247,8 +277,9 @@ private:
         auto nb = std::make_shared<Buf>();
         const size_t tail = cur_ ? cur_->len - pos_ : 0;
         nb->cap = std::max(BUF_BYTES, 2 * tail + READ_BYTES);
-        nb->data.reset(new char[nb->cap]);
-        if (tail) std::memcpy(nb->data.get(), cur_->data.get() + pos_, tail);
+        nb->own.reset(new char[nb->cap]);
+        nb->ptr = nb->own.get();
+        if (tail) std::memcpy(nb->ptr, cur_->data() + pos_, tail);
         nb->len = tail;
         const size_t shift = pos_;
         cur_ = std::move(nb);
@@ -417,7 +448,7 @@ struct StreamTotals {
 StreamTotals run_stream(const char* path1, const char* path2, uint32_t threads, Sink& sink) {
     const bool paired = path2 != nullptr;
     const uint32_t n_parsers = std::max<uint32_t>(1, std::min<uint32_t>(threads ? threads : 1, 64));
-    const uint64_t BLOCK_RECORDS = 1u << 17, BLOCK_BYTES = 48ull << 20;
+    const uint64_t BLOCK_RECORDS = 1u << 15, BLOCK_BYTES = 12ull << 20;
     // opened here so that a missing file fails before any thread starts
     Cutter c1(path1);
     std::unique_ptr<Cutter> c2;
@@ -527,9 +558,10 @@ extern "C" int speq_scan_fastq(speq_device_index* d, const char* path1, const ch
             throw std::invalid_argument("speq_scan_fastq: params->paired must match the presence of path2");
         const auto t0 = std::chrono::steady_clock::now();
         const uint32_t n_parsers = std::max<uint32_t>(1, std::min<uint32_t>(threads ? threads : 1, 64));
-        speq_pipeline* pl = nullptr;
-        check_rc(speq_pipeline_create(d, params, em, 24ull << 20, paired ? 2u << 17 : 1u << 17, n_parsers + 2, &pl));
-        std::unique_ptr<speq_pipeline, void (*)(speq_pipeline*)> pl_guard(pl, speq_pipeline_free);
+        std::unique_ptr<speq_pipeline, void (*)(speq_pipeline*)> pl_guard(
+            speq::acquire_cached_pipeline(d, params, em, 8ull << 20, paired ? 2u << 15 : 1u << 15, n_parsers + 2),
+            speq_pipeline_free);
+        speq_pipeline* pl = pl_guard.get();
         PipelineSink sink(pl);
         StreamTotals tot;
         try {
@@ -541,6 +573,7 @@ extern "C" int speq_scan_fastq(speq_device_index* d, const char* path1, const ch
             throw;
         }
         check_rc(speq_pipeline_finish(pl, counts, weights));
+        speq::return_cached_pipeline(d, pl_guard.release());
         if (stats) {
             stats->records = tot.records;
             stats->bases = tot.bases;

@@ -6,6 +6,9 @@
 #include "fm_index.hpp"
 
 #include <algorithm>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
 #include <cstdio>
 #include <cstring>
 #include <fstream>
@@ -168,9 +171,20 @@ void fm_build(FmIndex& idx, const char* seq, const uint64_t* rec_offsets, uint32
     idx.C[0] = 0;
     for (int c = 0; c < SYM_COUNT; ++c) idx.C[c + 1] = idx.C[c] + (uint32_t)cnt[c];
 
+    const bool show = std::getenv("SPEQ_BUILD_TIMING") != nullptr;
+    auto t_last = std::chrono::steady_clock::now();
+    auto phase = [&](const char* what) {
+        if (!show) return;
+        const auto t = std::chrono::steady_clock::now();
+        std::fprintf(stderr, "fm_build: %-10s %.3f s\n", what, std::chrono::duration<double>(t - t_last).count());
+        t_last = t;
+    };
+    phase("text");
+
     // Suffix array
     idx.sa.resize(n);
     sais_u8(idx.text.data(), idx.sa.data(), (int64_t)n, SYM_COUNT);
+    phase("sa");
 
     const uint64_t nb = idx.n_blocks();
     const uint8_t* T = idx.text.data();
@@ -188,6 +202,7 @@ void fm_build(FmIndex& idx, const char* seq, const uint64_t* rec_offsets, uint32
         }
     }
 
+    phase("occ");
     if (pair_steps) {
         // C2[ab] = #suffixes < "ab" = #positions p with T[p] < a, or T[p] == a and T[p+1] < b.
         uint64_t pc[SYM_COUNT][SYM_COUNT] = {{0}};
@@ -209,6 +224,7 @@ void fm_build(FmIndex& idx, const char* seq, const uint64_t* rec_offsets, uint32
         }
     }
 
+    phase("occ2");
     // Label of every SA position: group of the text that holds the suffix start.
     std::vector<uint16_t> label(n);
     const uint64_t* ts = idx.text_start.data();
@@ -237,6 +253,7 @@ void fm_build(FmIndex& idx, const char* seq, const uint64_t* rec_offsets, uint32
         }
     }
 
+    phase("labels");
     // q-mer interval table, built level by level by backward extension.
     if (prefix_q > 0) {
         const uint64_t Q = uint64_t(1) << (2 * prefix_q);
@@ -270,6 +287,7 @@ void fm_build(FmIndex& idx, const char* seq, const uint64_t* rec_offsets, uint32
         if (cur.size() != 2 * Q) throw std::runtime_error("fm_build: prefix table size mismatch");
         idx.prefix.swap(cur);
     }
+    phase("prefix");
 }
 
 // ---------------------------------------------------------------------------------------------

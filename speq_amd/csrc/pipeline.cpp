@@ -263,12 +263,13 @@ std::mutex g_cache_mu;
 auto* g_cache = new std::multimap<const speq_device_index*, speq_pipeline*>();
 
 speq_pipeline* take_pipeline(speq_device_index* d, const speq_scan_params* p, speq_em* em, uint64_t bytes,
-                             uint64_t recs) {
+                             uint64_t recs, uint32_t n_slots) {
     {
         std::lock_guard<std::mutex> lk(g_cache_mu);
-        auto it = g_cache->find(d);
-        if (it != g_cache->end()) {
+        auto r = g_cache->equal_range(d);
+        for (auto it = r.first; it != r.second; ++it) {
             speq_pipeline* pl = it->second;
+            if (pl->slots.size() < n_slots) continue;
             g_cache->erase(it);
             pl->p = *p;
             pl->em = em;
@@ -276,7 +277,7 @@ speq_pipeline* take_pipeline(speq_device_index* d, const speq_scan_params* p, sp
         }
     }
     speq_pipeline* pl = nullptr;
-    if (speq_pipeline_create(d, p, em, bytes, recs + (recs & 1), 6, &pl) != SPEQ_OK)
+    if (speq_pipeline_create(d, p, em, bytes, recs + (recs & 1), n_slots, &pl) != SPEQ_OK)
         throw speq::DeviceError(speq_last_error());
     return pl;
 }
@@ -289,6 +290,12 @@ void put_pipeline(speq_device_index* d, speq_pipeline* pl) {
 }  // namespace
 
 namespace speq {
+speq_pipeline* acquire_cached_pipeline(speq_device_index* d, const speq_scan_params* p, speq_em* em, uint64_t bytes,
+                                       uint64_t records, uint32_t n_slots) {
+    return take_pipeline(d, p, em, bytes, records, n_slots);
+}
+void return_cached_pipeline(speq_device_index* d, speq_pipeline* pl) { put_pipeline(d, pl); }
+
 void release_host_pipelines(const speq_device_index* d) {
     std::vector<speq_pipeline*> v;
     {
@@ -326,7 +333,7 @@ void scan_host_pipelined(speq_device_index* d, const uint8_t* seq, const uint8_t
         r0 = r1;
     }
     const uint32_t fillers = (uint32_t)std::min<size_t>(4, batches.size());
-    std::unique_ptr<speq_pipeline, void (*)(speq_pipeline*)> guard(take_pipeline(d, p, em, max_bytes, max_recs),
+    std::unique_ptr<speq_pipeline, void (*)(speq_pipeline*)> guard(take_pipeline(d, p, em, max_bytes, max_recs, 6),
                                                                    speq_pipeline_free);
     speq_pipeline* pl = guard.get();
     std::atomic<size_t> next{0};

@@ -14,6 +14,11 @@ void launch_reads_scan(speq_device_index* d, const uint8_t* d_seq, const uint8_t
 void scan_host_pipelined(speq_device_index* d, const uint8_t* seq, const uint8_t* qual, const uint64_t* offsets,
                          uint64_t n_reads, const speq_scan_params* p, speq_em* em, uint64_t* counts,
                          double* weights);
+// Per-device cache of idle pipelines (pinned slots are costly to allocate): take one with >= n_slots slots
+// (rebinding params/em) or create it; return it only after a successful speq_pipeline_finish (counters zero).
+speq_pipeline* acquire_cached_pipeline(speq_device_index* d, const speq_scan_params* p, speq_em* em, uint64_t bytes,
+                                       uint64_t records, uint32_t n_slots);
+void return_cached_pipeline(speq_device_index* d, speq_pipeline* pl);
 // Frees the idle host-scan pipelines cached for a device (called by speq_device_close).
 void release_host_pipelines(const speq_device_index* d);
 int device_ordinal(const speq_device_index* d);
