@@ -15,7 +15,7 @@ LIB      := speq_amd/libspeq_scan.so
 CLI      := bin/speq
 OBJDIR   := build/obj
 
-LIB_HIP  := speq_amd/csrc/scan_kernels.hip
+LIB_HIP  := speq_amd/csrc/scan_kernels.hip speq_amd/csrc/build_gpu.hip
 LIB_CPP  := speq_amd/csrc/sais.cpp speq_amd/csrc/fm_index.cpp speq_amd/csrc/capi.cpp speq_amd/csrc/comm.cpp \
             speq_amd/csrc/host_io.cpp speq_amd/csrc/em.cpp speq_amd/csrc/pipeline.cpp \
             speq_amd/csrc/fastq_stream.cpp
@@ -55,7 +55,7 @@ oracle:
 #   make variant NAME=hibranch VFLAGS=-DSPEQ_HI_BRANCH=1
 variant: $(filter-out $(OBJDIR)/scan_kernels.o,$(LIB_OBJS))
 	@mkdir -p build/variants/$(NAME)
-	$(HIPCC) $(HIPFLAGS) $(VFLAGS) -c $(LIB_HIP) -o build/variants/$(NAME)/scan_kernels.o
+	$(HIPCC) $(HIPFLAGS) $(VFLAGS) -c speq_amd/csrc/scan_kernels.hip -o build/variants/$(NAME)/scan_kernels.o
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o build/variants/$(NAME)/libspeq_scan.so \
 	    build/variants/$(NAME)/scan_kernels.o $^ -L/opt/rocm/lib -lrccl -lamdhip64 -lz -lpthread -Wl,-rpath,/opt/rocm/lib
 

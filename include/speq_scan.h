@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define SPEQ_ABI_VERSION 1
+#define SPEQ_ABI_VERSION 2
 
 enum {
     SPEQ_OK = 0,
@@ -55,6 +55,9 @@ typedef struct {
     uint32_t threads;    /* host threads for the build (0 = all) */
     uint32_t pair_steps; /* 1: add the 16 two-symbol occ planes (LF over two bases per gather pair) */
     uint32_t label_table;/* 1: add the per-SA-position {group, run distance} table (one-load classification) */
+    uint32_t gpu_build;  /* 1: build the suffix array and planes on GPU `device` (prefix doubling on radix sorts);
+                            0: host SA-IS. Both produce identical indexes. */
+    int32_t device;      /* GPU ordinal for gpu_build */
 } speq_build_opts;
 
 /* Per-scan parameters (reference: cmd_arguments in include/arg_parse.h:10-28). */

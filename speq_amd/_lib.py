@@ -27,7 +27,7 @@ SPEQ_MODE_GLOBAL, SPEQ_MODE_LOCAL = 0, 1
 
 class BuildOpts(C.Structure):
     _fields_ = [("prefix_q", C.c_uint32), ("threads", C.c_uint32), ("pair_steps", C.c_uint32),
-                ("label_table", C.c_uint32)]
+                ("label_table", C.c_uint32), ("gpu_build", C.c_uint32), ("device", C.c_int32)]
 
 
 class ScanParams(C.Structure):

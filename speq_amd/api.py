@@ -89,11 +89,13 @@ class FmIndex:
     @classmethod
     def build(cls, records: Sequence[bytes | str], group_of_record: Sequence[int], n_groups: int,
               prefix_q: int = 0, threads: int = 0, pair_steps: bool = False,
-              label_table: bool = False) -> "FmIndex":
+              label_table: bool = False, gpu_device: Optional[int] = None) -> "FmIndex":
+        """gpu_device: build the suffix array and planes on that GPU (None = host SA-IS); identical results."""
         seq, off = pack_records(records)
         grp = np.asarray(group_of_record, dtype=np.int32)
         h = C.c_void_p()
-        opts = BuildOpts(prefix_q, threads, int(pair_steps), int(label_table))
+        opts = BuildOpts(prefix_q, threads, int(pair_steps), int(label_table), int(gpu_device is not None),
+                         gpu_device if gpu_device is not None else 0)
         check(lib().speq_index_build(seq, _u64p(off), len(records), grp.ctypes.data_as(C.POINTER(C.c_int32)),
                                      len(grp), n_groups, C.byref(opts), C.byref(h)))
         return cls(h)

@@ -47,6 +47,7 @@ const char* HELP =
     "      --prefix-q N          q-mer lookup table of the FM-index (default 11, 0 = off)\n"
     "      --pair-steps 0|1      two-base LF planes in the FM-index (default 1)\n"
     "      --label-table 0|1     per-position group/run table: one-load classification (default 1)\n"
+    "      --gpu-build auto|0|1  build the suffix array on the GPU (default auto: when one is visible)\n"
     "      --device N            GPU ordinal (default $LOCAL_RANK or 0)\n";
 
 template <typename T>
@@ -115,6 +116,11 @@ CmdArguments parse(int argc, char** argv) {
         else if (allow_refs && opt == "--prefix-q") a.prefix_q = to_number<unsigned>(opt, value());
         else if (allow_refs && opt == "--pair-steps") a.pair_steps = to_number<unsigned>(opt, value()) != 0;
         else if (allow_refs && opt == "--label-table") a.label_table = to_number<unsigned>(opt, value()) != 0;
+        else if (allow_refs && opt == "--gpu-build") {
+            const std::string v = value();
+            if (v == "auto") a.gpu_build = -1;
+            else a.gpu_build = to_number<unsigned>(opt, v) != 0 ? 1 : 0;
+        }
         else if (opt == "--device") a.device = to_number<int>(opt, value());
         else if (allow_reads && opt == "--max-em-iterations") a.max_em_iterations = to_number<unsigned>(opt, value());
         else throw ParseError("Unknown option " + opt + ". In case this is meant to be a non-option/argument/parameter, "
@@ -266,7 +272,13 @@ bool read_index_header(const fs::path& p, IndexHeader& h) {
 void generate_fm_index(const CmdArguments& a, const fs::path& idx_path, const IndexHeader& h) {
     speq::SeqBatch refs = speq::read_sequences(a.in_file_references.string(), false);
     if (refs.size() == 0) throw CApiError("no sequences in reference file " + a.in_file_references.string());
-    speq_build_opts opts{a.prefix_q, a.threads, a.pair_steps ? 1u : 0u, a.label_table ? 1u : 0u};
+    int bdev = a.device;
+    if (bdev < 0) {
+        const char* lr = std::getenv("LOCAL_RANK");
+        bdev = lr ? std::atoi(lr) : 0;
+    }
+    const bool gpu = a.gpu_build == 1 || (a.gpu_build < 0 && speq_device_count() > 0);
+    speq_build_opts opts{a.prefix_q, a.threads, a.pair_steps ? 1u : 0u, a.label_table ? 1u : 0u, gpu ? 1u : 0u, bdev};
     speq_index* idx = nullptr;
     ok(speq_index_build(refs.seq.data(), refs.offsets.data(), (uint32_t)refs.size(), h.scaffolds.data(),
                         (uint32_t)h.scaffolds.size(), (uint32_t)h.names.size(), &opts, &idx),

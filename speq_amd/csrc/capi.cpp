@@ -28,10 +28,17 @@ int speq_index_build(const char* seq, const uint64_t* rec_offsets, uint32_t n_re
             throw std::invalid_argument("speq_index_build: null argument");
         for (uint32_t r = 0; r < n_records; ++r)
             if (rec_offsets[r + 1] < rec_offsets[r]) throw std::invalid_argument("speq_index_build: offsets must be non-decreasing");
+        int gpu = -1;
+        if (opts && opts->gpu_build) {
+            const int ndev = speq_device_count();
+            if (ndev <= 0) throw speq::DeviceError("speq_index_build: gpu_build requested but no GPU is visible");
+            if (opts->device < 0 || opts->device >= ndev) throw std::invalid_argument("speq_index_build: bad device ordinal");
+            gpu = opts->device;
+        }
         auto idx = std::make_unique<speq_index>();
         speq::fm_build(idx->fm, seq, rec_offsets, n_records, group_of_rec, n_group_entries, n_groups,
                        opts ? opts->prefix_q : 0, opts ? opts->threads : 0, opts ? opts->pair_steps != 0 : false,
-                       opts ? opts->label_table != 0 : false);
+                       opts ? opts->label_table != 0 : false, gpu);
         *out = idx.release();
     });
 }

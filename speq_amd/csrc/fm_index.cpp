@@ -118,69 +118,11 @@ uint32_t FmIndex::run_of(uint64_t i) const {
     return entry_rank(runs[b], r + 1);
 }
 
-void fm_build(FmIndex& idx, const char* seq, const uint64_t* rec_offsets, uint32_t n_records,
-              const int32_t* group_of_rec, uint32_t n_group_entries, uint32_t n_groups, uint32_t prefix_q,
-              uint32_t threads, bool pair_steps, bool label_table) {
-    if (n_records == 0) throw std::invalid_argument("fm_build: no reference records");
-    if (n_groups == 0 || n_groups > 65535) throw std::invalid_argument("fm_build: n_groups must be in [1, 65535]");
-    if (prefix_q > MAX_PREFIX_Q) throw std::invalid_argument("fm_build: prefix_q > 13");
-    // Every record must belong to a group: the reference indexes group_scaffolds[t/2] unchecked
-    // (fm_scanner.cpp:170, :1102, :1518) -- unassigned (-1) or missing entries are UB there, rejected here.
-    if (n_group_entries < n_records)
-        throw GroupsError("groupings assign " + std::to_string(n_group_entries) + " record indices but the reference has " +
-                          std::to_string(n_records) + " records");
-    for (uint32_t r = 0; r < n_records; ++r) {
-        if (group_of_rec[r] < 0 || (uint32_t)group_of_rec[r] >= n_groups)
-            throw GroupsError("reference record " + std::to_string(r) + " is not assigned to a group");
-    }
+namespace {
 
-    idx = FmIndex();
-    idx.n_records = n_records;
-    idx.n_texts = 2 * n_records;
-    idx.n_groups = n_groups;
-    idx.prefix_q = prefix_q;
-    idx.group_of_rec.assign(group_of_rec, group_of_rec + n_group_entries);
-
-    uint64_t total = 1;
-    for (uint32_t r = 0; r < n_records; ++r) total += 2 * (rec_offsets[r + 1] - rec_offsets[r] + 1);
-    if (total >= (uint64_t(1) << 31)) throw std::invalid_argument("fm_build: collection exceeds 2^31 symbols");
-    idx.n = total;
-    idx.text.resize(total);
-    idx.text_start.resize(idx.n_texts + 1);
-    idx.text_group.resize(idx.n_texts);
-    uint64_t p = 0;
-    for (uint32_t r = 0; r < n_records; ++r) {
-        uint64_t b = rec_offsets[r], e = rec_offsets[r + 1], len = e - b;
-        idx.text_start[2 * r] = p;
-        for (uint64_t i = 0; i < len; ++i) idx.text[p + i] = ascii_to_sym((unsigned char)seq[b + i]);
-        idx.text[p + len] = SYM_SEP;
-        uint64_t q = p + len + 1;
-        idx.text_start[2 * r + 1] = q;
-        for (uint64_t i = 0; i < len; ++i) idx.text[q + i] = complement_sym(idx.text[p + len - 1 - i]);
-        idx.text[q + len] = SYM_SEP;
-        p = q + len + 1;
-        idx.text_group[2 * r] = idx.text_group[2 * r + 1] = group_of_rec[r];
-    }
-    idx.text[p] = SYM_TERM;
-    idx.text_start[idx.n_texts] = p;  // == n - 1
+template <typename Phase>
+void build_arrays_host(FmIndex& idx, uint32_t threads, bool pair_steps, bool label_table, Phase&& phase) {
     const uint64_t n = idx.n;
-
-    // C array
-    uint64_t cnt[SYM_COUNT] = {0};
-    for (uint64_t i = 0; i < n; ++i) cnt[idx.text[i]]++;
-    idx.C[0] = 0;
-    for (int c = 0; c < SYM_COUNT; ++c) idx.C[c + 1] = idx.C[c] + (uint32_t)cnt[c];
-
-    const bool show = std::getenv("SPEQ_BUILD_TIMING") != nullptr;
-    auto t_last = std::chrono::steady_clock::now();
-    auto phase = [&](const char* what) {
-        if (!show) return;
-        const auto t = std::chrono::steady_clock::now();
-        std::fprintf(stderr, "fm_build: %-10s %.3f s\n", what, std::chrono::duration<double>(t - t_last).count());
-        t_last = t;
-    };
-    phase("text");
-
     // Suffix array
     idx.sa.resize(n);
     sais_u8(idx.text.data(), idx.sa.data(), (int64_t)n, SYM_COUNT);
@@ -253,6 +195,78 @@ void fm_build(FmIndex& idx, const char* seq, const uint64_t* rec_offsets, uint32
         }
     }
 
+}
+
+}  // namespace
+
+void fm_build(FmIndex& idx, const char* seq, const uint64_t* rec_offsets, uint32_t n_records,
+              const int32_t* group_of_rec, uint32_t n_group_entries, uint32_t n_groups, uint32_t prefix_q,
+              uint32_t threads, bool pair_steps, bool label_table, int gpu_device) {
+    if (n_records == 0) throw std::invalid_argument("fm_build: no reference records");
+    if (n_groups == 0 || n_groups > 65535) throw std::invalid_argument("fm_build: n_groups must be in [1, 65535]");
+    if (prefix_q > MAX_PREFIX_Q) throw std::invalid_argument("fm_build: prefix_q > 13");
+    // Every record must belong to a group: the reference indexes group_scaffolds[t/2] unchecked
+    // (fm_scanner.cpp:170, :1102, :1518) -- unassigned (-1) or missing entries are UB there, rejected here.
+    if (n_group_entries < n_records)
+        throw GroupsError("groupings assign " + std::to_string(n_group_entries) + " record indices but the reference has " +
+                          std::to_string(n_records) + " records");
+    for (uint32_t r = 0; r < n_records; ++r) {
+        if (group_of_rec[r] < 0 || (uint32_t)group_of_rec[r] >= n_groups)
+            throw GroupsError("reference record " + std::to_string(r) + " is not assigned to a group");
+    }
+
+    idx = FmIndex();
+    idx.n_records = n_records;
+    idx.n_texts = 2 * n_records;
+    idx.n_groups = n_groups;
+    idx.prefix_q = prefix_q;
+    idx.group_of_rec.assign(group_of_rec, group_of_rec + n_group_entries);
+
+    uint64_t total = 1;
+    for (uint32_t r = 0; r < n_records; ++r) total += 2 * (rec_offsets[r + 1] - rec_offsets[r] + 1);
+    if (total >= (uint64_t(1) << 31)) throw std::invalid_argument("fm_build: collection exceeds 2^31 symbols");
+    idx.n = total;
+    idx.text.resize(total);
+    idx.text_start.resize(idx.n_texts + 1);
+    idx.text_group.resize(idx.n_texts);
+    uint64_t p = 0;
+    for (uint32_t r = 0; r < n_records; ++r) {
+        uint64_t b = rec_offsets[r], e = rec_offsets[r + 1], len = e - b;
+        idx.text_start[2 * r] = p;
+        for (uint64_t i = 0; i < len; ++i) idx.text[p + i] = ascii_to_sym((unsigned char)seq[b + i]);
+        idx.text[p + len] = SYM_SEP;
+        uint64_t q = p + len + 1;
+        idx.text_start[2 * r + 1] = q;
+        for (uint64_t i = 0; i < len; ++i) idx.text[q + i] = complement_sym(idx.text[p + len - 1 - i]);
+        idx.text[q + len] = SYM_SEP;
+        p = q + len + 1;
+        idx.text_group[2 * r] = idx.text_group[2 * r + 1] = group_of_rec[r];
+    }
+    idx.text[p] = SYM_TERM;
+    idx.text_start[idx.n_texts] = p;  // == n - 1
+    const uint64_t n = idx.n;
+
+    // C array
+    uint64_t cnt[SYM_COUNT] = {0};
+    for (uint64_t i = 0; i < n; ++i) cnt[idx.text[i]]++;
+    idx.C[0] = 0;
+    for (int c = 0; c < SYM_COUNT; ++c) idx.C[c + 1] = idx.C[c] + (uint32_t)cnt[c];
+
+    const bool show = std::getenv("SPEQ_BUILD_TIMING") != nullptr;
+    auto t_last = std::chrono::steady_clock::now();
+    auto phase = [&](const char* what) {
+        if (!show) return;
+        const auto t = std::chrono::steady_clock::now();
+        std::fprintf(stderr, "fm_build: %-10s %.3f s\n", what, std::chrono::duration<double>(t - t_last).count());
+        t_last = t;
+    };
+    phase("text");
+
+    if (gpu_device >= 0) {
+        fm_build_arrays_gpu(idx, gpu_device, pair_steps, label_table, show);
+    } else {
+        build_arrays_host(idx, threads, pair_steps, label_table, phase);
+    }
     phase("labels");
     // q-mer interval table, built level by level by backward extension.
     if (prefix_q > 0) {

@@ -94,7 +94,9 @@ struct FmIndex {
 // Builds the index (throws std::invalid_argument / std::runtime_error).
 void fm_build(FmIndex& idx, const char* seq, const uint64_t* rec_offsets, uint32_t n_records,
               const int32_t* group_of_rec, uint32_t n_group_entries, uint32_t n_groups, uint32_t prefix_q,
-              uint32_t threads, bool pair_steps = false, bool label_table = false);
+              uint32_t threads, bool pair_steps = false, bool label_table = false, int gpu_device = -1);
+// GPU half of fm_build (build_gpu.hip): suffix array, occ/occ2/runs planes, run labels and label table.
+void fm_build_arrays_gpu(FmIndex& idx, int device, bool pair_steps, bool label_table, bool timing);
 
 void fm_save(const FmIndex& idx, const std::string& path, const void* header, uint64_t header_len);
 void fm_load(FmIndex& idx, const std::string& path, std::vector<uint8_t>* header);

@@ -1,0 +1,79 @@
+"""GPU index construction (build_gpu.hip: prefix-doubling suffix sort on radix sorts + planes/labels on the GPU)
+produces byte-identical index arrays to the host build (SA-IS + host planes), on the golden cases, on edge cases
+(single symbols, all-N records, long exact repeats that need many doubling rounds) and at config-3 size."""
+import time
+
+import numpy as np
+import pytest
+
+from golden_io import CASES, Case
+from speq_amd import DeviceIndex, FmIndex, synth
+
+pytestmark = pytest.mark.gpu
+
+ARRAYS = [("text", np.uint8), ("sa", np.int32), ("occ", np.uint32), ("occ2", np.uint32), ("runs", np.uint32),
+          ("run_label", np.uint16), ("lab", np.uint32), ("prefix", np.uint32), ("C", np.uint32),
+          ("text_start", np.uint64), ("text_group", np.int32)]
+
+
+def assert_same(records, groups, G, **kw):
+    a = FmIndex.build(records, groups, G, **kw)
+    b = FmIndex.build(records, groups, G, gpu_device=0, **kw)
+    for name, dt in ARRAYS:
+        x, y = a.array(name, dt), b.array(name, dt)
+        assert x.shape == y.shape, name
+        if not np.array_equal(x, y):
+            bad = np.flatnonzero(x != y)
+            raise AssertionError(f"{name}: {bad.size} mismatches, first at {bad[0]}: host {x[bad[0]]} gpu {y[bad[0]]}")
+    ia, ib = a.info(), b.info()
+    assert (ia.n, ia.n_runs, ia.device_bytes) == (ib.n, ib.n_runs, ib.device_bytes)
+    return b
+
+
+@pytest.mark.parametrize("name", CASES)
+def test_gpu_build_golden_cases(name):
+    c = Case(name)
+    for q, pairs, lab in ((4, True, True), (0, False, False), (7, True, False)):
+        assert_same(c.records, c.groups, c.G, prefix_q=q, pair_steps=pairs, label_table=lab)
+
+
+@pytest.mark.parametrize("records", [
+    [b"A"], [b"N"], [b"NNNNNNNNNN"], [b"ACGT"], [b"A" * 5000],               # single symbol / homopolymers
+    [b"ACGT" * 2000, b"ACGT" * 2000],                                       # periodic, identical records
+    [b"AC" * 3000 + b"G", b"AC" * 3000 + b"T", b"TTTT"],
+    [b""] * 3 + [b"ACGTN"],                                                  # empty records
+])
+def test_gpu_build_edge_cases(records):
+    G = len(records)
+    assert_same(records, list(range(G)), G, prefix_q=3, pair_steps=True, label_table=True)
+
+
+def test_gpu_build_long_repeats():
+    rng = np.random.default_rng(5)
+    base = "".join(rng.choice(list("ACGT"), 30_000))
+    recs = [base, base[:20_000] + "A" + base[20_001:], base[::-1], base[5000:] + base[:5000]]
+    recs = [r.encode() for r in recs]
+    assert_same(recs, [0, 1, 1, 2], 3, prefix_q=9, pair_steps=True, label_table=True)
+
+
+def test_gpu_build_scans_like_host():
+    ref = synth.make_reference(6, 2, 20_000, ref_n_rate=0.001)
+    reads = synth.make_reads(ref, 20_000, n_rate=0.001)
+    b = assert_same(ref.records, ref.groups, 6, prefix_q=10, pair_steps=True, label_table=True)
+    dev = DeviceIndex(b)
+    r = dev.scan(reads.seq.tobytes(), reads.qual.tobytes(), reads.offsets, k=21)
+    dev2 = DeviceIndex(FmIndex.build(ref.records, ref.groups, 6, prefix_q=10, pair_steps=True, label_table=True))
+    r2 = dev2.scan(reads.seq.tobytes(), reads.qual.tobytes(), reads.offsets, k=21)
+    assert (r.total, r.ambiguous, r.unique.tolist()) == (r2.total, r2.ambiguous, r2.unique.tolist())
+
+
+def test_gpu_build_config3_size():
+    c = synth.CONFIGS[3]
+    ref = synth.make_reference(c["n_variants"], c["n_isolates"], c["length"])
+    t0 = time.perf_counter()
+    FmIndex.build(ref.records, ref.groups, c["n_variants"], prefix_q=11, pair_steps=True, label_table=True,
+                  gpu_device=0)
+    t_gpu = time.perf_counter() - t0
+    t0 = time.perf_counter()
+    assert_same(ref.records, ref.groups, c["n_variants"], prefix_q=11, pair_steps=True, label_table=True)
+    print(f"config-3 index: gpu build {t_gpu:.2f} s (assert_same incl. host build {time.perf_counter() - t0:.2f} s)")

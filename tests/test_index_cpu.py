@@ -154,3 +154,11 @@ def test_label_table_saturated_runs():
         kmers = np.array([[s % 4 for s in range(j, j + k)] for j in range(16)])
         got = fm.classify(kmers)
         assert set(got.tolist()) <= {0, -1}
+
+
+def test_gpu_build_without_gpu_fails_loudly():
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("a GPU is visible")
+    with pytest.raises(SpeqError, match="no GPU"):
+        FmIndex.build([b"ACGT"], [0], 1, gpu_device=0)
