@@ -110,6 +110,7 @@ SIGNATURES = {
 }
 
 _lib = None
+ABI_VERSION = 2  # include/speq_scan.h SPEQ_ABI_VERSION (struct layouts above)
 
 
 def lib() -> C.CDLL:
@@ -127,6 +128,9 @@ def lib() -> C.CDLL:
             fn = getattr(L, name)
             fn.restype = res
             fn.argtypes = args
+        if L.speq_abi_version() != ABI_VERSION:
+            raise ImportError(f"{LIB_PATH} has ABI {L.speq_abi_version()}, this binding expects {ABI_VERSION}: "
+                              "rebuild with `make`")
         _lib = L
     return _lib
 
