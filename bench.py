@@ -36,10 +36,12 @@ def parse_args():
     p.add_argument("--k", type=int, default=0, help="override k")
     p.add_argument("--prefix-q", type=int, default=11)
     p.add_argument("--pair-steps", type=int, default=1)
-    p.add_argument("--label-table", type=int, default=1)
+    p.add_argument("--label-table", default="auto", help="auto|0|1 (auto: only for >= 4 M-symbol indexes)")
     p.add_argument("--mode", choices=["global", "local"], default="global")
+    p.add_argument("--ilp", type=int, default=0, help="windows per lane (1|2; 0 = the device default)")
     p.add_argument("--cpu-seconds", type=float, default=15.0, help="target CPU-baseline sample duration")
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--no-pcie", action="store_true", help="skip the PCIe-inclusive host-buffer measurement")
     return p.parse_args()
 
 
@@ -67,9 +69,12 @@ def main():
     ref = synth.make_reference(c["n_variants"], c["n_isolates"], c["length"])
     t0 = time.time()
     idx = FmIndex.build(ref.records, ref.groups, G, prefix_q=a.prefix_q, pair_steps=bool(a.pair_steps),
-                        label_table=bool(a.label_table))
+                        label_table="auto" if a.label_table == "auto" else bool(int(a.label_table)))
     build_s = time.time() - t0
     dev = DeviceIndex(idx, local_rank)
+    if a.ilp:
+        dev.tune(ilp=a.ilp)
+    ilp = dev.tuning("ilp")
 
     # this rank's shard of the deterministic read stream (pairs never split)
     reads = synth.make_reads(ref, n_reads, start_index=rank * n_reads, paired=paired)
@@ -129,12 +134,31 @@ def main():
     if os.path.exists(prof):
         try:
             tj = json.load(open(prof))
-            key = f"cfg{a.config}_k{k}_q{a.prefix_q}_pairs{a.pair_steps}_{a.mode}_reads{n_reads}"
+            lab = int(idx.info().label_table)
+            key = f"cfg{a.config}_k{k}_q{a.prefix_q}_pairs{a.pair_steps}_lab{lab}_ilp{ilp}_{a.mode}_reads{n_reads}"
             if key in tj:
                 traffic = tj[key]["hbm_bytes_per_launch"]
                 traffic_src = tj[key]["source"]
         except Exception:
             traffic = None
+
+    # PCIe-inclusive rate (not `value`): the same reads from pageable host memory through the pinned-slot pipeline
+    # (speq_scan_reads: memcpy into pinned slots, H2D on a copy stream overlapped with k_scan).
+    pcie = None
+    if not a.no_pcie:
+        seq_b, qual_b = reads.seq.tobytes(), reads.qual.tobytes()
+        dev.scan(seq_b, qual_b, reads.offsets[:3], k=k, paired=paired, local=local)  # pipeline warm-up
+        best = None
+        for _ in range(3):
+            t0 = time.perf_counter()
+            r = dev.scan(seq_b, qual_b, reads.offsets, k=k, paired=paired, local=local)
+            dt = time.perf_counter() - t0
+            best = dt if best is None else min(best, dt)
+        if r.total != int(counts[0]) and world == 1:
+            raise RuntimeError("host-buffer scan disagrees with the HBM-resident scan")
+        pcie = {"value": kmers_per_step / best, "unit": "k-mers/s", "per_gpu": True,
+                "path": "speq_scan_reads: pageable host arrays -> pinned slots -> H2D (copy stream) || k_scan",
+                "host_GB_per_s": 2 * len(seq_b) / best / 1e9}
 
     cpu = None
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
@@ -157,7 +181,7 @@ def main():
             "config": {
                 "workload": f"BASELINE config {a.config}: {c['n_variants']} variants x {c['n_isolates']} isolates x "
                             f"{c['length']} bp, {n_reads} x 150 bp {'pairs' if paired else 'reads'} per GPU, k={k}",
-                "k": k, "reads_per_gpu": n_reads, "paired": paired, "mode": a.mode, "prefix_q": a.prefix_q, "pair_steps": a.pair_steps, "label_table": a.label_table,
+                "k": k, "reads_per_gpu": n_reads, "paired": paired, "mode": a.mode, "prefix_q": a.prefix_q, "pair_steps": a.pair_steps, "label_table": int(idx.info().label_table), "ilp": ilp,
                 "kmers_per_step_per_gpu": kmers_per_step, "parallelism": f"dp{world} (reads sharded, index replicated)",
                 "index_build_s": round(build_s, 3), "fm_text_len": int(idx.info().n),
             },
@@ -174,6 +198,7 @@ def main():
                         "this kernel; traffic = measured L2->fabric bytes per launch (DESIGN.md 6)",
             },
             "cpu_baseline": cpu,
+            "pcie_inclusive": pcie,
             "check": {"T": int(counts[0]), "ambiguous": int(counts[1]), "U": [int(x) for x in counts[2:]]},
         }
         print(json.dumps(out), flush=True)

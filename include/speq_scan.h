@@ -54,7 +54,8 @@ typedef struct {
     uint32_t prefix_q;   /* length of the q-mer interval lookup table (0 = none, max 13) */
     uint32_t threads;    /* host threads for the build (0 = all) */
     uint32_t pair_steps; /* 1: add the 16 two-symbol occ planes (LF over two bases per gather pair) */
-    uint32_t label_table;/* 1: add the per-SA-position {group, run distance} table (one-load classification) */
+    uint32_t label_table;/* 1: add the per-SA-position {group, run distance} table (one-load classification);
+                            2: auto (only when the collection has >= 4 M symbols) */
     uint32_t gpu_build;  /* 1: build the suffix array and planes on GPU `device` (prefix doubling on radix sorts);
                             0: host SA-IS. Both produce identical indexes. */
     int32_t device;      /* GPU ordinal for gpu_build */
@@ -243,8 +244,10 @@ void speq_groupings_free(speq_groupings* g);
  * "blocks_per_cu": cap resident 256-thread workgroups per CU (0 = no cap; the kernel's LDS is padded);
  *                  default 3 when the index's occ planes exceed one XCD's L2, else 0;
  * "grid_blocks"  : upper bound of the grid (default 8192);
- * "ilp"          : k-mer windows each lane searches concurrently, 1 or 2 (default 1). */
+ * "ilp"          : k-mer windows each lane searches concurrently, 1 or 2 (default 2 when the occ planes fit in
+ *                  8 MiB, else 1). */
 int speq_device_set_tuning(speq_device_index* d, const char* key, int64_t value);
+int speq_device_get_tuning(const speq_device_index* d, const char* key, int64_t* value);
 
 /* ---- kernel timing (HIP events on the launch stream; bench/roofline support) ----
  * Returns the summed elapsed milliseconds of the scan kernels launched by speq_scan_reads_device on

@@ -105,6 +105,7 @@ SIGNATURES = {
     "speq_groupings_errors": (C.c_char_p, [_P]),
     "speq_groupings_free": (None, [_P]),
     "speq_device_set_tuning": (C.c_int, [_P, C.c_char_p, C.c_int64]),
+    "speq_device_get_tuning": (C.c_int, [_P, C.c_char_p, C.POINTER(C.c_int64)]),
     "speq_timing_enable": (C.c_int, [_P, C.c_int]),
     "speq_timing_read": (C.c_int, [_P, _F64P, _U64P]),
 }

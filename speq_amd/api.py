@@ -89,12 +89,14 @@ class FmIndex:
     @classmethod
     def build(cls, records: Sequence[bytes | str], group_of_record: Sequence[int], n_groups: int,
               prefix_q: int = 0, threads: int = 0, pair_steps: bool = False,
-              label_table: bool = False, gpu_device: Optional[int] = None) -> "FmIndex":
-        """gpu_device: build the suffix array and planes on that GPU (None = host SA-IS); identical results."""
+              label_table: bool | str = False, gpu_device: Optional[int] = None) -> "FmIndex":
+        """label_table: True/False or "auto" (only for collections of >= 4 M symbols).
+        gpu_device: build the suffix array and planes on that GPU (None = host SA-IS); identical results."""
         seq, off = pack_records(records)
         grp = np.asarray(group_of_record, dtype=np.int32)
         h = C.c_void_p()
-        opts = BuildOpts(prefix_q, threads, int(pair_steps), int(label_table), int(gpu_device is not None),
+        opts = BuildOpts(prefix_q, threads, int(pair_steps), 2 if label_table == "auto" else int(bool(label_table)),
+                         int(gpu_device is not None),
                          gpu_device if gpu_device is not None else 0)
         check(lib().speq_index_build(seq, _u64p(off), len(records), grp.ctypes.data_as(C.POINTER(C.c_int32)),
                                      len(grp), n_groups, C.byref(opts), C.byref(h)))
@@ -213,6 +215,11 @@ class DeviceIndex:
         """Launch tuning (blocks_per_cu=..., grid_blocks=...); never changes results."""
         for k, v in kw.items():
             check(lib().speq_device_set_tuning(self._h, k.encode(), int(v)))
+
+    def tuning(self, key: str) -> int:
+        v = C.c_int64()
+        check(lib().speq_device_get_tuning(self._h, key.encode(), C.byref(v)))
+        return v.value
 
     def timing(self, on: bool) -> None:
         check(lib().speq_timing_enable(self._h, int(on)))

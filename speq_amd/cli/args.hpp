@@ -30,7 +30,7 @@ struct CmdArguments {  // include/arg_parse.h:10-28
     unsigned int prefix_q{11};   // --prefix-q: q-mer interval table of the FM-index
     bool pair_steps{true};       // --pair-steps: two-symbol occ planes
     int gpu_build{-1};           // --gpu-build: -1 auto (GPU when one is visible), 0 host SA-IS, 1 GPU
-    bool label_table{true};      // --label-table: per-position {group, run distance} table
+    unsigned label_table{2};     // --label-table: per-position {group, run distance} table (2 = auto)
     int device{-1};              // --device: GPU ordinal (default: $LOCAL_RANK or 0)
     unsigned int max_em_iterations{1000};
 };

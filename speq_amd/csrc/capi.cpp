@@ -35,10 +35,18 @@ int speq_index_build(const char* seq, const uint64_t* rec_offsets, uint32_t n_re
             if (opts->device < 0 || opts->device >= ndev) throw std::invalid_argument("speq_index_build: bad device ordinal");
             gpu = opts->device;
         }
+        // label_table 2 = auto: the table pays off once the index outgrows L2 (n >= 4 M symbols; cfg 3 +3 %,
+        // cfg 2 -4 %: profiles/r01/ab_occupancy.txt)
+        bool lab = opts && opts->label_table == 1;
+        if (opts && opts->label_table == 2) {
+            uint64_t n = 1;
+            for (uint32_t r = 0; r < n_records; ++r) n += 2 * (rec_offsets[r + 1] - rec_offsets[r] + 1);
+            lab = n >= (4ull << 20);
+        }
         auto idx = std::make_unique<speq_index>();
         speq::fm_build(idx->fm, seq, rec_offsets, n_records, group_of_rec, n_group_entries, n_groups,
                        opts ? opts->prefix_q : 0, opts ? opts->threads : 0, opts ? opts->pair_steps != 0 : false,
-                       opts ? opts->label_table != 0 : false, gpu);
+                       lab, gpu);
         *out = idx.release();
     });
 }

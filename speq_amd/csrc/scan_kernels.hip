@@ -305,8 +305,13 @@ __device__ __forceinline__ void search_packed_n(const DevView& I, const Rsrc& R,
     }
 }
 
-template <int MODE, bool PAIRED, bool LDS_HIST, int NWIN>
-__global__ __launch_bounds__(BLOCK_THREADS) void k_scan(DevView I, UnitSrc src, unsigned long long* __restrict__ out_a,
+#ifndef SPEQ_MIN_WAVES  // A/B knob: minimum waves per SIMD the register allocator must allow
+#define SPEQ_MIN_WAVES 1
+#endif
+
+// EM: also record the SA interval of every passing multi-group window (EM histogram scans only).
+template <int MODE, bool PAIRED, bool LDS_HIST, int NWIN, bool EM>
+__global__ __launch_bounds__(BLOCK_THREADS, SPEQ_MIN_WAVES) void k_scan(DevView I, UnitSrc src, unsigned long long* __restrict__ out_a,
                                                         unsigned long long* __restrict__ out_b,
                                                         double* __restrict__ out_w) {
     // out_a: reads -> counts[G+2] (T, ambiguous, U[g]); ref -> U_ref[G]
@@ -510,7 +515,7 @@ __global__ __launch_bounds__(BLOCK_THREADS) void k_scan(DevView I, UnitSrc src, 
                 }
             } else if (valid[w]) {
                 ++t_cnt;
-                if (src.em_mult != nullptr && which[w] == -2) {
+                if (EM && which[w] == -2) {
                     // EM histogram: distinct k-mers have disjoint SA intervals, so lo
                     // identifies the interval; hi is the same for every window that hits it.
                     atomicAdd(&src.em_mult[ilo[w]], 1u);
@@ -664,10 +669,13 @@ struct DeviceGuard {
 
 template <int MODE, bool PAIRED, bool LDS>
 void allow_big_lds() {
-    HIP_OK(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_scan<MODE, PAIRED, LDS, 1>),
+    HIP_OK(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_scan<MODE, PAIRED, LDS, 1, false>),
                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-    HIP_OK(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_scan<MODE, PAIRED, LDS, 2>),
+    HIP_OK(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_scan<MODE, PAIRED, LDS, 2, false>),
                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    if (MODE != KM_REF)
+        HIP_OK(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_scan<MODE, PAIRED, LDS, 1, MODE != KM_REF>),
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
 }
 
 void allow_big_lds_all() {
@@ -686,10 +694,15 @@ void allow_big_lds_all() {
 template <int MODE, bool PAIRED, bool LDS>
 void launch_t(const speq_device_index* d, const UnitSrc& src, uint32_t grid, size_t lds, hipStream_t st,
               unsigned long long* a, unsigned long long* b, double* w) {
-    if (d->ilp == 2)
-        hipLaunchKernelGGL((k_scan<MODE, PAIRED, LDS, 2>), dim3(grid), dim3(BLOCK_THREADS), lds, st, d->view, src, a, b, w);
+    if (MODE != KM_REF && src.em_mult != nullptr)
+        hipLaunchKernelGGL((k_scan<MODE, PAIRED, LDS, 1, MODE != KM_REF>), dim3(grid), dim3(BLOCK_THREADS), lds, st,
+                           d->view, src, a, b, w);
+    else if (d->ilp == 2)
+        hipLaunchKernelGGL((k_scan<MODE, PAIRED, LDS, 2, false>), dim3(grid), dim3(BLOCK_THREADS), lds, st, d->view,
+                           src, a, b, w);
     else
-        hipLaunchKernelGGL((k_scan<MODE, PAIRED, LDS, 1>), dim3(grid), dim3(BLOCK_THREADS), lds, st, d->view, src, a, b, w);
+        hipLaunchKernelGGL((k_scan<MODE, PAIRED, LDS, 1, false>), dim3(grid), dim3(BLOCK_THREADS), lds, st, d->view,
+                           src, a, b, w);
 }
 
 void launch_scan(const speq_device_index* d, int mode, bool paired, const UnitSrc& src, uint64_t work_units,
@@ -818,6 +831,10 @@ int speq_device_open(const speq_index* idx, int device, speq_device_index** out)
         const uint64_t acgt_bytes = 4ull * fm.n_blocks() * sizeof(speq::OccEntry);
         d->blocks_per_cu = (fm.occ2.empty() && acgt_bytes > (4ull << 20)) ? 3u : 0u;
         d->grid_blocks = 8192;
+        // Two windows per lane pay off while every plane stays L2-resident (cfg 2: +3 %); on larger indexes the
+        // extra gathers in flight thrash L2 (cfg 3: -15 %). profiles/r01/ab_occupancy.txt
+        const uint64_t plane_bytes = (fm.occ.size() + fm.occ2.size()) * sizeof(speq::OccEntry);
+        d->ilp = plane_bytes <= (8ull << 20) ? 2u : 1u;
         allow_big_lds_all();
         *out = d.release();
     });
@@ -982,6 +999,17 @@ int speq_device_set_tuning(speq_device_index* d, const char* key, int64_t value)
         } else {
             throw std::invalid_argument("speq_device_set_tuning: unknown key " + k);
         }
+    });
+}
+
+int speq_device_get_tuning(const speq_device_index* d, const char* key, int64_t* value) {
+    return speq::guarded([&] {
+        if (!d || !key || !value) throw std::invalid_argument("speq_device_get_tuning: null argument");
+        const std::string k(key);
+        if (k == "blocks_per_cu") *value = d->blocks_per_cu;
+        else if (k == "ilp") *value = d->ilp;
+        else if (k == "grid_blocks") *value = d->grid_blocks;
+        else throw std::invalid_argument("speq_device_get_tuning: unknown key " + k);
     });
 }
 
