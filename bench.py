@@ -39,6 +39,7 @@ def parse_args():
     p.add_argument("--label-table", default="auto", help="auto|0|1 (auto: only for >= 4 M-symbol indexes)")
     p.add_argument("--mode", choices=["global", "local"], default="global")
     p.add_argument("--ilp", type=int, default=0, help="windows per lane (1|2; 0 = the device default)")
+    p.add_argument("--gpu-build", type=int, default=1, help="build the index on the GPU (1) or host SA-IS (0)")
     p.add_argument("--cpu-seconds", type=float, default=15.0, help="target CPU-baseline sample duration")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-pcie", action="store_true", help="skip the PCIe-inclusive host-buffer measurement")
@@ -69,7 +70,8 @@ def main():
     ref = synth.make_reference(c["n_variants"], c["n_isolates"], c["length"])
     t0 = time.time()
     idx = FmIndex.build(ref.records, ref.groups, G, prefix_q=a.prefix_q, pair_steps=bool(a.pair_steps),
-                        label_table="auto" if a.label_table == "auto" else bool(int(a.label_table)))
+                        label_table="auto" if a.label_table == "auto" else bool(int(a.label_table)),
+                        threads=16, gpu_device=local_rank if a.gpu_build else None)
     build_s = time.time() - t0
     dev = DeviceIndex(idx, local_rank)
     if a.ilp:
@@ -183,7 +185,7 @@ def main():
                             f"{c['length']} bp, {n_reads} x 150 bp {'pairs' if paired else 'reads'} per GPU, k={k}",
                 "k": k, "reads_per_gpu": n_reads, "paired": paired, "mode": a.mode, "prefix_q": a.prefix_q, "pair_steps": a.pair_steps, "label_table": int(idx.info().label_table), "ilp": ilp,
                 "kmers_per_step_per_gpu": kmers_per_step, "parallelism": f"dp{world} (reads sharded, index replicated)",
-                "index_build_s": round(build_s, 3), "fm_text_len": int(idx.info().n),
+                "index_build_s": round(build_s, 3), "index_builder": "gpu" if a.gpu_build else "host", "fm_text_len": int(idx.info().n),
             },
             "roofline": {
                 "bound": "hbm", "achieved": achieved_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",

@@ -2,9 +2,14 @@
 #include "em.hpp"
 
 #include <algorithm>
+#include <atomic>
 #include <cmath>
 #include <limits>
 #include <thread>
+
+namespace {
+constexpr uint64_t EM_CHUNKS = 64;  // fixed row partition of speq_em_step (deterministic across machines)
+}  // namespace
 
 namespace speq {
 
@@ -102,21 +107,45 @@ int speq_em_step(const speq_em* em, const double* percent, const int32_t* group_
                 const double a = percent[g] / (double)group_counts[g];
                 if (a > 0.0) next[g] += (double)unique[g];
             }
-            std::vector<double> a;
-            for (uint64_t r = 0; r < R; ++r) {
-                const uint64_t b = em->row_ptr[r], e = em->row_ptr[r + 1];
-                a.resize(e - b);
-                double norm = 0.0;
-                for (uint64_t x = b; x < e; ++x) {
-                    const uint32_t g = em->col_group[x];
-                    a[x - b] = (double)em->col_count[x] * percent[g] / (double)group_counts[g];
-                    norm += a[x - b];
+            // Rows are split into a FIXED number of contiguous chunks (independent of the machine's thread count),
+            // each summed into its own vector, and the chunk vectors are added in chunk order: the result is
+            // deterministic, and differs from a serial sweep only by fp64 re-association (tests: rtol 1e-9).
+            const uint64_t n_chunks = std::min<uint64_t>(EM_CHUNKS, std::max<uint64_t>(1, R / 4096));
+            std::vector<double> part(n_chunks * G, 0.0);
+            auto run_chunk = [&](uint64_t ci) {
+                const uint64_t r0 = R * ci / n_chunks, r1 = R * (ci + 1) / n_chunks;
+                double* acc = part.data() + ci * G;
+                std::vector<double> a;
+                for (uint64_t r = r0; r < r1; ++r) {
+                    const uint64_t b = em->row_ptr[r], e = em->row_ptr[r + 1];
+                    a.resize(e - b);
+                    double norm = 0.0;
+                    for (uint64_t x = b; x < e; ++x) {
+                        const uint32_t g = em->col_group[x];
+                        a[x - b] = (double)em->col_count[x] * percent[g] / (double)group_counts[g];
+                        norm += a[x - b];
+                    }
+                    if (norm > 0.0) {
+                        const double m = (double)em->row_mult[r];
+                        for (uint64_t x = b; x < e; ++x) acc[em->col_group[x]] += m * (a[x - b] / norm);
+                    }
                 }
-                if (norm > 0.0) {
-                    const double m = (double)em->row_mult[r];
-                    for (uint64_t x = b; x < e; ++x) next[em->col_group[x]] += m * (a[x - b] / norm);
-                }
+            };
+            const uint32_t hw = std::max(1u, std::thread::hardware_concurrency());
+            const uint32_t n_threads = (uint32_t)std::min<uint64_t>(std::min<uint32_t>(hw, 16u), n_chunks);
+            if (n_threads <= 1) {
+                for (uint64_t ci = 0; ci < n_chunks; ++ci) run_chunk(ci);
+            } else {
+                std::atomic<uint64_t> next_chunk{0};
+                std::vector<std::thread> pool;
+                for (uint32_t t = 0; t < n_threads; ++t)
+                    pool.emplace_back([&] {
+                        for (uint64_t ci; (ci = next_chunk++) < n_chunks;) run_chunk(ci);
+                    });
+                for (auto& t : pool) t.join();
             }
+            for (uint64_t ci = 0; ci < n_chunks; ++ci)
+                for (uint32_t g = 0; g < G; ++g) next[g] += part[ci * G + g];
         } else {
             // IEEE edge cases (a group count of 0, non-finite percentages): evaluate every group of every row
             // exactly as the reference does, zero terms included.
