@@ -34,12 +34,13 @@ def parse_args():
     p.add_argument("--config", type=int, default=2, help="BASELINE.json config number (1-5)")
     p.add_argument("--reads", type=int, default=0, help="override reads per GPU")
     p.add_argument("--k", type=int, default=0, help="override k")
-    p.add_argument("--prefix-q", type=int, default=11)
+    p.add_argument("--prefix-q", type=int, default=12)
     p.add_argument("--pair-steps", type=int, default=1)
     p.add_argument("--label-table", default="auto", help="auto|0|1 (auto: only for >= 4 M-symbol indexes)")
     p.add_argument("--mode", choices=["global", "local"], default="global")
     p.add_argument("--ilp", type=int, default=0, help="windows per lane (1|2; 0 = the device default)")
     p.add_argument("--gpu-build", type=int, default=1, help="build the index on the GPU (1) or host SA-IS (0)")
+    p.add_argument("--triple-steps", type=int, default=1, help="three-symbol occ planes (1) or not (0)")
     p.add_argument("--cpu-seconds", type=float, default=15.0, help="target CPU-baseline sample duration")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-pcie", action="store_true", help="skip the PCIe-inclusive host-buffer measurement")
@@ -71,12 +72,18 @@ def main():
     t0 = time.time()
     idx = FmIndex.build(ref.records, ref.groups, G, prefix_q=a.prefix_q, pair_steps=bool(a.pair_steps),
                         label_table="auto" if a.label_table == "auto" else bool(int(a.label_table)),
-                        threads=16, gpu_device=local_rank if a.gpu_build else None)
+                        threads=16, gpu_device=local_rank if a.gpu_build else None,
+                        triple_steps=bool(a.triple_steps))
     build_s = time.time() - t0
     dev = DeviceIndex(idx, local_rank)
     if a.ilp:
         dev.tune(ilp=a.ilp)
     ilp = dev.tuning("ilp")
+    # the q-mer table level the scan uses (view_for_k in scan_kernels.hip)
+    width = 3 if a.triple_steps else (2 if a.pair_steps else 1)
+    q_used = next((a.prefix_q - lv for lv in range(3)
+                   if a.prefix_q - lv >= 1 and a.prefix_q - lv <= k and (k - a.prefix_q + lv) % width == 0),
+                  a.prefix_q)
 
     # this rank's shard of the deterministic read stream (pairs never split)
     reads = synth.make_reads(ref, n_reads, start_index=rank * n_reads, paired=paired)
@@ -137,7 +144,9 @@ def main():
         try:
             tj = json.load(open(prof))
             lab = int(idx.info().label_table)
-            key = f"cfg{a.config}_k{k}_q{a.prefix_q}_pairs{a.pair_steps}_lab{lab}_ilp{ilp}_{a.mode}_reads{n_reads}"
+            steps = "_tri1" if a.triple_steps else ""
+            key = (f"cfg{a.config}_k{k}_q{a.prefix_q}_pairs{a.pair_steps}{steps}_lab{lab}_ilp{ilp}_{a.mode}"
+                   f"_reads{n_reads}")
             if key in tj:
                 traffic = tj[key]["hbm_bytes_per_launch"]
                 traffic_src = tj[key]["source"]
@@ -183,7 +192,7 @@ def main():
             "config": {
                 "workload": f"BASELINE config {a.config}: {c['n_variants']} variants x {c['n_isolates']} isolates x "
                             f"{c['length']} bp, {n_reads} x 150 bp {'pairs' if paired else 'reads'} per GPU, k={k}",
-                "k": k, "reads_per_gpu": n_reads, "paired": paired, "mode": a.mode, "prefix_q": a.prefix_q, "pair_steps": a.pair_steps, "label_table": int(idx.info().label_table), "ilp": ilp,
+                "k": k, "reads_per_gpu": n_reads, "paired": paired, "mode": a.mode, "prefix_q": a.prefix_q, "prefix_q_used": q_used, "pair_steps": a.pair_steps, "triple_steps": a.triple_steps, "label_table": int(idx.info().label_table), "ilp": ilp,
                 "kmers_per_step_per_gpu": kmers_per_step, "parallelism": f"dp{world} (reads sharded, index replicated)",
                 "index_build_s": round(build_s, 3), "index_builder": "gpu" if a.gpu_build else "host", "fm_text_len": int(idx.info().n),
             },

@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define SPEQ_ABI_VERSION 2
+#define SPEQ_ABI_VERSION 3
 
 enum {
     SPEQ_OK = 0,
@@ -59,6 +59,8 @@ typedef struct {
     uint32_t gpu_build;  /* 1: build the suffix array and planes on GPU `device` (prefix doubling on radix sorts);
                             0: host SA-IS. Both produce identical indexes. */
     int32_t device;      /* GPU ordinal for gpu_build */
+    uint32_t triple_steps; /* 1: also add the 64 three-symbol occ planes (LF over three bases per gather pair;
+                              10.7 bytes per text symbol); requires pair_steps */
 } speq_build_opts;
 
 /* Per-scan parameters (reference: cmd_arguments in include/arg_parse.h:10-28). */
@@ -112,11 +114,12 @@ typedef struct {
     uint32_t label_table;  /* 1 when the per-position label table is present */
     uint64_t n_runs;       /* runs of equal group label along the suffix array */
     uint64_t device_bytes; /* bytes a device replica occupies in HBM */
+    uint32_t triple_steps; /* 1 when the three-symbol occ planes are present */
 } speq_index_info;
 int speq_index_get_info(const speq_index* idx, speq_index_info* info);
 
 /* Read-only views of the host arrays (for tests and tools; layout documented in DESIGN.md §3).
- * name: "text", "sa", "occ", "occ2", "runs", "run_label", "lab", "prefix", "C", "text_start", "text_group". */
+ * name: "text", "sa", "occ", "occ2", "occ3", "runs", "run_label", "lab", "prefix", "C", "text_start", "text_group". */
 int speq_index_array(const speq_index* idx, const char* name, const void** ptr, uint64_t* bytes);
 
 /* ---- device replica ---- */
@@ -244,8 +247,10 @@ void speq_groupings_free(speq_groupings* g);
  * "blocks_per_cu": cap resident 256-thread workgroups per CU (0 = no cap; the kernel's LDS is padded);
  *                  default 3 when the index's occ planes exceed one XCD's L2, else 0;
  * "grid_blocks"  : upper bound of the grid (default 8192);
- * "ilp"          : k-mer windows each lane searches concurrently, 1 or 2 (default 2 when the occ planes fit in
- *                  8 MiB, else 1). */
+ * "ilp"          : k-mer windows each lane searches concurrently, 1 or 2 (default 2 for indexes of < 4 M
+ *                  symbols, else 1);
+ * "prefix_level" : q-mer table used by scans: -1 (default) picks, per k, the longest of q, q-1, q-2 that leaves a
+ *                  multiple of the widest LF step; 0..2 forces table q - level (results never change). */
 int speq_device_set_tuning(speq_device_index* d, const char* key, int64_t value);
 int speq_device_get_tuning(const speq_device_index* d, const char* key, int64_t* value);
 

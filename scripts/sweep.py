@@ -29,7 +29,7 @@ def main():
     ap.add_argument("--ref-pass", action="store_true")
     ap.add_argument("--bpc", default="0", help="blocks-per-CU caps to sweep (0 = none)")
     ap.add_argument("--grids", default="8192", help="grid caps to sweep")
-    ap.add_argument("--pairs", default="0,1", help="pair_steps values to sweep")
+    ap.add_argument("--pairs", default="0,1", help="multi-symbol steps to sweep: 0 single, 1 pairs, 2 pairs + triples")
     ap.add_argument("--labs", default="1", help="label_table values to sweep")
     ap.add_argument("--ilps", default="1", help="windows per lane to sweep (1, 2)")
     a = ap.parse_args()
@@ -55,8 +55,8 @@ def main():
             for pr in [int(x) for x in a.pairs.split(",")]:
                 for lb in [int(x) for x in a.labs.split(",")]:
                     t0 = time.time()
-                    idx = FmIndex.build(ref.records, ref.groups, G, prefix_q=q, pair_steps=bool(pr),
-                                        label_table=bool(lb))
+                    idx = FmIndex.build(ref.records, ref.groups, G, prefix_q=q, pair_steps=pr >= 1,
+                                        label_table=bool(lb), triple_steps=pr == 2, gpu_device=0)
                     info = idx.info()
                     devs[(q, pr, lb)] = (DeviceIndex(idx), time.time() - t0, info)
         times = {(q, m, b, g, il): [] for q in devs for m in a.modes.split(",")

@@ -27,7 +27,8 @@ SPEQ_MODE_GLOBAL, SPEQ_MODE_LOCAL = 0, 1
 
 class BuildOpts(C.Structure):
     _fields_ = [("prefix_q", C.c_uint32), ("threads", C.c_uint32), ("pair_steps", C.c_uint32),
-                ("label_table", C.c_uint32), ("gpu_build", C.c_uint32), ("device", C.c_int32)]
+                ("label_table", C.c_uint32), ("gpu_build", C.c_uint32), ("device", C.c_int32),
+                ("triple_steps", C.c_uint32)]
 
 
 class ScanParams(C.Structure):
@@ -38,7 +39,7 @@ class IndexInfo(C.Structure):
     _fields_ = [("n", C.c_uint64), ("n_texts", C.c_uint32), ("n_records", C.c_uint32), ("n_groups", C.c_uint32),
                 ("prefix_q", C.c_uint32), ("pair_steps", C.c_uint32), ("label_table", C.c_uint32),
                 ("n_runs", C.c_uint64),
-                ("device_bytes", C.c_uint64)]
+                ("device_bytes", C.c_uint64), ("triple_steps", C.c_uint32)]
 
 
 # name -> (restype, argtypes); every symbol declared in include/speq_scan.h
@@ -111,7 +112,7 @@ SIGNATURES = {
 }
 
 _lib = None
-ABI_VERSION = 2  # include/speq_scan.h SPEQ_ABI_VERSION (struct layouts above)
+ABI_VERSION = 3  # include/speq_scan.h SPEQ_ABI_VERSION (struct layouts above)
 
 
 def lib() -> C.CDLL:

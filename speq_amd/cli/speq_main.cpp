@@ -44,11 +44,12 @@ const char* HELP =
     "      --precision-cutoff X  EM convergence threshold (default 1e-6)\n"
     "      --phred-cutoff N      a window passes iff min(Q) > N (default 30)\n"
     "      --fixed-accuracy X    fixed per-base accuracy in [0,1]; 0 = Phred-weighted (default)\n"
-    "      --prefix-q N          q-mer lookup table of the FM-index (default 11, 0 = off)\n"
+    "      --prefix-q N          q-mer lookup tables of the FM-index, lengths N, N-1, N-2 (default 12, 0 = off)\n"
     "      --pair-steps 0|1      two-base LF planes in the FM-index (default 1)\n"
     "      --label-table auto|0|1 per-position group/run table: one-load classification (default auto:\n"
     "                            when the collection has >= 4 M symbols)\n"
     "      --gpu-build auto|0|1  build the suffix array on the GPU (default auto: when one is visible)\n"
+    "      --triple-steps 0|1    three-base LF planes in the FM-index (10.7 B per symbol; default 1)\n"
     "      --device N            GPU ordinal (default $LOCAL_RANK or 0)\n";
 
 template <typename T>
@@ -120,6 +121,7 @@ CmdArguments parse(int argc, char** argv) {
             const std::string v = value();
             a.label_table = v == "auto" ? 2u : (to_number<unsigned>(opt, v) != 0 ? 1u : 0u);
         }
+        else if (allow_refs && opt == "--triple-steps") a.triple_steps = to_number<unsigned>(opt, value()) != 0;
         else if (allow_refs && opt == "--gpu-build") {
             const std::string v = value();
             if (v == "auto") a.gpu_build = -1;
@@ -282,7 +284,8 @@ void generate_fm_index(const CmdArguments& a, const fs::path& idx_path, const In
         bdev = lr ? std::atoi(lr) : 0;
     }
     const bool gpu = a.gpu_build == 1 || (a.gpu_build < 0 && speq_device_count() > 0);
-    speq_build_opts opts{a.prefix_q, a.threads, a.pair_steps ? 1u : 0u, a.label_table, gpu ? 1u : 0u, bdev};
+    speq_build_opts opts{a.prefix_q, a.threads, a.pair_steps ? 1u : 0u, a.label_table, gpu ? 1u : 0u, bdev,
+                         (a.triple_steps && a.pair_steps) ? 1u : 0u};
     speq_index* idx = nullptr;
     ok(speq_index_build(refs.seq.data(), refs.offsets.data(), (uint32_t)refs.size(), h.scaffolds.data(),
                         (uint32_t)h.scaffolds.size(), (uint32_t)h.names.size(), &opts, &idx),

@@ -101,12 +101,22 @@ __global__ void k_compact(const uint32_t* __restrict__ keep, const uint32_t* __r
 // BWT symbol, the symbol before it (0xFF when absent) and the group label of every SA position.
 __global__ void k_bwt(const uint8_t* __restrict__ T, const uint32_t* __restrict__ sa, uint32_t n,
                       const uint64_t* __restrict__ text_start, uint32_t n_texts, const int32_t* __restrict__ text_group,
-                      uint8_t* __restrict__ bwt, uint8_t* __restrict__ bwt2, uint16_t* __restrict__ label) {
+                      uint8_t* __restrict__ bwt, uint8_t* __restrict__ bwt2, uint8_t* __restrict__ code3,
+                      uint16_t* __restrict__ label) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const uint32_t s = sa[i];
     bwt[i] = s == 0 ? (uint8_t)SYM_TERM : T[s - 1];
     bwt2[i] = s >= 2 ? T[s - 2] : (uint8_t)0xFF;
+    if (code3) {  // 16a + 4b + c for the three symbols before the suffix, 0xFF unless all are in A..T
+        uint8_t c = 0xFF;
+        if (s >= 3) {
+            const uint32_t x = T[s - 3], y = T[s - 2], z = T[s - 1];
+            if (x - SYM_A < 4u && y - SYM_A < 4u && z - SYM_A < 4u)
+                c = (uint8_t)((x - SYM_A) * 16u + (y - SYM_A) * 4u + (z - SYM_A));
+        }
+        code3[i] = c;
+    }
     // largest t with text_start[t] <= s, clamped to the last text (the terminator)
     uint32_t lo = 0, hi = n_texts + 1;
     while (hi - lo > 1) {
@@ -118,7 +128,7 @@ __global__ void k_bwt(const uint8_t* __restrict__ T, const uint32_t* __restrict_
     label[i] = (uint16_t)text_group[lo];
 }
 
-enum PlaneKind { PK_OCC = 0, PK_OCC2 = 1, PK_RUNS = 2 };
+enum PlaneKind { PK_OCC = 0, PK_OCC2 = 1, PK_RUNS = 2, PK_OCC3 = 3 };
 
 // One thread per (plane, 96-position block): bitmap + popcount.
 template <int KIND>
@@ -137,6 +147,8 @@ __global__ void k_planes(const uint8_t* __restrict__ bwt, const uint8_t* __restr
             on = bwt[i] == SYM_A + plane;
         } else if (KIND == PK_OCC2) {
             on = bwt2[i] == SYM_A + plane / 4 && bwt[i] == SYM_A + plane % 4;
+        } else if (KIND == PK_OCC3) {
+            on = bwt2[i] == plane;  // bwt2 carries code3 for this kind
         } else {
             on = i > 0 && label[i] != label[i - 1];
         }
@@ -226,7 +238,8 @@ uint32_t bits_for(uint64_t v) {
 
 // Fills idx.sa, occ, occ2 (pair_steps), runs, run_label and lab (label_table) from idx.text, idx.C, text_start and
 // text_group, on `device`. The caller has built the text and C and builds the prefix table afterwards.
-void fm_build_arrays_gpu(FmIndex& idx, int device, bool pair_steps, bool label_table, bool timing) {
+void fm_build_arrays_gpu(FmIndex& idx, int device, bool pair_steps, bool triple_steps, bool label_table,
+                         bool timing) {
     auto t_last = std::chrono::steady_clock::now();
     auto phase = [&](const char* what) {
         if (!timing) return;
@@ -317,9 +330,10 @@ void fm_build_arrays_gpu(FmIndex& idx, int device, bool pair_steps, bool label_t
     DevBuf<int32_t> d_tg(idx.text_group.size());
     BHIP(hipMemcpy(d_ts.p, idx.text_start.data(), idx.text_start.size() * 8, hipMemcpyHostToDevice));
     BHIP(hipMemcpy(d_tg.p, idx.text_group.data(), idx.text_group.size() * 4, hipMemcpyHostToDevice));
-    DevBuf<uint8_t> d_bwt(n), d_bwt2(n);
+    DevBuf<uint8_t> d_bwt(n), d_bwt2(n), d_code3(triple_steps ? n : 1);
     DevBuf<uint16_t> d_label(n);
-    k_bwt<<<grid(n), 256, 0, st>>>(d_text.p, d_sa.p, n, d_ts.p, idx.n_texts, d_tg.p, d_bwt.p, d_bwt2.p, d_label.p);
+    k_bwt<<<grid(n), 256, 0, st>>>(d_text.p, d_sa.p, n, d_ts.p, idx.n_texts, d_tg.p, d_bwt.p, d_bwt2.p,
+                                   triple_steps ? d_code3.p : nullptr, d_label.p);
     BHIP(hipGetLastError());
 
     // planes: bitmaps + popcounts, one exclusive scan per plane, counts = scan + base (C[s] / C2[ab] / 0)
@@ -333,6 +347,8 @@ void fm_build_arrays_gpu(FmIndex& idx, int device, bool pair_steps, bool label_t
             k_planes<PK_OCC><<<g, 256, 0, st>>>(d_bwt.p, d_bwt2.p, d_label.p, n, nb, n_planes, d_pl.p, d_pop.p);
         else if (kind == PK_OCC2)
             k_planes<PK_OCC2><<<g, 256, 0, st>>>(d_bwt.p, d_bwt2.p, d_label.p, n, nb, n_planes, d_pl.p, d_pop.p);
+        else if (kind == PK_OCC3)
+            k_planes<PK_OCC3><<<g, 256, 0, st>>>(d_bwt.p, d_code3.p, d_label.p, n, nb, n_planes, d_pl.p, d_pop.p);
         else
             k_planes<PK_RUNS><<<g, 256, 0, st>>>(d_bwt.p, d_bwt2.p, d_label.p, n, nb, n_planes, d_pl.p, d_pop.p);
         BHIP(hipGetLastError());
@@ -373,6 +389,14 @@ void fm_build_arrays_gpu(FmIndex& idx, int device, bool pair_steps, bool label_t
         idx.occ2.clear();
     }
     phase("occ2");
+    if (triple_steps) {
+        std::vector<uint32_t> base(64);
+        triple_bases(idx, base.data());
+        build_planes(PK_OCC3, 64, base, idx.occ3);
+    } else {
+        idx.occ3.clear();
+    }
+    phase("occ3");
     build_planes(PK_RUNS, 1, std::vector<uint32_t>(1, 0u), idx.runs);
     {
         DevBuf<uint32_t> flag(n), run_id(n);

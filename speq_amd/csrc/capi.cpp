@@ -46,7 +46,7 @@ int speq_index_build(const char* seq, const uint64_t* rec_offsets, uint32_t n_re
         auto idx = std::make_unique<speq_index>();
         speq::fm_build(idx->fm, seq, rec_offsets, n_records, group_of_rec, n_group_entries, n_groups,
                        opts ? opts->prefix_q : 0, opts ? opts->threads : 0, opts ? opts->pair_steps != 0 : false,
-                       lab, gpu);
+                       lab, gpu, opts && opts->triple_steps != 0);
         *out = idx.release();
     });
 }
@@ -101,6 +101,7 @@ int speq_index_get_info(const speq_index* idx, speq_index_info* info) {
         info->prefix_q = f.prefix_q;
         info->pair_steps = f.occ2.empty() ? 0u : 1u;
         info->label_table = f.lab.empty() ? 0u : 1u;
+        info->triple_steps = f.occ3.empty() ? 0u : 1u;
         info->n_runs = f.run_label.size();
         info->device_bytes = f.device_bytes();
     });
@@ -116,6 +117,7 @@ int speq_index_array(const speq_index* idx, const char* name, const void** ptr, 
         else if (n == "sa") set(f.sa.data(), f.sa.size() * 4);
         else if (n == "occ") set(f.occ.data(), f.occ.size() * sizeof(speq::OccEntry));
         else if (n == "occ2") set(f.occ2.data(), f.occ2.size() * sizeof(speq::OccEntry));
+        else if (n == "occ3") set(f.occ3.data(), f.occ3.size() * sizeof(speq::OccEntry));
         else if (n == "lab") set(f.lab.data(), f.lab.size() * 4);
         else if (n == "runs") set(f.runs.data(), f.runs.size() * sizeof(speq::OccEntry));
         else if (n == "run_label") set(f.run_label.data(), f.run_label.size() * 2);

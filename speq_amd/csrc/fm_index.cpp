@@ -77,8 +77,9 @@ void fill_bitvector(OccEntry* entries, size_t stride, uint64_t n, uint64_t n_blo
 }  // namespace
 
 uint64_t FmIndex::device_bytes() const {
-    return occ.size() * sizeof(OccEntry) + occ2.size() * sizeof(OccEntry) + runs.size() * sizeof(OccEntry) +
-           run_label.size() * 2 + lab.size() * 4 + prefix.size() * 4 + text.size() + text_start.size() * 8 + text_group.size() * 4;
+    return occ.size() * sizeof(OccEntry) + occ2.size() * sizeof(OccEntry) + occ3.size() * sizeof(OccEntry) +
+           runs.size() * sizeof(OccEntry) +
+           run_label.size() * 2 + lab.size() * 4 + (prefix.size() + prefix1.size() + prefix2.size()) * 4 + text.size() + text_start.size() * 8 + text_group.size() * 4;
 }
 
 uint32_t FmIndex::lf(uint8_t sym, uint64_t i) const {
@@ -94,6 +95,32 @@ uint32_t FmIndex::lf2(uint8_t a, uint8_t b, uint64_t i) const {
     uint64_t blk = i / OCC_BLOCK;
     uint32_t r = (uint32_t)(i - blk * OCC_BLOCK);
     return entry_rank(occ2[(uint64_t)((a - SYM_A) * 4 + (b - SYM_A)) * n_blocks() + blk], r);
+}
+
+uint32_t FmIndex::lf3(uint8_t a, uint8_t b, uint8_t c, uint64_t i) const {
+    uint64_t blk = i / OCC_BLOCK;
+    uint32_t r = (uint32_t)(i - blk * OCC_BLOCK);
+    return entry_rank(occ3[(uint64_t)((a - SYM_A) * 16 + (b - SYM_A) * 4 + (c - SYM_A)) * n_blocks() + blk], r);
+}
+
+void triple_bases(const FmIndex& idx, uint32_t out[64]) {
+    // #suffixes < "abc" = #p: T[p] < a, or T[p] = a and T[p+1] < b, or T[p..p+1] = ab and T[p+2] < c
+    const uint8_t* T = idx.text.data();
+    const uint64_t n = idx.n;
+    std::vector<uint64_t> pc(SYM_COUNT * SYM_COUNT, 0), tc(SYM_COUNT * SYM_COUNT * SYM_COUNT, 0);
+    for (uint64_t p = 0; p + 1 < n; ++p) {
+        pc[T[p] * SYM_COUNT + T[p + 1]]++;
+        if (p + 2 < n) tc[(T[p] * SYM_COUNT + T[p + 1]) * SYM_COUNT + T[p + 2]]++;
+    }
+    for (uint8_t a = SYM_A; a <= SYM_T; ++a)
+        for (uint8_t b = SYM_A; b <= SYM_T; ++b)
+            for (uint8_t c = SYM_A; c <= SYM_T; ++c) {
+                uint64_t v = idx.C[a];
+                for (uint8_t x = 0; x < b; ++x) v += pc[a * SYM_COUNT + x];
+                for (uint8_t x = 0; x < c; ++x) v += tc[(a * SYM_COUNT + b) * SYM_COUNT + x];
+                if (v > 0xFFFFFFFFull) throw std::runtime_error("fm_build: LF3 overflows 32 bits");
+                out[(a - SYM_A) * 16 + (b - SYM_A) * 4 + (c - SYM_A)] = (uint32_t)v;
+            }
 }
 
 uint64_t FmIndex::run_end(uint64_t i) const {
@@ -121,7 +148,8 @@ uint32_t FmIndex::run_of(uint64_t i) const {
 namespace {
 
 template <typename Phase>
-void build_arrays_host(FmIndex& idx, uint32_t threads, bool pair_steps, bool label_table, Phase&& phase) {
+void build_arrays_host(FmIndex& idx, uint32_t threads, bool pair_steps, bool triple_steps, bool label_table,
+                       Phase&& phase) {
     const uint64_t n = idx.n;
     // Suffix array
     idx.sa.resize(n);
@@ -167,6 +195,34 @@ void build_arrays_host(FmIndex& idx, uint32_t threads, bool pair_steps, bool lab
     }
 
     phase("occ2");
+    if (triple_steps) {
+        // three symbols before each suffix as one code (0xFF when any is not in A..T or missing)
+        std::vector<uint8_t> code(n);
+        parallel_for(n, threads, [&](uint64_t i0, uint64_t i1) {
+            for (uint64_t i = i0; i < i1; ++i) {
+                const int64_t s = SA[i];
+                uint8_t c = 0xFF;
+                if (s >= 3) {
+                    const uint8_t x = T[s - 3], y = T[s - 2], z = T[s - 1];
+                    if (x >= SYM_A && x <= SYM_T && y >= SYM_A && y <= SYM_T && z >= SYM_A && z <= SYM_T)
+                        c = (uint8_t)((x - SYM_A) * 16 + (y - SYM_A) * 4 + (z - SYM_A));
+                }
+                code[i] = c;
+            }
+        });
+        uint32_t base[64];
+        triple_bases(idx, base);
+        idx.occ3.assign(nb * 64, OccEntry{});
+        for (uint32_t pl = 0; pl < 64; ++pl) {
+            OccEntry* plane = idx.occ3.data() + (uint64_t)pl * nb;
+            fill_bitvector(plane, 1, n, nb, [&](uint64_t i) { return code[i] == pl; }, threads);
+            for (uint64_t blk = 0; blk < nb; ++blk) {
+                if ((uint64_t)plane[blk].count + base[pl] > 0xFFFFFFFFull) throw std::runtime_error("fm_build: LF3 overflows");
+                plane[blk].count += base[pl];
+            }
+        }
+    }
+    phase("occ3");
     // Label of every SA position: group of the text that holds the suffix start.
     std::vector<uint16_t> label(n);
     const uint64_t* ts = idx.text_start.data();
@@ -201,10 +257,11 @@ void build_arrays_host(FmIndex& idx, uint32_t threads, bool pair_steps, bool lab
 
 void fm_build(FmIndex& idx, const char* seq, const uint64_t* rec_offsets, uint32_t n_records,
               const int32_t* group_of_rec, uint32_t n_group_entries, uint32_t n_groups, uint32_t prefix_q,
-              uint32_t threads, bool pair_steps, bool label_table, int gpu_device) {
+              uint32_t threads, bool pair_steps, bool label_table, int gpu_device, bool triple_steps) {
     if (n_records == 0) throw std::invalid_argument("fm_build: no reference records");
     if (n_groups == 0 || n_groups > 65535) throw std::invalid_argument("fm_build: n_groups must be in [1, 65535]");
     if (prefix_q > MAX_PREFIX_Q) throw std::invalid_argument("fm_build: prefix_q > 13");
+    if (triple_steps && !pair_steps) throw std::invalid_argument("fm_build: triple steps need the pair planes");
     // Every record must belong to a group: the reference indexes group_scaffolds[t/2] unchecked
     // (fm_scanner.cpp:170, :1102, :1518) -- unassigned (-1) or missing entries are UB there, rejected here.
     if (n_group_entries < n_records)
@@ -226,6 +283,11 @@ void fm_build(FmIndex& idx, const char* seq, const uint64_t* rec_offsets, uint32
     for (uint32_t r = 0; r < n_records; ++r) total += 2 * (rec_offsets[r + 1] - rec_offsets[r] + 1);
     if (total >= (uint64_t(1) << 31)) throw std::invalid_argument("fm_build: collection exceeds 2^31 symbols");
     idx.n = total;
+    // the kernel addresses planes with 32-bit buffer offsets
+    if (pair_steps && (total / OCC_BLOCK + 1) * 16 * sizeof(OccEntry) >= (uint64_t(1) << 32) - 4096)
+        throw std::invalid_argument("fm_build: two-symbol planes exceed 4 GiB; build without pair steps");
+    if (triple_steps && (total / OCC_BLOCK + 1) * 64 * sizeof(OccEntry) >= (uint64_t(1) << 32) - 4096)
+        throw std::invalid_argument("fm_build: three-symbol planes exceed 4 GiB; build without triple steps");
     idx.text.resize(total);
     idx.text_start.resize(idx.n_texts + 1);
     idx.text_group.resize(idx.n_texts);
@@ -263,9 +325,9 @@ void fm_build(FmIndex& idx, const char* seq, const uint64_t* rec_offsets, uint32
     phase("text");
 
     if (gpu_device >= 0) {
-        fm_build_arrays_gpu(idx, gpu_device, pair_steps, label_table, show);
+        fm_build_arrays_gpu(idx, gpu_device, pair_steps, triple_steps, label_table, show);
     } else {
-        build_arrays_host(idx, threads, pair_steps, label_table, phase);
+        build_arrays_host(idx, threads, pair_steps, triple_steps, label_table, phase);
     }
     phase("labels");
     // q-mer interval table, built level by level by backward extension.
@@ -277,6 +339,8 @@ void fm_build(FmIndex& idx, const char* seq, const uint64_t* rec_offsets, uint32
             cur[2 * c + 1] = idx.C[SYM_A + c + 1];
         }
         for (uint32_t len = 1; len < prefix_q; ++len) {
+            if (len + 2 == prefix_q) idx.prefix2 = cur;
+            if (len + 1 == prefix_q) idx.prefix1 = cur;
             uint64_t m = uint64_t(1) << (2 * len);  // number of len-mers
             next.assign(2 * m * 4, 0);
             // new (len+1)-mer = c . y ; code = c * 4^len + code(y)
@@ -308,7 +372,7 @@ void fm_build(FmIndex& idx, const char* seq, const uint64_t* rec_offsets, uint32
 // Persistence: "SPEQIDX1" | u32 version | u32 0 | u64 header_len | header | fields | arrays
 namespace {
 constexpr char MAGIC[8] = {'S', 'P', 'E', 'Q', 'I', 'D', 'X', '1'};  // + FILE_VERSION
-constexpr uint32_t FILE_VERSION = 5;
+constexpr uint32_t FILE_VERSION = 7;
 
 template <typename T>
 void put(std::ofstream& os, const T& v) { os.write(reinterpret_cast<const char*>(&v), sizeof(T)); }
@@ -371,10 +435,13 @@ void fm_save(const FmIndex& idx, const std::string& path, const void* header, ui
     put_vec(os, idx.group_of_rec);
     put_vec(os, idx.occ);
     put_vec(os, idx.occ2);
+    put_vec(os, idx.occ3);
     put_vec(os, idx.runs);
     put_vec(os, idx.run_label);
     put_vec(os, idx.lab);
     put_vec(os, idx.prefix);
+    put_vec(os, idx.prefix1);
+    put_vec(os, idx.prefix2);
     if (!os) throw IoError("failed writing index file " + path);
 }
 
@@ -402,15 +469,22 @@ void fm_load(FmIndex& idx, const std::string& path, std::vector<uint8_t>* header
     get_vec(is, idx.group_of_rec, lim);
     get_vec(is, idx.occ, lim);
     get_vec(is, idx.occ2, lim);
+    get_vec(is, idx.occ3, lim);
     get_vec(is, idx.runs, lim);
     get_vec(is, idx.run_label, lim);
     get_vec(is, idx.lab, lim);
     get_vec(is, idx.prefix, lim);
+    get_vec(is, idx.prefix1, lim);
+    get_vec(is, idx.prefix2, lim);
     const uint64_t nb = idx.n_blocks();
     if (idx.text.size() != idx.n || idx.text_start.size() != (uint64_t)idx.n_texts + 1 ||
-        idx.text_group.size() != idx.n_texts || idx.occ.size() != nb * 5 || (!idx.occ2.empty() && idx.occ2.size() != nb * 16) || (!idx.lab.empty() && idx.lab.size() != idx.n) ||
+        idx.text_group.size() != idx.n_texts || idx.occ.size() != nb * 5 || (!idx.occ2.empty() && idx.occ2.size() != nb * 16) ||
+        (!idx.occ3.empty() && (idx.occ3.size() != nb * 64 || idx.occ2.empty())) || (!idx.lab.empty() && idx.lab.size() != idx.n) ||
         idx.runs.size() != nb || idx.prefix_q > MAX_PREFIX_Q ||
-        idx.prefix.size() != (idx.prefix_q ? 2 * (uint64_t(1) << (2 * idx.prefix_q)) : 0) || idx.n_groups == 0)
+        idx.prefix.size() != (idx.prefix_q ? 2 * (uint64_t(1) << (2 * idx.prefix_q)) : 0) ||
+        idx.prefix1.size() != (idx.prefix_q >= 2 ? 2 * (uint64_t(1) << (2 * (idx.prefix_q - 1))) : 0) ||
+        idx.prefix2.size() != (idx.prefix_q >= 3 ? 2 * (uint64_t(1) << (2 * (idx.prefix_q - 2))) : 0) ||
+        idx.n_groups == 0)
         throw IoError("inconsistent index file " + path);
 }
 

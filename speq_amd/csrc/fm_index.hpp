@@ -73,10 +73,14 @@ struct FmIndex {
     uint32_t C[SYM_COUNT + 1] = {0};      // C[c] = #symbols < c
     std::vector<OccEntry> occ;            // 5 * n_blocks, entry (s, b) at s * n_blocks + b
     std::vector<OccEntry> occ2;           // 16 * n_blocks or empty
+    std::vector<OccEntry> occ3;           // 64 * n_blocks or empty (three-symbol planes, plane 16a + 4b + c)
     std::vector<OccEntry> runs;           // n_blocks
     std::vector<uint16_t> run_label;      // n_runs
     std::vector<uint32_t> lab;            // n or empty
     std::vector<uint32_t> prefix;         // 2 * 4^q
+    // Shorter q-mer tables (levels q-1 and q-2, empty when q < 2 / 3): the scan picks the level that leaves a
+    // number of remaining symbols divisible by its step width (2 or 3), so no single step is needed.
+    std::vector<uint32_t> prefix1, prefix2;
     std::vector<int32_t> sa;              // n (host only, not persisted; empty after load)
 
     uint64_t n_blocks() const { return n / OCC_BLOCK + 1; }
@@ -85,6 +89,7 @@ struct FmIndex {
     // Host LF / rank used by the builder and by tests: LF(sym, i) = C[sym] + #sym in BWT[0, i).
     uint32_t lf(uint8_t sym, uint64_t i) const;
     uint32_t lf2(uint8_t a, uint8_t b, uint64_t i) const;  // two-symbol LF (requires occ2)
+    uint32_t lf3(uint8_t a, uint8_t b, uint8_t c, uint64_t i) const;  // three-symbol LF (requires occ3)
     uint32_t rank(uint8_t sym, uint64_t i) const;
     uint32_t run_of(uint64_t i) const;   // index of the label run holding SA position i
     uint64_t run_end(uint64_t i) const;  // one past the last position of the label run holding i
@@ -94,9 +99,13 @@ struct FmIndex {
 // Builds the index (throws std::invalid_argument / std::runtime_error).
 void fm_build(FmIndex& idx, const char* seq, const uint64_t* rec_offsets, uint32_t n_records,
               const int32_t* group_of_rec, uint32_t n_group_entries, uint32_t n_groups, uint32_t prefix_q,
-              uint32_t threads, bool pair_steps = false, bool label_table = false, int gpu_device = -1);
-// GPU half of fm_build (build_gpu.hip): suffix array, occ/occ2/runs planes, run labels and label table.
-void fm_build_arrays_gpu(FmIndex& idx, int device, bool pair_steps, bool label_table, bool timing);
+              uint32_t threads, bool pair_steps = false, bool label_table = false, int gpu_device = -1,
+              bool triple_steps = false);
+// GPU half of fm_build (build_gpu.hip): suffix array, occ/occ2/occ3/runs planes, run labels and label table.
+void fm_build_arrays_gpu(FmIndex& idx, int device, bool pair_steps, bool triple_steps, bool label_table,
+                         bool timing);
+// C3[abc] = #suffixes < "abc" (a, b, c in A..T), from symbol-pair and -triple counts of the text.
+void triple_bases(const FmIndex& idx, uint32_t out[64]);
 
 void fm_save(const FmIndex& idx, const std::string& path, const void* header, uint64_t header_len);
 void fm_load(FmIndex& idx, const std::string& path, std::vector<uint8_t>* header);

@@ -48,6 +48,7 @@ enum { KM_GLOBAL = 0, KM_LOCAL = 1, KM_REF = 2 };
 struct DevView {
     const uint4* occ;        // 5 planes x n_blocks entries {C[s] + count, bits[3]}: A, C, G, T, N (plane-major)
     const uint4* occ2;       // 16 two-symbol planes x n_blocks (plane 4a+b), or null
+    const uint4* occ3;       // 64 three-symbol planes x n_blocks (plane 16a+4b+c), or null (requires occ2)
     const uint4* runs;       // n_blocks entries over the label-change bitvector
     const uint16_t* run_label;
     const uint32_t* lab;     // per SA position {group | min(run_end - i, 65535) << 16}, or null
@@ -103,7 +104,7 @@ __device__ __forceinline__ uint32_t rank_entry(u32x4 v, uint32_t r) {  // v.x + 
 // both loads issue back to back with no branch and no wait on the first (a conditional plain load made hipcc
 // wait for the first load before issuing the second).
 struct Rsrc {
-    __amdgpu_buffer_rsrc_t occ, occ2, runs;
+    __amdgpu_buffer_rsrc_t occ, occ2, occ3, runs;
 };
 constexpr uint32_t OOB = 0xFFFFFFF0u;
 #ifndef SPEQ_HI_BRANCH
@@ -115,6 +116,8 @@ __device__ __forceinline__ Rsrc make_rsrc(const DevView& I) {
     R.occ = __builtin_amdgcn_make_buffer_rsrc((void*)I.occ, (short)0, (int)(5u * I.nb * 16u), 0x00020000);
     R.runs = __builtin_amdgcn_make_buffer_rsrc((void*)I.runs, (short)0, (int)(I.nb * 16u), 0x00020000);
     R.occ2 = __builtin_amdgcn_make_buffer_rsrc((void*)I.occ2, (short)0, I.occ2 ? (int)(16u * I.nb * 16u) : 0,
+                                               0x00020000);
+    R.occ3 = __builtin_amdgcn_make_buffer_rsrc((void*)I.occ3, (short)0, I.occ3 ? (int)(64u * I.nb * 16u) : 0,
                                                0x00020000);
     return R;
 }
@@ -201,7 +204,21 @@ __device__ __forceinline__ int search_lds(const DevView& I, const Rsrc& R, const
             s -= (int32_t)I.q;
         }
     }
-    if (I.occ2 != nullptr && no_n) {
+    if (I.occ3 != nullptr && no_n) {
+        // s mod 3 leftover first (one single or one pair step), then three bases per step
+        const int32_t rem = s % 3;
+        if (rem == 1 && lo < hi) {
+            lf_step(I, R.occ, w[s - 1], lo, hi);
+            --s;
+        } else if (rem == 2 && lo < hi) {
+            lf_step(I, R.occ2, (uint32_t)w[s - 2] * 4u + w[s - 1], lo, hi);
+            s -= 2;
+        }
+        while (s > 0 && lo < hi) {
+            lf_step(I, R.occ3, (uint32_t)w[s - 3] * 16u + (uint32_t)w[s - 2] * 4u + w[s - 1], lo, hi);
+            s -= 3;
+        }
+    } else if (I.occ2 != nullptr && no_n) {
         if ((s & 1) && lo < hi) {
             lf_step(I, R.occ, w[s - 1], lo, hi);
             --s;
@@ -264,7 +281,37 @@ __device__ __forceinline__ void search_packed_n(const DevView& I, const Rsrc& R,
         }
         s -= (int32_t)I.q;
     }
-    if (I.occ2 != nullptr) {
+    if (I.occ3 != nullptr) {
+        const int32_t rem = s % 3;  // leftover first: one single or one pair step
+        if (rem == 1) {
+#pragma unroll
+            for (int w = 0; w < NW; ++w) {
+                lf_step_pred(I, R.occ, (uint32_t)(P[w] & 3u), lo[w], hi[w]);
+                P[w] >>= 2;
+            }
+            --s;
+        } else if (rem == 2) {
+#pragma unroll
+            for (int w = 0; w < NW; ++w) {
+                lf_step_pred(I, R.occ2, (uint32_t)(((P[w] >> 2) & 3u) * 4u + (P[w] & 3u)), lo[w], hi[w]);
+                P[w] >>= 4;
+            }
+            s -= 2;
+        }
+        for (; s > 0; s -= 3) {
+            bool any = false;
+#pragma unroll
+            for (int w = 0; w < NW; ++w) any |= lo[w] < hi[w];
+            if (!any) break;
+#pragma unroll
+            for (int w = 0; w < NW; ++w) {
+                // pattern becomes "a b c P": c = next symbol left of P (low bits), then b, then a
+                const uint32_t plane = (uint32_t)(((P[w] >> 4) & 3u) * 16u + ((P[w] >> 2) & 3u) * 4u + (P[w] & 3u));
+                lf_step_pred(I, R.occ3, plane, lo[w], hi[w]);
+                P[w] >>= 6;
+            }
+        }
+    } else if (I.occ2 != nullptr) {
         if (s & 1) {
 #pragma unroll
             for (int w = 0; w < NW; ++w) {
@@ -648,6 +695,9 @@ struct speq_device_index {
     uint32_t grid_blocks = 8192;  // tuning: upper bound of the grid
     uint32_t ilp = 1;             // tuning: windows per lane searched concurrently (1 or 2; profiles/r01/sweep_ilp)
     uint32_t n_cus = 256;
+    const uint2* prefix_level[3] = {nullptr, nullptr, nullptr};  // q-mer tables for q, q-1, q-2
+    int prefix_choice = -1;       // tuning "prefix_level": -1 = by k (view_for_k), 0..2 = force q - level
+    uint32_t base_q = 0;          // the index's prefix_q
     std::vector<std::pair<hipEvent_t, hipEvent_t>> events;
     double timed_ms = 0.0;
     uint64_t timed_launches = 0;
@@ -691,17 +741,38 @@ void allow_big_lds_all() {
     allow_big_lds<KM_REF, false, false>();
 }
 
+// The q-mer table level for a scan of k-mers: the longest of q, q-1, q-2 that leaves a number of symbols divisible
+// by the widest LF step (3 with occ3, 2 with occ2), so the search needs no leftover single/pair step; any level
+// gives the same intervals (tests/test_gpu_parity.py runs each).
+DevView view_for_k(const speq_device_index* d, uint32_t k) {
+    DevView v = d->view;
+    const uint32_t q = d->base_q;
+    if (q == 0 || k < 1) return v;
+    const uint32_t step = v.occ3 ? 3u : (v.occ2 ? 2u : 1u);
+    for (uint32_t lvl = 0; lvl < 3; ++lvl) {
+        if (lvl >= q || d->prefix_level[lvl] == nullptr) break;
+        const uint32_t qq = q - lvl;
+        if (qq <= k && (k - qq) % step == 0) {
+            v.q = qq;
+            v.prefix = d->prefix_level[lvl];
+            return v;
+        }
+    }
+    return v;
+}
+
 template <int MODE, bool PAIRED, bool LDS>
 void launch_t(const speq_device_index* d, const UnitSrc& src, uint32_t grid, size_t lds, hipStream_t st,
               unsigned long long* a, unsigned long long* b, double* w) {
+    const DevView v = d->prefix_choice >= 0 ? d->view : view_for_k(d, src.k);
     if (MODE != KM_REF && src.em_mult != nullptr)
         hipLaunchKernelGGL((k_scan<MODE, PAIRED, LDS, 1, MODE != KM_REF>), dim3(grid), dim3(BLOCK_THREADS), lds, st,
-                           d->view, src, a, b, w);
+                           v, src, a, b, w);
     else if (d->ilp == 2)
-        hipLaunchKernelGGL((k_scan<MODE, PAIRED, LDS, 2, false>), dim3(grid), dim3(BLOCK_THREADS), lds, st, d->view,
+        hipLaunchKernelGGL((k_scan<MODE, PAIRED, LDS, 2, false>), dim3(grid), dim3(BLOCK_THREADS), lds, st, v,
                            src, a, b, w);
     else
-        hipLaunchKernelGGL((k_scan<MODE, PAIRED, LDS, 1, false>), dim3(grid), dim3(BLOCK_THREADS), lds, st, d->view,
+        hipLaunchKernelGGL((k_scan<MODE, PAIRED, LDS, 1, false>), dim3(grid), dim3(BLOCK_THREADS), lds, st, v,
                            src, a, b, w);
 }
 
@@ -802,14 +873,20 @@ int speq_device_open(const speq_index* idx, int device, speq_device_index** out)
         v.occ = reinterpret_cast<const uint4*>(dev_upload(fm.occ));
         v.nb = (uint32_t)fm.n_blocks();
         v.occ2 = reinterpret_cast<const uint4*>(dev_upload(fm.occ2));
+        v.occ3 = reinterpret_cast<const uint4*>(dev_upload(fm.occ3));
         v.runs = reinterpret_cast<const uint4*>(dev_upload(fm.runs));
         v.run_label = dev_upload(fm.run_label);
         v.lab = dev_upload(fm.lab);
         v.prefix = reinterpret_cast<const uint2*>(dev_upload(fm.prefix));
+        d->prefix_level[0] = v.prefix;
+        d->prefix_level[1] = reinterpret_cast<const uint2*>(dev_upload(fm.prefix1));
+        d->prefix_level[2] = reinterpret_cast<const uint2*>(dev_upload(fm.prefix2));
         v.n = (uint32_t)fm.n;
         v.q = fm.prefix_q;
+        d->base_q = fm.prefix_q;
         v.G = fm.n_groups;
-        d->allocs = {(void*)v.occ, (void*)v.occ2, (void*)v.runs, (void*)v.run_label, (void*)v.lab, (void*)v.prefix};
+        d->allocs = {(void*)v.occ, (void*)v.occ2, (void*)v.occ3, (void*)v.runs, (void*)v.run_label, (void*)v.lab, (void*)v.prefix,
+                     (void*)d->prefix_level[1], (void*)d->prefix_level[2]};
         d->d_text = dev_upload(fm.text);
         d->d_text_start = dev_upload(fm.text_start);
         d->d_text_group = dev_upload(fm.text_group);
@@ -831,10 +908,10 @@ int speq_device_open(const speq_index* idx, int device, speq_device_index** out)
         const uint64_t acgt_bytes = 4ull * fm.n_blocks() * sizeof(speq::OccEntry);
         d->blocks_per_cu = (fm.occ2.empty() && acgt_bytes > (4ull << 20)) ? 3u : 0u;
         d->grid_blocks = 8192;
-        // Two windows per lane pay off while every plane stays L2-resident (cfg 2: +3 %); on larger indexes the
-        // extra gathers in flight thrash L2 (cfg 3: -15 %). profiles/r01/ab_occupancy.txt
-        const uint64_t plane_bytes = (fm.occ.size() + fm.occ2.size()) * sizeof(speq::OccEntry);
-        d->ilp = plane_bytes <= (8ull << 20) ? 2u : 1u;
+        // Two windows per lane pay off on small (L2/MALL-hot) indexes (cfg 2, n = 1 M: +3 %); on larger ones the
+        // extra gathers in flight thrash the caches (cfg 3, n = 10 M: -15 %). profiles/r01/ab_occupancy.txt,
+        // sweep_triples.jsonl
+        d->ilp = fm.n < (4ull << 20) ? 2u : 1u;
         allow_big_lds_all();
         *out = d.release();
     });
@@ -996,6 +1073,13 @@ int speq_device_set_tuning(speq_device_index* d, const char* key, int64_t value)
         } else if (k == "grid_blocks") {
             if (value < 1 || value > (1 << 20)) throw std::invalid_argument("grid_blocks must be in [1, 2^20]");
             d->grid_blocks = (uint32_t)value;
+        } else if (k == "prefix_level") {
+            if (value < -1 || value > 2) throw std::invalid_argument("prefix_level must be -1 (auto) or 0..2");
+            if (value >= 0 && (d->prefix_level[value] == nullptr && value > 0))
+                throw std::invalid_argument("prefix_level: the index has no table at that level");
+            d->prefix_choice = (int)value;
+            d->view.prefix = value > 0 ? d->prefix_level[value] : d->prefix_level[0];
+            d->view.q = d->prefix_level[0] ? d->base_q - (uint32_t)(value > 0 ? value : 0) : 0;
         } else {
             throw std::invalid_argument("speq_device_set_tuning: unknown key " + k);
         }
@@ -1009,6 +1093,7 @@ int speq_device_get_tuning(const speq_device_index* d, const char* key, int64_t*
         if (k == "blocks_per_cu") *value = d->blocks_per_cu;
         else if (k == "ilp") *value = d->ilp;
         else if (k == "grid_blocks") *value = d->grid_blocks;
+        else if (k == "prefix_level") *value = d->prefix_choice;
         else throw std::invalid_argument("speq_device_get_tuning: unknown key " + k);
     });
 }

@@ -44,6 +44,8 @@ class NumpyFm:
         self.lab = lab if lab.size else None
         occ2 = index.array("occ2", np.uint32)
         self.occ2 = occ2.reshape(-1, 4) if occ2.size else None
+        occ3 = index.array("occ3", np.uint32)
+        self.occ3 = occ3.reshape(-1, 4) if occ3.size else None
 
     def lf(self, sym: np.ndarray, i: np.ndarray) -> np.ndarray:
         """LF(sym, i) = C[sym] + rank; sym: 0..3 ACGT, 4 N (entry counts include C)."""
@@ -55,6 +57,11 @@ class NumpyFm:
         blk, r = i // BLOCK, i % BLOCK
         return entry_rank(self.occ2, (a * 4 + b) * self.nb + blk, r)
 
+    def lf3(self, a: np.ndarray, b: np.ndarray, c: np.ndarray, i: np.ndarray) -> np.ndarray:
+        """Three-symbol LF: interval of abcP from that of P (plane 16a+4b+c)."""
+        blk, r = i // BLOCK, i % BLOCK
+        return entry_rank(self.occ3, (a * 16 + b * 4 + c) * self.nb + blk, r)
+
     def rank(self, sym: np.ndarray, i: np.ndarray) -> np.ndarray:
         return self.lf(sym, i) - self.C[np.asarray(sym) + 2]
 
@@ -62,7 +69,7 @@ class NumpyFm:
         return entry_rank(self.runs, i // BLOCK, i % BLOCK + 1)
 
     def classify(self, kmers: np.ndarray, use_prefix: bool = True, use_pairs: bool = True,
-                 use_lab: bool = True) -> np.ndarray:
+                 use_lab: bool = True, use_triples: bool = True) -> np.ndarray:
         """kmers: (m, k) symbols 0..4. Returns -1 / -2 / group per row (same contract as the kernel)."""
         m, k = kmers.shape
         lo = np.zeros(m, dtype=np.int64)
@@ -79,7 +86,37 @@ class NumpyFm:
             steps = np.where(okq, k - self.q, k)
         else:
             steps = np.full(m, k)
-        if self.occ2 is not None and use_pairs:
+        if self.occ3 is not None and use_triples:
+            # remainder mod 3 first (one single or one pair step), then triples (same order as the kernel)
+            ok = ~(kmers == 4).any(axis=1)
+            steps = steps.copy()
+            for rem in (1, 2):
+                rows = np.nonzero((steps % 3 == rem) & (lo < hi) & ok)[0]
+                if not rows.size:
+                    continue
+                if rem == 1:
+                    c = kmers[rows, steps[rows] - 1].astype(np.int64)
+                    lo[rows], hi[rows] = self.lf(c, lo[rows]), self.lf(c, hi[rows])
+                else:
+                    a = kmers[rows, steps[rows] - 2].astype(np.int64)
+                    b = kmers[rows, steps[rows] - 1].astype(np.int64)
+                    lo[rows], hi[rows] = self.lf2(a, b, lo[rows]), self.lf2(a, b, hi[rows])
+                steps[rows] -= rem
+            # windows that could not take multi-symbol steps (N) keep their single steps below
+            single_steps = np.where(ok, 0, steps)
+            steps = np.where(ok, steps, 0)
+            while True:
+                act = (steps > 0) & (lo < hi)
+                if not act.any():
+                    break
+                rows = np.nonzero(act)[0]
+                a = kmers[rows, steps[rows] - 3].astype(np.int64)
+                b = kmers[rows, steps[rows] - 2].astype(np.int64)
+                c = kmers[rows, steps[rows] - 1].astype(np.int64)
+                lo[rows], hi[rows] = self.lf3(a, b, c, lo[rows]), self.lf3(a, b, c, hi[rows])
+                steps[rows] -= 3
+            steps = single_steps
+        elif self.occ2 is not None and use_pairs:
             # odd remainder: one single step first, then pairs (same order as the kernel)
             pair_ok = ~(kmers == 4).any(axis=1)
             odd = (steps % 2 == 1) & (lo < hi) & pair_ok

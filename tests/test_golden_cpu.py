@@ -35,13 +35,14 @@ def test_groupings_file_matches_golden(name):
 
 @pytest.mark.parametrize("name", CASES)
 @pytest.mark.parametrize("q", [0, 3, 6])
-@pytest.mark.parametrize("pairs", [False, True])
+@pytest.mark.parametrize("steps", [1, 2, 3])
 @pytest.mark.parametrize("lab", [False, True])
-def test_fm_layout_classifies_like_oracle(name, q, pairs, lab):
+def test_fm_layout_classifies_like_oracle(name, q, steps, lab):
     """Backward search over the host arrays of OUR index reproduces the oracle label of every read window
-    and every reference window (N included), with single-base and two-base LF steps."""
+    and every reference window (N included), with single-base, two-base and three-base LF steps."""
     c = Case(name)
-    idx = FmIndex.build(c.records, c.groups, c.G, prefix_q=q, pair_steps=pairs, label_table=lab)
+    idx = FmIndex.build(c.records, c.groups, c.G, prefix_q=q, pair_steps=steps >= 2, label_table=lab,
+                        triple_steps=steps == 3)
     fm = NumpyFm(idx)
     for k in c.ks:
         orc = Oracle(c.records, c.groups, c.G, k)

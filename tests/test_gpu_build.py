@@ -11,7 +11,8 @@ from speq_amd import DeviceIndex, FmIndex, synth
 
 pytestmark = pytest.mark.gpu
 
-ARRAYS = [("text", np.uint8), ("sa", np.int32), ("occ", np.uint32), ("occ2", np.uint32), ("runs", np.uint32),
+ARRAYS = [("text", np.uint8), ("sa", np.int32), ("occ", np.uint32), ("occ2", np.uint32), ("occ3", np.uint32),
+          ("runs", np.uint32),
           ("run_label", np.uint16), ("lab", np.uint32), ("prefix", np.uint32), ("C", np.uint32),
           ("text_start", np.uint64), ("text_group", np.int32)]
 
@@ -33,8 +34,8 @@ def assert_same(records, groups, G, **kw):
 @pytest.mark.parametrize("name", CASES)
 def test_gpu_build_golden_cases(name):
     c = Case(name)
-    for q, pairs, lab in ((4, True, True), (0, False, False), (7, True, False)):
-        assert_same(c.records, c.groups, c.G, prefix_q=q, pair_steps=pairs, label_table=lab)
+    for q, pairs, lab, tri in ((4, True, True, False), (0, False, False, False), (7, True, False, True)):
+        assert_same(c.records, c.groups, c.G, prefix_q=q, pair_steps=pairs, label_table=lab, triple_steps=tri)
 
 
 @pytest.mark.parametrize("records", [
@@ -45,7 +46,7 @@ def test_gpu_build_golden_cases(name):
 ])
 def test_gpu_build_edge_cases(records):
     G = len(records)
-    assert_same(records, list(range(G)), G, prefix_q=3, pair_steps=True, label_table=True)
+    assert_same(records, list(range(G)), G, prefix_q=3, pair_steps=True, label_table=True, triple_steps=True)
 
 
 def test_gpu_build_long_repeats():
@@ -53,7 +54,7 @@ def test_gpu_build_long_repeats():
     base = "".join(rng.choice(list("ACGT"), 30_000))
     recs = [base, base[:20_000] + "A" + base[20_001:], base[::-1], base[5000:] + base[:5000]]
     recs = [r.encode() for r in recs]
-    assert_same(recs, [0, 1, 1, 2], 3, prefix_q=9, pair_steps=True, label_table=True)
+    assert_same(recs, [0, 1, 1, 2], 3, prefix_q=9, pair_steps=True, label_table=True, triple_steps=True)
 
 
 def test_gpu_build_scans_like_host():
@@ -75,5 +76,6 @@ def test_gpu_build_config3_size():
                   gpu_device=0)
     t_gpu = time.perf_counter() - t0
     t0 = time.perf_counter()
-    assert_same(ref.records, ref.groups, c["n_variants"], prefix_q=11, pair_steps=True, label_table=True)
+    assert_same(ref.records, ref.groups, c["n_variants"], prefix_q=11, pair_steps=True, label_table=True,
+                triple_steps=True)
     print(f"config-3 index: gpu build {t_gpu:.2f} s (assert_same incl. host build {time.perf_counter() - t0:.2f} s)")

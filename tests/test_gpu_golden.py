@@ -15,10 +15,11 @@ pytestmark = pytest.mark.gpu
 
 @pytest.mark.parametrize("name", CASES)
 @pytest.mark.parametrize("q", [0, 4, 8])
-@pytest.mark.parametrize("pairs", [False, True])
-def test_gpu_matches_golden(name, q, pairs):
+@pytest.mark.parametrize("steps", [1, 2, 3])
+def test_gpu_matches_golden(name, q, steps):
     c = Case(name)
-    dev = DeviceIndex(FmIndex.build(c.records, c.groups, c.G, prefix_q=q, pair_steps=pairs, label_table=pairs))
+    dev = DeviceIndex(FmIndex.build(c.records, c.groups, c.G, prefix_q=q, pair_steps=steps >= 2,
+                                    label_table=steps == 2, triple_steps=steps == 3))
     for k, ilp in [(k, ilp) for k in c.ks for ilp in (1, 2)]:
         dev.tune(ilp=ilp)
         e = c.exp["by_k"][str(k)]

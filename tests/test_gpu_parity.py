@@ -44,10 +44,11 @@ def cfg1():
 
 @pytest.mark.parametrize("q", [0, 10])
 @pytest.mark.parametrize("local", [False, True])
-@pytest.mark.parametrize("pairs", [False, True])
-def test_config1_single(cfg1, q, local, pairs):
+@pytest.mark.parametrize("steps", [1, 2, 3])
+def test_config1_single(cfg1, q, local, steps):
     ref, reads = cfg1
-    idx = FmIndex.build(ref.records, ref.groups, 3, prefix_q=q, pair_steps=pairs, label_table=pairs)
+    idx = FmIndex.build(ref.records, ref.groups, 3, prefix_q=q, pair_steps=steps >= 2, label_table=steps == 2,
+                        triple_steps=steps == 3)
     dev = DeviceIndex(idx)
     orc = Oracle(ref.records, ref.groups, 3, 21)
     got = _check(dev, orc, reads, 21, local=local)
@@ -65,10 +66,11 @@ def edge():
 
 
 @pytest.mark.parametrize("k", [1, 2, 5, 16, 21, 31, 32, 33, 70, 150, 151])
-@pytest.mark.parametrize("pairs", [False, True])
-def test_edge_reads_all_k(edge, k, pairs):
+@pytest.mark.parametrize("steps", [1, 2, 3])
+def test_edge_reads_all_k(edge, k, steps):
     ref, reads = edge
-    idx = FmIndex.build(ref.records, ref.groups, 4, prefix_q=6, pair_steps=pairs, label_table=not pairs)
+    idx = FmIndex.build(ref.records, ref.groups, 4, prefix_q=6, pair_steps=steps >= 2, label_table=steps != 2,
+                        triple_steps=steps == 3)
     dev = DeviceIndex(idx)
     orc = Oracle(ref.records, ref.groups, 4, k)
     _check(dev, orc, reads, k)
@@ -79,15 +81,36 @@ def test_edge_reads_all_k(edge, k, pairs):
     assert np.array_equal(u, ou) and np.array_equal(t, ot), (k, u, ou, t, ot)
 
 
+@pytest.mark.parametrize("steps", [1, 2, 3])
+def test_prefix_levels_agree(edge, steps):
+    """Every q-mer table level (q, q-1, q-2; auto picks by k) gives the oracle's counts."""
+    ref, reads = edge
+    idx = FmIndex.build(ref.records, ref.groups, 4, prefix_q=9, pair_steps=steps >= 2, triple_steps=steps == 3,
+                        label_table=True)
+    dev = DeviceIndex(idx)
+    for k in (5, 7, 8, 9, 10, 11, 21, 31, 70):
+        orc = Oracle(ref.records, ref.groups, 4, k)
+        for lvl in (-1, 0, 1, 2):
+            dev.tune(prefix_level=lvl)
+            assert dev.tuning("prefix_level") == lvl
+            _check_one(dev, orc, reads, k, 30, False, False)
+            u, t = dev.count_unique_kmers_per_group(k)
+            ou, ot = orc.ref_unique()
+            assert np.array_equal(u, ou) and np.array_equal(t, ot), (k, lvl)
+    dev.tune(prefix_level=-1)
+
+
 @pytest.mark.parametrize("local", [False, True])
 def test_paired(edge, local):
     ref, _ = edge
     reads = synth.make_reads(ref, 2_000, paired=True, n_rate=0.003, lowq_rate=0.01)
-    idx = FmIndex.build(ref.records, ref.groups, 4, prefix_q=8, pair_steps=True, label_table=True)
-    dev = DeviceIndex(idx)
-    for k in (21, 31, 64):
-        orc = Oracle(ref.records, ref.groups, 4, k)
-        _check(dev, orc, reads, k, paired=True, local=local)
+    for tri in (False, True):
+        idx = FmIndex.build(ref.records, ref.groups, 4, prefix_q=8, pair_steps=True, label_table=True,
+                            triple_steps=tri)
+        dev = DeviceIndex(idx)
+        for k in (21, 31, 64):
+            orc = Oracle(ref.records, ref.groups, 4, k)
+            _check(dev, orc, reads, k, paired=True, local=local)
 
 
 def test_empty_and_short_inputs(edge):
@@ -191,6 +214,10 @@ def test_config2_full_size_vs_oracle():
     u, t = dev.count_unique_kmers_per_group(k)
     ou, ot = orc.ref_unique()
     assert np.array_equal(u, ou) and np.array_equal(t, ot)
+    # three-symbol planes, built on the GPU: same counts
+    dev3 = DeviceIndex(FmIndex.build(ref.records, ref.groups, G, prefix_q=11, pair_steps=True, triple_steps=True,
+                                     label_table=True, gpu_device=0))
+    _check(dev3, orc, reads, k)
 
 
 def test_label_table_saturation_gpu():

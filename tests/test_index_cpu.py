@@ -79,12 +79,14 @@ def test_prefix_table_equals_search():
 
 def test_save_load_roundtrip(tmp_path):
     ref = synth.make_reference(3, 1, 3000, ref_n_rate=0.01)
-    idx = FmIndex.build(ref.records, ref.groups, 3, prefix_q=6)
+    idx = FmIndex.build(ref.records, ref.groups, 3, prefix_q=6, pair_steps=True, triple_steps=True, label_table=True)
     p = str(tmp_path / "x.idx")
     idx.save(p, b"hello header")
     back = FmIndex.load(p)
     assert back.header == b"hello header"
-    for name, dt in (("text", np.uint8), ("occ", np.uint32), ("runs", np.uint32),
+    assert back.info().triple_steps == 1 and back.info().pair_steps == 1 and back.info().label_table == 1
+    for name, dt in (("text", np.uint8), ("occ", np.uint32), ("occ2", np.uint32), ("occ3", np.uint32),
+                     ("lab", np.uint32), ("runs", np.uint32),
                      ("run_label", np.uint16), ("prefix", np.uint32), ("C", np.uint32), ("text_start", np.uint64),
                      ("text_group", np.int32)):
         assert np.array_equal(idx.array(name, dt), back.array(name, dt)), name
@@ -162,3 +164,49 @@ def test_gpu_build_without_gpu_fails_loudly():
         pytest.skip("a GPU is visible")
     with pytest.raises(SpeqError, match="no GPU"):
         FmIndex.build([b"ACGT"], [0], 1, gpu_device=0)
+
+
+@pytest.mark.parametrize("seed", range(3))
+def test_three_symbol_planes_match_bwt(seed):
+    """occ3 plane 16a+4b+c counts the SA rows whose suffix is preceded by abc, offset by C3[abc] = #suffixes < abc;
+    a three-symbol LF step equals three single steps."""
+    rng = np.random.default_rng(300 + seed)
+    recs = _random_records(rng, 4, 500, b"ACGT", n_rate=0.02)
+    idx = FmIndex.build(recs, [0, 1, 1, 2], 3, prefix_q=0, pair_steps=True, triple_steps=True)
+    text = idx.array("text", np.uint8).astype(np.int64)
+    sa = idx.array("sa", np.int32).astype(np.int64)
+    fm = NumpyFm(idx)
+    n = len(text)
+    code = np.full(n, -1)
+    ok = sa >= 3
+    x, y, z = (np.where(ok, text[np.maximum(sa - d, 0)], 0) for d in (3, 2, 1))
+    good = ok & (x >= 2) & (x <= 5) & (y >= 2) & (y <= 5) & (z >= 2) & (z <= 5)
+    code[good] = (x[good] - 2) * 16 + (y[good] - 2) * 4 + (z[good] - 2)
+    pos = np.arange(n + 1)
+    for pl in range(64):
+        a, b, c = pl // 16, (pl // 4) % 4, pl % 4
+        rank = fm.lf3(np.full(n + 1, a), np.full(n + 1, b), np.full(n + 1, c), pos)
+        expect = np.concatenate([[0], np.cumsum(code == pl)])
+        base = rank - expect
+        assert (base == base[0]).all(), pl  # constant offset C3[abc]
+        # the offset is the number of suffixes < "abc"
+        suffix_lt = sum(1 for p_ in range(n) if tuple(text[p_:p_ + 3]) < (a + 2, b + 2, c + 2))
+        assert base[0] == suffix_lt, pl
+    # LF3 == three single steps on random intervals of random patterns
+    for _ in range(200):
+        lo, hi = sorted(rng.integers(0, n + 1, 2))
+        a, b, c = rng.integers(0, 4, 3)
+        l1, h1 = fm.lf(np.array([c]), np.array([lo])), fm.lf(np.array([c]), np.array([hi]))
+        l1, h1 = fm.lf(np.array([b]), l1), fm.lf(np.array([b]), h1)
+        l1, h1 = fm.lf(np.array([a]), l1), fm.lf(np.array([a]), h1)
+        l3, h3 = fm.lf3(np.array([a]), np.array([b]), np.array([c]), np.array([lo])), \
+            fm.lf3(np.array([a]), np.array([b]), np.array([c]), np.array([hi]))
+        if lo < hi and (h1 - l1)[0] > 0:
+            assert (l1[0], h1[0]) == (l3[0], h3[0])
+        else:
+            assert (h3 - l3)[0] == (h1 - l1)[0] or lo >= hi
+
+
+def test_triple_steps_need_pairs():
+    with pytest.raises(SpeqError):
+        FmIndex.build([b"ACGTACGT"], [0], 1, pair_steps=False, triple_steps=True)
