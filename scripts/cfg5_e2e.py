@@ -28,7 +28,8 @@ def main():
     ref = synth.make_reference(G, c["n_isolates"], c["length"])
     emit(stage="synth_reference", seconds=time.perf_counter() - t0)
     t0 = time.perf_counter()
-    idx = FmIndex.build(ref.records, ref.groups, G, prefix_q=11, pair_steps=True, label_table="auto", gpu_device=0)
+    idx = FmIndex.build(ref.records, ref.groups, G, prefix_q=12, pair_steps=True, triple_steps=True, label_table="auto",
+                        gpu_device=0)
     info = idx.info()
     emit(stage="gpu_index_build", seconds=time.perf_counter() - t0, n=info.n, n_runs=info.n_runs,
          device_gb=info.device_bytes / 1e9, label_table=info.label_table)

@@ -26,7 +26,7 @@ def main():
         shutil.copy(st, os.path.join(dst, f"kernel_stats_{tag}.csv"))
         rows = list(csv.DictReader(open(st)))
         out["kernel_stats"] = [{k: r[k] for k in ("Name", "Calls", "AverageNs", "MinNs", "MaxNs", "Percentage")}
-                               for r in rows]
+                               for r in rows if "::k_scan<" in r["Name"]]
     pmc = collections.defaultdict(list)
     meta = {}
     for p in ("fetch", "write", "tcc", "sq"):
@@ -34,7 +34,7 @@ def main():
         if not os.path.exists(f):
             continue
         for r in csv.DictReader(open(f)):
-            if "k_scan" not in r["Kernel_Name"]:
+            if "::k_scan<" not in r["Kernel_Name"]:  # not rocPRIM's "lookback_scan" kernels of the GPU build
                 continue
             pmc[r["Counter_Name"]].append(float(r["Counter_Value"]))
             meta = {k: r[k] for k in ("Grid_Size", "Workgroup_Size", "LDS_Block_Size", "VGPR_Count", "SGPR_Count",
