@@ -248,7 +248,7 @@ void speq_groupings_free(speq_groupings* g);
  *                  default 3 when the index's occ planes exceed one XCD's L2, else 0;
  * "grid_blocks"  : upper bound of the grid (default 8192);
  * "ilp"          : k-mer windows each lane searches concurrently, 1 or 2 (default 2 for indexes of < 4 M
- *                  symbols, else 1);
+ *                  symbols, else 1); "ilp_local" the same for Phred-weighted scans (default 1);
  * "prefix_level" : q-mer table used by scans: -1 (default) picks, per k, the longest of q, q-1, q-2 that leaves a
  *                  multiple of the widest LF step; 0..2 forces table q - level (results never change). */
 int speq_device_set_tuning(speq_device_index* d, const char* key, int64_t value);

@@ -694,6 +694,7 @@ struct speq_device_index {
     uint32_t blocks_per_cu = 0;   // tuning: 0 = as many as registers/LDS allow; else pad LDS to cap occupancy
     uint32_t grid_blocks = 8192;  // tuning: upper bound of the grid
     uint32_t ilp = 1;             // tuning: windows per lane searched concurrently (1 or 2; profiles/r01/sweep_ilp)
+    uint32_t ilp_local = 1;       // the same for Phred-weighted scans (NWIN = 2 is slower there: sweep_local.jsonl)
     uint32_t n_cus = 256;
     const uint2* prefix_level[3] = {nullptr, nullptr, nullptr};  // q-mer tables for q, q-1, q-2
     int prefix_choice = -1;       // tuning "prefix_level": -1 = by k (view_for_k), 0..2 = force q - level
@@ -768,7 +769,7 @@ void launch_t(const speq_device_index* d, const UnitSrc& src, uint32_t grid, siz
     if (MODE != KM_REF && src.em_mult != nullptr)
         hipLaunchKernelGGL((k_scan<MODE, PAIRED, LDS, 1, MODE != KM_REF>), dim3(grid), dim3(BLOCK_THREADS), lds, st,
                            v, src, a, b, w);
-    else if (d->ilp == 2)
+    else if ((MODE == KM_LOCAL ? d->ilp_local : d->ilp) == 2)
         hipLaunchKernelGGL((k_scan<MODE, PAIRED, LDS, 2, false>), dim3(grid), dim3(BLOCK_THREADS), lds, st, v,
                            src, a, b, w);
     else
@@ -831,7 +832,7 @@ static void scan_device_impl(speq_device_index* d, const uint8_t* d_seq, const u
     src.end_adj = 0;
     src.k = p->k;
     src.cutoff = p->phred_cutoff;
-    src.buf_bytes = staging_bytes(p->k, d->ilp);
+    src.buf_bytes = staging_bytes(p->k, std::max(d->ilp, d->ilp_local));
     const int mode = p->mode == SPEQ_MODE_LOCAL ? KM_LOCAL : KM_GLOBAL;
     hipEvent_t e0 = nullptr, e1 = nullptr;
     if (d->timing) {
@@ -1067,9 +1068,9 @@ int speq_device_set_tuning(speq_device_index* d, const char* key, int64_t value)
         if (k == "blocks_per_cu") {
             if (value < 0 || value > 8) throw std::invalid_argument("blocks_per_cu must be in [0, 8]");
             d->blocks_per_cu = (uint32_t)value;
-        } else if (k == "ilp") {
-            if (value != 1 && value != 2) throw std::invalid_argument("ilp must be 1 or 2");
-            d->ilp = (uint32_t)value;
+        } else if (k == "ilp" || k == "ilp_local") {
+            if (value != 1 && value != 2) throw std::invalid_argument(k + " must be 1 or 2");
+            (k == "ilp" ? d->ilp : d->ilp_local) = (uint32_t)value;
         } else if (k == "grid_blocks") {
             if (value < 1 || value > (1 << 20)) throw std::invalid_argument("grid_blocks must be in [1, 2^20]");
             d->grid_blocks = (uint32_t)value;
@@ -1092,6 +1093,7 @@ int speq_device_get_tuning(const speq_device_index* d, const char* key, int64_t*
         const std::string k(key);
         if (k == "blocks_per_cu") *value = d->blocks_per_cu;
         else if (k == "ilp") *value = d->ilp;
+        else if (k == "ilp_local") *value = d->ilp_local;
         else if (k == "grid_blocks") *value = d->grid_blocks;
         else if (k == "prefix_level") *value = d->prefix_choice;
         else throw std::invalid_argument("speq_device_get_tuning: unknown key " + k);

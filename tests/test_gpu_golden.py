@@ -21,7 +21,7 @@ def test_gpu_matches_golden(name, q, steps):
     dev = DeviceIndex(FmIndex.build(c.records, c.groups, c.G, prefix_q=q, pair_steps=steps >= 2,
                                     label_table=steps == 2, triple_steps=steps == 3))
     for k, ilp in [(k, ilp) for k in c.ks for ilp in (1, 2)]:
-        dev.tune(ilp=ilp)
+        dev.tune(ilp=ilp, ilp_local=ilp)
         e = c.exp["by_k"][str(k)]
         u, t = dev.count_unique_kmers_per_group(k)
         assert u.tolist() == e["u_ref"] and t.tolist() == e["tot_ref"], (name, k)

@@ -17,9 +17,9 @@ W_RTOL = 1e-12
 def _check(dev, orc, reads, k, cutoff=30, paired=False, local=False, ilps=(1, 2)):
     """Every kernel variant (windows per lane = 1 and 2) must give the oracle's counts."""
     for ilp in ilps:
-        dev.tune(ilp=ilp)
+        dev.tune(ilp=ilp, ilp_local=ilp)
         got = _check_one(dev, orc, reads, k, cutoff, paired, local)
-    dev.tune(ilp=1)
+    dev.tune(ilp=1, ilp_local=1)
     return got
 
 
