@@ -126,3 +126,26 @@ def test_scan_end_to_end(tmp_path, name, mode):
         np.testing.assert_allclose(_parse_vec(last[1]), em[-1]["next_tkpg"], rtol=1e-5)
     got = [float(ln.split("\t")[1]) for ln in out]
     np.testing.assert_allclose(got, em[-1]["percent"], rtol=1e-5, atol=1e-9)
+
+
+@pytest.mark.gpu
+def test_all_subcommand_and_gzip_reads(tmp_path):
+    """`speq all` (index + scan in one call) on gzip-compressed reads gives the same percentages as index then
+    scan on the plain file."""
+    import gzip
+    c = Case("tiny_single")
+    for f in os.listdir(c.dir):
+        shutil.copy(os.path.join(c.dir, f), tmp_path / f)
+    with open(tmp_path / "reads_1.fq", "rb") as f, gzip.open(tmp_path / "reads_1.fq.gz", "wb") as g:
+        g.write(f.read())
+    k = c.ks[0]
+    r = run(["all", "-r", "refs.fa", "-g", "groups.txt", "-1", "reads_1.fq.gz", "-x", "ref", "-k", str(k),
+             "--phred-cutoff", str(c.cutoff), "--prefix-q", "5", "-o", "pa.txt"], tmp_path)
+    assert r.returncode == 0, r.stderr
+    r2 = run(["scan", "-1", "reads_1.fq", "-x", "ref", "-k", str(k), "--phred-cutoff", str(c.cutoff),
+              "-o", "pb.txt"], tmp_path)
+    assert r2.returncode == 0, r2.stderr
+    assert (tmp_path / "pa.txt").read_text() == (tmp_path / "pb.txt").read_text()
+    g = c.exp["by_k"][str(k)]["local"]
+    tl = [ln for ln in r.stderr.split("\n") if "\t" in ln]
+    assert tl[0] == f"{g['T']}\t{g['ambiguous']}"

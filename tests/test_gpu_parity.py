@@ -2,7 +2,7 @@
 
 Integer counters (T, ambiguous, U[g], U_ref[g], Tot_ref[g]) must be bit-exact. Phred-weighted W[g] is fp64: per
 window it is computed with the same left-to-right divisions as the reference (fm_scanner.cpp:454), but windows
-are summed in a different order, so W is compared with rtol = 1e-12.
+are summed in a different order, so W is compared with rtol = 1e-10 (worst-case re-association error ~N eps).
 """
 import numpy as np
 import pytest
@@ -11,7 +11,7 @@ from oracle.oracle import Oracle
 from speq_amd import DeviceIndex, FmIndex, synth
 
 pytestmark = pytest.mark.gpu
-W_RTOL = 1e-12
+W_RTOL = 1e-10  # fp64 sums of up to ~1e8 windows in a different order (worst case ~N * eps)
 
 
 def _check(dev, orc, reads, k, cutoff=30, paired=False, local=False, ilps=(1, 2)):
@@ -230,3 +230,31 @@ def test_label_table_saturation_gpu():
         for k in (1, 3, 12):
             orc = Oracle(ref.records, groups, G, k)
             _check(dev, orc, reads, k)
+
+
+@pytest.mark.parametrize("k", [21, 31, 70])
+def test_long_and_mixed_length_reads(k):
+    """Reads far longer than one wave pass (64 * NWIN windows) mixed with short ones: the flattened window cursor
+    must carry a read across passes and units."""
+    ref = synth.make_reference(3, 2, 40_000)
+    long_reads = synth.make_reads(ref, 300, read_len=12_000, n_rate=0.0005, lowq_rate=0.002)
+    short = synth.make_reads(ref, 2_000, read_len=100, short_frac=0.2, start_index=999)
+    segs, quals = [], []
+    for rd in (long_reads, short):
+        for i in range(rd.n):
+            a, b = int(rd.offsets[i]), int(rd.offsets[i + 1])
+            segs.append(rd.seq[a:b])
+            quals.append(rd.qual[a:b])
+    order = np.random.default_rng(k).permutation(len(segs))
+    segs = [segs[i] for i in order]
+    quals = [quals[i] for i in order]
+    off = np.zeros(len(segs) + 1, np.uint64)
+    off[1:] = np.cumsum([len(x) for x in segs])
+    reads = synth.Reads(np.concatenate(segs), np.concatenate(quals), off, np.zeros(len(segs), np.int32))
+    for tri in (False, True):
+        idx = FmIndex.build(ref.records, ref.groups, 3, prefix_q=10, pair_steps=True, triple_steps=tri,
+                            label_table=True)
+        dev = DeviceIndex(idx)
+        orc = Oracle(ref.records, ref.groups, 3, k)
+        _check(dev, orc, reads, k)
+        _check(dev, orc, reads, k, local=True)
