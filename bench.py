@@ -173,7 +173,7 @@ def main():
 
     cpu = None
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
-        cpu = cpu_baseline(ref, reads, k, G, a.cpu_seconds, local, paired)
+        cpu = cpu_baseline(ref, reads, k, G, a.cpu_seconds, local, paired, idx)
 
     if rank == 0:
         out = {
@@ -217,7 +217,17 @@ def main():
         dist.destroy_process_group()
 
 
-def cpu_baseline(ref, reads, k, G, target_s, local, paired=False):
+def cpu_model() -> str:
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_baseline(ref, reads, k, G, target_s, local, paired=False, idx=None):
     """CPU baselines on this host's cores over a bounded sample of the same reads (rank 0, N = 1 only).
 
     value: oracle/seqan_like.c — the reference's ALGORITHM restated (backward search on a wavelet structure, locate of
@@ -260,12 +270,23 @@ def cpu_baseline(ref, reads, k, G, target_s, local, paired=False):
                               target_s)
     hv, hn, hreps, hkm, ht = timed(lambda s, q, o: orc.scan(s, q, o, paired=paired, local=local, threads=threads),
                                    target_s / 3)
+    lr = None
+    if idx is not None and k <= 32 and not local:  # the build's own algorithm on CPU cores (oracle/fm_cpu.c), global mode
+        from oracle.oracle import FmCpu
+        fc = FmCpu(idx)
+        lv, ln, lreps, lkm, lt = timed(lambda s, q, o: fc.scan(s, q, o, k=k, paired=paired, threads=threads),
+                                       target_s / 3)
+        lr = {"value": lv, "unit": "k-mers/s", "cores": threads,
+              "sample": f"first {ln} x {lreps} passes ({lkm} k-mers, {lt:.1f} s), oracle/fm_cpu.c (this build's "
+                        f"label-run FM-index search on host cores, same index arrays as the GPU)"}
     unit = "pairs" if paired else "reads"
     return {"value": v, "unit": "k-mers/s", "cores": threads, "kind": "port",
             "sample": f"first {n} {unit} of the same workload x {reps} passes ({km} k-mers, {t:.1f} s) through "
                       f"oracle/seqan_like.c: the reference algorithm (wavelet backward search + SA-sample-16 locate "
                       f"of every hit + sorted hit list + first-hit rule; index build {sl_build:.1f} s not timed); "
                       f"the SeqAn3 binary cannot be built here (SURVEY.md 8(c))",
+            "cpu_model": cpu_model(),
+            "label_run_port": lr,
             "hash_port": {"value": hv, "unit": "k-mers/s", "cores": threads,
                           "sample": f"first {hn} {unit} x {hreps} passes ({hkm} k-mers, {ht:.1f} s), "
                                     f"oracle/kmer_oracle.c (hash map k-mer -> group label: no FM-index, no locate)"}}

@@ -119,7 +119,8 @@ typedef struct {
 int speq_index_get_info(const speq_index* idx, speq_index_info* info);
 
 /* Read-only views of the host arrays (for tests and tools; layout documented in DESIGN.md §3).
- * name: "text", "sa", "occ", "occ2", "occ3", "runs", "run_label", "lab", "prefix", "C", "text_start", "text_group". */
+ * name: "text", "sa", "occ", "occ2", "occ3", "runs", "run_label", "lab", "prefix", "prefix_q1", "prefix_q2", "C",
+ *       "text_start", "text_group". */
 int speq_index_array(const speq_index* idx, const char* name, const void** ptr, uint64_t* bytes);
 
 /* ---- device replica ---- */

@@ -55,6 +55,9 @@ def lib() -> C.CDLL:
                               U64P, C.POINTER(C.c_double), C.c_int]
         L.sl_text_len.restype = C.c_uint32
         L.sl_text_len.argtypes = [P]
+        L.fmcpu_scan.restype = C.c_int
+        L.fmcpu_scan.argtypes = [C.POINTER(FmCpuView), C.c_char_p, C.c_char_p, U64P, C.c_uint64, C.c_int, C.c_uint32,
+                                 C.c_uint32, U64P, C.c_int]
         _lib = L
     return _lib
 
@@ -175,6 +178,45 @@ class SeqanLike:
                 self._h = None
         except Exception:
             pass
+
+
+class FmCpuView(C.Structure):
+    _fields_ = [("occ", C.c_void_p), ("occ2", C.c_void_p), ("occ3", C.c_void_p), ("runs", C.c_void_p),
+                ("run_label", C.c_void_p), ("prefix", C.c_void_p * 3), ("q", C.c_uint32), ("n", C.c_uint32),
+                ("nb", C.c_uint32), ("G", C.c_uint32)]
+
+
+class FmCpu:
+    """The build's own label-run algorithm on host cores (fm_cpu.c) over the arrays of a built speq_amd index."""
+
+    def __init__(self, index):
+        info = index.info()
+        self._keep = {}
+
+        def arr(name, dt):
+            a = index.array(name, dt)
+            self._keep[name] = a
+            return a.ctypes.data if a.size else None
+
+        v = FmCpuView()
+        v.occ, v.occ2, v.occ3 = arr("occ", np.uint32), arr("occ2", np.uint32), arr("occ3", np.uint32)
+        v.runs, v.run_label = arr("runs", np.uint32), arr("run_label", np.uint16)
+        for i, name in enumerate(("prefix", "prefix_q1", "prefix_q2")):
+            v.prefix[i] = arr(name, np.uint32)
+        v.q, v.n, v.G = info.prefix_q, info.n, info.n_groups
+        v.nb = info.n // 96 + 1
+        self.view, self.G = v, info.n_groups
+
+    def scan(self, seq, qual, offsets, k: int, phred_cutoff: int = 30, paired: bool = False, threads: int = 0):
+        seq_b = seq.tobytes() if isinstance(seq, np.ndarray) else bytes(seq)
+        qual_b = qual.tobytes() if isinstance(qual, np.ndarray) else bytes(qual)
+        off = np.ascontiguousarray(offsets, dtype=np.uint64)
+        counts = np.zeros(self.G + 2, dtype=np.uint64)
+        rc = lib().fmcpu_scan(C.byref(self.view), seq_b, qual_b, _u64p(off), len(off) - 1, int(paired), k,
+                              phred_cutoff, _u64p(counts), threads)
+        if rc != 0:
+            raise ValueError("fmcpu_scan: bad arguments (k must be <= 32)")
+        return int(counts[0]), int(counts[1]), counts[2:].copy()
 
 
 def time_scan(oracle: Oracle, seq, qual, offsets, threads: int = 0, min_seconds: float = 0.0):

@@ -122,6 +122,8 @@ int speq_index_array(const speq_index* idx, const char* name, const void** ptr, 
         else if (n == "runs") set(f.runs.data(), f.runs.size() * sizeof(speq::OccEntry));
         else if (n == "run_label") set(f.run_label.data(), f.run_label.size() * 2);
         else if (n == "prefix") set(f.prefix.data(), f.prefix.size() * 4);
+        else if (n == "prefix_q1") set(f.prefix1.data(), f.prefix1.size() * 4);
+        else if (n == "prefix_q2") set(f.prefix2.data(), f.prefix2.size() * 4);
         else if (n == "C") set(f.C, sizeof(f.C));
         else if (n == "text_start") set(f.text_start.data(), f.text_start.size() * 8);
         else if (n == "text_group") set(f.text_group.data(), f.text_group.size() * 4);

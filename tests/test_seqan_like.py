@@ -62,3 +62,22 @@ def test_seqan_like_equals_hash_oracle(paired):
             assert a[:2] == b[:2] and a[2].tolist() == b[2].tolist()
             if local:
                 np.testing.assert_allclose(a[3], b[3], rtol=1e-12)
+
+
+@pytest.mark.parametrize("steps", [1, 2, 3])
+@pytest.mark.parametrize("paired", [False, True])
+def test_label_run_cpu_path_equals_hash_oracle(steps, paired):
+    """oracle/fm_cpu.c (the build's label-run algorithm on CPU cores, the bench's second CPU column) over our own
+    index arrays agrees with the hash-map oracle."""
+    from oracle.oracle import FmCpu
+    from speq_amd import FmIndex
+    ref = synth.make_reference(4, 2, 4_000, ref_n_rate=0.002)
+    reads = synth.make_reads(ref, 1_500, read_len=110, paired=paired, n_rate=0.003, lowq_rate=0.01)
+    for q in (0, 7):
+        idx = FmIndex.build(ref.records, ref.groups, 4, prefix_q=q, pair_steps=steps >= 2, triple_steps=steps == 3)
+        fc = FmCpu(idx)
+        for k in (9, 21, 32):
+            orc = Oracle(ref.records, ref.groups, 4, k)
+            a = fc.scan(reads.seq, reads.qual, reads.offsets, k=k, paired=paired, threads=4)
+            b = orc.scan(reads.seq, reads.qual, reads.offsets, paired=paired, threads=4)
+            assert a[:2] == b[:2] and a[2].tolist() == b[2].tolist(), (q, k)
