@@ -14,13 +14,16 @@
 //   occ2   : optional 16 two-symbol planes (pairs ab over ACGT, plane 4a+b), same entry format: bit j set iff
 //            T[SA[j]-2] T[SA[j]-1] == ab, count = C2[ab] + rank, with C2[ab] = #suffixes < "ab". One gather pair
 //            then extends the pattern by TWO bases: interval(abP) = (LF2(ab, lo), LF2(ab, hi)).
+//   occ3   : optional 64 three-symbol planes (plane 16a+4b+c), count = C3[abc] + rank with C3[abc] = #suffixes <
+//            "abc": one gather pair extends the pattern by THREE bases (same argument as occ2).
 //   runs   : 16-B entries over the label-change bitvector B[i] = [label(SA[i]) != label(SA[i-1])],
 //            label = group of the text holding suffix SA[i]
 //   run_label : group id of every run (u16)
 //   lab    : optional u32 per SA position: group (low 16 bits) | min(run_end - i, 65535) (high 16 bits), where
 //            run_end is one past the label run holding i. [lo,hi) is single-group iff hi - lo <= that distance, so
 //            the classification is one 4-B load (the runs/run_label rank path remains for saturated distances).
-//   prefix : for every q-mer over ACGT its SA interval (u32 lo, u32 hi)
+//   prefix : for every q-mer over ACGT its SA interval (u32 lo, u32 hi); prefix1 / prefix2 the same for q-1 / q-2
+//            (a scan picks the level that leaves k - q' divisible by its widest step)
 //
 // "All occurrences of a window lie in ONE group" <=> the window's SA interval [lo,hi) holds no label change,
 // i.e. run(lo) == run(hi-1). That replaces SeqAn3's locate of every occurrence.
