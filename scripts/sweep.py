@@ -32,6 +32,7 @@ def main():
     ap.add_argument("--pairs", default="0,1", help="multi-symbol steps to sweep: 0 single, 1 pairs, 2 pairs + triples")
     ap.add_argument("--labs", default="1", help="label_table values to sweep")
     ap.add_argument("--ilps", default="1", help="windows per lane to sweep (1, 2)")
+    ap.add_argument("--k", type=int, default=0, help="override the config's k")
     a = ap.parse_args()
     import torch
 
@@ -39,7 +40,7 @@ def main():
     dev_t = torch.device("cuda:0")
     for cfg in [int(x) for x in a.configs.split(",")]:
         c = synth.CONFIGS[cfg]
-        G, k = c["n_variants"], c["k"]
+        G, k = c["n_variants"], (a.k or c["k"])
         ref = synth.make_reference(c["n_variants"], c["n_isolates"], c["length"])
         reads = synth.make_reads(ref, a.reads, paired=c["paired"])
         lens = np.diff(reads.offsets).astype(np.int64)

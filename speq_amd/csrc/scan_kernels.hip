@@ -27,6 +27,7 @@
 #include <cstdint>
 #include <cstring>
 #include <memory>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -699,6 +700,7 @@ struct speq_device_index {
     const uint2* prefix_level[3] = {nullptr, nullptr, nullptr};  // q-mer tables for q, q-1, q-2
     int prefix_choice = -1;       // tuning "prefix_level": -1 = by k (view_for_k), 0..2 = force q - level
     uint32_t base_q = 0;          // the index's prefix_q
+    std::mutex events_mu;  // launches may come from several host threads (pipelines, concurrent scans)
     std::vector<std::pair<hipEvent_t, hipEvent_t>> events;
     double timed_ms = 0.0;
     uint64_t timed_launches = 0;
@@ -844,6 +846,7 @@ static void scan_device_impl(speq_device_index* d, const uint8_t* d_seq, const u
                 reinterpret_cast<unsigned long long*>(d_counts), nullptr, d_weights);
     if (d->timing) {
         HIP_OK(hipEventRecord(e1, st));
+        std::lock_guard<std::mutex> lk(d->events_mu);
         d->events.emplace_back(e0, e1);
     }
 }
@@ -1112,6 +1115,7 @@ int speq_timing_read(speq_device_index* d, double* total_ms, uint64_t* launches)
         if (!d || !total_ms || !launches) throw std::invalid_argument("speq_timing_read: null argument");
         DeviceGuard g(d->device);
         double ms = 0.0;
+        std::lock_guard<std::mutex> lk(d->events_mu);
         for (auto& e : d->events) {
             HIP_OK(hipEventSynchronize(e.second));
             float t = 0.f;
