@@ -199,6 +199,10 @@ def main():
             "roofline": {
                 "bound": "hbm", "achieved": achieved_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": achieved_gbs / HBM_PEAK_GBS, "traffic": traffic,
+                # measured L2->fabric bytes per launch over this run's launch time: the bandwidth the kernel really
+                # draws from Infinity Cache + HBM (an upper bound on HBM bytes), against the same 8 TB/s peak
+                "traffic_GBps": (traffic / avg_kernel_s / 1e9) if traffic else None,
+                "traffic_frac": (traffic / avg_kernel_s / 1e9 / HBM_PEAK_GBS) if traffic else None,
                 "kernel": "k_scan (speq_amd/csrc/scan_kernels.hip)",
                 "algorithmic_bytes_per_kmer": 2 * k * OCC_ENTRY_BYTES,
                 "avg_kernel_ms": avg_kernel_s * 1e3, "launches_timed": launches,

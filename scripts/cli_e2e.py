@@ -66,7 +66,7 @@ def main():
         ["-x", "ref", "-k", str(c["k"]), "-t", str(a.threads), "--fixed-accuracy", "0.99", "-o", "out.txt"]
     if rc == 0:
         run(scan, "scan (first: + .dat pass)")
-        run(scan, "scan (cached .dat)")
+        run(scan[:-2] + ["-o", "out2.txt"], "scan (cached .dat)")
         run(scan[:-4] + ["-o", "out_local.txt"], "scan local/Phred (cached .dat)")
     subprocess.run(["rm", "-rf", work])
 
