@@ -145,8 +145,8 @@ def main():
             tj = json.load(open(prof))
             lab = int(idx.info().label_table)
             steps = "_tri1" if a.triple_steps else ""
-            key = (f"cfg{a.config}_k{k}_q{a.prefix_q}_pairs{a.pair_steps}{steps}_lab{lab}_ilp{ilp}_{a.mode}"
-                   f"_reads{n_reads}")
+            key = (f"cfg{a.config}_k{k}_q{a.prefix_q}_pairs{a.pair_steps}{steps}_lab{lab}_ilp{ilp}"
+                   f"_bpc{dev.tuning('blocks_per_cu')}_{a.mode}_reads{n_reads}")
             if key in tj:
                 traffic = tj[key]["hbm_bytes_per_launch"]
                 traffic_src = tj[key]["source"]
@@ -193,6 +193,7 @@ def main():
                 "workload": f"BASELINE config {a.config}: {c['n_variants']} variants x {c['n_isolates']} isolates x "
                             f"{c['length']} bp, {n_reads} x 150 bp {'pairs' if paired else 'reads'} per GPU, k={k}",
                 "k": k, "reads_per_gpu": n_reads, "paired": paired, "mode": a.mode, "prefix_q": a.prefix_q, "prefix_q_used": q_used, "pair_steps": a.pair_steps, "triple_steps": a.triple_steps, "label_table": int(idx.info().label_table), "ilp": ilp,
+                "blocks_per_cu": dev.tuning("blocks_per_cu"), "grid_blocks": dev.tuning("grid_blocks"),
                 "kmers_per_step_per_gpu": kmers_per_step, "parallelism": f"dp{world} (reads sharded, index replicated)",
                 "index_build_s": round(build_s, 3), "index_builder": "gpu" if a.gpu_build else "host", "fm_text_len": int(idx.info().n),
             },

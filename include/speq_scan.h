@@ -246,8 +246,8 @@ void speq_groupings_free(speq_groupings* g);
 
 /* ---- launch tuning (performance only; results never depend on it) ----
  * "blocks_per_cu": cap resident 256-thread workgroups per CU (0 = no cap; the kernel's LDS is padded);
- *                  default 3 when the index's occ planes exceed one XCD's L2, else 0;
- * "grid_blocks"  : upper bound of the grid (default 8192);
+ *                  default by plane footprint: <= 16 MB none, <= 256 MB (Infinity Cache) 4, larger 3;
+ * "grid_blocks"  : upper bound of the grid (default 16384 below 4 M symbols, else 8192);
  * "ilp"          : k-mer windows each lane searches concurrently, 1 or 2 (default 2 for indexes of < 4 M
  *                  symbols, else 1); "ilp_local" the same for Phred-weighted scans (default 1);
  * "prefix_level" : q-mer table used by scans: -1 (default) picks, per k, the longest of q, q-1, q-2 that leaves a

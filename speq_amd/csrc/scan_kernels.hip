@@ -911,7 +911,14 @@ int speq_device_open(const speq_index* idx, int device, speq_device_index** out)
         // (With the two-symbol planes the gather chain is half as long and full occupancy wins again.)
         const uint64_t acgt_bytes = 4ull * fm.n_blocks() * sizeof(speq::OccEntry);
         d->blocks_per_cu = (fm.occ2.empty() && acgt_bytes > (4ull << 20)) ? 3u : 0u;
-        d->grid_blocks = 8192;
+        if (!fm.occ3.empty()) {
+            // With the three-symbol planes (measured, profiles/r01/sweep_grid_triples.jsonl, sweep_bpc_cfg*.jsonl):
+            // planes that spill L2 but fit the 256 MB Infinity Cache want 4 blocks/CU (cfg 3: +12 %); planes that
+            // spill the Infinity Cache too, so gathers go to HBM, want 3 (cfg 5: 2.1x); small ones want them all.
+            const uint64_t plane_bytes = (fm.occ.size() + fm.occ2.size() + fm.occ3.size()) * sizeof(speq::OccEntry);
+            d->blocks_per_cu = plane_bytes <= (16ull << 20) ? 0u : (plane_bytes <= (256ull << 20) ? 4u : 3u);
+        }
+        d->grid_blocks = fm.n < (4ull << 20) ? 16384u : 8192u;
         // Two windows per lane pay off on small (L2/MALL-hot) indexes (cfg 2, n = 1 M: +3 %); on larger ones the
         // extra gathers in flight thrash the caches (cfg 3, n = 10 M: -15 %). profiles/r01/ab_occupancy.txt,
         // sweep_triples.jsonl
