@@ -29,7 +29,7 @@ OCC_ENTRY_BYTES = 64   # algorithmic bytes per k-mer = k LF st
 def parse_args():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=10)
+    p.add_argument("--steps", type=int, default=20)
     p.add_argument("--warmup", type=int, default=2)
     p.add_argument("--config", type=int, default=2, help="BASELINE.json config number (1-5)")
     p.add_argument("--reads", type=int, default=0, help="override reads per GPU")
