@@ -27,11 +27,11 @@ def main():
     ap.add_argument("--modes", default="global,local")
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--ref-pass", action="store_true")
-    ap.add_argument("--bpc", default="0", help="blocks-per-CU caps to sweep (0 = none)")
-    ap.add_argument("--grids", default="8192", help="grid caps to sweep")
+    ap.add_argument("--bpc", default="auto", help="blocks-per-CU caps to sweep (0 = none; auto = device default)")
+    ap.add_argument("--grids", default="auto", help="grid caps to sweep (auto = device default)")
     ap.add_argument("--pairs", default="0,1", help="multi-symbol steps to sweep: 0 single, 1 pairs, 2 pairs + triples")
     ap.add_argument("--labs", default="1", help="label_table values to sweep")
-    ap.add_argument("--ilps", default="1", help="windows per lane to sweep (1, 2)")
+    ap.add_argument("--ilps", default="auto", help="windows per lane to sweep (1, 2; auto = device default)")
     ap.add_argument("--k", type=int, default=0, help="override the config's k")
     a = ap.parse_args()
     import torch
@@ -60,14 +60,20 @@ def main():
                                         label_table=bool(lb), triple_steps=pr == 2, gpu_device=0)
                     info = idx.info()
                     devs[(q, pr, lb)] = (DeviceIndex(idx), time.time() - t0, info)
+        def vals(arg):
+            return [-1] if arg == "auto" else [int(x) for x in arg.split(",")]
         times = {(q, m, b, g, il): [] for q in devs for m in a.modes.split(",")
-                 for b in [int(x) for x in a.bpc.split(",")] for g in [int(x) for x in a.grids.split(",")]
-                 for il in [int(x) for x in a.ilps.split(",")]}
+                 for b in vals(a.bpc) for g in vals(a.grids) for il in vals(a.ilps)}
+        defaults = {q: (d.tuning("blocks_per_cu"), d.tuning("grid_blocks"), d.tuning("ilp"), d.tuning("ilp_local"))
+                    for q, (d, _, _) in devs.items()}
         checks = {}
         for r in range(a.rounds):
             for (q, m, b, g, il) in times:
                 dev = devs[q][0]
-                dev.tune(blocks_per_cu=b, grid_blocks=g, ilp=il)
+                db, dg, di, dl = defaults[q]
+                dev.tune(blocks_per_cu=db if b < 0 else b, grid_blocks=dg if g < 0 else g,
+                         ilp=(dl if m == "local" else di) if il < 0 else il,
+                         ilp_local=dl if il < 0 else il)
                 d_counts.zero_()
                 d_w.zero_()
                 dev.timing(True)
@@ -84,8 +90,10 @@ def main():
             med = statistics.median(ts)
             if ref_check is None:
                 ref_check = checks[(q, m, b, g, il)]
-            out = {"config": cfg, "k": k, "reads": reads.n, "prefix_q": q[0], "pairs": q[1], "lab": q[2], "mode": m, "blocks_per_cu": b,
-                   "grid_blocks": g, "ilp": il, "kernel_ms_median": med,
+            db, dg, di, dl = defaults[q]
+            out = {"config": cfg, "k": k, "reads": reads.n, "prefix_q": q[0], "pairs": q[1], "lab": q[2], "mode": m,
+                   "blocks_per_cu": db if b < 0 else b, "grid_blocks": dg if g < 0 else g,
+                   "ilp": ((dl if m == "local" else di) if il < 0 else il), "kernel_ms_median": med,
                    "kernel_ms_min": min(ts), "kmers_per_s": kmers / (med / 1e3),
                    "algo_GBps": kmers * 2 * k * 64 / (med / 1e3) / 1e9,
                    "index_build_s": round(devs[q][1], 3), "n": int(devs[q][2].n), "n_runs": int(devs[q][2].n_runs),

@@ -123,6 +123,31 @@ __device__ __forceinline__ Rsrc make_rsrc(const DevView& I) {
     return R;
 }
 
+// Cache policy A/B knobs: read bytes are streamed once per launch, so loading them non-temporally keeps them from
+// evicting index lines in L2; the q-mer table is one random 8-B load per window.
+#ifndef SPEQ_NT_READS
+#define SPEQ_NT_READS 0
+#endif
+#ifndef SPEQ_NT_PREFIX
+#define SPEQ_NT_PREFIX 0
+#endif
+template <typename T>
+__device__ __forceinline__ T ld_stream(const T* p) {
+#if SPEQ_NT_READS
+    return __builtin_nontemporal_load(p);
+#else
+    return *p;
+#endif
+}
+__device__ __forceinline__ uint2 ld_prefix(const uint2* p) {
+#if SPEQ_NT_PREFIX
+    const uint64_t v = __builtin_nontemporal_load(reinterpret_cast<const uint64_t*>(p));
+    return make_uint2((uint32_t)v, (uint32_t)(v >> 32));
+#else
+    return *p;
+#endif
+}
+
 // One backward-search step for both ends of [lo, hi): the two ranks share one 16-B load when they fall in the
 // same 96-position block (narrow intervals, i.e. almost every step after the q-mer table). `rs` selects the
 // one-symbol planes (plane = symbol) or the two-symbol planes (plane = 4a + b: extends by two bases).
@@ -199,7 +224,7 @@ __device__ __forceinline__ int search_lds(const DevView& I, const Rsrc& R, const
             code = (code << 2) | (c & 3u);
         }
         if (!bad) {
-            const uint2 e = I.prefix[code];
+            const uint2 e = ld_prefix(I.prefix + code);
             lo = e.x;
             hi = e.y;
             s -= (int32_t)I.q;
@@ -274,7 +299,7 @@ __device__ __forceinline__ void search_packed_n(const DevView& I, const Rsrc& R,
 #pragma unroll
         for (int w = 0; w < NW; ++w) {
             if (act[w]) {
-                const uint2 e = I.prefix[(uint32_t)(P[w] & qmask)];
+                const uint2 e = ld_prefix(I.prefix + (uint32_t)(P[w] & qmask));
                 lo[w] = e.x;
                 hi[w] = e.y;
             }
@@ -421,8 +446,8 @@ __global__ __launch_bounds__(BLOCK_THREADS, SPEQ_MIN_WAVES) void k_scan(DevView 
         uint32_t wl = 0;
         uint64_t bl_ = 0;
         if (r + lane < r_end) {
-            bl_ = src.off[r + lane];
-            const uint64_t L = src.off[r + lane + 1] - src.end_adj - bl_;
+            bl_ = ld_stream(src.off + r + lane);
+            const uint64_t L = ld_stream(src.off + r + lane + 1) - src.end_adj - bl_;
             uint64_t W = L >= k ? L - k + 1 : 0;
             if (lane == 0) W = W > o ? W - o : 0;
             wl = (uint32_t)(W < 64u * NWIN + 1u ? W : 64u * NWIN + 1u);
@@ -476,7 +501,7 @@ __global__ __launch_bounds__(BLOCK_THREADS, SPEQ_MIN_WAVES) void k_scan(DevView 
             const uint32_t p = p0 + lane;
             uint32_t bad = 1, isn = 0;
             if (p < span) {
-                const uint32_t ch = src.seq[s0 + p];
+                const uint32_t ch = ld_stream(src.seq + s0 + p);
                 uint32_t sym;
                 if (MODE == KM_REF) {
                     sym = ch - 2u;            // SA alphabet A..N = 2..6
@@ -484,7 +509,7 @@ __global__ __launch_bounds__(BLOCK_THREADS, SPEQ_MIN_WAVES) void k_scan(DevView 
                     isn = sym == 4u ? 1u : 0u;
                 } else {
                     sym = ascii_sym(ch);
-                    int q = (int)src.qual[s0 + p] - 33;
+                    int q = (int)ld_stream(src.qual + s0 + p) - 33;
                     q = q < 0 ? 0 : (q > 41 ? 41 : q);
                     bad = ((uint32_t)q <= src.cutoff || sym == 4u) ? 1u : 0u;
                     if (MODE == KM_LOCAL) qbuf[p] = (unsigned char)q;
