@@ -60,7 +60,8 @@ typedef struct {
                             0: host SA-IS. Both produce identical indexes. */
     int32_t device;      /* GPU ordinal for gpu_build */
     uint32_t triple_steps; /* 1: also add the 64 three-symbol occ planes (LF over three bases per gather pair;
-                              10.7 bytes per text symbol); requires pair_steps */
+                              10.7 bytes per text symbol); requires pair_steps; 2: auto (on while the planes fit
+                              32-bit buffer offsets, ~400 M symbols) */
 } speq_build_opts;
 
 /* Per-scan parameters (reference: cmd_arguments in include/arg_parse.h:10-28). */

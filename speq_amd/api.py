@@ -90,7 +90,7 @@ class FmIndex:
     def build(cls, records: Sequence[bytes | str], group_of_record: Sequence[int], n_groups: int,
               prefix_q: int = 0, threads: int = 0, pair_steps: bool = False,
               label_table: bool | str = False, gpu_device: Optional[int] = None,
-              triple_steps: bool = False) -> "FmIndex":
+              triple_steps: bool | str = False) -> "FmIndex":
         """label_table: True/False or "auto" (only for collections of >= 4 M symbols).
         gpu_device: build the suffix array and planes on that GPU (None = host SA-IS); identical results."""
         seq, off = pack_records(records)
@@ -98,7 +98,8 @@ class FmIndex:
         h = C.c_void_p()
         opts = BuildOpts(prefix_q, threads, int(pair_steps), 2 if label_table == "auto" else int(bool(label_table)),
                          int(gpu_device is not None),
-                         gpu_device if gpu_device is not None else 0, int(triple_steps))
+                         gpu_device if gpu_device is not None else 0,
+                         2 if triple_steps == "auto" else int(bool(triple_steps)))
         check(lib().speq_index_build(seq, _u64p(off), len(records), grp.ctypes.data_as(C.POINTER(C.c_int32)),
                                      len(grp), n_groups, C.byref(opts), C.byref(h)))
         return cls(h)

@@ -29,7 +29,7 @@ struct CmdArguments {  // include/arg_parse.h:10-28
     // MI355X build extensions (not in the reference)
     unsigned int prefix_q{12};   // --prefix-q: q-mer interval table of the FM-index (levels q, q-1, q-2)
     bool pair_steps{true};       // --pair-steps: two-symbol occ planes
-    bool triple_steps{true};     // --triple-steps: three-symbol occ planes
+    unsigned triple_steps{2};    // --triple-steps: three-symbol occ planes (2 = auto)
     int gpu_build{-1};           // --gpu-build: -1 auto (GPU when one is visible), 0 host SA-IS, 1 GPU
     unsigned label_table{2};     // --label-table: per-position {group, run distance} table (2 = auto)
     int device{-1};              // --device: GPU ordinal (default: $LOCAL_RANK or 0)

@@ -49,7 +49,8 @@ const char* HELP =
     "      --label-table auto|0|1 per-position group/run table: one-load classification (default auto:\n"
     "                            when the collection has >= 4 M symbols)\n"
     "      --gpu-build auto|0|1  build the suffix array on the GPU (default auto: when one is visible)\n"
-    "      --triple-steps 0|1    three-base LF planes in the FM-index (10.7 B per symbol; default 1)\n"
+    "      --triple-steps auto|0|1 three-base LF planes in the FM-index (10.7 B per symbol; default auto:\n"
+    "                            on below ~400 M symbols)\n"
     "      --device N            GPU ordinal (default $LOCAL_RANK or 0)\n";
 
 template <typename T>
@@ -121,7 +122,10 @@ CmdArguments parse(int argc, char** argv) {
             const std::string v = value();
             a.label_table = v == "auto" ? 2u : (to_number<unsigned>(opt, v) != 0 ? 1u : 0u);
         }
-        else if (allow_refs && opt == "--triple-steps") a.triple_steps = to_number<unsigned>(opt, value()) != 0;
+        else if (allow_refs && opt == "--triple-steps") {
+            const std::string v = value();
+            a.triple_steps = v == "auto" ? 2u : (to_number<unsigned>(opt, v) != 0 ? 1u : 0u);
+        }
         else if (allow_refs && opt == "--gpu-build") {
             const std::string v = value();
             if (v == "auto") a.gpu_build = -1;
@@ -285,7 +289,7 @@ void generate_fm_index(const CmdArguments& a, const fs::path& idx_path, const In
     }
     const bool gpu = a.gpu_build == 1 || (a.gpu_build < 0 && speq_device_count() > 0);
     speq_build_opts opts{a.prefix_q, a.threads, a.pair_steps ? 1u : 0u, a.label_table, gpu ? 1u : 0u, bdev,
-                         (a.triple_steps && a.pair_steps) ? 1u : 0u};
+                         a.pair_steps ? a.triple_steps : 0u};
     speq_index* idx = nullptr;
     ok(speq_index_build(refs.seq.data(), refs.offsets.data(), (uint32_t)refs.size(), h.scaffolds.data(),
                         (uint32_t)h.scaffolds.size(), (uint32_t)h.names.size(), &opts, &idx),

@@ -43,10 +43,18 @@ int speq_index_build(const char* seq, const uint64_t* rec_offsets, uint32_t n_re
             for (uint32_t r = 0; r < n_records; ++r) n += 2 * (rec_offsets[r + 1] - rec_offsets[r] + 1);
             lab = n >= (4ull << 20);
         }
+        // triple_steps 2 = auto: the 64 three-symbol planes (10.7 B per symbol) while they stay addressable with
+        // 32-bit buffer offsets, i.e. below ~400 M symbols
+        bool tri = opts && opts->triple_steps == 1;
+        if (opts && opts->triple_steps == 2 && opts->pair_steps) {
+            uint64_t n = 1;
+            for (uint32_t r = 0; r < n_records; ++r) n += 2 * (rec_offsets[r + 1] - rec_offsets[r] + 1);
+            tri = (n / speq::OCC_BLOCK + 1) * 64 * 16 < (uint64_t(1) << 32) - 4096;
+        }
         auto idx = std::make_unique<speq_index>();
         speq::fm_build(idx->fm, seq, rec_offsets, n_records, group_of_rec, n_group_entries, n_groups,
                        opts ? opts->prefix_q : 0, opts ? opts->threads : 0, opts ? opts->pair_steps != 0 : false,
-                       lab, gpu, opts && opts->triple_steps != 0);
+                       lab, gpu, tri);
         *out = idx.release();
     });
 }
