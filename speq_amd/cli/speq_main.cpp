@@ -439,7 +439,13 @@ int run_scan(CmdArguments& a) {
     std::cerr << speq::format_vector(percent) << "\n";
     if (!(local && !paired)) std::cerr << speq::format_vector(unique_totals) << "\n";
     std::cerr << total << "\t" << ambiguous << "\n";
-    if (local && paired) std::cerr << "[({}," << ambiguous << ")]\n";  // fusion map: key always {} (:916)
+    // Fusion map (paired Phred mode, :915-1033): do_a_count takes set_groups BY VALUE (:916), so every key is the
+    // empty set and the map is {{} -> ambiguous pairs}, or empty; seqan3's debug_stream prints a map as a range of
+    // (key,value) tuples and a set as a range: "[([],N)]" or "[]".
+    if (local && paired) {
+        if (ambiguous) std::cerr << "[([]," << ambiguous << ")]\n";
+        else std::cerr << "[]\n";
+    }
 
     // EM refinement (fm_scanner.cpp:248-279, :515-545, :761-792, :1035-1065) over the histogram.
     ok(speq_em_finalize(em, a.threads), "building the EM histogram");

@@ -108,6 +108,9 @@ def test_scan_end_to_end(tmp_path, name, mode):
     np.testing.assert_allclose(_parse_vec(lines[2]), g["percent"], rtol=1e-5)
     tl = [ln for ln in lines if "\t" in ln]
     assert tl[0] == f"{g['T']}\t{g['ambiguous']}"
+    if c.paired and mode == "local":  # fusion map with its always-empty key (fm_scanner.cpp:916, :1033)
+        fm = lines[lines.index(tl[0]) + 1]
+        assert fm == (f"[([],{g['ambiguous']})]" if g["ambiguous"] else "[]")
     # second scan reuses the .dat (no U_ref/Tot_ref lines) and writes the percentages to -o
     r2 = run(args + ["-o", "p2.txt"], tmp_path)
     assert r2.returncode == 0
