@@ -79,3 +79,10 @@ def test_gpu_build_config3_size():
     assert_same(ref.records, ref.groups, c["n_variants"], prefix_q=11, pair_steps=True, label_table=True,
                 triple_steps=True)
     print(f"config-3 index: gpu build {t_gpu:.2f} s (assert_same incl. host build {time.perf_counter() - t0:.2f} s)")
+
+
+def test_gpu_build_many_records():
+    """2,500 records (5,000 texts): label lookup by binary search over text starts, many short runs."""
+    G = 2500
+    ref = synth.make_reference(G, 1, 300, ref_n_rate=0.002)
+    assert_same(ref.records, ref.groups, G, prefix_q=6, pair_steps=True, label_table=True, triple_steps=True)
