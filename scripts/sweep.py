@@ -33,6 +33,7 @@ def main():
     ap.add_argument("--labs", default="1", help="label_table values to sweep")
     ap.add_argument("--ilps", default="auto", help="windows per lane to sweep (1, 2; auto = device default)")
     ap.add_argument("--k", type=int, default=0, help="override the config's k")
+    ap.add_argument("--sparse", default="-1", help="sparse q-mer table choices (-1 auto, 0 dense, 1 sparse)")
     a = ap.parse_args()
     import torch
 
@@ -62,14 +63,16 @@ def main():
                     devs[(q, pr, lb)] = (DeviceIndex(idx), time.time() - t0, info)
         def vals(arg):
             return [-1] if arg == "auto" else [int(x) for x in arg.split(",")]
-        times = {(q, m, b, g, il): [] for q in devs for m in a.modes.split(",")
-                 for b in vals(a.bpc) for g in vals(a.grids) for il in vals(a.ilps)}
+        times = {(q, m, b, g, il, sp): [] for q in devs for m in a.modes.split(",")
+                 for b in vals(a.bpc) for g in vals(a.grids) for il in vals(a.ilps)
+                 for sp in [int(x) for x in a.sparse.split(",")]}
         defaults = {q: (d.tuning("blocks_per_cu"), d.tuning("grid_blocks"), d.tuning("ilp"), d.tuning("ilp_local"))
                     for q, (d, _, _) in devs.items()}
         checks = {}
         for r in range(a.rounds):
-            for (q, m, b, g, il) in times:
+            for (q, m, b, g, il, sp) in times:
                 dev = devs[q][0]
+                dev.tune(sparse_prefix=sp)
                 db, dg, di, dl = defaults[q]
                 dev.tune(blocks_per_cu=db if b < 0 else b, grid_blocks=dg if g < 0 else g,
                          ilp=(dl if m == "local" else di) if il < 0 else il,
@@ -83,13 +86,13 @@ def main():
                                 stream=stream)
                 torch.cuda.synchronize()
                 ms, n = dev.timing_read()
-                times[(q, m, b, g, il)].append(ms)
-                checks[(q, m, b, g, il)] = d_counts.cpu().numpy().tolist()
+                times[(q, m, b, g, il, sp)].append(ms)
+                checks[(q, m, b, g, il, sp)] = d_counts.cpu().numpy().tolist()
         ref_check = None
-        for (q, m, b, g, il), ts in times.items():
+        for (q, m, b, g, il, sp), ts in times.items():
             med = statistics.median(ts)
             if ref_check is None:
-                ref_check = checks[(q, m, b, g, il)]
+                ref_check = checks[(q, m, b, g, il, sp)]
             db, dg, di, dl = defaults[q]
             out = {"config": cfg, "k": k, "reads": reads.n, "prefix_q": q[0], "pairs": q[1], "lab": q[2], "mode": m,
                    "blocks_per_cu": db if b < 0 else b, "grid_blocks": dg if g < 0 else g,
@@ -97,7 +100,7 @@ def main():
                    "kernel_ms_min": min(ts), "kmers_per_s": kmers / (med / 1e3),
                    "algo_GBps": kmers * 2 * k * 64 / (med / 1e3) / 1e9,
                    "index_build_s": round(devs[q][1], 3), "n": int(devs[q][2].n), "n_runs": int(devs[q][2].n_runs),
-                   "device_MB": devs[q][2].device_bytes / 1e6, "counts_match_first": checks[(q, m, b, g, il)] == ref_check}
+                   "device_MB": devs[q][2].device_bytes / 1e6, "counts_match_first": checks[(q, m, b, g, il, sp)] == ref_check, "sparse_prefix": sp}
             print(json.dumps(out), flush=True)
         if a.ref_pass:
             for q, (dev, _, info) in devs.items():

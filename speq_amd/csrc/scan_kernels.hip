@@ -54,6 +54,8 @@ struct DevView {
     const uint16_t* run_label;
     const uint32_t* lab;     // per SA position {group | min(run_end - i, 65535) << 16}, or null
     const uint2* prefix;     // 4^q intervals (or null)
+    const uint4* pfx_rank;   // sparse form of `prefix` (or null): {count, 96-bit presence} per 96 codes ...
+    const uint2* pfx_iv;     // ... and the intervals of the present codes only, in code order
     uint32_t n, q, G, nb;
 };
 
@@ -138,6 +140,27 @@ __device__ __forceinline__ T ld_stream(const T* p) {
 #else
     return *p;
 #endif
+}
+// q-mer interval of `code`: dense table, or (when 4^q is much larger than the number of distinct q-mers) a presence
+// bitvector with ranks, L2-resident, plus the intervals of the present q-mers only. Absent q-mer: empty interval.
+__device__ __forceinline__ uint2 ld_prefix(const uint2* p);
+__device__ __forceinline__ uint2 prefix_lookup(const DevView& I, uint32_t code) {
+    if (I.pfx_rank != nullptr) {
+        const uint32_t b = code / 96u, r = code - b * 96u;
+        const uint4 e = I.pfx_rank[b];
+        const uint32_t word = r < 32u ? e.y : (r < 64u ? e.z : e.w);
+        if (!((word >> (r & 31u)) & 1u)) return make_uint2(0u, 0u);
+        const uint32_t bits[3] = {e.y, e.z, e.w};
+        uint32_t c = e.x;
+#pragma unroll
+        for (uint32_t w = 0; w < 3; ++w) {
+            const uint32_t lo = w * 32u;
+            if (r >= lo + 32u) c += __popc(bits[w]);
+            else if (r > lo) c += __popc(bits[w] & ((1u << (r - lo)) - 1u));
+        }
+        return I.pfx_iv[c];
+    }
+    return ld_prefix(I.prefix + code);
 }
 __device__ __forceinline__ uint2 ld_prefix(const uint2* p) {
 #if SPEQ_NT_PREFIX
@@ -224,7 +247,7 @@ __device__ __forceinline__ int search_lds(const DevView& I, const Rsrc& R, const
             code = (code << 2) | (c & 3u);
         }
         if (!bad) {
-            const uint2 e = ld_prefix(I.prefix + code);
+            const uint2 e = prefix_lookup(I, code);
             lo = e.x;
             hi = e.y;
             s -= (int32_t)I.q;
@@ -299,7 +322,7 @@ __device__ __forceinline__ void search_packed_n(const DevView& I, const Rsrc& R,
 #pragma unroll
         for (int w = 0; w < NW; ++w) {
             if (act[w]) {
-                const uint2 e = ld_prefix(I.prefix + (uint32_t)(P[w] & qmask));
+                const uint2 e = prefix_lookup(I, (uint32_t)(P[w] & qmask));
                 lo[w] = e.x;
                 hi[w] = e.y;
             }
@@ -723,6 +746,10 @@ struct speq_device_index {
     uint32_t ilp_local = 1;       // the same for Phred-weighted scans (NWIN = 2 is slower there: sweep_local.jsonl)
     uint32_t n_cus = 256;
     const uint2* prefix_level[3] = {nullptr, nullptr, nullptr};  // q-mer tables for q, q-1, q-2
+    const uint4* sparse_rank[3] = {nullptr, nullptr, nullptr};    // their sparse forms (see prefix_lookup)
+    const uint2* sparse_iv[3] = {nullptr, nullptr, nullptr};
+    uint64_t present[3] = {0, 0, 0};                              // distinct q-mers per level
+    int sparse_choice = -1;       // tuning "sparse_prefix": -1 auto (sparse when < 1/8 of the codes occur), 0, 1
     int prefix_choice = -1;       // tuning "prefix_level": -1 = by k (view_for_k), 0..2 = force q - level
     uint32_t base_q = 0;          // the index's prefix_q
     std::mutex events_mu;  // launches may come from several host threads (pipelines, concurrent scans)
@@ -772,6 +799,18 @@ void allow_big_lds_all() {
 // The q-mer table level for a scan of k-mers: the longest of q, q-1, q-2 that leaves a number of symbols divisible
 // by the widest LF step (3 with occ3, 2 with occ2), so the search needs no leftover single/pair step; any level
 // gives the same intervals (tests/test_gpu_parity.py runs each).
+void use_sparse(const speq_device_index* d, uint32_t lvl, DevView& v) {
+    v.pfx_rank = nullptr;
+    v.pfx_iv = nullptr;
+    if (d->sparse_rank[lvl] == nullptr) return;
+    const uint64_t codes = uint64_t(1) << (2 * (d->base_q - lvl));
+    const bool sparse = d->sparse_choice == 1 || (d->sparse_choice < 0 && d->present[lvl] * 8 < codes);
+    if (sparse) {
+        v.pfx_rank = d->sparse_rank[lvl];
+        v.pfx_iv = d->sparse_iv[lvl];
+    }
+}
+
 DevView view_for_k(const speq_device_index* d, uint32_t k) {
     DevView v = d->view;
     const uint32_t q = d->base_q;
@@ -783,16 +822,20 @@ DevView view_for_k(const speq_device_index* d, uint32_t k) {
         if (qq <= k && (k - qq) % step == 0) {
             v.q = qq;
             v.prefix = d->prefix_level[lvl];
+            use_sparse(d, lvl, v);
             return v;
         }
     }
+    use_sparse(d, 0, v);
     return v;
 }
 
 template <int MODE, bool PAIRED, bool LDS>
 void launch_t(const speq_device_index* d, const UnitSrc& src, uint32_t grid, size_t lds, hipStream_t st,
               unsigned long long* a, unsigned long long* b, double* w) {
-    const DevView v = d->prefix_choice >= 0 ? d->view : view_for_k(d, src.k);
+    DevView v = d->view;
+    if (d->prefix_choice >= 0) use_sparse(d, (uint32_t)d->prefix_choice, v);
+    else v = view_for_k(d, src.k);
     if (MODE != KM_REF && src.em_mult != nullptr)
         hipLaunchKernelGGL((k_scan<MODE, PAIRED, LDS, 1, MODE != KM_REF>), dim3(grid), dim3(BLOCK_THREADS), lds, st,
                            v, src, a, b, w);
@@ -910,12 +953,41 @@ int speq_device_open(const speq_index* idx, int device, speq_device_index** out)
         d->prefix_level[0] = v.prefix;
         d->prefix_level[1] = reinterpret_cast<const uint2*>(dev_upload(fm.prefix1));
         d->prefix_level[2] = reinterpret_cast<const uint2*>(dev_upload(fm.prefix2));
+        {
+            const std::vector<uint32_t>* tabs[3] = {&fm.prefix, &fm.prefix1, &fm.prefix2};
+            for (int lvl = 0; lvl < 3; ++lvl) {
+                const std::vector<uint32_t>& t = *tabs[lvl];
+                if (t.empty()) continue;
+                const uint64_t Q = t.size() / 2, nbk = Q / 96 + 1;
+                std::vector<speq::OccEntry> rk(nbk, speq::OccEntry{});
+                std::vector<uint32_t> iv;
+                uint32_t cnt = 0;
+                for (uint64_t c = 0; c < Q; ++c) {
+                    if (c % 96 == 0) rk[c / 96].count = cnt;
+                    if (t[2 * c] < t[2 * c + 1]) {
+                        rk[c / 96].bits[(c % 96) / 32] |= 1u << (c % 32);
+                        iv.push_back(t[2 * c]);
+                        iv.push_back(t[2 * c + 1]);
+                        ++cnt;
+                    }
+                }
+                if (Q % 96 == 0) rk[nbk - 1].count = cnt;
+                d->present[lvl] = cnt;
+                if (iv.empty()) iv.assign(2, 0u);
+                d->sparse_rank[lvl] = reinterpret_cast<const uint4*>(dev_upload(rk));
+                d->sparse_iv[lvl] = reinterpret_cast<const uint2*>(dev_upload(iv));
+            }
+        }
         v.n = (uint32_t)fm.n;
         v.q = fm.prefix_q;
         d->base_q = fm.prefix_q;
         v.G = fm.n_groups;
-        d->allocs = {(void*)v.occ, (void*)v.occ2, (void*)v.occ3, (void*)v.runs, (void*)v.run_label, (void*)v.lab, (void*)v.prefix,
-                     (void*)d->prefix_level[1], (void*)d->prefix_level[2]};
+        for (int lvl = 0; lvl < 3; ++lvl) {
+            d->allocs.push_back((void*)d->sparse_rank[lvl]);
+            d->allocs.push_back((void*)d->sparse_iv[lvl]);
+        }
+        d->allocs.insert(d->allocs.end(), {(void*)v.occ, (void*)v.occ2, (void*)v.occ3, (void*)v.runs, (void*)v.run_label, (void*)v.lab, (void*)v.prefix,
+                     (void*)d->prefix_level[1], (void*)d->prefix_level[2]});
         d->d_text = dev_upload(fm.text);
         d->d_text_start = dev_upload(fm.text_start);
         d->d_text_group = dev_upload(fm.text_group);
@@ -1109,6 +1181,9 @@ int speq_device_set_tuning(speq_device_index* d, const char* key, int64_t value)
         } else if (k == "grid_blocks") {
             if (value < 1 || value > (1 << 20)) throw std::invalid_argument("grid_blocks must be in [1, 2^20]");
             d->grid_blocks = (uint32_t)value;
+        } else if (k == "sparse_prefix") {
+            if (value < -1 || value > 1) throw std::invalid_argument("sparse_prefix must be -1 (auto), 0 or 1");
+            d->sparse_choice = (int)value;
         } else if (k == "prefix_level") {
             if (value < -1 || value > 2) throw std::invalid_argument("prefix_level must be -1 (auto) or 0..2");
             if (value >= 0 && (d->prefix_level[value] == nullptr && value > 0))
@@ -1131,6 +1206,7 @@ int speq_device_get_tuning(const speq_device_index* d, const char* key, int64_t*
         else if (k == "ilp_local") *value = d->ilp_local;
         else if (k == "grid_blocks") *value = d->grid_blocks;
         else if (k == "prefix_level") *value = d->prefix_choice;
+        else if (k == "sparse_prefix") *value = d->sparse_choice;
         else throw std::invalid_argument("speq_device_get_tuning: unknown key " + k);
     });
 }

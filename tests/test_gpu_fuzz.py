@@ -29,7 +29,8 @@ def test_random_configurations(seed):
     dev = DeviceIndex(idx)
     dev.tune(ilp=int(rng.integers(1, 3)), ilp_local=int(rng.integers(1, 3)),
              blocks_per_cu=int(rng.choice([0, 2, 4])), grid_blocks=int(rng.choice([7, 64, 16384])),
-             prefix_level=int(rng.choice([-1, 0, 1, 2])) if q >= 3 else -1)
+             prefix_level=int(rng.choice([-1, 0, 1, 2])) if q >= 3 else -1,
+             sparse_prefix=int(rng.choice([-1, 0, 1])))
     paired = bool(rng.random() < 0.4)
     reads = synth.make_reads(ref, int(rng.integers(50, 1500)), read_len=int(rng.integers(20, 250)),
                              paired=paired, fragment=int(rng.integers(250, 600)), n_rate=0.003,
