@@ -252,7 +252,9 @@ void speq_groupings_free(speq_groupings* g);
  * "ilp"          : k-mer windows each lane searches concurrently, 1 or 2 (default 2 for indexes of < 4 M
  *                  symbols, else 1); "ilp_local" the same for Phred-weighted scans (default 1);
  * "prefix_level" : q-mer table used by scans: -1 (default) picks, per k, the longest of q, q-1, q-2 that leaves a
- *                  multiple of the widest LF step; 0..2 forces table q - level (results never change). */
+ *                  multiple of the widest LF step; 0..2 forces table q - level (results never change);
+ * "sparse_prefix": 0 (default) dense q-mer tables; 1 a presence bitvector with ranks + the present intervals
+ *                  (less memory, one more dependent load per window); -1 sparse when < 1/8 of the codes occur. */
 int speq_device_set_tuning(speq_device_index* d, const char* key, int64_t value);
 int speq_device_get_tuning(const speq_device_index* d, const char* key, int64_t* value);
 

@@ -749,7 +749,9 @@ struct speq_device_index {
     const uint4* sparse_rank[3] = {nullptr, nullptr, nullptr};    // their sparse forms (see prefix_lookup)
     const uint2* sparse_iv[3] = {nullptr, nullptr, nullptr};
     uint64_t present[3] = {0, 0, 0};                              // distinct q-mers per level
-    int sparse_choice = -1;       // tuning "sparse_prefix": -1 auto (sparse when < 1/8 of the codes occur), 0, 1
+    int sparse_choice = 0;        // tuning "sparse_prefix": 0 dense (default), 1 sparse, -1 sparse when < 1/8 of
+                                  // the codes occur. Dense wins: the sparse form saves fabric bytes but adds a
+                                  // dependent load to every window (cfg 2: 4.63 -> 5.39 ms, sweep_sparse.jsonl)
     int prefix_choice = -1;       // tuning "prefix_level": -1 = by k (view_for_k), 0..2 = force q - level
     uint32_t base_q = 0;          // the index's prefix_q
     std::mutex events_mu;  // launches may come from several host threads (pipelines, concurrent scans)

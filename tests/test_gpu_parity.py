@@ -90,14 +90,14 @@ def test_prefix_levels_agree(edge, steps):
     dev = DeviceIndex(idx)
     for k in (5, 7, 8, 9, 10, 11, 21, 31, 70):
         orc = Oracle(ref.records, ref.groups, 4, k)
-        for lvl, sparse in ((-1, -1), (0, 0), (0, 1), (1, 1), (2, 0), (2, 1), (-1, 1)):
+        for lvl, sparse in ((-1, 0), (0, 0), (0, 1), (1, 1), (2, 0), (2, 1), (-1, 1), (-1, -1)):
             dev.tune(prefix_level=lvl, sparse_prefix=sparse)
             assert dev.tuning("prefix_level") == lvl and dev.tuning("sparse_prefix") == sparse
             _check_one(dev, orc, reads, k, 30, False, False)
             u, t = dev.count_unique_kmers_per_group(k)
             ou, ot = orc.ref_unique()
             assert np.array_equal(u, ou) and np.array_equal(t, ot), (k, lvl)
-    dev.tune(prefix_level=-1, sparse_prefix=-1)
+    dev.tune(prefix_level=-1, sparse_prefix=0)
 
 
 @pytest.mark.parametrize("local", [False, True])
