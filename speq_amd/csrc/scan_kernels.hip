@@ -730,7 +730,13 @@ T* dev_upload(const std::vector<T>& v) {
 struct speq_device_index {
     int device = 0;
     DevView view{};
-    std::vector<void*> allocs;
+    std::vector<void*> allocs;  // every device allocation of the replica, freed by the destructor
+    template <typename T>
+    T* track(T* p) {
+        if (p) allocs.push_back((void*)p);
+        return p;
+    }
+    ~speq_device_index();
     uint8_t* d_text = nullptr;
     uint64_t* d_text_start = nullptr;
     int32_t* d_text_group = nullptr;
@@ -944,17 +950,17 @@ int speq_device_open(const speq_index* idx, int device, speq_device_index** out)
         d->n_texts = fm.n_texts;
         d->text_start = fm.text_start;
         DevView& v = d->view;
-        v.occ = reinterpret_cast<const uint4*>(dev_upload(fm.occ));
+        v.occ = reinterpret_cast<const uint4*>(d->track(dev_upload(fm.occ)));
         v.nb = (uint32_t)fm.n_blocks();
-        v.occ2 = reinterpret_cast<const uint4*>(dev_upload(fm.occ2));
-        v.occ3 = reinterpret_cast<const uint4*>(dev_upload(fm.occ3));
-        v.runs = reinterpret_cast<const uint4*>(dev_upload(fm.runs));
-        v.run_label = dev_upload(fm.run_label);
-        v.lab = dev_upload(fm.lab);
-        v.prefix = reinterpret_cast<const uint2*>(dev_upload(fm.prefix));
+        v.occ2 = reinterpret_cast<const uint4*>(d->track(dev_upload(fm.occ2)));
+        v.occ3 = reinterpret_cast<const uint4*>(d->track(dev_upload(fm.occ3)));
+        v.runs = reinterpret_cast<const uint4*>(d->track(dev_upload(fm.runs)));
+        v.run_label = d->track(dev_upload(fm.run_label));
+        v.lab = d->track(dev_upload(fm.lab));
+        v.prefix = reinterpret_cast<const uint2*>(d->track(dev_upload(fm.prefix)));
         d->prefix_level[0] = v.prefix;
-        d->prefix_level[1] = reinterpret_cast<const uint2*>(dev_upload(fm.prefix1));
-        d->prefix_level[2] = reinterpret_cast<const uint2*>(dev_upload(fm.prefix2));
+        d->prefix_level[1] = reinterpret_cast<const uint2*>(d->track(dev_upload(fm.prefix1)));
+        d->prefix_level[2] = reinterpret_cast<const uint2*>(d->track(dev_upload(fm.prefix2)));
         {
             const std::vector<uint32_t>* tabs[3] = {&fm.prefix, &fm.prefix1, &fm.prefix2};
             for (int lvl = 0; lvl < 3; ++lvl) {
@@ -976,30 +982,20 @@ int speq_device_open(const speq_index* idx, int device, speq_device_index** out)
                 if (Q % 96 == 0) rk[nbk - 1].count = cnt;
                 d->present[lvl] = cnt;
                 if (iv.empty()) iv.assign(2, 0u);
-                d->sparse_rank[lvl] = reinterpret_cast<const uint4*>(dev_upload(rk));
-                d->sparse_iv[lvl] = reinterpret_cast<const uint2*>(dev_upload(iv));
+                d->sparse_rank[lvl] = reinterpret_cast<const uint4*>(d->track(dev_upload(rk)));
+                d->sparse_iv[lvl] = reinterpret_cast<const uint2*>(d->track(dev_upload(iv)));
             }
         }
         v.n = (uint32_t)fm.n;
         v.q = fm.prefix_q;
         d->base_q = fm.prefix_q;
         v.G = fm.n_groups;
-        for (int lvl = 0; lvl < 3; ++lvl) {
-            d->allocs.push_back((void*)d->sparse_rank[lvl]);
-            d->allocs.push_back((void*)d->sparse_iv[lvl]);
-        }
-        d->allocs.insert(d->allocs.end(), {(void*)v.occ, (void*)v.occ2, (void*)v.occ3, (void*)v.runs, (void*)v.run_label, (void*)v.lab, (void*)v.prefix,
-                     (void*)d->prefix_level[1], (void*)d->prefix_level[2]});
-        d->d_text = dev_upload(fm.text);
-        d->d_text_start = dev_upload(fm.text_start);
-        d->d_text_group = dev_upload(fm.text_group);
+        d->d_text = d->track(dev_upload(fm.text));
+        d->d_text_start = d->track(dev_upload(fm.text_start));
+        d->d_text_group = d->track(dev_upload(fm.text_group));
         std::vector<double> lut(QLUT_LEN);
         for (uint32_t q = 0; q < QLUT_LEN; ++q) lut[q] = 1.0 - 1.0 / std::pow(10.0, (double)q / 10.0);
-        d->d_qlut = dev_upload(lut);
-        d->allocs.push_back(d->d_text);
-        d->allocs.push_back(d->d_text_start);
-        d->allocs.push_back(d->d_text_group);
-        d->allocs.push_back(d->d_qlut);
+        d->d_qlut = d->track(dev_upload(lut));
         HIP_OK(hipStreamCreateWithFlags(&d->stream, hipStreamNonBlocking));
         hipDeviceProp_t prop;
         HIP_OK(hipGetDeviceProperties(&prop, device));
@@ -1027,18 +1023,22 @@ int speq_device_open(const speq_index* idx, int device, speq_device_index** out)
     });
 }
 
+speq_device_index::~speq_device_index() {
+    int prev = -1;
+    const bool switched = hipGetDevice(&prev) == hipSuccess && prev != device && hipSetDevice(device) == hipSuccess;
+    for (auto& e : events) {
+        (void)hipEventDestroy(e.first);
+        (void)hipEventDestroy(e.second);
+    }
+    for (void* p : allocs) (void)hipFree(p);
+    if (stream) (void)hipStreamDestroy(stream);
+    if (switched) (void)hipSetDevice(prev);
+}
+
 int speq_device_close(speq_device_index* d) {
     return speq::guarded([&] {
         if (!d) return;
         speq::release_host_pipelines(d);
-        DeviceGuard g(d->device);
-        for (auto& e : d->events) {
-            (void)hipEventDestroy(e.first);
-            (void)hipEventDestroy(e.second);
-        }
-        for (void* p : d->allocs)
-            if (p) (void)hipFree(p);
-        if (d->stream) (void)hipStreamDestroy(d->stream);
         delete d;
     });
 }
