@@ -279,3 +279,25 @@ def test_config3_index_vs_oracle():
     u, t = dev.count_unique_kmers_per_group(k)
     ou, ot = orc.ref_unique()
     assert np.array_equal(u, ou) and np.array_equal(t, ot)
+
+
+@pytest.mark.parametrize("paired", [False, True])
+def test_logical_shards_sum_to_unsharded(paired):
+    """S in {1, 2, 4, 8} logical shards of the bench's deterministic read stream (rank r scans
+    make_reads(start_index = r * n)), run one after another on one GPU, sum to the unsharded scan of all S * n reads
+    (the quantity the RCCL all-reduce forms across ranks)."""
+    ref = synth.make_reference(6, 2, 20_000)
+    dev = DeviceIndex(FmIndex.build(ref.records, ref.groups, 6, prefix_q=10, pair_steps=True, triple_steps=True,
+                                    label_table=True, gpu_device=0))
+    n = 4_000
+    whole = synth.make_reads(ref, 8 * n, paired=paired)
+    full = dev.scan(whole.seq.tobytes(), whole.qual.tobytes(), whole.offsets, k=21, paired=paired, local=True)
+    for S in (1, 2, 4, 8):
+        per = 8 * n // S
+        tot, amb, U, W = 0, 0, np.zeros(6, np.uint64), np.zeros(6)
+        for r in range(S):
+            sh = synth.make_reads(ref, per, start_index=r * per, paired=paired)
+            g = dev.scan(sh.seq.tobytes(), sh.qual.tobytes(), sh.offsets, k=21, paired=paired, local=True)
+            tot, amb, U, W = tot + g.total, amb + g.ambiguous, U + g.unique, W + g.weights
+        assert (tot, amb, U.tolist()) == (full.total, full.ambiguous, full.unique.tolist()), S
+        np.testing.assert_allclose(W, full.weights, rtol=1e-12)
