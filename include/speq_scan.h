@@ -254,7 +254,9 @@ void speq_groupings_free(speq_groupings* g);
  * "prefix_level" : q-mer table used by scans: -1 (default) picks, per k, the longest of q, q-1, q-2 that leaves a
  *                  multiple of the widest LF step; 0..2 forces table q - level (results never change);
  * "sparse_prefix": 0 (default) dense q-mer tables; 1 a presence bitvector with ranks + the present intervals
- *                  (less memory, one more dependent load per window); -1 sparse when < 1/8 of the codes occur. */
+ *                  (less memory, one more dependent load per window); -1 sparse when < 1/8 of the codes occur;
+ * "fastq_gpu_parse": 1 (default) speq_scan_fastq parses blocks of simple four-line records on the GPU (raw text
+ *                  to HBM); 0 parses every block on host threads. Results are identical. */
 int speq_device_set_tuning(speq_device_index* d, const char* key, int64_t value);
 int speq_device_get_tuning(const speq_device_index* d, const char* key, int64_t* value);
 

@@ -164,7 +164,7 @@ ScanResult scan_record(const char* data, size_t len, size_t pos, bool eof, size_
 // Four-line record (@header / bases / '+' / qualities of the same raw length) found with four memchr and no
 // per-byte work; anything else (blank lines, wrapped records, CR-only oddities) goes through scan_record. The
 // parser re-checks every record against the general grammar (parse_record), so a fast cut never changes results.
-inline bool fast_record(const char* data, size_t len, size_t pos, bool eof, size_t& end) {
+inline bool fast_record(const char* data, size_t len, size_t pos, bool eof, size_t& end, size_t& seq_len) {
     if (pos >= len || data[pos] != '@') return false;
     size_t nl[4];
     size_t p = pos;
@@ -187,6 +187,7 @@ inline bool fast_record(const char* data, size_t len, size_t pos, bool eof, size
     const size_t l2 = trimmed(nl[0] + 1, nl[1]), l4 = trimmed(nl[2] + 1, nl[3]);
     if (l2 != l4 || trimmed(pos, nl[0]) == 0) return false;
     end = p;
+    seq_len = l2;
     return true;
 }
 
@@ -208,6 +209,8 @@ struct Block {
     std::shared_ptr<Buf> buf;
     size_t begin = 0, end = 0;
     uint64_t n = 0;
+    bool simple = true;   // every record took the four-line fast path (eligible for GPU parsing)
+    uint64_t bases = 0;   // raw base-line bytes of those records
     const char* data() const { return buf ? buf->data() + begin : nullptr; }
     size_t size() const { return end - begin; }
 };
@@ -236,28 +239,31 @@ public:
     }
     // Up to max_records complete records, stopping after the record that reaches max_bytes.
     Block next(uint64_t max_records, uint64_t max_bytes) {
-        uint64_t n = 0;
+        uint64_t n = 0, bases = 0;
+        bool simple = true;
         if (!cur_) grow(0);
         size_t pos = pos_;
         while (n < max_records && (n == 0 || pos - pos_ < max_bytes)) {
             const char* data = cur_->data();
-            size_t end = 0;
-            if (fast_record(data, cur_->len, pos, eof_, end)) {
+            size_t end = 0, seq_len = 0;
+            if (fast_record(data, cur_->len, pos, eof_, end, seq_len)) {
                 pos = end;
                 ++n;
+                bases += seq_len;
                 continue;
             }
             const ScanResult r = scan_record(data, cur_->len, pos, eof_, end, src_.path());
             if (r == REC_COMPLETE) {
                 pos = end;
                 ++n;
+                simple = false;
             } else if (r == REC_NONE) {
                 break;
             } else {
                 pos = refill(pos);
             }
         }
-        Block blk{cur_, pos_, pos, n};
+        Block blk{cur_, pos_, pos, n, simple, bases};
         pos_ = pos;
         return blk;
     }
@@ -371,6 +377,11 @@ struct Sink {
     virtual ~Sink() = default;
     virtual void acquire(speq_slot& s, uint64_t bytes, uint64_t records) = 0;
     virtual void submit(const speq_slot& s, uint64_t records) = 0;  // records == 0 releases the slot
+    // raw four-line FASTQ text (file 1's block, then file 2's) in s.seq, n records per file
+    virtual void submit_raw(const speq_slot& s, uint64_t len1, uint64_t len2, uint64_t n, bool paired) {
+        (void)s; (void)len1; (void)len2; (void)n; (void)paired;
+        throw std::logic_error("this sink does not parse raw FASTQ");
+    }
 };
 
 struct PipelineSink final : Sink {
@@ -387,6 +398,9 @@ struct PipelineSink final : Sink {
         }
     }
     void submit(const speq_slot& s, uint64_t records) override { check_rc(speq_pipeline_submit(pl, s.slot, records)); }
+    void submit_raw(const speq_slot& s, uint64_t len1, uint64_t len2, uint64_t n, bool paired) override {
+        speq::pipeline_submit_raw(pl, s.slot, len1, len2, n, paired);
+    }
 };
 
 // Order-independent digest of the parsed records (sum over records of a 64-bit hash of length, bases and
@@ -445,7 +459,7 @@ struct StreamTotals {
 };
 
 // Reader thread (cutting blocks of both files in step) + n_parsers parser threads feeding `sink`.
-StreamTotals run_stream(const char* path1, const char* path2, uint32_t threads, Sink& sink) {
+StreamTotals run_stream(const char* path1, const char* path2, uint32_t threads, Sink& sink, bool gpu_parse) {
     const bool paired = path2 != nullptr;
     const uint32_t n_parsers = std::max<uint32_t>(1, std::min<uint32_t>(threads ? threads : 1, 64));
     const uint64_t BLOCK_RECORDS = 1u << 15, BLOCK_BYTES = 12ull << 20;
@@ -498,6 +512,19 @@ StreamTotals run_stream(const char* path1, const char* path2, uint32_t threads, 
                 }
                 speq_slot s;
                 const uint64_t recs = paired ? 2 * w.n : w.n;
+                if (gpu_parse && w.b1.simple && w.n == w.b1.n && (!paired || (w.b2.simple && w.n == w.b2.n))) {
+                    // raw four-line text straight to HBM; records are split on the GPU (fastq_gpu.hip)
+                    const uint64_t l1 = w.b1.size(), l2 = w.b2.size();
+                    sink.acquire(s, l1 + l2, recs);
+                    std::memcpy(s.seq, w.b1.data(), l1);
+                    if (paired) std::memcpy(s.seq + l1, w.b2.data(), l2);
+                    sink.submit_raw(s, l1, l2, w.n, paired);
+                    sh.records += recs;
+                    sh.bases += w.b1.bases + w.b2.bases;
+                    sh.batches += 1;
+                    if (sh.failed) return;
+                    continue;
+                }
                 sink.acquire(s, w.b1.size() + w.b2.size(), recs);
                 uint64_t out = 0;
                 size_t p1 = 0, p2 = 0;
@@ -565,7 +592,7 @@ extern "C" int speq_scan_fastq(speq_device_index* d, const char* path1, const ch
         PipelineSink sink(pl);
         StreamTotals tot;
         try {
-            tot = run_stream(path1, path2, threads, sink);
+            tot = run_stream(path1, path2, threads, sink, speq::device_fastq_gpu(d));
         } catch (...) {
             std::vector<uint64_t> scratch(SPEQ_COUNTS_LEN(speq::device_groups(d)));
             std::vector<double> wscratch(std::max<uint32_t>(speq::device_groups(d), 1));
@@ -588,7 +615,7 @@ extern "C" int speq_fastq_checksum(const char* path1, const char* path2, uint32_
     return speq::guarded([&] {
         if (!path1 || !records || !bases || !digest) throw std::invalid_argument("speq_fastq_checksum: null argument");
         ChecksumSink sink;
-        const StreamTotals tot = run_stream(path1, path2, threads, sink);
+        const StreamTotals tot = run_stream(path1, path2, threads, sink, false);
         *records = tot.records;
         *bases = tot.bases;
         *digest = sink.digest.load();

@@ -51,7 +51,26 @@ struct Slot {
     uint64_t cap_bytes = 0, cap_records = 0;
     hipEvent_t copied = nullptr, done = nullptr;
     bool pending = false;  // `done` recorded and not yet waited for
+    // GPU FASTQ parsing (raw submits): parsed bases/qualities/offsets and scratch, allocated on first use
+    uint8_t* d_pseq = nullptr;
+    uint8_t* d_pqual = nullptr;
+    uint64_t* d_poff = nullptr;
+    void* d_scratch = nullptr;
+    uint64_t parse_bytes = 0, parse_slots = 0;
+    size_t scratch_bytes = 0;
 };
+
+void free_parse(Slot& s) {
+    if (s.d_pseq) (void)hipFree(s.d_pseq);
+    if (s.d_pqual) (void)hipFree(s.d_pqual);
+    if (s.d_poff) (void)hipFree(s.d_poff);
+    if (s.d_scratch) (void)hipFree(s.d_scratch);
+    s.d_pseq = s.d_pqual = nullptr;
+    s.d_poff = nullptr;
+    s.d_scratch = nullptr;
+    s.parse_bytes = s.parse_slots = 0;
+    s.scratch_bytes = 0;
+}
 
 void free_buffers(Slot& s) {
     if (s.h_seq) (void)hipHostFree(s.h_seq);
@@ -96,12 +115,15 @@ struct speq_pipeline {
     std::condition_variable cv;
     std::deque<int> free_slots;
     std::mutex submit_mu;       // stream order of copies and launches
+    uint32_t* d_err = nullptr;  // GPU FASTQ parse errors (bit flags), checked by finish
 
     ~speq_pipeline() {
         if (compute) (void)hipStreamSynchronize(compute);
         if (copy) (void)hipStreamSynchronize(copy);
+        if (d_err) (void)hipFree(d_err);
         for (Slot& s : slots) {
             free_buffers(s);
+            free_parse(s);
             if (s.copied) (void)hipEventDestroy(s.copied);
             if (s.done) (void)hipEventDestroy(s.done);
         }
@@ -136,6 +158,8 @@ int speq_pipeline_create(speq_device_index* d, const speq_scan_params* params, s
         hip_ok(hipStreamCreateWithFlags(&pl->compute, hipStreamNonBlocking), "hipStreamCreate");
         hip_ok(hipMalloc(reinterpret_cast<void**>(&pl->d_counts), SPEQ_COUNTS_LEN(pl->G) * 8), "hipMalloc");
         hip_ok(hipMemsetAsync(pl->d_counts, 0, SPEQ_COUNTS_LEN(pl->G) * 8, pl->compute), "hipMemset");
+        hip_ok(hipMalloc(reinterpret_cast<void**>(&pl->d_err), 16), "hipMalloc");
+        hip_ok(hipMemsetAsync(pl->d_err, 0, 16, pl->compute), "hipMemset");
         hip_ok(hipMalloc(reinterpret_cast<void**>(&pl->d_w), std::max<uint32_t>(pl->G, 1) * 8), "hipMalloc");
         hip_ok(hipMemsetAsync(pl->d_w, 0, std::max<uint32_t>(pl->G, 1) * 8, pl->compute), "hipMemset");
         pl->slots.resize(n_slots);
@@ -233,6 +257,57 @@ int speq_pipeline_submit(speq_pipeline* pl, int32_t slot, uint64_t n_records) {
     return rc;
 }
 
+}  // extern "C"
+
+namespace speq {
+void pipeline_submit_raw(speq_pipeline* pl, int32_t slot, uint64_t len1, uint64_t len2, uint64_t n, bool paired) {
+    struct Release {
+        speq_pipeline* pl;
+        int32_t slot;
+        ~Release() {
+            {
+                std::lock_guard<std::mutex> lk(pl->mu);
+                pl->free_slots.push_back(slot);
+            }
+            pl->cv.notify_one();
+        }
+    } release{pl, slot};
+    if (slot < 0 || (size_t)slot >= pl->slots.size()) throw std::invalid_argument("pipeline_submit_raw: bad slot");
+    Slot& s = pl->slots[(size_t)slot];
+    if (n == 0) return;
+    if (len1 + len2 > s.cap_bytes) throw std::invalid_argument("pipeline_submit_raw: raw bytes exceed the slot");
+    if ((bool)pl->p.paired != paired) throw std::invalid_argument("pipeline_submit_raw: paired mismatch");
+    const uint64_t n_slots = paired ? 2 * n : n;
+    DevScope g(pl->device);
+    // parse buffers: bases <= raw bytes; the slot was acquired, so nothing in flight uses them
+    const size_t need_scratch = fastq_gpu_scratch_bytes(std::max(len1, len2), n, paired);
+    if (len1 + len2 > s.parse_bytes || n_slots > s.parse_slots || need_scratch > s.scratch_bytes) {
+        const uint64_t pb = std::max(len1 + len2, s.parse_bytes), ps = std::max(n_slots, s.parse_slots);
+        const size_t sb = std::max(need_scratch, s.scratch_bytes);
+        free_parse(s);
+        hip_ok(hipMalloc(reinterpret_cast<void**>(&s.d_pseq), pb), "hipMalloc");
+        hip_ok(hipMalloc(reinterpret_cast<void**>(&s.d_pqual), pb), "hipMalloc");
+        hip_ok(hipMalloc(reinterpret_cast<void**>(&s.d_poff), (ps + 1) * 8), "hipMalloc");
+        hip_ok(hipMalloc(&s.d_scratch, sb), "hipMalloc");
+        s.parse_bytes = pb;
+        s.parse_slots = ps;
+        s.scratch_bytes = sb;
+    }
+    std::lock_guard<std::mutex> lk(pl->submit_mu);
+    hip_ok(hipMemcpyAsync(s.d_seq, s.h_seq, len1 + len2, hipMemcpyHostToDevice, pl->copy), "hipMemcpyAsync");
+    hip_ok(hipEventRecord(s.copied, pl->copy), "hipEventRecord");
+    hip_ok(hipStreamWaitEvent(pl->compute, s.copied, 0), "hipStreamWaitEvent");
+    launch_fastq_parse(s.d_seq, len1, len2, n, paired, s.d_scratch, s.scratch_bytes, s.d_pseq, s.d_pqual, s.d_poff,
+                       pl->d_err, pl->compute);
+    launch_reads_scan(pl->d, s.d_pseq, s.d_pqual, s.d_poff, n_slots, &pl->p, pl->d_counts, pl->d_w,
+                      pl->em ? pl->em->d_mult : nullptr, pl->em ? pl->em->d_hi : nullptr, pl->compute);
+    hip_ok(hipEventRecord(s.done, pl->compute), "hipEventRecord");
+    s.pending = true;
+}
+}  // namespace speq
+
+extern "C" {
+
 int speq_pipeline_finish(speq_pipeline* pl, uint64_t* counts, double* weights) {
     return speq::guarded([&] {
         if (!pl || !counts) throw std::invalid_argument("speq_pipeline_finish: null argument");
@@ -246,7 +321,15 @@ int speq_pipeline_finish(speq_pipeline* pl, uint64_t* counts, double* weights) {
             hip_ok(hipMemcpyAsync(weights, pl->d_w, pl->G * 8, hipMemcpyDeviceToHost, pl->compute), "hipMemcpyAsync");
         hip_ok(hipMemsetAsync(pl->d_counts, 0, nc * 8, pl->compute), "hipMemsetAsync");
         if (pl->d_w) hip_ok(hipMemsetAsync(pl->d_w, 0, pl->G * 8, pl->compute), "hipMemsetAsync");
+        uint32_t err = 0;
+        hip_ok(hipMemcpyAsync(&err, pl->d_err, 4, hipMemcpyDeviceToHost, pl->compute), "hipMemcpyAsync");
+        hip_ok(hipMemsetAsync(pl->d_err, 0, 4, pl->compute), "hipMemsetAsync");
         hip_ok(hipStreamSynchronize(pl->compute), "hipStreamSynchronize");
+        if (err)
+            throw speq::IoError(std::string("malformed FASTQ record (GPU parse:") + ((err & 1) ? " header not '@'" : "") +
+                                ((err & 2) ? " separator not '+'" : "") +
+                                ((err & 4) ? " sequence/quality length mismatch" : "") +
+                                ((err & 8) ? " truncated record" : "") + ")");
     });
 }
 

@@ -21,6 +21,15 @@ speq_pipeline* acquire_cached_pipeline(speq_device_index* d, const speq_scan_par
 void return_cached_pipeline(speq_device_index* d, speq_pipeline* pl);
 // Frees the idle host-scan pipelines cached for a device (called by speq_device_close).
 void release_host_pipelines(const speq_device_index* d);
+// GPU FASTQ parsing (fastq_gpu.hip): scratch bytes for a block pair, and the asynchronous parse into k_scan's layout.
+size_t fastq_gpu_scratch_bytes(uint64_t raw_bytes, uint64_t records_per_file, bool paired);
+void launch_fastq_parse(const uint8_t* d_raw, uint64_t len1, uint64_t len2, uint64_t n, bool paired, void* d_scratch,
+                        size_t scratch_bytes, uint8_t* d_seq, uint8_t* d_qual, uint64_t* d_off, uint32_t* d_err,
+                        void* stream);
+// Submits an acquired pipeline slot whose host buffer holds RAW four-line FASTQ text (file 1's block, then file
+// 2's when paired, n records each): copied as is, parsed on the GPU, then scanned (pipeline.cpp).
+void pipeline_submit_raw(speq_pipeline* pl, int32_t slot, uint64_t len1, uint64_t len2, uint64_t n, bool paired);
+bool device_fastq_gpu(const speq_device_index* d);
 int device_ordinal(const speq_device_index* d);
 uint32_t device_groups(const speq_device_index* d);
 }  // namespace speq

@@ -755,6 +755,7 @@ struct speq_device_index {
     const uint4* sparse_rank[3] = {nullptr, nullptr, nullptr};    // their sparse forms (see prefix_lookup)
     const uint2* sparse_iv[3] = {nullptr, nullptr, nullptr};
     uint64_t present[3] = {0, 0, 0};                              // distinct q-mers per level
+    bool fastq_gpu = true;        // tuning "fastq_gpu_parse": parse simple four-line FASTQ blocks on the GPU
     int sparse_choice = 0;        // tuning "sparse_prefix": 0 dense (default), 1 sparse, -1 sparse when < 1/8 of
                                   // the codes occur. Dense wins: the sparse form saves fabric bytes but adds a
                                   // dependent load to every window (cfg 2: 4.63 -> 5.39 ms, sweep_sparse.jsonl)
@@ -1183,6 +1184,9 @@ int speq_device_set_tuning(speq_device_index* d, const char* key, int64_t value)
         } else if (k == "grid_blocks") {
             if (value < 1 || value > (1 << 20)) throw std::invalid_argument("grid_blocks must be in [1, 2^20]");
             d->grid_blocks = (uint32_t)value;
+        } else if (k == "fastq_gpu_parse") {
+            if (value != 0 && value != 1) throw std::invalid_argument("fastq_gpu_parse must be 0 or 1");
+            d->fastq_gpu = value != 0;
         } else if (k == "sparse_prefix") {
             if (value < -1 || value > 1) throw std::invalid_argument("sparse_prefix must be -1 (auto), 0 or 1");
             d->sparse_choice = (int)value;
@@ -1209,6 +1213,7 @@ int speq_device_get_tuning(const speq_device_index* d, const char* key, int64_t*
         else if (k == "grid_blocks") *value = d->grid_blocks;
         else if (k == "prefix_level") *value = d->prefix_choice;
         else if (k == "sparse_prefix") *value = d->sparse_choice;
+        else if (k == "fastq_gpu_parse") *value = d->fastq_gpu ? 1 : 0;
         else throw std::invalid_argument("speq_device_get_tuning: unknown key " + k);
     });
 }
@@ -1251,5 +1256,6 @@ void launch_reads_scan(speq_device_index* d, const uint8_t* d_seq, const uint8_t
                      static_cast<hipStream_t>(stream));
 }
 int device_ordinal(const speq_device_index* d) { return d->device; }
+bool device_fastq_gpu(const speq_device_index* d) { return d->fastq_gpu; }
 uint32_t device_groups(const speq_device_index* d) { return d->G; }
 }  // namespace speq

@@ -170,3 +170,69 @@ def test_pipeline_rejects_bad_input():
     with pytest.raises(SpeqError, match="even"):
         pl.put(b"ACGT" * 3, b"IIII" * 3, np.array([0, 4, 8, 12], dtype=np.uint64))
     pl.close()
+
+
+@pytest.mark.parametrize("fmt", [dict(), dict(crlf=True), dict(gz=True)])
+@pytest.mark.parametrize("paired", [False, True])
+def test_gpu_fastq_parse_equals_host_parse(tmp_path, fmt, paired):
+    """Simple four-line blocks are split into records on the GPU (fastq_gpu.hip); the host parser (knob off) must
+    give the same counters, EM histogram and stream statistics."""
+    ref = synth.make_reference(4, 2, 20_000)
+    reads = synth.make_reads(ref, 60_000 // (2 if paired else 1), paired=paired, n_rate=0.001, lowq_rate=0.01,
+                             short_frac=0.0 if paired else 0.05)
+    seqs, quals = split(reads)
+    if paired:
+        write_fastq(tmp_path / "r1.fq", seqs[0::2], quals[0::2], **fmt)
+        write_fastq(tmp_path / "r2.fq", seqs[1::2], quals[1::2], **fmt)
+        p1, p2 = str(tmp_path / "r1.fq"), str(tmp_path / "r2.fq")
+    else:
+        write_fastq(tmp_path / "r1.fq", seqs, quals, **fmt)
+        p1, p2 = str(tmp_path / "r1.fq"), None
+    dev = DeviceIndex(FmIndex.build(ref.records, ref.groups, 4, prefix_q=10, pair_steps=True, triple_steps=True))
+    assert dev.tuning("fastq_gpu_parse") == 1
+    res = {}
+    for gpu in (1, 0):
+        dev.tune(fastq_gpu_parse=gpu)
+        for local in (False, True):
+            em = EmHistogram(dev)
+            r, st = dev.scan_fastq(p1, p2, k=21, local=local, threads=3, em=em)
+            em.finalize()
+            res[(gpu, local)] = (r, st, em.info(), em.step(np.full(4, 25.0), [2, 2, 2, 2], r.unique))
+    exp = dev.scan(reads.seq.tobytes(), reads.qual.tobytes(), reads.offsets, k=21, paired=paired)
+    for local in (False, True):
+        (a, sa, ia, na), (b, sb, ib, nb) = res[(1, local)], res[(0, local)]
+        same(a, b, local)
+        assert (sa["records"], sa["bases"]) == (sb["records"], sb["bases"]) == (reads.n, int(reads.offsets[-1]))
+        assert ia == ib
+        np.testing.assert_allclose(na, nb, rtol=1e-12)
+    same(res[(1, False)][0], exp, False)
+
+
+def test_gpu_fastq_parse_blanks_and_errors(tmp_path):
+    """Four-line records whose lines hold blanks (dropped) take the GPU path's compaction; a base/quality count
+    mismatch that only the character filter reveals is an error on both paths."""
+    ref = synth.make_reference(2, 1, 4_000)
+    dev = DeviceIndex(FmIndex.build(ref.records, ref.groups, 2, prefix_q=6, pair_steps=True, triple_steps=True))
+    rd = synth.make_reads(ref, 500, read_len=60)
+    seqs, quals = split(rd)
+    lines = []
+    for i, (s, q) in enumerate(zip(seqs, quals)):
+        s, q = s.decode(), q.decode()
+        if i % 3 == 0:  # one blank in each line: raw lengths stay equal, the filtered counts too
+            s, q = s[:10] + " " + s[10:], q[:20] + " " + q[20:]
+        lines.append(f"@r{i}\n{s}\n+\n{q}\n")
+    (tmp_path / "b.fq").write_text("".join(lines))
+    got = {}
+    for gpu in (1, 0):
+        dev.tune(fastq_gpu_parse=gpu)
+        got[gpu] = dev.scan_fastq(str(tmp_path / "b.fq"), k=19, threads=2)
+    same(got[1][0], got[0][0], False)
+    assert got[1][1]["records"] == 500
+    exp = dev.scan(rd.seq.tobytes(), rd.qual.tobytes(), rd.offsets, k=19)
+    same(got[1][0], exp, False)
+    (tmp_path / "bad.fq").write_text("@a\nACGTACGTAC\n+\nIIIIIIIIII\n@b\nACGT7\n+\nIIIII\n")
+    for gpu in (1, 0):
+        dev.tune(fastq_gpu_parse=gpu)
+        with pytest.raises(SpeqError, match="mismatch"):
+            dev.scan_fastq(str(tmp_path / "bad.fq"), k=3)
+    dev.tune(fastq_gpu_parse=1)
