@@ -586,7 +586,7 @@ extern "C" int speq_scan_fastq(speq_device_index* d, const char* path1, const ch
         const auto t0 = std::chrono::steady_clock::now();
         const uint32_t n_parsers = std::max<uint32_t>(1, std::min<uint32_t>(threads ? threads : 1, 64));
         std::unique_ptr<speq_pipeline, void (*)(speq_pipeline*)> pl_guard(
-            speq::acquire_cached_pipeline(d, params, em, 8ull << 20, paired ? 2u << 15 : 1u << 15, n_parsers + 2),
+            speq::acquire_cached_pipeline(d, params, em, 8ull << 20, paired ? 2u << 15 : 1u << 15, std::min<uint32_t>(n_parsers, 6) + 2),
             speq_pipeline_free);
         speq_pipeline* pl = pl_guard.get();
         PipelineSink sink(pl);
