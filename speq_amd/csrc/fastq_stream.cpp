@@ -24,6 +24,7 @@
 #include <condition_variable>
 #include <cstring>
 #include <deque>
+#include <memory>
 #include <mutex>
 #include <string>
 #include <thread>
@@ -37,14 +38,133 @@ namespace {
 using speq::IoError;
 
 // Decompressed byte source: plain files through read(2), gzip (magic 1f 8b) through zlib.
+// BGZF (blocked gzip, as written by bgzip): a series of independent gzip members whose headers carry the member size
+// ("BC" extra subfield) and whose footers carry the uncompressed size, so members can be inflated in parallel
+// straight into their final positions. Plain gzip streams have no such index and are inflated sequentially.
+class Bgzf {
+public:
+    Bgzf(const std::string& path, int fd, uint32_t threads) : path_(path), threads_(std::max<uint32_t>(1, threads)) {
+        struct stat st {};
+        if (::fstat(fd, &st) != 0) throw IoError("cannot stat " + path);
+        size_ = (size_t)st.st_size;
+        map_ = static_cast<const uint8_t*>(::mmap(nullptr, size_, PROT_READ, MAP_PRIVATE, fd, 0));
+        if (map_ == MAP_FAILED) {
+            map_ = nullptr;
+            throw IoError("cannot map " + path);
+        }
+        (void)::madvise((void*)map_, size_, MADV_SEQUENTIAL);
+    }
+    ~Bgzf() {
+        if (map_) ::munmap((void*)map_, size_);
+    }
+    // True when the file starts with a BGZF member header.
+    static bool is_bgzf(const uint8_t* h, size_t n) {
+        if (n < 18 || h[0] != 0x1f || h[1] != 0x8b || h[2] != 8 || !(h[3] & 4)) return false;
+        const size_t xlen = h[10] | (h[11] << 8);
+        for (size_t i = 12; i + 4 <= 12 + xlen && i + 4 <= n;) {
+            const size_t slen = h[i + 2] | (h[i + 3] << 8);
+            if (h[i] == 'B' && h[i + 1] == 'C' && slen == 2) return true;
+            i += 4 + slen;
+        }
+        return false;
+    }
+    // Inflates the next members whose uncompressed sizes fit in n bytes (at least one) into dst, in parallel.
+    size_t read(char* dst, size_t n) {
+        struct Member {
+            size_t cpos, csize, dpos, dsize;
+        };
+        std::vector<Member> batch;
+        size_t out = 0;
+        while (pos_ < size_) {
+            const Next m = next_member(pos_);
+            if (!batch.empty() && out + m.dsize > n) break;
+            if (m.dsize > n) throw IoError("BGZF member larger than the read buffer in " + path_);
+            batch.push_back({m.cpos, m.csize, out, m.dsize});
+            out += m.dsize;
+            pos_ += m.csize;
+        }
+        if (batch.empty()) return 0;
+        std::atomic<size_t> next{0};
+        std::atomic<bool> bad{false};
+        auto work = [&] {
+            z_stream z;
+            std::memset(&z, 0, sizeof(z));
+            if (inflateInit2(&z, -15) != Z_OK) {
+                bad = true;
+                return;
+            }
+            for (size_t i; (i = next++) < batch.size() && !bad;) {
+                const Member& m = batch[i];
+                const uint8_t* h = map_ + m.cpos;
+                const size_t xlen = h[10] | (h[11] << 8);
+                const size_t hdr = 12 + xlen;
+                if (m.csize < hdr + 8) {
+                    bad = true;
+                    break;
+                }
+                (void)inflateReset(&z);
+                z.next_in = const_cast<Bytef*>(h + hdr);
+                z.avail_in = (uInt)(m.csize - hdr - 8);
+                z.next_out = reinterpret_cast<Bytef*>(dst + m.dpos);
+                z.avail_out = (uInt)m.dsize;
+                const int rc = inflate(&z, Z_FINISH);
+                const uint8_t* f = h + m.csize - 8;
+                const uint32_t crc = f[0] | (f[1] << 8) | (f[2] << 16) | ((uint32_t)f[3] << 24);
+                if (rc != Z_STREAM_END || z.total_out != m.dsize ||
+                    crc32(0L, reinterpret_cast<const Bytef*>(dst + m.dpos), (uInt)m.dsize) != crc)
+                    bad = true;
+            }
+            inflateEnd(&z);
+        };
+        const uint32_t t = (uint32_t)std::min<size_t>(threads_, batch.size());
+        std::vector<std::thread> pool;
+        for (uint32_t i = 1; i < t; ++i) pool.emplace_back(work);
+        work();
+        for (auto& th : pool) th.join();
+        if (bad) throw IoError("corrupt BGZF member in " + path_);
+        return out;
+    }
+
+private:
+    struct Next {
+        size_t cpos, csize, dsize;
+    };
+    Next next_member(size_t p) const {
+        const uint8_t* h = map_ + p;
+        if (size_ - p < 18 || h[0] != 0x1f || h[1] != 0x8b || h[2] != 8 || !(h[3] & 4))
+            throw IoError("not a BGZF member at byte " + std::to_string(p) + " of " + path_);
+        const size_t xlen = h[10] | (h[11] << 8);
+        size_t bsize = 0;
+        for (size_t i = 12; i + 4 <= 12 + xlen;) {
+            const size_t slen = h[i + 2] | (h[i + 3] << 8);
+            if (h[i] == 'B' && h[i + 1] == 'C' && slen == 2) bsize = (size_t)(h[i + 4] | (h[i + 5] << 8)) + 1;
+            i += 4 + slen;
+        }
+        if (bsize < 12 + xlen + 8 || p + bsize > size_) throw IoError("corrupt BGZF header in " + path_);
+        const uint8_t* f = h + bsize - 4;
+        const size_t isize = f[0] | (f[1] << 8) | (f[2] << 16) | ((size_t)f[3] << 24);
+        return {p, bsize, isize};
+    }
+    std::string path_;
+    uint32_t threads_;
+    const uint8_t* map_ = nullptr;
+    size_t size_ = 0, pos_ = 0;
+};
+
+// Decompressed byte source: plain files through read(2), BGZF through parallel member inflation, other gzip
+// (magic 1f 8b) through zlib.
 class Source {
 public:
-    explicit Source(const std::string& path) : path_(path) {
+    explicit Source(const std::string& path, uint32_t threads = 1) : path_(path) {
         fd_ = ::open(path.c_str(), O_RDONLY);
         if (fd_ < 0) throw IoError("cannot open reads file " + path);
-        unsigned char magic[2] = {0, 0};
-        const ssize_t m = ::pread(fd_, magic, 2, 0);
-        if (m == 2 && magic[0] == 0x1f && magic[1] == 0x8b) {
+        unsigned char head[64] = {0};
+        const ssize_t m = ::pread(fd_, head, sizeof(head), 0);
+        if (m >= 2 && head[0] == 0x1f && head[1] == 0x8b) {
+            if (Bgzf::is_bgzf(head, (size_t)m)) {
+                bgzf_ = std::make_unique<Bgzf>(path, fd_, threads);
+                return;
+            }
             gz_ = gzdopen(fd_, "rb");
             if (!gz_) throw IoError("cannot open gzip stream " + path);
             fd_ = -1;  // owned by gz_
@@ -54,10 +174,20 @@ public:
         }
     }
     ~Source() {
+        bgzf_.reset();
         if (gz_) gzclose(gz_);
         if (fd_ >= 0) ::close(fd_);
     }
     size_t read(char* dst, size_t n) {
+        if (bgzf_) {
+            size_t got = 0;
+            while (got < n) {
+                const size_t r = bgzf_->read(dst + got, n - got);
+                if (r == 0) break;
+                got += r;
+            }
+            return got;
+        }
         size_t got = 0;
         while (got < n) {
             const size_t want = std::min<size_t>(n - got, 1u << 30);
@@ -83,12 +213,13 @@ public:
         return got;
     }
     const std::string& path() const { return path_; }
-    bool plain() const { return gz_ == nullptr; }
+    bool plain() const { return gz_ == nullptr && !bgzf_; }
     int fd() const { return fd_; }
 
 private:
     int fd_ = -1;
     gzFile gz_ = nullptr;
+    std::unique_ptr<Bgzf> bgzf_;
     std::string path_;
 };
 
@@ -220,7 +351,7 @@ class Cutter {
 public:
     // Plain files are mapped whole (no read copies; parsers read the page cache directly); gzip is inflated into
     // 64 MiB buffers.
-    explicit Cutter(const std::string& path) : src_(path) {
+    explicit Cutter(const std::string& path, uint32_t threads = 1) : src_(path, threads) {
         if (!src_.plain()) return;
         struct stat st {};
         if (::fstat(src_.fd(), &st) != 0 || !S_ISREG(st.st_mode)) return;  // pipes etc.: read path
@@ -464,9 +595,9 @@ StreamTotals run_stream(const char* path1, const char* path2, uint32_t threads, 
     const uint32_t n_parsers = std::max<uint32_t>(1, std::min<uint32_t>(threads ? threads : 1, 64));
     const uint64_t BLOCK_RECORDS = 1u << 15, BLOCK_BYTES = 12ull << 20;
     // opened here so that a missing file fails before any thread starts
-    Cutter c1(path1);
+    Cutter c1(path1, threads);
     std::unique_ptr<Cutter> c2;
-    if (paired) c2 = std::make_unique<Cutter>(path2);
+    if (paired) c2 = std::make_unique<Cutter>(path2, threads);
     Shared sh;
     sh.max_q = n_parsers + 1;
     auto reader = [&] {

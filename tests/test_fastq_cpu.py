@@ -159,3 +159,43 @@ def test_missing_and_empty(tmp_path):
     # final record without a trailing newline
     (tmp_path / "t.fq").write_bytes(b"@a\nACGT\n+\nIIII\n@b\nGG\n+\nII")
     assert checksum(tmp_path / "t.fq")[:2] == (2, 6)
+
+
+def write_bgzf(path, data: bytes, block=65280):
+    """BGZF as bgzip writes it: independent raw-deflate gzip members with a BC extra field, then the EOF member."""
+    import struct
+    import zlib
+    out = []
+    for i in range(0, len(data), block):
+        chunk = data[i:i + block]
+        co = zlib.compressobj(6, zlib.DEFLATED, -15)
+        comp = co.compress(chunk) + co.flush()
+        bsize = 18 + len(comp) + 8 - 1
+        hdr = struct.pack("<BBBBIBBHBBHH", 0x1f, 0x8b, 8, 4, 0, 0, 0xff, 6, ord("B"), ord("C"), 2, bsize)
+        out.append(hdr + comp + struct.pack("<II", zlib.crc32(chunk) & 0xffffffff, len(chunk)))
+    out.append(bytes.fromhex("1f8b08040000000000ff0600424302001b0003000000000000000000"))
+    with open(path, "wb") as f:
+        f.write(b"".join(out))
+
+
+@pytest.mark.parametrize("threads", [1, 4])
+def test_bgzf_parallel_inflate(tmp_path, threads):
+    """BGZF members are inflated in parallel into their final positions; same records as the plain file."""
+    ref = synth.make_reference(2, 1, 3_000)
+    recs = records_of(synth.make_reads(ref, 20_000, read_len=90))
+    data = render(recs)
+    (tmp_path / "p.fq").write_bytes(data)
+    write_bgzf(tmp_path / "b.fq.gz", data)
+    assert checksum(tmp_path / "b.fq.gz", threads=threads) == checksum(tmp_path / "p.fq", threads=threads)
+    # plain gzip readers accept BGZF too (concatenated members): same records
+    assert gzip.decompress((tmp_path / "b.fq.gz").read_bytes()) == data
+
+
+def test_bgzf_corruption_is_reported(tmp_path):
+    data = render([(b"ACGT" * 10, b"I" * 40)] * 100)
+    write_bgzf(tmp_path / "b.fq.gz", data, block=1000)
+    raw = bytearray((tmp_path / "b.fq.gz").read_bytes())
+    raw[40] ^= 0xFF  # inside the first member's deflate data
+    (tmp_path / "c.fq.gz").write_bytes(bytes(raw))
+    with pytest.raises(SpeqError):
+        checksum(tmp_path / "c.fq.gz")
