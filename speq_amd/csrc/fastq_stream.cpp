@@ -77,8 +77,11 @@ public:
         size_t out = 0;
         while (pos_ < size_) {
             const Next m = next_member(pos_);
-            if (!batch.empty() && out + m.dsize > n) break;
-            if (m.dsize > n) throw IoError("BGZF member larger than the read buffer in " + path_);
+            if (out + m.dsize > n) {
+                // the caller's buffer is full; members hold at most 64 KiB, so a larger buffer always takes one
+                if (batch.empty() && n >= 65536) throw IoError("BGZF member larger than 64 KiB in " + path_);
+                break;
+            }
             batch.push_back({m.cpos, m.csize, out, m.dsize});
             out += m.dsize;
             pos_ += m.csize;

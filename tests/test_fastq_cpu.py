@@ -180,9 +180,10 @@ def write_bgzf(path, data: bytes, block=65280):
 
 @pytest.mark.parametrize("threads", [1, 4])
 def test_bgzf_parallel_inflate(tmp_path, threads):
-    """BGZF members are inflated in parallel into their final positions; same records as the plain file."""
+    """BGZF members are inflated in parallel into their final positions; same records as the plain file (> 16 MiB,
+    so the reader's buffer fills mid-stream and members continue in the next read)."""
     ref = synth.make_reference(2, 1, 3_000)
-    recs = records_of(synth.make_reads(ref, 20_000, read_len=90))
+    recs = records_of(synth.make_reads(ref, 110_000, read_len=90))
     data = render(recs)
     (tmp_path / "p.fq").write_bytes(data)
     write_bgzf(tmp_path / "b.fq.gz", data)
