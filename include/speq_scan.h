@@ -256,7 +256,10 @@ void speq_groupings_free(speq_groupings* g);
  * "sparse_prefix": 0 (default) dense q-mer tables; 1 a presence bitvector with ranks + the present intervals
  *                  (less memory, one more dependent load per window); -1 sparse when < 1/8 of the codes occur;
  * "fastq_gpu_parse": 1 (default) speq_scan_fastq parses blocks of simple four-line records on the GPU (raw text
- *                  to HBM); 0 parses every block on host threads. Results are identical. */
+ *                  to HBM); 0 parses every block on host threads. Results are identical;
+ * "stream_lanes" : compute streams of a pipeline created afterwards (speq_pipeline_create, speq_scan_fastq, host
+ *                  scans), 1..8 (default 3): consecutive batches are parsed and scanned on them in turn, so the
+ *                  short launches of different batches overlap on the CUs. */
 int speq_device_set_tuning(speq_device_index* d, const char* key, int64_t value);
 int speq_device_get_tuning(const speq_device_index* d, const char* key, int64_t* value);
 

@@ -24,6 +24,8 @@ def main():
     ap.add_argument("--reads", type=int, default=1_000_000)
     ap.add_argument("--threads", default="1,4,8,16")
     ap.add_argument("--gz", type=int, default=1)
+    ap.add_argument("--split", default="1,0", help="SPEQ_SPLIT_CUT values for the plain-file runs")
+    ap.add_argument("--lanes", default="", help="stream_lanes values to sweep (default: the device default)")
     ap.add_argument("--dir", default=os.environ.get("TMPDIR", "/tmp"))
     ap.add_argument("--out", default="")
     a = ap.parse_args()
@@ -67,15 +69,21 @@ def main():
             f.write(b"".join(parts))
     size = os.path.getsize(path)
     print(f"# wrote {size / 1e6:.0f} MB FASTQ in {time.perf_counter() - t0:.1f} s", flush=True)
-    for th in [int(x) for x in a.threads.split(",")]:
-        best = None
-        for _ in range(2):
-            r2, st = dev.scan_fastq(path, None, k=k, threads=th)
-            best = st if best is None or st["seconds"] < best["seconds"] else best
-        assert r2.total == r.total and r2.unique.tolist() == r.unique.tolist()
-        emit({"path": "fastq (speq_scan_fastq, plain, page cache)", "threads": th, "seconds": best["seconds"],
-              "kmers_per_s": kmers / best["seconds"], "MB_per_s_file": size / best["seconds"] / 1e6,
-              "batches": best["batches"]})
+    lane_opts = [int(x) for x in a.lanes.split(",")] if a.lanes else [dev.tuning("stream_lanes")]
+    for split_cut, lanes in [(sc, ln) for sc in a.split.split(",") for ln in lane_opts]:
+        os.environ["SPEQ_SPLIT_CUT"] = split_cut
+        dev.tune(stream_lanes=lanes)
+        for th in [int(x) for x in a.threads.split(",")]:
+            best = None
+            for _ in range(3):
+                r2, st = dev.scan_fastq(path, None, k=k, threads=th)
+                best = st if best is None or st["seconds"] < best["seconds"] else best
+            assert r2.total == r.total and r2.unique.tolist() == r.unique.tolist()
+            emit({"path": "fastq (speq_scan_fastq, plain, page cache)", "threads": th,
+                  "cut": "parallel" if split_cut != "0" else "sequential", "stream_lanes": lanes, "seconds": best["seconds"],
+                  "kmers_per_s": kmers / best["seconds"], "MB_per_s_file": size / best["seconds"] / 1e6,
+                  "batches": best["batches"]})
+    os.environ.pop("SPEQ_SPLIT_CUT", None)
     if a.gz:
         gpath = path + ".gz"
         with open(path, "rb") as f, gzip.open(gpath, "wb", compresslevel=1) as g:

@@ -15,6 +15,7 @@
 #include <rocprim/rocprim.hpp>
 
 #include <algorithm>
+#include <cstdint>
 #include <string>
 
 #include "speq_errors.hpp"
@@ -28,73 +29,136 @@ namespace {
         if (_e != hipSuccess) throw DeviceError(std::string("fastq gpu: ") + #expr + ": " + hipGetErrorString(_e)); \
     } while (0)
 
-constexpr uint32_t CHUNK = 256;  // bytes per thread in the newline count
+// Newline scan: each thread owns one 16-byte aligned window of the block's text (coalesced dwordx4 loads), each
+// workgroup 256 windows = 4 KiB.
+constexpr uint32_t NL_THREADS = 256, NL_WIN = 16, NL_SPAN = NL_THREADS * NL_WIN;
 
 enum : uint32_t { ERR_HEADER = 1u, ERR_PLUS = 2u, ERR_LENGTH = 4u, ERR_LINES = 8u };
 
 __device__ __forceinline__ bool is_space(uint32_t c) { return c == ' ' || (c >= '\t' && c <= '\r'); }
 __device__ __forceinline__ bool is_seq(uint32_t c) { return !is_space(c) && !(c >= '0' && c <= '9'); }
 
-__global__ void k_count_nl(const uint8_t* __restrict__ raw, uint64_t len, uint32_t* __restrict__ counts,
-                           uint32_t n_chunks) {
-    const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
-    if (c >= n_chunks) return;
-    const uint64_t b = (uint64_t)c * CHUNK, e = min(len, b + CHUNK);
-    uint32_t cnt = 0;
-    for (uint64_t i = b; i < e; ++i) cnt += raw[i] == '\n';
-    counts[c] = cnt;
+// bit i set when byte i of w is '\n' (exact: the 7-bit add cannot carry across bytes)
+__device__ __forceinline__ uint32_t nl4(uint32_t w) {
+    const uint32_t y = w ^ 0x0a0a0a0au;
+    const uint32_t t = ~(((y & 0x7f7f7f7fu) + 0x7f7f7f7fu) | y | 0x7f7f7f7fu);
+    return (((t >> 7) & 0x01010101u) * 0x01020408u) >> 24;
 }
 
-__global__ void k_write_nl(const uint8_t* __restrict__ raw, uint64_t len, const uint32_t* __restrict__ offs,
-                           uint32_t n_chunks, uint32_t* __restrict__ nl, uint32_t cap) {
-    const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
-    if (c >= n_chunks) return;
-    const uint64_t b = (uint64_t)c * CHUNK, e = min(len, b + CHUNK);
-    uint32_t o = offs[c];
-    for (uint64_t i = b; i < e; ++i)
-        if (raw[i] == '\n') {
-            if (o < cap) nl[o] = (uint32_t)i;
-            ++o;
-        }
+// '\n' mask of the window starting at byte a (16-aligned) of `base`, restricted to [begin, end)
+__device__ __forceinline__ uint32_t nl_mask(const uint8_t* __restrict__ base, uint64_t a, uint64_t begin,
+                                            uint64_t end) {
+    if (a >= end) return 0;
+    const uint4 v = *reinterpret_cast<const uint4*>(base + a);  // the buffer is padded past the text
+    uint32_t m = nl4(v.x) | (nl4(v.y) << 4) | (nl4(v.z) << 8) | (nl4(v.w) << 12);
+    if (a < begin) m &= 0xffffu << (uint32_t)(begin - a);
+    if (end - a < 16) m &= (1u << (uint32_t)(end - a)) - 1u;
+    return m;
+}
+
+__device__ __forceinline__ uint32_t wave_incl_sum(uint32_t v) {
+    const uint32_t lane = threadIdx.x & 63u;
+#pragma unroll
+    for (uint32_t d = 1; d < 64; d <<= 1) {
+        const uint32_t u = __shfl_up(v, d, 64);
+        if (lane >= d) v += u;
+    }
+    return v;
+}
+
+// Newlines per workgroup span; counts[g] for g < n_groups.
+__global__ __launch_bounds__(NL_THREADS) void k_count_nl(const uint8_t* __restrict__ base, uint64_t a0,
+                                                         uint64_t begin, uint64_t end,
+                                                         uint32_t* __restrict__ counts) {
+    __shared__ uint32_t part[NL_THREADS / 64];
+    const uint64_t a = a0 + (uint64_t)blockIdx.x * NL_SPAN + (uint64_t)threadIdx.x * NL_WIN;
+    uint32_t c = (uint32_t)__popc(nl_mask(base, a, begin, end));
+#pragma unroll
+    for (uint32_t d = 32; d > 0; d >>= 1) c += __shfl_xor(c, d, 64);
+    if ((threadIdx.x & 63u) == 0) part[threadIdx.x / 64u] = c;
+    __syncthreads();
+    if (threadIdx.x == 0) counts[blockIdx.x] = part[0] + part[1] + part[2] + part[3];
+}
+
+// Positions (relative to base) of the newlines, in order, from the exclusive sums of k_count_nl.
+__global__ __launch_bounds__(NL_THREADS) void k_write_nl(const uint8_t* __restrict__ base, uint64_t a0,
+                                                         uint64_t begin, uint64_t end,
+                                                         const uint32_t* __restrict__ offs,
+                                                         uint32_t* __restrict__ nl, uint32_t cap) {
+    __shared__ uint32_t part[NL_THREADS / 64];
+    const uint64_t a = a0 + (uint64_t)blockIdx.x * NL_SPAN + (uint64_t)threadIdx.x * NL_WIN;
+    uint32_t m = nl_mask(base, a, begin, end);
+    const uint32_t c = (uint32_t)__popc(m);
+    const uint32_t incl = wave_incl_sum(c);
+    const uint32_t w = threadIdx.x / 64u;
+    if ((threadIdx.x & 63u) == 63u) part[w] = incl;
+    __syncthreads();
+    uint32_t o = offs[blockIdx.x] + incl - c;
+    for (uint32_t i = 0; i < w; ++i) o += part[i];
+    while (m) {
+        const uint32_t b = (uint32_t)__ffs(m) - 1u;
+        m &= m - 1u;
+        if (o < cap) nl[o] = (uint32_t)(a + b);
+        ++o;
+    }
 }
 
 struct Rec {
-    uint32_t s0, s1, q0, q1;  // raw [begin, end) of the base line and of the quality line
+    uint32_t s0, s1, q0, q1;  // [begin, end) of the base line and of the quality line, relative to base
 };
 
-// One thread per record of one file: line bounds from the newline table, checks, valid character counts.
-__global__ void k_records(const uint8_t* __restrict__ raw, uint64_t len, uint32_t base_off,
-                          const uint32_t* __restrict__ nl, const uint32_t* __restrict__ n_nl, uint32_t n,
-                          uint32_t slot0, uint32_t slot_stride, Rec* __restrict__ rec, uint64_t* __restrict__ lens,
-                          uint32_t* __restrict__ err) {
-    const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+// Characters of [b, e) that pass the filter (bases: not blank, not a digit; qualities: not blank), one wave.
+template <bool SEQ>
+__device__ __forceinline__ uint64_t wave_count(const uint8_t* __restrict__ base, uint64_t b, uint64_t e,
+                                               uint32_t lane) {
+    uint64_t n = 0;
+    for (uint64_t i0 = b; i0 < e; i0 += 64u) {
+        const uint64_t i = i0 + lane;
+        const uint32_t c = i < e ? base[i] : (uint32_t)' ';
+        n += (uint64_t)__popcll(__ballot(i < e && (SEQ ? is_seq(c) : !is_space(c))));
+    }
+    return n;
+}
+
+// One wave per record of one file (lines 4r .. 4r+3 of the block): line bounds from the newline table, the
+// four-line checks, filtered character counts. A record that does not pass sets err (lens 0).
+__global__ __launch_bounds__(256) void k_records(const uint8_t* __restrict__ base, uint64_t begin, uint64_t end,
+                                                 const uint32_t* __restrict__ nl,
+                                                 const uint32_t* __restrict__ n_nl, uint32_t n, uint32_t slot0,
+                                                 uint32_t slot_stride, Rec* __restrict__ rec,
+                                                 uint64_t* __restrict__ lens, uint32_t* __restrict__ err) {
+    const uint32_t r = blockIdx.x * (blockDim.x / 64u) + threadIdx.x / 64u;
+    const uint32_t lane = threadIdx.x & 63u;
     if (r >= n) return;
     const uint32_t total = *n_nl;
-    auto line_end = [&](uint32_t j) -> uint64_t { return j < total ? nl[j] : len; };  // last line may be open
+    const uint32_t slot = slot0 + r * slot_stride;
     if (4u * r + 2u >= total) {  // fewer than three newlines before the quality line
-        atomicOr(err, ERR_LINES);
-        lens[slot0 + r * slot_stride] = 0;
-        rec[slot0 + r * slot_stride] = Rec{0, 0, 0, 0};
+        if (lane == 0) {
+            atomicOr(err, ERR_LINES);
+            lens[slot] = 0;
+            rec[slot] = Rec{0, 0, 0, 0};
+        }
         return;
     }
-    const uint64_t h = r == 0 ? 0 : (uint64_t)nl[4u * r - 1u] + 1u;
+    auto line_end = [&](uint32_t j) -> uint64_t { return j < total ? nl[j] : end; };  // last line may be open
+    const uint64_t h = r == 0 ? begin : (uint64_t)nl[4u * r - 1u] + 1u;
     const uint64_t s0 = line_end(4u * r) + 1u, s1 = line_end(4u * r + 1u);
     const uint64_t p0 = s1 + 1u;
     const uint64_t q0 = line_end(4u * r + 2u) + 1u, q1 = line_end(4u * r + 3u);
     uint64_t se = s1, qe = q1;
-    while (se > s0 && raw[se - 1] == '\r') --se;
-    while (qe > q0 && raw[qe - 1] == '\r') --qe;
+    while (se > s0 && base[se - 1] == '\r') --se;
+    while (qe > q0 && base[qe - 1] == '\r') --qe;
     uint32_t e = 0;
-    if (h >= len || raw[h] != '@') e |= ERR_HEADER;
-    if (p0 >= len || raw[p0] != '+') e |= ERR_PLUS;
-    uint64_t ns = 0, nq = 0;
-    for (uint64_t i = s0; i < se; ++i) ns += is_seq(raw[i]);
-    for (uint64_t i = q0; i < qe; ++i) nq += !is_space(raw[i]);
+    if (h >= end || base[h] != '@') e |= ERR_HEADER;
+    // the third line must open with '+', and the second must not (the host grammar would take it as the separator)
+    if (p0 >= end || base[p0] != '+' || (s0 < s1 && base[s0] == '+')) e |= ERR_PLUS;
+    const uint64_t ns = wave_count<true>(base, s0, se, lane), nq = wave_count<false>(base, q0, qe, lane);
     if (ns != nq) e |= ERR_LENGTH;
-    if (e) atomicOr(err, e);
-    lens[slot0 + r * slot_stride] = e ? 0 : ns;
-    rec[slot0 + r * slot_stride] = Rec{(uint32_t)s0 + base_off, (uint32_t)se + base_off, (uint32_t)q0 + base_off,
-                                       (uint32_t)qe + base_off};
+    if (lane == 0) {
+        if (e) atomicOr(err, e);
+        lens[slot] = e ? 0 : ns;
+        rec[slot] = Rec{(uint32_t)s0, (uint32_t)se, (uint32_t)q0, (uint32_t)qe};
+    }
 }
 
 // One wave per record slot: copy (and compact) the base and quality characters.
@@ -130,6 +194,11 @@ __global__ void k_copy(const uint8_t* __restrict__ raw, const Rec* __restrict__ 
     }
 }
 
+// Total parsed bases of the batch, accumulated for the stream statistics.
+__global__ void k_add_total(const uint64_t* __restrict__ off_end, unsigned long long* __restrict__ total) {
+    atomicAdd(total, (unsigned long long)*off_end);
+}
+
 inline uint32_t grid(uint64_t n, uint32_t bs = 256) { return (uint32_t)((n + bs - 1) / bs); }
 inline uint64_t align16(uint64_t x) { return (x + 15) & ~uint64_t(15); }
 
@@ -137,9 +206,12 @@ struct Layout {
     uint64_t counts, offs, nl, n_nl, rec, lens, temp, total;
 };
 
+// workgroups of the newline scan over [begin, begin + len) (first window aligned down to 16 bytes)
+inline uint64_t nl_groups(uint64_t len) { return (len + NL_WIN) / NL_SPAN + 1; }
+
 Layout layout(uint64_t raw_bytes, uint64_t n_slots, uint64_t n_lines, size_t temp_bytes) {
     Layout L{};
-    const uint64_t chunks = raw_bytes / CHUNK + 2;
+    const uint64_t chunks = nl_groups(raw_bytes) + 2;
     uint64_t p = 0;
     L.counts = p; p = align16(p + chunks * 4);
     L.offs = p; p = align16(p + chunks * 4);
@@ -154,7 +226,7 @@ Layout layout(uint64_t raw_bytes, uint64_t n_slots, uint64_t n_lines, size_t tem
 
 size_t temp_need(uint64_t raw_bytes, uint64_t n_slots) {
     size_t a = 0, b = 0;
-    const uint64_t chunks = raw_bytes / CHUNK + 2;
+    const uint64_t chunks = nl_groups(raw_bytes) + 2;
     (void)rocprim::exclusive_scan(nullptr, a, (uint32_t*)nullptr, (uint32_t*)nullptr, 0u, (size_t)chunks,
                                   rocprim::plus<uint32_t>());
     (void)rocprim::exclusive_scan(nullptr, b, (uint64_t*)nullptr, (uint64_t*)nullptr, uint64_t(0),
@@ -169,11 +241,12 @@ size_t fastq_gpu_scratch_bytes(uint64_t raw_bytes, uint64_t records_per_file, bo
     return layout(raw_bytes, n_slots, 4 * records_per_file, temp_need(raw_bytes, n_slots)).total;
 }
 
-// d_raw holds file 1's block [0, len1) followed by file 2's [len1, len1 + len2) (paired). Writes k_scan's input
-// layout: records interleaved (2i, 2i+1) when paired; d_off has n_slots + 1 entries. Asynchronous on `stream`.
+// d_raw holds file 1's block [0, len1) followed by file 2's [len1, len1 + len2) (paired), and at least 16 readable
+// bytes after them. Writes k_scan's input layout: records interleaved (2i, 2i+1) when paired; d_off has n_slots + 1
+// entries; the batch's base count is added to *d_total_bases. Asynchronous on `stream`.
 void launch_fastq_parse(const uint8_t* d_raw, uint64_t len1, uint64_t len2, uint64_t n, bool paired, void* d_scratch,
                         size_t scratch_bytes, uint8_t* d_seq, uint8_t* d_qual, uint64_t* d_off, uint32_t* d_err,
-                        void* stream) {
+                        uint64_t* d_total_bases, void* stream) {
     hipStream_t st = static_cast<hipStream_t>(stream);
     const uint64_t n_slots = n * (paired ? 2 : 1);
     const uint64_t raw_max = std::max(len1, len2);
@@ -181,30 +254,31 @@ void launch_fastq_parse(const uint8_t* d_raw, uint64_t len1, uint64_t len2, uint
     const Layout L = layout(raw_max, n_slots, 4 * n, tn);
     if (L.total > scratch_bytes) throw std::invalid_argument("fastq gpu: scratch too small");
     if (len1 + len2 >= (uint64_t(1) << 32)) throw std::invalid_argument("fastq gpu: block exceeds 4 GiB");
-    uint8_t* base = static_cast<uint8_t*>(d_scratch);
-    uint32_t* counts = reinterpret_cast<uint32_t*>(base + L.counts);
-    uint32_t* offs = reinterpret_cast<uint32_t*>(base + L.offs);
-    uint32_t* nl = reinterpret_cast<uint32_t*>(base + L.nl);
-    uint32_t* n_nl = reinterpret_cast<uint32_t*>(base + L.n_nl);
-    Rec* rec = reinterpret_cast<Rec*>(base + L.rec);
-    uint64_t* lens = reinterpret_cast<uint64_t*>(base + L.lens);
-    void* temp = base + L.temp;
+    if (reinterpret_cast<uintptr_t>(d_raw) & 15u) throw std::invalid_argument("fastq gpu: raw buffer not 16-aligned");
+    uint8_t* sb = static_cast<uint8_t*>(d_scratch);
+    uint32_t* counts = reinterpret_cast<uint32_t*>(sb + L.counts);
+    uint32_t* offs = reinterpret_cast<uint32_t*>(sb + L.offs);
+    uint32_t* nl = reinterpret_cast<uint32_t*>(sb + L.nl);
+    uint32_t* n_nl = reinterpret_cast<uint32_t*>(sb + L.n_nl);
+    Rec* rec = reinterpret_cast<Rec*>(sb + L.rec);
+    uint64_t* lens = reinterpret_cast<uint64_t*>(sb + L.lens);
+    void* temp = sb + L.temp;
     for (int f = 0; f < (paired ? 2 : 1); ++f) {
-        const uint8_t* raw = d_raw + (f ? len1 : 0);
-        const uint64_t len = f ? len2 : len1;
-        const uint32_t chunks = (uint32_t)(len / CHUNK + 1);
-        k_count_nl<<<grid(chunks), 256, 0, st>>>(raw, len, counts, chunks);
+        const uint64_t begin = f ? len1 : 0, end = begin + (f ? len2 : len1);
+        const uint64_t a0 = begin & ~uint64_t(NL_WIN - 1);
+        const uint32_t groups = (uint32_t)((end - a0 + NL_SPAN - 1) / NL_SPAN + (end == a0));
+        k_count_nl<<<groups, NL_THREADS, 0, st>>>(d_raw, a0, begin, end, counts);
         FHIP(hipGetLastError());
         size_t need = tn;
-        // chunks + 1 entries: the last exclusive sum is the total newline count
-        FHIP(hipMemsetAsync(counts + chunks, 0, 4, st));
-        FHIP(rocprim::exclusive_scan(temp, need, counts, offs, 0u, (size_t)chunks + 1, rocprim::plus<uint32_t>(), st));
-        FHIP(hipMemcpyAsync(n_nl, offs + chunks, 4, hipMemcpyDeviceToDevice, st));
-        k_write_nl<<<grid(chunks), 256, 0, st>>>(raw, len, offs, chunks, nl, (uint32_t)(4 * n + 1));
+        // groups + 1 entries: the last exclusive sum is the total newline count
+        FHIP(hipMemsetAsync(counts + groups, 0, 4, st));
+        FHIP(rocprim::exclusive_scan(temp, need, counts, offs, 0u, (size_t)groups + 1, rocprim::plus<uint32_t>(), st));
+        FHIP(hipMemcpyAsync(n_nl, offs + groups, 4, hipMemcpyDeviceToDevice, st));
+        k_write_nl<<<groups, NL_THREADS, 0, st>>>(d_raw, a0, begin, end, offs, nl, (uint32_t)(4 * n + 1));
         FHIP(hipGetLastError());
-        // record r of file f goes to slot paired ? 2r + f : r; raw offsets of file 2 are made global below
-        k_records<<<grid(n), 256, 0, st>>>(raw, len, f ? (uint32_t)len1 : 0u, nl, n_nl, (uint32_t)n,
-                                           paired ? (uint32_t)f : 0u, paired ? 2u : 1u, rec, lens, d_err);
+        // record r of file f goes to slot paired ? 2r + f : r
+        k_records<<<grid(n * 64u), 256, 0, st>>>(d_raw, begin, end, nl, n_nl, (uint32_t)n, paired ? (uint32_t)f : 0u,
+                                                 paired ? 2u : 1u, rec, lens, d_err);
         FHIP(hipGetLastError());
     }
     size_t need = tn;
@@ -213,6 +287,10 @@ void launch_fastq_parse(const uint8_t* d_raw, uint64_t len1, uint64_t len2, uint
                                  rocprim::plus<uint64_t>(), st));
     k_copy<<<grid(n_slots * 64u), 256, 0, st>>>(d_raw, rec, d_off, (uint32_t)n_slots, d_seq, d_qual);
     FHIP(hipGetLastError());
+    if (d_total_bases) {
+        k_add_total<<<1, 1, 0, st>>>(d_off + n_slots, reinterpret_cast<unsigned long long*>(d_total_bases));
+        FHIP(hipGetLastError());
+    }
 }
 
 }  // namespace speq

@@ -92,7 +92,7 @@ void alloc_buffers(Slot& s, uint64_t bytes, uint64_t records) {
     hip_ok(hipHostMalloc(reinterpret_cast<void**>(&s.h_qual), bytes, hipHostMallocDefault), "hipHostMalloc");
     hip_ok(hipHostMalloc(reinterpret_cast<void**>(&s.h_off), (records + 1) * 8, hipHostMallocDefault),
            "hipHostMalloc");
-    hip_ok(hipMalloc(reinterpret_cast<void**>(&s.d_seq), bytes), "hipMalloc");
+    hip_ok(hipMalloc(reinterpret_cast<void**>(&s.d_seq), bytes + 64), "hipMalloc");  // GPU parse reads 16-B windows
     hip_ok(hipMalloc(reinterpret_cast<void**>(&s.d_qual), bytes), "hipMalloc");
     hip_ok(hipMalloc(reinterpret_cast<void**>(&s.d_off), (records + 1) * 8), "hipMalloc");
     s.cap_bytes = bytes;
@@ -107,7 +107,9 @@ struct speq_pipeline {
     speq_em* em = nullptr;
     int device = 0;
     uint32_t G = 0;
-    hipStream_t copy = nullptr, compute = nullptr;
+    hipStream_t copy = nullptr, compute = nullptr;  // compute == lanes[0] (memsets and reads of the counters)
+    std::vector<hipStream_t> lanes;                 // compute streams, used in turn by submits
+    size_t next_lane = 0;                           // under submit_mu
     uint64_t* d_counts = nullptr;
     double* d_w = nullptr;
     std::vector<Slot> slots;
@@ -116,11 +118,18 @@ struct speq_pipeline {
     std::deque<int> free_slots;
     std::mutex submit_mu;       // stream order of copies and launches
     uint32_t* d_err = nullptr;  // GPU FASTQ parse errors (bit flags), checked by finish
+    uint64_t* d_bases = nullptr;  // bases parsed on the GPU since the last finish
+    uint64_t gpu_bases = 0;       // ... as of the last finish
 
+    hipStream_t lane() { return lanes[next_lane++ % lanes.size()]; }
+    void sync_lanes() {
+        for (hipStream_t l : lanes) hip_ok(hipStreamSynchronize(l), "hipStreamSynchronize");
+    }
     ~speq_pipeline() {
-        if (compute) (void)hipStreamSynchronize(compute);
+        for (hipStream_t l : lanes) (void)hipStreamSynchronize(l);
         if (copy) (void)hipStreamSynchronize(copy);
         if (d_err) (void)hipFree(d_err);
+        if (d_bases) (void)hipFree(d_bases);
         for (Slot& s : slots) {
             free_buffers(s);
             free_parse(s);
@@ -130,7 +139,7 @@ struct speq_pipeline {
         if (d_counts) (void)hipFree(d_counts);
         if (d_w) (void)hipFree(d_w);
         if (copy) (void)hipStreamDestroy(copy);
-        if (compute) (void)hipStreamDestroy(compute);
+        for (hipStream_t l : lanes) (void)hipStreamDestroy(l);
     }
 };
 
@@ -155,11 +164,15 @@ int speq_pipeline_create(speq_device_index* d, const speq_scan_params* params, s
         pl->G = speq::device_groups(d);
         DevScope g(pl->device);
         hip_ok(hipStreamCreateWithFlags(&pl->copy, hipStreamNonBlocking), "hipStreamCreate");
-        hip_ok(hipStreamCreateWithFlags(&pl->compute, hipStreamNonBlocking), "hipStreamCreate");
+        pl->lanes.resize(std::max<uint32_t>(1, speq::device_stream_lanes(d)), nullptr);
+        for (hipStream_t& l : pl->lanes) hip_ok(hipStreamCreateWithFlags(&l, hipStreamNonBlocking), "hipStreamCreate");
+        pl->compute = pl->lanes[0];
         hip_ok(hipMalloc(reinterpret_cast<void**>(&pl->d_counts), SPEQ_COUNTS_LEN(pl->G) * 8), "hipMalloc");
         hip_ok(hipMemsetAsync(pl->d_counts, 0, SPEQ_COUNTS_LEN(pl->G) * 8, pl->compute), "hipMemset");
         hip_ok(hipMalloc(reinterpret_cast<void**>(&pl->d_err), 16), "hipMalloc");
         hip_ok(hipMemsetAsync(pl->d_err, 0, 16, pl->compute), "hipMemset");
+        hip_ok(hipMalloc(reinterpret_cast<void**>(&pl->d_bases), 8), "hipMalloc");
+        hip_ok(hipMemsetAsync(pl->d_bases, 0, 8, pl->compute), "hipMemset");
         hip_ok(hipMalloc(reinterpret_cast<void**>(&pl->d_w), std::max<uint32_t>(pl->G, 1) * 8), "hipMalloc");
         hip_ok(hipMemsetAsync(pl->d_w, 0, std::max<uint32_t>(pl->G, 1) * 8, pl->compute), "hipMemset");
         pl->slots.resize(n_slots);
@@ -247,10 +260,11 @@ int speq_pipeline_submit(speq_pipeline* pl, int32_t slot, uint64_t n_records) {
         hip_ok(hipMemcpyAsync(s.d_off, s.h_off, (n_records + 1) * 8, hipMemcpyHostToDevice, pl->copy),
                "hipMemcpyAsync");
         hip_ok(hipEventRecord(s.copied, pl->copy), "hipEventRecord");
-        hip_ok(hipStreamWaitEvent(pl->compute, s.copied, 0), "hipStreamWaitEvent");
+        hipStream_t cs = pl->lane();
+        hip_ok(hipStreamWaitEvent(cs, s.copied, 0), "hipStreamWaitEvent");
         speq::launch_reads_scan(pl->d, s.d_seq, s.d_qual, s.d_off, n_records, &pl->p, pl->d_counts, pl->d_w,
-                                pl->em ? pl->em->d_mult : nullptr, pl->em ? pl->em->d_hi : nullptr, pl->compute);
-        hip_ok(hipEventRecord(s.done, pl->compute), "hipEventRecord");
+                                pl->em ? pl->em->d_mult : nullptr, pl->em ? pl->em->d_hi : nullptr, cs);
+        hip_ok(hipEventRecord(s.done, cs), "hipEventRecord");
         s.pending = true;
     });
     release();
@@ -282,8 +296,12 @@ void pipeline_submit_raw(speq_pipeline* pl, int32_t slot, uint64_t len1, uint64_
     // parse buffers: bases <= raw bytes; the slot was acquired, so nothing in flight uses them
     const size_t need_scratch = fastq_gpu_scratch_bytes(std::max(len1, len2), n, paired);
     if (len1 + len2 > s.parse_bytes || n_slots > s.parse_slots || need_scratch > s.scratch_bytes) {
-        const uint64_t pb = std::max(len1 + len2, s.parse_bytes), ps = std::max(n_slots, s.parse_slots);
-        const size_t sb = std::max(need_scratch, s.scratch_bytes);
+        // hipFree waits for the whole device, so size for the slot's capacity (and grow by half) to keep
+        // reallocation out of the steady state
+        const uint64_t pb = std::max({len1 + len2, s.parse_bytes * 3 / 2, s.cap_bytes});
+        const uint64_t ps = std::max({n_slots, s.parse_slots * 3 / 2, s.cap_records});
+        const size_t sb = std::max({need_scratch, s.scratch_bytes * 3 / 2,
+                                    fastq_gpu_scratch_bytes(pb / (paired ? 2 : 1), ps / (paired ? 2 : 1), paired)});
         free_parse(s);
         hip_ok(hipMalloc(reinterpret_cast<void**>(&s.d_pseq), pb), "hipMalloc");
         hip_ok(hipMalloc(reinterpret_cast<void**>(&s.d_pqual), pb), "hipMalloc");
@@ -296,14 +314,27 @@ void pipeline_submit_raw(speq_pipeline* pl, int32_t slot, uint64_t len1, uint64_
     std::lock_guard<std::mutex> lk(pl->submit_mu);
     hip_ok(hipMemcpyAsync(s.d_seq, s.h_seq, len1 + len2, hipMemcpyHostToDevice, pl->copy), "hipMemcpyAsync");
     hip_ok(hipEventRecord(s.copied, pl->copy), "hipEventRecord");
-    hip_ok(hipStreamWaitEvent(pl->compute, s.copied, 0), "hipStreamWaitEvent");
+    hipStream_t cs = pl->lane();
+    hip_ok(hipStreamWaitEvent(cs, s.copied, 0), "hipStreamWaitEvent");
     launch_fastq_parse(s.d_seq, len1, len2, n, paired, s.d_scratch, s.scratch_bytes, s.d_pseq, s.d_pqual, s.d_poff,
-                       pl->d_err, pl->compute);
+                       pl->d_err, pl->d_bases, cs);
     launch_reads_scan(pl->d, s.d_pseq, s.d_pqual, s.d_poff, n_slots, &pl->p, pl->d_counts, pl->d_w,
-                      pl->em ? pl->em->d_mult : nullptr, pl->em ? pl->em->d_hi : nullptr, pl->compute);
-    hip_ok(hipEventRecord(s.done, pl->compute), "hipEventRecord");
+                      pl->em ? pl->em->d_mult : nullptr, pl->em ? pl->em->d_hi : nullptr, cs);
+    hip_ok(hipEventRecord(s.done, cs), "hipEventRecord");
     s.pending = true;
 }
+
+uint32_t pipeline_take_parse_errors(speq_pipeline* pl) {
+    DevScope g(pl->device);
+    std::lock_guard<std::mutex> lk(pl->submit_mu);
+    pl->sync_lanes();
+    uint32_t err = 0;
+    hip_ok(hipMemcpy(&err, pl->d_err, 4, hipMemcpyDeviceToHost), "hipMemcpy");
+    if (err) hip_ok(hipMemset(pl->d_err, 0, 4), "hipMemset");
+    return err;
+}
+
+uint64_t pipeline_gpu_parsed_bases(const speq_pipeline* pl) { return pl->gpu_bases; }
 }  // namespace speq
 
 extern "C" {
@@ -315,6 +346,7 @@ int speq_pipeline_finish(speq_pipeline* pl, uint64_t* counts, double* weights) {
             throw std::invalid_argument("speq_pipeline_finish: local mode needs weights");
         DevScope g(pl->device);
         std::lock_guard<std::mutex> lk(pl->submit_mu);
+        pl->sync_lanes();  // every batch's kernels (any lane) before the counters are read
         const size_t nc = SPEQ_COUNTS_LEN(pl->G);
         hip_ok(hipMemcpyAsync(counts, pl->d_counts, nc * 8, hipMemcpyDeviceToHost, pl->compute), "hipMemcpyAsync");
         if (weights && pl->p.mode == SPEQ_MODE_LOCAL)
@@ -322,9 +354,13 @@ int speq_pipeline_finish(speq_pipeline* pl, uint64_t* counts, double* weights) {
         hip_ok(hipMemsetAsync(pl->d_counts, 0, nc * 8, pl->compute), "hipMemsetAsync");
         if (pl->d_w) hip_ok(hipMemsetAsync(pl->d_w, 0, pl->G * 8, pl->compute), "hipMemsetAsync");
         uint32_t err = 0;
+        uint64_t bases = 0;
         hip_ok(hipMemcpyAsync(&err, pl->d_err, 4, hipMemcpyDeviceToHost, pl->compute), "hipMemcpyAsync");
         hip_ok(hipMemsetAsync(pl->d_err, 0, 4, pl->compute), "hipMemsetAsync");
+        hip_ok(hipMemcpyAsync(&bases, pl->d_bases, 8, hipMemcpyDeviceToHost, pl->compute), "hipMemcpyAsync");
+        hip_ok(hipMemsetAsync(pl->d_bases, 0, 8, pl->compute), "hipMemsetAsync");
         hip_ok(hipStreamSynchronize(pl->compute), "hipStreamSynchronize");
+        pl->gpu_bases = bases;
         if (err)
             throw speq::IoError(std::string("malformed FASTQ record (GPU parse:") + ((err & 1) ? " header not '@'" : "") +
                                 ((err & 2) ? " separator not '+'" : "") +
@@ -352,10 +388,15 @@ speq_pipeline* take_pipeline(speq_device_index* d, const speq_scan_params* p, sp
         auto r = g_cache->equal_range(d);
         for (auto it = r.first; it != r.second; ++it) {
             speq_pipeline* pl = it->second;
-            if (pl->slots.size() < n_slots) continue;
+            if (pl->slots.size() < n_slots || pl->lanes.size() != speq::device_stream_lanes(d)) continue;
             g_cache->erase(it);
             pl->p = *p;
             pl->em = em;
+            // grow small slots now, while nothing is in flight (a mid-stream reserve would stall the device)
+            DevScope g(pl->device);
+            for (Slot& s : pl->slots)
+                if (s.cap_bytes < bytes || s.cap_records < recs + (recs & 1))
+                    alloc_buffers(s, std::max(bytes, s.cap_bytes), std::max(recs + (recs & 1), s.cap_records));
             return pl;
         }
     }

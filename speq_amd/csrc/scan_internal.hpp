@@ -25,11 +25,18 @@ void release_host_pipelines(const speq_device_index* d);
 size_t fastq_gpu_scratch_bytes(uint64_t raw_bytes, uint64_t records_per_file, bool paired);
 void launch_fastq_parse(const uint8_t* d_raw, uint64_t len1, uint64_t len2, uint64_t n, bool paired, void* d_scratch,
                         size_t scratch_bytes, uint8_t* d_seq, uint8_t* d_qual, uint64_t* d_off, uint32_t* d_err,
-                        void* stream);
+                        uint64_t* d_total_bases, void* stream);
 // Submits an acquired pipeline slot whose host buffer holds RAW four-line FASTQ text (file 1's block, then file
 // 2's when paired, n records each): copied as is, parsed on the GPU, then scanned (pipeline.cpp).
 void pipeline_submit_raw(speq_pipeline* pl, int32_t slot, uint64_t len1, uint64_t len2, uint64_t n, bool paired);
+// Waits for every submitted batch and returns (and clears) the GPU parse error flags raised so far (0 = none).
+uint32_t pipeline_take_parse_errors(speq_pipeline* pl);
+// Bases parsed on the GPU by raw submits up to the last speq_pipeline_finish.
+uint64_t pipeline_gpu_parsed_bases(const speq_pipeline* pl);
+// Zeroes the interval histogram an EM scan has recorded so far (a stream restarted from its first record).
+void em_clear(speq_em* em);
 bool device_fastq_gpu(const speq_device_index* d);
+uint32_t device_stream_lanes(const speq_device_index* d);
 int device_ordinal(const speq_device_index* d);
 uint32_t device_groups(const speq_device_index* d);
 }  // namespace speq

@@ -756,6 +756,7 @@ struct speq_device_index {
     const uint2* sparse_iv[3] = {nullptr, nullptr, nullptr};
     uint64_t present[3] = {0, 0, 0};                              // distinct q-mers per level
     bool fastq_gpu = true;        // tuning "fastq_gpu_parse": parse simple four-line FASTQ blocks on the GPU
+    uint32_t stream_lanes = 3;    // tuning "stream_lanes": compute streams per pipeline (batches scanned concurrently)
     int sparse_choice = 0;        // tuning "sparse_prefix": 0 dense (default), 1 sparse, -1 sparse when < 1/8 of
                                   // the codes occur. Dense wins: the sparse form saves fabric bytes but adds a
                                   // dependent load to every window (cfg 2: 4.63 -> 5.39 ms, sweep_sparse.jsonl)
@@ -1187,6 +1188,9 @@ int speq_device_set_tuning(speq_device_index* d, const char* key, int64_t value)
         } else if (k == "fastq_gpu_parse") {
             if (value != 0 && value != 1) throw std::invalid_argument("fastq_gpu_parse must be 0 or 1");
             d->fastq_gpu = value != 0;
+        } else if (k == "stream_lanes") {
+            if (value < 1 || value > 8) throw std::invalid_argument("stream_lanes must be in [1, 8]");
+            d->stream_lanes = (uint32_t)value;
         } else if (k == "sparse_prefix") {
             if (value < -1 || value > 1) throw std::invalid_argument("sparse_prefix must be -1 (auto), 0 or 1");
             d->sparse_choice = (int)value;
@@ -1214,6 +1218,7 @@ int speq_device_get_tuning(const speq_device_index* d, const char* key, int64_t*
         else if (k == "prefix_level") *value = d->prefix_choice;
         else if (k == "sparse_prefix") *value = d->sparse_choice;
         else if (k == "fastq_gpu_parse") *value = d->fastq_gpu ? 1 : 0;
+        else if (k == "stream_lanes") *value = d->stream_lanes;
         else throw std::invalid_argument("speq_device_get_tuning: unknown key " + k);
     });
 }
@@ -1247,6 +1252,16 @@ int speq_timing_read(speq_device_index* d, double* total_ms, uint64_t* launches)
 
 }  // extern "C"
 
+namespace speq {
+void em_clear(speq_em* em) {
+    if (!em) return;
+    if (em->finalized) throw std::logic_error("speq: EM histogram already finalized");
+    DeviceGuard g(em->dev->device);
+    HIP_OK(hipMemset(em->d_mult, 0, em->n * 4));
+}
+}  // namespace speq
+
+
 // ---- internal entry points for the streaming pipeline (pipeline.cpp; scan_internal.hpp) ----
 namespace speq {
 void launch_reads_scan(speq_device_index* d, const uint8_t* d_seq, const uint8_t* d_qual, const uint64_t* d_offsets,
@@ -1257,5 +1272,6 @@ void launch_reads_scan(speq_device_index* d, const uint8_t* d_seq, const uint8_t
 }
 int device_ordinal(const speq_device_index* d) { return d->device; }
 bool device_fastq_gpu(const speq_device_index* d) { return d->fastq_gpu; }
+uint32_t device_stream_lanes(const speq_device_index* d) { return d->stream_lanes; }
 uint32_t device_groups(const speq_device_index* d) { return d->G; }
 }  // namespace speq

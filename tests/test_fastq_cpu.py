@@ -200,3 +200,50 @@ def test_bgzf_corruption_is_reported(tmp_path):
     (tmp_path / "c.fq.gz").write_bytes(bytes(raw))
     with pytest.raises(SpeqError):
         checksum(tmp_path / "c.fq.gz")
+
+
+def _simple_records(n, seed, at_frac=0.3):
+    """Short four-line records whose quality lines often start with '@' (a header look-alike for the cutter)."""
+    rng = np.random.default_rng(seed)
+    lens = rng.integers(8, 40, n)
+    bases = np.frombuffer(b"ACGTN", np.uint8)
+    out = []
+    for i, L in enumerate(lens):
+        s = bases[rng.integers(0, 5, L)].tobytes()
+        q = bytearray(rng.integers(35, 74, L).astype(np.uint8).tobytes())
+        if rng.random() < at_frac:
+            q[0] = ord("@")
+        out.append((s, bytes(q)))
+    return out
+
+
+@pytest.mark.parametrize("case", ["simple", "no_final_newline", "wrapped_late", "blank_tail", "crlf", "error_late"])
+def test_parallel_cut_matches_sequential(tmp_path, monkeypatch, case):
+    """Single-end mapped files are cut at guessed headers (find_cut) and every block is checked as a chain of
+    four-line records; anything else restarts with the sequential cutter. Either way the records are the ones the
+    sequential cutter and the Python grammar find."""
+    recs = _simple_records(160_000, 7)  # ~9 MB: several 1 MiB+ blocks
+    data = render(recs, crlf=case == "crlf")
+    if case == "no_final_newline":
+        data = data[:-1]
+    elif case == "wrapped_late":
+        cut = len(data) * 3 // 4
+        cut = data.index(b"\n@r", cut) + 1
+        data = data[:cut] + b"@w\nACGT\nAC\n+\nIIII\nII\n" + data[cut:]
+    elif case == "blank_tail":
+        data += b"\n\n"
+    elif case == "error_late":
+        cut = data.index(b"\n@r", len(data) * 2 // 3) + 1
+        data = data[:cut] + b"@e\nACGT\n+\nII\n" + data[cut:]
+    p = tmp_path / "s.fq"
+    p.write_bytes(data)
+    if case == "error_late":
+        with pytest.raises(SpeqError, match="mismatch"):
+            checksum(p, threads=4)
+        return
+    exp = parse_py(data)
+    want = (len(exp), sum(len(s) for s, _ in exp), digest(exp))
+    for t in (1, 4, 8):
+        assert checksum(p, threads=t) == want
+    monkeypatch.setenv("SPEQ_SPLIT_CUT", "0")
+    assert checksum(p, threads=4) == want

@@ -236,3 +236,56 @@ def test_gpu_fastq_parse_blanks_and_errors(tmp_path):
         with pytest.raises(SpeqError, match="mismatch"):
             dev.scan_fastq(str(tmp_path / "bad.fq"), k=3)
     dev.tune(fastq_gpu_parse=1)
+
+
+PARALLEL_CASES = ["simple", "wrapped_late", "blank_late", "blank_tail", "crlf", "no_final_newline", "error_late",
+                  "plus_base_line"]
+
+
+@pytest.mark.parametrize("case", PARALLEL_CASES)
+def test_parallel_cut_stream_and_restart(tmp_path, monkeypatch, case):
+    """A single-end plain file is cut at guessed record starts in parallel (several blocks here) and parsed on the
+    GPU without host checks; a layout the GPU's four-line checks reject late in the file makes the stream restart
+    with the sequential cutter after blocks were already scanned, so the counters AND the EM histogram must have
+    been cleared first. Counters, EM histogram and statistics equal the sequential run (SPEQ_SPLIT_CUT=0) and the
+    in-memory scan; a malformed file raises the sequential reader's error."""
+    ref = synth.make_reference(4, 2, 20_000)
+    reads = synth.make_reads(ref, 120_000, read_len=100, n_rate=0.001, lowq_rate=0.01)
+    seqs, quals = split(reads)
+    p = tmp_path / "r.fq"
+    write_fastq(p, seqs, quals, crlf=case == "crlf")
+    data = p.read_bytes()
+    cut = data.index(b"\n@read", len(data) * 5 // 6) + 1
+    extra = {"wrapped_late": b"@w\nACGTACGTAC\nGTACGTACGT\n+\nIIIIIIIIII\nIIIIIIIIII\n", "blank_late": b"\n",
+             "error_late": b"@e\nACGT\n+\nII\n", "plus_base_line": b"@p\n+ACGT\n+\nIIIII\n"}.get(case)
+    if extra:
+        data = data[:cut] + extra + data[cut:]
+    if case == "blank_tail":
+        data += b"\n\n"
+    if case == "no_final_newline":
+        data = data[:-1]
+    p.write_bytes(data)
+    dev = DeviceIndex(FmIndex.build(ref.records, ref.groups, 4, prefix_q=10, pair_steps=True, triple_steps=True))
+    if case in ("error_late", "plus_base_line"):
+        for split_cut in ("1", "0"):
+            monkeypatch.setenv("SPEQ_SPLIT_CUT", split_cut)
+            with pytest.raises(SpeqError, match="mismatch" if case == "error_late" else "malformed"):
+                dev.scan_fastq(str(p), k=21, threads=6)
+        return
+    emx = EmHistogram(dev)
+    exp = emx.scan(reads.seq.tobytes(), reads.qual.tobytes(), reads.offsets, k=21)
+    emx.finalize()
+    got = {}
+    for split_cut in ("1", "0"):
+        monkeypatch.setenv("SPEQ_SPLIT_CUT", split_cut)
+        em = EmHistogram(dev)
+        r, st = dev.scan_fastq(str(p), k=21, em=em, threads=6)
+        em.finalize()
+        got[split_cut] = (r, st, em.info())
+    same(got["1"][0], got["0"][0], False)
+    n_extra = 1 if case == "wrapped_late" else 0
+    assert got["1"][1]["records"] == got["0"][1]["records"] == reads.n + n_extra
+    assert got["1"][1]["bases"] == got["0"][1]["bases"] == int(reads.offsets[-1]) + 20 * n_extra
+    assert got["1"][2] == got["0"][2]
+    same(got["1"][0], exp, False)  # the extra record is shorter than k
+    assert got["1"][2] == emx.info()
