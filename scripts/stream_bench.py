@@ -25,6 +25,7 @@ def main():
     ap.add_argument("--threads", default="1,4,8,16")
     ap.add_argument("--gz", type=int, default=1)
     ap.add_argument("--split", default="1,0", help="SPEQ_SPLIT_CUT values for the plain-file runs")
+    ap.add_argument("--paired", type=int, default=1, help="also time two-file paired streaming")
     ap.add_argument("--lanes", default="", help="stream_lanes values to sweep (default: the device default)")
     ap.add_argument("--dir", default=os.environ.get("TMPDIR", "/tmp"))
     ap.add_argument("--out", default="")
@@ -84,6 +85,41 @@ def main():
                   "kmers_per_s": kmers / best["seconds"], "MB_per_s_file": size / best["seconds"] / 1e6,
                   "batches": best["batches"]})
     os.environ.pop("SPEQ_SPLIT_CUT", None)
+    if a.paired:  # the same reads as mate pairs in two files (150 + 150 bp), k-mers of both mates
+        preads = synth.make_reads(ref, 2 * (a.reads // 2), paired=True)
+        plens = np.diff(preads.offsets).astype(np.int64)
+        pk = int(np.maximum(plens - k + 1, 0).sum())
+        pseq, pqual = preads.seq.tobytes(), preads.qual.tobytes()
+        rp = dev.scan(pseq, pqual, preads.offsets, k=k, paired=True)
+        paths = [path + ".1", path + ".2"]
+        for m, pp in enumerate(paths):
+            with open(pp, "wb") as f:
+                parts = []
+                for j in range(m, preads.n, 2):
+                    s0, s1 = int(preads.offsets[j]), int(preads.offsets[j + 1])
+                    parts.append(b"@r%d/%d\n%s\n+\n%s\n" % (j // 2, m + 1, pseq[s0:s1], pqual[s0:s1]))
+                f.write(b"".join(parts))
+        psize = sum(os.path.getsize(pp) for pp in paths)
+        th = max(int(x) for x in a.threads.split(","))
+        for split_cut in a.split.split(","):
+            os.environ["SPEQ_SPLIT_CUT"] = split_cut
+            best = None
+            for _ in range(3):
+                r5, st = dev.scan_fastq(paths[0], paths[1], k=k, threads=th)
+                best = st if best is None or st["seconds"] < best["seconds"] else best
+            assert r5.total == rp.total and r5.unique.tolist() == rp.unique.tolist()
+            d = {"path": "fastq paired (speq_scan_fastq, two plain files, page cache)", "threads": th,
+                 "cut": "parallel" if split_cut != "0" else "sequential", "seconds": best["seconds"],
+                 "kmers_per_s": pk / best["seconds"], "MB_per_s_file": psize / best["seconds"] / 1e6,
+                 "batches": best["batches"]}
+            d.update({"config": a.config, "reads": preads.n, "kmers": pk})
+            print(json.dumps(d), flush=True)
+            if out:
+                out.write(json.dumps(d) + "\n")
+                out.flush()
+        os.environ.pop("SPEQ_SPLIT_CUT", None)
+        for pp in paths:
+            os.remove(pp)
     if a.gz:
         gpath = path + ".gz"
         with open(path, "rb") as f, gzip.open(gpath, "wb", compresslevel=1) as g:

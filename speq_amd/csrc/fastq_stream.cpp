@@ -26,6 +26,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <deque>
+#include <exception>
 #include <memory>
 #include <mutex>
 #include <stdexcept>
@@ -659,6 +660,122 @@ struct StreamTotals {
     uint64_t records = 0, bases = 0, batches = 0;
 };
 
+// Offset just past the k-th '\n' of [p, p + n) (k >= 1), or n when there are fewer.
+size_t skip_lines(const char* p, size_t n, uint64_t k) {
+    const __m128i nl = _mm_set1_epi8('\n');
+    size_t i = 0;
+    for (; i + 16 <= n; i += 16) {
+        const uint32_t m = (uint32_t)_mm_movemask_epi8(
+            _mm_cmpeq_epi8(_mm_loadu_si128(reinterpret_cast<const __m128i*>(p + i)), nl));
+        const uint32_t c = (uint32_t)__builtin_popcount(m);
+        if (c < k) {
+            k -= c;
+            continue;
+        }
+        uint32_t mm = m;
+        for (uint64_t j = 1; j < k; ++j) mm &= mm - 1;
+        return i + (size_t)__builtin_ctz(mm) + 1;
+    }
+    for (; i < n; ++i)
+        if (p[i] == '\n' && --k == 0) return i + 1;
+    return n;
+}
+
+uint64_t count_nl(const char* p, size_t n) {
+    const __m128i nl = _mm_set1_epi8('\n');
+    uint64_t c = 0;
+    size_t i = 0;
+    for (; i + 16 <= n; i += 16)
+        c += (uint64_t)__builtin_popcount((uint32_t)_mm_movemask_epi8(
+            _mm_cmpeq_epi8(_mm_loadu_si128(reinterpret_cast<const __m128i*>(p + i)), nl)));
+    for (; i < n; ++i) c += p[i] == '\n';
+    return c;
+}
+
+// Block bounds of a mapped file for the parallel cut: 0, guessed record starts ~32 k records apart, len.
+std::vector<size_t> split_bounds(const char* data, size_t len, uint64_t block_records, uint64_t block_bytes) {
+    uint64_t target = block_bytes;
+    size_t p = 0, end = 0, sl = 0;
+    uint32_t i = 0;
+    for (; i < 256 && fast_record(data, len, p, true, end, sl); ++i) p = end;
+    if (i == 0) throw NotSimple();
+    target = std::min<uint64_t>(block_bytes, std::max<uint64_t>(1u << 20, p / i * block_records));
+    std::vector<size_t> b{0};
+    while (b.back() < len) b.push_back(len - b.back() <= target ? len : find_cut(data, len, b.back() + target));
+    return b;
+}
+
+// Runs fn(i) for i < n on `threads` threads; rethrows the first exception.
+template <class F>
+void parallel_for(uint32_t threads, size_t n, F&& fn) {
+    std::atomic<size_t> next{0};
+    std::atomic<bool> stop{false};
+    std::exception_ptr err;
+    std::mutex mu;
+    auto worker = [&] {
+        try {
+            for (size_t i; !stop && (i = next++) < n;) fn(i);
+        } catch (...) {
+            std::lock_guard<std::mutex> lk(mu);
+            if (!err) err = std::current_exception();
+            stop = true;
+        }
+    };
+    std::vector<std::thread> ts;
+    for (uint32_t t = 1; t < std::min<size_t>(threads, n); ++t) ts.emplace_back(worker);
+    worker();
+    for (auto& t : ts) t.join();
+    if (err) std::rethrow_exception(err);
+}
+
+// Paired parallel cut (plain mapped files, GPU parsing): both files are cut at guessed record starts, the newlines
+// of every block are counted in parallel (records per block = lines / 4), and each file-1 block is paired with the
+// same record range of file 2, located by counting lines inside one file-2 block. The GPU checks every line group of
+// both files, so any layout this does not fit fails there (or here) and the caller runs the sequential reader.
+// Files with different record counts also go to the sequential reader (its zip rule and read-ahead decide).
+StreamTotals run_paired_split(const std::shared_ptr<Buf>& m1, const std::shared_ptr<Buf>& m2, uint32_t threads,
+                              Sink& sink) {
+    const uint64_t BLOCK_RECORDS = 1u << 15, BLOCK_BYTES = 12ull << 20;
+    const char* d1 = m1->data();
+    const char* d2 = m2->data();
+    const std::vector<size_t> b1 = split_bounds(d1, m1->len, BLOCK_RECORDS, BLOCK_BYTES);
+    const std::vector<size_t> b2 = split_bounds(d2, m2->len, BLOCK_RECORDS, BLOCK_BYTES);
+    const size_t n1 = b1.size() - 1, n2 = b2.size() - 1;
+    std::vector<uint64_t> recs(n1 + n2 + 2, 0);  // records per block, then exclusive sums per file
+    parallel_for(threads, n1 + n2, [&](size_t i) {
+        const bool f2 = i >= n1;
+        const char* d = f2 ? d2 : d1;
+        const std::vector<size_t>& b = f2 ? b2 : b1;
+        const size_t j = f2 ? i - n1 : i, len = (f2 ? m2 : m1)->len;
+        uint64_t lines = count_nl(d + b[j], b[j + 1] - b[j]);
+        if (b[j + 1] == len && d[len - 1] != '\n') ++lines;
+        if (lines == 0 || lines % 4 != 0) throw NotSimple();
+        recs[i] = lines / 4;
+    });
+    std::vector<uint64_t> r1(n1 + 1, 0), r2(n2 + 1, 0);
+    for (size_t j = 0; j < n1; ++j) r1[j + 1] = r1[j] + recs[j];
+    for (size_t j = 0; j < n2; ++j) r2[j + 1] = r2[j] + recs[n1 + j];
+    if (r1[n1] != r2[n2]) throw NotSimple();
+    auto offset2 = [&](uint64_t r) -> size_t {  // byte offset of record r of file 2
+        const size_t j = (size_t)(std::upper_bound(r2.begin(), r2.end(), r) - r2.begin()) - 1;
+        if (j >= n2) return m2->len;
+        if (r == r2[j]) return b2[j];
+        return b2[j] + skip_lines(d2 + b2[j], b2[j + 1] - b2[j], 4 * (r - r2[j]));
+    };
+    std::atomic<uint64_t> batches{0};
+    parallel_for(threads, n1, [&](size_t i) {
+        const size_t s2 = offset2(r1[i]), e2 = offset2(r1[i + 1]);
+        const uint64_t l1 = b1[i + 1] - b1[i], l2 = e2 - s2, n = r1[i + 1] - r1[i];
+        speq_slot s;
+        sink.acquire(s, l1 + l2, 1);
+        std::memcpy(s.seq, d1 + b1[i], l1);
+        std::memcpy(s.seq + l1, d2 + s2, l2);
+        sink.submit_raw(s, l1, l2, n, true);
+        batches += 1;
+    });
+    return {2 * r1[n1], 0, batches.load()};
+}
+
 // Reader thread (cutting blocks of both files in step) + n_parsers parser threads feeding `sink`. With `split`, a
 // mapped single-end file is cut at guessed record starts (find_cut, no per-record work on the reader) and each
 // parser checks that its block is a chain of four-line records from its first byte to its last; since block 0
@@ -670,9 +787,14 @@ StreamTotals run_stream(const char* path1, const char* path2, uint32_t threads, 
     const uint32_t n_parsers = std::max<uint32_t>(1, std::min<uint32_t>(threads ? threads : 1, 64));
     const uint64_t BLOCK_RECORDS = 1u << 15, BLOCK_BYTES = 12ull << 20;  // pipeline slots hold SLOT_BYTES
     // opened here so that a missing file fails before any thread starts
-    Cutter c1(path1, threads, !split || paired);
+    const bool try_split = split && (!paired || gpu_parse);
+    Cutter c1(path1, threads, !try_split);
     std::unique_ptr<Cutter> c2;
-    if (paired) c2 = std::make_unique<Cutter>(path2, threads);
+    if (paired) c2 = std::make_unique<Cutter>(path2, threads, !try_split);
+    if (try_split && paired) {
+        std::shared_ptr<Buf> m1 = c1.mapping(), m2 = c2->mapping();
+        if (m1 && m2) return run_paired_split(m1, m2, n_parsers, sink);
+    }
     Shared sh;
     sh.max_q = n_parsers + 1;
     const std::shared_ptr<Buf> map = split && !paired ? c1.mapping() : nullptr;
@@ -873,7 +995,7 @@ extern "C" int speq_scan_fastq(speq_device_index* d, const char* path1, const ch
                 StreamTotals t = run_stream(path1, path2, threads, sink, gpu_parse, split);
                 // split blocks are parsed on the GPU unchecked by the host: any failed check means a layout the
                 // parallel cut cannot handle (or a malformed file) -> sequential run, which reports real errors
-                if (split && gpu_parse && !paired && speq::pipeline_take_parse_errors(pl)) throw NotSimple();
+                if (split && gpu_parse && speq::pipeline_take_parse_errors(pl)) throw NotSimple();
                 return t;
             } catch (...) {  // drain the pipeline and zero its counters
                 std::vector<uint64_t> scratch(SPEQ_COUNTS_LEN(speq::device_groups(d)));

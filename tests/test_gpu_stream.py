@@ -289,3 +289,62 @@ def test_parallel_cut_stream_and_restart(tmp_path, monkeypatch, case):
     assert got["1"][2] == got["0"][2]
     same(got["1"][0], exp, False)  # the extra record is shorter than k
     assert got["1"][2] == emx.info()
+
+
+PAIRED_CASES = ["simple", "crlf", "no_final_newline", "unequal", "wrapped_late_2", "blank_late_1", "error_late_2"]
+
+
+@pytest.mark.parametrize("case", PAIRED_CASES)
+def test_paired_parallel_cut(tmp_path, monkeypatch, case):
+    """Paired plain files are cut in parallel, newlines counted per block, and each file-1 block is paired with the
+    same records of file 2; layouts the GPU checks reject, or files of different record counts, restart with the
+    sequential reader. Counters, EM histogram and statistics equal the sequential run and the in-memory scan."""
+    ref = synth.make_reference(4, 2, 20_000)
+    reads = synth.make_reads(ref, 160_000, paired=True, n_rate=0.001, lowq_rate=0.01)
+    seqs, quals = split(reads)
+    p1, p2 = tmp_path / "r1.fq", tmp_path / "r2.fq"
+    write_fastq(p1, seqs[0::2], quals[0::2], crlf=case == "crlf")
+    write_fastq(p2, seqs[1::2], quals[1::2], crlf=case == "crlf")
+    n_pairs = reads.n // 2
+
+    def insert(path, extra):
+        data = path.read_bytes()
+        cut = data.index(b"\n@read", len(data) * 5 // 6) + 1
+        path.write_bytes(data[:cut] + extra + data[cut:])
+
+    if case == "no_final_newline":
+        p2.write_bytes(p2.read_bytes()[:-1])
+    elif case == "unequal":
+        data = p2.read_bytes()
+        cut = data.index(b"\n@read", len(data) * 3 // 4) + 1
+        p2.write_bytes(data[:cut])
+        n_pairs = data[:cut].count(b"\n@read") + 1
+    elif case == "wrapped_late_2":
+        insert(p2, b"@w\nACGTACGTAC\nGTACGTACGT\n+\nIIIIIIIIII\nIIIIIIIIII\n")
+    elif case == "blank_late_1":
+        insert(p1, b"\n")
+    elif case == "error_late_2":
+        insert(p2, b"@e\nACGT\n+\nII\n")
+    dev = DeviceIndex(FmIndex.build(ref.records, ref.groups, 4, prefix_q=10, pair_steps=True, triple_steps=True))
+    if case == "error_late_2":
+        for split_cut in ("1", "0"):
+            monkeypatch.setenv("SPEQ_SPLIT_CUT", split_cut)
+            with pytest.raises(SpeqError, match="mismatch"):
+                dev.scan_fastq(str(p1), str(p2), k=21, threads=6)
+        return
+    got = {}
+    for split_cut in ("1", "0"):
+        monkeypatch.setenv("SPEQ_SPLIT_CUT", split_cut)
+        em = EmHistogram(dev)
+        r, st = dev.scan_fastq(str(p1), str(p2), k=21, em=em, threads=6)
+        em.finalize()
+        got[split_cut] = (r, st, em.info())
+    same(got["1"][0], got["0"][0], False)
+    assert got["1"][1]["records"] == got["0"][1]["records"]
+    assert got["1"][1]["bases"] == got["0"][1]["bases"]
+    assert got["1"][2] == got["0"][2]
+    if case != "wrapped_late_2":  # the inserted record shifts the pairing after it
+        assert got["1"][1]["records"] == 2 * n_pairs
+        m = 2 * n_pairs
+        exp = dev.scan(reads.seq.tobytes(), reads.qual.tobytes(), reads.offsets[:m + 1], k=21, paired=True)
+        same(got["1"][0], exp, False)
