@@ -41,7 +41,7 @@ $(OBJDIR)/%.o: speq_amd/csrc/%.cpp $(HDRS)
 	$(CXX) $(HOSTFLAGS) -c $< -o $@
 
 $(LIB): $(LIB_OBJS)
-	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $^ -L/opt/rocm/lib -lrccl -lamdhip64 -lz -lpthread \
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $^ -L/opt/rocm/lib -lamdhip64 -lz -lpthread -ldl \
 	    -Wl,-rpath,/opt/rocm/lib
 
 $(CLI): $(CLI_CPP) $(LIB) $(HDRS) speq_amd/cli/*.hpp
@@ -57,7 +57,7 @@ variant: $(filter-out $(OBJDIR)/scan_kernels.o,$(LIB_OBJS))
 	@mkdir -p build/variants/$(NAME)
 	$(HIPCC) $(HIPFLAGS) $(VFLAGS) -c speq_amd/csrc/scan_kernels.hip -o build/variants/$(NAME)/scan_kernels.o
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o build/variants/$(NAME)/libspeq_scan.so \
-	    build/variants/$(NAME)/scan_kernels.o $^ -L/opt/rocm/lib -lrccl -lamdhip64 -lz -lpthread -Wl,-rpath,/opt/rocm/lib
+	    build/variants/$(NAME)/scan_kernels.o $^ -L/opt/rocm/lib -lamdhip64 -lz -lpthread -ldl -Wl,-rpath,/opt/rocm/lib
 
 clean:
 	rm -rf build bin $(LIB)

@@ -46,18 +46,23 @@ def main():
     lens = np.diff(reads.offsets).astype(np.int64)
     kmers = int(np.maximum(lens - c["k"] + 1, 0).sum())
     speq = os.path.join(ROOT, "bin", "speq")
-    env = dict(os.environ, SPEQ_STREAM_STATS="1")
+    env = dict(os.environ, SPEQ_STREAM_STATS="1", SPEQ_CLI_TIMING="1")
 
     def run(args, label):
         t0 = time.perf_counter()
         p = subprocess.run([speq] + args, cwd=work, capture_output=True, text=True, env=env)
         dt = time.perf_counter() - t0
         stream = [ln for ln in p.stderr.splitlines() if ln.startswith("speq: streamed")]
+        phases = {}
+        for ln in p.stderr.splitlines():
+            if ln.startswith("speq: ") and ln.endswith(" s") and not ln.startswith("speq: streamed"):
+                name, sec = ln[6:-2].rsplit(None, 1)
+                phases[name.strip()] = float(sec)
         em_iters = p.stderr.count("\n\n")
         print(json.dumps({"config": a.config, "command": label, "rc": p.returncode, "seconds": dt,
                           "reads": reads.n, "kmers": kmers, "fastq_bytes": fq_bytes,
                           "kmers_per_s": kmers / dt if label.startswith("scan") else None,
-                          "stream": stream[0] if stream else None, "em_iterations": em_iters,
+                          "stream": stream[0] if stream else None, "em_iterations": em_iters, "phases": phases,
                           "stderr_tail": p.stderr[-300:] if p.returncode else None}), flush=True)
         return p.returncode
 

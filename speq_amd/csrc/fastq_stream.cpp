@@ -574,6 +574,8 @@ void check_rc(int rc) {
 struct Sink {
     virtual ~Sink() = default;
     virtual void acquire(speq_slot& s, uint64_t bytes, uint64_t records) = 0;
+    // a slot for raw text only (s.seq; submit_raw or submit(s, 0) next)
+    virtual void acquire_raw(speq_slot& s, uint64_t bytes) { acquire(s, bytes, 1); }
     virtual void submit(const speq_slot& s, uint64_t records) = 0;  // records == 0 releases the slot
     // raw four-line FASTQ text (file 1's block, then file 2's) in s.seq, n records per file
     virtual void submit_raw(const speq_slot& s, uint64_t len1, uint64_t len2, uint64_t n, bool paired) {
@@ -594,6 +596,11 @@ struct PipelineSink final : Sink {
                 check_rc(rc);
             }
         }
+    }
+    void acquire_raw(speq_slot& s, uint64_t bytes) override {
+        s = speq_slot{};
+        s.slot = speq::pipeline_acquire_raw(pl, bytes, &s.seq);
+        s.cap_bytes = bytes;
     }
     void submit(const speq_slot& s, uint64_t records) override { check_rc(speq_pipeline_submit(pl, s.slot, records)); }
     void submit_raw(const speq_slot& s, uint64_t len1, uint64_t len2, uint64_t n, bool paired) override {
@@ -767,7 +774,7 @@ StreamTotals run_paired_split(const std::shared_ptr<Buf>& m1, const std::shared_
         const size_t s2 = offset2(r1[i]), e2 = offset2(r1[i + 1]);
         const uint64_t l1 = b1[i + 1] - b1[i], l2 = e2 - s2, n = r1[i + 1] - r1[i];
         speq_slot s;
-        sink.acquire(s, l1 + l2, 1);
+        sink.acquire_raw(s, l1 + l2);
         std::memcpy(s.seq, d1 + b1[i], l1);
         std::memcpy(s.seq + l1, d2 + s2, l2);
         sink.submit_raw(s, l1, l2, n, true);
@@ -877,7 +884,7 @@ StreamTotals run_stream(const char* path1, const char* path2, uint32_t threads, 
                     const uint64_t l1 = w.b1.size();
                     const bool eof = w.b1.end == w.b1.buf->len;
                     speq_slot s;
-                    sink.acquire(s, l1, 1);  // raw submits use no host offsets
+                    sink.acquire_raw(s, l1);
                     uint64_t lines = copy_count_nl(reinterpret_cast<char*>(s.seq), w.b1.data(), l1);
                     if (eof && l1 && w.b1.data()[l1 - 1] != '\n') ++lines;
                     if (lines == 0 || lines % 4 != 0) {
@@ -905,7 +912,7 @@ StreamTotals run_stream(const char* path1, const char* path2, uint32_t threads, 
                 if (gpu_parse && w.b1.simple && w.n == w.b1.n && (!paired || (w.b2.simple && w.n == w.b2.n))) {
                     // raw four-line text straight to HBM; records are split on the GPU (fastq_gpu.hip)
                     const uint64_t l1 = w.b1.size(), l2 = w.b2.size();
-                    sink.acquire(s, l1 + l2, recs);
+                    sink.acquire_raw(s, l1 + l2);
                     std::memcpy(s.seq, w.b1.data(), l1);
                     if (paired) std::memcpy(s.seq + l1, w.b2.data(), l2);
                     sink.submit_raw(s, l1, l2, w.n, paired);

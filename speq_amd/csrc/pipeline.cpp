@@ -84,19 +84,28 @@ void free_buffers(Slot& s) {
     s.cap_bytes = s.cap_records = 0;
 }
 
-void alloc_buffers(Slot& s, uint64_t bytes, uint64_t records) {
-    free_buffers(s);
+// Grows the slot to at least (bytes, records); qualities (host + device) only when asked for or already there:
+// raw-text submits (GPU FASTQ parsing) use the base buffer alone, which halves the pinned memory of a FASTQ stream.
+void ensure_buffers(Slot& s, uint64_t bytes, uint64_t records, bool qual) {
     bytes = std::max<uint64_t>(bytes, 64);
     records = std::max<uint64_t>(records, 2);
-    hip_ok(hipHostMalloc(reinterpret_cast<void**>(&s.h_seq), bytes, hipHostMallocDefault), "hipHostMalloc");
-    hip_ok(hipHostMalloc(reinterpret_cast<void**>(&s.h_qual), bytes, hipHostMallocDefault), "hipHostMalloc");
-    hip_ok(hipHostMalloc(reinterpret_cast<void**>(&s.h_off), (records + 1) * 8, hipHostMallocDefault),
-           "hipHostMalloc");
-    hip_ok(hipMalloc(reinterpret_cast<void**>(&s.d_seq), bytes + 64), "hipMalloc");  // GPU parse reads 16-B windows
-    hip_ok(hipMalloc(reinterpret_cast<void**>(&s.d_qual), bytes), "hipMalloc");
-    hip_ok(hipMalloc(reinterpret_cast<void**>(&s.d_off), (records + 1) * 8), "hipMalloc");
-    s.cap_bytes = bytes;
-    s.cap_records = records;
+    if (bytes > s.cap_bytes || records > s.cap_records) {
+        bytes = std::max(bytes, s.cap_bytes);
+        records = std::max(records, s.cap_records);
+        qual = qual || s.h_qual;
+        free_buffers(s);
+        hip_ok(hipHostMalloc(reinterpret_cast<void**>(&s.h_seq), bytes, hipHostMallocDefault), "hipHostMalloc");
+        hip_ok(hipHostMalloc(reinterpret_cast<void**>(&s.h_off), (records + 1) * 8, hipHostMallocDefault),
+               "hipHostMalloc");
+        hip_ok(hipMalloc(reinterpret_cast<void**>(&s.d_seq), bytes + 64), "hipMalloc");  // GPU parse: 16-B windows
+        hip_ok(hipMalloc(reinterpret_cast<void**>(&s.d_off), (records + 1) * 8), "hipMalloc");
+        s.cap_bytes = bytes;
+        s.cap_records = records;
+    }
+    if (qual && !s.h_qual) {
+        hip_ok(hipHostMalloc(reinterpret_cast<void**>(&s.h_qual), s.cap_bytes, hipHostMallocDefault), "hipHostMalloc");
+        hip_ok(hipMalloc(reinterpret_cast<void**>(&s.d_qual), s.cap_bytes), "hipMalloc");
+    }
 }
 
 }  // namespace
@@ -112,7 +121,8 @@ struct speq_pipeline {
     size_t next_lane = 0;                           // under submit_mu
     uint64_t* d_counts = nullptr;
     double* d_w = nullptr;
-    std::vector<Slot> slots;
+    std::vector<Slot> slots;    // buffers allocated on first acquire (ensure_buffers)
+    uint64_t slot_bytes = 0, slot_records = 0;
     std::mutex mu;              // free list
     std::condition_variable cv;
     std::deque<int> free_slots;
@@ -176,11 +186,12 @@ int speq_pipeline_create(speq_device_index* d, const speq_scan_params* params, s
         hip_ok(hipMalloc(reinterpret_cast<void**>(&pl->d_w), std::max<uint32_t>(pl->G, 1) * 8), "hipMalloc");
         hip_ok(hipMemsetAsync(pl->d_w, 0, std::max<uint32_t>(pl->G, 1) * 8, pl->compute), "hipMemset");
         pl->slots.resize(n_slots);
+        pl->slot_bytes = slot_bytes;
+        pl->slot_records = slot_records;
         for (uint32_t i = 0; i < n_slots; ++i) {
             Slot& s = pl->slots[i];
             hip_ok(hipEventCreateWithFlags(&s.copied, hipEventDisableTiming), "hipEventCreate");
             hip_ok(hipEventCreateWithFlags(&s.done, hipEventDisableTiming), "hipEventCreate");
-            alloc_buffers(s, slot_bytes, slot_records);
             pl->free_slots.push_back((int)i);
         }
         hip_ok(hipStreamSynchronize(pl->compute), "hipStreamSynchronize");
@@ -188,21 +199,45 @@ int speq_pipeline_create(speq_device_index* d, const speq_scan_params* params, s
     });
 }
 
-int speq_pipeline_acquire(speq_pipeline* pl, speq_slot* out) {
-    return speq::guarded([&] {
-        if (!pl || !out) throw std::invalid_argument("speq_pipeline_acquire: null argument");
-        int i;
-        {
-            std::unique_lock<std::mutex> lk(pl->mu);
-            pl->cv.wait(lk, [&] { return !pl->free_slots.empty(); });
-            i = pl->free_slots.front();
-            pl->free_slots.pop_front();
-        }
+}  // extern "C"
+
+namespace {
+// Next free slot (waits), its previous batch finished, buffers of at least (bytes, records) and qualities if asked.
+int take_slot(speq_pipeline* pl, uint64_t bytes, uint64_t records, bool qual) {
+    int i;
+    {
+        std::unique_lock<std::mutex> lk(pl->mu);
+        pl->cv.wait(lk, [&] { return !pl->free_slots.empty(); });
+        i = pl->free_slots.front();
+        pl->free_slots.pop_front();
+    }
+    try {
         Slot& s = pl->slots[(size_t)i];
         if (s.pending) {
             hip_ok(hipEventSynchronize(s.done), "hipEventSynchronize");
             s.pending = false;
         }
+        DevScope g(pl->device);
+        ensure_buffers(s, bytes, records, qual);
+    } catch (...) {
+        {
+            std::lock_guard<std::mutex> lk(pl->mu);
+            pl->free_slots.push_back(i);
+        }
+        pl->cv.notify_one();
+        throw;
+    }
+    return i;
+}
+}  // namespace
+
+extern "C" {
+
+int speq_pipeline_acquire(speq_pipeline* pl, speq_slot* out) {
+    return speq::guarded([&] {
+        if (!pl || !out) throw std::invalid_argument("speq_pipeline_acquire: null argument");
+        const int i = take_slot(pl, pl->slot_bytes, pl->slot_records, true);
+        Slot& s = pl->slots[(size_t)i];
         out->seq = s.h_seq;
         out->qual = s.h_qual;
         out->offsets = s.h_off;
@@ -217,9 +252,9 @@ int speq_pipeline_reserve(speq_pipeline* pl, speq_slot* slot, uint64_t bytes, ui
         if (!pl || !slot || slot->slot < 0 || (size_t)slot->slot >= pl->slots.size())
             throw std::invalid_argument("speq_pipeline_reserve: bad slot");
         Slot& s = pl->slots[(size_t)slot->slot];
-        if (bytes > s.cap_bytes || records > s.cap_records) {
+        if (bytes > s.cap_bytes || records > s.cap_records || !s.h_qual) {
             DevScope g(pl->device);
-            alloc_buffers(s, std::max(bytes, s.cap_bytes), std::max(records, s.cap_records));
+            ensure_buffers(s, bytes, records, true);
         }
         slot->seq = s.h_seq;
         slot->qual = s.h_qual;
@@ -324,6 +359,12 @@ void pipeline_submit_raw(speq_pipeline* pl, int32_t slot, uint64_t len1, uint64_
     s.pending = true;
 }
 
+int32_t pipeline_acquire_raw(speq_pipeline* pl, uint64_t bytes, uint8_t** text) {
+    const int i = take_slot(pl, std::max(bytes, pl->slot_bytes), pl->slot_records, false);
+    *text = pl->slots[(size_t)i].h_seq;
+    return i;
+}
+
 uint32_t pipeline_take_parse_errors(speq_pipeline* pl) {
     DevScope g(pl->device);
     std::lock_guard<std::mutex> lk(pl->submit_mu);
@@ -392,11 +433,13 @@ speq_pipeline* take_pipeline(speq_device_index* d, const speq_scan_params* p, sp
             g_cache->erase(it);
             pl->p = *p;
             pl->em = em;
-            // grow small slots now, while nothing is in flight (a mid-stream reserve would stall the device)
+            // grow allocated slots now, while nothing is in flight (a mid-stream hipFree stalls the device)
+            pl->slot_bytes = std::max(pl->slot_bytes, bytes);
+            pl->slot_records = std::max(pl->slot_records, recs + (recs & 1));
             DevScope g(pl->device);
             for (Slot& s : pl->slots)
-                if (s.cap_bytes < bytes || s.cap_records < recs + (recs & 1))
-                    alloc_buffers(s, std::max(bytes, s.cap_bytes), std::max(recs + (recs & 1), s.cap_records));
+                if (s.h_seq && (s.cap_bytes < bytes || s.cap_records < recs + (recs & 1)))
+                    ensure_buffers(s, bytes, recs + (recs & 1), false);
             return pl;
         }
     }

@@ -29,6 +29,9 @@ void launch_fastq_parse(const uint8_t* d_raw, uint64_t len1, uint64_t len2, uint
 // Submits an acquired pipeline slot whose host buffer holds RAW four-line FASTQ text (file 1's block, then file
 // 2's when paired, n records each): copied as is, parsed on the GPU, then scanned (pipeline.cpp).
 void pipeline_submit_raw(speq_pipeline* pl, int32_t slot, uint64_t len1, uint64_t len2, uint64_t n, bool paired);
+// Acquires a slot for raw FASTQ text of up to `bytes` (no quality buffer; submit it with pipeline_submit_raw or
+// release it with speq_pipeline_submit(pl, slot, 0)); *text receives the pinned host buffer.
+int32_t pipeline_acquire_raw(speq_pipeline* pl, uint64_t bytes, uint8_t** text);
 // Waits for every submitted batch and returns (and clears) the GPU parse error flags raised so far (0 = none).
 uint32_t pipeline_take_parse_errors(speq_pipeline* pl);
 // Bases parsed on the GPU by raw submits up to the last speq_pipeline_finish.
