@@ -348,3 +348,49 @@ def test_paired_parallel_cut(tmp_path, monkeypatch, case):
         m = 2 * n_pairs
         exp = dev.scan(reads.seq.tobytes(), reads.qual.tobytes(), reads.offsets[:m + 1], k=21, paired=True)
         same(got["1"][0], exp, False)
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_parallel_cut_fuzz(tmp_path, monkeypatch, seed):
+    """Random irregularities (blank lines, wrapped records, CRLF lines, quality lines opening with '@' or '+',
+    descriptions on the '+' line) dropped into a multi-block file at random places: the parallel cut (with its
+    fallback) and the sequential reader agree on counters, EM histogram and statistics, or raise the same error."""
+    rng = np.random.default_rng(1000 + seed)
+    ref = synth.make_reference(3, 2, 15_000)
+    reads = synth.make_reads(ref, 100_000, read_len=int(rng.integers(60, 200)), n_rate=0.002, lowq_rate=0.02,
+                             short_frac=0.05)
+    seqs, quals = split(reads)
+    recs = []
+    for i, (s, q) in enumerate(zip(seqs, quals)):
+        q = bytearray(q)
+        if q and rng.random() < 0.05:
+            q[0] = ord("@") if rng.random() < 0.5 else ord("+")
+        recs.append([b"@r%d" % i, s, b"+" if rng.random() < 0.7 else b"+r%d" % i, bytes(q)])
+    n_irr = int(rng.integers(0, 4))
+    for _ in range(n_irr):
+        j = int(rng.integers(len(recs) // 2, len(recs)))
+        kind = int(rng.integers(0, 3))
+        if kind == 0:
+            recs[j][0] = b"\n" + recs[j][0]  # blank line before the header
+        elif kind == 1 and len(recs[j][1]) > 10:
+            s, q = recs[j][1], recs[j][3]
+            recs[j][1] = s[:7] + b"\n" + s[7:]
+            recs[j][3] = q[:5] + b"\n" + q[5:]  # wrapped record
+        else:
+            recs[j][1] += b"\r"
+            recs[j][3] += b"\r"
+    data = b"".join(b"\n".join(r) + b"\n" for r in recs)
+    p = tmp_path / "f.fq"
+    p.write_bytes(data)
+    dev = DeviceIndex(FmIndex.build(ref.records, ref.groups, 3, prefix_q=8, pair_steps=True, triple_steps=True))
+    out = {}
+    for split_cut in ("1", "0"):
+        monkeypatch.setenv("SPEQ_SPLIT_CUT", split_cut)
+        em = EmHistogram(dev)
+        try:
+            r, st = dev.scan_fastq(str(p), k=19, em=em, threads=5)
+            em.finalize()
+            out[split_cut] = ((r.total, r.ambiguous, r.unique.tolist()), st["records"], st["bases"], em.info())
+        except SpeqError as e:
+            out[split_cut] = ("error", str(e))
+    assert out["1"] == out["0"]
