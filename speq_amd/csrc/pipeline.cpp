@@ -10,6 +10,7 @@
 #include <algorithm>
 #include <atomic>
 #include <condition_variable>
+#include <cstdlib>
 #include <cstring>
 #include <deque>
 #include <map>
@@ -415,7 +416,7 @@ void speq_pipeline_free(speq_pipeline* pl) { delete pl; }
 }  // extern "C"
 
 // ---- host-buffer scans (speq_scan_reads / speq_em_scan_reads) over the pipeline ----
-// Whole units are cut into batches of <= 32 MiB of bases; up to four filler threads copy batches into pinned slots
+// Whole units are cut into batches of <= 16 MiB of bases; up to four filler threads copy batches into pinned slots
 // (pageable -> pinned memcpy) and submit them, so the PCIe copy and the kernel of different batches overlap.
 namespace {
 // Idle host-scan pipelines per device (pinned allocation costs more than a typical scan); never destroyed at exit.
@@ -487,7 +488,9 @@ void scan_host_pipelined(speq_device_index* d, const uint8_t* seq, const uint8_t
     for (uint64_t i = 0; i < n_reads; ++i)
         if (offsets[i + 1] < offsets[i]) throw std::invalid_argument("speq_scan_reads: offsets must be non-decreasing");
     if (offsets[n_reads] > offsets[0] && (!seq || !qual)) throw std::invalid_argument("speq_scan_reads: null read buffer");
-    const uint64_t BATCH_BYTES = 32ull << 20, BATCH_RECORDS = 1u << 17;
+    // 16 MiB batches, four filler threads: 4-32 MiB x 4-8 fillers all land at 32-34 GB/s of host bytes on the box
+    // (profiles/r01/ab_host_batches.txt); 4 MiB loses to per-batch overheads.
+    const uint64_t BATCH_BYTES = 16ull << 20, BATCH_RECORDS = 1u << 16;
     const uint64_t step = p->paired ? 2 : 1;
     std::vector<std::pair<uint64_t, uint64_t>> batches;
     uint64_t max_bytes = 1, max_recs = step;
