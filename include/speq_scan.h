@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define SPEQ_ABI_VERSION 3
+#define SPEQ_ABI_VERSION 4
 
 enum {
     SPEQ_OK = 0,
@@ -230,6 +230,26 @@ int speq_scan_fastq(speq_device_index* d, const char* path1, const char* path2, 
  * order-independent digest = sum over records of mix64(FNV-1a-64 over (len, (base << 8 | qual) per position)). */
 int speq_fastq_checksum(const char* path1, const char* path2, uint32_t threads, uint64_t* records, uint64_t* bases,
                         uint64_t* digest);
+
+/* ---- several GPUs in one process ----
+ * Reads shard across the GPUs of a node, the index is replicated (one speq_device_index per GPU, opened from the
+ * same speq_index), and the only exchange is a sum of the counters. The reference sums its per-thread vectors after
+ * future.get() (fm_scanner.cpp:224-233, :1544-1557); here one host thread owns every replica, so the G + 2 counter
+ * words of each replica are added on the host, and the EM histograms (n words per replica) are added on the first
+ * replica's GPU (peer copy over xGMI + an add kernel). For one process per GPU use speq_allreduce_* (RCCL).
+ * Replicas may share a GPU (logical shards; results are the same). */
+/* speq_scan_fastq over n_devices replicas: record-aligned blocks are dealt to the replicas in turn. ems is NULL or
+ * holds one histogram per replica (ems[i] created on ds[i]); fold them with speq_em_merge before speq_em_finalize. */
+int speq_scan_fastq_multi(speq_device_index* const* ds, speq_em* const* ems, uint32_t n_devices, const char* path1,
+                          const char* path2, const speq_scan_params* params, uint32_t threads, uint64_t* counts,
+                          double* weights, speq_stream_stats* stats);
+/* speq_ref_unique with replica i scanning the i-th equal slice of the reference windows (the .dat pass sharded the
+ * same way as the reads; fm_scanner.cpp:1476-1560). */
+int speq_ref_unique_multi(speq_device_index* const* ds, uint32_t n_devices, uint32_t k, uint64_t* u_ref,
+                          uint64_t* tot_ref);
+/* dst += src for two unfinalized EM histograms of replicas of one index (any GPUs of this process). src's device
+ * arrays are released: afterwards src accepts only speq_em_free. */
+int speq_em_merge(speq_em* dst, speq_em* src);
 
 /* ---- groupings file (speq::file_to_map, /root/reference/src/file_to_map.cpp:20-119) ----
  * Same grammar "Name(count): i, j-k, …"; parse errors of single tokens are collected (the reference prints

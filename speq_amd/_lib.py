@@ -96,6 +96,10 @@ SIGNATURES = {
     "speq_pipeline_free": (None, [_P]),
     "speq_scan_fastq": (C.c_int, [_P, C.c_char_p, C.c_char_p, C.POINTER(ScanParams), _P, C.c_uint32, _U64P, _F64P,
                                   C.POINTER(StreamStats)]),
+    "speq_scan_fastq_multi": (C.c_int, [C.POINTER(_P), C.POINTER(_P), C.c_uint32, C.c_char_p, C.c_char_p,
+                                        C.POINTER(ScanParams), C.c_uint32, _U64P, _F64P, C.POINTER(StreamStats)]),
+    "speq_ref_unique_multi": (C.c_int, [C.POINTER(_P), C.c_uint32, C.c_uint32, _U64P, _U64P]),
+    "speq_em_merge": (C.c_int, [_P, _P]),
     "speq_fastq_checksum": (C.c_int, [C.c_char_p, C.c_char_p, C.c_uint32, _U64P, _U64P, _U64P]),
     "speq_groupings_parse": (C.c_int, [C.c_char_p, C.POINTER(_P)]),
     "speq_groupings_n_groups": (C.c_uint32, [_P]),
@@ -112,7 +116,7 @@ SIGNATURES = {
 }
 
 _lib = None
-ABI_VERSION = 3  # include/speq_scan.h SPEQ_ABI_VERSION (struct layouts above)
+ABI_VERSION = 4  # include/speq_scan.h SPEQ_ABI_VERSION (struct layouts above)
 
 
 def lib() -> C.CDLL:

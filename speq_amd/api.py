@@ -23,7 +23,7 @@ import numpy as np
 from ._lib import (SPEQ_MODE_GLOBAL, SPEQ_MODE_LOCAL, BuildOpts, IndexInfo, ScanParams, Slot, SpeqError,  # noqa: F401
                    StreamStats, check, lib)
 
-__all__ = ["FmIndex", "DeviceIndex", "Pipeline", "ScanResult", "Groupings", "EmHistogram", "file_to_map", "unique_to_percent",
+__all__ = ["FmIndex", "DeviceIndex", "Node", "Pipeline", "ScanResult", "Groupings", "EmHistogram", "file_to_map", "unique_to_percent",
            "em_refine", "pack_records", "SpeqError", "SPEQ_MODE_GLOBAL", "SPEQ_MODE_LOCAL"]
 
 
@@ -350,6 +350,63 @@ class EmHistogram:
             self.close()
         except Exception:
             pass
+
+
+class Node:
+    """Replicas of one FmIndex on several GPUs of this process (or logical shards on one GPU): SURVEY.md 8(e).
+
+    Reads shard across the replicas (speq_scan_fastq_multi), the .dat pass splits the reference windows
+    (speq_ref_unique_multi), and per-replica EM histograms fold into the first one (speq_em_merge)."""
+
+    def __init__(self, index: FmIndex, devices: Sequence[int]):
+        if not devices:
+            raise ValueError("Node needs at least one device")
+        self.index = index
+        self.devices = [DeviceIndex(index, d) for d in devices]
+        self.n_groups = self.devices[0].n_groups
+        n = len(self.devices)
+        self._arr = (C.c_void_p * n)(*[d.handle.value for d in self.devices])
+
+    def __len__(self):
+        return len(self.devices)
+
+    def em_histograms(self) -> list["EmHistogram"]:
+        return [EmHistogram(d) for d in self.devices]
+
+    def scan_fastq(self, path1: str, path2: Optional[str] = None, k: int = 21, phred_cutoff: int = 30,
+                   local: bool = False, threads: int = 4, ems: Optional[Sequence["EmHistogram"]] = None):
+        """speq_scan_fastq over every replica; returns (ScanResult, stats dict) of the whole node."""
+        G = self.n_groups
+        n = len(self.devices)
+        counts = np.zeros(G + 2, dtype=np.uint64)
+        w = np.zeros(G, dtype=np.float64) if local else None
+        p = ScanParams(k, phred_cutoff, int(path2 is not None), SPEQ_MODE_LOCAL if local else SPEQ_MODE_GLOBAL)
+        st = StreamStats()
+        em_arr = (C.c_void_p * n)(*[e._h.value for e in ems]) if ems is not None else None
+        check(lib().speq_scan_fastq_multi(self._arr, em_arr, n, path1.encode(), path2.encode() if path2 else None,
+                                          C.byref(p), threads, _u64p(counts),
+                                          w.ctypes.data_as(C.POINTER(C.c_double)) if w is not None else None,
+                                          C.byref(st)))
+        stats = {"records": st.records, "bases": st.bases, "batches": st.batches, "seconds": st.seconds}
+        return ScanResult(int(counts[0]), int(counts[1]), counts[2:].copy(), w), stats
+
+    def count_unique_kmers_per_group(self, k: int) -> tuple[np.ndarray, np.ndarray]:
+        G = self.n_groups
+        u = np.zeros(G, dtype=np.uint64)
+        t = np.zeros(G, dtype=np.uint64)
+        check(lib().speq_ref_unique_multi(self._arr, len(self.devices), k, _u64p(u), _u64p(t)))
+        return u, t
+
+    @staticmethod
+    def merge_em(ems: Sequence["EmHistogram"]) -> "EmHistogram":
+        """Folds ems[1:] into ems[0] (which is returned; the others accept only close())."""
+        for e in ems[1:]:
+            check(lib().speq_em_merge(ems[0]._h, e._h))
+        return ems[0]
+
+    def close(self):
+        for d in self.devices:
+            d.close()
 
 
 def em_refine(step, unique_totals, total, percent0, precision: float = 1e-6, max_iterations: int = 1000):

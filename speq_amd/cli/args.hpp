@@ -33,6 +33,8 @@ struct CmdArguments {  // include/arg_parse.h:10-28
     int gpu_build{-1};           // --gpu-build: -1 auto (GPU when one is visible), 0 host SA-IS, 1 GPU
     unsigned label_table{2};     // --label-table: per-position {group, run distance} table (2 = auto)
     int device{-1};              // --device: GPU ordinal (default: $LOCAL_RANK or 0)
+    int gpus{1};                 // --gpus: scan on GPUs 0..N-1 of this process (0 = every visible GPU)
+    std::vector<int> devices;    // --devices: explicit GPU ordinals (repeats = logical shards of one GPU)
     unsigned int max_em_iterations{1000};
 };
 

@@ -51,7 +51,9 @@ const char* HELP =
     "      --gpu-build auto|0|1  build the suffix array on the GPU (default auto: when one is visible)\n"
     "      --triple-steps auto|0|1 three-base LF planes in the FM-index (10.7 B per symbol; default auto:\n"
     "                            on below ~400 M symbols)\n"
-    "      --device N            GPU ordinal (default $LOCAL_RANK or 0)\n";
+    "      --device N            GPU ordinal (default $LOCAL_RANK or 0)\n"
+    "      --gpus N              scan: shard the reads over GPUs 0..N-1 (default 1; 0 = every visible GPU)\n"
+    "      --devices I,J,...     scan: shard the reads over these GPU ordinals (repeats allowed)\n";
 
 template <typename T>
 T to_number(const std::string& opt, const std::string& v) {
@@ -132,6 +134,17 @@ CmdArguments parse(int argc, char** argv) {
             else a.gpu_build = to_number<unsigned>(opt, v) != 0 ? 1 : 0;
         }
         else if (opt == "--device") a.device = to_number<int>(opt, value());
+        else if (allow_reads && opt == "--gpus") a.gpus = (int)to_number<unsigned>(opt, value());
+        else if (allow_reads && opt == "--devices") {
+            const std::string v = value();
+            a.devices.clear();
+            for (size_t b = 0; b <= v.size();) {
+                size_t e = v.find(',', b);
+                if (e == std::string::npos) e = v.size();
+                a.devices.push_back((int)to_number<unsigned>(opt, v.substr(b, e - b)));
+                b = e + 1;
+            }
+        }
         else if (allow_reads && opt == "--max-em-iterations") a.max_em_iterations = to_number<unsigned>(opt, value());
         else throw ParseError("Unknown option " + opt + ". In case this is meant to be a non-option/argument/parameter, "
                               "please specify the start of non-options with '--'.");
@@ -413,13 +426,40 @@ int run_scan(CmdArguments& a) {
     const size_t G = h.names.size();
     phase("index load");
 
-    int dev = a.device;
-    if (dev < 0) {
-        const char* lr = std::getenv("LOCAL_RANK");
-        dev = lr ? std::atoi(lr) : 0;
+    // GPUs: --devices list, --gpus N (0..N-1), or one (--device, $LOCAL_RANK, 0). Reads shard across them in-process
+    // (SURVEY 8(e)): one replica of the index per GPU, the counters summed at the end.
+    std::vector<int> devs = a.devices;
+    if (devs.empty() && a.gpus != 1) {
+        const int visible = speq_device_count();
+        const int n = a.gpus == 0 ? visible : a.gpus;
+        if (n < 1 || n > visible)
+            throw CApiError("--gpus " + std::to_string(a.gpus) + ": " + std::to_string(visible) + " GPU(s) visible");
+        for (int i = 0; i < n; ++i) devs.push_back(i);
     }
-    speq_device_index* d = nullptr;
-    ok(speq_device_open(idx, dev, &d), "opening the GPU");
+    if (devs.empty()) {
+        int dev = a.device;
+        if (dev < 0) {
+            const char* lr = std::getenv("LOCAL_RANK");
+            dev = lr ? std::atoi(lr) : 0;
+        }
+        devs.push_back(dev);
+    }
+    const uint32_t n_dev = (uint32_t)devs.size();
+    std::vector<speq_device_index*> ds(n_dev, nullptr);
+    {  // replicas are uploaded concurrently (one host thread per GPU)
+        std::vector<int> rcs(n_dev, SPEQ_OK);
+        std::vector<std::string> msgs(n_dev);
+        std::vector<std::thread> ts;
+        for (uint32_t i = 0; i < n_dev; ++i)
+            ts.emplace_back([&, i] {
+                rcs[i] = speq_device_open(idx, devs[i], &ds[i]);
+                if (rcs[i] != SPEQ_OK) msgs[i] = speq_last_error();
+            });
+        for (auto& t : ts) t.join();
+        for (uint32_t i = 0; i < n_dev; ++i)
+            if (rcs[i] != SPEQ_OK) throw CApiError("opening GPU " + std::to_string(devs[i]) + ": " + msgs[i]);
+    }
+    speq_device_index* d = ds[0];
     phase("device open");
 
     // Reference uniqueness per group, cached in <stem>_<k>mer.dat keyed by the index mtime.
@@ -429,7 +469,9 @@ int run_scan(CmdArguments& a) {
     if (!read_dat(dat, idx_mtime, G, u_ref, tot_ref)) {
         u_ref.assign(G, 0);
         tot_ref.assign(G, 0);
-        ok(speq_ref_unique(d, a.kmer, u_ref.data(), tot_ref.data()), "reference-uniqueness pass");
+        ok(n_dev == 1 ? speq_ref_unique(d, a.kmer, u_ref.data(), tot_ref.data())
+                      : speq_ref_unique_multi(ds.data(), n_dev, a.kmer, u_ref.data(), tot_ref.data()),
+           "reference-uniqueness pass");
         write_dat(dat, idx_mtime, u_ref, tot_ref);
         std::cerr << speq::format_vector(u_ref) << "\n" << speq::format_vector(tot_ref) << "\n";  // :1572-1573
     }
@@ -441,14 +483,16 @@ int run_scan(CmdArguments& a) {
     std::vector<uint64_t> counts(G + 2, 0);
     std::vector<double> weights(std::max<size_t>(G, 1), 0.0);
     // One scan also fills the EM histogram (the reference re-scans every read per EM iteration instead).
-    speq_em* em = nullptr;
-    ok(speq_em_create(idx, d, &em), "allocating the EM histogram");
+    std::vector<speq_em*> ems(n_dev, nullptr);
+    for (uint32_t i = 0; i < n_dev; ++i) ok(speq_em_create(idx, ds[i], &ems[i]), "allocating the EM histogram");
+    speq_em* em = ems[0];
     phase("EM histogram alloc");
     // FASTQ(.gz) streamed through pinned slots: -t parser threads, H2D overlapped with the kernel (fm_scanner.cpp:
     // 138-141 / :651-655 read through an async_input_buffer; paired files are zipped, stopping at the shorter one).
     speq_stream_stats st{};
-    ok(speq_scan_fastq(d, a.in_file_reads_path_1.c_str(), paired ? a.in_file_reads_path_2.c_str() : nullptr, &prm,
-                       em, a.threads, counts.data(), local ? weights.data() : nullptr, &st),
+    ok(speq_scan_fastq_multi(ds.data(), ems.data(), n_dev, a.in_file_reads_path_1.c_str(),
+                             paired ? a.in_file_reads_path_2.c_str() : nullptr, &prm, a.threads, counts.data(),
+                             local ? weights.data() : nullptr, &st),
        "scanning reads");
     phase("FASTQ stream + scan");
     if (const char* v = std::getenv("SPEQ_STREAM_STATS"); v && *v && *v != '0')
@@ -478,6 +522,10 @@ int run_scan(CmdArguments& a) {
     }
 
     // EM refinement (fm_scanner.cpp:248-279, :515-545, :761-792, :1035-1065) over the histogram.
+    for (uint32_t i = 1; i < n_dev; ++i) {
+        ok(speq_em_merge(em, ems[i]), "merging the EM histograms");
+        speq_em_free(ems[i]);
+    }
     ok(speq_em_finalize(em, a.threads), "building the EM histogram");
     phase("EM finalize");
     std::vector<uint64_t> unique(counts.begin() + 2, counts.end());

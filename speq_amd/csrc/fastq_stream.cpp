@@ -584,10 +584,19 @@ struct Sink {
     }
 };
 
+// Slots of one or more pipelines (one per GPU replica), dealt in turn: with equal GPUs every replica scans every
+// n-th block. The pipeline index travels in the slot id (slot * n + pipeline).
 struct PipelineSink final : Sink {
-    speq_pipeline* pl;
-    explicit PipelineSink(speq_pipeline* p) : pl(p) {}
+    std::vector<speq_pipeline*> pls;
+    std::atomic<uint64_t> next{0};
+    explicit PipelineSink(std::vector<speq_pipeline*> p) : pls(std::move(p)) {}
+    uint32_t pick() { return (uint32_t)(next++ % pls.size()); }
+    speq_pipeline* of(int32_t slot) const { return pls[(uint32_t)slot % pls.size()]; }
+    int32_t local(int32_t slot) const { return slot / (int32_t)pls.size(); }
+    int32_t global(int32_t slot, uint32_t i) const { return slot * (int32_t)pls.size() + (int32_t)i; }
     void acquire(speq_slot& s, uint64_t bytes, uint64_t records) override {
+        const uint32_t i = pick();
+        speq_pipeline* pl = pls[i];
         check_rc(speq_pipeline_acquire(pl, &s));
         if (bytes > s.cap_bytes || records > s.cap_records) {
             const int rc = speq_pipeline_reserve(pl, &s, bytes, records);
@@ -596,15 +605,19 @@ struct PipelineSink final : Sink {
                 check_rc(rc);
             }
         }
+        s.slot = global(s.slot, i);
     }
     void acquire_raw(speq_slot& s, uint64_t bytes) override {
+        const uint32_t i = pick();
         s = speq_slot{};
-        s.slot = speq::pipeline_acquire_raw(pl, bytes, &s.seq);
+        s.slot = global(speq::pipeline_acquire_raw(pls[i], bytes, &s.seq), i);
         s.cap_bytes = bytes;
     }
-    void submit(const speq_slot& s, uint64_t records) override { check_rc(speq_pipeline_submit(pl, s.slot, records)); }
+    void submit(const speq_slot& s, uint64_t records) override {
+        check_rc(speq_pipeline_submit(of(s.slot), local(s.slot), records));
+    }
     void submit_raw(const speq_slot& s, uint64_t len1, uint64_t len2, uint64_t n, bool paired) override {
-        speq::pipeline_submit_raw(pl, s.slot, len1, len2, n, paired);
+        speq::pipeline_submit_raw(of(s.slot), local(s.slot), len1, len2, n, paired);
     }
 };
 
@@ -976,57 +989,101 @@ bool split_cut_enabled() {
     return !(e && e[0] == '0');
 }
 
+
+// The FASTQ scan over n >= 1 replicas of one index (one per GPU of this process): blocks are dealt to the replicas'
+// pipelines in turn and each replica's counters accumulate on its own device; the sums over replicas are taken on
+// the host at the end (G + 2 words per replica; the EM histograms are merged by speq_em_merge).
+void scan_fastq_impl(speq_device_index* const* ds, speq_em* const* ems, uint32_t n_dev, const char* path1,
+                     const char* path2, const speq_scan_params* params, uint32_t threads, uint64_t* counts,
+                     double* weights, speq_stream_stats* stats) {
+    if (!ds || n_dev == 0 || !path1 || !params || !counts) throw std::invalid_argument("speq_scan_fastq: null argument");
+    if (params->mode == SPEQ_MODE_LOCAL && !weights)
+        throw std::invalid_argument("speq_scan_fastq: local mode needs weights");
+    const bool paired = path2 != nullptr;
+    if ((params->paired != 0) != paired)
+        throw std::invalid_argument("speq_scan_fastq: params->paired must match the presence of path2");
+    for (uint32_t i = 0; i < n_dev; ++i)
+        if (!ds[i] || speq::device_groups(ds[i]) != speq::device_groups(ds[0]) ||
+            speq::device_text_len(ds[i]) != speq::device_text_len(ds[0]))
+            throw std::invalid_argument("speq_scan_fastq_multi: replicas of different indexes");
+    const uint32_t G = speq::device_groups(ds[0]);
+    const auto t0 = std::chrono::steady_clock::now();
+    const uint32_t n_parsers = std::max<uint32_t>(1, std::min<uint32_t>(threads ? threads : 1, 64));
+    // one replica: parsers + 2 slots (up to 8); several: the same total spread over them, at least 3 each
+    const uint32_t want = std::min<uint32_t>(n_parsers, 6) + 2;
+    const uint32_t n_slots = n_dev == 1 ? want : std::max<uint32_t>(3, (want + n_dev - 1) / n_dev + 1);
+    std::vector<std::unique_ptr<speq_pipeline, void (*)(speq_pipeline*)>> guards;
+    std::vector<speq_pipeline*> pls;
+    for (uint32_t i = 0; i < n_dev; ++i) {
+        guards.emplace_back(speq::acquire_cached_pipeline(ds[i], params, ems ? ems[i] : nullptr,
+                                                          paired ? 2 * SLOT_BYTES : SLOT_BYTES,
+                                                          paired ? 2u << 15 : 1u << 15, n_slots),
+                            speq_pipeline_free);
+        pls.push_back(guards.back().get());
+    }
+    PipelineSink sink(pls);
+    bool gpu_parse = true;
+    for (uint32_t i = 0; i < n_dev; ++i) gpu_parse = gpu_parse && speq::device_fastq_gpu(ds[i]);
+    std::vector<uint64_t> scratch(SPEQ_COUNTS_LEN(G));
+    std::vector<double> wscratch(std::max<uint32_t>(G, 1));
+    auto attempt = [&](bool split) {
+        try {
+            StreamTotals t = run_stream(path1, path2, threads, sink, gpu_parse, split);
+            // split blocks are parsed on the GPU unchecked by the host: any failed check means a layout the
+            // parallel cut cannot handle (or a malformed file) -> sequential run, which reports real errors
+            if (split && gpu_parse) {
+                uint32_t err = 0;
+                for (speq_pipeline* pl : pls) err |= speq::pipeline_take_parse_errors(pl);
+                if (err) throw NotSimple();
+            }
+            return t;
+        } catch (...) {  // drain the pipelines and zero their counters
+            for (speq_pipeline* pl : pls) (void)speq_pipeline_finish(pl, scratch.data(), wscratch.data());
+            throw;
+        }
+    };
+    StreamTotals tot;
+    try {
+        tot = attempt(split_cut_enabled());
+    } catch (const NotSimple&) {
+        if (ems)
+            for (uint32_t i = 0; i < n_dev; ++i) speq::em_clear(ems[i]);
+        tot = attempt(false);
+    }
+    std::fill(counts, counts + SPEQ_COUNTS_LEN(G), 0);
+    if (weights) std::fill(weights, weights + G, 0.0);
+    for (uint32_t i = 0; i < n_dev; ++i) {  // replica order: the fp64 weight sums are deterministic
+        check_rc(speq_pipeline_finish(pls[i], scratch.data(), wscratch.data()));
+        for (size_t j = 0; j < scratch.size(); ++j) counts[j] += scratch[j];
+        if (weights && params->mode == SPEQ_MODE_LOCAL)
+            for (uint32_t g = 0; g < G; ++g) weights[g] += wscratch[g];
+        tot.bases += speq::pipeline_gpu_parsed_bases(pls[i]);
+    }
+    for (uint32_t i = 0; i < n_dev; ++i) speq::return_cached_pipeline(ds[i], guards[i].release());
+    if (stats) {
+        stats->records = tot.records;
+        stats->bases = tot.bases;
+        stats->batches = tot.batches;
+        stats->seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    }
+}
+
 }  // namespace
 
 extern "C" int speq_scan_fastq(speq_device_index* d, const char* path1, const char* path2,
                                const speq_scan_params* params, speq_em* em, uint32_t threads, uint64_t* counts,
                                double* weights, speq_stream_stats* stats) {
     return speq::guarded([&] {
-        if (!d || !path1 || !params || !counts) throw std::invalid_argument("speq_scan_fastq: null argument");
-        if (params->mode == SPEQ_MODE_LOCAL && !weights)
-            throw std::invalid_argument("speq_scan_fastq: local mode needs weights");
-        const bool paired = path2 != nullptr;
-        if ((params->paired != 0) != paired)
-            throw std::invalid_argument("speq_scan_fastq: params->paired must match the presence of path2");
-        const auto t0 = std::chrono::steady_clock::now();
-        const uint32_t n_parsers = std::max<uint32_t>(1, std::min<uint32_t>(threads ? threads : 1, 64));
-        std::unique_ptr<speq_pipeline, void (*)(speq_pipeline*)> pl_guard(
-            speq::acquire_cached_pipeline(d, params, em, paired ? 2 * SLOT_BYTES : SLOT_BYTES, paired ? 2u << 15 : 1u << 15,
-                                          std::min<uint32_t>(n_parsers, 6) + 2),
-            speq_pipeline_free);
-        speq_pipeline* pl = pl_guard.get();
-        PipelineSink sink(pl);
-        const bool gpu_parse = speq::device_fastq_gpu(d);
-        auto attempt = [&](bool split) {
-            try {
-                StreamTotals t = run_stream(path1, path2, threads, sink, gpu_parse, split);
-                // split blocks are parsed on the GPU unchecked by the host: any failed check means a layout the
-                // parallel cut cannot handle (or a malformed file) -> sequential run, which reports real errors
-                if (split && gpu_parse && speq::pipeline_take_parse_errors(pl)) throw NotSimple();
-                return t;
-            } catch (...) {  // drain the pipeline and zero its counters
-                std::vector<uint64_t> scratch(SPEQ_COUNTS_LEN(speq::device_groups(d)));
-                std::vector<double> wscratch(std::max<uint32_t>(speq::device_groups(d), 1));
-                (void)speq_pipeline_finish(pl, scratch.data(), wscratch.data());
-                throw;
-            }
-        };
-        StreamTotals tot;
-        try {
-            tot = attempt(split_cut_enabled());
-        } catch (const NotSimple&) {
-            speq::em_clear(em);
-            tot = attempt(false);
-        }
-        check_rc(speq_pipeline_finish(pl, counts, weights));
-        tot.bases += speq::pipeline_gpu_parsed_bases(pl);
-        speq::return_cached_pipeline(d, pl_guard.release());
-        if (stats) {
-            stats->records = tot.records;
-            stats->bases = tot.bases;
-            stats->batches = tot.batches;
-            stats->seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
-        }
+        speq_em* ems[1] = {em};
+        scan_fastq_impl(&d, em ? ems : nullptr, 1, path1, path2, params, threads, counts, weights, stats);
+    });
+}
+
+extern "C" int speq_scan_fastq_multi(speq_device_index* const* ds, speq_em* const* ems, uint32_t n_devices,
+                                     const char* path1, const char* path2, const speq_scan_params* params,
+                                     uint32_t threads, uint64_t* counts, double* weights, speq_stream_stats* stats) {
+    return speq::guarded([&] {
+        scan_fastq_impl(ds, ems, n_devices, path1, path2, params, threads, counts, weights, stats);
     });
 }
 

@@ -42,4 +42,5 @@ bool device_fastq_gpu(const speq_device_index* d);
 uint32_t device_stream_lanes(const speq_device_index* d);
 int device_ordinal(const speq_device_index* d);
 uint32_t device_groups(const speq_device_index* d);
+uint64_t device_text_len(const speq_device_index* d);  // FM text length n of the replica's index
 }  // namespace speq

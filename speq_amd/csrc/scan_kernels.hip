@@ -69,7 +69,8 @@ struct UnitSrc {
     uint32_t* em_mult;        // optional: per SA position, # passing multi-group windows whose interval starts there
     uint32_t* em_hi;          // optional: the end of that interval
     uint64_t n_units;         // reads (not pairs) or texts
-    uint64_t total_windows;   // ref only
+    uint64_t total_windows;   // ref only: windows of this launch (a shard of the flattened reference windows)
+    uint64_t win_base;        // ref only: first flattened window of the shard
     uint32_t end_adj;
     uint32_t k;
     uint32_t cutoff;
@@ -439,7 +440,8 @@ __global__ __launch_bounds__(BLOCK_THREADS, SPEQ_MIN_WAVES) void k_scan(DevView 
     const uint64_t gw = (uint64_t)blockIdx.x * WAVES_PER_BLOCK + wid;
     uint64_t r, r_end, o = 0, remaining;
     if (MODE == KM_REF) {
-        const uint64_t F0 = src.total_windows * gw / NW, F1 = src.total_windows * (gw + 1) / NW;
+        const uint64_t F0 = src.win_base + src.total_windows * gw / NW;
+        const uint64_t F1 = src.win_base + src.total_windows * (gw + 1) / NW;
         remaining = F1 - F0;
         uint64_t lo = 0, hi = src.n_units;  // largest t with cum_win[t] <= F0
         while (hi - lo > 1) {
@@ -930,6 +932,20 @@ static void scan_device_impl(speq_device_index* d, const uint8_t* d_seq, const u
 }
 
 
+// dst += src for the EM interval histogram; an interval's end is a function of its start, so a start that src
+// recorded takes src's end (dst's is either the same or unset). Grid-stride loop.
+__global__ void k_em_merge(uint32_t* __restrict__ dmult, uint32_t* __restrict__ dhi, const uint32_t* __restrict__ smult,
+                           const uint32_t* __restrict__ shi, uint64_t n) {
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        const uint32_t m = smult[i];
+        if (m) {
+            dmult[i] += m;
+            dhi[i] = shi[i];
+        }
+    }
+}
+
 extern "C" {
 
 int speq_device_count(void) {
@@ -1111,6 +1127,44 @@ int speq_em_finalize(speq_em* em, uint32_t threads) {
     });
 }
 
+// Adds the histogram `src` recorded on another replica (same index; any GPU of this process, or the same one) into
+// `dst`: src's arrays are copied to dst's device (peer copy over xGMI when the GPUs differ) and added by k_em_merge.
+// src stays usable for nothing but speq_em_free afterwards.
+int speq_em_merge(speq_em* dst, speq_em* src) {
+    return speq::guarded([&] {
+        if (!dst || !src || dst == src) throw std::invalid_argument("speq_em_merge: bad arguments");
+        if (dst->finalized || src->finalized || !src->d_mult)
+            throw std::invalid_argument("speq_em_merge: finalized or already merged histogram");
+        if (dst->n != src->n || dst->G != src->G) throw std::invalid_argument("speq_em_merge: histograms of different indexes");
+        {
+            DeviceGuard gs(src->dev->device);
+            HIP_OK(hipDeviceSynchronize());  // src's scans (any stream of its device) have completed
+        }
+        DeviceGuard g(dst->dev->device);
+        HIP_OK(hipDeviceSynchronize());
+        uint32_t *m = src->d_mult, *h = src->d_hi, *tmp = nullptr;
+        if (src->dev->device != dst->dev->device) {
+            HIP_OK(hipMalloc(&tmp, dst->n * 8));
+            m = tmp;
+            h = tmp + dst->n;
+            HIP_OK(hipMemcpyPeerAsync(m, dst->dev->device, src->d_mult, src->dev->device, dst->n * 4, dst->dev->stream));
+            HIP_OK(hipMemcpyPeerAsync(h, dst->dev->device, src->d_hi, src->dev->device, dst->n * 4, dst->dev->stream));
+        }
+        const uint64_t blocks = std::min<uint64_t>((dst->n + 1023) / 1024, 65536);
+        hipLaunchKernelGGL(k_em_merge, dim3((uint32_t)std::max<uint64_t>(blocks, 1)), dim3(256), 0, dst->dev->stream,
+                           dst->d_mult, dst->d_hi, m, h, dst->n);
+        HIP_OK(hipGetLastError());
+        HIP_OK(hipStreamSynchronize(dst->dev->stream));
+        if (tmp) HIP_OK(hipFree(tmp));
+        {
+            DeviceGuard gs(src->dev->device);
+            (void)hipFree(src->d_mult);
+            (void)hipFree(src->d_hi);
+        }
+        src->d_mult = src->d_hi = nullptr;
+    });
+}
+
 void speq_em_free(speq_em* em) {
     if (!em) return;
     if (em->d_mult) (void)hipFree(em->d_mult);
@@ -1118,36 +1172,110 @@ void speq_em_free(speq_em* em) {
     delete em;
 }
 
+}  // extern "C"
+
+namespace {
+// Enqueues the .dat pass over shard `shard` of `n_shards` equal slices of the flattened reference windows (every
+// text's fwd and rc windows in text order); the returned device buffer of window prefix sums must stay alive until
+// the launch completes (freed by the caller after synchronizing `st`).
+uint64_t* launch_ref_shard(speq_device_index* d, uint32_t k, uint32_t shard, uint32_t n_shards, uint64_t* d_u_ref,
+                           uint64_t* d_tot_ref, hipStream_t st) {
+    std::vector<uint64_t> cum(d->n_texts + 1, 0);
+    for (uint32_t t = 0; t < d->n_texts; ++t) {
+        const uint64_t L = d->text_start[t + 1] - d->text_start[t] - 1;  // minus separator
+        cum[t + 1] = cum[t] + (L >= k ? L - k + 1 : 0);
+    }
+    const uint64_t all = cum[d->n_texts];
+    const uint64_t w0 = all * shard / n_shards, w1 = all * (shard + 1) / n_shards;
+    if (w1 == w0) return nullptr;
+    uint64_t* d_cum = nullptr;
+    HIP_OK(hipMalloc(&d_cum, cum.size() * 8));
+    HIP_OK(hipMemcpyAsync(d_cum, cum.data(), cum.size() * 8, hipMemcpyHostToDevice, st));
+    UnitSrc src{};
+    src.seq = d->d_text;
+    src.off = d->d_text_start;
+    src.cum_win = d_cum;
+    src.unit_group = d->d_text_group;
+    src.n_units = d->n_texts;
+    src.total_windows = w1 - w0;
+    src.win_base = w0;
+    src.end_adj = 1;
+    src.k = k;
+    src.buf_bytes = staging_bytes(k, d->ilp);
+    launch_scan(d, KM_REF, false, src, (w1 - w0 + 255) / 256, st, reinterpret_cast<unsigned long long*>(d_u_ref),
+                reinterpret_cast<unsigned long long*>(d_tot_ref), nullptr);
+    return d_cum;
+}
+}  // namespace
+
+extern "C" {
+
 int speq_ref_unique_device(speq_device_index* d, uint32_t k, uint64_t* d_u_ref, uint64_t* d_tot_ref, void* stream) {
     return speq::guarded([&] {
         if (!d || !d_u_ref || !d_tot_ref) throw std::invalid_argument("speq_ref_unique_device: null argument");
         if (k < 1 || k > MAX_K) throw std::invalid_argument("speq_ref_unique_device: k must be in [1, 4096]");
         DeviceGuard g(d->device);
         hipStream_t st = static_cast<hipStream_t>(stream);  // NULL = the null (default) stream
-        std::vector<uint64_t> cum(d->n_texts + 1, 0);
-        for (uint32_t t = 0; t < d->n_texts; ++t) {
-            const uint64_t L = d->text_start[t + 1] - d->text_start[t] - 1;  // minus separator
-            cum[t + 1] = cum[t] + (L >= k ? L - k + 1 : 0);
-        }
-        const uint64_t total = cum[d->n_texts];
-        if (total == 0) return;
-        uint64_t* d_cum = nullptr;
-        HIP_OK(hipMalloc(&d_cum, cum.size() * 8));
-        HIP_OK(hipMemcpyAsync(d_cum, cum.data(), cum.size() * 8, hipMemcpyHostToDevice, st));
-        UnitSrc src{};
-        src.seq = d->d_text;
-        src.off = d->d_text_start;
-        src.cum_win = d_cum;
-        src.unit_group = d->d_text_group;
-        src.n_units = d->n_texts;
-        src.total_windows = total;
-        src.end_adj = 1;
-        src.k = k;
-        src.buf_bytes = staging_bytes(k, d->ilp);
-        launch_scan(d, KM_REF, false, src, (total + 255) / 256, st, reinterpret_cast<unsigned long long*>(d_u_ref),
-                    reinterpret_cast<unsigned long long*>(d_tot_ref), nullptr);
+        uint64_t* d_cum = launch_ref_shard(d, k, 0, 1, d_u_ref, d_tot_ref, st);
+        if (!d_cum) return;
         HIP_OK(hipStreamSynchronize(st));  // d_cum is freed below
         HIP_OK(hipFree(d_cum));
+    });
+}
+
+// Several replicas of one index (one per GPU of this process): replica i scans the i-th equal slice of the
+// reference windows on its own stream, all concurrently; the per-group sums are added on the host (SURVEY 8(e):
+// "the .dat pass shards reference records the same way" as the reads).
+int speq_ref_unique_multi(speq_device_index* const* ds, uint32_t n_devices, uint32_t k, uint64_t* u_ref,
+                          uint64_t* tot_ref) {
+    return speq::guarded([&] {
+        if (!ds || n_devices == 0 || !u_ref || !tot_ref) throw std::invalid_argument("speq_ref_unique_multi: null argument");
+        if (k < 1 || k > MAX_K) throw std::invalid_argument("speq_ref_unique_multi: k must be in [1, 4096]");
+        for (uint32_t i = 0; i < n_devices; ++i)
+            if (!ds[i] || ds[i]->G != ds[0]->G || ds[i]->view.n != ds[0]->view.n)
+                throw std::invalid_argument("speq_ref_unique_multi: replicas of different indexes");
+        const uint32_t G = ds[0]->G;
+        struct Shard {
+            uint64_t* buf = nullptr;
+            uint64_t* cum = nullptr;
+            std::vector<uint64_t> host;
+        };
+        std::vector<Shard> sh(n_devices);
+        auto release = [&] {
+            for (uint32_t i = 0; i < n_devices; ++i) {
+                DeviceGuard g(ds[i]->device);
+                if (sh[i].buf || sh[i].cum) (void)hipStreamSynchronize(ds[i]->stream);
+                if (sh[i].buf) (void)hipFree(sh[i].buf);
+                if (sh[i].cum) (void)hipFree(sh[i].cum);
+                sh[i].buf = sh[i].cum = nullptr;
+            }
+        };
+        try {
+            for (uint32_t i = 0; i < n_devices; ++i) {
+                speq_device_index* d = ds[i];
+                DeviceGuard g(d->device);
+                HIP_OK(hipMalloc(&sh[i].buf, 2ull * G * 8));
+                HIP_OK(hipMemsetAsync(sh[i].buf, 0, 2ull * G * 8, d->stream));
+                sh[i].cum = launch_ref_shard(d, k, i, n_devices, sh[i].buf, sh[i].buf + G, d->stream);
+                sh[i].host.assign(2ull * G, 0);
+                HIP_OK(hipMemcpyAsync(sh[i].host.data(), sh[i].buf, 2ull * G * 8, hipMemcpyDeviceToHost, d->stream));
+            }
+            for (uint32_t i = 0; i < n_devices; ++i) {
+                DeviceGuard g(ds[i]->device);
+                HIP_OK(hipStreamSynchronize(ds[i]->stream));
+            }
+        } catch (...) {
+            release();
+            throw;
+        }
+        release();
+        std::fill(u_ref, u_ref + G, 0);
+        std::fill(tot_ref, tot_ref + G, 0);
+        for (const Shard& s : sh)
+            for (uint32_t g = 0; g < G; ++g) {
+                u_ref[g] += s.host[g];
+                tot_ref[g] += s.host[G + g];
+            }
     });
 }
 
@@ -1274,4 +1402,5 @@ int device_ordinal(const speq_device_index* d) { return d->device; }
 bool device_fastq_gpu(const speq_device_index* d) { return d->fastq_gpu; }
 uint32_t device_stream_lanes(const speq_device_index* d) { return d->stream_lanes; }
 uint32_t device_groups(const speq_device_index* d) { return d->G; }
+uint64_t device_text_len(const speq_device_index* d) { return d->view.n; }
 }  // namespace speq

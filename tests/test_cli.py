@@ -152,3 +152,37 @@ def test_all_subcommand_and_gzip_reads(tmp_path):
     g = c.exp["by_k"][str(k)]["local"]
     tl = [ln for ln in r.stderr.split("\n") if "\t" in ln]
     assert tl[0] == f"{g['T']}\t{g['ambiguous']}"
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("paired", [False, True])
+def test_scan_sharded_over_replicas_matches_one_gpu(tmp_path, paired):
+    """`speq scan --devices 0,0,0` (three replicas: reads dealt across them, the .dat pass split three ways, EM
+    histograms merged) prints exactly what the one-GPU scan prints, and `--gpus 0` (every visible GPU) too."""
+    from speq_amd import synth
+    from test_gpu_stream import split, write_fastq
+    ref = synth.make_reference(4, 2, 20_000)
+    reads = synth.make_reads(ref, 60_000 if paired else 120_000, paired=paired, lowq_rate=0.002)
+    (tmp_path / "refs.fa").write_text(ref.fasta_text())
+    (tmp_path / "groups.txt").write_text(ref.groupings_text())
+    seqs, quals = split(reads)
+    if paired:
+        write_fastq(tmp_path / "r1.fq", seqs[0::2], quals[0::2])
+        write_fastq(tmp_path / "r2.fq", seqs[1::2], quals[1::2])
+    else:
+        write_fastq(tmp_path / "r1.fq", seqs, quals)
+    r = run(["index", "-r", "refs.fa", "-g", "groups.txt", "-x", "ref", "-o", "i.txt"], tmp_path)
+    assert r.returncode == 0, r.stderr
+    base = ["scan", "-1", "r1.fq", "-x", "ref", "-k", "21", "-t", "4", "--fixed-accuracy", "0.99"]
+    if paired:
+        base += ["-2", "r2.fq"]
+    outs = {}
+    for name, extra in (("one", []), ("three", ["--devices", "0,0,0"]), ("all", ["--gpus", "0"])):
+        for f in tmp_path.glob("ref_21mer.dat"):
+            f.unlink()  # every run recomputes the .dat pass (sharded when several replicas)
+        r = run(base + extra + ["-o", f"{name}.txt", "-f"], tmp_path)
+        assert r.returncode == 0, r.stderr
+        outs[name] = (r.stderr, (tmp_path / f"{name}.txt").read_text())
+    assert outs["three"] == outs["one"]
+    assert outs["all"] == outs["one"]
+    assert "\t" in outs["one"][0]
