@@ -41,6 +41,10 @@ def parse_args():
     p.add_argument("--ilp", type=int, default=0, help="windows per lane (1|2; 0 = the device default)")
     p.add_argument("--gpu-build", type=int, default=1, help="build the index on the GPU (1) or host SA-IS (0)")
     p.add_argument("--triple-steps", type=int, default=1, help="three-symbol occ planes (1) or not (0)")
+    p.add_argument("--kmer-table", type=int, default=1,
+                   help="k-mer interval table for k <= 31 (1, default) or LF steps for every window (0)")
+    p.add_argument("--no-lf-compare", action="store_true",
+                   help="skip timing the LF-step kernel beside the k-mer-table kernel")
     p.add_argument("--cpu-seconds", type=float, default=15.0, help="target CPU-baseline sample duration")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-pcie", action="store_true", help="skip the PCIe-inclusive host-buffer measurement")
@@ -79,6 +83,8 @@ def main():
     if a.ilp:
         dev.tune(ilp=a.ilp)
     ilp = dev.tuning("ilp")
+    dev.tune(kmer_table=a.kmer_table)
+    ktab = dev.prepare(k)  # per-k index structure (like the .dat cache): built once, outside the timed region
     # the q-mer table level the scan uses (view_for_k in scan_kernels.hip)
     width = 3 if a.triple_steps else (2 if a.pair_steps else 1)
     q_used = next((a.prefix_q - lv for lv in range(3)
@@ -108,28 +114,45 @@ def main():
             if local:
                 dist.all_reduce(d_w)
 
-    for _ in range(a.warmup):
-        step()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    dev.timing(True)
-    dev.timing_read()  # reset
-    t0 = time.perf_counter()
-    for _ in range(a.steps):
-        step()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    kernel_ms, launches = dev.timing_read()
-    dev.timing(False)
-    el = torch.tensor([elapsed], dtype=torch.float64, device=dev_t)
-    if world > 1:
-        dist.all_reduce(el, op=dist.ReduceOp.MAX)
-    elapsed = float(el.item())
+    def timed_run(steps, warmup):
+        for _ in range(warmup):
+            step()
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        dev.timing(True)
+        dev.timing_read()  # reset
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            step()
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        elapsed = time.perf_counter() - t0
+        kernel_ms, launches = dev.timing_read()
+        dev.timing(False)
+        el = torch.tensor([elapsed], dtype=torch.float64, device=dev_t)
+        if world > 1:
+            dist.all_reduce(el, op=dist.ReduceOp.MAX)
+        return float(el.item()), kernel_ms, launches
+
+    elapsed, kernel_ms, launches = timed_run(a.steps, a.warmup)
     counts = d_counts.cpu().numpy()
+
+    # the LF-step kernel on the same reads (the k-mer table replaces its chain of LF steps; results are identical)
+    lf = None
+    if a.kmer_table and ktab["table_bytes"] and not a.no_lf_compare:
+        dev.tune(kmer_table=0)
+        lf_el, lf_ms, lf_n = timed_run(a.steps, 1)
+        lf_counts = d_counts.cpu().numpy()
+        dev.tune(kmer_table=1)
+        if not np.array_equal(lf_counts, counts):
+            raise RuntimeError("LF-step scan disagrees with the k-mer-table scan")
+        lf = {"value": kmers_per_step * world * a.steps / lf_el, "unit": "k-mers/s",
+              "avg_kernel_ms": lf_ms / max(1, lf_n),
+              "achieved_GBps": kmers_per_step * 2 * k * OCC_ENTRY_BYTES / (lf_ms / 1e3 / max(1, lf_n)) / 1e9,
+              "path": "k_scan<..., KT = false>: q-mer table + three-base LF steps + label-run classification per window"}
 
     total_kmers = kmers_per_step * world * a.steps
     value = total_kmers / elapsed
@@ -145,8 +168,9 @@ def main():
             tj = json.load(open(prof))
             lab = int(idx.info().label_table)
             steps = "_tri1" if a.triple_steps else ""
+            kt = "_kt1" if ktab["table_bytes"] else ""
             key = (f"cfg{a.config}_k{k}_q{a.prefix_q}_pairs{a.pair_steps}{steps}_lab{lab}_ilp{ilp}"
-                   f"_bpc{dev.tuning('blocks_per_cu')}_{a.mode}_reads{n_reads}")
+                   f"_bpc{dev.tuning('blocks_per_cu')}_{a.mode}_reads{n_reads}{kt}")
             if key in tj:
                 traffic = tj[key]["hbm_bytes_per_launch"]
                 traffic_src = tj[key]["source"]
@@ -196,6 +220,8 @@ def main():
                 "blocks_per_cu": dev.tuning("blocks_per_cu"), "grid_blocks": dev.tuning("grid_blocks"),
                 "kmers_per_step_per_gpu": kmers_per_step, "parallelism": f"dp{world} (reads sharded, index replicated)",
                 "index_build_s": round(build_s, 3), "index_builder": "gpu" if a.gpu_build else "host", "fm_text_len": int(idx.info().n),
+                "kmer_table": {"on": bool(ktab["table_bytes"]), "distinct_kmers": ktab["distinct_kmers"],
+                               "bytes": ktab["table_bytes"], "build_s": round(ktab["build_ms"] / 1e3, 4)},
             },
             "roofline": {
                 "bound": "hbm", "achieved": achieved_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -209,11 +235,13 @@ def main():
                 "avg_kernel_ms": avg_kernel_s * 1e3, "launches_timed": launches,
                 "traffic_source": traffic_src,
                 "note": "achieved uses SURVEY.md 8(d)'s algorithmic 2*k*64 B per k-mer (k LF steps x 2 uncached "
-                        "64-B occ loads); the kernel issues ~0.3 of those gathers (q-mer table, two-base steps, "
-                        "shared lo/hi loads) and they hit L2/Infinity Cache, so frac > 1 means HBM does not bound "
-                        "this kernel; traffic = measured L2->fabric bytes per launch (DESIGN.md 6)",
+                        "64-B occ loads), fixed whatever the kernel does; the k-mer-table kernel reads one 64-B bucket "
+                        "per window instead (the LF-step kernel ~0.3 of the algorithmic gathers), mostly from "
+                        "L2/Infinity Cache, so frac > 1 means HBM does not bound this kernel; traffic = measured "
+                        "L2->fabric bytes per launch (DESIGN.md 6)",
             },
             "cpu_baseline": cpu,
+            "lf_steps": lf,
             "pcie_inclusive": pcie,
             "check": {"T": int(counts[0]), "ambiguous": int(counts[1]), "U": [int(x) for x in counts[2:]]},
         }

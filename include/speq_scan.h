@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define SPEQ_ABI_VERSION 4
+#define SPEQ_ABI_VERSION 5
 
 enum {
     SPEQ_OK = 0,
@@ -277,11 +277,25 @@ void speq_groupings_free(speq_groupings* g);
  *                  (less memory, one more dependent load per window); -1 sparse when < 1/8 of the codes occur;
  * "fastq_gpu_parse": 1 (default) speq_scan_fastq parses blocks of simple four-line records on the GPU (raw text
  *                  to HBM); 0 parses every block on host threads. Results are identical;
+ * "kmer_table"   : 1 (default) scans of k <= 31 look each N-free window up in the replica's k-mer interval table
+ *                  for k (built by the first scan with that k, or by speq_device_prepare); 0 searches every window
+ *                  with LF steps. Results are identical;
  * "stream_lanes" : compute streams of a pipeline created afterwards (speq_pipeline_create, speq_scan_fastq, host
  *                  scans), 1..8 (default 3): consecutive batches are parsed and scanned on them in turn, so the
  *                  short launches of different batches overlap on the CUs. */
 int speq_device_set_tuning(speq_device_index* d, const char* key, int64_t value);
 int speq_device_get_tuning(const speq_device_index* d, const char* key, int64_t* value);
+
+/* ---- k-mer interval table (the q-mer table of the FM-index taken to q = k) ----
+ * For a scan length k <= 31 the replica keeps a hash table of every distinct N-free k-mer of the reference texts
+ * with its SA interval start and its classification (one group, or the interval width when its occurrences span
+ * >= 2 groups), computed once per distinct k-mer by FM backward search; a scan then resolves each window with one
+ * 64-B bucket load instead of a chain of LF steps (an absent k-mer does not occur). Built on the replica's GPU by
+ * the first scan with k, or here ahead of time; blocking. Outputs may be NULL; all zero when tables are off
+ * (tuning "kmer_table" = 0) or k > 31 (those scans use LF steps). Replaces no reference call; the reference
+ * searches each window from scratch (fm_scanner.cpp:208). */
+int speq_device_prepare(speq_device_index* d, uint32_t k, uint64_t* distinct_kmers, uint64_t* table_bytes,
+                        double* build_ms);
 
 /* ---- kernel timing (HIP events on the launch stream; bench/roofline support) ----
  * Returns the summed elapsed milliseconds of the scan kernels launched by speq_scan_reads_device on

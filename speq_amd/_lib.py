@@ -111,12 +111,13 @@ SIGNATURES = {
     "speq_groupings_free": (None, [_P]),
     "speq_device_set_tuning": (C.c_int, [_P, C.c_char_p, C.c_int64]),
     "speq_device_get_tuning": (C.c_int, [_P, C.c_char_p, C.POINTER(C.c_int64)]),
+    "speq_device_prepare": (C.c_int, [_P, C.c_uint32, _U64P, _U64P, _F64P]),
     "speq_timing_enable": (C.c_int, [_P, C.c_int]),
     "speq_timing_read": (C.c_int, [_P, _F64P, _U64P]),
 }
 
 _lib = None
-ABI_VERSION = 4  # include/speq_scan.h SPEQ_ABI_VERSION (struct layouts above)
+ABI_VERSION = 5  # include/speq_scan.h SPEQ_ABI_VERSION (struct layouts above)
 
 
 def lib() -> C.CDLL:

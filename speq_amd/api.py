@@ -223,6 +223,12 @@ class DeviceIndex:
         check(lib().speq_device_get_tuning(self._h, key.encode(), C.byref(v)))
         return v.value
 
+    def prepare(self, k: int) -> dict:
+        """Builds the k-mer interval table of k now (speq_device_prepare); returns its size and build time."""
+        n, b, ms = C.c_uint64(), C.c_uint64(), C.c_double()
+        check(lib().speq_device_prepare(self._h, k, C.byref(n), C.byref(b), C.byref(ms)))
+        return {"distinct_kmers": n.value, "table_bytes": b.value, "build_ms": ms.value}
+
     def timing(self, on: bool) -> None:
         check(lib().speq_timing_enable(self._h, int(on)))
 

@@ -22,11 +22,13 @@
 //      (fm_scanner.cpp:183-190, :709-729) is a segmented min/max scan across the lanes of each unit.
 #include <hip/hip_runtime.h>
 
+#include <chrono>
 #include <climits>
 #include <cmath>
 #include <cstdint>
 #include <cstring>
 #include <memory>
+#include <map>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -56,7 +58,10 @@ struct DevView {
     const uint2* prefix;     // 4^q intervals (or null)
     const uint4* pfx_rank;   // sparse form of `prefix` (or null): {count, 96-bit presence} per 96 codes ...
     const uint2* pfx_iv;     // ... and the intervals of the present codes only, in code order
+    const uint4* ktab;       // k-mer interval table for k == kt_k (or null): 64-B buckets of 4 slots, see KmerTable
+    uint64_t kt_bmask;       // buckets - 1 (a power of two minus one)
     uint32_t n, q, G, nb;
+    uint32_t kt_k;
 };
 
 struct UnitSrc {
@@ -402,12 +407,87 @@ __device__ __forceinline__ void search_packed_n(const DevView& I, const Rsrc& R,
     }
 }
 
+// ---- k-mer interval table (the q-mer table taken to q = k; built per k by k_ktab_keys + k_ktab_fill) ----
+// Open addressing over 64-B buckets of four 16-B slots {key lo, key hi, lo, info}: key = the packed k-mer (2 bits per
+// base, last base lowest; k <= 31 so the all-ones key marks an empty slot), lo = start of its SA interval, info =
+// its classification: the group id, or 0x80000000 | (hi - lo) when the occurrences span >= 2 groups. Every distinct
+// N-free k-mer of the reference texts is present; a k-mer that is absent from the table does not occur. Keys are
+// placed by linear probing over buckets, slots in order, without deletions, so a lookup that meets an empty slot
+// before its key has proven the key absent.
+constexpr uint32_t KT_MAX_K = 31;
+constexpr unsigned long long KT_EMPTY = ~0ull;
+
+__host__ __device__ __forceinline__ uint64_t kt_hash(uint64_t x) {  // murmur3 fmix64
+    x ^= x >> 33;
+    x *= 0xff51afd7ed558ccdULL;
+    x ^= x >> 33;
+    x *= 0xc4ceb9fe1a85ec53ULL;
+    x ^= x >> 33;
+    return x;
+}
+
+// Same outputs as search_packed_n (group / -2 / -1 and, for -2, the SA interval) from one bucket load per window:
+// the four slots are four independent 16-B loads of one 64-B line, issued together. A window whose bucket holds
+// neither its key nor an empty slot probes the next bucket (rare at load factor <= 1/2).
+template <int NW>
+__device__ __forceinline__ void search_ktab_n(const DevView& I, const uint64_t (&P)[NW], const bool (&act)[NW],
+                                              int (&out)[NW], uint32_t (&lo_out)[NW], uint32_t (&hi_out)[NW]) {
+    uint64_t b[NW];
+    bool pend[NW];
+#pragma unroll
+    for (int w = 0; w < NW; ++w) {
+        out[w] = -1;
+        lo_out[w] = hi_out[w] = 0;
+        pend[w] = act[w];
+        b[w] = kt_hash(P[w]) & I.kt_bmask;
+    }
+    for (;;) {
+        bool any = false;
+#pragma unroll
+        for (int w = 0; w < NW; ++w) any |= pend[w];
+        if (!any) break;
+        u32x4 sl[NW][4];
+#pragma unroll
+        for (int w = 0; w < NW; ++w)
+            if (pend[w]) {
+                const u32x4* p = reinterpret_cast<const u32x4*>(I.ktab) + b[w] * 4u;
+#pragma unroll
+                for (int j = 0; j < 4; ++j) sl[w][j] = p[j];
+            }
+#pragma unroll
+        for (int w = 0; w < NW; ++w)
+            if (pend[w]) {
+                const uint32_t kl = (uint32_t)P[w], kh = (uint32_t)(P[w] >> 32);
+                bool empty = false, found = false;
+                uint32_t lo = 0, info = 0;
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const bool hit = sl[w][j][0] == kl && sl[w][j][1] == kh;
+                    lo = hit ? sl[w][j][2] : lo;
+                    info = hit ? sl[w][j][3] : info;
+                    found |= hit;
+                    empty |= sl[w][j][0] == 0xFFFFFFFFu && sl[w][j][1] == 0xFFFFFFFFu;
+                }
+                if (found) {
+                    const bool multi = (info >> 31) != 0u;
+                    out[w] = multi ? -2 : (int)info;
+                    lo_out[w] = lo;
+                    hi_out[w] = multi ? lo + (info & 0x7FFFFFFFu) : lo + 1u;  // single group: only lo is kept
+                }
+                pend[w] = !(found || empty);
+                b[w] = (b[w] + 1u) & I.kt_bmask;
+            }
+    }
+}
+
 #ifndef SPEQ_MIN_WAVES  // A/B knob: minimum waves per SIMD the register allocator must allow
 #define SPEQ_MIN_WAVES 1
 #endif
 
 // EM: also record the SA interval of every passing multi-group window (EM histogram scans only).
-template <int MODE, bool PAIRED, bool LDS_HIST, int NWIN, bool EM>
+// KT: windows of k <= 31 are resolved in the k-mer interval table (I.ktab, I.kt_k == k) instead of by LF steps; a
+// separate instantiation, so the LF-step kernel keeps its own register allocation.
+template <int MODE, bool PAIRED, bool LDS_HIST, int NWIN, bool EM, bool KT>
 __global__ __launch_bounds__(BLOCK_THREADS, SPEQ_MIN_WAVES) void k_scan(DevView I, UnitSrc src, unsigned long long* __restrict__ out_a,
                                                         unsigned long long* __restrict__ out_b,
                                                         double* __restrict__ out_w) {
@@ -587,7 +667,8 @@ __global__ __launch_bounds__(BLOCK_THREADS, SPEQ_MIN_WAVES) void k_scan(DevView 
         {
             int wp[NWIN];
             uint32_t plo[NWIN], phi[NWIN];
-            search_packed_n<NWIN>(I, R, P, packed, k, wp, plo, phi);
+            if (KT) search_ktab_n<NWIN>(I, P, packed, wp, plo, phi);
+            else search_packed_n<NWIN>(I, R, P, packed, k, wp, plo, phi);
 #pragma unroll
             for (int w = 0; w < NWIN; ++w)
                 if (packed[w]) {
@@ -711,6 +792,97 @@ __global__ __launch_bounds__(BLOCK_THREADS, SPEQ_MIN_WAVES) void k_scan(DevView 
     }
 }
 
+// ---- k-mer interval table construction (per k, once per replica) ----
+// Pass 1: every N-free window of every text inserts its packed k-mer into a set (8-B slots, linear probing, CAS);
+// each thread rolls the code over a run of consecutive windows. n_distinct counts the keys inserted.
+constexpr uint32_t KT_RUN = 64;
+__global__ void k_ktab_keys(const uint8_t* __restrict__ text, const uint64_t* __restrict__ tstart,
+                            const uint64_t* __restrict__ cum, uint32_t n_texts, uint64_t total, uint32_t k,
+                            unsigned long long* __restrict__ keys, uint64_t smask,
+                            unsigned long long* __restrict__ n_distinct) {
+    const uint64_t kmask = (1ull << (2u * k)) - 1ull;  // k <= 31
+    const uint64_t nruns = (total + KT_RUN - 1) / KT_RUN;
+    unsigned long long added = 0;
+    for (uint64_t run = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; run < nruns;
+         run += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t f0 = run * KT_RUN, f1 = min(total, f0 + KT_RUN);
+        uint32_t t = 0, hi = n_texts;  // largest t with cum[t] <= f0 (that text has windows beyond f0)
+        while (hi - t > 1) {
+            const uint32_t mid = (t + hi) >> 1;
+            if (cum[mid] <= f0) t = mid; else hi = mid;
+        }
+        uint64_t code = 0;
+        uint32_t good = 0;  // consecutive ACGT symbols ending at the window's last base
+        bool fresh = true;
+        for (uint64_t f = f0; f < f1; ++f) {
+            while (f >= cum[t + 1]) {
+                ++t;
+                fresh = true;
+            }
+            const uint8_t* base = text + tstart[t] + (f - cum[t]);
+            if (fresh) {
+                code = 0;
+                good = 0;
+                for (uint32_t i = 0; i < k; ++i) {
+                    const uint32_t c = base[i];  // SA alphabet: A..T = 2..5, N = 6
+                    const bool acgt = c >= 2u && c <= 5u;
+                    code = ((code << 2) | (acgt ? c - 2u : 0u)) & kmask;
+                    good = acgt ? good + 1u : 0u;
+                }
+                fresh = false;
+            } else {
+                const uint32_t c = base[k - 1];
+                const bool acgt = c >= 2u && c <= 5u;
+                code = ((code << 2) | (acgt ? c - 2u : 0u)) & kmask;
+                good = acgt ? good + 1u : 0u;
+            }
+            if (good < k) continue;
+            uint64_t sl = kt_hash(code) & smask;
+            for (;;) {
+                unsigned long long prev = __atomic_load_n(&keys[sl], __ATOMIC_RELAXED);
+                if (prev == KT_EMPTY) prev = atomicCAS(&keys[sl], KT_EMPTY, (unsigned long long)code);
+                if (prev == KT_EMPTY) {
+                    ++added;
+                    break;
+                }
+                if (prev == code) break;
+                sl = (sl + 1) & smask;
+            }
+        }
+    }
+    if (added) atomicAdd(n_distinct, added);
+}
+
+// Pass 2: each distinct k-mer is searched once with the FM-index (search_packed_n: q-mer table + LF steps + run
+// classification, exactly as a scan would) and stored with its interval and classification.
+__global__ void k_ktab_fill(DevView I, const unsigned long long* __restrict__ keys, uint64_t n_slots, uint32_t k,
+                            uint4* __restrict__ table, uint64_t bmask) {
+    const Rsrc R = make_rsrc(I);
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n_slots;
+         i += (uint64_t)gridDim.x * blockDim.x) {
+        const unsigned long long code = keys[i];
+        if (code == KT_EMPTY) continue;
+        const uint64_t P[1] = {code};
+        const bool act[1] = {true};
+        int out[1];
+        uint32_t lo[1], hi[1];
+        search_packed_n<1>(I, R, P, act, k, out, lo, hi);
+        if (out[0] == -1) continue;  // unreachable: every key occurs in the texts
+        const uint32_t info = out[0] == -2 ? (0x80000000u | (hi[0] - lo[0])) : (uint32_t)out[0];
+        uint64_t b = kt_hash(code) & bmask;
+        for (bool placed = false; !placed; b = (b + 1) & bmask) {
+            for (uint32_t j = 0; j < 4u && !placed; ++j) {
+                uint4* slot = table + b * 4u + j;
+                if (atomicCAS(reinterpret_cast<unsigned long long*>(slot), KT_EMPTY, code) == KT_EMPTY) {
+                    slot->z = lo[0];
+                    slot->w = info;
+                    placed = true;
+                }
+            }
+        }
+    }
+}
+
 #define HIP_OK(expr)                                                                                         \
     do {                                                                                                     \
         hipError_t _e = (expr);                                                                              \
@@ -764,6 +936,14 @@ struct speq_device_index {
                                   // dependent load to every window (cfg 2: 4.63 -> 5.39 ms, sweep_sparse.jsonl)
     int prefix_choice = -1;       // tuning "prefix_level": -1 = by k (view_for_k), 0..2 = force q - level
     uint32_t base_q = 0;          // the index's prefix_q
+    bool kmer_table = true;       // tuning "kmer_table": scans of k <= 31 look windows up in a per-k k-mer table
+    struct KmerTable {
+        uint4* table = nullptr;
+        uint64_t buckets = 0, distinct = 0;
+        double build_ms = 0.0;
+    };
+    std::mutex kt_mu;                        // the first scan with a new k builds its table
+    std::map<uint32_t, KmerTable> ktabs;     // k -> table (kept until the replica closes)
     std::mutex events_mu;  // launches may come from several host threads (pipelines, concurrent scans)
     std::vector<std::pair<hipEvent_t, hipEvent_t>> events;
     double timed_ms = 0.0;
@@ -784,15 +964,21 @@ struct DeviceGuard {
     }
 };
 
-template <int MODE, bool PAIRED, bool LDS>
-void allow_big_lds() {
-    HIP_OK(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_scan<MODE, PAIRED, LDS, 1, false>),
+template <int MODE, bool PAIRED, bool LDS, bool KT>
+void allow_big_lds_kt() {
+    HIP_OK(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_scan<MODE, PAIRED, LDS, 1, false, KT>),
                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-    HIP_OK(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_scan<MODE, PAIRED, LDS, 2, false>),
+    HIP_OK(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_scan<MODE, PAIRED, LDS, 2, false, KT>),
                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     if (MODE != KM_REF)
-        HIP_OK(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_scan<MODE, PAIRED, LDS, 1, MODE != KM_REF>),
+        HIP_OK(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_scan<MODE, PAIRED, LDS, 1, MODE != KM_REF, KT>),
                                    hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+}
+
+template <int MODE, bool PAIRED, bool LDS>
+void allow_big_lds() {
+    allow_big_lds_kt<MODE, PAIRED, LDS, false>();
+    allow_big_lds_kt<MODE, PAIRED, LDS, true>();
 }
 
 void allow_big_lds_all() {
@@ -842,25 +1028,124 @@ DevView view_for_k(const speq_device_index* d, uint32_t k) {
     return v;
 }
 
-template <int MODE, bool PAIRED, bool LDS>
-void launch_t(const speq_device_index* d, const UnitSrc& src, uint32_t grid, size_t lds, hipStream_t st,
-              unsigned long long* a, unsigned long long* b, double* w) {
+// The index view a scan of k-mers uses (q-mer table level by k unless forced), without the k-mer table.
+DevView scan_view(const speq_device_index* d, uint32_t k) {
     DevView v = d->view;
     if (d->prefix_choice >= 0) use_sparse(d, (uint32_t)d->prefix_choice, v);
-    else v = view_for_k(d, src.k);
+    else v = view_for_k(d, k);
+    v.ktab = nullptr;
+    v.kt_bmask = 0;
+    v.kt_k = 0;
+    return v;
+}
+
+uint64_t next_pow2(uint64_t x) {
+    uint64_t p = 1;
+    while (p < x) p <<= 1;
+    return p;
+}
+
+// Builds the k-mer interval table of k on the replica's stream (blocking): the distinct N-free k-mers of the texts
+// (k_ktab_keys into a set of 2x the window count), then one FM-index search per distinct k-mer (k_ktab_fill) into
+// buckets sized for a load factor in (1/4, 1/2].
+speq_device_index::KmerTable build_ktab(speq_device_index* d, uint32_t k) {
+    DeviceGuard g(d->device);
+    const auto t0 = std::chrono::steady_clock::now();
+    std::vector<uint64_t> cum(d->n_texts + 1, 0);
+    for (uint32_t t = 0; t < d->n_texts; ++t) {
+        const uint64_t L = d->text_start[t + 1] - d->text_start[t] - 1;
+        cum[t + 1] = cum[t] + (L >= k ? L - k + 1 : 0);
+    }
+    const uint64_t total = cum[d->n_texts];
+    speq_device_index::KmerTable kt;
+    void* keys = nullptr;
+    uint64_t* d_cum = nullptr;
+    unsigned long long* d_cnt = nullptr;
+    auto cleanup = [&] {
+        (void)hipStreamSynchronize(d->stream);
+        if (keys) (void)hipFree(keys);
+        if (d_cum) (void)hipFree(d_cum);
+        if (d_cnt) (void)hipFree(d_cnt);
+    };
+    try {
+        unsigned long long distinct = 0;
+        const uint64_t slots = next_pow2(std::max<uint64_t>(2 * total, 64));
+        if (total > 0) {
+            HIP_OK(hipMalloc(&keys, slots * 8));
+            HIP_OK(hipMalloc(&d_cum, cum.size() * 8));
+            HIP_OK(hipMalloc(&d_cnt, 8));
+            HIP_OK(hipMemsetAsync(keys, 0xFF, slots * 8, d->stream));
+            HIP_OK(hipMemsetAsync(d_cnt, 0, 8, d->stream));
+            HIP_OK(hipMemcpyAsync(d_cum, cum.data(), cum.size() * 8, hipMemcpyHostToDevice, d->stream));
+            const uint64_t runs = (total + KT_RUN - 1) / KT_RUN;
+            const uint32_t grid = (uint32_t)std::min<uint64_t>((runs + 255) / 256, 8192);
+            hipLaunchKernelGGL(k_ktab_keys, dim3(grid), dim3(256), 0, d->stream, d->d_text, d->d_text_start, d_cum,
+                               d->n_texts, total, k, reinterpret_cast<unsigned long long*>(keys), slots - 1, d_cnt);
+            HIP_OK(hipGetLastError());
+            HIP_OK(hipMemcpyAsync(&distinct, d_cnt, 8, hipMemcpyDeviceToHost, d->stream));
+            HIP_OK(hipStreamSynchronize(d->stream));
+        }
+        kt.distinct = distinct;
+        kt.buckets = next_pow2(std::max<uint64_t>(1, (distinct + 1) / 2));  // 4 slots per bucket: load <= 1/2
+        HIP_OK(hipMalloc(&kt.table, kt.buckets * 64));
+        d->track(kt.table);
+        HIP_OK(hipMemsetAsync(kt.table, 0xFF, kt.buckets * 64, d->stream));
+        if (distinct > 0) {
+            const DevView v = scan_view(d, k);
+            const uint32_t grid = (uint32_t)std::min<uint64_t>((slots + 255) / 256, 16384);
+            hipLaunchKernelGGL(k_ktab_fill, dim3(grid), dim3(256), 0, d->stream, v,
+                               reinterpret_cast<const unsigned long long*>(keys), slots, k, kt.table, kt.buckets - 1);
+            HIP_OK(hipGetLastError());
+        }
+        HIP_OK(hipStreamSynchronize(d->stream));
+    } catch (...) {
+        cleanup();
+        throw;
+    }
+    cleanup();
+    kt.build_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    return kt;
+}
+
+// The table of k (built on first use), or null when tables are off or k is outside 1..31.
+const speq_device_index::KmerTable* ensure_ktab(speq_device_index* d, uint32_t k) {
+    if (!d->kmer_table || k < 1 || k > KT_MAX_K) return nullptr;
+    std::lock_guard<std::mutex> lk(d->kt_mu);
+    auto it = d->ktabs.find(k);
+    if (it == d->ktabs.end()) it = d->ktabs.emplace(k, build_ktab(d, k)).first;
+    return &it->second;
+}
+
+template <int MODE, bool PAIRED, bool LDS, bool KT>
+void launch_v(const speq_device_index* d, const DevView& v, const UnitSrc& src, uint32_t grid, size_t lds,
+              hipStream_t st, unsigned long long* a, unsigned long long* b, double* w) {
     if (MODE != KM_REF && src.em_mult != nullptr)
-        hipLaunchKernelGGL((k_scan<MODE, PAIRED, LDS, 1, MODE != KM_REF>), dim3(grid), dim3(BLOCK_THREADS), lds, st,
-                           v, src, a, b, w);
+        hipLaunchKernelGGL((k_scan<MODE, PAIRED, LDS, 1, MODE != KM_REF, KT>), dim3(grid), dim3(BLOCK_THREADS), lds,
+                           st, v, src, a, b, w);
     else if ((MODE == KM_LOCAL ? d->ilp_local : d->ilp) == 2)
-        hipLaunchKernelGGL((k_scan<MODE, PAIRED, LDS, 2, false>), dim3(grid), dim3(BLOCK_THREADS), lds, st, v,
+        hipLaunchKernelGGL((k_scan<MODE, PAIRED, LDS, 2, false, KT>), dim3(grid), dim3(BLOCK_THREADS), lds, st, v,
                            src, a, b, w);
     else
-        hipLaunchKernelGGL((k_scan<MODE, PAIRED, LDS, 1, false>), dim3(grid), dim3(BLOCK_THREADS), lds, st, v,
+        hipLaunchKernelGGL((k_scan<MODE, PAIRED, LDS, 1, false, KT>), dim3(grid), dim3(BLOCK_THREADS), lds, st, v,
                            src, a, b, w);
 }
 
-void launch_scan(const speq_device_index* d, int mode, bool paired, const UnitSrc& src, uint64_t work_units,
+template <int MODE, bool PAIRED, bool LDS>
+void launch_t(const speq_device_index* d, const UnitSrc& src, uint32_t grid, size_t lds, hipStream_t st,
+              unsigned long long* a, unsigned long long* b, double* w, const speq_device_index::KmerTable* kt) {
+    DevView v = scan_view(d, src.k);
+    if (kt) {
+        v.ktab = kt->table;
+        v.kt_bmask = kt->buckets - 1;
+        v.kt_k = src.k;
+    }
+    if (kt) launch_v<MODE, PAIRED, LDS, true>(d, v, src, grid, lds, st, a, b, w);
+    else launch_v<MODE, PAIRED, LDS, false>(d, v, src, grid, lds, st, a, b, w);
+}
+
+void launch_scan(speq_device_index* d, int mode, bool paired, const UnitSrc& src, uint64_t work_units,
                  hipStream_t st, unsigned long long* a, unsigned long long* b, double* w) {
+    const speq_device_index::KmerTable* kt = ensure_ktab(d, src.k);
     const bool lds_hist = d->G <= LDS_HIST_MAX_G;
     const uint32_t hist_words = lds_hist ? ((mode == KM_GLOBAL) ? d->G : 2u * d->G) : 0u;
     const size_t lds = ((hist_words * 8u + 15u) & ~15u) +
@@ -877,8 +1162,8 @@ void launch_scan(const speq_device_index* d, int mode, bool paired, const UnitSr
     const uint32_t grid = (uint32_t)blocks;
 #define SPEQ_DISPATCH(M, P)                                                            \
     do {                                                                               \
-        if (lds_hist) launch_t<M, P, true>(d, src, grid, lds_launch, st, a, b, w);    \
-        else launch_t<M, P, false>(d, src, grid, lds_launch, st, a, b, w);            \
+        if (lds_hist) launch_t<M, P, true>(d, src, grid, lds_launch, st, a, b, w, kt); \
+        else launch_t<M, P, false>(d, src, grid, lds_launch, st, a, b, w, kt);         \
     } while (0)
     if (mode == KM_REF) SPEQ_DISPATCH(KM_REF, false);
     else if (mode == KM_GLOBAL) { if (paired) SPEQ_DISPATCH(KM_GLOBAL, true); else SPEQ_DISPATCH(KM_GLOBAL, false); }
@@ -1300,6 +1585,18 @@ int speq_ref_unique(speq_device_index* d, uint32_t k, uint64_t* u_ref, uint64_t*
     });
 }
 
+int speq_device_prepare(speq_device_index* d, uint32_t k, uint64_t* distinct_kmers, uint64_t* table_bytes,
+                        double* build_ms) {
+    return speq::guarded([&] {
+        if (!d) throw std::invalid_argument("speq_device_prepare: null handle");
+        if (k < 1 || k > MAX_K) throw std::invalid_argument("speq_device_prepare: k must be in [1, 4096]");
+        const speq_device_index::KmerTable* kt = ensure_ktab(d, k);
+        if (distinct_kmers) *distinct_kmers = kt ? kt->distinct : 0;
+        if (table_bytes) *table_bytes = kt ? kt->buckets * 64 : 0;
+        if (build_ms) *build_ms = kt ? kt->build_ms : 0.0;
+    });
+}
+
 int speq_device_set_tuning(speq_device_index* d, const char* key, int64_t value) {
     return speq::guarded([&] {
         if (!d || !key) throw std::invalid_argument("speq_device_set_tuning: null argument");
@@ -1322,6 +1619,9 @@ int speq_device_set_tuning(speq_device_index* d, const char* key, int64_t value)
         } else if (k == "sparse_prefix") {
             if (value < -1 || value > 1) throw std::invalid_argument("sparse_prefix must be -1 (auto), 0 or 1");
             d->sparse_choice = (int)value;
+        } else if (k == "kmer_table") {
+            if (value != 0 && value != 1) throw std::invalid_argument("kmer_table must be 0 or 1");
+            d->kmer_table = value != 0;
         } else if (k == "prefix_level") {
             if (value < -1 || value > 2) throw std::invalid_argument("prefix_level must be -1 (auto) or 0..2");
             if (value >= 0 && (d->prefix_level[value] == nullptr && value > 0))
@@ -1347,6 +1647,7 @@ int speq_device_get_tuning(const speq_device_index* d, const char* key, int64_t*
         else if (k == "sparse_prefix") *value = d->sparse_choice;
         else if (k == "fastq_gpu_parse") *value = d->fastq_gpu ? 1 : 0;
         else if (k == "stream_lanes") *value = d->stream_lanes;
+        else if (k == "kmer_table") *value = d->kmer_table ? 1 : 0;
         else throw std::invalid_argument("speq_device_get_tuning: unknown key " + k);
     });
 }

@@ -1,5 +1,6 @@
 """GPU: the HIP path reproduces the committed golden vectors (tests/golden/*/expected.json) bit-exactly
-(fp64 Phred weights to rtol 1e-12), for every k of every case and several q-mer table sizes; plus the RCCL
+(fp64 Phred weights to rtol 1e-12), for every k of every case and several q-mer table sizes, with and without the
+k-mer interval table; plus the RCCL
 counter all-reduce through the C ABI on a single-rank communicator."""
 import ctypes as C
 
@@ -20,8 +21,8 @@ def test_gpu_matches_golden(name, q, steps):
     c = Case(name)
     dev = DeviceIndex(FmIndex.build(c.records, c.groups, c.G, prefix_q=q, pair_steps=steps >= 2,
                                     label_table=steps == 2, triple_steps=steps == 3))
-    for k, ilp in [(k, ilp) for k in c.ks for ilp in (1, 2)]:
-        dev.tune(ilp=ilp, ilp_local=ilp)
+    for k, ilp, kt in [(k, ilp, kt) for k in c.ks for ilp in (1, 2) for kt in (1, 0)]:
+        dev.tune(ilp=ilp, ilp_local=ilp, kmer_table=kt)  # k-mer interval table (k <= 31) or LF steps
         e = c.exp["by_k"][str(k)]
         u, t = dev.count_unique_kmers_per_group(k)
         assert u.tolist() == e["u_ref"] and t.tolist() == e["tot_ref"], (name, k)

@@ -1,0 +1,96 @@
+"""GPU: the k-mer interval table gives exactly what LF-step search gives: counters, Phred weights
+(same per-window arithmetic, rtol 1e-12 for the different summation order), EM histograms and the .dat pass; its
+key set is the set of distinct N-free k-mers of the reference texts (fwd and rc of every record); k-mers absent
+from the reference are found absent; k > 31 has no table."""
+import numpy as np
+import pytest
+
+from oracle.oracle import Oracle
+from speq_amd import DeviceIndex, EmHistogram, FmIndex, synth
+
+pytestmark = pytest.mark.gpu
+
+COMP = bytes.maketrans(b"ACGTN", b"TGCAN")
+
+
+def distinct_kmers(records, k):
+    seen = set()
+    for r in records:
+        r = r.upper()
+        for s in (r, r.translate(COMP)[::-1]):
+            for i in range(len(s) - k + 1):
+                w = s[i:i + k]
+                if b"N" not in w:
+                    seen.add(w)
+    return len(seen)
+
+
+@pytest.fixture(scope="module")
+def small():
+    ref = synth.make_reference(3, 2, 5_000, ref_n_rate=0.002)
+    idx = FmIndex.build(ref.records, ref.groups, 3, prefix_q=8, pair_steps=True, triple_steps=True)
+    return ref, idx
+
+
+@pytest.mark.parametrize("k", [1, 2, 7, 16, 21, 31])
+def test_key_set_is_the_distinct_reference_kmers(small, k):
+    ref, idx = small
+    dev = DeviceIndex(idx)
+    info = dev.prepare(k)
+    assert info["distinct_kmers"] == distinct_kmers(ref.records, k)
+    assert info["table_bytes"] >= 64 and info["table_bytes"] * 4 // 64 >= 2 * info["distinct_kmers"]  # load <= 1/2
+
+
+def test_no_table_above_31_or_when_off(small):
+    _, idx = small
+    dev = DeviceIndex(idx)
+    assert dev.prepare(32)["table_bytes"] == 0
+    dev.tune(kmer_table=0)
+    assert dev.prepare(21)["table_bytes"] == 0
+    assert dev.tuning("kmer_table") == 0
+
+
+@pytest.mark.parametrize("paired", [False, True])
+@pytest.mark.parametrize("local", [False, True])
+def test_table_equals_lf_steps_with_em(paired, local):
+    ref = synth.make_reference(6, 3, 12_000, ref_n_rate=0.0005)
+    idx = FmIndex.build(ref.records, ref.groups, 6, prefix_q=10, pair_steps=True, triple_steps=True)
+    reads = synth.make_reads(ref, 30_000, paired=paired, n_rate=0.001, lowq_rate=0.005, err_rate=0.004)
+    res = {}
+    for kt in (1, 0):
+        dev = DeviceIndex(idx)
+        dev.tune(kmer_table=kt)
+        for k in (31, 21, 15):  # several tables on one replica, built in turn
+            em = EmHistogram(dev)
+            r = em.scan(reads.seq.tobytes(), reads.qual.tobytes(), reads.offsets, k=k, paired=paired, local=local)
+            em.finalize()
+            p = np.linspace(5.0, 30.0, 6)
+            res[(kt, k)] = (r, em.info(), em.step(p, [3] * 6, r.unique))
+            u = dev.count_unique_kmers_per_group(k)
+            res[(kt, k, "dat")] = (u[0].tolist(), u[1].tolist())
+    for k in (31, 21, 15):
+        a, b = res[(1, k)], res[(0, k)]
+        assert (a[0].total, a[0].ambiguous, a[0].unique.tolist()) == (b[0].total, b[0].ambiguous, b[0].unique.tolist())
+        if local:
+            np.testing.assert_allclose(a[0].weights, b[0].weights, rtol=1e-12)
+        assert a[1] == b[1]
+        np.testing.assert_array_equal(a[2], b[2])
+        assert res[(1, k, "dat")] == res[(0, k, "dat")]
+
+
+def test_absent_kmers_and_oracle():
+    ref = synth.make_reference(4, 1, 8_000)
+    idx = FmIndex.build(ref.records, ref.groups, 4, prefix_q=6, pair_steps=True, triple_steps=True)
+    dev = DeviceIndex(idx)
+    rng = np.random.default_rng(7)
+    n, L = 2_000, 120
+    seq = rng.choice(np.frombuffer(b"ACGT", dtype=np.uint8), size=n * L)  # random reads: absent 21-mers
+    mixed = synth.make_reads(ref, n, read_len=L)
+    seq = np.concatenate([seq, mixed.seq])
+    qual = np.full(seq.size, ord("I"), dtype=np.uint8)
+    off = np.arange(0, seq.size + 1, L, dtype=np.uint64)
+    for k in (11, 21, 31):
+        r = dev.scan(seq.tobytes(), qual.tobytes(), off, k=k)
+        T, amb, U, _ = Oracle(ref.records, ref.groups, 4, k).scan(seq, qual, off)
+        assert (r.total, r.ambiguous, r.unique.tolist()) == (T, amb, U.tolist())
+        assert r.total == 2 * n * (L - k + 1)

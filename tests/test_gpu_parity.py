@@ -15,11 +15,13 @@ W_RTOL = 1e-10  # fp64 sums of up to ~1e8 windows in a different order (worst ca
 
 
 def _check(dev, orc, reads, k, cutoff=30, paired=False, local=False, ilps=(1, 2)):
-    """Every kernel variant (windows per lane = 1 and 2) must give the oracle's counts."""
+    """Every kernel variant (windows per lane = 1 and 2; k-mer interval table or LF steps) must give the oracle's
+    counts."""
     for ilp in ilps:
-        dev.tune(ilp=ilp, ilp_local=ilp)
-        got = _check_one(dev, orc, reads, k, cutoff, paired, local)
-    dev.tune(ilp=1, ilp_local=1)
+        for kt in (1, 0):
+            dev.tune(ilp=ilp, ilp_local=ilp, kmer_table=kt)
+            got = _check_one(dev, orc, reads, k, cutoff, paired, local)
+    dev.tune(ilp=1, ilp_local=1, kmer_table=1)
     return got
 
 
