@@ -43,6 +43,8 @@ def parse_args():
     p.add_argument("--triple-steps", type=int, default=1, help="three-symbol occ planes (1) or not (0)")
     p.add_argument("--kmer-table", type=int, default=1,
                    help="k-mer interval table for k <= 31 (1, default) or LF steps for every window (0)")
+    p.add_argument("--tune", action="append", default=[],
+                   help="extra launch tuning key=value (speq_device_set_tuning), e.g. ilp_kt=2; repeatable")
     p.add_argument("--no-lf-compare", action="store_true",
                    help="skip timing the LF-step kernel beside the k-mer-table kernel")
     p.add_argument("--cpu-seconds", type=float, default=15.0, help="target CPU-baseline sample duration")
@@ -84,6 +86,9 @@ def main():
         dev.tune(ilp=a.ilp)
     ilp = dev.tuning("ilp")
     dev.tune(kmer_table=a.kmer_table)
+    for kv in a.tune:
+        key, val = kv.split("=")
+        dev.tune(**{key: int(val)})
     ktab = dev.prepare(k)  # per-k index structure (like the .dat cache): built once, outside the timed region
     # the q-mer table level the scan uses (view_for_k in scan_kernels.hip)
     width = 3 if a.triple_steps else (2 if a.pair_steps else 1)
@@ -218,6 +223,7 @@ def main():
                             f"{c['length']} bp, {n_reads} x 150 bp {'pairs' if paired else 'reads'} per GPU, k={k}",
                 "k": k, "reads_per_gpu": n_reads, "paired": paired, "mode": a.mode, "prefix_q": a.prefix_q, "prefix_q_used": q_used, "pair_steps": a.pair_steps, "triple_steps": a.triple_steps, "label_table": int(idx.info().label_table), "ilp": ilp,
                 "blocks_per_cu": dev.tuning("blocks_per_cu"), "grid_blocks": dev.tuning("grid_blocks"),
+                "ilp_kt": dev.tuning("ilp_kt"), "kt_slots": dev.tuning("kt_slots"),
                 "kmers_per_step_per_gpu": kmers_per_step, "parallelism": f"dp{world} (reads sharded, index replicated)",
                 "index_build_s": round(build_s, 3), "index_builder": "gpu" if a.gpu_build else "host", "fm_text_len": int(idx.info().n),
                 "kmer_table": {"on": bool(ktab["table_bytes"]), "distinct_kmers": ktab["distinct_kmers"],

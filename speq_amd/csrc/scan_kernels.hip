@@ -23,6 +23,7 @@
 #include <hip/hip_runtime.h>
 
 #include <chrono>
+#include <algorithm>
 #include <climits>
 #include <cmath>
 #include <cstdint>
@@ -45,6 +46,18 @@ constexpr uint32_t BLOCK_THREADS = 64 * WAVES_PER_BLOCK;
 constexpr uint32_t MAX_K = 4096;
 constexpr uint32_t LDS_HIST_MAX_G = 2048;
 constexpr uint32_t QLUT_LEN = 42;  // phred42 ranks 0..41
+constexpr uint32_t QTAB_BYTES = QLUT_LEN * 16u;  // local mode: per-block LDS copy of {1 - 10^(-q/10), its reciprocal}
+
+// a / b correctly rounded (IEEE division) from y = RN(1 / b) by two FMA corrections: q0 = a y is within 2 ulp, the
+// first correction makes it faithful, and from a faithful quotient the second gives the correctly rounded one
+// (Markstein). Bit-identical to `a / b` for the finite, normal operands of the Phred weights (b in [0.2, 1)).
+__device__ __forceinline__ double div_rn(double a, double b, double y) {
+    double q = a * y;
+    double r = __fma_rn(-q, b, a);
+    q = __fma_rn(r, y, q);
+    r = __fma_rn(-q, b, a);
+    return __fma_rn(r, y, q);
+}
 
 enum { KM_GLOBAL = 0, KM_LOCAL = 1, KM_REF = 2 };
 
@@ -70,7 +83,7 @@ struct UnitSrc {
     const uint64_t* off;      // unit u spans [off[u], off[u+1] - end_adj)
     const uint64_t* cum_win;  // ref only: prefix sums of windows per text
     const int32_t* unit_group;  // ref only: group of each text
-    const double* qlut;       // local only: 1 - 10^(-q/10), q = 0..41
+    const double* qlut;       // local only: {1 - 10^(-q/10), 1 / that} for q = 0..41
     uint32_t* em_mult;        // optional: per SA position, # passing multi-group windows whose interval starts there
     uint32_t* em_hi;          // optional: the end of that interval
     uint64_t n_units;         // reads (not pairs) or texts
@@ -82,13 +95,14 @@ struct UnitSrc {
     uint32_t buf_bytes;       // per-wave staging buffer (bases)
 };
 
-// Per-wave LDS: bases [buf_bytes] | qualities [buf_bytes] (local mode) | bad-mask words | N-mask words.
+// Per-wave LDS: bases [buf_bytes] | qualities [buf_bytes] (local mode) | bad-mask words | N-mask words |
+// base bit-plane words (bit 0 of every base's 2-bit code, then bit 1; k-mer table scans).
 __host__ __device__ inline uint32_t staging_bytes(uint32_t k, uint32_t nwin) {
     return ((2u * (64u * nwin + k)) + 63u) & ~63u;
 }
 __host__ __device__ inline uint32_t mask_words(uint32_t buf) { return buf / 64u + 1u; }
 __host__ __device__ inline uint32_t wave_lds_bytes(uint32_t buf, bool local) {
-    return buf * (local ? 2u : 1u) + 16u * mask_words(buf);
+    return buf * (local ? 2u : 1u) + 32u * mask_words(buf);
 }
 
 __device__ __forceinline__ void wave_sync() {
@@ -408,22 +422,40 @@ __device__ __forceinline__ void search_packed_n(const DevView& I, const Rsrc& R,
 }
 
 // ---- k-mer interval table (the q-mer table taken to q = k; built per k by k_ktab_keys + k_ktab_fill) ----
-// Open addressing over 64-B buckets of four 16-B slots {key lo, key hi, lo, info}: key = the packed k-mer (2 bits per
-// base, last base lowest; k <= 31 so the all-ones key marks an empty slot), lo = start of its SA interval, info =
-// its classification: the group id, or 0x80000000 | (hi - lo) when the occurrences span >= 2 groups. Every distinct
+// Open addressing over 64-B buckets of four 16-B slots {key lo, key hi, lo, info}: key = the k-mer's two bit planes
+// (bit j of the low word = bit 0 of base j's 2-bit code, bit j of the high word = its bit 1; k <= 31, so bit 31 of
+// both words is clear and the all-ones key marks an empty slot), lo = start of its SA interval, info = its
+// classification: the group id, or 0x80000000 | (hi - lo) when the occurrences span >= 2 groups. Every distinct
 // N-free k-mer of the reference texts is present; a k-mer that is absent from the table does not occur. Keys are
 // placed by linear probing over buckets, slots in order, without deletions, so a lookup that meets an empty slot
-// before its key has proven the key absent.
+// before its key has proven the key absent. A scan reads a window's key straight from the ballots of its bases.
 constexpr uint32_t KT_MAX_K = 31;
 constexpr unsigned long long KT_EMPTY = ~0ull;
 
-__host__ __device__ __forceinline__ uint64_t kt_hash(uint64_t x) {  // murmur3 fmix64
-    x ^= x >> 33;
-    x *= 0xff51afd7ed558ccdULL;
-    x ^= x >> 33;
-    x *= 0xc4ceb9fe1a85ec53ULL;
-    x ^= x >> 33;
+__host__ __device__ __forceinline__ uint32_t kt_hash(uint64_t key) {  // two 31-bit planes -> 32-bit bucket hash
+    uint32_t x = (uint32_t)key ^ ((uint32_t)(key >> 32) * 0x9E3779B1u);
+    x ^= x >> 16;  // murmur3 fmix32
+    x *= 0x85EBCA6Bu;
+    x ^= x >> 13;
+    x *= 0xC2B2AE35u;
+    x ^= x >> 16;
     return x;
+}
+
+// Bits [off, off + k) of a wave's plane words (k <= 31): bit j = base off + j.
+__device__ __forceinline__ uint64_t plane_bits(const unsigned long long* pl, uint32_t off, uint32_t k) {
+    const uint32_t w0 = off >> 6, sh = off & 63u;
+    uint64_t v = pl[w0] >> sh;
+    if (sh + k > 64u) v |= pl[w0 + 1u] << (64u - sh);
+    return v & ((1ull << k) - 1ull);
+}
+
+// The packed code (2 bits per base, last base lowest: the form search_packed_n takes) of a plane key.
+__device__ __forceinline__ uint64_t kt_code(uint64_t key, uint32_t k) {
+    uint64_t code = 0;
+    for (uint32_t j = 0; j < k; ++j)
+        code = (code << 2) | ((key >> j) & 1ull) | (((key >> (32u + j)) & 1ull) << 1);
+    return code;
 }
 
 // Same outputs as search_packed_n (group / -2 / -1 and, for -2, the SA interval) from one bucket load per window:
@@ -432,14 +464,14 @@ __host__ __device__ __forceinline__ uint64_t kt_hash(uint64_t x) {  // murmur3 f
 template <int NW>
 __device__ __forceinline__ void search_ktab_n(const DevView& I, const uint64_t (&P)[NW], const bool (&act)[NW],
                                               int (&out)[NW], uint32_t (&lo_out)[NW], uint32_t (&hi_out)[NW]) {
-    uint64_t b[NW];
+    uint32_t b[NW];
     bool pend[NW];
 #pragma unroll
     for (int w = 0; w < NW; ++w) {
         out[w] = -1;
         lo_out[w] = hi_out[w] = 0;
         pend[w] = act[w];
-        b[w] = kt_hash(P[w]) & I.kt_bmask;
+        b[w] = kt_hash(P[w]) & (uint32_t)I.kt_bmask;
     }
     for (;;) {
         bool any = false;
@@ -475,7 +507,7 @@ __device__ __forceinline__ void search_ktab_n(const DevView& I, const uint64_t (
                     hi_out[w] = multi ? lo + (info & 0x7FFFFFFFu) : lo + 1u;  // single group: only lo is kept
                 }
                 pend[w] = !(found || empty);
-                b[w] = (b[w] + 1u) & I.kt_bmask;
+                b[w] = (b[w] + 1u) & (uint32_t)I.kt_bmask;
             }
     }
 }
@@ -483,12 +515,15 @@ __device__ __forceinline__ void search_ktab_n(const DevView& I, const uint64_t (
 #ifndef SPEQ_MIN_WAVES  // A/B knob: minimum waves per SIMD the register allocator must allow
 #define SPEQ_MIN_WAVES 1
 #endif
+#ifndef SPEQ_KT_MIN_WAVES  // the same for global-mode k-mer-table scans, one window per lane: 6 waves/SIMD (<= 80 VGPRs)
+#define SPEQ_KT_MIN_WAVES 6  // keep more lookups in flight (cfg 2: +9 %, profiles/r01/ab_kt_occupancy.jsonl)
+#endif
 
 // EM: also record the SA interval of every passing multi-group window (EM histogram scans only).
 // KT: windows of k <= 31 are resolved in the k-mer interval table (I.ktab, I.kt_k == k) instead of by LF steps; a
 // separate instantiation, so the LF-step kernel keeps its own register allocation.
 template <int MODE, bool PAIRED, bool LDS_HIST, int NWIN, bool EM, bool KT>
-__global__ __launch_bounds__(BLOCK_THREADS, SPEQ_MIN_WAVES) void k_scan(DevView I, UnitSrc src, unsigned long long* __restrict__ out_a,
+__global__ __launch_bounds__(BLOCK_THREADS, (KT && NWIN == 1 && MODE == KM_GLOBAL) ? SPEQ_KT_MIN_WAVES : SPEQ_MIN_WAVES) void k_scan(DevView I, UnitSrc src, unsigned long long* __restrict__ out_a,
                                                         unsigned long long* __restrict__ out_b,
                                                         double* __restrict__ out_w) {
     // out_a: reads -> counts[G+2] (T, ambiguous, U[g]); ref -> U_ref[G]
@@ -503,17 +538,22 @@ __global__ __launch_bounds__(BLOCK_THREADS, SPEQ_MIN_WAVES) void k_scan(DevView 
     unsigned long long* hB = hA + G;              // KM_REF: Tot_ref
     double* hW = reinterpret_cast<double*>(hA + G);  // KM_LOCAL: W
     const uint32_t buf = src.buf_bytes;
-    unsigned char* sbuf = smem + hist_bytes + wid * wave_lds_bytes(buf, MODE == KM_LOCAL);
+    double2* qtab = reinterpret_cast<double2*>(smem + hist_bytes);  // KM_LOCAL only
+    const uint32_t qtab_bytes = MODE == KM_LOCAL ? QTAB_BYTES : 0u;
+    unsigned char* sbuf = smem + hist_bytes + qtab_bytes + wid * wave_lds_bytes(buf, MODE == KM_LOCAL);
     unsigned char* qbuf = sbuf + buf;
     unsigned long long* mbuf =
         reinterpret_cast<unsigned long long*>(sbuf + buf * (MODE == KM_LOCAL ? 2u : 1u));
     unsigned long long* nbuf = mbuf + mask_words(buf);  // KM_REF: N positions (windows with N search via LDS)
+    unsigned long long* pbuf = nbuf + mask_words(buf);  // KT: bit 0 planes, then (+ mask_words) bit 1 planes
     const Rsrc R = make_rsrc(I);
 
-    if (LDS_HIST) {
+    if (MODE == KM_LOCAL)
+        for (uint32_t i = threadIdx.x; i < QLUT_LEN; i += BLOCK_THREADS)
+            qtab[i] = make_double2(src.qlut[2 * i], src.qlut[2 * i + 1]);
+    if (LDS_HIST)
         for (uint32_t i = threadIdx.x; i < hist_words; i += BLOCK_THREADS) hA[i] = 0ull;
-        __syncthreads();
-    }
+    if (LDS_HIST || MODE == KM_LOCAL) __syncthreads();
     unsigned long long* gU = (MODE == KM_REF) ? out_a : out_a + 2;
 
     const uint64_t NW = (uint64_t)gridDim.x * WAVES_PER_BLOCK;
@@ -604,10 +644,9 @@ __global__ __launch_bounds__(BLOCK_THREADS, SPEQ_MIN_WAVES) void k_scan(DevView 
         // ---- 2. stage bases [s0, s0 + span) into LDS; ballot the "bad" mask 64 bases at a time
         for (uint32_t p0 = 0; p0 < span; p0 += 64u) {
             const uint32_t p = p0 + lane;
-            uint32_t bad = 1, isn = 0;
+            uint32_t bad = 1, isn = 0, sym = 0;
             if (p < span) {
                 const uint32_t ch = ld_stream(src.seq + s0 + p);
-                uint32_t sym;
                 if (MODE == KM_REF) {
                     sym = ch - 2u;            // SA alphabet A..N = 2..6
                     bad = ch < 2u ? 1u : 0u;  // separator / terminator
@@ -623,6 +662,13 @@ __global__ __launch_bounds__(BLOCK_THREADS, SPEQ_MIN_WAVES) void k_scan(DevView 
             }
             const uint64_t m = __ballot(bad != 0u);
             if (lane == 0) mbuf[p0 >> 6] = m;
+            if (KT) {  // the k-mer table key of a window is its two base bit planes (see kt_key)
+                const uint64_t b0 = __ballot((sym & 1u) != 0u), b1 = __ballot((sym & 2u) != 0u);
+                if (lane == 0) {
+                    pbuf[p0 >> 6] = b0;
+                    pbuf[mask_words(buf) + (p0 >> 6)] = b1;
+                }
+            }
             if (MODE == KM_REF) {
                 const uint64_t nm = __ballot(isn != 0u);
                 if (lane == 0) nbuf[p0 >> 6] = nm;
@@ -654,12 +700,14 @@ __global__ __launch_bounds__(BLOCK_THREADS, SPEQ_MIN_WAVES) void k_scan(DevView 
                 }
                 valid[w] = badbits == 0;
                 packed[w] = valid[w] && k <= 32u && nbits == 0;
-                if (packed[w]) {
+                if (KT && packed[w]) {
+                    P[w] = plane_bits(pbuf, off[w], k) | (plane_bits(pbuf + mask_words(buf), off[w], k) << 32);
+                } else if (packed[w]) {
                     const unsigned char* ws = sbuf + off[w];
                     uint64_t x = 0;
                     for (uint32_t i = 0; i < k; ++i) x = (x << 2) | (uint64_t)(ws[i] & 3u);
                     P[w] = x;
-                } else if (valid[w]) {
+                } else if (valid[w] && !(KT && MODE != KM_REF)) {  // KT read scans: k <= 31, no N -> packed
                     which[w] = search_lds(I, R, sbuf + off[w], k, nbits == 0, ilo[w], ihi[w]);
                 }
             }
@@ -706,7 +754,10 @@ __global__ __launch_bounds__(BLOCK_THREADS, SPEQ_MIN_WAVES) void k_scan(DevView 
                         // w = 1.0; for q in window: w = w / (1 - 1/10^(q/10))   (fm_scanner.cpp:454, left to right)
                         const unsigned char* qw = qbuf + off[w];
                         double x = 1.0;
-                        for (uint32_t i = 0; i < k; ++i) x = x / src.qlut[qw[i]];
+                        for (uint32_t i = 0; i < k; ++i) {
+                            const double2 t = qtab[qw[i]];
+                            x = div_rn(x, t.x, t.y);  // == x / t.x
+                        }
                         wgt = x;
                     }
                     if (LDS_HIST) {
@@ -800,7 +851,6 @@ __global__ void k_ktab_keys(const uint8_t* __restrict__ text, const uint64_t* __
                             const uint64_t* __restrict__ cum, uint32_t n_texts, uint64_t total, uint32_t k,
                             unsigned long long* __restrict__ keys, uint64_t smask,
                             unsigned long long* __restrict__ n_distinct) {
-    const uint64_t kmask = (1ull << (2u * k)) - 1ull;  // k <= 31
     const uint64_t nruns = (total + KT_RUN - 1) / KT_RUN;
     unsigned long long added = 0;
     for (uint64_t run = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; run < nruns;
@@ -811,7 +861,7 @@ __global__ void k_ktab_keys(const uint8_t* __restrict__ text, const uint64_t* __
             const uint32_t mid = (t + hi) >> 1;
             if (cum[mid] <= f0) t = mid; else hi = mid;
         }
-        uint64_t code = 0;
+        uint64_t lo_pl = 0, hi_pl = 0;  // bit planes of the window (bit j = base j)
         uint32_t good = 0;  // consecutive ACGT symbols ending at the window's last base
         bool fresh = true;
         for (uint64_t f = f0; f < f1; ++f) {
@@ -821,23 +871,28 @@ __global__ void k_ktab_keys(const uint8_t* __restrict__ text, const uint64_t* __
             }
             const uint8_t* base = text + tstart[t] + (f - cum[t]);
             if (fresh) {
-                code = 0;
+                lo_pl = hi_pl = 0;
                 good = 0;
                 for (uint32_t i = 0; i < k; ++i) {
                     const uint32_t c = base[i];  // SA alphabet: A..T = 2..5, N = 6
                     const bool acgt = c >= 2u && c <= 5u;
-                    code = ((code << 2) | (acgt ? c - 2u : 0u)) & kmask;
+                    const uint32_t sym = acgt ? c - 2u : 0u;
+                    lo_pl |= (uint64_t)(sym & 1u) << i;
+                    hi_pl |= (uint64_t)(sym >> 1) << i;
                     good = acgt ? good + 1u : 0u;
                 }
                 fresh = false;
             } else {
                 const uint32_t c = base[k - 1];
                 const bool acgt = c >= 2u && c <= 5u;
-                code = ((code << 2) | (acgt ? c - 2u : 0u)) & kmask;
+                const uint32_t sym = acgt ? c - 2u : 0u;
+                lo_pl = (lo_pl >> 1) | ((uint64_t)(sym & 1u) << (k - 1));
+                hi_pl = (hi_pl >> 1) | ((uint64_t)(sym >> 1) << (k - 1));
                 good = acgt ? good + 1u : 0u;
             }
+            const uint64_t code = lo_pl | (hi_pl << 32);
             if (good < k) continue;
-            uint64_t sl = kt_hash(code) & smask;
+            uint64_t sl = kt_hash(code) & smask;  // smask < 2^32
             for (;;) {
                 unsigned long long prev = __atomic_load_n(&keys[sl], __ATOMIC_RELAXED);
                 if (prev == KT_EMPTY) prev = atomicCAS(&keys[sl], KT_EMPTY, (unsigned long long)code);
@@ -862,14 +917,14 @@ __global__ void k_ktab_fill(DevView I, const unsigned long long* __restrict__ ke
          i += (uint64_t)gridDim.x * blockDim.x) {
         const unsigned long long code = keys[i];
         if (code == KT_EMPTY) continue;
-        const uint64_t P[1] = {code};
+        const uint64_t P[1] = {kt_code(code, k)};
         const bool act[1] = {true};
         int out[1];
         uint32_t lo[1], hi[1];
         search_packed_n<1>(I, R, P, act, k, out, lo, hi);
         if (out[0] == -1) continue;  // unreachable: every key occurs in the texts
         const uint32_t info = out[0] == -2 ? (0x80000000u | (hi[0] - lo[0])) : (uint32_t)out[0];
-        uint64_t b = kt_hash(code) & bmask;
+        uint64_t b = kt_hash(code) & bmask;  // bmask < 2^32
         for (bool placed = false; !placed; b = (b + 1) & bmask) {
             for (uint32_t j = 0; j < 4u && !placed; ++j) {
                 uint4* slot = table + b * 4u + j;
@@ -937,6 +992,9 @@ struct speq_device_index {
     int prefix_choice = -1;       // tuning "prefix_level": -1 = by k (view_for_k), 0..2 = force q - level
     uint32_t base_q = 0;          // the index's prefix_q
     bool kmer_table = true;       // tuning "kmer_table": scans of k <= 31 look windows up in a per-k k-mer table
+    uint32_t ilp_kt = 1;          // tuning "ilp_kt": windows per lane of k-mer-table scans (1, 2 or 4)
+    uint32_t blocks_per_cu_kt = 0;  // tuning "blocks_per_cu_kt": blocks_per_cu of k-mer-table scans (default: no cap)
+    uint32_t kt_slots = 4;        // tuning "kt_slots": table slots per distinct k-mer (load factor 1/kt_slots .. 2/kt_slots)
     struct KmerTable {
         uint4* table = nullptr;
         uint64_t buckets = 0, distinct = 0;
@@ -972,6 +1030,9 @@ void allow_big_lds_kt() {
                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     if (MODE != KM_REF)
         HIP_OK(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_scan<MODE, PAIRED, LDS, 1, MODE != KM_REF, KT>),
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    if (KT && MODE == KM_GLOBAL)
+        HIP_OK(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_scan<MODE, PAIRED, LDS, 4, false, KT>),
                                    hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
 }
 
@@ -1070,6 +1131,7 @@ speq_device_index::KmerTable build_ktab(speq_device_index* d, uint32_t k) {
     try {
         unsigned long long distinct = 0;
         const uint64_t slots = next_pow2(std::max<uint64_t>(2 * total, 64));
+        if (slots > (1ull << 32)) throw std::invalid_argument("k-mer table: more than 2^31 reference windows");
         if (total > 0) {
             HIP_OK(hipMalloc(&keys, slots * 8));
             HIP_OK(hipMalloc(&d_cum, cum.size() * 8));
@@ -1086,7 +1148,7 @@ speq_device_index::KmerTable build_ktab(speq_device_index* d, uint32_t k) {
             HIP_OK(hipStreamSynchronize(d->stream));
         }
         kt.distinct = distinct;
-        kt.buckets = next_pow2(std::max<uint64_t>(1, (distinct + 1) / 2));  // 4 slots per bucket: load <= 1/2
+        kt.buckets = next_pow2(std::max<uint64_t>(1, (distinct * d->kt_slots + 3) / 4));  // 4 slots per bucket
         HIP_OK(hipMalloc(&kt.table, kt.buckets * 64));
         d->track(kt.table);
         HIP_OK(hipMemsetAsync(kt.table, 0xFF, kt.buckets * 64, d->stream));
@@ -1119,10 +1181,14 @@ const speq_device_index::KmerTable* ensure_ktab(speq_device_index* d, uint32_t k
 template <int MODE, bool PAIRED, bool LDS, bool KT>
 void launch_v(const speq_device_index* d, const DevView& v, const UnitSrc& src, uint32_t grid, size_t lds,
               hipStream_t st, unsigned long long* a, unsigned long long* b, double* w) {
+    const uint32_t ilp = KT ? d->ilp_kt : (MODE == KM_LOCAL ? d->ilp_local : d->ilp);
     if (MODE != KM_REF && src.em_mult != nullptr)
         hipLaunchKernelGGL((k_scan<MODE, PAIRED, LDS, 1, MODE != KM_REF, KT>), dim3(grid), dim3(BLOCK_THREADS), lds,
                            st, v, src, a, b, w);
-    else if ((MODE == KM_LOCAL ? d->ilp_local : d->ilp) == 2)
+    else if (KT && MODE == KM_GLOBAL && ilp == 4)
+        hipLaunchKernelGGL((k_scan<MODE, PAIRED, LDS, 4, false, KT>), dim3(grid), dim3(BLOCK_THREADS), lds, st, v,
+                           src, a, b, w);
+    else if (ilp >= 2)
         hipLaunchKernelGGL((k_scan<MODE, PAIRED, LDS, 2, false, KT>), dim3(grid), dim3(BLOCK_THREADS), lds, st, v,
                            src, a, b, w);
     else
@@ -1148,15 +1214,16 @@ void launch_scan(speq_device_index* d, int mode, bool paired, const UnitSrc& src
     const speq_device_index::KmerTable* kt = ensure_ktab(d, src.k);
     const bool lds_hist = d->G <= LDS_HIST_MAX_G;
     const uint32_t hist_words = lds_hist ? ((mode == KM_GLOBAL) ? d->G : 2u * d->G) : 0u;
-    const size_t lds = ((hist_words * 8u + 15u) & ~15u) +
+    const size_t lds = ((hist_words * 8u + 15u) & ~15u) + (mode == KM_LOCAL ? QTAB_BYTES : 0u) +
                        (size_t)WAVES_PER_BLOCK * wave_lds_bytes(src.buf_bytes, mode == KM_LOCAL);
     // >= 4 units (or 256 windows) per wave; grid capped (default 4096 = 2x the 8 resident blocks x 256 CUs).
     uint64_t blocks = (work_units + 4 * WAVES_PER_BLOCK - 1) / (4 * WAVES_PER_BLOCK);
     if (blocks < 1) blocks = 1;
     if (blocks > d->grid_blocks) blocks = d->grid_blocks;
     size_t lds_launch = lds;
-    if (d->blocks_per_cu > 0) {  // occupancy cap: pad dynamic LDS so only blocks_per_cu blocks fit a CU
-        const size_t pad = (160u * 1024u) / d->blocks_per_cu;
+    const uint32_t bpc = kt ? d->blocks_per_cu_kt : d->blocks_per_cu;
+    if (bpc > 0) {  // occupancy cap: pad dynamic LDS so only bpc blocks fit a CU
+        const size_t pad = (160u * 1024u) / bpc;
         if (pad > lds_launch) lds_launch = pad & ~(size_t)15;
     }
     const uint32_t grid = (uint32_t)blocks;
@@ -1199,7 +1266,7 @@ static void scan_device_impl(speq_device_index* d, const uint8_t* d_seq, const u
     src.end_adj = 0;
     src.k = p->k;
     src.cutoff = p->phred_cutoff;
-    src.buf_bytes = staging_bytes(p->k, std::max(d->ilp, d->ilp_local));
+    src.buf_bytes = staging_bytes(p->k, std::max({d->ilp, d->ilp_local, d->ilp_kt}));
     const int mode = p->mode == SPEQ_MODE_LOCAL ? KM_LOCAL : KM_GLOBAL;
     hipEvent_t e0 = nullptr, e1 = nullptr;
     if (d->timing) {
@@ -1296,8 +1363,11 @@ int speq_device_open(const speq_index* idx, int device, speq_device_index** out)
         d->d_text = d->track(dev_upload(fm.text));
         d->d_text_start = d->track(dev_upload(fm.text_start));
         d->d_text_group = d->track(dev_upload(fm.text_group));
-        std::vector<double> lut(QLUT_LEN);
-        for (uint32_t q = 0; q < QLUT_LEN; ++q) lut[q] = 1.0 - 1.0 / std::pow(10.0, (double)q / 10.0);
+        std::vector<double> lut(2 * QLUT_LEN);  // {1 - 1/10^(q/10) (fm_scanner.cpp:454), its reciprocal}
+        for (uint32_t q = 0; q < QLUT_LEN; ++q) {
+            lut[2 * q] = 1.0 - 1.0 / std::pow(10.0, (double)q / 10.0);
+            lut[2 * q + 1] = 1.0 / lut[2 * q];  // q = 0: inf, never used (a passing window has every q > cutoff >= 0)
+        }
         d->d_qlut = d->track(dev_upload(lut));
         HIP_OK(hipStreamCreateWithFlags(&d->stream, hipStreamNonBlocking));
         hipDeviceProp_t prop;
@@ -1486,7 +1556,7 @@ uint64_t* launch_ref_shard(speq_device_index* d, uint32_t k, uint32_t shard, uin
     src.win_base = w0;
     src.end_adj = 1;
     src.k = k;
-    src.buf_bytes = staging_bytes(k, d->ilp);
+    src.buf_bytes = staging_bytes(k, std::max(d->ilp, d->ilp_kt));
     launch_scan(d, KM_REF, false, src, (w1 - w0 + 255) / 256, st, reinterpret_cast<unsigned long long*>(d_u_ref),
                 reinterpret_cast<unsigned long long*>(d_tot_ref), nullptr);
     return d_cum;
@@ -1619,6 +1689,15 @@ int speq_device_set_tuning(speq_device_index* d, const char* key, int64_t value)
         } else if (k == "sparse_prefix") {
             if (value < -1 || value > 1) throw std::invalid_argument("sparse_prefix must be -1 (auto), 0 or 1");
             d->sparse_choice = (int)value;
+        } else if (k == "blocks_per_cu_kt") {
+            if (value < 0 || value > 8) throw std::invalid_argument("blocks_per_cu_kt must be in [0, 8]");
+            d->blocks_per_cu_kt = (uint32_t)value;
+        } else if (k == "ilp_kt") {
+            if (value != 1 && value != 2 && value != 4) throw std::invalid_argument("ilp_kt must be 1, 2 or 4");
+            d->ilp_kt = (uint32_t)value;
+        } else if (k == "kt_slots") {
+            if (value < 2 || value > 16) throw std::invalid_argument("kt_slots must be in [2, 16]");
+            d->kt_slots = (uint32_t)value;
         } else if (k == "kmer_table") {
             if (value != 0 && value != 1) throw std::invalid_argument("kmer_table must be 0 or 1");
             d->kmer_table = value != 0;
@@ -1648,6 +1727,9 @@ int speq_device_get_tuning(const speq_device_index* d, const char* key, int64_t*
         else if (k == "fastq_gpu_parse") *value = d->fastq_gpu ? 1 : 0;
         else if (k == "stream_lanes") *value = d->stream_lanes;
         else if (k == "kmer_table") *value = d->kmer_table ? 1 : 0;
+        else if (k == "ilp_kt") *value = d->ilp_kt;
+        else if (k == "blocks_per_cu_kt") *value = d->blocks_per_cu_kt;
+        else if (k == "kt_slots") *value = d->kt_slots;
         else throw std::invalid_argument("speq_device_get_tuning: unknown key " + k);
     });
 }

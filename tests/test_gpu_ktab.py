@@ -94,3 +94,45 @@ def test_absent_kmers_and_oracle():
         T, amb, U, _ = Oracle(ref.records, ref.groups, 4, k).scan(seq, qual, off)
         assert (r.total, r.ambiguous, r.unique.tolist()) == (T, amb, U.tolist())
         assert r.total == 2 * n * (L - k + 1)
+
+
+@pytest.mark.parametrize("ilp_kt", [1, 2, 4])
+@pytest.mark.parametrize("kt_slots", [2, 5, 16])
+def test_launch_knobs_keep_results(small, ilp_kt, kt_slots):
+    ref, idx = small
+    reads = synth.make_reads(ref, 4_000, n_rate=0.002, lowq_rate=0.01, short_frac=0.05)
+    dev = DeviceIndex(idx)
+    dev.tune(ilp_kt=ilp_kt, kt_slots=kt_slots)
+    for k in (13, 21, 31):
+        r = dev.scan(reads.seq.tobytes(), reads.qual.tobytes(), reads.offsets, k=k)
+        T, amb, U, _ = Oracle(ref.records, ref.groups, 3, k).scan(reads.seq, reads.qual, reads.offsets)
+        assert (r.total, r.ambiguous, r.unique.tolist()) == (T, amb, U.tolist())
+
+
+def test_phred_weight_of_one_window_is_bit_exact(small):
+    """A read of exactly k bases that occurs in one group: W[g] is that window's weight, which must equal the
+    reference's left-to-right divisions w = w / (1 - 1/10^(q/10)) (fm_scanner.cpp:454) to the last bit."""
+    ref, idx = small
+    dev = DeviceIndex(idx)
+    rng = np.random.default_rng(11)
+    k = 31
+    checked = 0
+    for _ in range(150):
+        r = int(rng.integers(0, len(ref.records)))
+        rec = ref.records[r]
+        p = int(rng.integers(0, len(rec) - k))
+        seq = rec[p:p + k].upper()
+        if b"N" in seq:
+            continue
+        q = rng.integers(31, 42, size=k)
+        qual = bytes((q + 33).astype(np.uint8))
+        res = dev.scan(seq, qual, np.array([0, k], dtype=np.uint64), k=k, local=True)
+        if res.unique.sum() != 1:
+            continue  # the window is shared by several groups
+        w = 1.0
+        for x in q:
+            w = w / (1.0 - 1.0 / (10.0 ** (float(x) / 10.0)))
+        g = int(np.argmax(res.unique))
+        assert res.weights[g] == w, (res.weights[g], w)
+        checked += 1
+    assert checked > 50
