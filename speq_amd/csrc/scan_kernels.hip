@@ -843,6 +843,356 @@ __global__ __launch_bounds__(BLOCK_THREADS, (KT && NWIN == 1 && MODE == KM_GLOBA
     }
 }
 
+// ---- software-pipelined k-mer-table read scan (one window per lane) ----
+// k_scan runs each pass of 64 windows as three dependent global round trips (read offsets -> bases -> table), so a
+// wave spends most of a pass waiting. k_scan_kt overlaps them across passes: while the table lookups of pass i are
+// in flight, the offsets of pass i + 2 and the bases of pass i + 1 are already loading. Same results as k_scan
+// (KM_GLOBAL / KM_LOCAL reads, paired or not, EM or not); the pass logic is k_scan's with NWIN = 1.
+// Wave-uniform lane reads (v_readlane: the result lives in a scalar register, unlike __shfl's ds_bpermute).
+__device__ __forceinline__ uint32_t rl32(uint32_t v, uint32_t l) { return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)l); }
+__device__ __forceinline__ int rli(int v, uint32_t l) { return __builtin_amdgcn_readlane(v, (int)l); }
+__device__ __forceinline__ uint64_t rl64(uint64_t v, uint32_t l) {
+    return (uint64_t)rl32((uint32_t)v, l) | ((uint64_t)rl32((uint32_t)(v >> 32), l) << 32);
+}
+
+struct KtCursor {
+    uint64_t r, o;             // first unit of the pass and the window offset in it
+    uint64_t s0;               // first base of the pass
+    uint32_t ri, oo, off;      // this lane's slot: read r + ri, window oo of it, first base s0 + off
+    uint32_t span, ri_last, oo_last;
+    uint32_t has;              // this lane holds a window (0/1)
+    uint32_t any;              // the pass holds a window (0/1; wave-uniform)
+};
+
+// Offsets of reads r + lane and r + lane + 1 (issued here, consumed by kt_cursor). Every lane loads (indices are
+// clamped to the valid range off[0 .. r_end]): unconditional loads let the compiler count them, so a later wait for
+// these does not also wait for the table lookups issued after them.
+__device__ __forceinline__ void kt_load_offsets(const UnitSrc& src, uint64_t r, uint64_t r_end, uint32_t lane,
+                                                uint64_t& b, uint64_t& e) {
+    const uint64_t i = r + lane < r_end ? r + lane : r_end;
+    b = src.off[i];
+    e = src.off[i + 1 <= r_end ? i + 1 : r_end];
+}
+
+constexpr uint32_t KT_SPAN = 128;  // bases a pass of k_scan_kt stages: two chunks of 64 (windows past it wait)
+
+__device__ __forceinline__ KtCursor kt_cursor(uint64_t r, uint64_t o, uint64_t r_end,
+                                              uint64_t bl_, uint64_t el_, uint32_t lane, uint32_t k) {
+    KtCursor c;
+    c.r = r;
+    c.o = o;
+    uint32_t wl = 0;
+    if (r + lane < r_end) {
+        const uint64_t L = el_ - bl_;
+        uint64_t W = L >= k ? L - k + 1 : 0;
+        if (lane == 0) W = W > o ? W - o : 0;
+        wl = (uint32_t)(W < 65u ? W : 65u);
+    }
+    uint32_t incl = wl;
+    for (uint32_t d = 1; d < 64u; d <<= 1) {
+        const uint32_t y = __shfl_up(incl, d);
+        if (lane >= d) incl += y;
+    }
+    const uint32_t total = rl32(incl, 63);
+    c.any = total > 0 ? 1u : 0u;
+    uint32_t i_lo = 0;
+    for (uint32_t step = 32; step >= 1; step >>= 1) {
+        const uint32_t v = __shfl(incl, (int)(i_lo + step - 1u));
+        if (v <= lane) i_lo += step;
+    }
+    c.ri = i_lo > 63u ? 63u : i_lo;
+    const uint32_t excl_i = __shfl(incl, (int)c.ri) - __shfl(wl, (int)c.ri);
+    c.oo = lane - excl_i;
+    const uint64_t pos = __shfl(bl_, (int)c.ri) + c.oo + (c.ri == 0 ? o : 0);
+    c.s0 = rl64(pos, 0);
+    c.off = (uint32_t)(pos - c.s0);
+    c.has = (lane < total && pos + k - c.s0 <= KT_SPAN) ? 1u : 0u;  // the first window (pos == s0) fits: k <= 31
+    const uint32_t n = (uint32_t)__popcll(__ballot(c.has != 0u));
+    const uint32_t off_last = n ? rl32(c.off, n - 1u) : 0u;
+    c.ri_last = n ? rl32(c.ri, n - 1u) : 0u;
+    c.oo_last = n ? rl32(c.oo, n - 1u) : 0u;
+    c.span = off_last + k;
+    return c;
+}
+
+// Where the pass after `c` starts (k_scan's cursor advance); a pass without windows skips 64 units.
+__device__ __forceinline__ void kt_advance(const KtCursor& c, uint64_t r_end, uint64_t& r, uint64_t& o) {
+    if (!c.any) {
+        r = (c.r + 64 < r_end) ? c.r + 64 : r_end;
+        o = 0;
+    } else {
+        o = (c.ri_last == 0 ? c.o : 0) + c.oo_last + 1;
+        r = c.r + c.ri_last;
+    }
+}
+
+// One 64-base chunk of a k_scan_kt pass into LDS: qualities (local mode), the bad mask and the two base bit planes.
+template <int MODE>
+__device__ __forceinline__ void kt_stage_chunk(const UnitSrc& src, uint32_t ch, uint32_t qv, uint32_t p,
+                                               uint32_t span, unsigned char* qbuf, unsigned long long* mbuf,
+                                               unsigned long long* p0buf, unsigned long long* p1buf, uint32_t j) {
+    uint32_t bad = 1, sym = 0;
+    if (p < span) {
+        sym = ascii_sym(ch);
+        int q = (int)qv - 33;
+        q = q < 0 ? 0 : (q > 41 ? 41 : q);
+        bad = ((uint32_t)q <= src.cutoff || sym == 4u) ? 1u : 0u;
+        if (MODE == KM_LOCAL) qbuf[p] = (unsigned char)q;
+    }
+    const uint64_t m = __ballot(bad != 0u);
+    const uint64_t b0 = __ballot((sym & 1u) != 0u), b1 = __ballot((sym & 2u) != 0u);
+    if ((p & 63u) == 0u) {
+        mbuf[j] = m;
+        p0buf[j] = b0;
+        p1buf[j] = b1;
+    }
+}
+
+#ifndef SPEQ_KTP_MIN_WAVES
+#define SPEQ_KTP_MIN_WAVES 1
+#endif
+template <int MODE, bool PAIRED, bool LDS_HIST, bool EM>
+__global__ __launch_bounds__(BLOCK_THREADS, SPEQ_KTP_MIN_WAVES)
+void k_scan_kt(DevView I, UnitSrc src, unsigned long long* __restrict__ out_a, double* __restrict__ out_w) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const uint32_t lane = threadIdx.x & 63u, wid = threadIdx.x >> 6;
+    const uint32_t G = I.G, k = src.k;
+    const uint32_t hist_words = LDS_HIST ? ((MODE == KM_GLOBAL) ? G : 2u * G) : 0u;
+    const uint32_t hist_bytes = (hist_words * 8u + 15u) & ~15u;
+    unsigned long long* hA = reinterpret_cast<unsigned long long*>(smem);
+    double* hW = reinterpret_cast<double*>(hA + G);  // KM_LOCAL: W
+    const uint32_t buf = src.buf_bytes;
+    double2* qtab = reinterpret_cast<double2*>(smem + hist_bytes);  // KM_LOCAL only
+    const uint32_t qtab_bytes = MODE == KM_LOCAL ? QTAB_BYTES : 0u;
+    // per wave: qualities [buf] (local mode) | bad-mask words | bit-0 plane words | bit-1 plane words
+    const uint32_t mw = mask_words(buf);
+    unsigned char* wbase = smem + hist_bytes + qtab_bytes + wid * (buf * (MODE == KM_LOCAL ? 1u : 0u) + 24u * mw);
+    unsigned char* qbuf = wbase;
+    unsigned long long* mbuf = reinterpret_cast<unsigned long long*>(wbase + (MODE == KM_LOCAL ? buf : 0u));
+    unsigned long long* p0buf = mbuf + mw;
+    unsigned long long* p1buf = p0buf + mw;
+
+    if (MODE == KM_LOCAL)
+        for (uint32_t i = threadIdx.x; i < QLUT_LEN; i += BLOCK_THREADS)
+            qtab[i] = make_double2(src.qlut[2 * i], src.qlut[2 * i + 1]);
+    if (LDS_HIST)
+        for (uint32_t i = threadIdx.x; i < hist_words; i += BLOCK_THREADS) hA[i] = 0ull;
+    if (LDS_HIST || MODE == KM_LOCAL) __syncthreads();
+    unsigned long long* gU = out_a + 2;
+
+    const uint64_t NW = (uint64_t)gridDim.x * WAVES_PER_BLOCK;
+    const uint64_t gw = (uint64_t)blockIdx.x * WAVES_PER_BLOCK + wid;
+    const uint64_t nu = PAIRED ? src.n_units / 2 : src.n_units;
+    const uint64_t u0 = nu * gw / NW, u1 = nu * (gw + 1) / NW;
+    const uint64_t r_end = PAIRED ? 2 * u1 : u1;
+
+    uint32_t t_cnt = 0, amb = 0;
+    int cmin = INT_MAX, cmax = -1;
+    uint64_t cunit = ~0ull;
+
+    // staging registers of one pass: 2 chunks of 64 bases (span <= KT_SPAN)
+    uint32_t sc0 = 0, sc1 = 0, sq0 = 0, sq1 = 0;
+#define KT_STAGE_LOAD(c, fallback)                                                             \
+    do {                                                                                       \
+        const uint64_t b_ = (c).any ? (c).s0 : (fallback);                                     \
+        const uint32_t l_ = (c).any ? (c).span - 1u : 0u;                                      \
+        sc0 = ld_stream(src.seq + b_ + min(lane, l_));                                         \
+        sq0 = ld_stream(src.qual + b_ + min(lane, l_));                                        \
+        sc1 = ld_stream(src.seq + b_ + min(64u + lane, l_));                                   \
+        sq1 = ld_stream(src.qual + b_ + min(64u + lane, l_));                                  \
+    } while (0)
+#define KT_STAGE_STORE(c)                                                                      \
+    do {                                                                                       \
+        kt_stage_chunk<MODE>(src, sc0, sq0, lane, (c).span, qbuf, mbuf, p0buf, p1buf, 0u);     \
+        kt_stage_chunk<MODE>(src, sc1, sq1, 64u + lane, (c).span, qbuf, mbuf, p0buf, p1buf, 1u); \
+        wave_sync();                                                                           \
+    } while (0)
+
+    // prologue: cursor of pass 0, offsets of pass 1 in flight, bases of pass 0 in LDS
+    uint64_t r = PAIRED ? 2 * u0 : u0, o = 0;
+    uint64_t ob, oe;
+    KtCursor cur;
+    for (;;) {
+        kt_load_offsets(src, r, r_end, lane, ob, oe);
+        cur = kt_cursor(r, o, r_end, ob, oe, lane, k);
+        if (cur.any || r >= r_end) break;
+        kt_advance(cur, r_end, r, o);
+    }
+    uint64_t rn = r_end, on = 0, nb = 0, ne = 0;
+    if (cur.any) {  // (a wave without windows still reaches the block's final __syncthreads)
+        kt_advance(cur, r_end, rn, on);
+        kt_load_offsets(src, rn, r_end, lane, nb, ne);
+        KT_STAGE_LOAD(cur, cur.s0);
+        KT_STAGE_STORE(cur);
+    }
+
+    while (cur.any) {
+        // ---- keys of pass i; the first bucket of every lookup in flight (every lane loads: see kt_load_offsets)
+        bool valid = false;
+        uint64_t key = 0;
+        if (cur.has) {
+            const uint32_t w0 = cur.off >> 6, w1 = (cur.off + k - 1u) >> 6;
+            uint64_t badbits = 0;
+            for (uint32_t wi = w0; wi <= w1; ++wi) {
+                uint64_t sel = ~0ull;
+                if (wi == w0) sel &= ~0ull << (cur.off & 63u);
+                if (wi == w1) sel &= ~0ull >> (63u - ((cur.off + k - 1u) & 63u));
+                badbits |= mbuf[wi] & sel;
+            }
+            valid = badbits == 0;
+            if (valid) key = plane_bits(p0buf, cur.off, k) | (plane_bits(p1buf, cur.off, k) << 32);
+        }
+        uint32_t bk = valid ? (kt_hash(key) & (uint32_t)I.kt_bmask) : 0u;
+
+        // ---- cursor of pass i + 1 (its offsets were loaded one pass ago)
+        KtCursor nxt = kt_cursor(rn, on, r_end, nb, ne, lane, k);
+        const bool skipped = !nxt.any && rn < r_end;  // 64 units without a window (rare): handled below
+        kt_advance(nxt, r_end, rn, on);
+
+        // ---- in flight together: the table buckets of pass i, the offsets of pass i + 2, the bases of pass i + 1
+        u32x4 sl[4];
+        {
+            const u32x4* pb = reinterpret_cast<const u32x4*>(I.ktab) + (uint64_t)bk * 4u;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) sl[j] = pb[j];
+        }
+        kt_load_offsets(src, rn, r_end, lane, nb, ne);
+        KT_STAGE_LOAD(nxt, cur.s0);
+
+        // ---- resolve the lookups of pass i (rarely a further bucket)
+        int which = -1;
+        uint32_t ilo = 0, ihi = 0;
+        bool pend = valid;
+        while (pend) {
+            const uint32_t kl = (uint32_t)key, kh = (uint32_t)(key >> 32);
+            bool empty = false, found = false;
+            uint32_t lo = 0, info = 0;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const bool hit = sl[j][0] == kl && sl[j][1] == kh;
+                lo = hit ? sl[j][2] : lo;
+                info = hit ? sl[j][3] : info;
+                found |= hit;
+                empty |= sl[j][0] == 0xFFFFFFFFu && sl[j][1] == 0xFFFFFFFFu;
+            }
+            if (found) {
+                const bool multi = (info >> 31) != 0u;
+                which = multi ? -2 : (int)info;
+                ilo = lo;
+                ihi = multi ? lo + (info & 0x7FFFFFFFu) : lo + 1u;
+            }
+            pend = !(found || empty);
+            if (pend) {
+                bk = (bk + 1u) & (uint32_t)I.kt_bmask;
+                const u32x4* pb = reinterpret_cast<const u32x4*>(I.ktab) + (uint64_t)bk * 4u;
+#pragma unroll
+                for (int j = 0; j < 4; ++j) sl[j] = pb[j];
+            }
+        }
+
+        // ---- tallies of pass i (k_scan step 5)
+        if (valid) {
+            ++t_cnt;
+            if (EM && which == -2) {
+                atomicAdd(&src.em_mult[ilo], 1u);
+                src.em_hi[ilo] = ihi;
+            }
+            if (which >= 0) {
+                double wgt = 0.0;
+                if (MODE == KM_LOCAL) {
+                    const unsigned char* qw = qbuf + cur.off;
+                    double x = 1.0;
+                    for (uint32_t i = 0; i < k; ++i) {
+                        const double2 t = qtab[qw[i]];
+                        x = div_rn(x, t.x, t.y);  // == x / t.x (fm_scanner.cpp:454)
+                    }
+                    wgt = x;
+                }
+                if (LDS_HIST) {
+                    atomicAdd(&hA[which], 1ull);
+                    if (MODE == KM_LOCAL) atomicAdd(&hW[which], wgt);
+                } else {
+                    atomicAdd(&gU[which], 1ull);
+                    if (MODE == KM_LOCAL) atomicAdd(&out_w[which], wgt);
+                }
+            }
+        }
+        // ---- ambiguity of pass i (k_scan step 6, one sub-pass)
+        {
+            const uint64_t hm = __ballot(cur.has != 0u);
+            const uint32_t last = (uint32_t)__popcll(hm) - 1u;
+            const uint64_t unit = PAIRED ? ((cur.r + cur.ri) >> 1) : (cur.r + cur.ri);
+            int vmin = (valid && which >= 0) ? which : INT_MAX;
+            int vmax = (valid && which >= 0) ? which : -1;
+            const uint64_t unit0 = rl64(unit, 0);
+            if (cunit != ~0ull && unit0 != cunit) {
+                amb += (cmax >= 0 && cmin != cmax) ? 1u : 0u;
+                cunit = ~0ull;
+            }
+            if (lane == 0 && unit == cunit) {
+                vmin = min(vmin, cmin);
+                vmax = max(vmax, cmax);
+            }
+            const uint64_t uprev = __shfl_up(unit, 1);
+            const bool head = cur.has != 0u && (lane == 0 || unit != uprev);
+            const uint64_t heads = __ballot(head);
+            const uint64_t below = heads & ((lane == 63u) ? ~0ull : ((2ull << lane) - 1ull));
+            const uint32_t seg_start = 63u - (uint32_t)__clzll(below);
+            for (uint32_t d = 1; d < 64u; d <<= 1) {
+                const int om = __shfl_up(vmin, d), oM = __shfl_up(vmax, d);
+                if (lane >= d && lane - d >= seg_start) {
+                    vmin = min(vmin, om);
+                    vmax = max(vmax, oM);
+                }
+            }
+            const bool tail = cur.has != 0u && (lane == last || ((heads >> (lane + 1u)) & 1ull));
+            const bool amb_lane = tail && lane != last && vmax >= 0 && vmin != vmax;
+            amb += (uint32_t)__popcll(__ballot(amb_lane));
+            cmin = rli(vmin, last);
+            cmax = rli(vmax, last);
+            cunit = rl64(unit, last);
+        }
+        if (skipped) {  // walk past units without windows (serial loads; rare: 64 units shorter than k)
+            for (;;) {
+                nxt = kt_cursor(rn, on, r_end, nb, ne, lane, k);
+                if (nxt.any || rn >= r_end) break;
+                kt_advance(nxt, r_end, rn, on);
+                kt_load_offsets(src, rn, r_end, lane, nb, ne);
+            }
+            if (nxt.any) {
+                kt_advance(nxt, r_end, rn, on);
+                kt_load_offsets(src, rn, r_end, lane, nb, ne);
+                KT_STAGE_LOAD(nxt, cur.s0);
+            }
+        }
+        wave_sync();  // every lane is done with pass i's LDS words
+        // ---- bases of pass i + 1 into LDS
+        if (nxt.any) KT_STAGE_STORE(nxt);
+        cur = nxt;
+    }
+#undef KT_STAGE_LOAD
+#undef KT_STAGE_STORE
+
+    if (cunit != ~0ull) amb += (cmax >= 0 && cmin != cmax) ? 1u : 0u;
+    const unsigned long long tsum = wave_sum<unsigned long long>((unsigned long long)t_cnt);
+    if (lane == 0) {
+        if (tsum) atomicAdd(&out_a[0], tsum);
+        if (amb) atomicAdd(&out_a[1], (unsigned long long)amb);
+    }
+    if (LDS_HIST) {
+        __syncthreads();
+        for (uint32_t g = threadIdx.x; g < G; g += BLOCK_THREADS) {
+            const unsigned long long a = hA[g];
+            if (a) atomicAdd(&gU[g], a);
+            if (MODE == KM_LOCAL) {
+                const double x = hW[g];
+                if (x != 0.0) atomicAdd(&out_w[g], x);
+            }
+        }
+    }
+}
+
+
 // ---- k-mer interval table construction (per k, once per replica) ----
 // Pass 1: every N-free window of every text inserts its packed k-mer into a set (8-B slots, linear probing, CAS);
 // each thread rolls the code over a run of consecutive windows. n_distinct counts the keys inserted.
@@ -994,6 +1344,7 @@ struct speq_device_index {
     bool kmer_table = true;       // tuning "kmer_table": scans of k <= 31 look windows up in a per-k k-mer table
     uint32_t ilp_kt = 1;          // tuning "ilp_kt": windows per lane of k-mer-table scans (1, 2 or 4)
     uint32_t blocks_per_cu_kt = 0;  // tuning "blocks_per_cu_kt": blocks_per_cu of k-mer-table scans (default: no cap)
+    bool kt_pipeline = true;        // tuning "kt_pipeline": k_scan_kt (software-pipelined) for ilp_kt == 1 read scans
     uint32_t kt_slots = 4;        // tuning "kt_slots": table slots per distinct k-mer (load factor 1/kt_slots .. 2/kt_slots)
     struct KmerTable {
         uint4* table = nullptr;
@@ -1040,6 +1391,12 @@ template <int MODE, bool PAIRED, bool LDS>
 void allow_big_lds() {
     allow_big_lds_kt<MODE, PAIRED, LDS, false>();
     allow_big_lds_kt<MODE, PAIRED, LDS, true>();
+    if constexpr (MODE != KM_REF) {
+        HIP_OK(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_scan_kt<MODE, PAIRED, LDS, false>),
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+        HIP_OK(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_scan_kt<MODE, PAIRED, LDS, true>),
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    }
 }
 
 void allow_big_lds_all() {
@@ -1182,6 +1539,17 @@ template <int MODE, bool PAIRED, bool LDS, bool KT>
 void launch_v(const speq_device_index* d, const DevView& v, const UnitSrc& src, uint32_t grid, size_t lds,
               hipStream_t st, unsigned long long* a, unsigned long long* b, double* w) {
     const uint32_t ilp = KT ? d->ilp_kt : (MODE == KM_LOCAL ? d->ilp_local : d->ilp);
+    if constexpr (KT && MODE != KM_REF) {
+        if (ilp == 1 && d->kt_pipeline) {  // software-pipelined table scan
+            if (src.em_mult != nullptr)
+                hipLaunchKernelGGL((k_scan_kt<MODE, PAIRED, LDS, true>), dim3(grid), dim3(BLOCK_THREADS), lds, st, v,
+                                   src, a, w);
+            else
+                hipLaunchKernelGGL((k_scan_kt<MODE, PAIRED, LDS, false>), dim3(grid), dim3(BLOCK_THREADS), lds, st, v,
+                                   src, a, w);
+            return;
+        }
+    }
     if (MODE != KM_REF && src.em_mult != nullptr)
         hipLaunchKernelGGL((k_scan<MODE, PAIRED, LDS, 1, MODE != KM_REF, KT>), dim3(grid), dim3(BLOCK_THREADS), lds,
                            st, v, src, a, b, w);
@@ -1692,6 +2060,9 @@ int speq_device_set_tuning(speq_device_index* d, const char* key, int64_t value)
         } else if (k == "blocks_per_cu_kt") {
             if (value < 0 || value > 8) throw std::invalid_argument("blocks_per_cu_kt must be in [0, 8]");
             d->blocks_per_cu_kt = (uint32_t)value;
+        } else if (k == "kt_pipeline") {
+            if (value != 0 && value != 1) throw std::invalid_argument("kt_pipeline must be 0 or 1");
+            d->kt_pipeline = value != 0;
         } else if (k == "ilp_kt") {
             if (value != 1 && value != 2 && value != 4) throw std::invalid_argument("ilp_kt must be 1, 2 or 4");
             d->ilp_kt = (uint32_t)value;
@@ -1728,6 +2099,7 @@ int speq_device_get_tuning(const speq_device_index* d, const char* key, int64_t*
         else if (k == "stream_lanes") *value = d->stream_lanes;
         else if (k == "kmer_table") *value = d->kmer_table ? 1 : 0;
         else if (k == "ilp_kt") *value = d->ilp_kt;
+        else if (k == "kt_pipeline") *value = d->kt_pipeline ? 1 : 0;
         else if (k == "blocks_per_cu_kt") *value = d->blocks_per_cu_kt;
         else if (k == "kt_slots") *value = d->kt_slots;
         else throw std::invalid_argument("speq_device_get_tuning: unknown key " + k);
