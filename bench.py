@@ -100,6 +100,7 @@ def main():
     reads = synth.make_reads(ref, n_reads, start_index=rank * n_reads, paired=paired)
     lens = np.diff(reads.offsets).astype(np.int64)
     kmers_per_step = int(np.maximum(lens - k + 1, 0).sum())
+    read_bytes = int(reads.offsets[-1])  # bases per step (qualities: as many again)
     d_seq = torch.from_numpy(reads.seq).to(dev_t)
     d_qual = torch.from_numpy(reads.qual).to(dev_t)
     d_off = torch.from_numpy(reads.offsets.astype(np.int64)).to(dev_t)
@@ -144,6 +145,12 @@ def main():
 
     elapsed, kernel_ms, launches = timed_run(a.steps, a.warmup)
     counts = d_counts.cpu().numpy()
+    if ktab["table_bytes"] and dev.tuning("ilp_kt") == 1 and dev.tuning("kt_pipeline") == 1:
+        kernel_name = "k_scan_kt (software-pipelined k-mer-table scan, speq_amd/csrc/scan_kernels.hip)"
+    elif ktab["table_bytes"]:
+        kernel_name = "k_scan<..., KT = true> (k-mer-table scan, speq_amd/csrc/scan_kernels.hip)"
+    else:
+        kernel_name = "k_scan<..., KT = false> (LF-step scan, speq_amd/csrc/scan_kernels.hip)"
 
     # the LF-step kernel on the same reads (the k-mer table replaces its chain of LF steps; results are identical)
     lf = None
@@ -236,10 +243,17 @@ def main():
                 # draws from Infinity Cache + HBM (an upper bound on HBM bytes), against the same 8 TB/s peak
                 "traffic_GBps": (traffic / avg_kernel_s / 1e9) if traffic else None,
                 "traffic_frac": (traffic / avg_kernel_s / 1e9 / HBM_PEAK_GBS) if traffic else None,
-                "kernel": "k_scan (speq_amd/csrc/scan_kernels.hip)",
+                "kernel": kernel_name,
                 "algorithmic_bytes_per_kmer": 2 * k * OCC_ENTRY_BYTES,
                 "avg_kernel_ms": avg_kernel_s * 1e3, "launches_timed": launches,
                 "traffic_source": traffic_src,
+                # the table kernel's own bytes: one 64-B bucket per window plus the read bytes (bases + qualities)
+                "table_kernel_model": ({"bytes_per_kmer": round(64 + 2 * read_bytes / max(1, kmers_per_step), 3),
+                                        "achieved_GBps": kmers_per_step * (64 + 2 * read_bytes / max(1, kmers_per_step))
+                                        / avg_kernel_s / 1e9,
+                                        "frac": kmers_per_step * (64 + 2 * read_bytes / max(1, kmers_per_step))
+                                        / avg_kernel_s / 1e9 / HBM_PEAK_GBS}
+                                       if ktab["table_bytes"] else None),
                 "note": "achieved uses SURVEY.md 8(d)'s algorithmic 2*k*64 B per k-mer (k LF steps x 2 uncached "
                         "64-B occ loads), fixed whatever the kernel does; the k-mer-table kernel reads one 64-B bucket "
                         "per window instead (the LF-step kernel ~0.3 of the algorithmic gathers), mostly from "

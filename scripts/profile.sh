@@ -7,7 +7,7 @@ cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
 OUT=gpurun_out/prof
 mkdir -p $OUT
-BENCH="bench.py --steps 5 --warmup 1 --no-cpu-baseline --no-pcie $*"
+BENCH="bench.py --steps 5 --warmup 1 --no-cpu-baseline --no-pcie --no-lf-compare $*"
 run() {  # name, rocprof args...
     local name=$1; shift
     echo "== $name" >&2
@@ -17,5 +17,6 @@ run trace --kernel-trace --stats && \
 run fetch --pmc FETCH_SIZE && \
 run write --pmc WRITE_SIZE && \
 run tcc --pmc TCC_HIT_sum TCC_MISS_sum TCC_EA0_RDREQ_sum && \
-run sq --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_INSTS_LDS SQ_WAIT_INST_ANY SQ_WAVE_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE
+run sq --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_INSTS_LDS SQ_WAIT_INST_ANY SQ_WAVE_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE && \
+run sq2 --pmc SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_SALU GRBM_GUI_ACTIVE
 echo "profile rc=$?" >&2

@@ -26,15 +26,15 @@ def main():
         shutil.copy(st, os.path.join(dst, f"kernel_stats_{tag}.csv"))
         rows = list(csv.DictReader(open(st)))
         out["kernel_stats"] = [{k: r[k] for k in ("Name", "Calls", "AverageNs", "MinNs", "MaxNs", "Percentage")}
-                               for r in rows if "::k_scan<" in r["Name"]]
+                               for r in rows if "::k_scan<" in r["Name"] or "::k_scan_kt<" in r["Name"]]
     pmc = collections.defaultdict(list)
     meta = {}
-    for p in ("fetch", "write", "tcc", "sq"):
+    for p in ("fetch", "write", "tcc", "sq", "sq2"):
         f = os.path.join(src, p, f"{p}_counter_collection.csv")
         if not os.path.exists(f):
             continue
         for r in csv.DictReader(open(f)):
-            if "::k_scan<" not in r["Kernel_Name"]:  # not rocPRIM's "lookback_scan" kernels of the GPU build
+            if "::k_scan<" not in r["Kernel_Name"] and "::k_scan_kt<" not in r["Kernel_Name"]:  # not rocPRIM's scans
                 continue
             pmc[r["Counter_Name"]].append(float(r["Counter_Value"]))
             meta = {k: r[k] for k in ("Grid_Size", "Workgroup_Size", "LDS_Block_Size", "VGPR_Count", "SGPR_Count",
