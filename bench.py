@@ -145,7 +145,7 @@ def main():
 
     elapsed, kernel_ms, launches = timed_run(a.steps, a.warmup)
     counts = d_counts.cpu().numpy()
-    if ktab["table_bytes"] and dev.tuning("ilp_kt") == 1 and dev.tuning("kt_pipeline") == 1:
+    if ktab["table_bytes"] and dev.tuning("ilp_kt") <= 2 and dev.tuning("kt_pipeline") == 1:
         kernel_name = "k_scan_kt (software-pipelined k-mer-table scan, speq_amd/csrc/scan_kernels.hip)"
     elif ktab["table_bytes"]:
         kernel_name = "k_scan<..., KT = true> (k-mer-table scan, speq_amd/csrc/scan_kernels.hip)"

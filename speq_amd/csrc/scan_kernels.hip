@@ -843,11 +843,12 @@ __global__ __launch_bounds__(BLOCK_THREADS, (KT && NWIN == 1 && MODE == KM_GLOBA
     }
 }
 
-// ---- software-pipelined k-mer-table read scan (one window per lane) ----
-// k_scan runs each pass of 64 windows as three dependent global round trips (read offsets -> bases -> table), so a
+// ---- software-pipelined k-mer-table read scan ----
+// k_scan runs each pass of windows as three dependent global round trips (read offsets -> bases -> table), so a
 // wave spends most of a pass waiting. k_scan_kt overlaps them across passes: while the table lookups of pass i are
 // in flight, the offsets of pass i + 2 and the bases of pass i + 1 are already loading. Same results as k_scan
-// (KM_GLOBAL / KM_LOCAL reads, paired or not, EM or not); the pass logic is k_scan's with NWIN = 1.
+// (KM_GLOBAL / KM_LOCAL reads, paired or not, EM or not); the pass logic is k_scan's, with NW windows per lane.
+
 // Wave-uniform lane reads (v_readlane: the result lives in a scalar register, unlike __shfl's ds_bpermute).
 __device__ __forceinline__ uint32_t rl32(uint32_t v, uint32_t l) { return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)l); }
 __device__ __forceinline__ int rli(int v, uint32_t l) { return __builtin_amdgcn_readlane(v, (int)l); }
@@ -855,13 +856,15 @@ __device__ __forceinline__ uint64_t rl64(uint64_t v, uint32_t l) {
     return (uint64_t)rl32((uint32_t)v, l) | ((uint64_t)rl32((uint32_t)(v >> 32), l) << 32);
 }
 
+template <int NW>
 struct KtCursor {
     uint64_t r, o;             // first unit of the pass and the window offset in it
     uint64_t s0;               // first base of the pass
-    uint32_t ri, oo, off;      // this lane's slot: read r + ri, window oo of it, first base s0 + off
+    uint32_t ri[NW], oo[NW], off[NW];  // slot lane + 64 w: read r + ri, window oo of it, first base s0 + off
+    uint32_t has[NW];          // the slot holds a window (0/1)
     uint32_t span, ri_last, oo_last;
-    uint32_t has;              // this lane holds a window (0/1)
     uint32_t any;              // the pass holds a window (0/1; wave-uniform)
+    uint64_t units;            // bit i: unit r + i has windows in the pass (wave-uniform)
 };
 
 // Offsets of reads r + lane and r + lane + 1 (issued here, consumed by kt_cursor). Every lane loads (indices are
@@ -874,11 +877,17 @@ __device__ __forceinline__ void kt_load_offsets(const UnitSrc& src, uint64_t r, 
     e = src.off[i + 1 <= r_end ? i + 1 : r_end];
 }
 
-constexpr uint32_t KT_SPAN = 128;  // bases a pass of k_scan_kt stages: two chunks of 64 (windows past it wait)
+// bases a pass of k_scan_kt stages: NW + 1 chunks of 64 (windows past it wait for the next pass)
+template <int NW>
+__host__ __device__ constexpr uint32_t kt_span() { return 64u * (NW + 1); }
 
-__device__ __forceinline__ KtCursor kt_cursor(uint64_t r, uint64_t o, uint64_t r_end,
-                                              uint64_t bl_, uint64_t el_, uint32_t lane, uint32_t k) {
-    KtCursor c;
+// The slots of a pass: units r, r+1, ... (lane i holds the window count of unit r + i) are walked in a wave-uniform
+// loop over the units that have windows in the pass (one or two for 150-bp reads), each assigning its window range
+// to the slots it covers: no prefix sum or per-slot binary search (those cost ~15 ds_bpermute per pass in k_scan).
+template <int NW>
+__device__ __forceinline__ KtCursor<NW> kt_cursor(uint64_t r, uint64_t o, uint64_t r_end, uint64_t bl_,
+                                                  uint64_t el_, uint32_t lane, uint32_t k) {
+    KtCursor<NW> c;
     c.r = r;
     c.o = o;
     uint32_t wl = 0;
@@ -886,37 +895,67 @@ __device__ __forceinline__ KtCursor kt_cursor(uint64_t r, uint64_t o, uint64_t r
         const uint64_t L = el_ - bl_;
         uint64_t W = L >= k ? L - k + 1 : 0;
         if (lane == 0) W = W > o ? W - o : 0;
-        wl = (uint32_t)(W < 65u ? W : 65u);
+        wl = (uint32_t)(W < 64u * NW + 1u ? W : 64u * NW + 1u);
     }
-    uint32_t incl = wl;
-    for (uint32_t d = 1; d < 64u; d <<= 1) {
-        const uint32_t y = __shfl_up(incl, d);
-        if (lane >= d) incl += y;
+    uint64_t pos[NW];
+#pragma unroll
+    for (int w = 0; w < NW; ++w) {
+        c.ri[w] = c.oo[w] = 0;
+        pos[w] = 0;
     }
-    const uint32_t total = rl32(incl, 63);
+    uint64_t nz = __ballot(wl != 0u);  // units with windows
+    uint32_t start = 0;
+    c.units = 0;
+    while (nz != 0 && start < 64u * NW) {
+        const uint32_t i = (uint32_t)__builtin_ctzll(nz);
+        nz &= nz - 1;
+        const uint32_t wi = rl32(wl, i);
+        const uint64_t base = rl64(bl_, i) + (i == 0 ? o : 0);
+        c.units |= 1ull << i;
+#pragma unroll
+        for (int w = 0; w < NW; ++w) {
+            const uint32_t slot = lane + 64u * (uint32_t)w;
+            const bool in = slot >= start && slot - start < wi;
+            c.ri[w] = in ? i : c.ri[w];
+            c.oo[w] = in ? slot - start : c.oo[w];
+            pos[w] = in ? base + (slot - start) : pos[w];
+        }
+        start += wi;
+    }
+    const uint32_t total = start;
     c.any = total > 0 ? 1u : 0u;
-    uint32_t i_lo = 0;
-    for (uint32_t step = 32; step >= 1; step >>= 1) {
-        const uint32_t v = __shfl(incl, (int)(i_lo + step - 1u));
-        if (v <= lane) i_lo += step;
+    const uint64_t s0 = rl64(pos[0], 0);
+    c.s0 = s0;
+    uint32_t n_all = 0, last_w = 0, last_lane = 0;
+#pragma unroll
+    for (int w = 0; w < NW; ++w) {
+        const uint32_t slot = lane + 64u * (uint32_t)w;
+        c.off[w] = (uint32_t)(pos[w] - s0);
+        // valid slots are a prefix in slot order; the first window (pos == s0) always fits: k <= 31 < kt_span
+        c.has[w] = (slot < total && pos[w] + k - s0 <= kt_span<NW>()) ? 1u : 0u;
+        const uint32_t n = (uint32_t)__popcll(__ballot(c.has[w] != 0u));
+        if (n > 0) {
+            last_w = (uint32_t)w;
+            last_lane = n - 1u;
+        }
+        n_all += n;
     }
-    c.ri = i_lo > 63u ? 63u : i_lo;
-    const uint32_t excl_i = __shfl(incl, (int)c.ri) - __shfl(wl, (int)c.ri);
-    c.oo = lane - excl_i;
-    const uint64_t pos = __shfl(bl_, (int)c.ri) + c.oo + (c.ri == 0 ? o : 0);
-    c.s0 = rl64(pos, 0);
-    c.off = (uint32_t)(pos - c.s0);
-    c.has = (lane < total && pos + k - c.s0 <= KT_SPAN) ? 1u : 0u;  // the first window (pos == s0) fits: k <= 31
-    const uint32_t n = (uint32_t)__popcll(__ballot(c.has != 0u));
-    const uint32_t off_last = n ? rl32(c.off, n - 1u) : 0u;
-    c.ri_last = n ? rl32(c.ri, n - 1u) : 0u;
-    c.oo_last = n ? rl32(c.oo, n - 1u) : 0u;
+    uint32_t off_last = 0;
+    c.ri_last = c.oo_last = 0;
+#pragma unroll
+    for (int w = 0; w < NW; ++w)
+        if (n_all > 0 && last_w == (uint32_t)w) {
+            off_last = rl32(c.off[w], last_lane);
+            c.ri_last = rl32(c.ri[w], last_lane);
+            c.oo_last = rl32(c.oo[w], last_lane);
+        }
     c.span = off_last + k;
     return c;
 }
 
 // Where the pass after `c` starts (k_scan's cursor advance); a pass without windows skips 64 units.
-__device__ __forceinline__ void kt_advance(const KtCursor& c, uint64_t r_end, uint64_t& r, uint64_t& o) {
+template <int NW>
+__device__ __forceinline__ void kt_advance(const KtCursor<NW>& c, uint64_t r_end, uint64_t& r, uint64_t& o) {
     if (!c.any) {
         r = (c.r + 64 < r_end) ? c.r + 64 : r_end;
         o = 0;
@@ -948,10 +987,32 @@ __device__ __forceinline__ void kt_stage_chunk(const UnitSrc& src, uint32_t ch, 
     }
 }
 
+// Staging registers of one pass: NW + 1 chunks of 64 bases; every lane loads (addresses clamped into the pass, or
+// to `fallback`, a base of the current pass, when the pass is empty).
+template <int NW>
+struct KtStage {
+    uint32_t c[NW + 1], q[NW + 1];
+};
+template <int NW>
+__device__ __forceinline__ void kt_stage_load(const UnitSrc& src, const KtCursor<NW>& cu, uint64_t fallback,
+                                              uint32_t lane, KtStage<NW>& st) {
+    const uint64_t b = cu.any ? cu.s0 : fallback;
+    const uint32_t l = cu.any ? cu.span - 1u : 0u;
+#pragma unroll
+    for (int j = 0; j <= NW; ++j) {
+        const uint32_t p = min(64u * (uint32_t)j + lane, l);
+        st.c[j] = ld_stream(src.seq + b + p);
+        st.q[j] = ld_stream(src.qual + b + p);
+    }
+}
+
 #ifndef SPEQ_KTP_MIN_WAVES
 #define SPEQ_KTP_MIN_WAVES 1
 #endif
-template <int MODE, bool PAIRED, bool LDS_HIST, bool EM>
+#ifndef SPEQ_PROBE_NOLOOKUP
+#define SPEQ_PROBE_NOLOOKUP 0
+#endif
+template <int MODE, bool PAIRED, bool LDS_HIST, bool EM, int NW>
 __global__ __launch_bounds__(BLOCK_THREADS, SPEQ_KTP_MIN_WAVES)
 void k_scan_kt(DevView I, UnitSrc src, unsigned long long* __restrict__ out_a, double* __restrict__ out_w) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -980,41 +1041,31 @@ void k_scan_kt(DevView I, UnitSrc src, unsigned long long* __restrict__ out_a, d
     if (LDS_HIST || MODE == KM_LOCAL) __syncthreads();
     unsigned long long* gU = out_a + 2;
 
-    const uint64_t NW = (uint64_t)gridDim.x * WAVES_PER_BLOCK;
+    const uint64_t NWV = (uint64_t)gridDim.x * WAVES_PER_BLOCK;
     const uint64_t gw = (uint64_t)blockIdx.x * WAVES_PER_BLOCK + wid;
     const uint64_t nu = PAIRED ? src.n_units / 2 : src.n_units;
-    const uint64_t u0 = nu * gw / NW, u1 = nu * (gw + 1) / NW;
+    const uint64_t u0 = nu * gw / NWV, u1 = nu * (gw + 1) / NWV;
     const uint64_t r_end = PAIRED ? 2 * u1 : u1;
 
     uint32_t t_cnt = 0, amb = 0;
-    int cmin = INT_MAX, cmax = -1;
+    int cmin = -1, cmax = 0;  // carried unit: its first counted group (-1: none yet), ambiguous so far (0/1)
     uint64_t cunit = ~0ull;
-
-    // staging registers of one pass: 2 chunks of 64 bases (span <= KT_SPAN)
-    uint32_t sc0 = 0, sc1 = 0, sq0 = 0, sq1 = 0;
-#define KT_STAGE_LOAD(c, fallback)                                                             \
-    do {                                                                                       \
-        const uint64_t b_ = (c).any ? (c).s0 : (fallback);                                     \
-        const uint32_t l_ = (c).any ? (c).span - 1u : 0u;                                      \
-        sc0 = ld_stream(src.seq + b_ + min(lane, l_));                                         \
-        sq0 = ld_stream(src.qual + b_ + min(lane, l_));                                        \
-        sc1 = ld_stream(src.seq + b_ + min(64u + lane, l_));                                   \
-        sq1 = ld_stream(src.qual + b_ + min(64u + lane, l_));                                  \
-    } while (0)
-#define KT_STAGE_STORE(c)                                                                      \
-    do {                                                                                       \
-        kt_stage_chunk<MODE>(src, sc0, sq0, lane, (c).span, qbuf, mbuf, p0buf, p1buf, 0u);     \
-        kt_stage_chunk<MODE>(src, sc1, sq1, 64u + lane, (c).span, qbuf, mbuf, p0buf, p1buf, 1u); \
-        wave_sync();                                                                           \
-    } while (0)
+    KtStage<NW> stg;
+    auto stage_store = [&](const KtCursor<NW>& cu) {
+#pragma unroll
+        for (int j = 0; j <= NW; ++j)
+            kt_stage_chunk<MODE>(src, stg.c[j], stg.q[j], 64u * (uint32_t)j + lane, cu.span, qbuf, mbuf, p0buf,
+                                 p1buf, (uint32_t)j);
+        wave_sync();
+    };
 
     // prologue: cursor of pass 0, offsets of pass 1 in flight, bases of pass 0 in LDS
     uint64_t r = PAIRED ? 2 * u0 : u0, o = 0;
     uint64_t ob, oe;
-    KtCursor cur;
+    KtCursor<NW> cur;
     for (;;) {
         kt_load_offsets(src, r, r_end, lane, ob, oe);
-        cur = kt_cursor(r, o, r_end, ob, oe, lane, k);
+        cur = kt_cursor<NW>(r, o, r_end, ob, oe, lane, k);
         if (cur.any || r >= r_end) break;
         kt_advance(cur, r_end, r, o);
     }
@@ -1022,85 +1073,114 @@ void k_scan_kt(DevView I, UnitSrc src, unsigned long long* __restrict__ out_a, d
     if (cur.any) {  // (a wave without windows still reaches the block's final __syncthreads)
         kt_advance(cur, r_end, rn, on);
         kt_load_offsets(src, rn, r_end, lane, nb, ne);
-        KT_STAGE_LOAD(cur, cur.s0);
-        KT_STAGE_STORE(cur);
+        kt_stage_load(src, cur, cur.s0, lane, stg);
+        stage_store(cur);
     }
 
     while (cur.any) {
-        // ---- keys of pass i; the first bucket of every lookup in flight (every lane loads: see kt_load_offsets)
-        bool valid = false;
-        uint64_t key = 0;
-        if (cur.has) {
-            const uint32_t w0 = cur.off >> 6, w1 = (cur.off + k - 1u) >> 6;
-            uint64_t badbits = 0;
-            for (uint32_t wi = w0; wi <= w1; ++wi) {
-                uint64_t sel = ~0ull;
-                if (wi == w0) sel &= ~0ull << (cur.off & 63u);
-                if (wi == w1) sel &= ~0ull >> (63u - ((cur.off + k - 1u) & 63u));
-                badbits |= mbuf[wi] & sel;
+        // ---- keys of pass i
+        bool valid[NW];
+        uint64_t key[NW];
+        uint32_t bk[NW];
+#pragma unroll
+        for (int w = 0; w < NW; ++w) {
+            valid[w] = false;
+            key[w] = 0;
+            if (cur.has[w]) {
+                const uint32_t off = cur.off[w];
+                const uint32_t w0 = off >> 6, w1 = (off + k - 1u) >> 6;
+                uint64_t badbits = 0;
+                for (uint32_t wi = w0; wi <= w1; ++wi) {
+                    uint64_t sel = ~0ull;
+                    if (wi == w0) sel &= ~0ull << (off & 63u);
+                    if (wi == w1) sel &= ~0ull >> (63u - ((off + k - 1u) & 63u));
+                    badbits |= mbuf[wi] & sel;
+                }
+                valid[w] = badbits == 0;
+                if (valid[w]) key[w] = plane_bits(p0buf, off, k) | (plane_bits(p1buf, off, k) << 32);
             }
-            valid = badbits == 0;
-            if (valid) key = plane_bits(p0buf, cur.off, k) | (plane_bits(p1buf, cur.off, k) << 32);
+            bk[w] = valid[w] ? (kt_hash(key[w]) & (uint32_t)I.kt_bmask) : 0u;
         }
-        uint32_t bk = valid ? (kt_hash(key) & (uint32_t)I.kt_bmask) : 0u;
 
         // ---- cursor of pass i + 1 (its offsets were loaded one pass ago)
-        KtCursor nxt = kt_cursor(rn, on, r_end, nb, ne, lane, k);
+        KtCursor<NW> nxt = kt_cursor<NW>(rn, on, r_end, nb, ne, lane, k);
         const bool skipped = !nxt.any && rn < r_end;  // 64 units without a window (rare): handled below
         kt_advance(nxt, r_end, rn, on);
 
         // ---- in flight together: the table buckets of pass i, the offsets of pass i + 2, the bases of pass i + 1
-        u32x4 sl[4];
-        {
-            const u32x4* pb = reinterpret_cast<const u32x4*>(I.ktab) + (uint64_t)bk * 4u;
+        u32x4 sl[NW][4];
 #pragma unroll
-            for (int j = 0; j < 4; ++j) sl[j] = pb[j];
+        for (int w = 0; w < NW; ++w) {
+#if SPEQ_PROBE_NOLOOKUP  // timing probe only (wrong results): every lookup finds an empty bucket
+            for (int j = 0; j < 4; ++j) sl[w][j] = u32x4{0xFFFFFFFFu, 0xFFFFFFFFu, bk[w], 0u};
+#else
+            const u32x4* pb = reinterpret_cast<const u32x4*>(I.ktab) + (uint64_t)bk[w] * 4u;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) sl[w][j] = pb[j];
+#endif
         }
         kt_load_offsets(src, rn, r_end, lane, nb, ne);
-        KT_STAGE_LOAD(nxt, cur.s0);
+        kt_stage_load(src, nxt, cur.s0, lane, stg);
 
         // ---- resolve the lookups of pass i (rarely a further bucket)
-        int which = -1;
-        uint32_t ilo = 0, ihi = 0;
-        bool pend = valid;
-        while (pend) {
-            const uint32_t kl = (uint32_t)key, kh = (uint32_t)(key >> 32);
-            bool empty = false, found = false;
-            uint32_t lo = 0, info = 0;
+        int which[NW];
+        uint32_t ilo[NW], ihi[NW];
+        bool pend[NW];
 #pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                const bool hit = sl[j][0] == kl && sl[j][1] == kh;
-                lo = hit ? sl[j][2] : lo;
-                info = hit ? sl[j][3] : info;
-                found |= hit;
-                empty |= sl[j][0] == 0xFFFFFFFFu && sl[j][1] == 0xFFFFFFFFu;
-            }
-            if (found) {
-                const bool multi = (info >> 31) != 0u;
-                which = multi ? -2 : (int)info;
-                ilo = lo;
-                ihi = multi ? lo + (info & 0x7FFFFFFFu) : lo + 1u;
-            }
-            pend = !(found || empty);
-            if (pend) {
-                bk = (bk + 1u) & (uint32_t)I.kt_bmask;
-                const u32x4* pb = reinterpret_cast<const u32x4*>(I.ktab) + (uint64_t)bk * 4u;
+        for (int w = 0; w < NW; ++w) {
+            which[w] = -1;
+            ilo[w] = ihi[w] = 0;
+            pend[w] = valid[w];
+        }
+        for (;;) {
+            bool more = false;
 #pragma unroll
-                for (int j = 0; j < 4; ++j) sl[j] = pb[j];
+            for (int w = 0; w < NW; ++w) {
+                if (!pend[w]) continue;
+                const uint32_t kl = (uint32_t)key[w], kh = (uint32_t)(key[w] >> 32);
+                bool empty = false, found = false;
+                uint32_t lo = 0, info = 0;
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const bool hit = sl[w][j][0] == kl && sl[w][j][1] == kh;
+                    lo = hit ? sl[w][j][2] : lo;
+                    info = hit ? sl[w][j][3] : info;
+                    found |= hit;
+                    empty |= sl[w][j][0] == 0xFFFFFFFFu && sl[w][j][1] == 0xFFFFFFFFu;
+                }
+                if (found) {
+                    const bool multi = (info >> 31) != 0u;
+                    which[w] = multi ? -2 : (int)info;
+                    ilo[w] = lo;
+                    ihi[w] = multi ? lo + (info & 0x7FFFFFFFu) : lo + 1u;
+                }
+                pend[w] = !(found || empty);
+                more |= pend[w];
             }
+            if (!more) break;
+#pragma unroll
+            for (int w = 0; w < NW; ++w)
+                if (pend[w]) {
+                    bk[w] = (bk[w] + 1u) & (uint32_t)I.kt_bmask;
+                    const u32x4* pb = reinterpret_cast<const u32x4*>(I.ktab) + (uint64_t)bk[w] * 4u;
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) sl[w][j] = pb[j];
+                }
         }
 
         // ---- tallies of pass i (k_scan step 5)
-        if (valid) {
+#pragma unroll
+        for (int w = 0; w < NW; ++w) {
+            if (!valid[w]) continue;
             ++t_cnt;
-            if (EM && which == -2) {
-                atomicAdd(&src.em_mult[ilo], 1u);
-                src.em_hi[ilo] = ihi;
+            if (EM && which[w] == -2) {
+                atomicAdd(&src.em_mult[ilo[w]], 1u);
+                src.em_hi[ilo[w]] = ihi[w];
             }
-            if (which >= 0) {
+            if (which[w] >= 0) {
                 double wgt = 0.0;
                 if (MODE == KM_LOCAL) {
-                    const unsigned char* qw = qbuf + cur.off;
+                    const unsigned char* qw = qbuf + cur.off[w];
                     double x = 1.0;
                     for (uint32_t i = 0; i < k; ++i) {
                         const double2 t = qtab[qw[i]];
@@ -1109,52 +1189,48 @@ void k_scan_kt(DevView I, UnitSrc src, unsigned long long* __restrict__ out_a, d
                     wgt = x;
                 }
                 if (LDS_HIST) {
-                    atomicAdd(&hA[which], 1ull);
-                    if (MODE == KM_LOCAL) atomicAdd(&hW[which], wgt);
+                    atomicAdd(&hA[which[w]], 1ull);
+                    if (MODE == KM_LOCAL) atomicAdd(&hW[which[w]], wgt);
                 } else {
-                    atomicAdd(&gU[which], 1ull);
-                    if (MODE == KM_LOCAL) atomicAdd(&out_w[which], wgt);
+                    atomicAdd(&gU[which[w]], 1ull);
+                    if (MODE == KM_LOCAL) atomicAdd(&out_w[which[w]], wgt);
                 }
             }
         }
-        // ---- ambiguity of pass i (k_scan step 6, one sub-pass)
+        // ---- ambiguity (k_scan step 6): per unit, its first counted group and whether another group follows. A
+        // wave-uniform loop over the pass's units (in order) with two ballots each replaces the segmented min/max scan.
         {
-            const uint64_t hm = __ballot(cur.has != 0u);
-            const uint32_t last = (uint32_t)__popcll(hm) - 1u;
-            const uint64_t unit = PAIRED ? ((cur.r + cur.ri) >> 1) : (cur.r + cur.ri);
-            int vmin = (valid && which >= 0) ? which : INT_MAX;
-            int vmax = (valid && which >= 0) ? which : -1;
-            const uint64_t unit0 = rl64(unit, 0);
-            if (cunit != ~0ull && unit0 != cunit) {
-                amb += (cmax >= 0 && cmin != cmax) ? 1u : 0u;
-                cunit = ~0ull;
-            }
-            if (lane == 0 && unit == cunit) {
-                vmin = min(vmin, cmin);
-                vmax = max(vmax, cmax);
-            }
-            const uint64_t uprev = __shfl_up(unit, 1);
-            const bool head = cur.has != 0u && (lane == 0 || unit != uprev);
-            const uint64_t heads = __ballot(head);
-            const uint64_t below = heads & ((lane == 63u) ? ~0ull : ((2ull << lane) - 1ull));
-            const uint32_t seg_start = 63u - (uint32_t)__clzll(below);
-            for (uint32_t d = 1; d < 64u; d <<= 1) {
-                const int om = __shfl_up(vmin, d), oM = __shfl_up(vmax, d);
-                if (lane >= d && lane - d >= seg_start) {
-                    vmin = min(vmin, om);
-                    vmax = max(vmax, oM);
+            uint64_t um = cur.units;
+            while (um != 0) {
+                const uint32_t i = (uint32_t)__builtin_ctzll(um);
+                um &= um - 1;
+                const uint64_t unit = PAIRED ? ((cur.r + i) >> 1) : (cur.r + i);
+                bool seen = false, differs = false;
+                int g = -1;
+#pragma unroll
+                for (int w = 0; w < NW; ++w) {
+                    const bool counted = cur.has[w] != 0u && cur.ri[w] == i && valid[w] && which[w] >= 0;
+                    const uint64_t m = __ballot(counted);
+                    if (m == 0) continue;
+                    if (!seen) g = rli(which[w], (uint32_t)__builtin_ctzll(m));
+                    seen = true;
+                    differs |= __ballot(counted && which[w] != g) != 0;
+                }
+                if (unit != cunit) {  // the carried unit is complete
+                    if (cunit != ~0ull) amb += cmax;
+                    cunit = unit;
+                    cmin = seen ? g : -1;  // first counted group of the unit
+                    cmax = differs ? 1 : 0;  // ambiguous so far
+                } else if (seen) {
+                    if (cmin < 0) cmin = g;
+                    else if (g != cmin) cmax = 1;
+                    if (differs) cmax = 1;
                 }
             }
-            const bool tail = cur.has != 0u && (lane == last || ((heads >> (lane + 1u)) & 1ull));
-            const bool amb_lane = tail && lane != last && vmax >= 0 && vmin != vmax;
-            amb += (uint32_t)__popcll(__ballot(amb_lane));
-            cmin = rli(vmin, last);
-            cmax = rli(vmax, last);
-            cunit = rl64(unit, last);
         }
         if (skipped) {  // walk past units without windows (serial loads; rare: 64 units shorter than k)
             for (;;) {
-                nxt = kt_cursor(rn, on, r_end, nb, ne, lane, k);
+                nxt = kt_cursor<NW>(rn, on, r_end, nb, ne, lane, k);
                 if (nxt.any || rn >= r_end) break;
                 kt_advance(nxt, r_end, rn, on);
                 kt_load_offsets(src, rn, r_end, lane, nb, ne);
@@ -1162,18 +1238,16 @@ void k_scan_kt(DevView I, UnitSrc src, unsigned long long* __restrict__ out_a, d
             if (nxt.any) {
                 kt_advance(nxt, r_end, rn, on);
                 kt_load_offsets(src, rn, r_end, lane, nb, ne);
-                KT_STAGE_LOAD(nxt, cur.s0);
+                kt_stage_load(src, nxt, cur.s0, lane, stg);
             }
         }
         wave_sync();  // every lane is done with pass i's LDS words
         // ---- bases of pass i + 1 into LDS
-        if (nxt.any) KT_STAGE_STORE(nxt);
+        if (nxt.any) stage_store(nxt);
         cur = nxt;
     }
-#undef KT_STAGE_LOAD
-#undef KT_STAGE_STORE
 
-    if (cunit != ~0ull) amb += (cmax >= 0 && cmin != cmax) ? 1u : 0u;
+    if (cunit != ~0ull) amb += (uint32_t)cmax;
     const unsigned long long tsum = wave_sum<unsigned long long>((unsigned long long)t_cnt);
     if (lane == 0) {
         if (tsum) atomicAdd(&out_a[0], tsum);
@@ -1191,7 +1265,6 @@ void k_scan_kt(DevView I, UnitSrc src, unsigned long long* __restrict__ out_a, d
         }
     }
 }
-
 
 // ---- k-mer interval table construction (per k, once per replica) ----
 // Pass 1: every N-free window of every text inserts its packed k-mer into a set (8-B slots, linear probing, CAS);
@@ -1344,7 +1417,7 @@ struct speq_device_index {
     bool kmer_table = true;       // tuning "kmer_table": scans of k <= 31 look windows up in a per-k k-mer table
     uint32_t ilp_kt = 1;          // tuning "ilp_kt": windows per lane of k-mer-table scans (1, 2 or 4)
     uint32_t blocks_per_cu_kt = 0;  // tuning "blocks_per_cu_kt": blocks_per_cu of k-mer-table scans (default: no cap)
-    bool kt_pipeline = true;        // tuning "kt_pipeline": k_scan_kt (software-pipelined) for ilp_kt == 1 read scans
+    bool kt_pipeline = true;        // tuning "kt_pipeline": k_scan_kt (software-pipelined) for ilp_kt <= 2 read scans
     uint32_t kt_slots = 4;        // tuning "kt_slots": table slots per distinct k-mer (load factor 1/kt_slots .. 2/kt_slots)
     struct KmerTable {
         uint4* table = nullptr;
@@ -1392,9 +1465,11 @@ void allow_big_lds() {
     allow_big_lds_kt<MODE, PAIRED, LDS, false>();
     allow_big_lds_kt<MODE, PAIRED, LDS, true>();
     if constexpr (MODE != KM_REF) {
-        HIP_OK(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_scan_kt<MODE, PAIRED, LDS, false>),
+        HIP_OK(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_scan_kt<MODE, PAIRED, LDS, false, 1>),
                                    hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-        HIP_OK(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_scan_kt<MODE, PAIRED, LDS, true>),
+        HIP_OK(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_scan_kt<MODE, PAIRED, LDS, false, 2>),
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+        HIP_OK(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_scan_kt<MODE, PAIRED, LDS, true, 1>),
                                    hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     }
 }
@@ -1540,13 +1615,16 @@ void launch_v(const speq_device_index* d, const DevView& v, const UnitSrc& src, 
               hipStream_t st, unsigned long long* a, unsigned long long* b, double* w) {
     const uint32_t ilp = KT ? d->ilp_kt : (MODE == KM_LOCAL ? d->ilp_local : d->ilp);
     if constexpr (KT && MODE != KM_REF) {
-        if (ilp == 1 && d->kt_pipeline) {  // software-pipelined table scan
+        if (ilp <= 2 && d->kt_pipeline) {  // software-pipelined table scan
             if (src.em_mult != nullptr)
-                hipLaunchKernelGGL((k_scan_kt<MODE, PAIRED, LDS, true>), dim3(grid), dim3(BLOCK_THREADS), lds, st, v,
-                                   src, a, w);
+                hipLaunchKernelGGL((k_scan_kt<MODE, PAIRED, LDS, true, 1>), dim3(grid), dim3(BLOCK_THREADS), lds, st,
+                                   v, src, a, w);
+            else if (ilp == 2)
+                hipLaunchKernelGGL((k_scan_kt<MODE, PAIRED, LDS, false, 2>), dim3(grid), dim3(BLOCK_THREADS), lds, st,
+                                   v, src, a, w);
             else
-                hipLaunchKernelGGL((k_scan_kt<MODE, PAIRED, LDS, false>), dim3(grid), dim3(BLOCK_THREADS), lds, st, v,
-                                   src, a, w);
+                hipLaunchKernelGGL((k_scan_kt<MODE, PAIRED, LDS, false, 1>), dim3(grid), dim3(BLOCK_THREADS), lds, st,
+                                   v, src, a, w);
             return;
         }
     }
