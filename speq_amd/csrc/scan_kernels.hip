@@ -431,6 +431,10 @@ __device__ __forceinline__ void search_packed_n(const DevView& I, const Rsrc& R,
 // before its key has proven the key absent. A scan reads a window's key straight from the ballots of its bases.
 constexpr uint32_t KT_MAX_K = 31;
 constexpr unsigned long long KT_EMPTY = ~0ull;
+#ifndef SPEQ_KT_BSLOTS  // slots per bucket (A/B knob): a lookup reads 16 * SPEQ_KT_BSLOTS bytes
+#define SPEQ_KT_BSLOTS 4
+#endif
+constexpr uint32_t KT_BSLOTS = SPEQ_KT_BSLOTS;
 
 __host__ __device__ __forceinline__ uint32_t kt_hash(uint64_t key) {  // two 31-bit planes -> 32-bit bucket hash
     uint32_t x = (uint32_t)key ^ ((uint32_t)(key >> 32) * 0x9E3779B1u);
@@ -478,13 +482,13 @@ __device__ __forceinline__ void search_ktab_n(const DevView& I, const uint64_t (
 #pragma unroll
         for (int w = 0; w < NW; ++w) any |= pend[w];
         if (!any) break;
-        u32x4 sl[NW][4];
+        u32x4 sl[NW][KT_BSLOTS];
 #pragma unroll
         for (int w = 0; w < NW; ++w)
             if (pend[w]) {
-                const u32x4* p = reinterpret_cast<const u32x4*>(I.ktab) + b[w] * 4u;
+                const u32x4* p = reinterpret_cast<const u32x4*>(I.ktab) + b[w] * KT_BSLOTS;
 #pragma unroll
-                for (int j = 0; j < 4; ++j) sl[w][j] = p[j];
+                for (int j = 0; j < (int)KT_BSLOTS; ++j) sl[w][j] = p[j];
             }
 #pragma unroll
         for (int w = 0; w < NW; ++w)
@@ -493,7 +497,7 @@ __device__ __forceinline__ void search_ktab_n(const DevView& I, const uint64_t (
                 bool empty = false, found = false;
                 uint32_t lo = 0, info = 0;
 #pragma unroll
-                for (int j = 0; j < 4; ++j) {
+                for (int j = 0; j < (int)KT_BSLOTS; ++j) {
                     const bool hit = sl[w][j][0] == kl && sl[w][j][1] == kh;
                     lo = hit ? sl[w][j][2] : lo;
                     info = hit ? sl[w][j][3] : info;
@@ -1025,11 +1029,11 @@ void k_scan_kt(DevView I, UnitSrc src, unsigned long long* __restrict__ out_a, d
     const uint32_t buf = src.buf_bytes;
     double2* qtab = reinterpret_cast<double2*>(smem + hist_bytes);  // KM_LOCAL only
     const uint32_t qtab_bytes = MODE == KM_LOCAL ? QTAB_BYTES : 0u;
-    // per wave: qualities [buf] (local mode) | bad-mask words | bit-0 plane words | bit-1 plane words
+    // per wave: qualities of two passes [2 x buf] (local mode) | bad-mask words | bit-0 planes | bit-1 planes
     const uint32_t mw = mask_words(buf);
-    unsigned char* wbase = smem + hist_bytes + qtab_bytes + wid * (buf * (MODE == KM_LOCAL ? 1u : 0u) + 24u * mw);
-    unsigned char* qbuf = wbase;
-    unsigned long long* mbuf = reinterpret_cast<unsigned long long*>(wbase + (MODE == KM_LOCAL ? buf : 0u));
+    unsigned char* wbase = smem + hist_bytes + qtab_bytes + wid * (buf * (MODE == KM_LOCAL ? 2u : 0u) + 24u * mw);
+    unsigned char* qbuf0 = wbase;
+    unsigned long long* mbuf = reinterpret_cast<unsigned long long*>(wbase + (MODE == KM_LOCAL ? 2u * buf : 0u));
     unsigned long long* p0buf = mbuf + mw;
     unsigned long long* p1buf = p0buf + mw;
 
@@ -1051,43 +1055,21 @@ void k_scan_kt(DevView I, UnitSrc src, unsigned long long* __restrict__ out_a, d
     int cmin = -1, cmax = 0;  // carried unit: its first counted group (-1: none yet), ambiguous so far (0/1)
     uint64_t cunit = ~0ull;
     KtStage<NW> stg;
-    auto stage_store = [&](const KtCursor<NW>& cu) {
+    auto stage_store = [&](const KtCursor<NW>& cu, unsigned char* qb) {
 #pragma unroll
         for (int j = 0; j <= NW; ++j)
-            kt_stage_chunk<MODE>(src, stg.c[j], stg.q[j], 64u * (uint32_t)j + lane, cu.span, qbuf, mbuf, p0buf,
+            kt_stage_chunk<MODE>(src, stg.c[j], stg.q[j], 64u * (uint32_t)j + lane, cu.span, qb, mbuf, p0buf,
                                  p1buf, (uint32_t)j);
         wave_sync();
     };
-
-    // prologue: cursor of pass 0, offsets of pass 1 in flight, bases of pass 0 in LDS
-    uint64_t r = PAIRED ? 2 * u0 : u0, o = 0;
-    uint64_t ob, oe;
-    KtCursor<NW> cur;
-    for (;;) {
-        kt_load_offsets(src, r, r_end, lane, ob, oe);
-        cur = kt_cursor<NW>(r, o, r_end, ob, oe, lane, k);
-        if (cur.any || r >= r_end) break;
-        kt_advance(cur, r_end, r, o);
-    }
-    uint64_t rn = r_end, on = 0, nb = 0, ne = 0;
-    if (cur.any) {  // (a wave without windows still reaches the block's final __syncthreads)
-        kt_advance(cur, r_end, rn, on);
-        kt_load_offsets(src, rn, r_end, lane, nb, ne);
-        kt_stage_load(src, cur, cur.s0, lane, stg);
-        stage_store(cur);
-    }
-
-    while (cur.any) {
-        // ---- keys of pass i
-        bool valid[NW];
-        uint64_t key[NW];
-        uint32_t bk[NW];
+    // keys of a staged pass (LDS bad mask + bit planes) and their first buckets
+    auto make_keys = [&](const KtCursor<NW>& cu, bool (&valid)[NW], uint64_t (&key)[NW], uint32_t (&bk)[NW]) {
 #pragma unroll
         for (int w = 0; w < NW; ++w) {
             valid[w] = false;
             key[w] = 0;
-            if (cur.has[w]) {
-                const uint32_t off = cur.off[w];
+            if (cu.has[w]) {
+                const uint32_t off = cu.off[w];
                 const uint32_t w0 = off >> 6, w1 = (off + k - 1u) >> 6;
                 uint64_t badbits = 0;
                 for (uint32_t wi = w0; wi <= w1; ++wi) {
@@ -1101,26 +1083,78 @@ void k_scan_kt(DevView I, UnitSrc src, unsigned long long* __restrict__ out_a, d
             }
             bk[w] = valid[w] ? (kt_hash(key[w]) & (uint32_t)I.kt_bmask) : 0u;
         }
-
-        // ---- cursor of pass i + 1 (its offsets were loaded one pass ago)
-        KtCursor<NW> nxt = kt_cursor<NW>(rn, on, r_end, nb, ne, lane, k);
-        const bool skipped = !nxt.any && rn < r_end;  // 64 units without a window (rare): handled below
-        kt_advance(nxt, r_end, rn, on);
-
-        // ---- in flight together: the table buckets of pass i, the offsets of pass i + 2, the bases of pass i + 1
-        u32x4 sl[NW][4];
+    };
+    auto issue_lookups = [&](const uint32_t (&bk)[NW], u32x4 (&sl)[NW][KT_BSLOTS]) {
 #pragma unroll
         for (int w = 0; w < NW; ++w) {
 #if SPEQ_PROBE_NOLOOKUP  // timing probe only (wrong results): every lookup finds an empty bucket
-            for (int j = 0; j < 4; ++j) sl[w][j] = u32x4{0xFFFFFFFFu, 0xFFFFFFFFu, bk[w], 0u};
+            for (int j = 0; j < (int)KT_BSLOTS; ++j) sl[w][j] = u32x4{0xFFFFFFFFu, 0xFFFFFFFFu, bk[w], 0u};
 #else
-            const u32x4* pb = reinterpret_cast<const u32x4*>(I.ktab) + (uint64_t)bk[w] * 4u;
+            const u32x4* pb = reinterpret_cast<const u32x4*>(I.ktab) + (uint64_t)bk[w] * KT_BSLOTS;
 #pragma unroll
-            for (int j = 0; j < 4; ++j) sl[w][j] = pb[j];
+            for (int j = 0; j < (int)KT_BSLOTS; ++j) sl[w][j] = pb[j];
 #endif
         }
+    };
+
+    // Two passes deep: at the top of iteration i, the table lookups of pass i are in flight, the cursor of pass
+    // i + 1 is known and its bases are loading (issued before the lookups, so waiting for them does not wait for the
+    // lookups), and the offsets of pass i + 2 are loading. Iteration i stages pass i + 1, computes its keys and the
+    // cursor of pass i + 2, issues the next loads (lookups of pass i + 1 last), and only then resolves pass i: the
+    // lookup latency of pass i is covered by the work on pass i + 1.
+    uint64_t r = PAIRED ? 2 * u0 : u0, o = 0;
+    uint64_t ob, oe;
+    KtCursor<NW> cur;
+    for (;;) {
+        kt_load_offsets(src, r, r_end, lane, ob, oe);
+        cur = kt_cursor<NW>(r, o, r_end, ob, oe, lane, k);
+        if (cur.any || r >= r_end) break;
+        kt_advance(cur, r_end, r, o);
+    }
+    uint64_t rn = r_end, on = 0, nb = 0, ne = 0;
+    KtCursor<NW> nxt;
+    nxt.any = 0u;
+    bool valid[NW];
+    uint64_t key[NW];
+    uint32_t bk[NW];
+    u32x4 sl[NW][KT_BSLOTS];
+    uint32_t par = 0;  // local mode: qualities of pass i in qbuf0 + par * buf
+    if (cur.any) {  // (a wave without windows still reaches the block's final __syncthreads)
+        kt_advance(cur, r_end, rn, on);
+        kt_load_offsets(src, rn, r_end, lane, nb, ne);
+        kt_stage_load(src, cur, cur.s0, lane, stg);
+        stage_store(cur, qbuf0);
+        make_keys(cur, valid, key, bk);
+        for (;;) {  // cursor of pass 1 (serially past units without windows)
+            nxt = kt_cursor<NW>(rn, on, r_end, nb, ne, lane, k);
+            if (nxt.any || rn >= r_end) break;
+            kt_advance(nxt, r_end, rn, on);
+            kt_load_offsets(src, rn, r_end, lane, nb, ne);
+        }
+        kt_advance(nxt, r_end, rn, on);
         kt_load_offsets(src, rn, r_end, lane, nb, ne);
         kt_stage_load(src, nxt, cur.s0, lane, stg);
+        issue_lookups(bk, sl);
+    }
+
+    while (cur.any) {
+        unsigned char* qbuf = qbuf0 + (MODE == KM_LOCAL ? par * buf : 0u);        // pass i
+        unsigned char* qbufn = qbuf0 + (MODE == KM_LOCAL ? (par ^ 1u) * buf : 0u);  // pass i + 1
+        // ---- stage pass i + 1 (pass i's keys are already computed), its keys and first buckets
+        bool valid_n[NW];
+        uint64_t key_n[NW];
+        uint32_t bk_n[NW];
+        if (nxt.any) stage_store(nxt, qbufn);
+        make_keys(nxt, valid_n, key_n, bk_n);
+        // ---- cursor of pass i + 2 (its offsets were loaded one pass ago)
+        KtCursor<NW> nx2 = kt_cursor<NW>(rn, on, r_end, nb, ne, lane, k);
+        const bool skipped = !nx2.any && rn < r_end;  // 64 units without a window (rare): handled below
+        kt_advance(nx2, r_end, rn, on);
+        // ---- issue: offsets of pass i + 3, bases of pass i + 2, then the lookups of pass i + 1
+        kt_load_offsets(src, rn, r_end, lane, nb, ne);
+        kt_stage_load(src, nx2, cur.s0, lane, stg);
+        u32x4 sl_n[NW][KT_BSLOTS];
+        issue_lookups(bk_n, sl_n);
 
         // ---- resolve the lookups of pass i (rarely a further bucket)
         int which[NW];
@@ -1141,7 +1175,7 @@ void k_scan_kt(DevView I, UnitSrc src, unsigned long long* __restrict__ out_a, d
                 bool empty = false, found = false;
                 uint32_t lo = 0, info = 0;
 #pragma unroll
-                for (int j = 0; j < 4; ++j) {
+                for (int j = 0; j < (int)KT_BSLOTS; ++j) {
                     const bool hit = sl[w][j][0] == kl && sl[w][j][1] == kh;
                     lo = hit ? sl[w][j][2] : lo;
                     info = hit ? sl[w][j][3] : info;
@@ -1162,9 +1196,9 @@ void k_scan_kt(DevView I, UnitSrc src, unsigned long long* __restrict__ out_a, d
             for (int w = 0; w < NW; ++w)
                 if (pend[w]) {
                     bk[w] = (bk[w] + 1u) & (uint32_t)I.kt_bmask;
-                    const u32x4* pb = reinterpret_cast<const u32x4*>(I.ktab) + (uint64_t)bk[w] * 4u;
+                    const u32x4* pb = reinterpret_cast<const u32x4*>(I.ktab) + (uint64_t)bk[w] * KT_BSLOTS;
 #pragma unroll
-                    for (int j = 0; j < 4; ++j) sl[w][j] = pb[j];
+                    for (int j = 0; j < (int)KT_BSLOTS; ++j) sl[w][j] = pb[j];
                 }
         }
 
@@ -1230,21 +1264,29 @@ void k_scan_kt(DevView I, UnitSrc src, unsigned long long* __restrict__ out_a, d
         }
         if (skipped) {  // walk past units without windows (serial loads; rare: 64 units shorter than k)
             for (;;) {
-                nxt = kt_cursor<NW>(rn, on, r_end, nb, ne, lane, k);
-                if (nxt.any || rn >= r_end) break;
-                kt_advance(nxt, r_end, rn, on);
+                nx2 = kt_cursor<NW>(rn, on, r_end, nb, ne, lane, k);
+                if (nx2.any || rn >= r_end) break;
+                kt_advance(nx2, r_end, rn, on);
                 kt_load_offsets(src, rn, r_end, lane, nb, ne);
             }
-            if (nxt.any) {
-                kt_advance(nxt, r_end, rn, on);
+            if (nx2.any) {
+                kt_advance(nx2, r_end, rn, on);
                 kt_load_offsets(src, rn, r_end, lane, nb, ne);
-                kt_stage_load(src, nxt, cur.s0, lane, stg);
+                kt_stage_load(src, nx2, cur.s0, lane, stg);
             }
         }
-        wave_sync();  // every lane is done with pass i's LDS words
-        // ---- bases of pass i + 1 into LDS
-        if (nxt.any) stage_store(nxt);
+        // ---- rotate: pass i + 1 becomes pass i
         cur = nxt;
+        nxt = nx2;
+        par ^= 1u;
+#pragma unroll
+        for (int w = 0; w < NW; ++w) {
+            valid[w] = valid_n[w];
+            key[w] = key_n[w];
+            bk[w] = bk_n[w];
+#pragma unroll
+            for (int j = 0; j < (int)KT_BSLOTS; ++j) sl[w][j] = sl_n[w][j];
+        }
     }
 
     if (cunit != ~0ull) amb += (uint32_t)cmax;
@@ -1349,8 +1391,8 @@ __global__ void k_ktab_fill(DevView I, const unsigned long long* __restrict__ ke
         const uint32_t info = out[0] == -2 ? (0x80000000u | (hi[0] - lo[0])) : (uint32_t)out[0];
         uint64_t b = kt_hash(code) & bmask;  // bmask < 2^32
         for (bool placed = false; !placed; b = (b + 1) & bmask) {
-            for (uint32_t j = 0; j < 4u && !placed; ++j) {
-                uint4* slot = table + b * 4u + j;
+            for (uint32_t j = 0; j < KT_BSLOTS && !placed; ++j) {
+                uint4* slot = table + b * KT_BSLOTS + j;
                 if (atomicCAS(reinterpret_cast<unsigned long long*>(slot), KT_EMPTY, code) == KT_EMPTY) {
                     slot->z = lo[0];
                     slot->w = info;
@@ -1580,10 +1622,10 @@ speq_device_index::KmerTable build_ktab(speq_device_index* d, uint32_t k) {
             HIP_OK(hipStreamSynchronize(d->stream));
         }
         kt.distinct = distinct;
-        kt.buckets = next_pow2(std::max<uint64_t>(1, (distinct * d->kt_slots + 3) / 4));  // 4 slots per bucket
-        HIP_OK(hipMalloc(&kt.table, kt.buckets * 64));
+        kt.buckets = next_pow2(std::max<uint64_t>(1, (distinct * d->kt_slots + KT_BSLOTS - 1) / KT_BSLOTS));
+        HIP_OK(hipMalloc(&kt.table, kt.buckets * 16 * KT_BSLOTS));
         d->track(kt.table);
-        HIP_OK(hipMemsetAsync(kt.table, 0xFF, kt.buckets * 64, d->stream));
+        HIP_OK(hipMemsetAsync(kt.table, 0xFF, kt.buckets * 16 * KT_BSLOTS, d->stream));
         if (distinct > 0) {
             const DevView v = scan_view(d, k);
             const uint32_t grid = (uint32_t)std::min<uint64_t>((slots + 255) / 256, 16384);
@@ -2108,7 +2150,7 @@ int speq_device_prepare(speq_device_index* d, uint32_t k, uint64_t* distinct_kme
         if (k < 1 || k > MAX_K) throw std::invalid_argument("speq_device_prepare: k must be in [1, 4096]");
         const speq_device_index::KmerTable* kt = ensure_ktab(d, k);
         if (distinct_kmers) *distinct_kmers = kt ? kt->distinct : 0;
-        if (table_bytes) *table_bytes = kt ? kt->buckets * 64 : 0;
+        if (table_bytes) *table_bytes = kt ? kt->buckets * 16 * KT_BSLOTS : 0;
         if (build_ms) *build_ms = kt ? kt->build_ms : 0.0;
     });
 }

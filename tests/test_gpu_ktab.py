@@ -38,7 +38,7 @@ def test_key_set_is_the_distinct_reference_kmers(small, k):
     dev = DeviceIndex(idx)
     info = dev.prepare(k)
     assert info["distinct_kmers"] == distinct_kmers(ref.records, k)
-    assert info["table_bytes"] >= 64 and info["table_bytes"] * 4 // 64 >= 2 * info["distinct_kmers"]  # load <= 1/2
+    assert info["table_bytes"] >= 16 and info["table_bytes"] // 16 >= 2 * info["distinct_kmers"]  # load <= 1/2
 
 
 def test_no_table_above_31_or_when_off(small):
