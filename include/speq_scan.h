@@ -292,7 +292,7 @@ int speq_device_get_tuning(const speq_device_index* d, const char* key, int64_t*
  * >= 2 groups), computed once per distinct k-mer by FM backward search; a scan then resolves each window with one
  * 64-B bucket load instead of a chain of LF steps (an absent k-mer does not occur). Built on the replica's GPU by
  * the first scan with k, or here ahead of time; blocking. Outputs may be NULL; all zero when tables are off
- * (tuning "kmer_table" = 0) or k > 31 (those scans use LF steps). Replaces no reference call; the reference
+ * (tuning "kmer_table" = 0), k > 31, or the table would not fit the free HBM (those scans use LF steps). Replaces no reference call; the reference
  * searches each window from scratch (fm_scanner.cpp:208). */
 int speq_device_prepare(speq_device_index* d, uint32_t k, uint64_t* distinct_kmers, uint64_t* table_bytes,
                         double* build_ms);

@@ -1605,7 +1605,12 @@ speq_device_index::KmerTable build_ktab(speq_device_index* d, uint32_t k) {
     try {
         unsigned long long distinct = 0;
         const uint64_t slots = next_pow2(std::max<uint64_t>(2 * total, 64));
-        if (slots > (1ull << 32)) throw std::invalid_argument("k-mer table: more than 2^31 reference windows");
+        // too large for 32-bit bucket hashing, or for the free HBM (key set + a table of up to 4 slots per window):
+        // no table, scans of this k use LF steps (same results)
+        size_t free_b = 0, total_b = 0;
+        HIP_OK(hipMemGetInfo(&free_b, &total_b));
+        const uint64_t need = slots * 8 + next_pow2(std::max<uint64_t>(1, total * d->kt_slots / KT_BSLOTS)) * 16 * KT_BSLOTS;
+        if (slots > (1ull << 32) || need > free_b / 10 * 9) return kt;  // kt.table == nullptr
         if (total > 0) {
             HIP_OK(hipMalloc(&keys, slots * 8));
             HIP_OK(hipMalloc(&d_cum, cum.size() * 8));
@@ -1649,7 +1654,7 @@ const speq_device_index::KmerTable* ensure_ktab(speq_device_index* d, uint32_t k
     std::lock_guard<std::mutex> lk(d->kt_mu);
     auto it = d->ktabs.find(k);
     if (it == d->ktabs.end()) it = d->ktabs.emplace(k, build_ktab(d, k)).first;
-    return &it->second;
+    return it->second.table ? &it->second : nullptr;  // null table: too large, LF steps
 }
 
 template <int MODE, bool PAIRED, bool LDS, bool KT>
