@@ -1460,7 +1460,7 @@ struct speq_device_index {
     uint32_t ilp_kt = 1;          // tuning "ilp_kt": windows per lane of k-mer-table scans (1, 2 or 4)
     uint32_t blocks_per_cu_kt = 0;  // tuning "blocks_per_cu_kt": blocks_per_cu of k-mer-table scans (default: no cap)
     bool kt_pipeline = true;        // tuning "kt_pipeline": k_scan_kt (software-pipelined) for ilp_kt <= 2 read scans
-    uint32_t kt_slots = 4;        // tuning "kt_slots": table slots per distinct k-mer (load factor 1/kt_slots .. 2/kt_slots)
+    uint32_t kt_slots = 2;        // tuning "kt_slots": table slots per distinct k-mer (load factor 1/kt_slots .. 2/kt_slots)
     struct KmerTable {
         uint4* table = nullptr;
         uint64_t buckets = 0, distinct = 0;
