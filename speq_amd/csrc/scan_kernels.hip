@@ -72,9 +72,11 @@ struct DevView {
     const uint4* pfx_rank;   // sparse form of `prefix` (or null): {count, 96-bit presence} per 96 codes ...
     const uint2* pfx_iv;     // ... and the intervals of the present codes only, in code order
     const uint4* ktab;       // k-mer interval table for k == kt_k (or null): 64-B buckets of 4 slots, see KmerTable
-    uint64_t kt_bmask;       // buckets - 1 (a power of two minus one)
+    uint64_t kt_bmask;       // buckets - 1 (a power of two minus one); compact tables: the bucket count
+    const uint2* kt_multi;   // compact tables: {lo, hi} of each multi-group k-mer
     uint32_t n, q, G, nb;
     uint32_t kt_k;
+    uint32_t kt_compact;     // 1: ktab holds the compact 8-B-slot form (k <= KT8_MAX_K)
 };
 
 struct UnitSrc {
@@ -460,6 +462,20 @@ __device__ __forceinline__ uint64_t kt_code(uint64_t key, uint32_t k) {
     for (uint32_t j = 0; j < k; ++j)
         code = (code << 2) | ((key >> j) & 1ull) | (((key >> (32u + j)) & 1ull) << 1);
     return code;
+}
+
+// ---- compact k-mer table (k <= KT8_MAX_K): 64-B buckets of eight 8-B slots ----
+// slot = ck | payload << 2k with ck = plane0 | plane1 << k (the window's two bit planes, k bits each); payload = the
+// group id, or (1 << (pb - 1)) | m for a k-mer whose occurrences span >= 2 groups, m indexing kt_multi[] = {lo, hi}
+// (read by EM scans only); pb = 64 - 2k >= 18 bits. All-ones = empty (no valid payload is all ones). Any bucket count
+// nb (bucket = mulhi(hash, nb)), so the table is sized for a load of exactly 1/2: 4.6 MB at cfg 2 against 16 MB for
+// the 16-B-slot form, small enough to stay mostly in L2.
+constexpr uint32_t KT8_MAX_K = 23;
+__host__ __device__ __forceinline__ uint32_t kt8_bucket(uint64_t key64, uint32_t nb) {
+    return (uint32_t)(((uint64_t)kt_hash(key64) * nb) >> 32);
+}
+__host__ __device__ __forceinline__ uint64_t kt8_ck(uint64_t key64, uint32_t k) {
+    return (key64 & 0xFFFFFFFFull) | ((key64 >> 32) << k);
 }
 
 // Same outputs as search_packed_n (group / -2 / -1 and, for -2, the SA interval) from one bucket load per window:
@@ -1016,7 +1032,7 @@ __device__ __forceinline__ void kt_stage_load(const UnitSrc& src, const KtCursor
 #ifndef SPEQ_PROBE_NOLOOKUP
 #define SPEQ_PROBE_NOLOOKUP 0
 #endif
-template <int MODE, bool PAIRED, bool LDS_HIST, bool EM, int NW>
+template <int MODE, bool PAIRED, bool LDS_HIST, bool EM, int NW, bool CK>
 __global__ __launch_bounds__(BLOCK_THREADS, SPEQ_KTP_MIN_WAVES)
 void k_scan_kt(DevView I, UnitSrc src, unsigned long long* __restrict__ out_a, double* __restrict__ out_w) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -1081,7 +1097,12 @@ void k_scan_kt(DevView I, UnitSrc src, unsigned long long* __restrict__ out_a, d
                 valid[w] = badbits == 0;
                 if (valid[w]) key[w] = plane_bits(p0buf, off, k) | (plane_bits(p1buf, off, k) << 32);
             }
-            bk[w] = valid[w] ? (kt_hash(key[w]) & (uint32_t)I.kt_bmask) : 0u;
+            if (CK) {
+                bk[w] = valid[w] ? kt8_bucket(key[w], (uint32_t)I.kt_bmask) : 0u;
+                key[w] = kt8_ck(key[w], k);  // compared with the low 2k bits of the slots
+            } else {
+                bk[w] = valid[w] ? (kt_hash(key[w]) & (uint32_t)I.kt_bmask) : 0u;
+            }
         }
     };
     auto issue_lookups = [&](const uint32_t (&bk)[NW], u32x4 (&sl)[NW][KT_BSLOTS]) {
@@ -1171,22 +1192,49 @@ void k_scan_kt(DevView I, UnitSrc src, unsigned long long* __restrict__ out_a, d
 #pragma unroll
             for (int w = 0; w < NW; ++w) {
                 if (!pend[w]) continue;
-                const uint32_t kl = (uint32_t)key[w], kh = (uint32_t)(key[w] >> 32);
                 bool empty = false, found = false;
-                uint32_t lo = 0, info = 0;
+                if (CK) {
+                    const uint32_t kb = 2u * k;
+                    const uint64_t kmask = (1ull << kb) - 1ull;
+                    uint64_t hitv = 0;
 #pragma unroll
-                for (int j = 0; j < (int)KT_BSLOTS; ++j) {
-                    const bool hit = sl[w][j][0] == kl && sl[w][j][1] == kh;
-                    lo = hit ? sl[w][j][2] : lo;
-                    info = hit ? sl[w][j][3] : info;
-                    found |= hit;
-                    empty |= sl[w][j][0] == 0xFFFFFFFFu && sl[w][j][1] == 0xFFFFFFFFu;
-                }
-                if (found) {
-                    const bool multi = (info >> 31) != 0u;
-                    which[w] = multi ? -2 : (int)info;
-                    ilo[w] = lo;
-                    ihi[w] = multi ? lo + (info & 0x7FFFFFFFu) : lo + 1u;
+                    for (int j = 0; j < 8; ++j) {
+                        const uint64_t v = (uint64_t)sl[w][j >> 1][2 * (j & 1)] |
+                                           ((uint64_t)sl[w][j >> 1][2 * (j & 1) + 1] << 32);
+                        const bool e = v == ~0ull;
+                        const bool hit = !e && (v & kmask) == key[w];
+                        hitv = hit ? v : hitv;
+                        found |= hit;
+                        empty |= e;
+                    }
+                    if (found) {
+                        const uint32_t pbits = 64u - kb;
+                        const uint64_t pl = hitv >> kb;
+                        const bool multi = (pl >> (pbits - 1u)) != 0u;
+                        which[w] = multi ? -2 : (int)pl;
+                        if (EM && multi) {
+                            const uint2 iv = I.kt_multi[pl & ((1ull << (pbits - 1u)) - 1ull)];
+                            ilo[w] = iv.x;
+                            ihi[w] = iv.y;
+                        }
+                    }
+                } else {
+                    const uint32_t kl = (uint32_t)key[w], kh = (uint32_t)(key[w] >> 32);
+                    uint32_t lo = 0, info = 0;
+#pragma unroll
+                    for (int j = 0; j < (int)KT_BSLOTS; ++j) {
+                        const bool hit = sl[w][j][0] == kl && sl[w][j][1] == kh;
+                        lo = hit ? sl[w][j][2] : lo;
+                        info = hit ? sl[w][j][3] : info;
+                        found |= hit;
+                        empty |= sl[w][j][0] == 0xFFFFFFFFu && sl[w][j][1] == 0xFFFFFFFFu;
+                    }
+                    if (found) {
+                        const bool multi = (info >> 31) != 0u;
+                        which[w] = multi ? -2 : (int)info;
+                        ilo[w] = lo;
+                        ihi[w] = multi ? lo + (info & 0x7FFFFFFFu) : lo + 1u;
+                    }
                 }
                 pend[w] = !(found || empty);
                 more |= pend[w];
@@ -1195,7 +1243,8 @@ void k_scan_kt(DevView I, UnitSrc src, unsigned long long* __restrict__ out_a, d
 #pragma unroll
             for (int w = 0; w < NW; ++w)
                 if (pend[w]) {
-                    bk[w] = (bk[w] + 1u) & (uint32_t)I.kt_bmask;
+                    if (CK) bk[w] = bk[w] + 1u == (uint32_t)I.kt_bmask ? 0u : bk[w] + 1u;
+                    else bk[w] = (bk[w] + 1u) & (uint32_t)I.kt_bmask;
                     const u32x4* pb = reinterpret_cast<const u32x4*>(I.ktab) + (uint64_t)bk[w] * KT_BSLOTS;
 #pragma unroll
                     for (int j = 0; j < (int)KT_BSLOTS; ++j) sl[w][j] = pb[j];
@@ -1403,6 +1452,40 @@ __global__ void k_ktab_fill(DevView I, const unsigned long long* __restrict__ ke
     }
 }
 
+// Pass 2 of a compact table (k <= KT8_MAX_K): same search per distinct k-mer; multi-group k-mers get an index into
+// `multi` ({lo, hi}, for EM); slots are placed with one 64-bit CAS. n_multi > multi_cap means the payload bits did not
+// suffice: the caller builds the 16-B-slot table instead.
+__global__ void k_ktab_fill8(DevView I, const unsigned long long* __restrict__ keys, uint64_t n_slots, uint32_t k,
+                             unsigned long long* __restrict__ table, uint32_t nb, uint2* __restrict__ multi,
+                             unsigned int* __restrict__ n_multi, uint32_t multi_cap) {
+    const Rsrc R = make_rsrc(I);
+    const uint32_t kb = 2u * k, pbits = 64u - kb;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n_slots;
+         i += (uint64_t)gridDim.x * blockDim.x) {
+        const unsigned long long key = keys[i];
+        if (key == KT_EMPTY) continue;
+        const uint64_t P[1] = {kt_code(key, k)};
+        const bool act[1] = {true};
+        int out[1];
+        uint32_t lo[1], hi[1];
+        search_packed_n<1>(I, R, P, act, k, out, lo, hi);
+        if (out[0] == -1) continue;  // unreachable: every key occurs in the texts
+        uint64_t pl;
+        if (out[0] == -2) {
+            const uint32_t m = atomicAdd(n_multi, 1u);
+            if (m < multi_cap) multi[m] = make_uint2(lo[0], hi[0]);
+            pl = (1ull << (pbits - 1u)) | (uint64_t)(m < multi_cap ? m : 0u);
+        } else {
+            pl = (uint64_t)out[0];
+        }
+        const unsigned long long v = kt8_ck(key, k) | (pl << kb);
+        uint32_t b = kt8_bucket(key, nb);
+        for (bool placed = false; !placed; b = (b + 1u == nb) ? 0u : b + 1u)
+            for (uint32_t j = 0; j < 8u && !placed; ++j)
+                placed = atomicCAS(&table[(uint64_t)b * 8u + j], KT_EMPTY, v) == KT_EMPTY;
+    }
+}
+
 #define HIP_OK(expr)                                                                                         \
     do {                                                                                                     \
         hipError_t _e = (expr);                                                                              \
@@ -1460,11 +1543,16 @@ struct speq_device_index {
     uint32_t ilp_kt = 1;          // tuning "ilp_kt": windows per lane of k-mer-table scans (1, 2 or 4)
     uint32_t blocks_per_cu_kt = 0;  // tuning "blocks_per_cu_kt": blocks_per_cu of k-mer-table scans (default: no cap)
     bool kt_pipeline = true;        // tuning "kt_pipeline": k_scan_kt (software-pipelined) for ilp_kt <= 2 read scans
+    bool kt_compact = true;       // tuning "kt_compact": 8-B-slot tables for k <= 23 (smaller, mostly L2-resident)
+    uint32_t kt_load8 = 25;       // tuning "kt_load8": load factor of compact tables, percent (20-35 within 1 %)
     uint32_t kt_slots = 2;        // tuning "kt_slots": table slots per distinct k-mer (load factor 1/kt_slots .. 2/kt_slots)
     struct KmerTable {
         uint4* table = nullptr;
         uint64_t buckets = 0, distinct = 0;
         double build_ms = 0.0;
+        bool compact = false;   // 8-B slots (k <= KT8_MAX_K), `buckets` of 64 B, any count
+        uint2* multi = nullptr; // compact: {lo, hi} per multi-group k-mer
+        uint64_t bytes = 0;     // device bytes of the table (+ multi array)
     };
     std::mutex kt_mu;                        // the first scan with a new k builds its table
     std::map<uint32_t, KmerTable> ktabs;     // k -> table (kept until the replica closes)
@@ -1502,17 +1590,23 @@ void allow_big_lds_kt() {
                                    hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
 }
 
+template <int MODE, bool PAIRED, bool LDS, bool CK>
+void allow_big_lds_ktp() {
+    HIP_OK(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_scan_kt<MODE, PAIRED, LDS, false, 1, CK>),
+                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    HIP_OK(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_scan_kt<MODE, PAIRED, LDS, false, 2, CK>),
+                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    HIP_OK(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_scan_kt<MODE, PAIRED, LDS, true, 1, CK>),
+                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+}
+
 template <int MODE, bool PAIRED, bool LDS>
 void allow_big_lds() {
     allow_big_lds_kt<MODE, PAIRED, LDS, false>();
     allow_big_lds_kt<MODE, PAIRED, LDS, true>();
     if constexpr (MODE != KM_REF) {
-        HIP_OK(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_scan_kt<MODE, PAIRED, LDS, false, 1>),
-                                   hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-        HIP_OK(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_scan_kt<MODE, PAIRED, LDS, false, 2>),
-                                   hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-        HIP_OK(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_scan_kt<MODE, PAIRED, LDS, true, 1>),
-                                   hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+        allow_big_lds_ktp<MODE, PAIRED, LDS, false>();
+        allow_big_lds_ktp<MODE, PAIRED, LDS, true>();
     }
 }
 
@@ -1627,7 +1721,46 @@ speq_device_index::KmerTable build_ktab(speq_device_index* d, uint32_t k) {
             HIP_OK(hipStreamSynchronize(d->stream));
         }
         kt.distinct = distinct;
+        // compact form first (k <= KT8_MAX_K): sized for the load factor kt_load8; if the multi-group k-mers outgrow the
+        // payload bits, fall through to the 16-B-slot form
+        const uint32_t pbits = 64u - 2u * k;
+        const uint64_t multi_cap = std::min<uint64_t>(distinct, (1ull << (pbits - 1u)) - 2u);
+        const uint64_t nb8 = std::max<uint64_t>(1, (uint64_t)((double)distinct * 100.0 / (8.0 * d->kt_load8)) + 1);
+        if (d->kt_compact && KT_BSLOTS == 4 && k <= KT8_MAX_K && distinct > 0 && nb8 < (1ull << 32)) {
+            void* tab = nullptr;
+            uint2* multi = nullptr;
+            unsigned int* d_nm = nullptr;
+            HIP_OK(hipMalloc(&tab, nb8 * 64));
+            HIP_OK(hipMalloc(&multi, std::max<uint64_t>(multi_cap, 1) * 8));
+            HIP_OK(hipMalloc(&d_nm, 4));
+            HIP_OK(hipMemsetAsync(tab, 0xFF, nb8 * 64, d->stream));
+            HIP_OK(hipMemsetAsync(d_nm, 0, 4, d->stream));
+            const DevView v = scan_view(d, k);
+            const uint32_t grid = (uint32_t)std::min<uint64_t>((slots + 255) / 256, 16384);
+            hipLaunchKernelGGL(k_ktab_fill8, dim3(grid), dim3(256), 0, d->stream, v,
+                               reinterpret_cast<const unsigned long long*>(keys), slots, k,
+                               reinterpret_cast<unsigned long long*>(tab), (uint32_t)nb8, multi, d_nm,
+                               (uint32_t)multi_cap);
+            HIP_OK(hipGetLastError());
+            unsigned int n_multi = 0;
+            HIP_OK(hipMemcpyAsync(&n_multi, d_nm, 4, hipMemcpyDeviceToHost, d->stream));
+            HIP_OK(hipStreamSynchronize(d->stream));
+            (void)hipFree(d_nm);
+            if (n_multi <= multi_cap) {
+                kt.compact = true;
+                kt.table = reinterpret_cast<uint4*>(d->track(tab));
+                kt.multi = d->track(multi);
+                kt.buckets = nb8;
+                kt.bytes = nb8 * 64 + (uint64_t)n_multi * 8;
+                cleanup();
+                kt.build_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+                return kt;
+            }
+            (void)hipFree(tab);
+            (void)hipFree(multi);
+        }
         kt.buckets = next_pow2(std::max<uint64_t>(1, (distinct * d->kt_slots + KT_BSLOTS - 1) / KT_BSLOTS));
+        kt.bytes = kt.buckets * 16 * KT_BSLOTS;
         HIP_OK(hipMalloc(&kt.table, kt.buckets * 16 * KT_BSLOTS));
         d->track(kt.table);
         HIP_OK(hipMemsetAsync(kt.table, 0xFF, kt.buckets * 16 * KT_BSLOTS, d->stream));
@@ -1657,21 +1790,28 @@ const speq_device_index::KmerTable* ensure_ktab(speq_device_index* d, uint32_t k
     return it->second.table ? &it->second : nullptr;  // null table: too large, LF steps
 }
 
+template <int MODE, bool PAIRED, bool LDS, bool CK>
+void launch_kt(const DevView& v, const UnitSrc& src, uint32_t grid, size_t lds, hipStream_t st, unsigned long long* a,
+               double* w, uint32_t ilp) {
+    if (src.em_mult != nullptr)
+        hipLaunchKernelGGL((k_scan_kt<MODE, PAIRED, LDS, true, 1, CK>), dim3(grid), dim3(BLOCK_THREADS), lds, st, v,
+                           src, a, w);
+    else if (ilp == 2)
+        hipLaunchKernelGGL((k_scan_kt<MODE, PAIRED, LDS, false, 2, CK>), dim3(grid), dim3(BLOCK_THREADS), lds, st, v,
+                           src, a, w);
+    else
+        hipLaunchKernelGGL((k_scan_kt<MODE, PAIRED, LDS, false, 1, CK>), dim3(grid), dim3(BLOCK_THREADS), lds, st, v,
+                           src, a, w);
+}
+
 template <int MODE, bool PAIRED, bool LDS, bool KT>
 void launch_v(const speq_device_index* d, const DevView& v, const UnitSrc& src, uint32_t grid, size_t lds,
               hipStream_t st, unsigned long long* a, unsigned long long* b, double* w) {
     const uint32_t ilp = KT ? d->ilp_kt : (MODE == KM_LOCAL ? d->ilp_local : d->ilp);
     if constexpr (KT && MODE != KM_REF) {
         if (ilp <= 2 && d->kt_pipeline) {  // software-pipelined table scan
-            if (src.em_mult != nullptr)
-                hipLaunchKernelGGL((k_scan_kt<MODE, PAIRED, LDS, true, 1>), dim3(grid), dim3(BLOCK_THREADS), lds, st,
-                                   v, src, a, w);
-            else if (ilp == 2)
-                hipLaunchKernelGGL((k_scan_kt<MODE, PAIRED, LDS, false, 2>), dim3(grid), dim3(BLOCK_THREADS), lds, st,
-                                   v, src, a, w);
-            else
-                hipLaunchKernelGGL((k_scan_kt<MODE, PAIRED, LDS, false, 1>), dim3(grid), dim3(BLOCK_THREADS), lds, st,
-                                   v, src, a, w);
+            if (v.kt_compact) launch_kt<MODE, PAIRED, LDS, true>(v, src, grid, lds, st, a, w, ilp);
+            else launch_kt<MODE, PAIRED, LDS, false>(v, src, grid, lds, st, a, w, ilp);
             return;
         }
     }
@@ -1693,9 +1833,14 @@ template <int MODE, bool PAIRED, bool LDS>
 void launch_t(const speq_device_index* d, const UnitSrc& src, uint32_t grid, size_t lds, hipStream_t st,
               unsigned long long* a, unsigned long long* b, double* w, const speq_device_index::KmerTable* kt) {
     DevView v = scan_view(d, src.k);
+    // a compact table is read only by the pipelined table kernel; other scans of this k take LF steps
+    if (kt && kt->compact && !(MODE != KM_REF && d->ilp_kt <= 2 && d->kt_pipeline))
+        kt = nullptr;
     if (kt) {
         v.ktab = kt->table;
-        v.kt_bmask = kt->buckets - 1;
+        v.kt_bmask = kt->compact ? kt->buckets : kt->buckets - 1;
+        v.kt_multi = kt->multi;
+        v.kt_compact = kt->compact ? 1u : 0u;
         v.kt_k = src.k;
     }
     if (kt) launch_v<MODE, PAIRED, LDS, true>(d, v, src, grid, lds, st, a, b, w);
@@ -2155,7 +2300,7 @@ int speq_device_prepare(speq_device_index* d, uint32_t k, uint64_t* distinct_kme
         if (k < 1 || k > MAX_K) throw std::invalid_argument("speq_device_prepare: k must be in [1, 4096]");
         const speq_device_index::KmerTable* kt = ensure_ktab(d, k);
         if (distinct_kmers) *distinct_kmers = kt ? kt->distinct : 0;
-        if (table_bytes) *table_bytes = kt ? kt->buckets * 16 * KT_BSLOTS : 0;
+        if (table_bytes) *table_bytes = kt ? kt->bytes : 0;
         if (build_ms) *build_ms = kt ? kt->build_ms : 0.0;
     });
 }
@@ -2191,6 +2336,12 @@ int speq_device_set_tuning(speq_device_index* d, const char* key, int64_t value)
         } else if (k == "ilp_kt") {
             if (value != 1 && value != 2 && value != 4) throw std::invalid_argument("ilp_kt must be 1, 2 or 4");
             d->ilp_kt = (uint32_t)value;
+        } else if (k == "kt_compact") {
+            if (value != 0 && value != 1) throw std::invalid_argument("kt_compact must be 0 or 1");
+            d->kt_compact = value != 0;
+        } else if (k == "kt_load8") {
+            if (value < 10 || value > 90) throw std::invalid_argument("kt_load8 must be in [10, 90] (percent)");
+            d->kt_load8 = (uint32_t)value;
         } else if (k == "kt_slots") {
             if (value < 2 || value > 16) throw std::invalid_argument("kt_slots must be in [2, 16]");
             d->kt_slots = (uint32_t)value;
@@ -2227,6 +2378,8 @@ int speq_device_get_tuning(const speq_device_index* d, const char* key, int64_t*
         else if (k == "kt_pipeline") *value = d->kt_pipeline ? 1 : 0;
         else if (k == "blocks_per_cu_kt") *value = d->blocks_per_cu_kt;
         else if (k == "kt_slots") *value = d->kt_slots;
+        else if (k == "kt_compact") *value = d->kt_compact ? 1 : 0;
+        else if (k == "kt_load8") *value = d->kt_load8;
         else throw std::invalid_argument("speq_device_get_tuning: unknown key " + k);
     });
 }

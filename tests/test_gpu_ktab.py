@@ -38,7 +38,8 @@ def test_key_set_is_the_distinct_reference_kmers(small, k):
     dev = DeviceIndex(idx)
     info = dev.prepare(k)
     assert info["distinct_kmers"] == distinct_kmers(ref.records, k)
-    assert info["table_bytes"] >= 16 and info["table_bytes"] // 16 >= 2 * info["distinct_kmers"]  # load <= 1/2
+    # 16-B slots at load <= 1/2, or (k <= 23) 8-B slots at load 1/2: >= 16 B per distinct k-mer either way
+    assert info["table_bytes"] >= 16 * info["distinct_kmers"]
 
 
 def test_no_table_above_31_or_when_off(small):
@@ -136,3 +137,35 @@ def test_phred_weight_of_one_window_is_bit_exact(small):
         assert res.weights[g] == w, (res.weights[g], w)
         checked += 1
     assert checked > 50
+
+
+@pytest.mark.parametrize("paired", [False, True])
+def test_compact_table_equals_wide_table(paired):
+    """k <= 23 uses the compact 8-B-slot table by default; it must give what the 16-B-slot table and LF steps give
+    (counters, Phred weights, EM rows and steps); k = 24 falls back to the wide table."""
+    ref = synth.make_reference(5, 3, 10_000, ref_n_rate=0.0005)
+    idx = FmIndex.build(ref.records, ref.groups, 5, prefix_q=9, pair_steps=True, triple_steps=True)
+    reads = synth.make_reads(ref, 20_000, paired=paired, n_rate=0.001, lowq_rate=0.005, err_rate=0.004)
+    res = {}
+    for mode in ("compact", "wide", "lf"):
+        dev = DeviceIndex(idx)
+        dev.tune(kt_compact=int(mode == "compact"), kmer_table=int(mode != "lf"))
+        for k in (11, 21, 23, 24):
+            info = dev.prepare(k)
+            em = EmHistogram(dev)
+            r = em.scan(reads.seq.tobytes(), reads.qual.tobytes(), reads.offsets, k=k, paired=paired, local=True)
+            em.finalize()
+            p = np.linspace(5.0, 30.0, 5)
+            res[(mode, k)] = (r.total, r.ambiguous, r.unique.tolist(), r.weights, em.info(),
+                              em.step(p, [2] * 5, r.unique), info["table_bytes"])
+    for k in (11, 21, 23, 24):
+        for other in ("wide", "lf"):
+            a, b = res[("compact", k)], res[(other, k)]
+            assert a[:3] == b[:3], (k, other)
+            np.testing.assert_allclose(a[3], b[3], rtol=1e-12)
+            assert a[4] == b[4]
+            np.testing.assert_array_equal(a[5], b[5])
+    # the compact table is smaller than the wide one for k <= 23, and the same table for k = 24
+    for k in (11, 21, 23):
+        assert res[("compact", k)][6] < res[("wide", k)][6]
+    assert res[("compact", 24)][6] == res[("wide", 24)][6]
