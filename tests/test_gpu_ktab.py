@@ -149,7 +149,7 @@ def test_compact_table_equals_wide_table(paired):
     res = {}
     for mode in ("compact", "wide", "lf"):
         dev = DeviceIndex(idx)
-        dev.tune(kt_compact=int(mode == "compact"), kmer_table=int(mode != "lf"))
+        dev.tune(kt_compact=int(mode == "compact"), kmer_table=int(mode != "lf"), kt_load8=50)
         for k in (11, 21, 23, 24):
             info = dev.prepare(k)
             em = EmHistogram(dev)
@@ -165,7 +165,8 @@ def test_compact_table_equals_wide_table(paired):
             np.testing.assert_allclose(a[3], b[3], rtol=1e-12)
             assert a[4] == b[4]
             np.testing.assert_array_equal(a[5], b[5])
-    # the compact table is smaller than the wide one for k <= 23, and the same table for k = 24
+    # at load 1/2 the compact table (16 B per k-mer + 8 B per multi-group k-mer) is smaller than the wide one (>= 32 B
+    # per k-mer) for k <= 23; k = 24 uses the wide table either way
     for k in (11, 21, 23):
         assert res[("compact", k)][6] < res[("wide", k)][6]
     assert res[("compact", 24)][6] == res[("wide", 24)][6]
