@@ -46,7 +46,9 @@ constexpr uint32_t BLOCK_THREADS = 64 * WAVES_PER_BLOCK;
 constexpr uint32_t MAX_K = 4096;
 constexpr uint32_t LDS_HIST_MAX_G = 2048;
 constexpr uint32_t QLUT_LEN = 42;  // phred42 ranks 0..41
-constexpr uint32_t QTAB_BYTES = QLUT_LEN * 16u;  // local mode: per-block LDS copy of {1 - 10^(-q/10), its reciprocal}
+// local mode, per block in LDS: {1 - 10^(-q/10), its reciprocal} for q = 0..41, then (k_scan_kt) the weight of a window
+// of k bases that all have quality q
+constexpr uint32_t QTAB_BYTES = QLUT_LEN * 24u;
 
 // a / b correctly rounded (IEEE division) from y = RN(1 / b) by two FMA corrections: q0 = a y is within 2 ulp, the
 // first correction makes it faithful, and from a faithful quotient the second gives the correctly rounded one
@@ -986,24 +988,37 @@ __device__ __forceinline__ void kt_advance(const KtCursor<NW>& c, uint64_t r_end
 }
 
 // One 64-base chunk of a k_scan_kt pass into LDS: qualities (local mode), the bad mask and the two base bit planes.
+// Local mode also: the quality-change mask (bit p: q[p] != q[p - 1]; `qprev` = the previous chunk's last quality,
+// updated here), so a window whose qualities are all equal takes its weight from a per-block table.
 template <int MODE>
 __device__ __forceinline__ void kt_stage_chunk(const UnitSrc& src, uint32_t ch, uint32_t qv, uint32_t p,
                                                uint32_t span, unsigned char* qbuf, unsigned long long* mbuf,
-                                               unsigned long long* p0buf, unsigned long long* p1buf, uint32_t j) {
+                                               unsigned long long* p0buf, unsigned long long* p1buf,
+                                               unsigned long long* dbuf, uint32_t& qprev, uint32_t j) {
     uint32_t bad = 1, sym = 0;
+    int q = 0;
     if (p < span) {
         sym = ascii_sym(ch);
-        int q = (int)qv - 33;
+        q = (int)qv - 33;
         q = q < 0 ? 0 : (q > 41 ? 41 : q);
         bad = ((uint32_t)q <= src.cutoff || sym == 4u) ? 1u : 0u;
         if (MODE == KM_LOCAL) qbuf[p] = (unsigned char)q;
     }
     const uint64_t m = __ballot(bad != 0u);
     const uint64_t b0 = __ballot((sym & 1u) != 0u), b1 = __ballot((sym & 2u) != 0u);
+    uint64_t dm = 0;
+    if (MODE == KM_LOCAL) {
+        const uint32_t lane = p & 63u;
+        int qp = __shfl_up(q, 1);
+        if (lane == 0) qp = (int)qprev;
+        dm = __ballot(q != qp);
+        qprev = (uint32_t)__builtin_amdgcn_readlane(q, 63);
+    }
     if ((p & 63u) == 0u) {
         mbuf[j] = m;
         p0buf[j] = b0;
         p1buf[j] = b1;
+        if (MODE == KM_LOCAL) dbuf[j] = dm;
     }
 }
 
@@ -1044,18 +1059,26 @@ void k_scan_kt(DevView I, UnitSrc src, unsigned long long* __restrict__ out_a, d
     double* hW = reinterpret_cast<double*>(hA + G);  // KM_LOCAL: W
     const uint32_t buf = src.buf_bytes;
     double2* qtab = reinterpret_cast<double2*>(smem + hist_bytes);  // KM_LOCAL only
+    double* wtab = reinterpret_cast<double*>(qtab + QLUT_LEN);         // KM_LOCAL: weight of a uniform-q window
     const uint32_t qtab_bytes = MODE == KM_LOCAL ? QTAB_BYTES : 0u;
-    // per wave: qualities of two passes [2 x buf] (local mode) | bad-mask words | bit-0 planes | bit-1 planes
+    // per wave: qualities of two passes [2 x buf] (local mode) | bad-mask words | bit-0 planes | bit-1 planes |
+    // quality-change words (local mode)
     const uint32_t mw = mask_words(buf);
-    unsigned char* wbase = smem + hist_bytes + qtab_bytes + wid * (buf * (MODE == KM_LOCAL ? 2u : 0u) + 24u * mw);
+    unsigned char* wbase = smem + hist_bytes + qtab_bytes + wid * (buf * (MODE == KM_LOCAL ? 2u : 0u) + 32u * mw);
     unsigned char* qbuf0 = wbase;
     unsigned long long* mbuf = reinterpret_cast<unsigned long long*>(wbase + (MODE == KM_LOCAL ? 2u * buf : 0u));
     unsigned long long* p0buf = mbuf + mw;
     unsigned long long* p1buf = p0buf + mw;
+    unsigned long long* dbuf = p1buf + mw;
 
     if (MODE == KM_LOCAL)
-        for (uint32_t i = threadIdx.x; i < QLUT_LEN; i += BLOCK_THREADS)
-            qtab[i] = make_double2(src.qlut[2 * i], src.qlut[2 * i + 1]);
+        for (uint32_t i = threadIdx.x; i < QLUT_LEN; i += BLOCK_THREADS) {
+            const double lut = src.qlut[2 * i], inv = src.qlut[2 * i + 1];
+            qtab[i] = make_double2(lut, inv);
+            double x = 1.0;  // the window loop below, for k bases of quality i (fm_scanner.cpp:454)
+            for (uint32_t j = 0; j < k; ++j) x = div_rn(x, lut, inv);
+            wtab[i] = x;
+        }
     if (LDS_HIST)
         for (uint32_t i = threadIdx.x; i < hist_words; i += BLOCK_THREADS) hA[i] = 0ull;
     if (LDS_HIST || MODE == KM_LOCAL) __syncthreads();
@@ -1072,29 +1095,37 @@ void k_scan_kt(DevView I, UnitSrc src, unsigned long long* __restrict__ out_a, d
     uint64_t cunit = ~0ull;
     KtStage<NW> stg;
     auto stage_store = [&](const KtCursor<NW>& cu, unsigned char* qb) {
+        uint32_t qprev = 0;
 #pragma unroll
         for (int j = 0; j <= NW; ++j)
             kt_stage_chunk<MODE>(src, stg.c[j], stg.q[j], 64u * (uint32_t)j + lane, cu.span, qb, mbuf, p0buf,
-                                 p1buf, (uint32_t)j);
+                                 p1buf, dbuf, qprev, (uint32_t)j);
         wave_sync();
     };
     // keys of a staged pass (LDS bad mask + bit planes) and their first buckets
-    auto make_keys = [&](const KtCursor<NW>& cu, bool (&valid)[NW], uint64_t (&key)[NW], uint32_t (&bk)[NW]) {
+    auto make_keys = [&](const KtCursor<NW>& cu, bool (&valid)[NW], uint64_t (&key)[NW], uint32_t (&bk)[NW],
+                         bool (&uni)[NW]) {
 #pragma unroll
         for (int w = 0; w < NW; ++w) {
             valid[w] = false;
             key[w] = 0;
+            uni[w] = false;
             if (cu.has[w]) {
                 const uint32_t off = cu.off[w];
                 const uint32_t w0 = off >> 6, w1 = (off + k - 1u) >> 6;
-                uint64_t badbits = 0;
+                uint64_t badbits = 0, chg = 0;
                 for (uint32_t wi = w0; wi <= w1; ++wi) {
                     uint64_t sel = ~0ull;
                     if (wi == w0) sel &= ~0ull << (off & 63u);
                     if (wi == w1) sel &= ~0ull >> (63u - ((off + k - 1u) & 63u));
                     badbits |= mbuf[wi] & sel;
+                    if (MODE == KM_LOCAL) {  // quality changes at bases off + 1 .. off + k - 1
+                        if (wi == w0) sel &= ~(1ull << (off & 63u));
+                        chg |= dbuf[wi] & sel;
+                    }
                 }
                 valid[w] = badbits == 0;
+                uni[w] = MODE == KM_LOCAL && chg == 0;
                 if (valid[w]) key[w] = plane_bits(p0buf, off, k) | (plane_bits(p1buf, off, k) << 32);
             }
             if (CK) {
@@ -1135,7 +1166,7 @@ void k_scan_kt(DevView I, UnitSrc src, unsigned long long* __restrict__ out_a, d
     uint64_t rn = r_end, on = 0, nb = 0, ne = 0;
     KtCursor<NW> nxt;
     nxt.any = 0u;
-    bool valid[NW];
+    bool valid[NW], uni[NW];
     uint64_t key[NW];
     uint32_t bk[NW];
     u32x4 sl[NW][KT_BSLOTS];
@@ -1145,7 +1176,7 @@ void k_scan_kt(DevView I, UnitSrc src, unsigned long long* __restrict__ out_a, d
         kt_load_offsets(src, rn, r_end, lane, nb, ne);
         kt_stage_load(src, cur, cur.s0, lane, stg);
         stage_store(cur, qbuf0);
-        make_keys(cur, valid, key, bk);
+        make_keys(cur, valid, key, bk, uni);
         for (;;) {  // cursor of pass 1 (serially past units without windows)
             nxt = kt_cursor<NW>(rn, on, r_end, nb, ne, lane, k);
             if (nxt.any || rn >= r_end) break;
@@ -1162,11 +1193,11 @@ void k_scan_kt(DevView I, UnitSrc src, unsigned long long* __restrict__ out_a, d
         unsigned char* qbuf = qbuf0 + (MODE == KM_LOCAL ? par * buf : 0u);        // pass i
         unsigned char* qbufn = qbuf0 + (MODE == KM_LOCAL ? (par ^ 1u) * buf : 0u);  // pass i + 1
         // ---- stage pass i + 1 (pass i's keys are already computed), its keys and first buckets
-        bool valid_n[NW];
+        bool valid_n[NW], uni_n[NW];
         uint64_t key_n[NW];
         uint32_t bk_n[NW];
         if (nxt.any) stage_store(nxt, qbufn);
-        make_keys(nxt, valid_n, key_n, bk_n);
+        make_keys(nxt, valid_n, key_n, bk_n, uni_n);
         // ---- cursor of pass i + 2 (its offsets were loaded one pass ago)
         KtCursor<NW> nx2 = kt_cursor<NW>(rn, on, r_end, nb, ne, lane, k);
         const bool skipped = !nx2.any && rn < r_end;  // 64 units without a window (rare): handled below
@@ -1264,12 +1295,16 @@ void k_scan_kt(DevView I, UnitSrc src, unsigned long long* __restrict__ out_a, d
                 double wgt = 0.0;
                 if (MODE == KM_LOCAL) {
                     const unsigned char* qw = qbuf + cur.off[w];
-                    double x = 1.0;
-                    for (uint32_t i = 0; i < k; ++i) {
-                        const double2 t = qtab[qw[i]];
-                        x = div_rn(x, t.x, t.y);  // == x / t.x (fm_scanner.cpp:454)
+                    if (uni[w]) {
+                        wgt = wtab[qw[0]];  // the same k divisions, done once per block
+                    } else {
+                        double x = 1.0;
+                        for (uint32_t i = 0; i < k; ++i) {
+                            const double2 t = qtab[qw[i]];
+                            x = div_rn(x, t.x, t.y);  // == x / t.x (fm_scanner.cpp:454)
+                        }
+                        wgt = x;
                     }
-                    wgt = x;
                 }
                 if (LDS_HIST) {
                     atomicAdd(&hA[which[w]], 1ull);
@@ -1331,6 +1366,7 @@ void k_scan_kt(DevView I, UnitSrc src, unsigned long long* __restrict__ out_a, d
 #pragma unroll
         for (int w = 0; w < NW; ++w) {
             valid[w] = valid_n[w];
+            uni[w] = uni_n[w];
             key[w] = key_n[w];
             bk[w] = bk_n[w];
 #pragma unroll

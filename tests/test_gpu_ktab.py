@@ -125,7 +125,8 @@ def test_phred_weight_of_one_window_is_bit_exact(small):
         seq = rec[p:p + k].upper()
         if b"N" in seq:
             continue
-        q = rng.integers(31, 42, size=k)
+        # varied qualities, or one quality for the whole window (weight from the per-block uniform-q table)
+        q = rng.integers(31, 42, size=k) if checked % 2 else np.full(k, int(rng.integers(31, 42)))
         qual = bytes((q + 33).astype(np.uint8))
         res = dev.scan(seq, qual, np.array([0, k], dtype=np.uint64), k=k, local=True)
         if res.unique.sum() != 1:
