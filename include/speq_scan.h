@@ -280,6 +280,12 @@ void speq_groupings_free(speq_groupings* g);
  * "kmer_table"   : 1 (default) scans of k <= 31 look each N-free window up in the replica's k-mer interval table
  *                  for k (built by the first scan with that k, or by speq_device_prepare); 0 searches every window
  *                  with LF steps. Results are identical;
+ * "kt_compact"   : 1 (default) 8-B-slot tables for k <= 23 (0: 16-B slots); "kt_load8": their load factor in percent
+ *                  (default 25); "kt_slots": 16-B slots per distinct k-mer of the wide form (default 2). These apply to
+ *                  tables built afterwards;
+ * "ilp_kt"       : windows per lane of table scans, 1 (default) or 2 (pipelined kernel), 4 (k_scan);
+ *                  "kt_pipeline": 1 (default) the software-pipelined table kernel k_scan_kt, 0 k_scan;
+ *                  "blocks_per_cu_kt": blocks_per_cu of table scans (default 0: no cap);
  * "stream_lanes" : compute streams of a pipeline created afterwards (speq_pipeline_create, speq_scan_fastq, host
  *                  scans), 1..8 (default 3): consecutive batches are parsed and scanned on them in turn, so the
  *                  short launches of different batches overlap on the CUs. */
