@@ -1578,6 +1578,8 @@ struct speq_device_index {
     bool kmer_table = true;       // tuning "kmer_table": scans of k <= 31 look windows up in a per-k k-mer table
     uint32_t ilp_kt = 1;          // tuning "ilp_kt": windows per lane of k-mer-table scans (1, 2 or 4)
     uint32_t blocks_per_cu_kt = 0;  // tuning "blocks_per_cu_kt": blocks_per_cu of k-mer-table scans (default: no cap)
+    uint32_t grid_blocks_kt = 8192;  // tuning "grid_blocks_kt": grid cap of k-mer-table scans (cfg 2: 8192 +4.6 % over
+                                     // 16384; fewer is slower: sweep_kt_grid.txt)
     bool kt_pipeline = true;        // tuning "kt_pipeline": k_scan_kt (software-pipelined) for ilp_kt <= 2 read scans
     bool kt_compact = true;       // tuning "kt_compact": 8-B-slot tables for k <= 23 (smaller, mostly L2-resident)
     uint32_t kt_load8 = 25;       // tuning "kt_load8": load factor of compact tables, percent (20-35 within 1 %)
@@ -1893,7 +1895,8 @@ void launch_scan(speq_device_index* d, int mode, bool paired, const UnitSrc& src
     // >= 4 units (or 256 windows) per wave; grid capped (default 4096 = 2x the 8 resident blocks x 256 CUs).
     uint64_t blocks = (work_units + 4 * WAVES_PER_BLOCK - 1) / (4 * WAVES_PER_BLOCK);
     if (blocks < 1) blocks = 1;
-    if (blocks > d->grid_blocks) blocks = d->grid_blocks;
+    const uint32_t grid_cap = kt ? d->grid_blocks_kt : d->grid_blocks;
+    if (blocks > grid_cap) blocks = grid_cap;
     size_t lds_launch = lds;
     const uint32_t bpc = kt ? d->blocks_per_cu_kt : d->blocks_per_cu;
     if (bpc > 0) {  // occupancy cap: pad dynamic LDS so only bpc blocks fit a CU
@@ -2363,6 +2366,9 @@ int speq_device_set_tuning(speq_device_index* d, const char* key, int64_t value)
         } else if (k == "sparse_prefix") {
             if (value < -1 || value > 1) throw std::invalid_argument("sparse_prefix must be -1 (auto), 0 or 1");
             d->sparse_choice = (int)value;
+        } else if (k == "grid_blocks_kt") {
+            if (value < 1 || value > (1 << 20)) throw std::invalid_argument("grid_blocks_kt must be in [1, 2^20]");
+            d->grid_blocks_kt = (uint32_t)value;
         } else if (k == "blocks_per_cu_kt") {
             if (value < 0 || value > 8) throw std::invalid_argument("blocks_per_cu_kt must be in [0, 8]");
             d->blocks_per_cu_kt = (uint32_t)value;
@@ -2413,6 +2419,7 @@ int speq_device_get_tuning(const speq_device_index* d, const char* key, int64_t*
         else if (k == "ilp_kt") *value = d->ilp_kt;
         else if (k == "kt_pipeline") *value = d->kt_pipeline ? 1 : 0;
         else if (k == "blocks_per_cu_kt") *value = d->blocks_per_cu_kt;
+        else if (k == "grid_blocks_kt") *value = d->grid_blocks_kt;
         else if (k == "kt_slots") *value = d->kt_slots;
         else if (k == "kt_compact") *value = d->kt_compact ? 1 : 0;
         else if (k == "kt_load8") *value = d->kt_load8;
