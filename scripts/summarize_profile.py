@@ -27,6 +27,14 @@ def main():
         rows = list(csv.DictReader(open(st)))
         out["kernel_stats"] = [{k: r[k] for k in ("Name", "Calls", "AverageNs", "MinNs", "MaxNs", "Percentage")}
                                for r in rows if "::k_scan<" in r["Name"] or "::k_scan_kt<" in r["Name"]]
+    tr = os.path.join(src, "trace", "trace_kernel_trace.csv")
+    if os.path.exists(tr):  # steady state: the later half of the scan dispatches (the first ones run on cold caches)
+        d = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) for r in csv.DictReader(open(tr))
+             if "::k_scan<" in r["Kernel_Name"] or "::k_scan_kt<" in r["Kernel_Name"]]
+        if d:
+            tail = d[len(d) // 2:]
+            out["scan_dispatch_ns"] = d
+            out["scan_steady_state_avg_ns"] = sum(tail) / len(tail)
     pmc = collections.defaultdict(list)
     meta = {}
     for p in ("fetch", "write", "tcc", "sq", "sq2"):
