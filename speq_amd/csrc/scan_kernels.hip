@@ -452,9 +452,20 @@ __host__ __device__ __forceinline__ uint32_t kt_hash(uint64_t key) {  // two 31-
 
 // Bits [off, off + k) of a wave's plane words (k <= 31): bit j = base off + j.
 __device__ __forceinline__ uint64_t plane_bits(const unsigned long long* pl, uint32_t off, uint32_t k) {
+    // branch-free (no divergent path): the second word is read only when the bits straddle it
     const uint32_t w0 = off >> 6, sh = off & 63u;
-    uint64_t v = pl[w0] >> sh;
-    if (sh + k > 64u) v |= pl[w0 + 1u] << (64u - sh);
+    const bool two = sh + k > 64u;
+    const uint64_t lo = pl[w0], hi = pl[w0 + (two ? 1u : 0u)];
+    const uint64_t v = (lo >> sh) | (two ? ((hi << 1) << (63u - sh)) : 0ull);
+    return v & ((1ull << k) - 1ull);
+}
+
+// plane_bits for k_scan_kt's LDS words: both words are always read (one ds_read2_b64; the arrays hold >= 4 words and a
+// pass never starts a window past word 2), then selected without a branch.
+__device__ __forceinline__ uint64_t plane_bits2(const unsigned long long* pl, uint32_t off, uint32_t k) {
+    const uint32_t w0 = off >> 6, sh = off & 63u;
+    const uint64_t lo = pl[w0], hi = pl[w0 + 1u];
+    const uint64_t v = (lo >> sh) | (sh + k > 64u ? ((hi << 1) << (63u - sh)) : 0ull);
     return v & ((1ull << k) - 1ull);
 }
 
@@ -1112,21 +1123,10 @@ void k_scan_kt(DevView I, UnitSrc src, unsigned long long* __restrict__ out_a, d
             uni[w] = false;
             if (cu.has[w]) {
                 const uint32_t off = cu.off[w];
-                const uint32_t w0 = off >> 6, w1 = (off + k - 1u) >> 6;
-                uint64_t badbits = 0, chg = 0;
-                for (uint32_t wi = w0; wi <= w1; ++wi) {
-                    uint64_t sel = ~0ull;
-                    if (wi == w0) sel &= ~0ull << (off & 63u);
-                    if (wi == w1) sel &= ~0ull >> (63u - ((off + k - 1u) & 63u));
-                    badbits |= mbuf[wi] & sel;
-                    if (MODE == KM_LOCAL) {  // quality changes at bases off + 1 .. off + k - 1
-                        if (wi == w0) sel &= ~(1ull << (off & 63u));
-                        chg |= dbuf[wi] & sel;
-                    }
-                }
-                valid[w] = badbits == 0;
-                uni[w] = MODE == KM_LOCAL && chg == 0;
-                if (valid[w]) key[w] = plane_bits(p0buf, off, k) | (plane_bits(p1buf, off, k) << 32);
+                valid[w] = plane_bits2(mbuf, off, k) == 0;  // no bad base in [off, off + k)
+                // quality changes at bases off + 1 .. off + k - 1
+                uni[w] = MODE == KM_LOCAL && plane_bits2(dbuf, off + 1u, k - 1u) == 0;
+                if (valid[w]) key[w] = plane_bits2(p0buf, off, k) | (plane_bits2(p1buf, off, k) << 32);
             }
             if (CK) {
                 bk[w] = valid[w] ? kt8_bucket(key[w], (uint32_t)I.kt_bmask) : 0u;
