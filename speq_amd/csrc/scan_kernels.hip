@@ -478,7 +478,7 @@ __device__ __forceinline__ uint64_t kt_code(uint64_t key, uint32_t k) {
 }
 
 // ---- compact k-mer table (k <= KT8_MAX_K): 64-B buckets of eight 8-B slots ----
-// slot = ck | payload << 2k with ck = plane0 | plane1 << k (the window's two bit planes, k bits each); payload = the
+// slot = ck << (64 - 2k) | payload with ck = plane0 | plane1 << k (the window's two bit planes, k bits each); payload = the
 // group id, or (1 << (pb - 1)) | m for a k-mer whose occurrences span >= 2 groups, m indexing kt_multi[] = {lo, hi}
 // (read by EM scans only); pb = 64 - 2k >= 18 bits. All-ones = empty (no valid payload is all ones). Any bucket count
 // nb (bucket = mulhi(hash, nb)), so the table is sized for a load of exactly 1/2: 4.6 MB at cfg 2 against 16 MB for
@@ -1225,22 +1225,21 @@ void k_scan_kt(DevView I, UnitSrc src, unsigned long long* __restrict__ out_a, d
                 if (!pend[w]) continue;
                 bool empty = false, found = false;
                 if (CK) {
-                    const uint32_t kb = 2u * k;
-                    const uint64_t kmask = (1ull << kb) - 1ull;
-                    uint64_t hitv = 0;
+                    // Slots fill a bucket in order (k_ktab_fill8), so the first slot whose key bits match is the
+                    // k-mer's or (the all-T k-mer only) the first empty one, and the bucket has an empty slot iff
+                    // its last slot is empty: one shift + compare + select per slot.
+                    const uint32_t pbits = 64u - 2u * k;
+                    uint64_t hitv = ~0ull;
 #pragma unroll
-                    for (int j = 0; j < 8; ++j) {
+                    for (int j = 7; j >= 0; --j) {
                         const uint64_t v = (uint64_t)sl[w][j >> 1][2 * (j & 1)] |
                                            ((uint64_t)sl[w][j >> 1][2 * (j & 1) + 1] << 32);
-                        const bool e = v == ~0ull;
-                        const bool hit = !e && (v & kmask) == key[w];
-                        hitv = hit ? v : hitv;
-                        found |= hit;
-                        empty |= e;
+                        hitv = (v >> pbits) == key[w] ? v : hitv;
                     }
+                    found = hitv != ~0ull;
+                    empty = sl[w][3][2] == 0xFFFFFFFFu && sl[w][3][3] == 0xFFFFFFFFu;
                     if (found) {
-                        const uint32_t pbits = 64u - kb;
-                        const uint64_t pl = hitv >> kb;
+                        const uint64_t pl = hitv & ((1ull << pbits) - 1ull);
                         const bool multi = (pl >> (pbits - 1u)) != 0u;
                         which[w] = multi ? -2 : (int)pl;
                         if (EM && multi) {
@@ -1252,14 +1251,16 @@ void k_scan_kt(DevView I, UnitSrc src, unsigned long long* __restrict__ out_a, d
                 } else {
                     const uint32_t kl = (uint32_t)key[w], kh = (uint32_t)(key[w] >> 32);
                     uint32_t lo = 0, info = 0;
+                    // key planes are < 2^31, so no key matches an empty slot; slots fill in order (k_ktab_fill),
+                    // so the bucket has an empty slot iff its last one is empty
 #pragma unroll
                     for (int j = 0; j < (int)KT_BSLOTS; ++j) {
                         const bool hit = sl[w][j][0] == kl && sl[w][j][1] == kh;
                         lo = hit ? sl[w][j][2] : lo;
                         info = hit ? sl[w][j][3] : info;
                         found |= hit;
-                        empty |= sl[w][j][0] == 0xFFFFFFFFu && sl[w][j][1] == 0xFFFFFFFFu;
                     }
+                    empty = sl[w][KT_BSLOTS - 1][0] == 0xFFFFFFFFu && sl[w][KT_BSLOTS - 1][1] == 0xFFFFFFFFu;
                     if (found) {
                         const bool multi = (info >> 31) != 0u;
                         which[w] = multi ? -2 : (int)info;
@@ -1514,7 +1515,7 @@ __global__ void k_ktab_fill8(DevView I, const unsigned long long* __restrict__ k
         } else {
             pl = (uint64_t)out[0];
         }
-        const unsigned long long v = kt8_ck(key, k) | (pl << kb);
+        const unsigned long long v = (kt8_ck(key, k) << pbits) | pl;
         uint32_t b = kt8_bucket(key, nb);
         for (bool placed = false; !placed; b = (b + 1u == nb) ? 0u : b + 1u)
             for (uint32_t j = 0; j < 8u && !placed; ++j)
