@@ -563,7 +563,10 @@ __global__ __launch_bounds__(BLOCK_THREADS, (KT && NWIN == 1 && MODE == KM_GLOBA
     // out_b: ref -> Tot_ref[G];  out_w: local -> W[G]
     // A pass covers 64 * NWIN consecutive windows of the wave's stream: slot j = lane + 64 * w.
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    const uint32_t lane = threadIdx.x & 63u, wid = threadIdx.x >> 6;
+    const uint32_t lane = threadIdx.x & 63u;
+    // the wave index is uniform: in an SGPR, so the wave's unit range, cursor and carried unit stay scalar and the
+    // branches on them are uniform (no exec-mask bookkeeping)
+    const uint32_t wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t G = I.G, k = src.k;
     const uint32_t hist_words = LDS_HIST ? ((MODE == KM_GLOBAL) ? G : 2u * G) : 0u;
     const uint32_t hist_bytes = (hist_words * 8u + 15u) & ~15u;
@@ -1062,7 +1065,10 @@ template <int MODE, bool PAIRED, bool LDS_HIST, bool EM, int NW, bool CK>
 __global__ __launch_bounds__(BLOCK_THREADS, SPEQ_KTP_MIN_WAVES)
 void k_scan_kt(DevView I, UnitSrc src, unsigned long long* __restrict__ out_a, double* __restrict__ out_w) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    const uint32_t lane = threadIdx.x & 63u, wid = threadIdx.x >> 6;
+    const uint32_t lane = threadIdx.x & 63u;
+    // the wave index is uniform: in an SGPR, so the wave's unit range, cursor and carried unit stay scalar and the
+    // branches on them are uniform (no exec-mask bookkeeping)
+    const uint32_t wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t G = I.G, k = src.k;
     const uint32_t hist_words = LDS_HIST ? ((MODE == KM_GLOBAL) ? G : 2u * G) : 0u;
     const uint32_t hist_bytes = (hist_words * 8u + 15u) & ~15u;
