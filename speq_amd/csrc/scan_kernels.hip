@@ -315,8 +315,11 @@ __device__ __forceinline__ int search_lds(const DevView& I, const Rsrc& R, const
 }
 
 __device__ __forceinline__ uint32_t ascii_sym(uint32_t ch) {  // dna5: A C G T/U -> 0..3, else N (4)
-    ch |= 0x20u;
-    return ch == 'a' ? 0u : ch == 'c' ? 1u : ch == 'g' ? 2u : (ch == 't' || ch == 'u') ? 3u : 4u;
+    // branch-free: ((x >> 1) ^ (x >> 2)) & 3 is 0 1 2 3 3 for a c g t u, and bits 0 2 6 19 20 of 0x180045 mark those
+    // five letters at x - 'a' (any case; x = ch | 0x20)
+    const uint32_t x = ch | 0x20u, d = x - 0x61u;
+    const bool ok = d < 32u && ((0x180045u >> (d & 31u)) & 1u) != 0u;
+    return ok ? (((x >> 1) ^ (x >> 2)) & 3u) : 4u;
 }
 
 template <typename T>
@@ -1009,15 +1012,15 @@ __device__ __forceinline__ void kt_stage_chunk(const UnitSrc& src, uint32_t ch, 
                                                uint32_t span, unsigned char* qbuf, unsigned long long* mbuf,
                                                unsigned long long* p0buf, unsigned long long* p1buf,
                                                unsigned long long* dbuf, uint32_t& qprev, uint32_t j) {
-    uint32_t bad = 1, sym = 0;
-    int q = 0;
-    if (p < span) {
-        sym = ascii_sym(ch);
-        q = (int)qv - 33;
-        q = q < 0 ? 0 : (q > 41 ? 41 : q);
-        bad = ((uint32_t)q <= src.cutoff || sym == 4u) ? 1u : 0u;
-        if (MODE == KM_LOCAL) qbuf[p] = (unsigned char)q;
-    }
+    // branch-free (the loads were clamped into the pass, so ch and qv are defined for every lane)
+    const bool in = p < span;
+    const uint32_t s5 = ascii_sym(ch);
+    int q = (int)qv - 33;
+    q = q < 0 ? 0 : (q > 41 ? 41 : q);
+    const uint32_t sym = in ? s5 : 0u;
+    const uint32_t bad = (!in || (uint32_t)q <= src.cutoff || s5 == 4u) ? 1u : 0u;
+    if (!in) q = 0;
+    if (MODE == KM_LOCAL && in) qbuf[p] = (unsigned char)q;
     const uint64_t m = __ballot(bad != 0u);
     const uint64_t b0 = __ballot((sym & 1u) != 0u), b1 = __ballot((sym & 2u) != 0u);
     uint64_t dm = 0;
