@@ -230,7 +230,8 @@ def main():
                             f"{c['length']} bp, {n_reads} x 150 bp {'pairs' if paired else 'reads'} per GPU, k={k}",
                 "k": k, "reads_per_gpu": n_reads, "paired": paired, "mode": a.mode, "prefix_q": a.prefix_q, "prefix_q_used": q_used, "pair_steps": a.pair_steps, "triple_steps": a.triple_steps, "label_table": int(idx.info().label_table), "ilp": ilp,
                 "blocks_per_cu": dev.tuning("blocks_per_cu"), "grid_blocks": dev.tuning("grid_blocks"),
-                "ilp_kt": dev.tuning("ilp_kt"), "kt_slots": dev.tuning("kt_slots"),
+                "ilp_kt": dev.tuning("ilp_kt") or (1 if k <= 23 and dev.tuning("kt_compact") else 2),
+                "kt_slots": dev.tuning("kt_slots"),
                 "kmers_per_step_per_gpu": kmers_per_step, "parallelism": f"dp{world} (reads sharded, index replicated)",
                 "index_build_s": round(build_s, 3), "index_builder": "gpu" if a.gpu_build else "host", "fm_text_len": int(idx.info().n),
                 "kmer_table": {"on": bool(ktab["table_bytes"]), "distinct_kmers": ktab["distinct_kmers"],

@@ -283,7 +283,8 @@ void speq_groupings_free(speq_groupings* g);
  * "kt_compact"   : 1 (default) 8-B-slot tables for k <= 23 (0: 16-B slots); "kt_load8": their load factor in percent
  *                  (default 25); "kt_slots": 16-B slots per distinct k-mer of the wide form (default 2). These apply to
  *                  tables built afterwards;
- * "ilp_kt"       : windows per lane of table scans, 1 (default) or 2 (pipelined kernel), 4 (k_scan);
+ * "ilp_kt"       : windows per lane of table scans, 1 or 2 (pipelined kernel), 4 (k_scan); 0 (default) = 1 for
+ *                  compact tables (k <= 23), 2 for 16-B-slot tables;
  *                  "kt_pipeline": 1 (default) the software-pipelined table kernel k_scan_kt, 0 k_scan;
  *                  "blocks_per_cu_kt": blocks_per_cu of table scans (default 0: no cap);
  * "stream_lanes" : compute streams of a pipeline created afterwards (speq_pipeline_create, speq_scan_fastq, host

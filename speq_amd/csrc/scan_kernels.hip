@@ -1586,7 +1586,8 @@ struct speq_device_index {
     int prefix_choice = -1;       // tuning "prefix_level": -1 = by k (view_for_k), 0..2 = force q - level
     uint32_t base_q = 0;          // the index's prefix_q
     bool kmer_table = true;       // tuning "kmer_table": scans of k <= 31 look windows up in a per-k k-mer table
-    uint32_t ilp_kt = 1;          // tuning "ilp_kt": windows per lane of k-mer-table scans (1, 2 or 4)
+    uint32_t ilp_kt = 0;          // tuning "ilp_kt": windows per lane of k-mer-table scans (1, 2 or 4; 0 = auto:
+                                  // 1 for compact tables, 2 for 16-B-slot tables, profiles/r01/ab_notes.txt)
     uint32_t blocks_per_cu_kt = 0;  // tuning "blocks_per_cu_kt": blocks_per_cu of k-mer-table scans (default: no cap)
     uint32_t grid_blocks_kt = 8192;  // tuning "grid_blocks_kt": grid cap of k-mer-table scans (cfg 2: 8192 +4.6 % over
                                      // 16384; fewer is slower: sweep_kt_grid.txt)
@@ -1855,7 +1856,8 @@ void launch_kt(const DevView& v, const UnitSrc& src, uint32_t grid, size_t lds, 
 template <int MODE, bool PAIRED, bool LDS, bool KT>
 void launch_v(const speq_device_index* d, const DevView& v, const UnitSrc& src, uint32_t grid, size_t lds,
               hipStream_t st, unsigned long long* a, unsigned long long* b, double* w) {
-    const uint32_t ilp = KT ? d->ilp_kt : (MODE == KM_LOCAL ? d->ilp_local : d->ilp);
+    const uint32_t ilp = KT ? (d->ilp_kt ? d->ilp_kt : (v.kt_compact ? 1u : 2u))
+                            : (MODE == KM_LOCAL ? d->ilp_local : d->ilp);
     if constexpr (KT && MODE != KM_REF) {
         if (ilp <= 2 && d->kt_pipeline) {  // software-pipelined table scan
             if (v.kt_compact) launch_kt<MODE, PAIRED, LDS, true>(v, src, grid, lds, st, a, w, ilp);
@@ -1953,7 +1955,7 @@ static void scan_device_impl(speq_device_index* d, const uint8_t* d_seq, const u
     src.end_adj = 0;
     src.k = p->k;
     src.cutoff = p->phred_cutoff;
-    src.buf_bytes = staging_bytes(p->k, std::max({d->ilp, d->ilp_local, d->ilp_kt}));
+    src.buf_bytes = staging_bytes(p->k, std::max({d->ilp, d->ilp_local, d->ilp_kt ? d->ilp_kt : 2u}));
     const int mode = p->mode == SPEQ_MODE_LOCAL ? KM_LOCAL : KM_GLOBAL;
     hipEvent_t e0 = nullptr, e1 = nullptr;
     if (d->timing) {
@@ -2243,7 +2245,7 @@ uint64_t* launch_ref_shard(speq_device_index* d, uint32_t k, uint32_t shard, uin
     src.win_base = w0;
     src.end_adj = 1;
     src.k = k;
-    src.buf_bytes = staging_bytes(k, std::max(d->ilp, d->ilp_kt));
+    src.buf_bytes = staging_bytes(k, std::max(d->ilp, d->ilp_kt ? d->ilp_kt : 2u));
     launch_scan(d, KM_REF, false, src, (w1 - w0 + 255) / 256, st, reinterpret_cast<unsigned long long*>(d_u_ref),
                 reinterpret_cast<unsigned long long*>(d_tot_ref), nullptr);
     return d_cum;
@@ -2386,7 +2388,8 @@ int speq_device_set_tuning(speq_device_index* d, const char* key, int64_t value)
             if (value != 0 && value != 1) throw std::invalid_argument("kt_pipeline must be 0 or 1");
             d->kt_pipeline = value != 0;
         } else if (k == "ilp_kt") {
-            if (value != 1 && value != 2 && value != 4) throw std::invalid_argument("ilp_kt must be 1, 2 or 4");
+            if (value != 0 && value != 1 && value != 2 && value != 4)
+                throw std::invalid_argument("ilp_kt must be 0 (auto), 1, 2 or 4");
             d->ilp_kt = (uint32_t)value;
         } else if (k == "kt_compact") {
             if (value != 0 && value != 1) throw std::invalid_argument("kt_compact must be 0 or 1");

@@ -97,7 +97,7 @@ def test_absent_kmers_and_oracle():
         assert r.total == 2 * n * (L - k + 1)
 
 
-@pytest.mark.parametrize("ilp_kt", [1, 2, 4])
+@pytest.mark.parametrize("ilp_kt", [0, 1, 2, 4])
 @pytest.mark.parametrize("kt_slots", [2, 5, 16])
 def test_launch_knobs_keep_results(small, ilp_kt, kt_slots):
     ref, idx = small
