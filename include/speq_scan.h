@@ -281,7 +281,7 @@ void speq_groupings_free(speq_groupings* g);
  *                  for k (built by the first scan with that k, or by speq_device_prepare); 0 searches every window
  *                  with LF steps. Results are identical;
  * "kt_compact"   : 1 (default) 8-B-slot tables for k <= 23 (0: 16-B slots); "kt_load8": their load factor in percent
- *                  (default 25); "kt_slots": 16-B slots per distinct k-mer of the wide form (default 2). These apply to
+ *                  (default 35); "kt_slots": 16-B slots per distinct k-mer of the wide form (default 2). These apply to
  *                  tables built afterwards;
  * "ilp_kt"       : windows per lane of table scans, 1 or 2 (pipelined kernel), 4 (k_scan); 0 (default) = 1 for
  *                  compact tables (k <= 23), 2 for 16-B-slot tables;

@@ -1593,7 +1593,8 @@ struct speq_device_index {
                                      // 16384; fewer is slower: sweep_kt_grid.txt)
     bool kt_pipeline = true;        // tuning "kt_pipeline": k_scan_kt (software-pipelined) for ilp_kt <= 2 read scans
     bool kt_compact = true;       // tuning "kt_compact": 8-B-slot tables for k <= 23 (smaller, mostly L2-resident)
-    uint32_t kt_load8 = 25;       // tuning "kt_load8": load factor of compact tables, percent (20-35 within 1 %)
+    uint32_t kt_load8 = 35;       // tuning "kt_load8": load factor of compact tables, percent (35-42 best at cfg 2,
+                                  // sweep_kt_load8_sgpr.jsonl)
     uint32_t kt_slots = 2;        // tuning "kt_slots": table slots per distinct k-mer (load factor 1/kt_slots .. 2/kt_slots)
     struct KmerTable {
         uint4* table = nullptr;
