@@ -25,7 +25,14 @@ LIB_OBJS := $(patsubst speq_amd/csrc/%.hip,$(OBJDIR)/%.o,$(LIB_HIP)) \
             $(patsubst speq_amd/csrc/%.cpp,$(OBJDIR)/%.o,$(LIB_CPP))
 HDRS     := include/speq_scan.h $(wildcard speq_amd/csrc/*.hpp)
 
-all: $(LIB) $(CLI) oracle
+SYNTH    := tools/build/libsynth_gen.so
+
+all: $(LIB) $(CLI) oracle $(SYNTH)
+
+# synthetic-input generator for bench.py / tests (makes inputs, computes no counts)
+$(SYNTH): tools/synth_gen.c
+	@mkdir -p tools/build
+	$(CC) -O2 -fopenmp -fPIC -shared -Wall -Wextra -o $@ $<
 
 $(OBJDIR)/%.o: speq_amd/csrc/%.hip $(HDRS)
 	@mkdir -p $(OBJDIR)
@@ -60,7 +67,7 @@ variant: $(filter-out $(OBJDIR)/scan_kernels.o,$(LIB_OBJS))
 	    build/variants/$(NAME)/scan_kernels.o $^ -L/opt/rocm/lib -lamdhip64 -lz -lpthread -ldl -Wl,-rpath,/opt/rocm/lib
 
 clean:
-	rm -rf build bin $(LIB)
+	rm -rf build bin $(LIB) tools/build
 	$(MAKE) -C oracle clean
 
 .PHONY: all oracle clean variant

@@ -1,10 +1,14 @@
 #!/usr/bin/env python3
 """bench.py — k-mers scanned/sec of the MI355X SPeQ scan path (BASELINE.json `metric`).
 
-One "step" = one pass of the hot path (exact FM-index backward search of every k-mer window + unique-to-one-group
-tally) over this rank's batch of synthetic 150-bp reads already resident in HBM, followed by the RCCL
-all-reduce of the G+2 counters (N > 1). Default workload = BASELINE config 2 (10 variants x 50 kb, 1M reads per
-GPU, k = 21). Weak scaling: every rank scans its own 1M-read shard of the deterministic read stream.
+One "step" = one pass of the hot path (exact search of every k-mer window + unique-to-one-group tally) over this
+rank's batch of synthetic 150-bp reads already resident in HBM, followed by the RCCL all-reduce of the G+2
+counters (N > 1). Default workload = BASELINE config 2 (10 variants x 50 kb, 1M reads per GPU, k = 21, global
+mode) -> `value`. The same run also measures, as secondary lines in the same JSON object:
+  * "local_mode": config 2 in the reference's default Phred-weighted mode (fixed_accuracy 0, arg_parse.h:23);
+  * "k31": BASELINE config 3 (50 variants x 3 isolates, k = 31) at its full 10 M reads per GPU — at N = 8 the
+    per-rank shard of config 4 (100 M reads over 8 GPUs, 12.5 M each).
+Weak scaling: every rank scans its own shard of the deterministic read stream.
 
 Launch: python bench.py [--gpus 1 --steps K --warmup W]; for N > 1 the driver uses torch.distributed.run.
 Prints ONE JSON line on rank 0.
@@ -31,244 +35,45 @@ def parse_args():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=20)
     p.add_argument("--warmup", type=int, default=2)
-    p.add_argument("--config", type=int, default=2, help="BASELINE.json config number (1-5)")
+    p.add_argument("--config", type=int, default=2, help="BASELINE.json config number (1-5) of the headline")
     p.add_argument("--reads", type=int, default=0, help="override reads per GPU")
     p.add_argument("--k", type=int, default=0, help="override k")
     p.add_argument("--prefix-q", type=int, default=12)
     p.add_argument("--pair-steps", type=int, default=1)
     p.add_argument("--label-table", default="auto", help="auto|0|1 (auto: only for >= 4 M-symbol indexes)")
     p.add_argument("--mode", choices=["global", "local"], default="global")
-    p.add_argument("--ilp", type=int, default=0, help="windows per lane (1|2; 0 = the device default)")
+    p.add_argument("--ilp", type=int, default=0, help="windows per lane of the LF-step kernel (1|2; 0 = default)")
     p.add_argument("--gpu-build", type=int, default=1, help="build the index on the GPU (1) or host SA-IS (0)")
     p.add_argument("--triple-steps", type=int, default=1, help="three-symbol occ planes (1) or not (0)")
     p.add_argument("--kmer-table", type=int, default=1,
-                   help="k-mer interval table for k <= 31 (1, default) or LF steps for every window (0)")
+                   help="per-k interval table (1, default) or LF steps for every window (0)")
     p.add_argument("--tune", action="append", default=[],
                    help="extra launch tuning key=value (speq_device_set_tuning), e.g. ilp_kt=2; repeatable")
     p.add_argument("--no-lf-compare", action="store_true",
-                   help="skip timing the LF-step kernel beside the k-mer-table kernel")
+                   help="skip timing the LF-step kernel beside the table kernel")
+    p.add_argument("--no-extra", action="store_true", help="skip the local-mode and k=31 secondary lines")
+    p.add_argument("--k31-reads", type=int, default=0, help="reads per GPU of the k=31 line (0 = config 3/4)")
     p.add_argument("--cpu-seconds", type=float, default=15.0, help="target CPU-baseline sample duration")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-pcie", action="store_true", help="skip the PCIe-inclusive host-buffer measurement")
     return p.parse_args()
 
 
-def main():
-    a = parse_args()
-    import torch
-    import torch.distributed as dist
-
-    from speq_amd import DeviceIndex, FmIndex, synth
-
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local_rank}"))
-    torch.cuda.set_device(local_rank)
-    dev_t = torch.device(f"cuda:{local_rank}")
-
-    c = dict(synth.CONFIGS[a.config])
-    k = a.k or c["k"]
-    n_reads = a.reads or (c["n_reads"] if a.config <= 3 else c["n_reads"] // 8)
-    paired = c["paired"]
-    G = c["n_variants"]
-
-    ref = synth.make_reference(c["n_variants"], c["n_isolates"], c["length"])
-    t0 = time.time()
-    idx = FmIndex.build(ref.records, ref.groups, G, prefix_q=a.prefix_q, pair_steps=bool(a.pair_steps),
-                        label_table="auto" if a.label_table == "auto" else bool(int(a.label_table)),
-                        threads=16, gpu_device=local_rank if a.gpu_build else None,
-                        triple_steps=bool(a.triple_steps))
-    build_s = time.time() - t0
-    dev = DeviceIndex(idx, local_rank)
-    if a.ilp:
-        dev.tune(ilp=a.ilp)
-    ilp = dev.tuning("ilp")
-    dev.tune(kmer_table=a.kmer_table)
-    for kv in a.tune:
-        key, val = kv.split("=")
-        dev.tune(**{key: int(val)})
-    ktab = dev.prepare(k)  # per-k index structure (like the .dat cache): built once, outside the timed region
-    # the q-mer table level the scan uses (view_for_k in scan_kernels.hip)
-    width = 3 if a.triple_steps else (2 if a.pair_steps else 1)
-    q_used = next((a.prefix_q - lv for lv in range(3)
-                   if a.prefix_q - lv >= 1 and a.prefix_q - lv <= k and (k - a.prefix_q + lv) % width == 0),
-                  a.prefix_q)
-
-    # this rank's shard of the deterministic read stream (pairs never split)
-    reads = synth.make_reads(ref, n_reads, start_index=rank * n_reads, paired=paired)
-    lens = np.diff(reads.offsets).astype(np.int64)
-    kmers_per_step = int(np.maximum(lens - k + 1, 0).sum())
-    read_bytes = int(reads.offsets[-1])  # bases per step (qualities: as many again)
-    d_seq = torch.from_numpy(reads.seq).to(dev_t)
-    d_qual = torch.from_numpy(reads.qual).to(dev_t)
-    d_off = torch.from_numpy(reads.offsets.astype(np.int64)).to(dev_t)
-    d_counts = torch.zeros(G + 2, dtype=torch.int64, device=dev_t)
-    d_w = torch.zeros(G, dtype=torch.float64, device=dev_t)
-    local = a.mode == "local"
-    stream = torch.cuda.current_stream(dev_t).cuda_stream
-
-    def step():
-        d_counts.zero_()
-        if local:
-            d_w.zero_()
-        dev.scan_device(d_seq.data_ptr(), d_qual.data_ptr(), d_off.data_ptr(), reads.n, k, d_counts.data_ptr(),
-                        d_w.data_ptr(), paired=paired, local=local, stream=stream)
-        if world > 1:
-            dist.all_reduce(d_counts)  # one RCCL all-reduce of the G+2 counters over xGMI
-            if local:
-                dist.all_reduce(d_w)
-
-    def timed_run(steps, warmup):
-        for _ in range(warmup):
-            step()
-        torch.cuda.synchronize()
-        if world > 1:
-            dist.barrier()
-        torch.cuda.synchronize()
-        dev.timing(True)
-        dev.timing_read()  # reset
-        t0 = time.perf_counter()
-        for _ in range(steps):
-            step()
-        torch.cuda.synchronize()
-        if world > 1:
-            dist.barrier()
-        elapsed = time.perf_counter() - t0
-        kernel_ms, launches = dev.timing_read()
-        dev.timing(False)
-        el = torch.tensor([elapsed], dtype=torch.float64, device=dev_t)
-        if world > 1:
-            dist.all_reduce(el, op=dist.ReduceOp.MAX)
-        return float(el.item()), kernel_ms, launches
-
-    elapsed, kernel_ms, launches = timed_run(a.steps, a.warmup)
-    counts = d_counts.cpu().numpy()
-    if ktab["table_bytes"] and dev.tuning("ilp_kt") <= 2 and dev.tuning("kt_pipeline") == 1:
-        kernel_name = "k_scan_kt (software-pipelined k-mer-table scan, speq_amd/csrc/scan_kernels.hip)"
-    elif ktab["table_bytes"]:
-        kernel_name = "k_scan<..., KT = true> (k-mer-table scan, speq_amd/csrc/scan_kernels.hip)"
-    else:
-        kernel_name = "k_scan<..., KT = false> (LF-step scan, speq_amd/csrc/scan_kernels.hip)"
-
-    # the LF-step kernel on the same reads (the k-mer table replaces its chain of LF steps; results are identical)
-    lf = None
-    if a.kmer_table and ktab["table_bytes"] and not a.no_lf_compare:
-        dev.tune(kmer_table=0)
-        lf_el, lf_ms, lf_n = timed_run(a.steps, 1)
-        lf_counts = d_counts.cpu().numpy()
-        dev.tune(kmer_table=1)
-        if not np.array_equal(lf_counts, counts):
-            raise RuntimeError("LF-step scan disagrees with the k-mer-table scan")
-        lf = {"value": kmers_per_step * world * a.steps / lf_el, "unit": "k-mers/s",
-              "avg_kernel_ms": lf_ms / max(1, lf_n),
-              "achieved_GBps": kmers_per_step * 2 * k * OCC_ENTRY_BYTES / (lf_ms / 1e3 / max(1, lf_n)) / 1e9,
-              "path": "k_scan<..., KT = false>: q-mer table + three-base LF steps + label-run classification per window"}
-
-    total_kmers = kmers_per_step * world * a.steps
-    value = total_kmers / elapsed
-    avg_kernel_s = (kernel_ms / 1e3) / max(1, launches)
-    algo_bytes_per_launch = kmers_per_step * 2 * k * OCC_ENTRY_BYTES
-    achieved_gbs = algo_bytes_per_launch / avg_kernel_s / 1e9
-
-    traffic = None
-    traffic_src = None
-    prof = os.path.join(ROOT, "profiles", "traffic.json")
-    if os.path.exists(prof):
-        try:
-            tj = json.load(open(prof))
-            lab = int(idx.info().label_table)
-            steps = "_tri1" if a.triple_steps else ""
-            kt = "_kt1" if ktab["table_bytes"] else ""
-            key = (f"cfg{a.config}_k{k}_q{a.prefix_q}_pairs{a.pair_steps}{steps}_lab{lab}_ilp{ilp}"
-                   f"_bpc{dev.tuning('blocks_per_cu')}_{a.mode}_reads{n_reads}{kt}")
-            if key in tj:
-                traffic = tj[key]["hbm_bytes_per_launch"]
-                traffic_src = tj[key]["source"]
-        except Exception:
-            traffic = None
-
-    # PCIe-inclusive rate (not `value`): the same reads from pageable host memory through the pinned-slot pipeline
-    # (speq_scan_reads: memcpy into pinned slots, H2D on a copy stream overlapped with k_scan).
-    pcie = None
-    if not a.no_pcie:
-        seq_b, qual_b = reads.seq.tobytes(), reads.qual.tobytes()
-        dev.scan(seq_b, qual_b, reads.offsets[:3], k=k, paired=paired, local=local)  # pipeline warm-up
-        best = None
-        for _ in range(3):
-            t0 = time.perf_counter()
-            r = dev.scan(seq_b, qual_b, reads.offsets, k=k, paired=paired, local=local)
-            dt = time.perf_counter() - t0
-            best = dt if best is None else min(best, dt)
-        if r.total != int(counts[0]) and world == 1:
-            raise RuntimeError("host-buffer scan disagrees with the HBM-resident scan")
-        pcie = {"value": kmers_per_step / best, "unit": "k-mers/s", "per_gpu": True,
-                "path": "speq_scan_reads: pageable host arrays -> pinned slots -> H2D (copy stream) || k_scan",
-                "host_GB_per_s": 2 * len(seq_b) / best / 1e9}
-
-    cpu = None
-    if rank == 0 and world == 1 and not a.no_cpu_baseline:
-        cpu = cpu_baseline(ref, reads, k, G, a.cpu_seconds, local, paired, idx)
-
-    if rank == 0:
-        out = {
-            "metric": "k-mers scanned/sec (whole node) at k=%d, 150 bp reads" % k,
-            "value": value,
-            "unit": "k-mers/s",
-            "n_gpus": world,
-            "steps": a.steps,
-            "warmup": a.warmup,
-            "ms_per_step": elapsed / a.steps * 1e3,
-            "higher_is_better": True,
-            "scaling": "weak",
-            "vs_baseline": None,
-            "dtype": "u32",
-            "data": "synthetic (splitmix64 references/reads, SURVEY.md §8(d))",
-            "config": {
-                "workload": f"BASELINE config {a.config}: {c['n_variants']} variants x {c['n_isolates']} isolates x "
-                            f"{c['length']} bp, {n_reads} x 150 bp {'pairs' if paired else 'reads'} per GPU, k={k}",
-                "k": k, "reads_per_gpu": n_reads, "paired": paired, "mode": a.mode, "prefix_q": a.prefix_q, "prefix_q_used": q_used, "pair_steps": a.pair_steps, "triple_steps": a.triple_steps, "label_table": int(idx.info().label_table), "ilp": ilp,
-                "blocks_per_cu": dev.tuning("blocks_per_cu"), "grid_blocks": dev.tuning("grid_blocks"),
-                "ilp_kt": dev.tuning("ilp_kt") or (1 if k <= 23 and dev.tuning("kt_compact") else 2),
-                "kt_slots": dev.tuning("kt_slots"),
-                "kmers_per_step_per_gpu": kmers_per_step, "parallelism": f"dp{world} (reads sharded, index replicated)",
-                "index_build_s": round(build_s, 3), "index_builder": "gpu" if a.gpu_build else "host", "fm_text_len": int(idx.info().n),
-                "kmer_table": {"on": bool(ktab["table_bytes"]), "distinct_kmers": ktab["distinct_kmers"],
-                               "bytes": ktab["table_bytes"], "build_s": round(ktab["build_ms"] / 1e3, 4)},
-            },
-            "roofline": {
-                "bound": "hbm", "achieved": achieved_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": achieved_gbs / HBM_PEAK_GBS, "traffic": traffic,
-                # measured L2->fabric bytes per launch over this run's launch time: the bandwidth the kernel really
-                # draws from Infinity Cache + HBM (an upper bound on HBM bytes), against the same 8 TB/s peak
-                "traffic_GBps": (traffic / avg_kernel_s / 1e9) if traffic else None,
-                "traffic_frac": (traffic / avg_kernel_s / 1e9 / HBM_PEAK_GBS) if traffic else None,
-                "kernel": kernel_name,
-                "algorithmic_bytes_per_kmer": 2 * k * OCC_ENTRY_BYTES,
-                "avg_kernel_ms": avg_kernel_s * 1e3, "launches_timed": launches,
-                "traffic_source": traffic_src,
-                # the table kernel's own bytes: one 64-B bucket per window plus the read bytes (bases + qualities)
-                "table_kernel_model": ({"bytes_per_kmer": round(64 + 2 * read_bytes / max(1, kmers_per_step), 3),
-                                        "achieved_GBps": kmers_per_step * (64 + 2 * read_bytes / max(1, kmers_per_step))
-                                        / avg_kernel_s / 1e9,
-                                        "frac": kmers_per_step * (64 + 2 * read_bytes / max(1, kmers_per_step))
-                                        / avg_kernel_s / 1e9 / HBM_PEAK_GBS}
-                                       if ktab["table_bytes"] else None),
-                "note": "achieved uses SURVEY.md 8(d)'s algorithmic 2*k*64 B per k-mer (k LF steps x 2 uncached "
-                        "64-B occ loads), fixed whatever the kernel does; the k-mer-table kernel reads one 64-B bucket "
-                        "per window instead (the LF-step kernel ~0.3 of the algorithmic gathers), mostly from "
-                        "L2/Infinity Cache, so frac > 1 means HBM does not bound this kernel; traffic = measured "
-                        "L2->fabric bytes per launch (DESIGN.md 6)",
-            },
-            "cpu_baseline": cpu,
-            "lf_steps": lf,
-            "pcie_inclusive": pcie,
-            "check": {"T": int(counts[0]), "ambiguous": int(counts[1]), "U": [int(x) for x in counts[2:]]},
-        }
-        print(json.dumps(out), flush=True)
-    if world > 1:
-        dist.destroy_process_group()
+def host_cpu_info() -> dict:
+    """The CPUs this process may use: affinity mask, machine count and the cgroup CPU quota (the GPU box gives
+    each job a share of a larger machine: its nproc shows every CPU, the quota says how many it may keep busy)."""
+    aff = len(os.sched_getaffinity(0))
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = int(q) / int(per)
+    except (OSError, ValueError):
+        pass
+    threads = aff if quota is None else max(1, min(aff, int(quota)))
+    return {"threads": threads, "affinity_cpus": aff, "nproc": os.cpu_count(), "cgroup_cpu_quota": quota,
+            "omp_num_threads_env": os.environ.get("OMP_NUM_THREADS"), "cpu_model": cpu_model(),
+            "rule": "threads = min(affinity CPUs, cgroup CPU quota) (all CPUs this job may keep busy)"}
 
 
 def cpu_model() -> str:
@@ -281,6 +86,270 @@ def cpu_model() -> str:
     return "unknown"
 
 
+class Ctx:
+    def __init__(self, a):
+        import torch
+        import torch.distributed as dist
+        self.torch, self.dist, self.a = torch, dist, a
+        self.world = int(os.environ.get("WORLD_SIZE", "1"))
+        self.rank = int(os.environ.get("RANK", "0"))
+        self.local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+        if self.world > 1:
+            dist.init_process_group("nccl", device_id=torch.device(f"cuda:{self.local_rank}"))
+        torch.cuda.set_device(self.local_rank)
+        self.dev_t = torch.device(f"cuda:{self.local_rank}")
+
+    def barrier(self):
+        if self.world > 1:
+            self.dist.barrier()
+
+    def allreduce_max(self, x: float) -> float:
+        t = self.torch.tensor([x], dtype=self.torch.float64, device=self.dev_t)
+        if self.world > 1:
+            self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
+        return float(t.item())
+
+
+def kernel_model(dev, k: int, table_on: bool, kmers: int, read_bytes: int) -> dict:
+    """The timed kernel and the bytes IT must move per k-mer window (its own roofline model).
+
+    Table path (k_scan_kt): one 64-B table bucket per window + the read bytes (bases + qualities).
+    LF-step path (k_scan): SURVEY.md 8(d)'s 2*k*64 B per window (k LF steps x 2 occ loads)."""
+    rb = 2.0 * read_bytes / max(1, kmers)
+    if table_on:
+        return {"kernel": "k_scan_kt (pipelined k-mer-table scan, speq_amd/csrc/scan_kernels.hip)",
+                "bytes_per_kmer": 64.0 + rb,
+                "model": "one 64-B table bucket per window + the read's bases and qualities"}
+    return {"kernel": "k_scan<..., KT = false> (LF-step scan, speq_amd/csrc/scan_kernels.hip)",
+            "bytes_per_kmer": float(2 * k * OCC_ENTRY_BYTES),
+            "model": "SURVEY.md 8(d): k LF steps x 2 occ-block loads x 64 B"}
+
+
+def traffic_lookup(cfg, k, q, pair_steps, triple, lab, ilp, bpc, mode, n_reads, kt, dev=None):
+    prof = os.path.join(ROOT, "profiles", "traffic.json")
+    if not os.path.exists(prof):
+        return None, None
+    try:
+        tj = json.load(open(prof))
+    except ValueError:
+        return None, None
+    steps = "_tri1" if triple else ""
+    key = (f"cfg{cfg}_k{k}_q{q}_pairs{pair_steps}{steps}_lab{lab}_ilp{ilp}_bpc{bpc}_{mode}_reads{n_reads}"
+           f"{'_kt1' if kt else ''}")
+    if key in tj:
+        return tj[key]["hbm_bytes_per_launch"], tj[key]["source"]
+    return None, None
+
+
+def run_workload(ctx: Ctx, cfg_no: int, k: int, n_reads: int, mode: str, steps: int, warmup: int,
+                 with_lf: bool, with_pcie: bool, with_cpu: bool, cpu_seconds: float, prepared=None) -> dict:
+    """Builds the index of BASELINE config `cfg_no` (or reuses `prepared`), stages this rank's reads in HBM, times
+    `steps` scans and returns the measurement (plus the objects for reuse)."""
+    torch, a = ctx.torch, ctx.a
+    from speq_amd import DeviceIndex, FmIndex, synth
+
+    c = dict(synth.CONFIGS[cfg_no])
+    paired, G = c["paired"], c["n_variants"]
+    if prepared is None:
+        ref = synth.make_reference(c["n_variants"], c["n_isolates"], c["length"])
+        t0 = time.time()
+        idx = FmIndex.build(ref.records, ref.groups, G, prefix_q=a.prefix_q, pair_steps=bool(a.pair_steps),
+                            label_table="auto" if a.label_table == "auto" else bool(int(a.label_table)),
+                            threads=16, gpu_device=ctx.local_rank if a.gpu_build else None,
+                            triple_steps=bool(a.triple_steps))
+        build_s = time.time() - t0
+        dev = DeviceIndex(idx, ctx.local_rank)
+        if a.ilp:
+            dev.tune(ilp=a.ilp)
+        dev.tune(kmer_table=a.kmer_table)
+        for kv in a.tune:
+            key, val = kv.split("=")
+            dev.tune(**{key: int(val)})
+        reads = synth.make_reads(ref, n_reads, start_index=ctx.rank * n_reads, paired=paired)
+        d_seq = torch.from_numpy(reads.seq).to(ctx.dev_t)
+        d_qual = torch.from_numpy(reads.qual).to(ctx.dev_t)
+        d_off = torch.from_numpy(reads.offsets.astype(np.int64)).to(ctx.dev_t)
+        prepared = dict(ref=ref, idx=idx, dev=dev, reads=reads, d_seq=d_seq, d_qual=d_qual, d_off=d_off,
+                        build_s=build_s)
+    ref, idx, dev, reads = prepared["ref"], prepared["idx"], prepared["dev"], prepared["reads"]
+    d_seq, d_qual, d_off = prepared["d_seq"], prepared["d_qual"], prepared["d_off"]
+    ktab = dev.prepare(k)  # per-k index structure (like the .dat cache): built once, outside the timed region
+    lens = np.diff(reads.offsets).astype(np.int64)
+    kmers_per_step = int(np.maximum(lens - k + 1, 0).sum())
+    read_bytes = int(reads.offsets[-1])
+    d_counts = torch.zeros(G + 2, dtype=torch.int64, device=ctx.dev_t)
+    d_w = torch.zeros(G, dtype=torch.float64, device=ctx.dev_t)
+    local = mode == "local"
+    stream = torch.cuda.current_stream(ctx.dev_t).cuda_stream
+
+    def step():
+        d_counts.zero_()
+        if local:
+            d_w.zero_()
+        dev.scan_device(d_seq.data_ptr(), d_qual.data_ptr(), d_off.data_ptr(), reads.n, k, d_counts.data_ptr(),
+                        d_w.data_ptr(), paired=paired, local=local, stream=stream)
+        if ctx.world > 1:
+            ctx.dist.all_reduce(d_counts)  # one RCCL all-reduce of the G+2 counters over xGMI
+            if local:
+                ctx.dist.all_reduce(d_w)
+
+    def timed_run(n_steps, n_warm):
+        for _ in range(n_warm):
+            step()
+        torch.cuda.synchronize()
+        ctx.barrier()
+        torch.cuda.synchronize()
+        dev.timing(True)
+        dev.timing_read()  # reset
+        t0 = time.perf_counter()
+        for _ in range(n_steps):
+            step()
+        torch.cuda.synchronize()
+        ctx.barrier()
+        elapsed = time.perf_counter() - t0
+        kernel_ms, launches = dev.timing_read()
+        dev.timing(False)
+        return ctx.allreduce_max(elapsed), kernel_ms, launches
+
+    elapsed, kernel_ms, launches = timed_run(steps, warmup)
+    counts = d_counts.cpu().numpy()
+    weights = d_w.cpu().numpy() if local else None
+    table_on = bool(ktab["table_bytes"])
+    km = kernel_model(dev, k, table_on, kmers_per_step, read_bytes)
+
+    lf = None
+    if with_lf and a.kmer_table and table_on:
+        dev.tune(kmer_table=0)
+        lf_el, lf_ms, lf_n = timed_run(steps, 1)
+        lf_counts = d_counts.cpu().numpy()
+        dev.tune(kmer_table=1)
+        if not np.array_equal(lf_counts, counts):
+            raise RuntimeError("LF-step scan disagrees with the k-mer-table scan")
+        lf = {"value": kmers_per_step * ctx.world * steps / lf_el, "unit": "k-mers/s",
+              "avg_kernel_ms": lf_ms / max(1, lf_n),
+              "achieved_GBps": kmers_per_step * 2 * k * OCC_ENTRY_BYTES / (lf_ms / 1e3 / max(1, lf_n)) / 1e9,
+              "path": "k_scan<..., KT = false>: q-mer table + three-base LF steps + label-run classification"}
+
+    total_kmers = kmers_per_step * ctx.world * steps
+    value = total_kmers / elapsed
+    avg_kernel_s = (kernel_ms / 1e3) / max(1, launches)
+    own_bytes = kmers_per_step * km["bytes_per_kmer"]
+    own_gbs = own_bytes / avg_kernel_s / 1e9
+    survey_gbs = kmers_per_step * 2 * k * OCC_ENTRY_BYTES / avg_kernel_s / 1e9
+    lab = int(idx.info().label_table)
+    traffic, traffic_src = traffic_lookup(cfg_no, k, a.prefix_q, a.pair_steps, a.triple_steps, lab,
+                                          dev.tuning("ilp"), dev.tuning("blocks_per_cu"), mode, n_reads, table_on)
+    roofline = {
+        "bound": "hbm", "achieved": own_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": own_gbs / HBM_PEAK_GBS,
+        "traffic": traffic,
+        "kernel": km["kernel"], "bytes_per_kmer": round(km["bytes_per_kmer"], 3), "bytes_model": km["model"],
+        "avg_kernel_ms": avg_kernel_s * 1e3, "launches_timed": launches,
+        # measured L2->fabric bytes per launch (rocprofv3 PMC, profiles/): what the kernel really draws from
+        # Infinity Cache + HBM, over this run's launch time, against the same 8 TB/s
+        "traffic_GBps": (traffic / avg_kernel_s / 1e9) if traffic else None,
+        "traffic_frac": (traffic / avg_kernel_s / 1e9 / HBM_PEAK_GBS) if traffic else None,
+        "traffic_source": traffic_src,
+        # SURVEY.md 8(d)'s fixed model (2*k*64 B per k-mer: k uncached LF steps) — not what this kernel moves
+        "survey_model_bytes_per_kmer": 2 * k * OCC_ENTRY_BYTES,
+        "survey_model_frac": survey_gbs / HBM_PEAK_GBS,
+    }
+
+    pcie = None
+    if with_pcie:
+        seq_b, qual_b = reads.seq.tobytes(), reads.qual.tobytes()
+        dev.scan(seq_b, qual_b, reads.offsets[:3], k=k, paired=paired, local=local)  # pipeline warm-up
+        best = None
+        for _ in range(3):
+            t0 = time.perf_counter()
+            r = dev.scan(seq_b, qual_b, reads.offsets, k=k, paired=paired, local=local)
+            dt = time.perf_counter() - t0
+            best = dt if best is None else min(best, dt)
+        if r.total != int(counts[0]) and ctx.world == 1:
+            raise RuntimeError("host-buffer scan disagrees with the HBM-resident scan")
+        pcie = {"value": kmers_per_step / best, "unit": "k-mers/s", "per_gpu": True,
+                "path": "speq_scan_reads: pageable host arrays -> pinned slots -> H2D (copy stream) || scan",
+                "host_GB_per_s": 2 * len(seq_b) / best / 1e9}
+
+    cpu = None
+    if with_cpu and ctx.rank == 0 and ctx.world == 1:
+        cpu = cpu_baseline(ref, reads, k, G, cpu_seconds, local, paired, idx)
+
+    out = {
+        "value": value, "ms_per_step": elapsed / steps * 1e3, "k": k, "mode": mode,
+        "workload": f"BASELINE config {cfg_no}: {c['n_variants']} variants x {c['n_isolates']} isolates x "
+                    f"{c['length']} bp, {n_reads} x 150 bp {'pairs' if paired else 'reads'} per GPU, k={k}, {mode}",
+        "reads_per_gpu": n_reads, "kmers_per_step_per_gpu": kmers_per_step, "paired": paired,
+        "index_build_s": round(prepared["build_s"], 3), "fm_text_len": int(idx.info().n),
+        "kmer_table": {"on": table_on, "distinct_kmers": ktab["distinct_kmers"], "bytes": ktab["table_bytes"],
+                       "build_s": round(ktab["build_ms"] / 1e3, 4)},
+        "roofline": roofline, "cpu_baseline": cpu, "lf_steps": lf, "pcie_inclusive": pcie,
+        "check": {"T": int(counts[0]), "ambiguous": int(counts[1]), "U": [int(x) for x in counts[2:]],
+                  **({"W_sum": float(weights.sum())} if weights is not None else {})},
+    }
+    return out, prepared
+
+
+def main():
+    a = parse_args()
+    ctx = Ctx(a)
+    from speq_amd import synth
+
+    c = dict(synth.CONFIGS[a.config])
+    k = a.k or c["k"]
+    n_reads = a.reads or (c["n_reads"] if a.config <= 3 else c["n_reads"] // 8)
+    head, prep = run_workload(ctx, a.config, k, n_reads, a.mode, a.steps, a.warmup, with_lf=not a.no_lf_compare,
+                              with_pcie=not a.no_pcie, with_cpu=not a.no_cpu_baseline, cpu_seconds=a.cpu_seconds)
+    dev = prep["dev"]
+    extra = {}
+    if not a.no_extra and a.config == 2 and not a.k and not a.reads:
+        other = "local" if a.mode == "global" else "global"
+        extra[f"{other}_mode"], _ = run_workload(ctx, 2, k, n_reads, other, a.steps, a.warmup, with_lf=False,
+                                                 with_pcie=False, with_cpu=False, cpu_seconds=0, prepared=prep)
+        n31 = a.k31_reads or (10_000_000 if ctx.world == 1 else synth.CONFIGS[4]["n_reads"] // 8)
+        extra["k31"], p31 = run_workload(ctx, 3, 31, n31, "global", max(3, a.steps // 4), max(1, a.warmup // 2),
+                                         with_lf=False, with_pcie=False, with_cpu=not a.no_cpu_baseline,
+                                         cpu_seconds=a.cpu_seconds)
+        extra["k31"]["note"] = ("config 3 (10 M reads on one GPU); with 8 ranks each scans config 4's 12.5 M-read "
+                                "shard of the same index")
+        p31["dev"].close()
+
+    if ctx.rank == 0:
+        out = {
+            "metric": "k-mers scanned/sec (whole node) at k=%d, 150 bp reads" % k,
+            "value": head["value"],
+            "unit": "k-mers/s",
+            "n_gpus": ctx.world,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": head["ms_per_step"],
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u32",
+            "data": "synthetic (splitmix64 references/reads, SURVEY.md §8(d))",
+            "config": {
+                "workload": head["workload"],
+                "k": k, "reads_per_gpu": n_reads, "paired": head["paired"], "mode": a.mode,
+                "prefix_q": a.prefix_q, "pair_steps": a.pair_steps, "triple_steps": a.triple_steps,
+                "label_table": int(prep["idx"].info().label_table),
+                "blocks_per_cu": dev.tuning("blocks_per_cu"), "grid_blocks": dev.tuning("grid_blocks"),
+                "kmers_per_step_per_gpu": head["kmers_per_step_per_gpu"],
+                "parallelism": f"dp{ctx.world} (reads sharded, index replicated)",
+                "index_build_s": head["index_build_s"], "index_builder": "gpu" if a.gpu_build else "host",
+                "fm_text_len": head["fm_text_len"], "kmer_table": head["kmer_table"],
+            },
+            "roofline": head["roofline"],
+            "cpu_baseline": head["cpu_baseline"],
+            "lf_steps": head["lf_steps"],
+            "pcie_inclusive": head["pcie_inclusive"],
+            "check": head["check"],
+            **extra,
+        }
+        print(json.dumps(out), flush=True)
+    if ctx.world > 1:
+        ctx.dist.destroy_process_group()
+
+
 def cpu_baseline(ref, reads, k, G, target_s, local, paired=False, idx=None):
     """CPU baselines on this host's cores over a bounded sample of the same reads (rank 0, N = 1 only).
 
@@ -289,8 +358,8 @@ def cpu_baseline(ref, reads, k, G, target_s, local, paired=False, idx=None):
     the SeqAn3 binary, which cannot be built here (8(c)). "hash_port" beside it: oracle/kmer_oracle.c, a hash-map
     restatement of the same semantics (no FM-index, no locate) — an upper bound for any CPU port."""
     from oracle.oracle import Oracle, SeqanLike
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or (os.cpu_count() or 1)
-    threads = max(1, min(threads, 16))
+    hw = host_cpu_info()
+    threads = hw["threads"]
     t0 = time.perf_counter()
     sl = SeqanLike(ref.records, ref.groups, G)
     sl_build = time.perf_counter() - t0
@@ -325,7 +394,7 @@ def cpu_baseline(ref, reads, k, G, target_s, local, paired=False, idx=None):
     hv, hn, hreps, hkm, ht = timed(lambda s, q, o: orc.scan(s, q, o, paired=paired, local=local, threads=threads),
                                    target_s / 3)
     lr = None
-    if idx is not None and k <= 32 and not local:  # the build's own algorithm on CPU cores (oracle/fm_cpu.c), global mode
+    if idx is not None and k <= 32 and not local:  # the build's own algorithm on CPU cores (oracle/fm_cpu.c)
         from oracle.oracle import FmCpu
         fc = FmCpu(idx)
         lv, ln, lreps, lkm, lt = timed(lambda s, q, o: fc.scan(s, q, o, k=k, paired=paired, threads=threads),
@@ -339,7 +408,7 @@ def cpu_baseline(ref, reads, k, G, target_s, local, paired=False, idx=None):
                       f"oracle/seqan_like.c: the reference algorithm (wavelet backward search + SA-sample-16 locate "
                       f"of every hit + sorted hit list + first-hit rule; index build {sl_build:.1f} s not timed); "
                       f"the SeqAn3 binary cannot be built here (SURVEY.md 8(c))",
-            "cpu_model": cpu_model(),
+            "host": hw,
             "label_run_port": lr,
             "hash_port": {"value": hv, "unit": "k-mers/s", "cores": threads,
                           "sample": f"first {hn} {unit} x {hreps} passes ({hkm} k-mers, {ht:.1f} s), "

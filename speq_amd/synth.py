@@ -13,6 +13,8 @@ low-quality bases and short reads on request.
 """
 from __future__ import annotations
 
+import ctypes as C
+import os
 from dataclasses import dataclass
 
 import numpy as np
@@ -122,6 +124,10 @@ def make_reads(ref: Reference, n_reads: int, read_len: int = 150, start_index: i
 
     paired=True returns 2*n_reads records (mate 1 = forward first read_len of a fragment, mate 2 = reverse
     complement of its last read_len), interleaved as (2i, 2i+1). Generated in chunks to bound memory."""
+    fast = _make_reads_native(ref, n_reads, read_len, start_index, err_rate, n_rate, lowq_rate, short_frac, paired,
+                              fragment)
+    if fast is not None:
+        return fast
     parts = []
     for c0 in range(0, n_reads, chunk):
         c1 = min(n_reads, c0 + chunk)
@@ -190,6 +196,50 @@ def _make_reads_chunk(ref: Reference, n_reads: int, read_len: int, start_index: 
     off = np.zeros(nrec + 1, dtype=np.uint64)
     off[1:] = np.cumsum(lens, dtype=np.uint64)
     return Reads(np.ascontiguousarray(seq_flat), np.ascontiguousarray(qual_flat), off, tv)
+
+
+_SYNTH_LIB = None
+_SYNTH_PATH = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools", "build",
+                           "libsynth_gen.so")
+
+
+def _synth_lib():
+    """tools/synth_gen.c (multithreaded, byte-identical to _make_reads_chunk), or None when it is not built."""
+    global _SYNTH_LIB
+    if _SYNTH_LIB is None:
+        if os.environ.get("SPEQ_SYNTH_NUMPY") == "1" or not os.path.exists(_SYNTH_PATH):
+            return None
+        L = C.CDLL(_SYNTH_PATH)
+        L.synth_reads.restype = C.c_int
+        L.synth_reads.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint64, C.c_uint64, C.c_uint32, C.c_uint64,
+                                  C.c_double, C.c_double, C.c_double, C.c_double, C.c_int, C.c_uint32, C.c_void_p,
+                                  C.c_void_p, C.c_void_p, C.c_void_p]
+        _SYNTH_LIB = L
+    return _SYNTH_LIB
+
+
+def _make_reads_native(ref, n_reads, read_len, start_index, err_rate, n_rate, lowq_rate, short_frac, paired,
+                       fragment):
+    L = _synth_lib()
+    if L is None or n_reads == 0:
+        return None
+    genomes = np.ascontiguousarray(_genome_matrix(ref))
+    nrec = 2 * n_reads if paired else n_reads
+    seq = np.empty(nrec * read_len, dtype=np.uint8)
+    qual = np.empty(nrec * read_len, dtype=np.uint8)
+    lens = np.empty(nrec, dtype=np.int64)
+    var = np.empty(nrec, dtype=np.int32)
+    rc = L.synth_reads(genomes.ctypes.data, ref.n_variants, ref.n_isolates, ref.length, n_reads, read_len,
+                       start_index, err_rate, n_rate, lowq_rate, short_frac, int(paired), fragment, seq.ctypes.data,
+                       qual.ctypes.data, lens.ctypes.data, var.ctypes.data)
+    if rc != 0:
+        raise ValueError("reads longer than the reference records")
+    if short_frac > 0:
+        keep = (np.arange(read_len)[None, :] < lens[:, None]).reshape(-1)
+        seq, qual = seq[keep], qual[keep]
+    off = np.zeros(nrec + 1, dtype=np.uint64)
+    off[1:] = np.cumsum(lens, dtype=np.uint64)
+    return Reads(seq, qual, off, var)
 
 
 _GENOME_CACHE: dict = {}
