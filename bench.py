@@ -110,12 +110,19 @@ class Ctx:
         return float(t.item())
 
 
-def kernel_model(dev, k: int, table_on: bool, kmers: int, read_bytes: int) -> dict:
+def kernel_model(dev, k: int, table_on: bool, kmers: int, read_bytes: int, n_reads: int = 0) -> dict:
     """The timed kernel and the bytes IT must move per k-mer window (its own roofline model).
 
+    Anchor-and-extend path (k_scan_ax): the read bytes (bases + qualities), one 4-B class per window, the 2-bit text
+    its runs compare (k - 1 + 32 bases per run of 32 windows) and at least one 64-B anchor bucket per read.
     Table path (k_scan_kt): one 64-B table bucket per window + the read bytes (bases + qualities).
     LF-step path (k_scan): SURVEY.md 8(d)'s 2*k*64 B per window (k LF steps x 2 occ loads)."""
     rb = 2.0 * read_bytes / max(1, kmers)
+    if dev.tuning("last_kernel") == 3:
+        per = rb + 4.0 + (k - 1 + 32) / 4.0 / 32.0 + 64.0 * n_reads / max(1, kmers)
+        return {"kernel": "k_scan_ax (anchor-and-extend scan, speq_amd/csrc/ax_scan.hip)", "bytes_per_kmer": per,
+                "model": "read bases + qualities, one 4-B class per window, the 2-bit text of each 32-window run "
+                         "((k - 1 + 32) / 4 B), one 64-B anchor bucket per read"}
     if table_on:
         return {"kernel": "k_scan_kt (pipelined k-mer-table scan, speq_amd/csrc/scan_kernels.hip)",
                 "bytes_per_kmer": 64.0 + rb,
@@ -215,16 +222,30 @@ def run_workload(ctx: Ctx, cfg_no: int, k: int, n_reads: int, mode: str, steps: 
     counts = d_counts.cpu().numpy()
     weights = d_w.cpu().numpy() if local else None
     table_on = bool(ktab["table_bytes"])
-    km = kernel_model(dev, k, table_on, kmers_per_step, read_bytes)
+    km = kernel_model(dev, k, table_on, kmers_per_step, read_bytes, reads.n)
 
     lf = None
+    prev = None
+    if with_lf and a.kmer_table and table_on and dev.tuning("last_kernel") == 3:
+        # the previous hot path (k-mer-table kernel for k <= 31, else LF steps) on the same reads
+        dev.tune(ax_scan=0)
+        pv_el, pv_ms, pv_n = timed_run(steps, 1)
+        pv_counts = d_counts.cpu().numpy()
+        kind = dev.tuning("last_kernel")
+        dev.tune(ax_scan=1)
+        if not np.array_equal(pv_counts, counts):
+            raise RuntimeError("k-mer-table scan disagrees with the anchor-and-extend scan")
+        prev = {"value": kmers_per_step * ctx.world * steps / pv_el, "unit": "k-mers/s",
+                "avg_kernel_ms": pv_ms / max(1, pv_n),
+                "path": {0: "k_scan (LF steps)", 1: "k_scan<KT> (k-mer table)",
+                         2: "k_scan_kt (pipelined k-mer-table scan, round-1 hot path)"}.get(kind, str(kind))}
     if with_lf and a.kmer_table and table_on:
-        dev.tune(kmer_table=0)
+        dev.tune(kmer_table=0, ax_scan=0)
         lf_el, lf_ms, lf_n = timed_run(steps, 1)
         lf_counts = d_counts.cpu().numpy()
-        dev.tune(kmer_table=1)
+        dev.tune(kmer_table=1, ax_scan=1)
         if not np.array_equal(lf_counts, counts):
-            raise RuntimeError("LF-step scan disagrees with the k-mer-table scan")
+            raise RuntimeError("LF-step scan disagrees with the hot path")
         lf = {"value": kmers_per_step * ctx.world * steps / lf_el, "unit": "k-mers/s",
               "avg_kernel_ms": lf_ms / max(1, lf_n),
               "achieved_GBps": kmers_per_step * 2 * k * OCC_ENTRY_BYTES / (lf_ms / 1e3 / max(1, lf_n)) / 1e9,
@@ -282,7 +303,7 @@ def run_workload(ctx: Ctx, cfg_no: int, k: int, n_reads: int, mode: str, steps: 
         "index_build_s": round(prepared["build_s"], 3), "fm_text_len": int(idx.info().n),
         "kmer_table": {"on": table_on, "distinct_kmers": ktab["distinct_kmers"], "bytes": ktab["table_bytes"],
                        "build_s": round(ktab["build_ms"] / 1e3, 4)},
-        "roofline": roofline, "cpu_baseline": cpu, "lf_steps": lf, "pcie_inclusive": pcie,
+        "roofline": roofline, "cpu_baseline": cpu, "lf_steps": lf, "kmer_table_kernel": prev, "pcie_inclusive": pcie,
         "check": {"T": int(counts[0]), "ambiguous": int(counts[1]), "U": [int(x) for x in counts[2:]],
                   **({"W_sum": float(weights.sum())} if weights is not None else {})},
     }
@@ -341,6 +362,7 @@ def main():
             "roofline": head["roofline"],
             "cpu_baseline": head["cpu_baseline"],
             "lf_steps": head["lf_steps"],
+            "kmer_table_kernel": head["kmer_table_kernel"],
             "pcie_inclusive": head["pcie_inclusive"],
             "check": head["check"],
             **extra,

@@ -95,6 +95,9 @@ struct speq_device_index {
     std::vector<std::pair<hipEvent_t, hipEvent_t>> events;
     double timed_ms = 0.0;
     uint64_t timed_launches = 0;
+    // kernel of the last read scan (tuning key "last_kernel", read only): 0 LF steps (k_scan), 1 k-mer table
+    // (k_scan, KT), 2 pipelined k-mer table (k_scan_kt), 3 anchor-and-extend (k_scan_ax)
+    int last_kernel = -1;
 };
 
 namespace speq {

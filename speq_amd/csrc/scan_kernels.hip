@@ -1426,6 +1426,9 @@ void launch_t(const speq_device_index* d, const UnitSrc& src, uint32_t grid, siz
         v.kt_compact = kt->compact ? 1u : 0u;
         v.kt_k = src.k;
     }
+    if (MODE != KM_REF)
+        const_cast<speq_device_index*>(d)->last_kernel =
+            kt ? ((d->ilp_kt <= 2 && d->kt_pipeline) || kt->compact ? 2 : 1) : 0;
     if (kt) launch_v<MODE, PAIRED, LDS, true>(d, v, src, grid, lds, st, a, b, w);
     else launch_v<MODE, PAIRED, LDS, false>(d, v, src, grid, lds, st, a, b, w);
 }
@@ -1433,7 +1436,10 @@ void launch_t(const speq_device_index* d, const UnitSrc& src, uint32_t grid, siz
 void launch_scan(speq_device_index* d, int mode, bool paired, const UnitSrc& src, uint64_t work_units,
                  hipStream_t st, unsigned long long* a, unsigned long long* b, double* w) {
     // read scans: the anchor-and-extend kernel when the replica has (or can build) its structures for k (ax_scan.hip)
-    if (mode != KM_REF && speq::launch_ax(d, mode, paired, src, st, a, w)) return;
+    if (mode != KM_REF && speq::launch_ax(d, mode, paired, src, st, a, w)) {
+        d->last_kernel = 3;
+        return;
+    }
     const speq_device_index::KmerTable* kt = ensure_ktab(d, src.k);
     const bool lds_hist = d->G <= LDS_HIST_MAX_G;
     const uint32_t hist_words = lds_hist ? ((mode == KM_GLOBAL) ? d->G : 2u * d->G) : 0u;
@@ -1997,6 +2003,7 @@ int speq_device_get_tuning(const speq_device_index* d, const char* key, int64_t*
         else if (k == "kt_compact") *value = d->kt_compact ? 1 : 0;
         else if (k == "kt_load8") *value = d->kt_load8;
         else if (k == "ax_scan") *value = d->ax_scan ? 1 : 0;
+        else if (k == "last_kernel") *value = d->last_kernel;
         else if (k == "ax_load") *value = d->ax_load;
         else if (k == "grid_blocks_ax") *value = d->grid_blocks_ax;
         else if (k == "blocks_per_cu_ax") *value = d->blocks_per_cu_ax;

@@ -1,0 +1,200 @@
+"""GPU: the anchor-and-extend read scan (k_scan_ax) against the CPU oracle and the other kernels.
+
+The scan classifies a window from the class of the text position its bases were compared equal with, and finds a
+window absent only after its anchor-table chain ended without a verified match; these tests aim at the places where
+that could go wrong: windows that match the 2-bit text across a separator or an N (class SENT, deferred), reads
+with many errors or no match at all (deferred-list overflow), low-complexity references (poly-A/T: long chains of
+equal fingerprints and hash buckets), every anchor-table load factor, reads longer than a lane's staging segment,
+k at the word boundaries of the compare (32/33, 64/65, 96/97, 127/128), and EM histograms.
+Integer counters bit-exact; W to rtol 1e-10 (re-associated fp64 sums)."""
+import numpy as np
+import pytest
+
+from oracle.oracle import Oracle
+from speq_amd import DeviceIndex, EmHistogram, FmIndex, synth
+
+pytestmark = pytest.mark.gpu
+
+COMP = bytes.maketrans(b"ACGTN", b"TGCAN")
+
+
+def distinct_kmers(records, k):
+    seen = set()
+    for r in records:
+        r = r.upper()
+        for s in (r, r.translate(COMP)[::-1]):
+            for i in range(len(s) - k + 1):
+                w = s[i:i + k]
+                if b"N" not in w:
+                    seen.add(w)
+    return len(seen)
+
+
+def check(dev, orc, seq, qual, off, k, paired=False, local=False, cutoff=30):
+    got = dev.scan(seq.tobytes(), qual.tobytes(), off, k=k, paired=paired, local=local, phred_cutoff=cutoff)
+    T, amb, U, W = orc.scan(seq, qual, off, paired=paired, local=local, phred_cutoff=cutoff)
+    assert (got.total, got.ambiguous, got.unique.tolist()) == (T, amb, U.tolist()), (k, paired, local)
+    if local:
+        np.testing.assert_allclose(got.weights, W, rtol=1e-10, atol=0)
+    return got
+
+
+@pytest.fixture(scope="module")
+def small():
+    ref = synth.make_reference(4, 2, 6_000, ref_n_rate=0.002)
+    idx = FmIndex.build(ref.records, ref.groups, 4, prefix_q=8, pair_steps=True, triple_steps=True)
+    return ref, idx
+
+
+@pytest.mark.parametrize("k", [1, 2, 7, 16, 21, 31, 40, 70, 128])
+def test_distinct_kmers_and_last_kernel(small, k):
+    ref, idx = small
+    dev = DeviceIndex(idx)
+    info = dev.prepare(k)
+    assert info["distinct_kmers"] == distinct_kmers(ref.records, k)
+    reads = synth.make_reads(ref, 300)
+    dev.scan(reads.seq.tobytes(), reads.qual.tobytes(), reads.offsets, k=k)
+    assert dev.tuning("last_kernel") == 3  # k_scan_ax
+
+
+@pytest.mark.parametrize("k", [1, 5, 31, 32, 33, 64, 65, 96, 97, 127, 128])
+@pytest.mark.parametrize("paired", [False, True])
+def test_word_boundary_k_vs_oracle(small, k, paired):
+    ref, idx = small
+    dev = DeviceIndex(idx)
+    reads = synth.make_reads(ref, 1_500, n_rate=0.003, lowq_rate=0.01, err_rate=0.003, paired=paired,
+                             short_frac=0.0 if paired else 0.05)
+    orc = Oracle(ref.records, ref.groups, 4, k)
+    for local in (False, True):
+        check(dev, orc, reads.seq, reads.qual, reads.offsets, k, paired=paired, local=local)
+
+
+def test_k_above_128_falls_back(small):
+    ref, idx = small
+    dev = DeviceIndex(idx)
+    reads = synth.make_reads(ref, 300, read_len=250)
+    check(dev, Oracle(ref.records, ref.groups, 4, 129), reads.seq, reads.qual, reads.offsets, 129)
+    assert dev.tuning("last_kernel") == 0  # LF steps
+
+
+@pytest.mark.parametrize("read_len", [191, 192, 193, 250, 400, 1000])
+def test_long_reads_span_segments(small, read_len):
+    ref, idx = small
+    dev = DeviceIndex(idx)
+    reads = synth.make_reads(ref, 400, read_len=read_len, err_rate=0.002, n_rate=0.001)
+    for k in (21, 70, 128):
+        orc = Oracle(ref.records, ref.groups, 4, k)
+        check(dev, orc, reads.seq, reads.qual, reads.offsets, k, local=k == 21)
+
+
+@pytest.mark.parametrize("ax_load", [10, 35, 90])
+def test_table_load_factor(small, ax_load):
+    ref, idx = small
+    dev = DeviceIndex(idx)
+    dev.tune(ax_load=ax_load)
+    reads = synth.make_reads(ref, 2_000, err_rate=0.005)
+    for k in (11, 21, 31, 55):
+        check(dev, Oracle(ref.records, ref.groups, 4, k), reads.seq, reads.qual, reads.offsets, k)
+
+
+def test_random_and_error_heavy_reads_overflow_the_deferred_list(small):
+    """Random reads: every anchor is absent, so each lane defers k - 1 windows per lookup and the wave's list
+    overflows (the lane then keeps its windows); reads with 5 % errors defer most of their windows too."""
+    ref, idx = small
+    dev = DeviceIndex(idx)
+    rng = np.random.default_rng(5)
+    n, L = 3_000, 150
+    rnd = rng.choice(np.frombuffer(b"ACGT", dtype=np.uint8), size=n * L)
+    noisy = synth.make_reads(ref, n, err_rate=0.05)
+    clean = synth.make_reads(ref, n)
+    seq = np.concatenate([rnd, noisy.seq, clean.seq])
+    qual = np.full(seq.size, ord("I"), dtype=np.uint8)
+    off = np.arange(0, seq.size + 1, L, dtype=np.uint64)
+    for k in (11, 21, 31, 45):
+        for local in (False, True):
+            check(dev, Oracle(ref.records, ref.groups, 4, k), seq, qual, off, k, local=local)
+
+
+@pytest.mark.parametrize("k", [11, 21, 23, 31])
+def test_low_complexity_references(k):
+    """Poly-A / poly-T runs and short tandem repeats in the references and in the reads: one k-mer with thousands of
+    occurrences, reads that match the 2-bit text across separators (coded as A) and Ns, and (for the k-mer table)
+    the all-T key; compared with the k-mer table at two load factors, LF steps and the oracle."""
+    rng = np.random.default_rng(k)
+    recs = []
+    for r in range(6):
+        parts = [bytes(rng.choice(np.frombuffer(b"ACGT", dtype=np.uint8), size=300))]
+        parts.append(b"A" * int(rng.integers(40, 120)))
+        parts.append(b"CAG" * int(rng.integers(10, 40)))
+        parts.append(bytes(rng.choice(np.frombuffer(b"ACGT", dtype=np.uint8), size=200)))
+        parts.append(b"T" * int(rng.integers(40, 120)))
+        parts.append(b"N" * int(rng.integers(0, 3)))
+        parts.append(bytes(rng.choice(np.frombuffer(b"ACGT", dtype=np.uint8), size=250)))
+        recs.append(b"".join(parts))
+    groups = [r % 3 for r in range(6)]
+    idx = FmIndex.build(recs, groups, 3, prefix_q=6, pair_steps=True, triple_steps=True)
+    reads = []
+    for _ in range(3_000):
+        r = recs[int(rng.integers(0, 6))]
+        p = int(rng.integers(0, len(r) - 100))
+        s = r[p:p + 100]
+        if rng.random() < 0.5:
+            s = s.translate(COMP)[::-1]
+        reads.append(s)
+    reads += [b"A" * 100, b"T" * 100, b"CAG" * 33 + b"C", b"A" * 60 + b"C" * 40]
+    seq = np.frombuffer(b"".join(reads), dtype=np.uint8).copy()
+    qual = np.full(seq.size, ord("I"), dtype=np.uint8)
+    off = np.zeros(len(reads) + 1, dtype=np.uint64)
+    off[1:] = np.cumsum([len(x) for x in reads])
+    orc = Oracle(recs, groups, 3, k)
+    for tune in (dict(ax_scan=1), dict(ax_scan=1, ax_load=90), dict(ax_scan=0, kt_load8=35),
+                 dict(ax_scan=0, kt_load8=90), dict(ax_scan=0, kt_compact=0), dict(ax_scan=0, kmer_table=0)):
+        dev = DeviceIndex(idx)
+        dev.tune(**tune)
+        check(dev, orc, seq, qual, off, k)
+        check(dev, orc, seq, qual, off, k, local=True)
+
+
+@pytest.mark.parametrize("paired", [False, True])
+def test_em_histogram_equals_other_kernels(paired):
+    ref = synth.make_reference(5, 3, 8_000, ref_n_rate=0.0005)
+    idx = FmIndex.build(ref.records, ref.groups, 5, prefix_q=9, pair_steps=True, triple_steps=True)
+    reads = synth.make_reads(ref, 15_000, paired=paired, n_rate=0.001, lowq_rate=0.005, err_rate=0.004)
+    res = {}
+    for name, tune in (("ax", dict(ax_scan=1)), ("kt", dict(ax_scan=0)), ("lf", dict(ax_scan=0, kmer_table=0))):
+        dev = DeviceIndex(idx)
+        dev.tune(**tune)
+        for k in (21, 31, 50):
+            em = EmHistogram(dev)
+            r = em.scan(reads.seq.tobytes(), reads.qual.tobytes(), reads.offsets, k=k, paired=paired, local=True)
+            em.finalize()
+            p = np.linspace(5.0, 30.0, 5)
+            res[(name, k)] = (r.total, r.ambiguous, r.unique.tolist(), r.weights, em.info(),
+                              em.step(p, [3] * 5, r.unique))
+    for k in (21, 31, 50):
+        for other in ("kt", "lf"):
+            a, b = res[("ax", k)], res[(other, k)]
+            assert a[:3] == b[:3], (k, other)
+            np.testing.assert_allclose(a[3], b[3], rtol=1e-12)
+            assert a[4] == b[4]
+            np.testing.assert_array_equal(a[5], b[5])
+
+
+def test_device_buffers_and_grid_knobs(small):
+    """The HBM-resident entry point with tiny grids (many batches per wave) and occupancy caps."""
+    import torch
+    ref, idx = small
+    reads = synth.make_reads(ref, 5_000, err_rate=0.002)
+    d_seq = torch.from_numpy(reads.seq).cuda()
+    d_qual = torch.from_numpy(reads.qual).cuda()
+    d_off = torch.from_numpy(reads.offsets.astype(np.int64)).cuda()
+    orc = Oracle(ref.records, ref.groups, 4, 21)
+    T, amb, U, _ = orc.scan(reads.seq, reads.qual, reads.offsets)
+    dev = DeviceIndex(idx)
+    for grid, bpc in ((1, 0), (3, 2), (65535, 0), (100, 1)):
+        dev.tune(grid_blocks_ax=grid, blocks_per_cu_ax=bpc)
+        cnt = torch.zeros(6, dtype=torch.int64, device="cuda")
+        dev.scan_device(d_seq.data_ptr(), d_qual.data_ptr(), d_off.data_ptr(), reads.n, 21, cnt.data_ptr())
+        torch.cuda.synchronize()
+        c = cnt.cpu().numpy()
+        assert (int(c[0]), int(c[1]), c[2:].tolist()) == (T, amb, U.tolist()), (grid, bpc)

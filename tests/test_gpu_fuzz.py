@@ -1,7 +1,7 @@
 """GPU: randomized parameter sweep against the C oracle (same seeded inputs): reference shapes (record counts and
 lengths, N rate, groups), index options (q, one/two/three-symbol steps, label table, host or GPU build), scan
 options (k, cutoff, paired, local) and launch knobs (windows per lane, occupancy cap, grid, q-mer table level,
-k-mer interval table).
+k-mer interval table, anchor-and-extend scan and its table load).
 Integer counters bit-exact, W to rtol 1e-10."""
 import numpy as np
 import pytest
@@ -31,7 +31,9 @@ def test_random_configurations(seed):
     dev.tune(ilp=int(rng.integers(1, 3)), ilp_local=int(rng.integers(1, 3)),
              blocks_per_cu=int(rng.choice([0, 2, 4])), grid_blocks=int(rng.choice([7, 64, 16384])),
              prefix_level=int(rng.choice([-1, 0, 1, 2])) if q >= 3 else -1,
-             sparse_prefix=int(rng.choice([-1, 0, 1])), kmer_table=int(rng.integers(0, 2)))
+             sparse_prefix=int(rng.choice([-1, 0, 1])), kmer_table=int(rng.integers(0, 2)),
+             ax_scan=int(rng.random() < 0.7), ax_load=int(rng.choice([10, 35, 90])),
+             grid_blocks_ax=int(rng.choice([1, 7, 65535])))
     paired = bool(rng.random() < 0.4)
     reads = synth.make_reads(ref, int(rng.integers(50, 1500)), read_len=int(rng.integers(20, 250)),
                              paired=paired, fragment=int(rng.integers(250, 600)), n_rate=0.003,

@@ -1,6 +1,6 @@
 """GPU: the HIP path reproduces the committed golden vectors (tests/golden/*/expected.json) bit-exactly
-(fp64 Phred weights to rtol 1e-12), for every k of every case and several q-mer table sizes, with and without the
-k-mer interval table; plus the RCCL
+(fp64 Phred weights to rtol 1e-12), for every k of every case and several q-mer table sizes, with each read-scan
+kernel (anchor-and-extend, k-mer interval table, LF steps); plus the RCCL
 counter all-reduce through the C ABI on a single-rank communicator."""
 import ctypes as C
 
@@ -21,8 +21,9 @@ def test_gpu_matches_golden(name, q, steps):
     c = Case(name)
     dev = DeviceIndex(FmIndex.build(c.records, c.groups, c.G, prefix_q=q, pair_steps=steps >= 2,
                                     label_table=steps == 2, triple_steps=steps == 3))
-    for k, ilp, kt in [(k, ilp, kt) for k in c.ks for ilp in (1, 2) for kt in (1, 0)]:
-        dev.tune(ilp=ilp, ilp_local=ilp, kmer_table=kt)  # k-mer interval table (k <= 31) or LF steps
+    variants = [(1, 1, 1), (1, 1, 0), (1, 0, 0), (2, 0, 0)]  # (ilp, k-mer table, anchor-and-extend)
+    for k, ilp, kt, ax in [(k,) + v for k in c.ks for v in variants]:
+        dev.tune(ilp=ilp, ilp_local=ilp, kmer_table=kt, ax_scan=ax)
         e = c.exp["by_k"][str(k)]
         u, t = dev.count_unique_kmers_per_group(k)
         assert u.tolist() == e["u_ref"] and t.tolist() == e["tot_ref"], (name, k)

@@ -36,6 +36,7 @@ def small():
 def test_key_set_is_the_distinct_reference_kmers(small, k):
     ref, idx = small
     dev = DeviceIndex(idx)
+    dev.tune(ax_scan=0)  # the k-mer table (the anchor-and-extend structures: tests/test_gpu_ax.py)
     info = dev.prepare(k)
     assert info["distinct_kmers"] == distinct_kmers(ref.records, k)
     # 16-B slots at load <= 1/2, or (k <= 23) 8-B slots at load 1/2: >= 16 B per distinct k-mer either way
@@ -45,6 +46,7 @@ def test_key_set_is_the_distinct_reference_kmers(small, k):
 def test_no_table_above_31_or_when_off(small):
     _, idx = small
     dev = DeviceIndex(idx)
+    dev.tune(ax_scan=0)
     assert dev.prepare(32)["table_bytes"] == 0
     dev.tune(kmer_table=0)
     assert dev.prepare(21)["table_bytes"] == 0
@@ -60,7 +62,7 @@ def test_table_equals_lf_steps_with_em(paired, local):
     res = {}
     for kt in (1, 0):
         dev = DeviceIndex(idx)
-        dev.tune(kmer_table=kt)
+        dev.tune(kmer_table=kt, ax_scan=0)
         for k in (31, 21, 15):  # several tables on one replica, built in turn
             em = EmHistogram(dev)
             r = em.scan(reads.seq.tobytes(), reads.qual.tobytes(), reads.offsets, k=k, paired=paired, local=local)
@@ -83,6 +85,7 @@ def test_absent_kmers_and_oracle():
     ref = synth.make_reference(4, 1, 8_000)
     idx = FmIndex.build(ref.records, ref.groups, 4, prefix_q=6, pair_steps=True, triple_steps=True)
     dev = DeviceIndex(idx)
+    dev.tune(ax_scan=0)
     rng = np.random.default_rng(7)
     n, L = 2_000, 120
     seq = rng.choice(np.frombuffer(b"ACGT", dtype=np.uint8), size=n * L)  # random reads: absent 21-mers
@@ -103,7 +106,7 @@ def test_launch_knobs_keep_results(small, ilp_kt, kt_slots):
     ref, idx = small
     reads = synth.make_reads(ref, 4_000, n_rate=0.002, lowq_rate=0.01, short_frac=0.05)
     dev = DeviceIndex(idx)
-    dev.tune(ilp_kt=ilp_kt, kt_slots=kt_slots)
+    dev.tune(ilp_kt=ilp_kt, kt_slots=kt_slots, ax_scan=0)
     for k in (13, 21, 31):
         r = dev.scan(reads.seq.tobytes(), reads.qual.tobytes(), reads.offsets, k=k)
         T, amb, U, _ = Oracle(ref.records, ref.groups, 3, k).scan(reads.seq, reads.qual, reads.offsets)
@@ -114,8 +117,9 @@ def test_phred_weight_of_one_window_is_bit_exact(small):
     """A read of exactly k bases that occurs in one group: W[g] is that window's weight, which must equal the
     reference's left-to-right divisions w = w / (1 - 1/10^(q/10)) (fm_scanner.cpp:454) to the last bit."""
     ref, idx = small
-    dev = DeviceIndex(idx)
     rng = np.random.default_rng(11)
+    devs = [DeviceIndex(idx), DeviceIndex(idx)]
+    devs[1].tune(ax_scan=0)  # both read-scan kernels
     k = 31
     checked = 0
     for _ in range(150):
@@ -128,15 +132,17 @@ def test_phred_weight_of_one_window_is_bit_exact(small):
         # varied qualities, or one quality for the whole window (weight from the per-block uniform-q table)
         q = rng.integers(31, 42, size=k) if checked % 2 else np.full(k, int(rng.integers(31, 42)))
         qual = bytes((q + 33).astype(np.uint8))
-        res = dev.scan(seq, qual, np.array([0, k], dtype=np.uint64), k=k, local=True)
-        if res.unique.sum() != 1:
-            continue  # the window is shared by several groups
-        w = 1.0
-        for x in q:
-            w = w / (1.0 - 1.0 / (10.0 ** (float(x) / 10.0)))
-        g = int(np.argmax(res.unique))
-        assert res.weights[g] == w, (res.weights[g], w)
-        checked += 1
+        for dev in devs:
+            res = dev.scan(seq, qual, np.array([0, k], dtype=np.uint64), k=k, local=True)
+            if res.unique.sum() != 1:
+                break  # the window is shared by several groups
+            w = 1.0
+            for x in q:
+                w = w / (1.0 - 1.0 / (10.0 ** (float(x) / 10.0)))
+            g = int(np.argmax(res.unique))
+            assert res.weights[g] == w, (res.weights[g], w)
+        else:
+            checked += 1
     assert checked > 50
 
 
@@ -150,7 +156,7 @@ def test_compact_table_equals_wide_table(paired):
     res = {}
     for mode in ("compact", "wide", "lf"):
         dev = DeviceIndex(idx)
-        dev.tune(kt_compact=int(mode == "compact"), kmer_table=int(mode != "lf"), kt_load8=50)
+        dev.tune(kt_compact=int(mode == "compact"), kmer_table=int(mode != "lf"), kt_load8=50, ax_scan=0)
         for k in (11, 21, 23, 24):
             info = dev.prepare(k)
             em = EmHistogram(dev)

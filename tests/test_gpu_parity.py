@@ -14,14 +14,20 @@ pytestmark = pytest.mark.gpu
 W_RTOL = 1e-10  # fp64 sums of up to ~1e8 windows in a different order (worst case ~N * eps)
 
 
+# kernel variants: anchor-and-extend (the default), the k-mer-table kernel, LF steps (one and two windows per lane)
+VARIANTS = [dict(ax_scan=1, kmer_table=1, ilp=1), dict(ax_scan=0, kmer_table=1, ilp=1),
+            dict(ax_scan=0, kmer_table=0, ilp=1), dict(ax_scan=0, kmer_table=0, ilp=2)]
+
+
 def _check(dev, orc, reads, k, cutoff=30, paired=False, local=False, ilps=(1, 2)):
-    """Every kernel variant (windows per lane = 1 and 2; k-mer interval table or LF steps) must give the oracle's
-    counts."""
-    for ilp in ilps:
-        for kt in (1, 0):
-            dev.tune(ilp=ilp, ilp_local=ilp, kmer_table=kt)
-            got = _check_one(dev, orc, reads, k, cutoff, paired, local)
-    dev.tune(ilp=1, ilp_local=1, kmer_table=1)
+    """Every kernel variant (anchor-and-extend; k-mer interval table; LF steps with 1 and 2 windows per lane) must
+    give the oracle's counts."""
+    for v in VARIANTS:
+        if v["ilp"] not in ilps:
+            continue
+        dev.tune(ilp=v["ilp"], ilp_local=v["ilp"], kmer_table=v["kmer_table"], ax_scan=v["ax_scan"])
+        got = _check_one(dev, orc, reads, k, cutoff, paired, local)
+    dev.tune(ilp=1, ilp_local=1, kmer_table=1, ax_scan=1)
     return got
 
 
