@@ -70,4 +70,11 @@ clean:
 	rm -rf build bin $(LIB) tools/build
 	$(MAKE) -C oracle clean
 
-.PHONY: all oracle clean variant
+# A/B variants of the anchor-and-extend kernel: make axvariant NAME=w3 VFLAGS=-DSPEQ_AX_MIN_WAVES=3
+axvariant: $(filter-out $(OBJDIR)/ax_scan.o,$(LIB_OBJS))
+	@mkdir -p build/variants/$(NAME)
+	$(HIPCC) $(HIPFLAGS) $(VFLAGS) -c speq_amd/csrc/ax_scan.hip -o build/variants/$(NAME)/ax_scan.o
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o build/variants/$(NAME)/libspeq_scan.so \
+	    build/variants/$(NAME)/ax_scan.o $^ -L/opt/rocm/lib -lamdhip64 -lz -lpthread -ldl -Wl,-rpath,/opt/rocm/lib
+
+.PHONY: all oracle clean variant axvariant

@@ -26,11 +26,11 @@ def main():
         shutil.copy(st, os.path.join(dst, f"kernel_stats_{tag}.csv"))
         rows = list(csv.DictReader(open(st)))
         out["kernel_stats"] = [{k: r[k] for k in ("Name", "Calls", "AverageNs", "MinNs", "MaxNs", "Percentage")}
-                               for r in rows if "::k_scan<" in r["Name"] or "::k_scan_kt<" in r["Name"]]
+                               for r in rows if any(t in r["Name"] for t in ("::k_scan<", "::k_scan_kt<", "::k_scan_ax<"))]
     tr = os.path.join(src, "trace", "trace_kernel_trace.csv")
     if os.path.exists(tr):  # steady state: the later half of the scan dispatches (the first ones run on cold caches)
         d = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) for r in csv.DictReader(open(tr))
-             if "::k_scan<" in r["Kernel_Name"] or "::k_scan_kt<" in r["Kernel_Name"]]
+             if any(t in r["Kernel_Name"] for t in ("::k_scan<", "::k_scan_kt<", "::k_scan_ax<"))]
         if d:
             tail = d[len(d) // 2:]
             out["scan_dispatch_ns"] = d
@@ -42,7 +42,7 @@ def main():
         if not os.path.exists(f):
             continue
         for r in csv.DictReader(open(f)):
-            if "::k_scan<" not in r["Kernel_Name"] and "::k_scan_kt<" not in r["Kernel_Name"]:  # not rocPRIM's scans
+            if not any(t in r["Kernel_Name"] for t in ("::k_scan<", "::k_scan_kt<", "::k_scan_ax<")):  # not rocPRIM's scans
                 continue
             pmc[r["Counter_Name"]].append(float(r["Counter_Value"]))
             meta = {k: r[k] for k in ("Grid_Size", "Workgroup_Size", "LDS_Block_Size", "VGPR_Count", "SGPR_Count",

@@ -5,31 +5,35 @@
 //
 // Why: consecutive windows of a read that matches the reference are consecutive positions of the reference text, and
 // whether a k-mer is unique to one group is a property of the k-mer, i.e. of ANY of its occurrences. So per k the
-// replica keeps the classification of the k-mer that starts at every text position (`cls`, one u32 per position: the
-// group, MULTI | SA-interval start, or SENT for a window that crosses a text end or holds an N), plus a hash table
-// of one representative position per distinct k-mer (`atab`). A lane takes one READ: it looks its first window up
-// once (the anchor: bucket -> fingerprint -> representative p), then compares the read with the 2-bit text at p,
-// 32 windows at a time (one XOR per 32 bases), and reads the classes of all matched windows with coalesced 16-B loads
-// of cls[p + d]. A mismatch (a SNP against the representative, or a sequencing error) ends the run and the next
-// window is looked up again. Every verdict is exact: a window is classified from cls[p'] only after its k bases were
-// compared equal with text[p', p' + k), and a window is absent only after the hash chain of its key ran into an empty
-// slot without a verified fingerprint match.
+// replica keeps the class of the k-mer that starts at every text position (`cls`, 1 byte per position when the
+// index has <= 253 groups, else 2: the group, MULTI, or SENT for a window that crosses a text end or holds an N), plus
+// a hash table of one representative position per distinct k-mer (`atab`). A lane takes one READ: it looks one window
+// up (the anchor: bucket -> fingerprint -> representative p), then compares the read with the 2-bit text at p, 64
+// windows at a time (one XOR per 32 bases), and reads the classes of the matched windows (64 bytes: four 16-B loads).
+// A mismatch (a SNP against the representative, or a sequencing error) ends the run and the next window is looked up
+// again. Every verdict is exact: a window is classified from cls[p'] only after its k bases were compared equal with
+// text[p', p' + k), and a window is absent only after its key's chain in the anchor table ran into an empty slot
+// without a verified fingerprint match (or its bits are missing from the table's blocked Bloom filter, which holds
+// every k-mer of the texts).
 //
 // Windows whose anchor lookup finds nothing (the k windows over a sequencing error) and windows that matched a text
-// position whose class is SENT are DEFERRED: the wave collects them in LDS and resolves them after the per-read
-// pass, 64 at a time, one window per lane (phase 2), so one erroneous read does not hold its wave for k lookups.
+// position whose class is SENT are DEFERRED: the wave collects them in LDS and, after the per-read pass, tests them
+// against the Bloom filter (four per lane per round trip) and looks the survivors up one per lane, so one erroneous
+// read does not hold its wave for k lookups.
 //
-// Cost per read (150 bp, k = 21, no error): one bucket gather + ~4 x (a 3-word text load, eight 16-B class loads,
-// one XOR compare, 32 tallies). The k-mer table kernel (k_scan_kt) pays one 64-B bucket gather + a hash + an
-// 8-slot compare for EVERY window, and its per-window bookkeeping (cursor, staging, ballots) runs for every lane.
+// What bounds it (profiles/r02): the per-CU vector-memory path, which serves the lanes' scattered 16-B loads one
+// cache line per lane; so the classes are bytes (a 64-window run is four loads, not sixteen), a load group is issued
+// only when some lane of the wave needs it, and one iteration costs one round trip.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
 #include <chrono>
+#include <climits>
 #include <cstdint>
 #include <cstring>
 #include <mutex>
 #include <stdexcept>
+#include <type_traits>
 #include <vector>
 
 #include "device_index.hpp"
@@ -44,19 +48,34 @@ constexpr uint32_t AX_MAX_K = 128;    // longest k the scan takes (AX_CAP - k + 
 constexpr uint32_t AX_CAP = 192;      // bases of a read a lane stages at once (longer reads: segments of AX_CAP bases)
 constexpr uint32_t AX_STREAM = AX_CAP + 16;  // staged bases incl. the 16-B alignment slack before the read
 constexpr uint32_t AX_CHUNKS = AX_STREAM / 16;
-constexpr uint32_t AX_RUN = 32;       // windows a lane classifies per iteration (one compare, eight 16-B class loads)
+constexpr uint32_t AX_RUN = 64;       // windows a lane classifies per iteration (one compare, 64 class bytes)
 constexpr uint32_t AX_PKW = 9;        // staged 2-bit words per lane (AX_STREAM bases + extraction slack)
 constexpr uint32_t AX_VWW = 4;        // valid-window words per lane
 constexpr uint32_t AX_CGW = 5;        // quality-change words per lane (local mode)
-constexpr uint32_t AX_DEF = 512;      // deferred-window entries per wave
-constexpr uint32_t AX_VOID = 0xFFFFFFFFu;  // a deferred-list slot reserved by a lane that then kept its windows
-constexpr uint32_t AX_SENT = 0xFFFFFFFFu;
-constexpr uint32_t AX_MULTI = 0x80000000u;
+constexpr uint32_t AX_DEF = 1024;     // deferred-window entries per wave (u16: lane | window << 6)
+constexpr uint32_t AX_F = 4;          // deferred windows a lane tests against the filter per round trip
 constexpr uint32_t AX_EMPTY = 0xFFFFFFFFu;
+constexpr uint16_t AX_VOID = 0xFFFFu;  // a deferred-list slot reserved by a lane that then kept its windows
 constexpr unsigned long long AX_SLOT_EMPTY = ~0ull;
-constexpr uint32_t AX_OOB = 0xFFFFFFF0u;  // buffer offset past every class array (n < 2^30)
+constexpr uint32_t AX_OOB = 0xFFFFFFF0u;  // buffer offset past every array (n < 2^30)
+constexpr uint32_t AX_FILTER_BITS = 16;   // Bloom filter bits per distinct k-mer (3 bits set per k-mer, one 64-bit word)
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
 
 static_assert(AX_STREAM % 16 == 0, "chunks of 16 bases");
+static_assert(AX_CAP < 1024, "deferred entries hold the window in 10 bits");
+
+// class values (CW bytes per text position): groups 0 .. G-1 < NONE; NONE is never stored
+template <int CW>
+struct AxCls {
+    static constexpr uint32_t SENT = CW == 1 ? 0xFFu : 0xFFFFu;
+    static constexpr uint32_t MULTI = SENT - 1u;
+    static constexpr uint32_t NONE = SENT - 2u;
+    static constexpr uint32_t MAX_G = NONE;
+    static constexpr uint32_t PER = 4 / CW;                                   // classes per dword
+    static constexpr uint32_t REP = CW == 1 ? 0x01010101u : 0x00010001u;      // broadcast factor
+    static constexpr uint32_t FLAGS = CW == 1 ? 0x80808080u : 0x80008000u;    // top bit of every element
+    static constexpr uint32_t LOW7 = CW == 1 ? 0x7F7F7F7Fu : 0x7FFF7FFFu;
+};
 
 __host__ __device__ __forceinline__ uint64_t ax_fmix(uint64_t x) {  // murmur3 fmix64 (a bijection)
     x ^= x >> 33;
@@ -86,6 +105,13 @@ __device__ __forceinline__ uint64_t ax_hash(const uint64_t (&w)[NW], uint32_t k)
 __host__ __device__ __forceinline__ uint32_t ax_bucket(uint64_t h, uint64_t nb) {
     return (uint32_t)(((h >> 32) * nb) >> 32);
 }
+// Bloom filter of the distinct k-mers: one 64-bit word per key, three bits in it
+__host__ __device__ __forceinline__ uint32_t ax_fword(uint64_t h, uint64_t nf) {
+    return (uint32_t)((((h >> 24) & 0xFFFFFFFFull) * nf) >> 32);
+}
+__host__ __device__ __forceinline__ uint64_t ax_fbits(uint64_t h) {
+    return (1ull << (h & 63u)) | (1ull << ((h >> 6) & 63u)) | (1ull << ((h >> 12) & 63u));
+}
 
 __device__ __forceinline__ uint64_t funnel(uint64_t lo, uint64_t hi, uint32_t sh) {  // bits [sh, sh + 64) of hi:lo
     return sh == 0u ? lo : ((lo >> sh) | (hi << (64u - sh)));
@@ -95,12 +121,23 @@ __device__ __forceinline__ uint64_t funnel(uint64_t lo, uint64_t hi, uint32_t sh
 __device__ __forceinline__ uint32_t zero_bytes(uint32_t v) {
     return ~(((v & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | v) & 0x80808080u;
 }
+// the same per element of a class dword
+template <int CW>
+__device__ __forceinline__ uint32_t zero_elems(uint32_t v) {
+    return ~(((v & AxCls<CW>::LOW7) + AxCls<CW>::LOW7) | v) & AxCls<CW>::FLAGS;
+}
 // the 0x80 flags of the four bytes -> bits 0..3
 __device__ __forceinline__ uint32_t flags4(uint32_t m) {
     uint32_t y = m >> 7;
     y |= y >> 7;
     y |= y >> 14;
     return y & 0xFu;
+}
+// bits 0 .. PER-1 of b -> the top bit of each element of a class dword
+template <int CW>
+__device__ __forceinline__ uint32_t spread(uint32_t b) {
+    if (CW == 1) return ((b * 0x00204081u) & 0x01010101u) << 7;
+    return ((b * 0x00008001u) & 0x00010001u) << 15;
 }
 
 // ---------------------------------------------------------------------------------------------------------------
@@ -131,8 +168,8 @@ __global__ void k_ax_text2(const uint8_t* __restrict__ text, uint64_t n, uint64_
 
 // Backward search of the k symbols text[pos .. pos + k) (all ACGT): q-mer table, then three/two/one-symbol LF steps
 // (search_lds with the symbols read from the text), then the label-run classification.
-__device__ int ax_search_text(const DevView& I, const Rsrc& R, const uint8_t* __restrict__ t, uint32_t k, uint32_t& lo_out,
-                              uint32_t& hi_out) {
+__device__ int ax_search_text(const DevView& I, const Rsrc& R, const uint8_t* __restrict__ t, uint32_t k,
+                              uint32_t& lo_out, uint32_t& hi_out) {
     uint32_t lo = 0, hi = I.n;
     int32_t s = (int32_t)k;
     auto sym = [&](int32_t i) -> uint32_t { return (uint32_t)t[i] - 2u; };
@@ -178,10 +215,15 @@ __device__ int ax_search_text(const DevView& I, const Rsrc& R, const uint8_t* __
 }
 
 // Pass A: the class of the k-mer at every text position, and one representative position per distinct k-mer (the
-// first to claim owner[lo] of its SA interval). Multi-group k-mers also record their interval end (mhi[lo], for EM).
+// first to claim owner[lo] of its SA interval). Multi-group k-mers also record their interval: mlo[pos] = its start
+// and mhi[start] = its end (EM histograms).
+template <int CW>
 __global__ void k_ax_classify(DevView I, const uint8_t* __restrict__ text, const uint64_t* __restrict__ tbad,
-                              uint64_t n, uint32_t k, uint32_t* __restrict__ cls, uint32_t* __restrict__ mhi,
-                              uint32_t* __restrict__ owner, unsigned long long* __restrict__ n_distinct) {
+                              uint64_t n, uint32_t k, void* __restrict__ cls_v, uint32_t* __restrict__ mlo,
+                              uint32_t* __restrict__ mhi, uint32_t* __restrict__ owner,
+                              unsigned long long* __restrict__ n_distinct) {
+    using T = typename std::conditional<CW == 1, uint8_t, uint16_t>::type;
+    T* cls = static_cast<T*>(cls_v);
     const Rsrc R = make_rsrc(I);
     unsigned long long claimed = 0;
     for (uint64_t pos = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; pos < n;
@@ -196,14 +238,17 @@ __global__ void k_ax_classify(DevView I, const uint8_t* __restrict__ text, const
             b += span;
         }
         if (!valid) {
-            cls[pos] = AX_SENT;
+            cls[pos] = (T)AxCls<CW>::SENT;
             continue;
         }
         uint32_t lo = 0, hi = 0;
         const int g = ax_search_text(I, R, text + pos, k, lo, hi);
         // g == -1 cannot happen: the window occurs at pos
-        cls[pos] = g >= 0 ? (uint32_t)g : (AX_MULTI | lo);
-        if (g == -2) mhi[lo] = hi;
+        cls[pos] = (T)(g >= 0 ? (uint32_t)g : AxCls<CW>::MULTI);
+        if (g == -2) {
+            mlo[pos] = lo;
+            mhi[lo] = hi;
+        }
         if (atomicCAS(&owner[lo], AX_EMPTY, (uint32_t)pos) == AX_EMPTY) ++claimed;
     }
     if (claimed) atomicAdd(n_distinct, claimed);
@@ -222,15 +267,17 @@ __device__ __forceinline__ void ax_text_words(const uint64_t* __restrict__ t2, u
 }
 
 // Pass B: every representative position inserts {fingerprint, position} into the anchor table (8 slots per 64-B
-// bucket, first empty slot in order, linear probing over buckets; no deletions).
+// bucket, first empty slot in order, linear probing over buckets; no deletions) and sets its filter bits.
 __global__ void k_ax_insert(const uint32_t* __restrict__ owner, uint64_t n, const uint64_t* __restrict__ t2, uint32_t k,
-                            unsigned long long* __restrict__ atab, uint64_t nb) {
+                            unsigned long long* __restrict__ atab, uint64_t nb, unsigned long long* __restrict__ filt,
+                            uint64_t nf) {
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
         const uint32_t p = owner[i];
         if (p == AX_EMPTY) continue;
         uint64_t w[4];
         ax_text_words<4>(t2, p, w);
         const uint64_t h = ax_hash<4>(w, k);
+        atomicOr(&filt[ax_fword(h, nf)], (unsigned long long)ax_fbits(h));
         const unsigned long long v = ((unsigned long long)p << 32) | (uint32_t)h;
         uint32_t b = ax_bucket(h, nb);
         for (bool placed = false; !placed; b = (b + 1u == nb) ? 0u : b + 1u)
@@ -245,26 +292,34 @@ __global__ void k_ax_insert(const uint32_t* __restrict__ owner, uint64_t n, cons
 
 struct AxView {
     const uint64_t* t2;        // 2-bit text
-    const uint32_t* cls;       // class per text position (+ padding)
-    const uint32_t* mhi;       // interval end of multi-group k-mers, by interval start (EM)
+    const void* cls;           // class per text position (CW bytes each, + padding)
+    const uint32_t* mlo;       // SA interval start of the multi-group k-mer at a text position (EM)
+    const uint32_t* mhi;       // its end, by interval start (EM)
     const unsigned long long* atab;
+    const unsigned long long* filt;
     uint64_t nb;               // buckets
+    uint64_t nf;               // filter words
     uint64_t n;                // text length
+    uint64_t t2_bytes;         // bytes of the 2-bit text (incl. padding)
+    uint64_t cls_bytes;        // bytes of cls (incl. padding)
     uint32_t G;
 };
 
-// One probe of the anchor table from bucket *b, slot *s: returns the first slot >= *s whose fingerprint matches
-// (position in *p), or "absent" when an empty slot comes first; a full bucket without either moves to the next one.
-// On a match *b/*s point at that slot (a failed verification resumes at *s + 1).
-__device__ __forceinline__ bool ax_probe(const AxView& A, uint32_t fp, uint32_t& b, uint32_t& s, uint32_t& p,
-                                         bool active) {
+// One probe of the anchor table from bucket *b, slot *s: the first slot >= *s whose fingerprint matches (position in
+// *p), or "absent" when an empty slot comes first; a full bucket without either moves to the next one. On a match
+// *s is that slot (a failed verification resumes at *s + 1). Phase 2 only (phase 1 resolves its buckets inline).
+__device__ __forceinline__ bool ax_probe(const AxView& A, const __amdgpu_buffer_rsrc_t& rs_atab, uint32_t fp,
+                                         uint32_t& b, uint32_t& s, uint32_t& p, bool active) {
     bool found = false, pending = active;
     while (__ballot(pending) != 0) {
+        const uint32_t boff = pending ? b * 64u : AX_OOB;
+        const u32x4 v0 = __builtin_amdgcn_raw_buffer_load_b128(rs_atab, boff, 0, 0);
+        const u32x4 v1 = __builtin_amdgcn_raw_buffer_load_b128(rs_atab, boff + 16u, 0, 0);
+        const u32x4 v2 = __builtin_amdgcn_raw_buffer_load_b128(rs_atab, boff + 32u, 0, 0);
+        const u32x4 v3 = __builtin_amdgcn_raw_buffer_load_b128(rs_atab, boff + 48u, 0, 0);
         if (pending) {
-            const uint4* pb = reinterpret_cast<const uint4*>(A.atab + (uint64_t)b * 8u);
-            const uint4 v0 = pb[0], v1 = pb[1], v2 = pb[2], v3 = pb[3];
-            const uint32_t fps[8] = {v0.x, v0.z, v1.x, v1.z, v2.x, v2.z, v3.x, v3.z};
-            const uint32_t pos[8] = {v0.y, v0.w, v1.y, v1.w, v2.y, v2.w, v3.y, v3.w};
+            const uint32_t fps[8] = {v0[0], v0[2], v1[0], v1[2], v2[0], v2[2], v3[0], v3[2]};
+            const uint32_t pos[8] = {v0[1], v0[3], v1[1], v1[3], v2[1], v2[3], v3[1], v3[3]};
             uint32_t mm = 0, me = 0;
 #pragma unroll
             for (int t = 0; t < 8; ++t) {
@@ -272,7 +327,7 @@ __device__ __forceinline__ bool ax_probe(const AxView& A, uint32_t fp, uint32_t&
                 me |= (empty ? 1u : 0u) << t;
                 mm |= ((!empty && fps[t] == fp) ? 1u : 0u) << t;
             }
-            const uint32_t from = s >= 8u ? 0u : (0xFFu << s) & 0xFFu;
+            const uint32_t from = s >= 8u ? 0u : ((0xFFu << s) & 0xFFu);
             mm &= from;
             me &= from;
             const uint32_t fm = mm ? (uint32_t)__builtin_ctz(mm) : 8u, fe = me ? (uint32_t)__builtin_ctz(me) : 8u;
@@ -295,9 +350,21 @@ __device__ __forceinline__ bool ax_probe(const AxView& A, uint32_t fp, uint32_t&
     return found;
 }
 
-template <int MODE, bool PAIRED, bool LDS_HIST, bool EM, int NWC>
-__global__ __launch_bounds__(BLOCK_THREADS) void k_scan_ax(AxView A, UnitSrc src, unsigned long long* __restrict__ out_a,
+template <int MODE>
+constexpr uint32_t ax_wave_bytes() {
+    // pk | vw | (local: cg, rbase) | deferred list (u16) | counters | ambiguity | off0
+    return 8u * 64u * (AX_PKW + AX_VWW + (MODE == KM_LOCAL ? AX_CGW + 1u : 0u)) + 2u * AX_DEF + 16u + 8u * 64u + 64u;
+}
+
+#ifndef SPEQ_AX_MIN_WAVES  // minimum waves per SIMD the register allocator must allow (A/B knob)
+#define SPEQ_AX_MIN_WAVES 4
+#endif
+template <int MODE, bool PAIRED, bool LDS_HIST, bool EM, int NWC, int CW>
+__global__ __launch_bounds__(BLOCK_THREADS, SPEQ_AX_MIN_WAVES) void k_scan_ax(AxView A, UnitSrc src, unsigned long long* __restrict__ out_a,
                                                            double* __restrict__ out_w) {
+    using C = AxCls<CW>;
+    constexpr uint32_t PER = C::PER;
+    constexpr uint32_t RUNW = AX_RUN / PER;  // class dwords of one run
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -309,15 +376,14 @@ __global__ __launch_bounds__(BLOCK_THREADS) void k_scan_ax(AxView A, UnitSrc src
     double2* qtab = reinterpret_cast<double2*>(smem + hist_bytes);  // KM_LOCAL
     double* wtab = reinterpret_cast<double*>(qtab + QLUT_LEN);
     const uint32_t qtab_bytes = MODE == KM_LOCAL ? QTAB_BYTES : 0u;
-    constexpr uint32_t WAVE_BYTES = 8u * 64u * (AX_PKW + AX_VWW + (MODE == KM_LOCAL ? AX_CGW + 1u : 0u)) +
-                                    4u * AX_DEF + 16u + 8u * 64u + 64u;
+    constexpr uint32_t WAVE_BYTES = ax_wave_bytes<MODE>();
     unsigned char* wb = smem + hist_bytes + qtab_bytes + wid * WAVE_BYTES;
     uint64_t* pk = reinterpret_cast<uint64_t*>(wb);                 // [AX_PKW][64]
     uint64_t* vwl = pk + AX_PKW * 64u;                               // [AX_VWW][64]
     uint64_t* cg = vwl + AX_VWW * 64u;                               // [AX_CGW][64] (local)
     uint64_t* rbase = cg + (MODE == KM_LOCAL ? AX_CGW * 64u : 0u);   // [64] (local): segment start offsets
-    uint32_t* defl = reinterpret_cast<uint32_t*>(rbase + (MODE == KM_LOCAL ? 64u : 0u));  // [AX_DEF]
-    uint32_t* defn = defl + AX_DEF;                                  // [4]
+    uint16_t* defl = reinterpret_cast<uint16_t*>(rbase + (MODE == KM_LOCAL ? 64u : 0u));  // [AX_DEF]
+    uint32_t* defn = reinterpret_cast<uint32_t*>(defl + AX_DEF);     // [4]: entries, survivors
     int32_t* ambf = reinterpret_cast<int32_t*>(defn + 4);            // [64] first counted group
     int32_t* ambd = ambf + 64;                                       // [64] another group seen
     uint8_t* off0s = reinterpret_cast<uint8_t*>(ambd + 64);          // [64] alignment slack of each lane's stream
@@ -335,10 +401,16 @@ __global__ __launch_bounds__(BLOCK_THREADS) void k_scan_ax(AxView A, UnitSrc src
     __syncthreads();
     unsigned long long* gU = out_a + 2;
 
-    // class loads go through a buffer descriptor (dword-aligned 16-B loads; a lane without a run gets an out-of-range
-    // offset, which issues no memory request)
+    // every table is read through a buffer descriptor: 16-B loads need only dword alignment, and a lane that has
+    // nothing to load gets an out-of-range offset, which issues no memory request
     const __amdgpu_buffer_rsrc_t rs_cls =
-        __builtin_amdgcn_make_buffer_rsrc((void*)A.cls, (short)0, (int)(uint32_t)((A.n + 256u) * 4u), 0x00020000);
+        __builtin_amdgcn_make_buffer_rsrc((void*)A.cls, (short)0, (int)(uint32_t)A.cls_bytes, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rs_atab =
+        __builtin_amdgcn_make_buffer_rsrc((void*)A.atab, (short)0, (int)(uint32_t)(A.nb * 64u), 0x00020000);
+    const __amdgpu_buffer_rsrc_t rs_t2 =
+        __builtin_amdgcn_make_buffer_rsrc((void*)A.t2, (short)0, (int)(uint32_t)A.t2_bytes, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rs_filt =
+        __builtin_amdgcn_make_buffer_rsrc((void*)A.filt, (short)0, (int)(uint32_t)(A.nf * 8u), 0x00020000);
     const uint64_t NWV = (uint64_t)gridDim.x * WAVES_PER_BLOCK;
     const uint64_t gw = (uint64_t)blockIdx.x * WAVES_PER_BLOCK + wid;
     const uint64_t nu = PAIRED ? src.n_units / 2 : src.n_units;
@@ -349,22 +421,20 @@ __global__ __launch_bounds__(BLOCK_THREADS) void k_scan_ax(AxView A, UnitSrc src
 
     uint32_t t_cnt = 0, amb = 0;
 
-    // run-length tally of the current lane (flushed when the group changes)
-    int32_t run_g = -1;
-    uint32_t run_n = 0;
-    double run_w = 0.0;
-    auto flush = [&]() {
-        if (run_n) {
-            if (LDS_HIST) {
-                atomicAdd(&hA[run_g], (unsigned long long)run_n);
-                if (MODE == KM_LOCAL) atomicAdd(&hW[run_g], run_w);
-            } else {
-                atomicAdd(&gU[run_g], (unsigned long long)run_n);
-                if (MODE == KM_LOCAL) atomicAdd(&out_w[run_g], run_w);
-            }
+    auto add_count = [&](uint32_t g, uint32_t cnt, double wsum) {
+        if (LDS_HIST) {
+            atomicAdd(&hA[g], (unsigned long long)cnt);
+            if (MODE == KM_LOCAL) atomicAdd(&hW[g], wsum);
+        } else {
+            atomicAdd(&gU[g], (unsigned long long)cnt);
+            if (MODE == KM_LOCAL) atomicAdd(&out_w[g], wsum);
         }
-        run_n = 0;
-        run_w = 0.0;
+    };
+    // one class from a text position (phase 2)
+    auto load_class = [&](uint32_t p, bool act) -> uint32_t {
+        const uint32_t by = p * (uint32_t)CW;
+        const uint32_t v = __builtin_amdgcn_raw_buffer_load_b32(rs_cls, act ? (by & ~3u) : AX_OOB, 0, 0);
+        return (v >> (8u * (by & 3u))) & C::SENT;
     };
 
     for (uint64_t r0 = r_begin; r0 < r_end; r0 += 64) {
@@ -393,12 +463,29 @@ __global__ __launch_bounds__(BLOCK_THREADS) void k_scan_ax(AxView A, UnitSrc src
             uint32_t qprev = 0;
             const uint32_t qt = 33u + src.cutoff;  // Phred+33 byte <= qt  <=>  clamp(q, 0, 41) <= cutoff (cutoff < 41)
             const uint32_t qt4 = (qt > 0x7Fu ? 0x7Fu : qt) * 0x01010101u;
+            const uint32_t allbad = src.cutoff >= 41u ? 0x80808080u : 0u;  // every window fails the quality filter
+            // the chunks' loads are issued in two batches before any is used (a load per chunk under its own branch
+            // was sunk into the branch and waited for one chunk at a time); lanes past their read load a chunk they
+            // own and ignore it
+            const uint8_t* sb0 = src.seq + (nch ? a16 : 0ull);
+            const uint8_t* qb0 = src.qual + (nch ? a16 : 0ull);
+            const uint32_t clast = nch ? nch - 1u : 0u;
+            constexpr uint32_t HALF = (AX_CHUNKS + 1) / 2;
 #pragma unroll
-            for (uint32_t c = 0; c < AX_CHUNKS; ++c) {
-                if (c < nch) {
-                    const uint4 sv = *reinterpret_cast<const uint4*>(src.seq + a16 + 16u * c);
-                    const uint4 qv = *reinterpret_cast<const uint4*>(src.qual + a16 + 16u * c);
-                    const uint32_t sd[4] = {sv.x, sv.y, sv.z, sv.w}, qd[4] = {qv.x, qv.y, qv.z, qv.w};
+            for (uint32_t h0 = 0; h0 < AX_CHUNKS; h0 += HALF) {
+                uint4 sv[HALF], qv[HALF];
+#pragma unroll
+                for (uint32_t t = 0; t < HALF; ++t) {
+                    const uint32_t cc = min(h0 + t, clast);
+                    sv[t] = *reinterpret_cast<const uint4*>(sb0 + 16u * cc);
+                    qv[t] = *reinterpret_cast<const uint4*>(qb0 + 16u * cc);
+                }
+#pragma unroll
+                for (uint32_t t = 0; t < HALF; ++t) {
+                    const uint32_t c = h0 + t;
+                    if (c >= AX_CHUNKS) break;
+                    const uint32_t sd[4] = {sv[t].x, sv[t].y, sv[t].z, sv[t].w};
+                    const uint32_t qd[4] = {qv[t].x, qv[t].y, qv[t].z, qv[t].w};
                     uint32_t codes = 0, bad = 0, chg = 0;
 #pragma unroll
                     for (int i = 0; i < 4; ++i) {
@@ -408,9 +495,7 @@ __global__ __launch_bounds__(BLOCK_THREADS) void k_scan_ax(AxView A, UnitSrc src
                         const uint32_t canon = __builtin_amdgcn_perm(0u, 0x74676361u, c4);  // the letter of that code
                         const uint32_t okb = zero_bytes(x ^ canon) | zero_bytes(x ^ 0x75757575u);  // ACGT or U
                         const uint32_t y = qd[i];
-                        const uint32_t badq = src.cutoff >= 41u
-                                                  ? 0x80808080u
-                                                  : (((0x80808080u | qt4) - (y & 0x7F7F7F7Fu)) & ~y & 0x80808080u);
+                        const uint32_t badq = (((0x80808080u | qt4) - (y & 0x7F7F7F7Fu)) & ~y & 0x80808080u) | allbad;
                         bad |= flags4((~okb & 0x80808080u) | badq) << (4 * i);
                         if (MODE == KM_LOCAL) {
                             const uint32_t prev = (y << 8) | (qprev >> 24);
@@ -418,10 +503,12 @@ __global__ __launch_bounds__(BLOCK_THREADS) void k_scan_ax(AxView A, UnitSrc src
                             qprev = y;
                         }
                     }
-                    reinterpret_cast<uint32_t*>(pk + (c >> 1) * 64u + lane)[c & 1u] = codes;
-                    badw[c >> 2] &= ~(0xFFFFull << (16u * (c & 3u)));
-                    badw[c >> 2] |= (uint64_t)bad << (16u * (c & 3u));
-                    if (MODE == KM_LOCAL) cgw[c >> 2] |= (uint64_t)chg << (16u * (c & 3u));
+                    if (c < nch) {
+                        reinterpret_cast<uint32_t*>(pk + (c >> 1) * 64u + lane)[c & 1u] = codes;
+                        badw[c >> 2] &= ~(0xFFFFull << (16u * (c & 3u)));
+                        badw[c >> 2] |= (uint64_t)bad << (16u * (c & 3u));
+                        if (MODE == KM_LOCAL) cgw[c >> 2] |= (uint64_t)chg << (16u * (c & 3u));
+                    }
                 }
             }
             // valid windows: AND of k consecutive "good" bits (doubling), then shifted to the read's first base
@@ -440,7 +527,6 @@ __global__ __launch_bounds__(BLOCK_THREADS) void k_scan_ax(AxView A, UnitSrc src
                 for (int i = 0; i < 4; ++i) ok[i] = nx[i];
                 len += sft;
             }
-            uint64_t vw[AX_VWW];
 #pragma unroll
             for (uint32_t i = 0; i < AX_VWW; ++i) {
                 const uint64_t lo = i < 4 ? ok[i] : 0ull, hi = i + 1 < 4 ? ok[i + 1] : 0ull;
@@ -448,7 +534,6 @@ __global__ __launch_bounds__(BLOCK_THREADS) void k_scan_ax(AxView A, UnitSrc src
                 const uint32_t bit0 = 64u * i;
                 if (wend <= bit0) v = 0;
                 else if (wend < bit0 + 64u) v &= (1ull << (wend - bit0)) - 1ull;
-                vw[i] = v;
                 vwl[i * 64u + lane] = v;
                 t_cnt += (uint32_t)__popcll(v);
             }
@@ -458,7 +543,10 @@ __global__ __launch_bounds__(BLOCK_THREADS) void k_scan_ax(AxView A, UnitSrc src
                 rbase[lane] = a;
             }
             off0s[lane] = (uint8_t)off0;
-            if (lane == 0) defn[0] = 0;
+            if (lane == 0) {
+                defn[0] = 0;
+                defn[1] = 0;
+            }
             wave_sync();
 
             // per-lane readers of the staged stream
@@ -475,7 +563,7 @@ __global__ __launch_bounds__(BLOCK_THREADS) void k_scan_ax(AxView A, UnitSrc src
 #pragma unroll
                 for (int i = (int)AX_VWW - 1; i >= 0; --i) {
                     const uint32_t b0 = 64u * (uint32_t)i;
-                    uint64_t v = vw[i];
+                    uint64_t v = vwl[(uint32_t)i * 64u + lane];
                     if (j > b0) v = (j - b0 >= 64u) ? 0ull : (v & (~0ull << (j - b0)));
                     if (v) res = b0 + (uint32_t)__builtin_ctzll(v);
                 }
@@ -483,10 +571,10 @@ __global__ __launch_bounds__(BLOCK_THREADS) void k_scan_ax(AxView A, UnitSrc src
             };
             auto defer_push = [&](uint32_t o, uint32_t jj) -> bool {
                 const uint32_t slot = atomicAdd(&defn[0], 1u);
-                if (slot < AX_DEF) defl[slot] = o | (jj << 6);
+                if (slot < AX_DEF) defl[slot] = (uint16_t)(o | (jj << 6));
                 return slot < AX_DEF;
             };
-            // Phred weight of window jj (bases a + jj ..) of the read whose segment starts at `base` (global offset)
+            // Phred weight of a window whose first quality byte is at qbase (fm_scanner.cpp:454)
             auto weight = [&](const uint8_t* qbase, bool uniform, uint32_t qcur) -> double {
                 if (uniform) return wtab[qcur];
                 double x = 1.0;
@@ -494,217 +582,337 @@ __global__ __launch_bounds__(BLOCK_THREADS) void k_scan_ax(AxView A, UnitSrc src
                     int q = (int)qbase[i] - 33;
                     q = q < 0 ? 0 : (q > 41 ? 41 : q);
                     const double2 t = qtab[q];
-                    x = div_rn(x, t.x, t.y);  // == x / t.x (fm_scanner.cpp:454)
+                    x = div_rn(x, t.x, t.y);  // == x / t.x
                 }
                 return x;
             };
-            auto uniform_at = [&](uint32_t o, uint32_t off0o, uint32_t jj) -> bool {  // no quality change in (jj, jj + k)
-                // stream bits [off0o + jj + 1, off0o + jj + k): k - 1 <= 127 bits over <= 3 words
-                uint32_t b = off0o + jj + 1u, left = k - 1u;
+            // quality-change bits of lane o's stream over bases [off0o + b, off0o + b + len) all zero (local mode)
+            auto chg_zero = [&](uint32_t o, uint32_t off0o, uint32_t b, uint32_t len) -> bool {
+                uint32_t x = off0o + b, left = len;
                 bool u = true;
                 while (left) {
-                    const uint32_t w = b >> 6, sh = b & 63u, span = min(64u - sh, left);
-                    const uint64_t m = span == 64u ? ~0ull : ((1ull << span) - 1ull);
-                    u = u && ((cg[w * 64u + o] >> sh) & m) == 0;
-                    b += span;
+                    const uint32_t w = x >> 6, sh = x & 63u, span = min(64u - sh, left);
+                    const uint64_t mk = span == 64u ? ~0ull : ((1ull << span) - 1ull);
+                    u = u && (w >= AX_CGW || ((cg[w * 64u + o] >> sh) & mk) == 0);
+                    x += span;
                     left -= span;
                 }
                 return u;
             };
 
-            // ---- phase 1: one read per lane
+            // ---- phase 1: one read per lane, one memory round trip per iteration: a lane either probes the anchor
+            // table (its candidate is compared in the next iteration) or extends a run by up to AX_RUN windows
             uint32_t j = 0;
-            bool lookup = true;        // the next window needs an anchor lookup
-            uint64_t p = 0;            // text position of window j when !lookup
+            uint32_t st = wend > 0 ? 0u : 2u;  // 0: look window j up, 1: extend from text position p, 2: done
+            bool verify = false;       // st 1: p came from the anchor table (window j itself not compared yet)
+            uint64_t p = 0;
             int32_t last_mm = -1;      // base (relative to the segment) of the last observed mismatch
-            uint32_t rb_b = 0, rb_s = 0;  // probe resume after a failed verification
-            bool resume = false;
-            int32_t qpos = -1;         // local mode: window whose (uniform) quality is qcur
-            uint32_t qcur = 0;
+            uint32_t pb = 0, ps = 0;   // probe position of the current lookup (bucket, first slot)
+            bool resume = false;       // continue the current lookup at (pb, ps): full bucket, or failed verification
+            uint32_t gcur = C::NONE;   // the group of this read's last counted run (the fast path's guess)
             for (;;) {
-                if (lookup && j < wend) j = next_valid(j);
-                const bool act = j < wend;
-                if (__ballot(act) == 0) break;
+                if (st == 0u) {
+                    j = next_valid(j);
+                    if (j >= wend) st = 2u;
+                }
+                if (__ballot(st != 2u) == 0) break;
+                const bool lk = st == 0u, rn = st == 1u;
                 uint64_t ra[NWC];
                 read_words(lane, off0 + j, ra);
-                // anchor lookup
-                uint32_t pp = 0;
-                const bool need = act && lookup;
                 const uint64_t h = ax_hash<NWC>(ra, k);
-                if (need && !resume) {
-                    rb_b = ax_bucket(h, A.nb);
-                    rb_s = 0;
+                if (lk && !resume) {
+                    pb = ax_bucket(h, A.nb);
+                    ps = 0;
                 }
-                if (need) resume = false;
-                const bool cand = ax_probe(A, (uint32_t)h, rb_b, rb_s, pp, need);
-                const bool have = act && (!lookup || cand);
-                const uint64_t pt = lookup ? (uint64_t)pp : p;
-                // text words and the classes of up to AX_RUN windows at pt (both depend only on pt)
-                uint64_t tw[NWC];
-                uint32_t cv[AX_RUN];
-                {
-                    const uint64_t ps = have ? pt : 0;
-                    ax_text_words<NWC>(A.t2, ps, tw);
-                    const uint32_t boff = have ? (uint32_t)(ps * 4u) : AX_OOB;
+                // ---- this iteration's loads: a bucket (lookup lanes), text words + classes (run lanes), the quality
+                // of window j (local mode); a group is issued only when some lane of the wave needs it
+                u32x4 q0 = {0u, 0u, 0u, 0u}, q1 = q0, q2 = q0, q3 = q0;
+                if (__ballot(lk) != 0) {
+                    const uint32_t boff = lk ? pb * 64u : AX_OOB;
+                    q0 = __builtin_amdgcn_raw_buffer_load_b128(rs_atab, boff, 0, 0);
+                    q1 = __builtin_amdgcn_raw_buffer_load_b128(rs_atab, boff + 16u, 0, 0);
+                    q2 = __builtin_amdgcn_raw_buffer_load_b128(rs_atab, boff + 32u, 0, 0);
+                    q3 = __builtin_amdgcn_raw_buffer_load_b128(rs_atab, boff + 48u, 0, 0);
+                }
+                uint64_t traw[NWC + 1];
+                uint32_t craw[RUNW + 1];
+                uint32_t qj = 0;
+                const bool any_rn = __ballot(rn) != 0;
+                if (any_rn) {
+                    const uint32_t toff = rn ? (uint32_t)((p >> 5) * 8u) : AX_OOB;
 #pragma unroll
-                    for (uint32_t c = 0; c < AX_RUN / 4; ++c) {
-                        const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rs_cls, boff + 16u * c, 0, 0);
-                        cv[4 * c] = v[0];
-                        cv[4 * c + 1] = v[1];
-                        cv[4 * c + 2] = v[2];
-                        cv[4 * c + 3] = v[3];
+                    for (int i = 0; i <= NWC; ++i) {
+                        const u32x2 v = __builtin_amdgcn_raw_buffer_load_b64(rs_t2, toff + 8u * (uint32_t)i, 0, 0);
+                        traw[i] = (uint64_t)v[0] | ((uint64_t)v[1] << 32);
                     }
-                }
-                // compare read [j, j + cmpb) with text [pt, pt + cmpb): e = bases equal before the first mismatch
-                uint32_t e = cmpb;
+                    const uint32_t cby = (uint32_t)(p * (uint32_t)CW);
+                    const uint32_t coff = rn ? (cby & ~3u) : AX_OOB;
 #pragma unroll
-                for (int i = NWC - 1; i >= 0; --i) {
-                    uint64_t x = ra[i] ^ tw[i];
-                    const uint32_t b0 = 32u * (uint32_t)i;
-                    if (cmpb <= b0) x = 0;
-                    else if (cmpb < b0 + 32u) x &= (1ull << (2u * (cmpb - b0))) - 1ull;
-                    if (x) e = b0 + ((uint32_t)__builtin_ctzll(x) >> 1);
-                }
-                bool absent = act && lookup && !cand;
-                bool fpfail = false;
-                if (have && lookup && e < k) {  // fingerprint collision: resume probing after that slot
-                    fpfail = true;
-                    resume = true;
-                    ++rb_s;
-                }
-                const bool run = have && !fpfail;
-                uint32_t R = 0;
-                if (run) {
-                    R = e >= k - 1u ? e - (k - 1u) : 0u;
-                    R = min(R, AX_RUN);
-                    R = min(R, wend - j);
-                }
-                // ---- absent anchor: defer the windows that share the mismatch (or the next k - 1), skip past them
-                if (absent) {
-                    uint32_t dend = (last_mm >= (int32_t)j && last_mm < (int32_t)(j + k)) ? (uint32_t)last_mm : j + k - 1u;
-                    dend = min(dend, wend - 1u);
-                    uint32_t cnt = 0;
-                    for (uint32_t w = j + 1; w <= dend; ++w) cnt += (uint32_t)((vwl[(w >> 6) * 64u + lane] >> (w & 63u)) & 1u);
-                    bool ok_def = true;
-                    if (cnt) {
-                        const uint32_t slot0 = atomicAdd(&defn[0], cnt);
-                        ok_def = slot0 + cnt <= AX_DEF;
-                        if (ok_def) {
-                            uint32_t sl = slot0;
-                            for (uint32_t w = j + 1; w <= dend; ++w)
-                                if ((vwl[(w >> 6) * 64u + lane] >> (w & 63u)) & 1u) defl[sl++] = lane | (w << 6);
-                        } else {  // no room: the windows stay in this pass; void the slots reserved below the end
-                            for (uint32_t sl = slot0; sl < AX_DEF && sl < slot0 + cnt; ++sl) defl[sl] = AX_VOID;
-                        }
+                    for (uint32_t c = 0; c < RUNW / 4; ++c) {
+                        const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rs_cls, coff + 16u * c, 0, 0);
+                        craw[4 * c] = v[0];
+                        craw[4 * c + 1] = v[1];
+                        craw[4 * c + 2] = v[2];
+                        craw[4 * c + 3] = v[3];
                     }
-                    j = ok_def ? dend + 1u : j + 1u;
-                    lookup = true;
-                    last_mm = -1;
+                    craw[RUNW] = __builtin_amdgcn_raw_buffer_load_b32(rs_cls, coff + 4u * RUNW, 0, 0);
+                    if (MODE == KM_LOCAL) qj = src.qual[a + (rn ? j : 0u)];
                 }
-                // ---- tally the run: windows j .. j + R - 1 at text positions pt .. pt + R - 1
-                uint32_t vwin = 0;
-                if (run) {
-                    const uint32_t w0 = j >> 6, sh = j & 63u;
-                    uint64_t lo = 0, hi = 0;
+
+                // ---- lookup lanes: resolve the bucket
+                if (lk) {
+                    const uint32_t fps[8] = {q0[0], q0[2], q1[0], q1[2], q2[0], q2[2], q3[0], q3[2]};
+                    const uint32_t pos[8] = {q0[1], q0[3], q1[1], q1[3], q2[1], q2[3], q3[1], q3[3]};
+                    uint32_t mm = 0, me = 0;
 #pragma unroll
-                    for (uint32_t i = 0; i < AX_VWW; ++i) {
-                        lo = w0 == i ? vw[i] : lo;
-                        hi = w0 + 1u == i ? vw[i] : hi;
+                    for (int t = 0; t < 8; ++t) {
+                        const bool empty = pos[t] == AX_EMPTY;
+                        me |= (empty ? 1u : 0u) << t;
+                        mm |= ((!empty && fps[t] == (uint32_t)h) ? 1u : 0u) << t;
                     }
-                    vwin = (uint32_t)funnel(lo, hi, sh);
-                }
-                bool stop = false;
-                uint32_t rstop = R;
+                    const uint32_t from = ps >= 8u ? 0u : ((0xFFu << ps) & 0xFFu);
+                    mm &= from;
+                    me &= from;
+                    const uint32_t fm = mm ? (uint32_t)__builtin_ctz(mm) : 8u, fe = me ? (uint32_t)__builtin_ctz(me) : 8u;
+                    if (fm < fe) {  // candidate: compared with the text in the next iteration
+                        uint32_t pp = pos[0];
 #pragma unroll
-                for (uint32_t c = 0; c < AX_RUN / 4; ++c) {
-                    if (__ballot(run && 4u * c < R) == 0) break;
-#pragma unroll
-                    for (uint32_t t = 0; t < 4; ++t) {
-                        const uint32_t d = 4u * c + t;
-                        const uint32_t cl = cv[d];
-                        bool v = run && !stop && d < R && ((vwin >> d) & 1u);
-                        if (v && cl == AX_SENT) {  // matched bases, but no valid text window there: look it up later
-                            v = false;
-                            if (!defer_push(lane, j + d)) {
-                                stop = true;
-                                rstop = d;
+                        for (int t = 1; t < 8; ++t) pp = fm == (uint32_t)t ? pos[t] : pp;
+                        p = pp;
+                        ps = fm;
+                        st = 1u;
+                        verify = true;
+                        resume = false;
+                    } else if (fe < 8u) {
+                        // absent: defer the windows that share the mismatch (or the next k - 1), skip past them
+                        resume = false;
+                        uint32_t dend = (last_mm >= (int32_t)j && last_mm < (int32_t)(j + k)) ? (uint32_t)last_mm
+                                                                                               : j + k - 1u;
+                        dend = min(dend, wend - 1u);
+                        uint32_t cnt = 0;
+                        for (uint32_t w = j + 1; w <= dend; ++w)
+                            cnt += (uint32_t)((vwl[(w >> 6) * 64u + lane] >> (w & 63u)) & 1u);
+                        bool ok_def = true;
+                        if (cnt) {
+                            const uint32_t slot0 = atomicAdd(&defn[0], cnt);
+                            ok_def = slot0 + cnt <= AX_DEF;
+                            if (ok_def) {
+                                uint32_t sl = slot0;
+                                for (uint32_t w = j + 1; w <= dend; ++w)
+                                    if ((vwl[(w >> 6) * 64u + lane] >> (w & 63u)) & 1u)
+                                        defl[sl++] = (uint16_t)(lane | (w << 6));
+                            } else {  // no room: the windows stay with this lane; void the slots reserved below the end
+                                for (uint32_t sl = slot0; sl < AX_DEF && sl < slot0 + cnt; ++sl) defl[sl] = AX_VOID;
                             }
                         }
-                        if (v && cl < G) {
-                            double wgt = 0.0;
-                            if (MODE == KM_LOCAL) {
-                                const uint32_t jj = j + d;
-                                const bool uni = uniform_at(lane, off0, jj);
-                                if (uni && !(qpos >= 0 && jj - (uint32_t)qpos < k)) {
-                                    int q = (int)src.qual[a + jj] - 33;
-                                    qcur = (uint32_t)(q < 0 ? 0 : (q > 41 ? 41 : q));
-                                    qpos = (int32_t)jj;
-                                } else if (uni) {
-                                    qpos = (int32_t)jj;
-                                }
-                                wgt = weight(src.qual + a + jj, uni, qcur);
-                            }
-                            if ((int32_t)cl != run_g) {
-                                flush();
-                                run_g = (int32_t)cl;
-                            }
-                            ++run_n;
-                            if (MODE == KM_LOCAL) run_w += wgt;
-                            if (af < 0) af = (int32_t)cl;
-                            else if ((int32_t)cl != af) ad = 1;
-                        } else if (EM && v && (cl & AX_MULTI)) {
-                            const uint32_t lo = cl & ~AX_MULTI;
-                            atomicAdd(&src.em_mult[lo], 1u);
-                            src.em_hi[lo] = A.mhi[lo];
-                        }
-                    }
-                }
-                if (run) {
-                    if (stop) {
-                        j += rstop;
-                        lookup = true;
+                        j = ok_def ? dend + 1u : j + 1u;
                         last_mm = -1;
+                    } else {  // full bucket without the key or an empty slot: the next bucket
+                        pb = pb + 1u == (uint32_t)A.nb ? 0u : pb + 1u;
+                        ps = 0;
+                        resume = true;
+                    }
+                }
+
+                // ---- run lanes: compare read [j, j + cmpb) with text [p, p + cmpb), classify the matched windows
+                if (any_rn && rn) {
+                    const uint32_t sh = 2u * (uint32_t)(p & 31u);
+                    uint32_t e = cmpb;
+#pragma unroll
+                    for (int i = NWC - 1; i >= 0; --i) {
+                        uint64_t x = ra[i] ^ funnel(traw[i], traw[i + 1], sh);
+                        const uint32_t b0 = 32u * (uint32_t)i;
+                        if (cmpb <= b0) x = 0;
+                        else if (cmpb < b0 + 32u) x &= (1ull << (2u * (cmpb - b0))) - 1ull;
+                        if (x) e = b0 + ((uint32_t)__builtin_ctzll(x) >> 1);
+                    }
+                    if (verify && e < k) {  // fingerprint collision: resume probing after that slot
+                        st = 0u;
+                        resume = true;
+                        ++ps;
                     } else {
-                        const bool mism = e < cmpb;  // the run ended at a mismatch (base j + e)
-                        if (mism && R < wend - j) last_mm = (int32_t)(j + e);
-                        j += R;
-                        if (mism || R == 0) {
-                            lookup = true;
-                        } else {
-                            lookup = false;
-                            p = pt + R;
+                        uint32_t R = e - (k - 1u);  // e >= k - 1: a candidate matched k bases, a run k - 1
+                        R = min(R, AX_RUN);
+                        R = min(R, wend - j);
+                        uint64_t m;
+                        {
+                            const uint32_t w0 = j >> 6, s6 = j & 63u;
+                            const uint64_t lo = vwl[w0 * 64u + lane];
+                            const uint64_t hi = w0 + 1u < AX_VWW ? vwl[(w0 + 1u) * 64u + lane] : 0ull;
+                            m = funnel(lo, hi, s6) & (R >= 64u ? ~0ull : ((1ull << R) - 1ull));
                         }
-                        if (R == 0) lookup = true;
+                        // the run's classes, aligned so that window d is element d
+                        const uint32_t ca = (uint32_t)(p * (uint32_t)CW) & 3u;
+                        uint32_t cw[RUNW];
+#pragma unroll
+                        for (uint32_t i = 0; i < RUNW; ++i) cw[i] = __builtin_amdgcn_alignbyte(craw[i + 1], craw[i], ca);
+                        // One group per run: g = this read's group so far (else the run's first window's, when single).
+                        // A branch-free pass finds d0, the first valid window that is neither g nor multi-group
+                        // (another group, or SENT); windows [0, d0) are tallied at once and the run is cut at d0, which
+                        // starts the next iteration (with that group as g, or deferred when SENT).
+                        const uint32_t c0 = cw[0] & C::SENT;
+                        const uint32_t g = gcur != C::NONE ? gcur : (c0 < G ? c0 : C::NONE);
+                        const uint32_t gr = g * C::REP, mr = C::MULTI * C::REP;
+                        uint32_t cnt = 0, fo = RUNW, fflags = 0;
+                        uint64_t gm = 0, mm = 0;  // bit d: window d is g (local mode) / multi-group (EM)
+#pragma unroll
+                        for (uint32_t i = 0; i < RUNW; ++i) {
+                            const uint32_t vm = spread<CW>((uint32_t)(m >> (PER * i)) & ((1u << PER) - 1u));
+                            const uint32_t eg = zero_elems<CW>(cw[i] ^ gr) & vm;
+                            const uint32_t em = zero_elems<CW>(cw[i] ^ mr) & vm;
+                            const uint32_t ot = vm & ~(eg | em);
+                            const bool before = fo == RUNW;
+                            const uint32_t below = ot ? ((ot & (0u - ot)) - 1u) : ~0u;  // elements before the first other
+                            cnt += before ? (uint32_t)__popc(eg & below) : 0u;
+                            if (MODE == KM_LOCAL)
+                                gm |= (uint64_t)(CW == 1 ? flags4(eg) : (((eg >> 15) & 1u) | ((eg >> 30) & 2u))) << (PER * i);
+                            if (EM)
+                                mm |= (uint64_t)(CW == 1 ? flags4(em) : (((em >> 15) & 1u) | ((em >> 30) & 2u))) << (PER * i);
+                            fflags = (before && ot) ? ot : fflags;
+                            fo = (before && ot) ? i : fo;
+                        }
+                        const uint32_t d0 = fo == RUNW ? AX_RUN : PER * fo + (uint32_t)__builtin_ctz(fflags) / (8u * CW);
+                        const bool cut = d0 < R;
+                        const uint32_t Rc = cut ? d0 : R;  // windows tallied in this iteration
+                        const uint64_t mRc = Rc >= 64u ? ~0ull : ((1ull << Rc) - 1ull);
+                        if (cnt) {
+                            double wsum = 0.0;
+                            if (MODE == KM_LOCAL) {
+                                // one quality for the whole cut run when no base in (j, j + Rc - 1 + k) changes it
+                                if (chg_zero(lane, off0, j + 1u, Rc + k - 2u)) {
+                                    int q = (int)qj - 33;
+                                    q = q < 0 ? 0 : (q > 41 ? 41 : q);
+                                    wsum = (double)cnt * wtab[q];
+                                } else {
+                                    uint64_t todo = gm & mRc;
+                                    while (todo) {
+                                        const uint32_t d = (uint32_t)__builtin_ctzll(todo);
+                                        todo &= todo - 1;
+                                        const uint32_t jj = j + d;
+                                        const uint8_t* qb = src.qual + a + jj;
+                                        int q = (int)qb[0] - 33;
+                                        q = q < 0 ? 0 : (q > 41 ? 41 : q);
+                                        wsum += weight(qb, chg_zero(lane, off0, jj + 1u, k - 1u), (uint32_t)q);
+                                    }
+                                }
+                            }
+                            add_count(g, cnt, wsum);
+                            if (af < 0) af = (int32_t)g;
+                            else if ((int32_t)g != af) ad = 1;
+                            gcur = g;
+                        }
+                        if (EM) {  // multi-group windows of the cut run: the EM histogram
+                            uint64_t todo = mm & mRc;
+                            while (todo) {
+                                const uint32_t d = (uint32_t)__builtin_ctzll(todo);
+                                todo &= todo - 1;
+                                const uint32_t lo = A.mlo[p + d];
+                                atomicAdd(&src.em_mult[lo], 1u);
+                                src.em_hi[lo] = A.mhi[lo];
+                            }
+                        }
+                        // next state
+                        if (cut) {
+                            uint32_t x = cw[0];
+#pragma unroll
+                            for (uint32_t i = 1; i < RUNW; ++i) x = (fo == i) ? cw[i] : x;
+                            const uint32_t cl = (x >> (8u * CW * (d0 % PER))) & C::SENT;
+                            uint32_t adv = d0;
+                            if (cl == C::SENT) {  // matched bases, but no valid text window there: looked up later
+                                if (defer_push(lane, j + d0)) {
+                                    adv = d0 + 1u;
+                                    st = 1u;
+                                } else {
+                                    st = 0u;  // the list is full: look that window up now
+                                    last_mm = -1;
+                                }
+                            } else {
+                                gcur = cl;  // another group: the next iteration tallies from d0 with it
+                                st = 1u;
+                            }
+                            j += adv;
+                            p += adv;
+                            verify = false;
+                        } else {
+                            const bool mism = e < cmpb;  // the run ended at a mismatch (base j + e)
+                            if (mism && R < wend - j) last_mm = (int32_t)(j + e);
+                            j += R;
+                            p += R;
+                            verify = false;
+                            st = (mism || R == 0u) ? 0u : 1u;
+                        }
+                        if (j >= wend) st = 2u;
                     }
                 }
             }
-            flush();
 
-            // ---- phase 2: the deferred windows of the wave, one per lane
+            // ---- phase 2: the deferred windows of the wave. (a) the Bloom filter, AX_F windows per lane per round
+            // trip; the windows it cannot rule out are compacted to the front of the list; (b) those are looked up one
+            // per lane (bucket -> fingerprint -> compare with the text -> class)
             ambf[lane] = af;
             ambd[lane] = ad;
             wave_sync();
             const uint32_t n2 = min(__builtin_amdgcn_readfirstlane(defn[0]), AX_DEF);
-            for (uint32_t base = 0; base < n2; base += 64) {
+            for (uint32_t base = 0; base < n2; base += 64u * AX_F) {
+                uint32_t ent[AX_F];
+                uint64_t hh[AX_F];
+                uint64_t fw[AX_F];
+#pragma unroll
+                for (uint32_t t = 0; t < AX_F; ++t) {
+                    const uint32_t idx = base + 64u * t + lane;
+                    const uint16_t e16 = idx < n2 ? defl[idx] : AX_VOID;
+                    ent[t] = e16 == AX_VOID ? AX_EMPTY : (uint32_t)e16;
+                    const uint32_t o = ent[t] & 63u, jj = (ent[t] >> 6) & 1023u;
+                    uint64_t ra[NWC];
+                    read_words(o, off0s[o] + jj, ra);
+                    hh[t] = ax_hash<NWC>(ra, k);
+                }
+#pragma unroll
+                for (uint32_t t = 0; t < AX_F; ++t) {
+                    const uint32_t foff = ent[t] != AX_EMPTY ? ax_fword(hh[t], A.nf) * 8u : AX_OOB;
+                    const u32x2 v = __builtin_amdgcn_raw_buffer_load_b64(rs_filt, foff, 0, 0);
+                    fw[t] = (uint64_t)v[0] | ((uint64_t)v[1] << 32);
+                }
+                wave_sync();  // every lane has read its entries before any survivor overwrites the list's front
+#pragma unroll
+                for (uint32_t t = 0; t < AX_F; ++t) {
+                    const uint64_t bits = ax_fbits(hh[t]);
+                    if (ent[t] != AX_EMPTY && (fw[t] & bits) == bits) {
+                        const uint32_t slot = atomicAdd(&defn[1], 1u);
+                        defl[slot] = (uint16_t)ent[t];
+                    }
+                }
+                wave_sync();
+            }
+            const uint32_t n3 = __builtin_amdgcn_readfirstlane(defn[1]);
+            for (uint32_t base = 0; base < n3; base += 64) {
                 const uint32_t idx = base + lane;
-                const bool act = idx < n2;
-                uint32_t ent = act ? defl[idx] : AX_VOID;
-                const bool act2 = ent != AX_VOID;
-                if (!act2) ent = 0u;
+                const bool act = idx < n3;
+                const uint32_t ent = act ? (uint32_t)defl[idx] : 0u;
                 const uint32_t o = ent & 63u, jj = ent >> 6;
                 const uint32_t off0o = off0s[o];
                 uint64_t ra[NWC];
                 read_words(o, off0o + jj, ra);
                 const uint64_t h = ax_hash<NWC>(ra, k);
-                uint32_t b = act2 ? ax_bucket(h, A.nb) : 0u, sl = 0, pp = 0;
-                bool pend = act2, found = false;
-                uint32_t cl = AX_SENT;
+                uint32_t b = act ? ax_bucket(h, A.nb) : 0u, sl = 0, pp = 0;
+                bool pend = act, found = false;
+                uint32_t cl = C::SENT;
                 while (__ballot(pend) != 0) {
-                    const bool c = ax_probe(A, (uint32_t)h, b, sl, pp, pend);
+                    const bool c = ax_probe(A, rs_atab, (uint32_t)h, b, sl, pp, pend);
+                    const bool cand = pend && c;
                     uint64_t tw[NWC];
-                    ax_text_words<NWC>(A.t2, (pend && c) ? pp : 0u, tw);
-                    const u32x4 cvv = __builtin_amdgcn_raw_buffer_load_b128(rs_cls, (pend && c) ? pp * 4u : AX_OOB,
-                                                                             0, 0);
+                    {
+                        const uint32_t toff = cand ? (pp >> 5) * 8u : AX_OOB;
+                        uint64_t raw[NWC + 1];
+#pragma unroll
+                        for (int i = 0; i <= NWC; ++i) {
+                            const u32x2 v = __builtin_amdgcn_raw_buffer_load_b64(rs_t2, toff + 8u * (uint32_t)i, 0, 0);
+                            raw[i] = (uint64_t)v[0] | ((uint64_t)v[1] << 32);
+                        }
+#pragma unroll
+                        for (int i = 0; i < NWC; ++i) tw[i] = funnel(raw[i], raw[i + 1], 2u * (pp & 31u));
+                    }
+                    const uint32_t cc = load_class(pp, cand);
                     if (pend) {
                         if (!c) {
                             pend = false;  // absent
@@ -720,7 +928,7 @@ __global__ __launch_bounds__(BLOCK_THREADS) void k_scan_ax(AxView A, UnitSrc src
                             }
                             if (eq) {
                                 found = true;
-                                cl = cvv[0];
+                                cl = cc;
                                 pend = false;
                             } else {
                                 ++sl;  // fingerprint collision: keep probing
@@ -732,22 +940,16 @@ __global__ __launch_bounds__(BLOCK_THREADS) void k_scan_ax(AxView A, UnitSrc src
                     double wgt = 0.0;
                     if (MODE == KM_LOCAL) {
                         const uint8_t* qb = src.qual + rbase[o] + jj;
-                        const bool uni = uniform_at(o, off0o, jj);
+                        const bool uni = chg_zero(o, off0o, jj + 1u, k - 1u);
                         int q = (int)qb[0] - 33;
                         q = q < 0 ? 0 : (q > 41 ? 41 : q);
                         wgt = weight(qb, uni, (uint32_t)q);
                     }
-                    if (LDS_HIST) {
-                        atomicAdd(&hA[cl], 1ull);
-                        if (MODE == KM_LOCAL) atomicAdd(&hW[cl], wgt);
-                    } else {
-                        atomicAdd(&gU[cl], 1ull);
-                        if (MODE == KM_LOCAL) atomicAdd(&out_w[cl], wgt);
-                    }
+                    add_count(cl, 1u, wgt);
                     const int32_t old = atomicCAS(&ambf[o], -1, (int32_t)cl);
                     if (old != -1 && old != (int32_t)cl) ambd[o] = 1;
-                } else if (EM && found && (cl & AX_MULTI) && cl != AX_SENT) {
-                    const uint32_t lo = cl & ~AX_MULTI;
+                } else if (EM && found && cl == C::MULTI) {
+                    const uint32_t lo = A.mlo[pp];
                     atomicAdd(&src.em_mult[lo], 1u);
                     src.em_hi[lo] = A.mhi[lo];
                 }
@@ -786,36 +988,39 @@ __global__ __launch_bounds__(BLOCK_THREADS) void k_scan_ax(AxView A, UnitSrc src
     }
 }
 
-template <int MODE>
-constexpr uint32_t ax_wave_bytes() {
-    return 8u * 64u * (AX_PKW + AX_VWW + (MODE == KM_LOCAL ? AX_CGW + 1u : 0u)) + 4u * AX_DEF + 16u + 8u * 64u + 64u;
-}
-
-template <int MODE, bool PAIRED, bool LDS, bool EM, int NWC>
+template <int MODE, bool PAIRED, bool LDS, bool EM, int NWC, int CW>
 void ax_launch_one(const AxView& A, const UnitSrc& src, uint32_t grid, size_t lds, hipStream_t st,
                    unsigned long long* a, double* w) {
     if (lds > 64 * 1024)  // dynamic LDS above 64 KiB must be allowed (occupancy caps pad it)
-        HIP_OK(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_scan_ax<MODE, PAIRED, LDS, EM, NWC>),
+        HIP_OK(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_scan_ax<MODE, PAIRED, LDS, EM, NWC, CW>),
                                    hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-    hipLaunchKernelGGL((k_scan_ax<MODE, PAIRED, LDS, EM, NWC>), dim3(grid), dim3(BLOCK_THREADS), lds, st, A, src, a, w);
+    hipLaunchKernelGGL((k_scan_ax<MODE, PAIRED, LDS, EM, NWC, CW>), dim3(grid), dim3(BLOCK_THREADS), lds, st, A, src, a,
+                       w);
 }
 
-template <int MODE, bool PAIRED, bool LDS, bool EM>
-void ax_launch_nwc(uint32_t nwc, const AxView& A, const UnitSrc& src, uint32_t grid, size_t lds, hipStream_t st,
+// NWC = words covering the k - 1 + AX_RUN bases of one compare: 3 (k <= 33), 4 (k <= 65), 6 (k <= 128)
+template <int MODE, bool PAIRED, bool LDS, bool EM, int CW>
+void ax_launch_nwc(uint32_t k, const AxView& A, const UnitSrc& src, uint32_t grid, size_t lds, hipStream_t st,
                    unsigned long long* a, double* w) {
-    switch (nwc) {
-        case 2: ax_launch_one<MODE, PAIRED, LDS, EM, 2>(A, src, grid, lds, st, a, w); break;
-        case 3: ax_launch_one<MODE, PAIRED, LDS, EM, 3>(A, src, grid, lds, st, a, w); break;
-        case 4: ax_launch_one<MODE, PAIRED, LDS, EM, 4>(A, src, grid, lds, st, a, w); break;
-        default: ax_launch_one<MODE, PAIRED, LDS, EM, 5>(A, src, grid, lds, st, a, w); break;
-    }
+    if (k <= 33) ax_launch_one<MODE, PAIRED, LDS, EM, 3, CW>(A, src, grid, lds, st, a, w);
+    else if (k <= 65) ax_launch_one<MODE, PAIRED, LDS, EM, 4, CW>(A, src, grid, lds, st, a, w);
+    else ax_launch_one<MODE, PAIRED, LDS, EM, 6, CW>(A, src, grid, lds, st, a, w);
 }
 
-template <int MODE, bool PAIRED, bool LDS>
-void ax_launch_em(uint32_t nwc, const AxView& A, const UnitSrc& src, uint32_t grid, size_t lds, hipStream_t st,
-                  unsigned long long* a, double* w) {
-    if (src.em_mult != nullptr) ax_launch_nwc<MODE, PAIRED, LDS, true>(nwc, A, src, grid, lds, st, a, w);
-    else ax_launch_nwc<MODE, PAIRED, LDS, false>(nwc, A, src, grid, lds, st, a, w);
+template <int MODE, bool PAIRED>
+void ax_launch_mode(uint32_t cw, bool lds_hist, uint32_t k, const AxView& A, const UnitSrc& src, uint32_t grid,
+                    size_t lds, hipStream_t st, unsigned long long* a, double* w) {
+    const bool em = src.em_mult != nullptr;
+    if (cw == 1) {  // <= 253 groups: always the LDS histogram
+        if (em) ax_launch_nwc<MODE, PAIRED, true, true, 1>(k, A, src, grid, lds, st, a, w);
+        else ax_launch_nwc<MODE, PAIRED, true, false, 1>(k, A, src, grid, lds, st, a, w);
+    } else if (lds_hist) {
+        if (em) ax_launch_nwc<MODE, PAIRED, true, true, 2>(k, A, src, grid, lds, st, a, w);
+        else ax_launch_nwc<MODE, PAIRED, true, false, 2>(k, A, src, grid, lds, st, a, w);
+    } else {
+        if (em) ax_launch_nwc<MODE, PAIRED, false, true, 2>(k, A, src, grid, lds, st, a, w);
+        else ax_launch_nwc<MODE, PAIRED, false, false, 2>(k, A, src, grid, lds, st, a, w);
+    }
 }
 
 }  // namespace
@@ -823,20 +1028,24 @@ void ax_launch_em(uint32_t nwc, const AxView& A, const UnitSrc& src, uint32_t gr
 namespace speq {
 
 // Builds the per-k anchor structures of replica d (blocking, on its stream). Returns a table with ok == false when
-// k or the index is outside what the scan supports, or the structures would not fit the free HBM.
+// k, the group count or the index is outside what the scan supports, or the structures would not fit the free HBM.
 AxTable build_ax(speq_device_index* d, uint32_t k) {
     DeviceGuard g(d->device);
     const auto t0 = std::chrono::steady_clock::now();
     AxTable ax;
     const uint64_t n = d->view.n;
-    if (k < 1 || k > AX_MAX_K || n >= (1ull << 30)) return ax;
+    if (k < 1 || k > AX_MAX_K || n >= (1ull << 30) || d->G > AxCls<2>::MAX_G) return ax;
+    ax.cw = d->G <= AxCls<1>::MAX_G ? 1u : 2u;
     const uint64_t nw64 = (n + 63) / 64 + 4;
+    const uint64_t cls_bytes = ((n + 512) * ax.cw + 15) & ~15ull;
     size_t free_b = 0, total_b = 0;
     HIP_OK(hipMemGetInfo(&free_b, &total_b));
-    const uint64_t need = (n + 256) * 4 * 3 + nw64 * 24 + n * 8;  // cls, mhi, owner, text2 + tbad, table (bound)
+    // cls, mlo, mhi, owner, text2 + tbad, table + filter (bounds)
+    const uint64_t need = cls_bytes + (n + 64) * 4 * 3 + nw64 * 24 + n * 12;
     if (need > free_b / 10 * 9) return ax;
     uint32_t* owner = nullptr;
     unsigned long long* d_cnt = nullptr;
+    std::vector<void*> mine;  // this table's allocations (tracked by the replica once the table is complete)
     auto cleanup = [&] {
         (void)hipStreamSynchronize(d->stream);
         if (owner) (void)hipFree(owner);
@@ -844,51 +1053,69 @@ AxTable build_ax(speq_device_index* d, uint32_t k) {
         owner = nullptr;
         d_cnt = nullptr;
     };
+    auto alloc = [&](void** pp, uint64_t bytes) {
+        HIP_OK(hipMalloc(pp, bytes));
+        mine.push_back(*pp);
+    };
     try {
         if (!d->d_text2) {  // 2-bit text + non-ACGT bitmap, once per replica
             HIP_OK(hipMalloc(&d->d_text2, nw64 * 16));
-            HIP_OK(hipMalloc(&d->d_tbad, nw64 * 8));
             d->track(d->d_text2);
+            HIP_OK(hipMalloc(&d->d_tbad, nw64 * 8));
             d->track(d->d_tbad);
             const uint32_t grid = (uint32_t)std::min<uint64_t>((nw64 + 255) / 256, 4096);
             hipLaunchKernelGGL(k_ax_text2, dim3(grid), dim3(256), 0, d->stream, d->d_text, n, d->d_text2, d->d_tbad,
                                nw64);
             HIP_OK(hipGetLastError());
         }
-        HIP_OK(hipMalloc(&ax.cls, (n + 256) * 4));
-        d->track(ax.cls);
-        HIP_OK(hipMalloc(&ax.mhi, (n + 1) * 4));
-        d->track(ax.mhi);
+        alloc(&ax.cls, cls_bytes);
+        alloc(reinterpret_cast<void**>(&ax.mlo), (n + 64) * 4);
+        alloc(reinterpret_cast<void**>(&ax.mhi), (n + 64) * 4);
         HIP_OK(hipMalloc(&owner, (n + 1) * 4));
         HIP_OK(hipMalloc(&d_cnt, 8));
-        HIP_OK(hipMemsetAsync(ax.cls, 0xFF, (n + 256) * 4, d->stream));
+        HIP_OK(hipMemsetAsync(ax.cls, 0xFF, cls_bytes, d->stream));
         HIP_OK(hipMemsetAsync(owner, 0xFF, (n + 1) * 4, d->stream));
         HIP_OK(hipMemsetAsync(d_cnt, 0, 8, d->stream));
         const DevView v = search_view(d, k);
         const uint32_t grid = (uint32_t)std::min<uint64_t>((n + 255) / 256, 16384);
-        hipLaunchKernelGGL(k_ax_classify, dim3(grid), dim3(256), 0, d->stream, v, d->d_text, d->d_tbad, n, k, ax.cls,
-                           ax.mhi, owner, d_cnt);
+        if (ax.cw == 1)
+            hipLaunchKernelGGL(k_ax_classify<1>, dim3(grid), dim3(256), 0, d->stream, v, d->d_text, d->d_tbad, n, k,
+                               ax.cls, ax.mlo, ax.mhi, owner, d_cnt);
+        else
+            hipLaunchKernelGGL(k_ax_classify<2>, dim3(grid), dim3(256), 0, d->stream, v, d->d_text, d->d_tbad, n, k,
+                               ax.cls, ax.mlo, ax.mhi, owner, d_cnt);
         HIP_OK(hipGetLastError());
         unsigned long long distinct = 0;
         HIP_OK(hipMemcpyAsync(&distinct, d_cnt, 8, hipMemcpyDeviceToHost, d->stream));
         HIP_OK(hipStreamSynchronize(d->stream));
         ax.distinct = distinct;
         ax.nb = std::max<uint64_t>(1, (uint64_t)((double)distinct * 100.0 / (8.0 * d->ax_load)) + 1);
-        if (ax.nb >= (1ull << 32)) throw DeviceError("anchor table too large");
-        HIP_OK(hipMalloc(&ax.atab, ax.nb * 64));
-        d->track(ax.atab);
+        ax.nf = std::max<uint64_t>(1, distinct * AX_FILTER_BITS / 64);
+        if (ax.nb * 64 >= (1ull << 32) - 64 || ax.nf * 8 >= (1ull << 32) - 64) {
+            // the scan addresses the tables with 32-bit buffer offsets: leave this k to the other kernels
+            cleanup();
+            for (void* q : mine) (void)hipFree(q);
+            return AxTable{};
+        }
+        alloc(&ax.atab, ax.nb * 64);
+        alloc(&ax.filt, ax.nf * 8);
         HIP_OK(hipMemsetAsync(ax.atab, 0xFF, ax.nb * 64, d->stream));
+        HIP_OK(hipMemsetAsync(ax.filt, 0, ax.nf * 8, d->stream));
         hipLaunchKernelGGL(k_ax_insert, dim3(grid), dim3(256), 0, d->stream, owner, n, d->d_text2, k,
-                           reinterpret_cast<unsigned long long*>(ax.atab), ax.nb);
+                           reinterpret_cast<unsigned long long*>(ax.atab), ax.nb,
+                           reinterpret_cast<unsigned long long*>(ax.filt), ax.nf);
         HIP_OK(hipGetLastError());
         HIP_OK(hipStreamSynchronize(d->stream));
-        ax.bytes = ax.nb * 64 + (n + 256) * 4 + (n + 1) * 4;
+        ax.cls_bytes = cls_bytes;
+        ax.bytes = ax.nb * 64 + ax.nf * 8 + cls_bytes + (n + 64) * 8;
         ax.ok = true;
     } catch (...) {
         cleanup();
+        for (void* q : mine) (void)hipFree(q);
         throw;
     }
     cleanup();
+    for (void* q : mine) d->track(q);
     ax.build_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     return ax;
 }
@@ -910,10 +1137,15 @@ bool launch_ax(speq_device_index* d, int mode, bool paired, const UnitSrc& src, 
     AxView A;
     A.t2 = d->d_text2;
     A.cls = ax->cls;
+    A.mlo = ax->mlo;
     A.mhi = ax->mhi;
     A.atab = reinterpret_cast<const unsigned long long*>(ax->atab);
+    A.filt = reinterpret_cast<const unsigned long long*>(ax->filt);
     A.nb = ax->nb;
+    A.nf = ax->nf;
     A.n = d->view.n;
+    A.t2_bytes = ((d->view.n + 63) / 64 + 4) * 16;
+    A.cls_bytes = ax->cls_bytes;
     A.G = d->G;
     const bool lds_hist = d->G <= LDS_HIST_MAX_G;
     const uint32_t hist_words = lds_hist ? (mode == KM_GLOBAL ? d->G : 2u * d->G) : 0u;
@@ -927,21 +1159,14 @@ bool launch_ax(speq_device_index* d, int mode, bool paired, const UnitSrc& src, 
         const size_t pad = (160u * 1024u) / d->blocks_per_cu_ax;
         if (pad > lds_launch) lds_launch = pad & ~(size_t)15;
     }
-    const uint32_t nwc = (src.k + 31u + 31u) / 32u;  // words covering k - 1 + AX_RUN bases
     const uint32_t grid = (uint32_t)blocks;
-#define SPEQ_AX(M, P)                                                                        \
-    do {                                                                                     \
-        if (lds_hist) ax_launch_em<M, P, true>(nwc, A, src, grid, lds_launch, st, a, w);     \
-        else ax_launch_em<M, P, false>(nwc, A, src, grid, lds_launch, st, a, w);             \
-    } while (0)
     if (mode == KM_GLOBAL) {
-        if (paired) SPEQ_AX(KM_GLOBAL, true);
-        else SPEQ_AX(KM_GLOBAL, false);
+        if (paired) ax_launch_mode<KM_GLOBAL, true>(ax->cw, lds_hist, src.k, A, src, grid, lds_launch, st, a, w);
+        else ax_launch_mode<KM_GLOBAL, false>(ax->cw, lds_hist, src.k, A, src, grid, lds_launch, st, a, w);
     } else {
-        if (paired) SPEQ_AX(KM_LOCAL, true);
-        else SPEQ_AX(KM_LOCAL, false);
+        if (paired) ax_launch_mode<KM_LOCAL, true>(ax->cw, lds_hist, src.k, A, src, grid, lds_launch, st, a, w);
+        else ax_launch_mode<KM_LOCAL, false>(ax->cw, lds_hist, src.k, A, src, grid, lds_launch, st, a, w);
     }
-#undef SPEQ_AX
     HIP_OK(hipGetLastError());
     return true;
 }

@@ -15,12 +15,17 @@ using speq_dev::DevView;
 namespace speq {
 // Per-k structures of the anchor-and-extend scan (ax_scan.hip).
 struct AxTable {
-    uint32_t* cls = nullptr;   // class of the k-mer at every text position (n + 256 entries; see ax_scan.hip)
-    uint32_t* mhi = nullptr;   // SA interval end of each multi-group k-mer, indexed by its interval start
+    void* cls = nullptr;       // class of the k-mer at every text position (cw bytes each; see ax_scan.hip)
+    uint32_t* mlo = nullptr;   // SA interval start of the multi-group k-mer at a text position (EM)
+    uint32_t* mhi = nullptr;   // SA interval end of each multi-group k-mer, indexed by its interval start (EM)
     void* atab = nullptr;      // anchor table: 64-B buckets of 8 {fingerprint, representative position} slots
+    void* filt = nullptr;      // blocked Bloom filter of the distinct k-mers (one 64-bit word per k-mer, 3 bits)
     uint64_t nb = 0;           // buckets
+    uint64_t nf = 0;           // filter words
+    uint64_t cls_bytes = 0;
+    uint32_t cw = 1;           // bytes per class: 1 for <= 253 groups, else 2
     uint64_t distinct = 0;     // distinct k-mers of the texts
-    uint64_t bytes = 0;        // device bytes of cls + mhi + atab
+    uint64_t bytes = 0;        // device bytes of the structures
     double build_ms = 0.0;
     bool ok = false;
 };
