@@ -356,6 +356,9 @@ constexpr uint32_t ax_wave_bytes() {
     return 8u * 64u * (AX_PKW + AX_VWW + (MODE == KM_LOCAL ? AX_CGW + 1u : 0u)) + 2u * AX_DEF + 16u + 8u * 64u + 64u;
 }
 
+#ifndef SPEQ_AX_PROBE  // timing probes (scripts/ax_probe.py A/B only; results are wrong): 1 staging only, 2 no phase 2
+#define SPEQ_AX_PROBE 0
+#endif
 #ifndef SPEQ_AX_MIN_WAVES  // minimum waves per SIMD the register allocator must allow (A/B knob)
 #define SPEQ_AX_MIN_WAVES 4
 #endif
@@ -600,6 +603,9 @@ __global__ __launch_bounds__(BLOCK_THREADS, SPEQ_AX_MIN_WAVES) void k_scan_ax(Ax
                 return u;
             };
 
+#if SPEQ_AX_PROBE == 1  // timing probe only (wrong results): staging alone
+            if (wend > 0u) continue;
+#endif
             // ---- phase 1: one read per lane, one memory round trip per iteration: a lane either probes the anchor
             // table (its candidate is compared in the next iteration) or extends a run by up to AX_RUN windows
             uint32_t j = 0;
@@ -852,7 +858,11 @@ __global__ __launch_bounds__(BLOCK_THREADS, SPEQ_AX_MIN_WAVES) void k_scan_ax(Ax
             ambf[lane] = af;
             ambd[lane] = ad;
             wave_sync();
+#if SPEQ_AX_PROBE == 2  // timing probe only (wrong results): no deferred windows
+            const uint32_t n2 = 0;
+#else
             const uint32_t n2 = min(__builtin_amdgcn_readfirstlane(defn[0]), AX_DEF);
+#endif
             for (uint32_t base = 0; base < n2; base += 64u * AX_F) {
                 uint32_t ent[AX_F];
                 uint64_t hh[AX_F];
