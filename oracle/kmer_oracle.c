@@ -122,33 +122,59 @@ oracle_t* oracle_build(const char* seq, const uint64_t* rec_off, uint32_t n_reco
     o->cap = cap;
     o->slot_pos = (uint64_t*)calloc(cap, sizeof(uint64_t));
     o->slot_label = (int32_t*)malloc(sizeof(int32_t) * cap);
+    for (uint64_t i = 0; i < cap; ++i) o->slot_label[i] = -3; /* unset */
     o->slot_first = (int64_t*)malloc(sizeof(int64_t) * cap);
     o->occ_text = (uint32_t*)malloc(sizeof(uint32_t) * (n_windows + 1));
     o->occ_next = (int64_t*)malloc(sizeof(int64_t) * (n_windows + 1));
+    /* Insertion runs on all host threads (config 5's 200 M windows: minutes on one). A slot is claimed by a CAS on
+     * slot_pos; its label is the merge of the groups of every occurrence (unset + g = g, g + g = g, g + h = -2), an
+     * order-free rule, so the result does not depend on the interleaving; the occurrence lists are pushed with an
+     * atomic exchange, and their order only reorders additions of the same f (oracle_em_pass), which is exact. */
+    memset(o->slot_first, 0xFF, sizeof(int64_t) * cap);
+    uint64_t* wbase = (uint64_t*)malloc(sizeof(uint64_t) * (2 * (size_t)n_records + 1));
+    wbase[0] = 0;
     for (uint32_t t = 0; t < 2 * n_records; ++t) {
         uint64_t s = o->text_start[t], e = o->text_start[t + 1] - 1;
+        wbase[t + 1] = wbase[t] + (e - s >= k ? e - s - k + 1 : 0);
+    }
+#pragma omp parallel for schedule(dynamic, 1)
+    for (int64_t t = 0; t < 2 * (int64_t)n_records; ++t) {
+        uint64_t s = o->text_start[t], e = o->text_start[t + 1] - 1;
         if (e - s < k) continue;
+        const int32_t g = o->text_group[t];
         for (uint64_t w = s; w + k <= e; ++w) {
             const uint8_t* kp = o->text + w;
             uint64_t m = cap - 1, i = hash_kmer(kp, k) & m;
             for (;;) {
-                uint64_t sp = o->slot_pos[i];
+                uint64_t sp = __atomic_load_n(&o->slot_pos[i], __ATOMIC_ACQUIRE);
                 if (!sp) {
-                    o->slot_pos[i] = w + 1;
-                    o->slot_label[i] = o->text_group[t];
-                    o->slot_first[i] = -1;
+                    uint64_t expect = 0;
+                    if (__atomic_compare_exchange_n(&o->slot_pos[i], &expect, w + 1, 0, __ATOMIC_ACQ_REL,
+                                                    __ATOMIC_ACQUIRE))
+                        sp = w + 1;
+                    else
+                        sp = expect;
                 }
-                if (!sp || memcmp(o->text + (sp - 1), kp, k) == 0) {
-                    if (sp && o->slot_label[i] != o->text_group[t]) o->slot_label[i] = -2;
-                    o->occ_text[o->n_occ] = t;
-                    o->occ_next[o->n_occ] = o->slot_first[i];
-                    o->slot_first[i] = (int64_t)o->n_occ++;
+                if (sp == w + 1 || memcmp(o->text + (sp - 1), kp, k) == 0) {
+                    int32_t cur = __atomic_load_n(&o->slot_label[i], __ATOMIC_RELAXED);
+                    for (;;) {
+                        int32_t nxt = cur == -3 ? g : (cur == g ? g : -2);
+                        if (nxt == cur ||
+                            __atomic_compare_exchange_n(&o->slot_label[i], &cur, nxt, 0, __ATOMIC_RELAXED,
+                                                        __ATOMIC_RELAXED))
+                            break;
+                    }
+                    const uint64_t x = wbase[t] + (w - s);
+                    o->occ_text[x] = (uint32_t)t;
+                    o->occ_next[x] = __atomic_exchange_n(&o->slot_first[i], (int64_t)x, __ATOMIC_RELAXED);
                     break;
                 }
                 i = (i + 1) & m;
             }
         }
     }
+    o->n_occ = wbase[2 * n_records];
+    free(wbase);
     return o;
 }
 
@@ -249,14 +275,18 @@ int oracle_ref_unique(const oracle_t* o, uint64_t* u_ref, uint64_t* tot_ref) {
     const uint32_t k = o->k;
     memset(u_ref, 0, sizeof(uint64_t) * o->n_groups);
     memset(tot_ref, 0, sizeof(uint64_t) * o->n_groups);
-    for (uint32_t t = 0; t < 2 * o->n_records; ++t) {
+#pragma omp parallel for schedule(dynamic, 1)
+    for (int64_t t = 0; t < 2 * (int64_t)o->n_records; ++t) {
         uint64_t s = o->text_start[t], e = o->text_start[t + 1] - 1;
         int32_t g = o->text_group[t];
         if (e - s < k) continue;
+        uint64_t tot = 0, u = 0;
         for (uint64_t w = s; w + k <= e; ++w) {
-            ++tot_ref[g];
-            if (lookup(o, o->text + w) == g) ++u_ref[g];
+            ++tot;
+            if (lookup(o, o->text + w) == g) ++u;
         }
+        __atomic_fetch_add(&tot_ref[g], tot, __ATOMIC_RELAXED);
+        __atomic_fetch_add(&u_ref[g], u, __ATOMIC_RELAXED);
     }
     return 0;
 }
