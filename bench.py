@@ -98,6 +98,16 @@ class Ctx:
             dist.init_process_group("nccl", device_id=torch.device(f"cuda:{self.local_rank}"))
         torch.cuda.set_device(self.local_rank)
         self.dev_t = torch.device(f"cuda:{self.local_rank}")
+        self.comm = None
+        if self.world > 1:
+            # the product's own collective (C ABI speq_allreduce_*, ncclAllReduce over xGMI): rank 0's 128-byte
+            # RCCL id reaches the other ranks through torch.distributed, which keeps only the barrier and timing
+            from speq_amd import Comm
+            uid = torch.zeros(Comm.ID_BYTES, dtype=torch.uint8, device=self.dev_t)
+            if self.rank == 0:
+                uid.copy_(torch.frombuffer(bytearray(Comm.unique_id()), dtype=torch.uint8))
+            dist.broadcast(uid, 0)
+            self.comm = Comm(self.world, self.rank, bytes(uid.cpu().numpy().tobytes()))
 
     def barrier(self):
         if self.world > 1:
@@ -132,7 +142,9 @@ def kernel_model(dev, k: int, table_on: bool, kmers: int, read_bytes: int, n_rea
             "model": "SURVEY.md 8(d): k LF steps x 2 occ-block loads x 64 B"}
 
 
-def traffic_lookup(cfg, k, q, pair_steps, triple, lab, ilp, bpc, mode, n_reads, kt, dev=None):
+def traffic_lookup(cfg: int, k: int, mode: str, n_reads: int, kernel: str):
+    """Measured fabric bytes per launch of this exact workload and kernel (rocprofv3 PMC passes summarised into
+    profiles/traffic.json by scripts/summarize_profile.py --traffic-key), or (None, None)."""
     prof = os.path.join(ROOT, "profiles", "traffic.json")
     if not os.path.exists(prof):
         return None, None
@@ -140,12 +152,14 @@ def traffic_lookup(cfg, k, q, pair_steps, triple, lab, ilp, bpc, mode, n_reads, 
         tj = json.load(open(prof))
     except ValueError:
         return None, None
-    steps = "_tri1" if triple else ""
-    key = (f"cfg{cfg}_k{k}_q{q}_pairs{pair_steps}{steps}_lab{lab}_ilp{ilp}_bpc{bpc}_{mode}_reads{n_reads}"
-           f"{'_kt1' if kt else ''}")
+    key = f"cfg{cfg}_k{k}_{mode}_reads{n_reads}_{kernel}"
     if key in tj:
-        return tj[key]["hbm_bytes_per_launch"], tj[key]["source"]
+        src = tj[key]["source"]
+        return tj[key]["hbm_bytes_per_launch"], os.path.normpath(os.path.join("profiles", src))
     return None, None
+
+
+KERNEL_TAG = {0: "lf", 1: "kt", 2: "kt", 3: "ax"}  # speq_device_get_tuning("last_kernel")
 
 
 def run_workload(ctx: Ctx, cfg_no: int, k: int, n_reads: int, mode: str, steps: int, warmup: int,
@@ -195,10 +209,10 @@ def run_workload(ctx: Ctx, cfg_no: int, k: int, n_reads: int, mode: str, steps: 
             d_w.zero_()
         dev.scan_device(d_seq.data_ptr(), d_qual.data_ptr(), d_off.data_ptr(), reads.n, k, d_counts.data_ptr(),
                         d_w.data_ptr(), paired=paired, local=local, stream=stream)
-        if ctx.world > 1:
-            ctx.dist.all_reduce(d_counts)  # one RCCL all-reduce of the G+2 counters over xGMI
+        if ctx.comm is not None:  # one RCCL all-reduce of the G+2 counters over xGMI (speq_allreduce_u64)
+            ctx.comm.allreduce_u64(d_counts.data_ptr(), G + 2, stream)
             if local:
-                ctx.dist.all_reduce(d_w)
+                ctx.comm.allreduce_f64(d_w.data_ptr(), G, stream)
 
     def timed_run(n_steps, n_warm):
         for _ in range(n_warm):
@@ -222,6 +236,7 @@ def run_workload(ctx: Ctx, cfg_no: int, k: int, n_reads: int, mode: str, steps: 
     counts = d_counts.cpu().numpy()
     weights = d_w.cpu().numpy() if local else None
     table_on = bool(ktab["table_bytes"])
+    hot_kernel = dev.tuning("last_kernel")
     km = kernel_model(dev, k, table_on, kmers_per_step, read_bytes, reads.n)
 
     lf = None
@@ -257,9 +272,7 @@ def run_workload(ctx: Ctx, cfg_no: int, k: int, n_reads: int, mode: str, steps: 
     own_bytes = kmers_per_step * km["bytes_per_kmer"]
     own_gbs = own_bytes / avg_kernel_s / 1e9
     survey_gbs = kmers_per_step * 2 * k * OCC_ENTRY_BYTES / avg_kernel_s / 1e9
-    lab = int(idx.info().label_table)
-    traffic, traffic_src = traffic_lookup(cfg_no, k, a.prefix_q, a.pair_steps, a.triple_steps, lab,
-                                          dev.tuning("ilp"), dev.tuning("blocks_per_cu"), mode, n_reads, table_on)
+    traffic, traffic_src = traffic_lookup(cfg_no, k, mode, n_reads, KERNEL_TAG.get(hot_kernel, "lf"))
     roofline = {
         "bound": "hbm", "achieved": own_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": own_gbs / HBM_PEAK_GBS,
         "traffic": traffic,
@@ -333,6 +346,10 @@ def main():
         extra["k31"]["note"] = ("config 3 (10 M reads on one GPU); with 8 ranks each scans config 4's 12.5 M-read "
                                 "shard of the same index")
         p31["dev"].close()
+        # the reference CLI's defaults: k = 70 (include/arg_parse.h:21), Phred-weighted local mode (:23)
+        extra["k70_reference_defaults"], _ = run_workload(ctx, 2, 70, n_reads, "local", a.steps, a.warmup,
+                                                          with_lf=False, with_pcie=False, with_cpu=False,
+                                                          cpu_seconds=0, prepared=prep)
 
     if ctx.rank == 0:
         out = {
@@ -356,6 +373,8 @@ def main():
                 "blocks_per_cu": dev.tuning("blocks_per_cu"), "grid_blocks": dev.tuning("grid_blocks"),
                 "kmers_per_step_per_gpu": head["kmers_per_step_per_gpu"],
                 "parallelism": f"dp{ctx.world} (reads sharded, index replicated)",
+                "collective": ("speq_allreduce_u64/_f64 (C ABI; RCCL ncclAllReduce of the G + 2 counters per step)"
+                               if ctx.comm is not None else "none (one GPU)"),
                 "index_build_s": head["index_build_s"], "index_builder": "gpu" if a.gpu_build else "host",
                 "fm_text_len": head["fm_text_len"], "kmer_table": head["kmer_table"],
             },
@@ -368,6 +387,8 @@ def main():
             **extra,
         }
         print(json.dumps(out), flush=True)
+    if ctx.comm is not None:
+        ctx.comm.close()
     if ctx.world > 1:
         ctx.dist.destroy_process_group()
 

@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define SPEQ_ABI_VERSION 5
+#define SPEQ_ABI_VERSION 6
 
 enum {
     SPEQ_OK = 0,
@@ -41,7 +41,9 @@ enum {
     SPEQ_E_IO = -2,       /* file could not be read / written / has a bad format */
     SPEQ_E_DEVICE = -3,   /* no GPU, HIP runtime failure, or kernel launch failure */
     SPEQ_E_GROUPS = -4,   /* groupings do not cover every reference record */
-    SPEQ_E_NOMEM = -5
+    SPEQ_E_NOMEM = -5,
+    SPEQ_E_RETRY = -6     /* speq_scan_fastq_shard, cut = 1: the parallel cut does not fit this file; counters and
+                             EM histogram are cleared, scan again with cut = 0 (every rank) */
 };
 
 /* Scan modes: fm_scanner.cpp:5-32 picks "local" (Phred-weighted) when --fixed-accuracy == 0. */
@@ -250,6 +252,33 @@ int speq_ref_unique_multi(speq_device_index* const* ds, uint32_t n_devices, uint
 /* dst += src for two unfinalized EM histograms of replicas of one index (any GPUs of this process). src's device
  * arrays are released: afterwards src accepts only speq_em_free. */
 int speq_em_merge(speq_em* dst, speq_em* src);
+
+/* ---- one process per GPU (RANK / WORLD_SIZE of a launcher such as torchrun; `speq scan` runs this way when
+ * WORLD_SIZE > 1). Every rank opens its own replica, scans ITS share of the input, and the exchange is RCCL:
+ * speq_allreduce_u64/_f64 of the counters, speq_em_allreduce of the EM histogram. This replaces the reference's
+ * future.get() sums (fm_scanner.cpp:224-233) across processes instead of threads. ---- */
+/* speq_scan_fastq over shard `shard` of `n_shards`: the input is cut into record-aligned blocks exactly as on every
+ * other rank and this rank scans the blocks b with b % n_shards == shard (counts, weights, em and stats cover those
+ * only). cut: -1 = parallel cut, falling back to the sequential cutter on this rank alone (n_shards = 1 only);
+ * 1 = parallel cut only, failing with SPEQ_E_RETRY (counters, weights, em cleared) when the file does not fit it —
+ * the ranks then agree (an all-reduce of the flag) and all scan again with cut = 0 (sequential cutter). */
+int speq_scan_fastq_shard(speq_device_index* d, speq_em* em, const char* path1, const char* path2,
+                          const speq_scan_params* params, uint32_t threads, uint32_t shard, uint32_t n_shards, int cut,
+                          uint64_t* counts, double* weights, speq_stream_stats* stats);
+/* speq_fastq_checksum over one shard (same blocks as speq_scan_fastq_shard; cut 0 or 1, SPEQ_E_RETRY as there). */
+int speq_fastq_checksum_shard(const char* path1, const char* path2, uint32_t threads, uint32_t shard,
+                              uint32_t n_shards, int cut, uint64_t* records, uint64_t* bases, uint64_t* digest);
+/* The .dat pass over shard `shard` of `n_shards` equal slices of the reference windows (host outputs, this
+ * shard's partial sums; fm_scanner.cpp:1476-1560). */
+int speq_ref_unique_shard(speq_device_index* d, uint32_t k, uint32_t shard, uint32_t n_shards, uint64_t* u_ref,
+                          uint64_t* tot_ref);
+/* Sums an unfinalized EM histogram over the ranks of comm (multiplicities added, interval ends by max: a position
+ * that starts a multi-group interval on any rank starts the same interval everywhere), enqueued on stream and
+ * synchronized. Every rank then holds the whole job's histogram (speq_em_finalize / speq_em_step as usual). */
+int speq_em_allreduce(speq_em* em, void* comm, void* stream);
+/* In-place sum over the ranks of comm of `count` u64 (is_f64 = 0) or f64 (is_f64 = 1) words in HOST memory, staged
+ * through GPU `device` (blocking): the CLI's counters, weights, .dat sums, statistics and status flags. */
+int speq_allreduce_host(void* comm, int device, void* buf, uint64_t count, int is_f64);
 
 /* ---- groupings file (speq::file_to_map, /root/reference/src/file_to_map.cpp:20-119) ----
  * Same grammar "Name(count): i, j-k, …"; parse errors of single tokens are collected (the reference prints

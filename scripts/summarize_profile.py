@@ -2,6 +2,9 @@
 """Summarises a scripts/profile.sh output directory into profiles/<round>/ (kernel stats + per-launch PMC means).
 
 Usage: python scripts/summarize_profile.py gpurun_out/prof profiles/r01 [--tag cfg2_k21_q10_global]
+           [--traffic-key cfg2_k21_global_reads1000000_ax]
+--traffic-key also records the launch's fabric bytes in profiles/traffic.json under that key, where bench.py looks
+them up (cfg<N>_k<k>_<mode>_reads<reads per GPU>_<ax|kt|lf>) for the `traffic` field of its roofline.
 HBM/fabric bytes follow MI355X_MICROARCH.md §HBM: FETCH_SIZE and WRITE_SIZE are in KiB and derive from the L2's
 memory-side request counters (TCC_EA0_RDREQ x 64 B); Infinity-Cache hits are counted, not excluded, so they are an
 upper bound on HBM bytes for an index that stays MALL-resident. (The documented x2 correction applies to wide
@@ -18,7 +21,9 @@ import sys
 
 def main():
     src, dst = sys.argv[1], sys.argv[2]
-    tag = sys.argv[4] if len(sys.argv) > 4 and sys.argv[3] == "--tag" else "default"
+    opts = dict(zip(sys.argv[3::2], sys.argv[4::2]))
+    tag = opts.get("--tag", "default")
+    tkey = opts.get("--traffic-key")
     os.makedirs(dst, exist_ok=True)
     out = {"tag": tag}
     st = os.path.join(src, "trace", "trace_kernel_stats.csv")
@@ -62,6 +67,16 @@ def main():
         out["l2_hit_rate"] = h / max(1.0, h + m)
     json.dump(out, open(os.path.join(dst, f"pmc_{tag}.json"), "w"), indent=1)
     print(json.dumps(out, indent=1))
+    if tkey and "fabric_read_bytes_per_launch" in out:
+        tp = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "profiles", "traffic.json")
+        tj = json.load(open(tp)) if os.path.exists(tp) else {}
+        tj[tkey] = {"hbm_bytes_per_launch": out["fabric_read_bytes_per_launch"] + out.get("fabric_write_bytes_per_launch", 0.0),
+                    "note": "FETCH_SIZE+WRITE_SIZE (KiB x 1024) per scan launch; L2->fabric bytes incl. Infinity-Cache "
+                            "hits (upper bound on HBM bytes)",
+                    "source": os.path.relpath(os.path.join(dst, f"pmc_{tag}.json"), os.path.join(os.path.dirname(tp))),
+                    "l2_hit_rate": out.get("l2_hit_rate"),
+                    "kernel_steady_state_ns_rocprof": out.get("scan_steady_state_avg_ns")}
+        json.dump(tj, open(tp, "w"), indent=1)
 
 
 if __name__ == "__main__":

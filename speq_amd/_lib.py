@@ -21,7 +21,7 @@ class SpeqError(RuntimeError):
         self.code = code
 
 
-SPEQ_OK, SPEQ_E_ARG, SPEQ_E_IO, SPEQ_E_DEVICE, SPEQ_E_GROUPS, SPEQ_E_NOMEM = 0, -1, -2, -3, -4, -5
+SPEQ_OK, SPEQ_E_ARG, SPEQ_E_IO, SPEQ_E_DEVICE, SPEQ_E_GROUPS, SPEQ_E_NOMEM, SPEQ_E_RETRY = 0, -1, -2, -3, -4, -5, -6
 SPEQ_MODE_GLOBAL, SPEQ_MODE_LOCAL = 0, 1
 
 
@@ -101,6 +101,13 @@ SIGNATURES = {
     "speq_ref_unique_multi": (C.c_int, [C.POINTER(_P), C.c_uint32, C.c_uint32, _U64P, _U64P]),
     "speq_em_merge": (C.c_int, [_P, _P]),
     "speq_fastq_checksum": (C.c_int, [C.c_char_p, C.c_char_p, C.c_uint32, _U64P, _U64P, _U64P]),
+    "speq_scan_fastq_shard": (C.c_int, [_P, _P, C.c_char_p, C.c_char_p, C.POINTER(ScanParams), C.c_uint32, C.c_uint32,
+                                        C.c_uint32, C.c_int, _U64P, _F64P, C.POINTER(StreamStats)]),
+    "speq_fastq_checksum_shard": (C.c_int, [C.c_char_p, C.c_char_p, C.c_uint32, C.c_uint32, C.c_uint32, C.c_int,
+                                            _U64P, _U64P, _U64P]),
+    "speq_ref_unique_shard": (C.c_int, [_P, C.c_uint32, C.c_uint32, C.c_uint32, _U64P, _U64P]),
+    "speq_em_allreduce": (C.c_int, [_P, _P, _P]),
+    "speq_allreduce_host": (C.c_int, [_P, C.c_int, _P, C.c_uint64, C.c_int]),
     "speq_groupings_parse": (C.c_int, [C.c_char_p, C.POINTER(_P)]),
     "speq_groupings_n_groups": (C.c_uint32, [_P]),
     "speq_groupings_name": (C.c_char_p, [_P, C.c_uint32]),
@@ -117,7 +124,7 @@ SIGNATURES = {
 }
 
 _lib = None
-ABI_VERSION = 5  # include/speq_scan.h SPEQ_ABI_VERSION (struct layouts above)
+ABI_VERSION = 6  # include/speq_scan.h SPEQ_ABI_VERSION (struct layouts above)
 
 
 def lib() -> C.CDLL:

@@ -23,7 +23,7 @@ import numpy as np
 from ._lib import (SPEQ_MODE_GLOBAL, SPEQ_MODE_LOCAL, BuildOpts, IndexInfo, ScanParams, Slot, SpeqError,  # noqa: F401
                    StreamStats, check, lib)
 
-__all__ = ["FmIndex", "DeviceIndex", "Node", "Pipeline", "ScanResult", "Groupings", "EmHistogram", "file_to_map", "unique_to_percent",
+__all__ = ["FmIndex", "DeviceIndex", "Node", "Pipeline", "ScanResult", "Groupings", "EmHistogram", "Comm", "file_to_map", "unique_to_percent",
            "em_refine", "pack_records", "SpeqError", "SPEQ_MODE_GLOBAL", "SPEQ_MODE_LOCAL"]
 
 
@@ -205,6 +205,32 @@ class DeviceIndex:
         stats = {"records": st.records, "bases": st.bases, "batches": st.batches, "seconds": st.seconds}
         return ScanResult(int(counts[0]), int(counts[1]), counts[2:].copy(), w), stats
 
+    def scan_fastq_shard(self, path1: str, path2: Optional[str], k: int, shard: int, n_shards: int, cut: int = 0,
+                         phred_cutoff: int = 30, local: bool = False, threads: int = 4,
+                         em: Optional["EmHistogram"] = None):
+        """One rank's share of a FASTQ scan (speq_scan_fastq_shard): the blocks b % n_shards == shard of the cut every
+        rank makes. cut 1 (parallel cut) raises SpeqError with code SPEQ_E_RETRY when the input does not fit it."""
+        G = self.n_groups
+        counts = np.zeros(G + 2, dtype=np.uint64)
+        w = np.zeros(G, dtype=np.float64) if local else None
+        p = ScanParams(k, phred_cutoff, int(path2 is not None), SPEQ_MODE_LOCAL if local else SPEQ_MODE_GLOBAL)
+        st = StreamStats()
+        check(lib().speq_scan_fastq_shard(self._h, em._h if em is not None else None, path1.encode(),
+                                          path2.encode() if path2 else None, C.byref(p), threads, shard, n_shards,
+                                          cut, _u64p(counts),
+                                          w.ctypes.data_as(C.POINTER(C.c_double)) if w is not None else None,
+                                          C.byref(st)))
+        stats = {"records": st.records, "bases": st.bases, "batches": st.batches, "seconds": st.seconds}
+        return ScanResult(int(counts[0]), int(counts[1]), counts[2:].copy(), w), stats
+
+    def count_unique_kmers_per_group_shard(self, k: int, shard: int, n_shards: int):
+        """This shard's partial (U_ref, Tot_ref) of the .dat pass (speq_ref_unique_shard)."""
+        G = self.n_groups
+        u = np.zeros(G, dtype=np.uint64)
+        t = np.zeros(G, dtype=np.uint64)
+        check(lib().speq_ref_unique_shard(self._h, k, shard, n_shards, _u64p(u), _u64p(t)))
+        return u, t
+
     def count_unique_kmers_per_group(self, k: int) -> tuple[np.ndarray, np.ndarray]:
         """(U_ref[G], Tot_ref[G]) of the reference-uniqueness pass."""
         G = self.n_groups
@@ -240,6 +266,48 @@ class DeviceIndex:
     def close(self):
         if self._h:
             lib().speq_device_close(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class Comm:
+    """One RCCL communicator of a one-process-per-GPU job (speq_comm_* / speq_allreduce_*; ncclAllReduce over xGMI).
+
+    Replaces the host `future.get()` sums of per-thread count vectors (/root/reference/src/fm_scanner.cpp:224-233):
+    every rank scans its own read shard and one all-reduce sums the G + 2 counters (and the G weights). Rank 0 makes
+    the 128-byte id with `Comm.unique_id()` and hands it to the other ranks out of band (bench.py broadcasts it with
+    torch.distributed; `speq scan` writes it to a rendezvous file)."""
+
+    ID_BYTES = 128
+
+    @staticmethod
+    def unique_id() -> bytes:
+        buf = C.create_string_buffer(Comm.ID_BYTES)
+        check(lib().speq_comm_unique_id(buf))
+        return buf.raw
+
+    def __init__(self, nranks: int, rank: int, uid: bytes):
+        if len(uid) != Comm.ID_BYTES:
+            raise ValueError("the RCCL unique id is 128 bytes")
+        h = C.c_void_p()
+        check(lib().speq_comm_init(nranks, rank, C.create_string_buffer(uid, Comm.ID_BYTES), C.byref(h)))
+        self._h, self.nranks, self.rank = h, nranks, rank
+
+    def allreduce_u64(self, d_buf: int, count: int, stream: int = 0) -> None:
+        """In-place sum of `count` u64 at device pointer d_buf, enqueued on `stream` (raw hipStream_t)."""
+        check(lib().speq_allreduce_u64(self._h, d_buf, count, stream or None))
+
+    def allreduce_f64(self, d_buf: int, count: int, stream: int = 0) -> None:
+        check(lib().speq_allreduce_f64(self._h, d_buf, count, stream or None))
+
+    def close(self):
+        if self._h:
+            lib().speq_comm_destroy(self._h)
             self._h = None
 
     def __del__(self):
@@ -327,6 +395,10 @@ class EmHistogram:
         check(lib().speq_em_scan_reads(self._h, seq, qual, _u64p(off), len(off) - 1, C.byref(p), _u64p(counts),
                                        w.ctypes.data_as(C.POINTER(C.c_double)) if w is not None else None))
         return ScanResult(int(counts[0]), int(counts[1]), counts[2:].copy(), w)
+
+    def allreduce(self, comm: "Comm", stream: int = 0) -> None:
+        """Sums the unfinalized histogram over the ranks of comm (speq_em_allreduce)."""
+        check(lib().speq_em_allreduce(self._h, comm._h, stream or None))
 
     def finalize(self, threads: int = 0) -> None:
         check(lib().speq_em_finalize(self._h, threads))

@@ -20,6 +20,8 @@
 #include <thread>
 #include <vector>
 
+#include <unistd.h>
+
 #include "args.hpp"
 #include "host_io.hpp"
 #include "speq_scan.h"
@@ -53,7 +55,10 @@ const char* HELP =
     "                            on below ~400 M symbols)\n"
     "      --device N            GPU ordinal (default $LOCAL_RANK or 0)\n"
     "      --gpus N              scan: shard the reads over GPUs 0..N-1 (default 1; 0 = every visible GPU)\n"
-    "      --devices I,J,...     scan: shard the reads over these GPU ordinals (repeats allowed)\n";
+    "      --devices I,J,...     scan: shard the reads over these GPU ordinals (repeats allowed)\n"
+    "one process per GPU: run under a launcher that sets WORLD_SIZE > 1, RANK and LOCAL_RANK (e.g. torchrun\n"
+    "--no-python bin/speq scan ...): each rank scans its share of the reads on GPU $LOCAL_RANK and the counts are\n"
+    "summed with RCCL; rank 0 prints and writes the results ($SPEQ_RENDEZVOUS: the id file, default under /tmp)\n";
 
 template <typename T>
 T to_number(const std::string& opt, const std::string& v) {
@@ -404,8 +409,85 @@ struct PhaseClock {
     }
 };
 
+// ---- one process per GPU (RANK / WORLD_SIZE / LOCAL_RANK from a launcher such as `torchrun --no-python`) ----
+// Every rank opens its own replica on GPU $LOCAL_RANK, scans its share of the FASTQ blocks and of the reference
+// windows, and the sums are RCCL all-reduces (speq_allreduce_host / speq_em_allreduce): the reference's future.get()
+// sums (fm_scanner.cpp:224-233) across processes. Rank 0 prints and writes everything; the others print nothing.
+// The RCCL id travels through a rendezvous file ($SPEQ_RENDEZVOUS, default /tmp/speq_rdzv_<parent pid>_<MASTER_PORT>:
+// the launcher is every rank's parent), written by rank 0 only after its index step, so `speq all` ranks also wait
+// for the index there.
+struct Dist {
+    int rank = 0, world = 1, device = 0;
+    void* comm = nullptr;
+    bool on() const { return world > 1; }
+};
+
+int env_int(const char* name, int dflt) {
+    const char* v = std::getenv(name);
+    return v && *v ? std::atoi(v) : dflt;
+}
+
+Dist dist_from_env(const CmdArguments& a) {
+    Dist dd;
+    const int world = env_int("WORLD_SIZE", 1);
+    if (world <= 1 || !a.devices.empty() || a.gpus != 1) return dd;
+    dd.world = world;
+    dd.rank = env_int("RANK", 0);
+    dd.device = a.device >= 0 ? a.device : env_int("LOCAL_RANK", 0);
+    if (dd.rank < 0 || dd.rank >= world) throw CApiError("RANK " + std::to_string(dd.rank) + " outside WORLD_SIZE");
+    return dd;
+}
+
+void dist_connect(Dist& dd) {
+    std::string path;
+    if (const char* v = std::getenv("SPEQ_RENDEZVOUS"); v && *v) path = v;
+    else {
+        const char* port = std::getenv("MASTER_PORT");
+        const char* tmp = std::getenv("TMPDIR");
+        path = std::string(tmp && *tmp ? tmp : "/tmp") + "/speq_rdzv_" + std::to_string((long)getppid()) + "_" +
+               (port ? port : "0");
+    }
+    unsigned char id[128];
+    if (dd.rank == 0) {
+        ok(speq_comm_unique_id(id), "creating the RCCL id");
+        const std::string tmp = path + ".tmp." + std::to_string((long)getpid());
+        {
+            std::ofstream os(tmp, std::ios::binary | std::ios::trunc);
+            os.write(reinterpret_cast<const char*>(id), sizeof(id));
+            if (!os) throw CApiError("cannot write the rendezvous file " + tmp);
+        }
+        fs::rename(tmp, path);
+    } else {
+        const int limit_s = env_int("SPEQ_RENDEZVOUS_TIMEOUT", 600);
+        const auto t0 = std::chrono::steady_clock::now();
+        for (;;) {
+            std::ifstream is(path, std::ios::binary);
+            if (is.read(reinterpret_cast<char*>(id), sizeof(id))) break;
+            if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(limit_s))
+                throw CApiError("rank " + std::to_string(dd.rank) + ": no rendezvous file " + path + " after " +
+                                std::to_string(limit_s) + " s");
+            std::this_thread::sleep_for(std::chrono::milliseconds(20));
+        }
+    }
+    ok(speq_comm_init(dd.world, dd.rank, id, &dd.comm), "joining the RCCL communicator");
+    if (dd.rank == 0) {  // every rank has joined (ncclCommInitRank is collective): the file has been read
+        std::error_code ec;
+        fs::remove(path, ec);
+    }
+}
+
+// Sums u64 (or f64) words over the ranks, in place.
+void dist_sum(const Dist& dd, void* buf, size_t n, bool f64) {
+    if (dd.on() && n) ok(speq_allreduce_host(dd.comm, dd.device, buf, n, f64 ? 1 : 0), "all-reduce over ranks");
+}
+
 int run_scan(CmdArguments& a) {
     PhaseClock phase;
+    Dist dd = dist_from_env(a);
+    if (dd.on()) {
+        dist_connect(dd);
+        phase("rendezvous");
+    }
     // HIP runtime start-up (device enumeration, ~0.1 s) overlaps the index read
     std::thread hip_init([] { (void)speq_device_count(); });
     struct Joiner {
@@ -429,6 +511,7 @@ int run_scan(CmdArguments& a) {
     // GPUs: --devices list, --gpus N (0..N-1), or one (--device, $LOCAL_RANK, 0). Reads shard across them in-process
     // (SURVEY 8(e)): one replica of the index per GPU, the counters summed at the end.
     std::vector<int> devs = a.devices;
+    if (dd.on()) devs = {dd.device};
     if (devs.empty() && a.gpus != 1) {
         const int visible = speq_device_count();
         const int n = a.gpus == 0 ? visible : a.gpus;
@@ -466,14 +549,25 @@ int run_scan(CmdArguments& a) {
     const int64_t idx_mtime = mtime_ns(idx_path);
     const fs::path dat = dat_path(idx_path, a.kmer);
     std::vector<uint64_t> u_ref, tot_ref;
-    if (!read_dat(dat, idx_mtime, G, u_ref, tot_ref)) {
+    uint64_t have_dat = (!dd.on() || dd.rank == 0) && read_dat(dat, idx_mtime, G, u_ref, tot_ref) ? 1 : 0;
+    dist_sum(dd, &have_dat, 1, false);  // rank 0's cache decides for every rank
+    if (!have_dat) {
         u_ref.assign(G, 0);
         tot_ref.assign(G, 0);
-        ok(n_dev == 1 ? speq_ref_unique(d, a.kmer, u_ref.data(), tot_ref.data())
-                      : speq_ref_unique_multi(ds.data(), n_dev, a.kmer, u_ref.data(), tot_ref.data()),
-           "reference-uniqueness pass");
-        write_dat(dat, idx_mtime, u_ref, tot_ref);
-        std::cerr << speq::format_vector(u_ref) << "\n" << speq::format_vector(tot_ref) << "\n";  // :1572-1573
+        if (dd.on()) {
+            ok(speq_ref_unique_shard(d, a.kmer, (uint32_t)dd.rank, (uint32_t)dd.world, u_ref.data(), tot_ref.data()),
+               "reference-uniqueness pass");
+            dist_sum(dd, u_ref.data(), G, false);
+            dist_sum(dd, tot_ref.data(), G, false);
+        } else {
+            ok(n_dev == 1 ? speq_ref_unique(d, a.kmer, u_ref.data(), tot_ref.data())
+                          : speq_ref_unique_multi(ds.data(), n_dev, a.kmer, u_ref.data(), tot_ref.data()),
+               "reference-uniqueness pass");
+        }
+        if (dd.rank == 0) {
+            write_dat(dat, idx_mtime, u_ref, tot_ref);
+            std::cerr << speq::format_vector(u_ref) << "\n" << speq::format_vector(tot_ref) << "\n";  // :1572-1573
+        }
     }
     phase(".dat");
 
@@ -490,10 +584,50 @@ int run_scan(CmdArguments& a) {
     // FASTQ(.gz) streamed through pinned slots: -t parser threads, H2D overlapped with the kernel (fm_scanner.cpp:
     // 138-141 / :651-655 read through an async_input_buffer; paired files are zipped, stopping at the shorter one).
     speq_stream_stats st{};
-    ok(speq_scan_fastq_multi(ds.data(), ems.data(), n_dev, a.in_file_reads_path_1.c_str(),
-                             paired ? a.in_file_reads_path_2.c_str() : nullptr, &prm, a.threads, counts.data(),
-                             local ? weights.data() : nullptr, &st),
-       "scanning reads");
+    if (dd.on()) {
+        // this rank's blocks; the parallel cut unless SPEQ_SPLIT_CUT=0, and when it does not fit the input on ANY
+        // rank, every rank scans again with the sequential cutter (same blocks everywhere)
+        const char* sc = std::getenv("SPEQ_SPLIT_CUT");
+        int cut = sc && sc[0] == '0' ? 0 : 1;
+        for (;;) {
+            const int rc = speq_scan_fastq_shard(d, em, a.in_file_reads_path_1.c_str(),
+                                                 paired ? a.in_file_reads_path_2.c_str() : nullptr, &prm, a.threads,
+                                                 (uint32_t)dd.rank, (uint32_t)dd.world, cut, counts.data(),
+                                                 local ? weights.data() : nullptr, &st);
+            const std::string msg = rc == SPEQ_OK ? "" : speq_last_error();
+            uint64_t flags[2] = {rc != SPEQ_OK && rc != SPEQ_E_RETRY ? 1u : 0u, rc == SPEQ_E_RETRY ? 1u : 0u};
+            dist_sum(dd, flags, 2, false);
+            if (flags[0]) {
+                if (rc != SPEQ_OK && rc != SPEQ_E_RETRY) ok(rc, "scanning reads");
+                throw CApiError("scanning reads: another rank failed");
+            }
+            if (!flags[1]) break;
+            cut = 0;  // the histogram of a rank whose parallel scan went through is rebuilt from scratch
+            speq_em_free(em);
+            em = ems[0] = nullptr;
+            ok(speq_em_create(idx, d, &em), "allocating the EM histogram");
+            ems[0] = em;
+        }
+        dist_sum(dd, counts.data(), counts.size(), false);
+        if (local) dist_sum(dd, weights.data(), G, true);
+        uint64_t sv[3] = {st.records, st.bases, st.batches};
+        dist_sum(dd, sv, 3, false);
+        st.records = sv[0];
+        st.bases = sv[1];
+        st.batches = sv[2];
+        ok(speq_em_allreduce(em, dd.comm, nullptr), "summing the EM histograms over ranks");
+        speq_comm_destroy(dd.comm);
+        dd.comm = nullptr;
+        if (dd.rank != 0) {  // rank 0 refines, prints and writes
+            speq_em_free(em);
+            return 1;
+        }
+    } else {
+        ok(speq_scan_fastq_multi(ds.data(), ems.data(), n_dev, a.in_file_reads_path_1.c_str(),
+                                 paired ? a.in_file_reads_path_2.c_str() : nullptr, &prm, a.threads, counts.data(),
+                                 local ? weights.data() : nullptr, &st),
+           "scanning reads");
+    }
     phase("FASTQ stream + scan");
     if (const char* v = std::getenv("SPEQ_STREAM_STATS"); v && *v && *v != '0')
         std::fprintf(stderr, "speq: streamed %llu records, %llu bases in %llu batches, %.3f s (%.1f M records/s)\n",
@@ -582,7 +716,9 @@ int main(int argc, char** argv) {
     }
     if (!a.is_parsed) return 0;
     try {
-        if (a.is_indexer) run_index(a);
+        // one process per GPU: rank 0 alone builds the index; the others wait for it at the rendezvous in run_scan
+        const bool other_rank = a.is_scanner && dist_from_env(a).rank != 0;
+        if (a.is_indexer && !other_rank) run_index(a);
         if (a.is_scanner) run_scan(a);
     } catch (const std::exception& e) {
         std::cerr << "speq: error: " << e.what() << "\n";

@@ -30,6 +30,9 @@ int guarded(F&& f) {
     } catch (const DeviceError& e) {
         set_last_error(e.what());
         return SPEQ_E_DEVICE;
+    } catch (const RetryError& e) {
+        set_last_error(e.what());
+        return SPEQ_E_RETRY;
     } catch (const std::bad_alloc&) {
         set_last_error("out of host memory");
         return SPEQ_E_NOMEM;

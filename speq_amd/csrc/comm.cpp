@@ -13,6 +13,8 @@
 #include <string>
 
 #include "capi_internal.hpp"
+#include "em.hpp"
+#include "scan_internal.hpp"
 
 namespace {
 struct Rccl {
@@ -91,6 +93,53 @@ int speq_allreduce_u64(void* comm, uint64_t* d_buf, uint64_t count, void* stream
         nccl_ok(rccl().all_reduce(d_buf, d_buf, count, ncclUint64, ncclSum, static_cast<ncclComm_t>(comm),
                               static_cast<hipStream_t>(stream)),
                 "ncclAllReduce");
+    });
+}
+
+int speq_allreduce_host(void* comm, int device, void* buf, uint64_t count, int is_f64) {
+    return speq::guarded([&] {
+        if (!comm || (!buf && count)) throw std::invalid_argument("speq_allreduce_host: null argument");
+        if (count == 0) return;
+        int prev = 0;
+        if (hipGetDevice(&prev) != hipSuccess || hipSetDevice(device) != hipSuccess)
+            throw speq::DeviceError("speq_allreduce_host: cannot select GPU " + std::to_string(device));
+        void* d = nullptr;
+        struct Release {
+            int dev;
+            void*& p;
+            ~Release() {
+                if (p) (void)hipFree(p);
+                (void)hipSetDevice(dev);
+            }
+        } release{prev, d};
+        const size_t bytes = (size_t)count * 8;
+        if (hipMalloc(&d, bytes) != hipSuccess) throw speq::DeviceError("speq_allreduce_host: hipMalloc failed");
+        if (hipMemcpy(d, buf, bytes, hipMemcpyHostToDevice) != hipSuccess)
+            throw speq::DeviceError("speq_allreduce_host: copy to the device failed");
+        nccl_ok(rccl().all_reduce(d, d, count, is_f64 ? ncclFloat64 : ncclUint64, ncclSum,
+                                  static_cast<ncclComm_t>(comm), nullptr),
+                "ncclAllReduce");
+        if (hipMemcpy(buf, d, bytes, hipMemcpyDeviceToHost) != hipSuccess)
+            throw speq::DeviceError("speq_allreduce_host: copy to the host failed");
+    });
+}
+
+int speq_em_allreduce(speq_em* em, void* comm, void* stream) {
+    return speq::guarded([&] {
+        if (!em || !comm) throw std::invalid_argument("speq_em_allreduce: null argument");
+        if (em->finalized || !em->d_mult) throw std::invalid_argument("speq_em_allreduce: histogram already finalized");
+        int prev = 0;
+        if (hipGetDevice(&prev) != hipSuccess || hipSetDevice(speq::device_ordinal(em->dev)) != hipSuccess)
+            throw speq::DeviceError("speq_em_allreduce: cannot select the histogram's GPU");
+        struct Restore {
+            int dev;
+            ~Restore() { (void)hipSetDevice(dev); }
+        } restore{prev};
+        hipStream_t st = static_cast<hipStream_t>(stream);
+        ncclComm_t c = static_cast<ncclComm_t>(comm);
+        nccl_ok(rccl().all_reduce(em->d_mult, em->d_mult, em->n, ncclUint32, ncclSum, c, st), "ncclAllReduce");
+        nccl_ok(rccl().all_reduce(em->d_hi, em->d_hi, em->n, ncclUint32, ncclMax, c, st), "ncclAllReduce");
+        if (hipStreamSynchronize(st) != hipSuccess) throw speq::DeviceError("speq_em_allreduce: stream failed");
     });
 }
 

@@ -540,6 +540,15 @@ struct Work {
     Block b1, b2;
     uint64_t n = 0;      // records (pairs when paired) to parse
     bool split = false;  // cut by find_cut: records not yet counted or checked
+    uint64_t seq = 0;    // block number in file order (the rank sharding deals blocks by it)
+};
+
+// Which blocks this process scans: block b belongs to shard b % n (one process per GPU, `speq scan` under a
+// launcher that sets RANK / WORLD_SIZE). The blocks are cut the same way on every rank, so the shards partition the
+// records. n = 1: every block.
+struct ShardSel {
+    uint32_t index = 0, n = 1;
+    bool mine(uint64_t block) const { return n <= 1 || block % n == index; }
 };
 
 struct Shared {
@@ -754,7 +763,7 @@ void parallel_for(uint32_t threads, size_t n, F&& fn) {
 // both files, so any layout this does not fit fails there (or here) and the caller runs the sequential reader.
 // Files with different record counts also go to the sequential reader (its zip rule and read-ahead decide).
 StreamTotals run_paired_split(const std::shared_ptr<Buf>& m1, const std::shared_ptr<Buf>& m2, uint32_t threads,
-                              Sink& sink) {
+                              Sink& sink, ShardSel shard) {
     const uint64_t BLOCK_RECORDS = 1u << 15, BLOCK_BYTES = 12ull << 20;
     const char* d1 = m1->data();
     const char* d2 = m2->data();
@@ -782,8 +791,9 @@ StreamTotals run_paired_split(const std::shared_ptr<Buf>& m1, const std::shared_
         if (r == r2[j]) return b2[j];
         return b2[j] + skip_lines(d2 + b2[j], b2[j + 1] - b2[j], 4 * (r - r2[j]));
     };
-    std::atomic<uint64_t> batches{0};
+    std::atomic<uint64_t> batches{0}, records{0};
     parallel_for(threads, n1, [&](size_t i) {
+        if (!shard.mine(i)) return;
         const size_t s2 = offset2(r1[i]), e2 = offset2(r1[i + 1]);
         const uint64_t l1 = b1[i + 1] - b1[i], l2 = e2 - s2, n = r1[i + 1] - r1[i];
         speq_slot s;
@@ -792,8 +802,9 @@ StreamTotals run_paired_split(const std::shared_ptr<Buf>& m1, const std::shared_
         std::memcpy(s.seq + l1, d2 + s2, l2);
         sink.submit_raw(s, l1, l2, n, true);
         batches += 1;
+        records += 2 * n;
     });
-    return {2 * r1[n1], 0, batches.load()};
+    return {records.load(), 0, batches.load()};
 }
 
 // Reader thread (cutting blocks of both files in step) + n_parsers parser threads feeding `sink`. With `split`, a
@@ -802,7 +813,7 @@ StreamTotals run_paired_split(const std::shared_ptr<Buf>& m1, const std::shared_
 // starts at byte 0, the chains join into exactly the records the sequential cutter finds. Throws NotSimple when a
 // block is not such a chain (the caller discards what was submitted and runs again without `split`).
 StreamTotals run_stream(const char* path1, const char* path2, uint32_t threads, Sink& sink, bool gpu_parse,
-                        bool split) {
+                        bool split, ShardSel shard = {}) {
     const bool paired = path2 != nullptr;
     const uint32_t n_parsers = std::max<uint32_t>(1, std::min<uint32_t>(threads ? threads : 1, 64));
     const uint64_t BLOCK_RECORDS = 1u << 15, BLOCK_BYTES = 12ull << 20;  // pipeline slots hold SLOT_BYTES
@@ -813,7 +824,7 @@ StreamTotals run_stream(const char* path1, const char* path2, uint32_t threads, 
     if (paired) c2 = std::make_unique<Cutter>(path2, threads, !try_split);
     if (try_split && paired) {
         std::shared_ptr<Buf> m1 = c1.mapping(), m2 = c2->mapping();
-        if (m1 && m2) return run_paired_split(m1, m2, n_parsers, sink);
+        if (m1 && m2) return run_paired_split(m1, m2, n_parsers, sink, shard);
     }
     Shared sh;
     sh.max_q = n_parsers + 1;
@@ -838,12 +849,13 @@ StreamTotals run_stream(const char* path1, const char* path2, uint32_t threads, 
             if (i == 0) throw NotSimple();
             target = std::min<uint64_t>(BLOCK_BYTES, std::max<uint64_t>(1u << 20, p / i * BLOCK_RECORDS));
         }
-        for (size_t pos = 0; pos < len;) {
+        for (size_t pos = 0, b = 0; pos < len; ++b) {
             const size_t e = len - pos <= target ? len : find_cut(data, len, pos + target);
             Work w;
             w.b1 = Block{map, pos, e, 0, true, 0};
             w.split = true;
-            if (!push(std::move(w))) return;
+            w.seq = b;
+            if (shard.mine(b) && !push(std::move(w))) return;
             pos = e;
         }
     };
@@ -856,7 +868,7 @@ StreamTotals run_stream(const char* path1, const char* path2, uint32_t threads, 
                 sh.cv_get.notify_all();
                 return;
             }
-            for (;;) {
+            for (uint64_t b = 0;; ++b) {
                 Work w;
                 w.b1 = c1.next(BLOCK_RECORDS, BLOCK_BYTES);
                 w.n = w.b1.n;
@@ -865,7 +877,8 @@ StreamTotals run_stream(const char* path1, const char* path2, uint32_t threads, 
                     w.n = std::min(w.n, w.b2.n);  // views::zip stops at the shorter file
                 }
                 const bool last = w.n == 0 || (paired && w.b2.n < w.b1.n);
-                if (w.n && !push(std::move(w))) return;
+                w.seq = b;
+                if (w.n && shard.mine(b) && !push(std::move(w))) return;
                 if (last) break;
             }
             std::lock_guard<std::mutex> lk(sh.mu);
@@ -993,9 +1006,10 @@ bool split_cut_enabled() {
 // The FASTQ scan over n >= 1 replicas of one index (one per GPU of this process): blocks are dealt to the replicas'
 // pipelines in turn and each replica's counters accumulate on its own device; the sums over replicas are taken on
 // the host at the end (G + 2 words per replica; the EM histograms are merged by speq_em_merge).
+// shard / cut: speq_scan_fastq_shard (one process per GPU); the defaults are the single-process behaviour.
 void scan_fastq_impl(speq_device_index* const* ds, speq_em* const* ems, uint32_t n_dev, const char* path1,
                      const char* path2, const speq_scan_params* params, uint32_t threads, uint64_t* counts,
-                     double* weights, speq_stream_stats* stats) {
+                     double* weights, speq_stream_stats* stats, ShardSel shard = {}, int cut = -1) {
     if (!ds || n_dev == 0 || !path1 || !params || !counts) throw std::invalid_argument("speq_scan_fastq: null argument");
     if (params->mode == SPEQ_MODE_LOCAL && !weights)
         throw std::invalid_argument("speq_scan_fastq: local mode needs weights");
@@ -1028,7 +1042,7 @@ void scan_fastq_impl(speq_device_index* const* ds, speq_em* const* ems, uint32_t
     std::vector<double> wscratch(std::max<uint32_t>(G, 1));
     auto attempt = [&](bool split) {
         try {
-            StreamTotals t = run_stream(path1, path2, threads, sink, gpu_parse, split);
+            StreamTotals t = run_stream(path1, path2, threads, sink, gpu_parse, split, shard);
             // split blocks are parsed on the GPU unchecked by the host: any failed check means a layout the
             // parallel cut cannot handle (or a malformed file) -> sequential run, which reports real errors
             if (split && gpu_parse) {
@@ -1044,10 +1058,14 @@ void scan_fastq_impl(speq_device_index* const* ds, speq_em* const* ems, uint32_t
     };
     StreamTotals tot;
     try {
-        tot = attempt(split_cut_enabled());
+        tot = attempt(cut < 0 ? split_cut_enabled() : cut == 1);
     } catch (const NotSimple&) {
         if (ems)
             for (uint32_t i = 0; i < n_dev; ++i) speq::em_clear(ems[i]);
+        if (cut == 1) {  // the other ranks must agree before anyone runs the sequential cutter
+            for (uint32_t i = 0; i < n_dev; ++i) speq::return_cached_pipeline(ds[i], guards[i].release());
+            throw speq::RetryError("speq_scan_fastq_shard: the parallel cut does not fit this input");
+        }
         tot = attempt(false);
     }
     std::fill(counts, counts + SPEQ_COUNTS_LEN(G), 0);
@@ -1084,6 +1102,41 @@ extern "C" int speq_scan_fastq_multi(speq_device_index* const* ds, speq_em* cons
                                      uint32_t threads, uint64_t* counts, double* weights, speq_stream_stats* stats) {
     return speq::guarded([&] {
         scan_fastq_impl(ds, ems, n_devices, path1, path2, params, threads, counts, weights, stats);
+    });
+}
+
+extern "C" int speq_scan_fastq_shard(speq_device_index* d, speq_em* em, const char* path1, const char* path2,
+                                     const speq_scan_params* params, uint32_t threads, uint32_t shard,
+                                     uint32_t n_shards, int cut, uint64_t* counts, double* weights,
+                                     speq_stream_stats* stats) {
+    return speq::guarded([&] {
+        if (n_shards == 0 || shard >= n_shards) throw std::invalid_argument("speq_scan_fastq_shard: bad shard");
+        if (cut < -1 || cut > 1) throw std::invalid_argument("speq_scan_fastq_shard: cut must be -1, 0 or 1");
+        if (cut == -1 && n_shards > 1)
+            throw std::invalid_argument("speq_scan_fastq_shard: several shards need cut 0 or 1 (ranks must agree)");
+        speq_em* ems[1] = {em};
+        scan_fastq_impl(&d, em ? ems : nullptr, 1, path1, path2, params, threads, counts, weights, stats,
+                        ShardSel{shard, n_shards}, cut);
+    });
+}
+
+extern "C" int speq_fastq_checksum_shard(const char* path1, const char* path2, uint32_t threads, uint32_t shard,
+                                         uint32_t n_shards, int cut, uint64_t* records, uint64_t* bases,
+                                         uint64_t* digest) {
+    return speq::guarded([&] {
+        if (!path1 || !records || !bases || !digest) throw std::invalid_argument("speq_fastq_checksum_shard: null argument");
+        if (n_shards == 0 || shard >= n_shards) throw std::invalid_argument("speq_fastq_checksum_shard: bad shard");
+        if (cut != 0 && cut != 1) throw std::invalid_argument("speq_fastq_checksum_shard: cut must be 0 or 1");
+        auto sink = std::make_unique<ChecksumSink>();
+        StreamTotals tot;
+        try {
+            tot = run_stream(path1, path2, threads, *sink, false, cut == 1, ShardSel{shard, n_shards});
+        } catch (const NotSimple&) {
+            throw speq::RetryError("speq_fastq_checksum_shard: the parallel cut does not fit this input");
+        }
+        *records = tot.records;
+        *bases = tot.bases;
+        *digest = sink->digest.load();
     });
 }
 

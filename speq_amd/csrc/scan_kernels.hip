@@ -1889,6 +1889,34 @@ int speq_ref_unique(speq_device_index* d, uint32_t k, uint64_t* u_ref, uint64_t*
     });
 }
 
+int speq_ref_unique_shard(speq_device_index* d, uint32_t k, uint32_t shard, uint32_t n_shards, uint64_t* u_ref,
+                          uint64_t* tot_ref) {
+    return speq::guarded([&] {
+        if (!d || !u_ref || !tot_ref) throw std::invalid_argument("speq_ref_unique_shard: null argument");
+        if (k < 1 || k > MAX_K) throw std::invalid_argument("speq_ref_unique_shard: k must be in [1, 4096]");
+        if (n_shards == 0 || shard >= n_shards) throw std::invalid_argument("speq_ref_unique_shard: bad shard");
+        DeviceGuard g(d->device);
+        const uint32_t G = d->G;
+        uint64_t* buf = nullptr;
+        uint64_t* d_cum = nullptr;
+        try {
+            HIP_OK(hipMalloc(&buf, 2ull * G * 8));
+            HIP_OK(hipMemsetAsync(buf, 0, 2ull * G * 8, d->stream));
+            d_cum = launch_ref_shard(d, k, shard, n_shards, buf, buf + G, d->stream);
+            HIP_OK(hipMemcpyAsync(u_ref, buf, G * 8, hipMemcpyDeviceToHost, d->stream));
+            HIP_OK(hipMemcpyAsync(tot_ref, buf + G, G * 8, hipMemcpyDeviceToHost, d->stream));
+            HIP_OK(hipStreamSynchronize(d->stream));
+        } catch (...) {
+            (void)hipStreamSynchronize(d->stream);
+            if (d_cum) (void)hipFree(d_cum);
+            if (buf) (void)hipFree(buf);
+            throw;
+        }
+        if (d_cum) HIP_OK(hipFree(d_cum));
+        HIP_OK(hipFree(buf));
+    });
+}
+
 int speq_device_prepare(speq_device_index* d, uint32_t k, uint64_t* distinct_kmers, uint64_t* table_bytes,
                         double* build_ms) {
     return speq::guarded([&] {

@@ -15,5 +15,9 @@ struct GroupsError : std::runtime_error {
 struct DeviceError : std::runtime_error {
     explicit DeviceError(const std::string& m) : std::runtime_error(m) {}
 };
+// the parallel FASTQ cut does not fit the file (SPEQ_E_RETRY): the caller runs the sequential cutter on every rank
+struct RetryError : std::runtime_error {
+    explicit RetryError(const std::string& m) : std::runtime_error(m) {}
+};
 
 }  // namespace speq

@@ -34,7 +34,7 @@ def test_python_binding_covers_header():
     L = lib()
     for name in declared():
         assert hasattr(L, name)
-    assert L.speq_abi_version() == 5
+    assert L.speq_abi_version() == 6
 
 
 def test_device_count_never_fails():

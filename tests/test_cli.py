@@ -186,3 +186,52 @@ def test_scan_sharded_over_replicas_matches_one_gpu(tmp_path, paired):
     assert outs["three"] == outs["one"]
     assert outs["all"] == outs["one"]
     assert "\t" in outs["one"][0]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("paired", [False, True])
+def test_scan_one_process_per_gpu_matches_one_process(tmp_path, paired):
+    """`torchrun --no-python bin/speq scan ...` with WORLD_SIZE = 2: each rank scans its share of the FASTQ blocks
+    and of the .dat windows on GPU $LOCAL_RANK and the counters, weights, .dat sums and EM histograms are summed with
+    RCCL (speq_allreduce_host / speq_em_allreduce); rank 0 prints and writes exactly what one process prints. With
+    one visible GPU both ranks use GPU 0 (--device 0); if RCCL refuses two ranks on one GPU the test is skipped."""
+    import socket
+    import sys
+    from speq_amd import synth
+    from test_gpu_stream import split, write_fastq
+    ref = synth.make_reference(4, 2, 20_000)
+    reads = synth.make_reads(ref, 60_000 if paired else 120_000, paired=paired, lowq_rate=0.002)
+    (tmp_path / "refs.fa").write_text(ref.fasta_text())
+    (tmp_path / "groups.txt").write_text(ref.groupings_text())
+    seqs, quals = split(reads)
+    if paired:
+        write_fastq(tmp_path / "r1.fq", seqs[0::2], quals[0::2])
+        write_fastq(tmp_path / "r2.fq", seqs[1::2], quals[1::2])
+    else:
+        write_fastq(tmp_path / "r1.fq", seqs, quals)
+    r = run(["index", "-r", "refs.fa", "-g", "groups.txt", "-x", "ref", "-o", "i.txt"], tmp_path)
+    assert r.returncode == 0, r.stderr
+    base = ["scan", "-1", "r1.fq", "-x", "ref", "-k", "21", "-t", "4"] + (["-2", "r2.fq"] if paired else [])
+    one = run(base + ["-o", "one.txt", "-f"], tmp_path)
+    assert one.returncode == 0, one.stderr
+    one_dat = (tmp_path / "ref_21mer.dat").read_bytes()
+    (tmp_path / "ref_21mer.dat").unlink()  # the ranks recompute the .dat pass, split two ways
+    import torch
+    extra = [] if torch.cuda.device_count() >= 2 else ["--device", "0"]
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    env = dict(os.environ, SPEQ_RENDEZVOUS=str(tmp_path / "rdzv"))
+    two = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node", "2",
+                          "--master-addr", "127.0.0.1", "--master-port", str(port), "--no-python", SPEQ] + base +
+                         extra + ["-o", "two.txt", "-f"], cwd=tmp_path, capture_output=True, text=True, timeout=300,
+                         env=env)
+    if two.returncode != 0 and not extra == [] and ("Duplicate GPU" in two.stderr or "ncclCommInitRank" in two.stderr
+                                                    or "joining the RCCL communicator" in two.stderr):
+        pytest.skip("RCCL refuses two ranks on one GPU: " + two.stderr[-300:])
+    assert two.returncode == 0, two.stderr[-3000:]
+    assert (tmp_path / "two.txt").read_text() == (tmp_path / "one.txt").read_text()
+    for line in one.stderr.splitlines():  # every result line of the one-process run, once, from rank 0
+        assert line in two.stderr, line
+    assert (tmp_path / "ref_21mer.dat").read_bytes() == one_dat  # written by rank 0 from the summed shards

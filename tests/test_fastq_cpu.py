@@ -247,3 +247,53 @@ def test_parallel_cut_matches_sequential(tmp_path, monkeypatch, case):
         assert checksum(p, threads=t) == want
     monkeypatch.setenv("SPEQ_SPLIT_CUT", "0")
     assert checksum(p, threads=4) == want
+
+
+def checksum_shard(p1, p2, shard, n_shards, cut, threads=3):
+    r, b, d = C.c_uint64(), C.c_uint64(), C.c_uint64()
+    check(lib().speq_fastq_checksum_shard(str(p1).encode(), str(p2).encode() if p2 else None, threads, shard,
+                                          n_shards, cut, C.byref(r), C.byref(b), C.byref(d)))
+    return r.value, b.value, d.value
+
+
+@pytest.mark.parametrize("case", ["simple", "wrapped_late", "gz", "paired"])
+def test_rank_shards_partition_the_records(tmp_path, case):
+    """`speq scan` with one process per GPU (speq_scan_fastq_shard): rank r of W takes the blocks b with b % W == r of
+    the same cut on every rank, so the W shards' records, bases and digests sum to the whole input. With the parallel
+    cut (cut = 1) a file it cannot take fails with SPEQ_E_RETRY on the rank that meets the irregular block (the CLI
+    then all-reduces that flag and every rank rescans with the sequential cutter, cut = 0)."""
+    recs = _simple_records(160_000, 11)
+    p2 = None
+    if case == "paired":
+        data1, data2 = render(recs[0::2]), render(recs[1::2])
+        p, p2 = tmp_path / "1.fq", tmp_path / "2.fq"
+        p.write_bytes(data1)
+        p2.write_bytes(data2)
+        exp = [r for pair in zip(parse_py(data1), parse_py(data2)) for r in pair]
+    else:
+        data = render(recs)
+        if case == "wrapped_late":
+            cut = data.index(b"\n@r", len(data) * 3 // 4) + 1
+            data = data[:cut] + b"@w\nACGT\nAC\n+\nIIII\nII\n" + data[cut:]
+        p = tmp_path / ("s.fq.gz" if case == "gz" else "s.fq")
+        (gzip.open(p, "wb", compresslevel=1) if case == "gz" else open(p, "wb")).write(data)
+        exp = parse_py(data)
+    want = (len(exp), sum(len(s) for s, _ in exp), digest(exp))
+    for W in (1, 2, 3, 4):
+        for cut in (0, 1):
+            parts, retry = [], 0
+            for r in range(W):
+                try:
+                    parts.append(checksum_shard(p, p2, r, W, cut))
+                except SpeqError as e:
+                    assert e.code == -6 and cut == 1 and case == "wrapped_late"
+                    retry += 1
+            if case == "wrapped_late" and cut == 1:
+                assert retry == 1  # exactly the rank holding the wrapped record's block
+                continue
+            tot = (sum(x[0] for x in parts), sum(x[1] for x in parts), sum(x[2] for x in parts) & M64)
+            assert tot == want, (W, cut)
+            if W > 1 and case != "paired":
+                assert all(x[0] > 0 for x in parts)  # several blocks: every rank has work
+    with pytest.raises(SpeqError):
+        checksum_shard(p, p2, 2, 2, 0)

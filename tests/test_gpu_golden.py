@@ -51,3 +51,32 @@ def test_rccl_allreduce_single_rank():
     torch.cuda.synchronize()
     assert x.cpu().tolist() == list(range(12)) and y.cpu().tolist() == [0.25] * 5
     check(L.speq_comm_destroy(comm))
+
+
+def test_comm_class_scan_allreduce_single_rank():
+    """The one-process-per-GPU step of bench.py at nranks = 1: scan on HBM-resident reads, then the product's RCCL
+    all-reduce (speq_amd.Comm -> speq_allreduce_u64/_f64) on the scan's stream leaves the counters unchanged."""
+    torch = pytest.importorskip("torch")
+    from speq_amd import Comm, DeviceIndex, FmIndex, synth
+    ref = synth.make_reference(4, 1, 8_000)
+    reads = synth.make_reads(ref, 3_000)
+    dev = DeviceIndex(FmIndex.build(ref.records, ref.groups, 4, prefix_q=8, pair_steps=True))
+    host = dev.scan(reads.seq.tobytes(), reads.qual.tobytes(), reads.offsets, k=21, local=True)
+    comm = Comm(1, 0, Comm.unique_id())
+    d_seq = torch.from_numpy(reads.seq).cuda()
+    d_qual = torch.from_numpy(reads.qual).cuda()
+    d_off = torch.from_numpy(reads.offsets.astype(np.int64)).cuda()
+    c = torch.zeros(6, dtype=torch.int64, device="cuda")
+    w = torch.zeros(4, dtype=torch.float64, device="cuda")
+    s = torch.cuda.current_stream().cuda_stream
+    dev.scan_device(d_seq.data_ptr(), d_qual.data_ptr(), d_off.data_ptr(), reads.n, 21, c.data_ptr(), w.data_ptr(),
+                    local=True, stream=s)
+    comm.allreduce_u64(c.data_ptr(), 6, s)
+    comm.allreduce_f64(w.data_ptr(), 4, s)
+    torch.cuda.synchronize()
+    got = c.cpu().numpy().astype(np.uint64)
+    assert got[0] == host.total and got[1] == host.ambiguous and np.array_equal(got[2:], host.unique)
+    np.testing.assert_allclose(w.cpu().numpy(), host.weights, rtol=1e-12)
+    comm.close()
+    with pytest.raises(ValueError):
+        Comm(1, 0, b"short")
