@@ -236,6 +236,51 @@ size_t temp_need(uint64_t raw_bytes, uint64_t n_slots) {
 
 }  // namespace
 
+namespace {
+// Packed host reads (pipeline_submit_packed): one byte per base, bits 0-1 the base (A C G T = 0..3), bits 2-7 the
+// Phred value clamped to [0, 41] (phred42), 63 for a base that is not A/C/G/T/U (dna5 N). Back to the (seq, qual)
+// bytes the scan kernels read: 'A' 'C' 'G' 'T' or 'N', quality 33 + q. 16 bases per thread, coalesced.
+__global__ void k_unpack_bases(const uint8_t* __restrict__ packed, uint64_t n, uint8_t* __restrict__ seq,
+                               uint8_t* __restrict__ qual) {
+    const uint64_t nv = (n + 15) / 16;
+    for (uint64_t v = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; v < nv; v += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t a = v * 16;
+        if (a + 16 <= n) {
+            const uint4 x = *reinterpret_cast<const uint4*>(packed + a);
+            const uint32_t w[4] = {x.x, x.y, x.z, x.w};
+            uint32_t so[4], qo[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const uint32_t c = w[i] & 0x03030303u, q = (w[i] >> 2) & 0x3F3F3F3Fu;
+                const uint32_t letters = __builtin_amdgcn_perm(0u, 0x54474341u, c);  // "ACGT" by code
+                const uint32_t y = q ^ 0x3F3F3F3Fu;  // zero byte <=> N
+                const uint32_t isn = ~(((y & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | y) & 0x80808080u;
+                const uint32_t nm = (isn >> 7) * 0xFFu;  // 0xFF in every N byte
+                so[i] = (letters & ~nm) | (0x4E4E4E4Eu & nm);
+                qo[i] = ((q + 0x21212121u) & ~nm) | (0x21212121u & nm);
+            }
+            *reinterpret_cast<uint4*>(seq + a) = make_uint4(so[0], so[1], so[2], so[3]);
+            *reinterpret_cast<uint4*>(qual + a) = make_uint4(qo[0], qo[1], qo[2], qo[3]);
+        } else {
+            for (uint64_t i = a; i < n; ++i) {
+                const uint32_t b = packed[i], q = b >> 2;
+                seq[i] = q == 63u ? 'N' : "ACGT"[b & 3u];
+                qual[i] = (uint8_t)(q == 63u ? 33u : 33u + q);
+            }
+        }
+    }
+}
+}  // namespace
+
+void launch_unpack_bases(const uint8_t* d_packed, uint64_t n, uint8_t* d_seq, uint8_t* d_qual, void* stream) {
+    if (n == 0) return;
+    const uint64_t nv = (n + 15) / 16;
+    const uint32_t grid = (uint32_t)std::min<uint64_t>((nv + 255) / 256, 8192);
+    hipLaunchKernelGGL(k_unpack_bases, dim3(grid), dim3(256), 0, static_cast<hipStream_t>(stream), d_packed, n, d_seq,
+                       d_qual);
+    FHIP(hipGetLastError());
+}
+
 size_t fastq_gpu_scratch_bytes(uint64_t raw_bytes, uint64_t records_per_file, bool paired) {
     const uint64_t n_slots = records_per_file * (paired ? 2 : 1);
     return layout(raw_bytes, n_slots, 4 * records_per_file, temp_need(raw_bytes, n_slots)).total;

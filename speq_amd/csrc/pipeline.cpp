@@ -6,6 +6,7 @@
 // behind that event, so the PCIe copy of slot i+1 overlaps the scan of slot i. A slot is handed out again only after
 // the event recorded behind its kernel has completed (its host and device buffers are then free).
 #include <hip/hip_runtime.h>
+#include <immintrin.h>
 
 #include <algorithm>
 #include <atomic>
@@ -360,6 +361,93 @@ void pipeline_submit_raw(speq_pipeline* pl, int32_t slot, uint64_t len1, uint64_
     s.pending = true;
 }
 
+// Host packer of the one-byte-per-base format (launch_unpack_bases): dna5 (A C G T, U as T, any case; everything else
+// N = 63) and phred42 (byte - 33 clamped to [0, 41]), as the kernels read them. AVX2 when the CPU has it.
+namespace {
+inline uint8_t pack_one(uint8_t sc, uint8_t qc) {
+    const uint32_t x = sc | 0x20u;
+    const bool ok = x == 'a' || x == 'c' || x == 'g' || x == 't' || x == 'u';
+    if (!ok) return 63u << 2;
+    const uint32_t code = ((x >> 1) ^ (x >> 2)) & 3u;
+    const uint32_t q = qc < 33u ? 0u : std::min<uint32_t>(qc - 33u, 41u);
+    return (uint8_t)(code | (q << 2));
+}
+
+__attribute__((target("avx2"))) void pack_avx2(uint8_t* out, const uint8_t* seq, const uint8_t* qual, uint64_t n) {
+    const __m256i lc = _mm256_set1_epi8(0x20), q33 = _mm256_set1_epi8(33), q41 = _mm256_set1_epi8(41);
+    const __m256i A = _mm256_set1_epi8('a'), Cc = _mm256_set1_epi8('c'), Gg = _mm256_set1_epi8('g'),
+                  Tt = _mm256_set1_epi8('t'), Uu = _mm256_set1_epi8('u'), three = _mm256_set1_epi8(3),
+                  nval = _mm256_set1_epi8((char)(63 << 2));
+    uint64_t i = 0;
+    for (; i + 32 <= n; i += 32) {
+        const __m256i x = _mm256_or_si256(_mm256_loadu_si256(reinterpret_cast<const __m256i*>(seq + i)), lc);
+        const __m256i ok = _mm256_or_si256(
+            _mm256_or_si256(_mm256_cmpeq_epi8(x, A), _mm256_cmpeq_epi8(x, Cc)),
+            _mm256_or_si256(_mm256_or_si256(_mm256_cmpeq_epi8(x, Gg), _mm256_cmpeq_epi8(x, Tt)),
+                            _mm256_cmpeq_epi8(x, Uu)));
+        // ((x >> 1) ^ (x >> 2)) & 3 per byte (16-bit shifts: the bits that cross bytes are masked off)
+        const __m256i code = _mm256_and_si256(_mm256_xor_si256(_mm256_srli_epi16(x, 1), _mm256_srli_epi16(x, 2)), three);
+        const __m256i q = _mm256_min_epu8(
+            _mm256_subs_epu8(_mm256_loadu_si256(reinterpret_cast<const __m256i*>(qual + i)), q33), q41);
+        const __m256i v = _mm256_or_si256(code, _mm256_slli_epi16(q, 2));  // q <= 41: q << 2 stays in its byte
+        _mm256_storeu_si256(reinterpret_cast<__m256i*>(out + i), _mm256_blendv_epi8(nval, v, ok));
+    }
+    for (; i < n; ++i) out[i] = pack_one(seq[i], qual[i]);
+}
+}  // namespace
+
+void pack_bases(uint8_t* out, const uint8_t* seq, const uint8_t* qual, uint64_t n) {
+    static const bool avx2 = __builtin_cpu_supports("avx2");
+    if (avx2) {
+        pack_avx2(out, seq, qual, n);
+        return;
+    }
+    for (uint64_t i = 0; i < n; ++i) out[i] = pack_one(seq[i], qual[i]);
+}
+
+void pipeline_submit_packed(speq_pipeline* pl, int32_t slot, uint64_t n_records) {
+    struct Release {
+        speq_pipeline* pl;
+        int32_t slot;
+        ~Release() {
+            {
+                std::lock_guard<std::mutex> lk(pl->mu);
+                pl->free_slots.push_back(slot);
+            }
+            pl->cv.notify_one();
+        }
+    } release{pl, slot};
+    if (slot < 0 || (size_t)slot >= pl->slots.size()) throw std::invalid_argument("pipeline_submit_packed: bad slot");
+    Slot& s = pl->slots[(size_t)slot];
+    if (n_records == 0) return;
+    if (n_records > s.cap_records) throw std::invalid_argument("pipeline_submit_packed: more records than capacity");
+    if (pl->p.paired && (n_records & 1))
+        throw std::invalid_argument("pipeline_submit_packed: paired scan needs an even record count");
+    const uint64_t bytes = s.h_off[n_records];
+    if (s.h_off[0] != 0 || bytes > s.cap_bytes) throw std::invalid_argument("pipeline_submit_packed: bad offsets");
+    DevScope g(pl->device);
+    if (bytes > s.parse_bytes || n_records > s.parse_slots) {  // unpacked (seq, qual): the parse buffers
+        const uint64_t pb = std::max({bytes, s.parse_bytes * 3 / 2, s.cap_bytes});
+        const uint64_t ps = std::max({n_records, s.parse_slots * 3 / 2, s.cap_records});
+        free_parse(s);
+        hip_ok(hipMalloc(reinterpret_cast<void**>(&s.d_pseq), pb + 16), "hipMalloc");
+        hip_ok(hipMalloc(reinterpret_cast<void**>(&s.d_pqual), pb + 16), "hipMalloc");
+        s.parse_bytes = pb;
+        s.parse_slots = ps;
+    }
+    std::lock_guard<std::mutex> lk(pl->submit_mu);
+    if (bytes) hip_ok(hipMemcpyAsync(s.d_seq, s.h_seq, bytes, hipMemcpyHostToDevice, pl->copy), "hipMemcpyAsync");
+    hip_ok(hipMemcpyAsync(s.d_off, s.h_off, (n_records + 1) * 8, hipMemcpyHostToDevice, pl->copy), "hipMemcpyAsync");
+    hip_ok(hipEventRecord(s.copied, pl->copy), "hipEventRecord");
+    hipStream_t cs = pl->lane();
+    hip_ok(hipStreamWaitEvent(cs, s.copied, 0), "hipStreamWaitEvent");
+    launch_unpack_bases(s.d_seq, bytes, s.d_pseq, s.d_pqual, cs);
+    launch_reads_scan(pl->d, s.d_pseq, s.d_pqual, s.d_off, n_records, &pl->p, pl->d_counts, pl->d_w,
+                      pl->em ? pl->em->d_mult : nullptr, pl->em ? pl->em->d_hi : nullptr, cs);
+    hip_ok(hipEventRecord(s.done, cs), "hipEventRecord");
+    s.pending = true;
+}
+
 int32_t pipeline_acquire_raw(speq_pipeline* pl, uint64_t bytes, uint8_t** text) {
     const int i = take_slot(pl, std::max(bytes, pl->slot_bytes), pl->slot_records, false);
     *text = pl->slots[(size_t)i].h_seq;
@@ -502,7 +590,11 @@ void scan_host_pipelined(speq_device_index* d, const uint8_t* seq, const uint8_t
         max_recs = std::max(max_recs, r1 - r0);
         r0 = r1;
     }
-    const uint32_t fillers = (uint32_t)std::min<size_t>(4, batches.size());
+    // Reads cross PCIe packed, one byte per base instead of two (pack_bases; SPEQ_HOST_PACK=0: ASCII bases and
+    // qualities as given, for A/B), with eight filler threads packing batches into the pinned slots.
+    const char* hp = std::getenv("SPEQ_HOST_PACK");
+    const bool packed = !(hp && hp[0] == '0');
+    const uint32_t fillers = (uint32_t)std::min<size_t>(packed ? 8 : 4, batches.size());
     std::unique_ptr<speq_pipeline, void (*)(speq_pipeline*)> guard(take_pipeline(d, p, em, max_bytes, max_recs, 6),
                                                                    speq_pipeline_free);
     speq_pipeline* pl = guard.get();
@@ -528,11 +620,22 @@ void scan_host_pipelined(speq_device_index* d, const uint8_t* seq, const uint8_t
                 (void)speq_pipeline_submit(pl, s.slot, 0);
                 return;
             }
+            for (uint64_t i = r0; i <= r1; ++i) s.offsets[i - r0] = offsets[i] - base;
+            if (packed) {
+                if (nb) pack_bases(s.seq, seq + base, qual + base, nb);
+                try {
+                    pipeline_submit_packed(pl, s.slot, r1 - r0);
+                } catch (const std::exception& e) {
+                    std::lock_guard<std::mutex> lk(err_mu);
+                    if (err.empty()) err = e.what();
+                    return;
+                }
+                continue;
+            }
             if (nb) {
                 std::memcpy(s.seq, seq + base, nb);
                 std::memcpy(s.qual, qual + base, nb);
             }
-            for (uint64_t i = r0; i <= r1; ++i) s.offsets[i - r0] = offsets[i] - base;
             if (speq_pipeline_submit(pl, s.slot, r1 - r0) != SPEQ_OK) {
                 std::lock_guard<std::mutex> lk(err_mu);
                 if (err.empty()) err = speq_last_error();

@@ -26,6 +26,13 @@ size_t fastq_gpu_scratch_bytes(uint64_t raw_bytes, uint64_t records_per_file, bo
 void launch_fastq_parse(const uint8_t* d_raw, uint64_t len1, uint64_t len2, uint64_t n, bool paired, void* d_scratch,
                         size_t scratch_bytes, uint8_t* d_seq, uint8_t* d_qual, uint64_t* d_off, uint32_t* d_err,
                         uint64_t* d_total_bases, void* stream);
+// Packed bases (one byte per base: bits 0-1 A C G T, bits 2-7 Phred clamped to [0, 41] or 63 for N) back to the
+// ASCII (seq, qual) layout of the scan kernels (fastq_gpu.hip), and the host packer of that format (pipeline.cpp).
+void launch_unpack_bases(const uint8_t* d_packed, uint64_t n, uint8_t* d_seq, uint8_t* d_qual, void* stream);
+void pack_bases(uint8_t* out, const uint8_t* seq, const uint8_t* qual, uint64_t n);
+// Submits an acquired slot whose base buffer holds n_records PACKED reads (offsets as usual): half the bytes of
+// (seq, qual) cross PCIe, and the GPU unpacks them before the scan (pipeline.cpp).
+void pipeline_submit_packed(speq_pipeline* pl, int32_t slot, uint64_t n_records);
 // Submits an acquired pipeline slot whose host buffer holds RAW four-line FASTQ text (file 1's block, then file
 // 2's when paired, n records each): copied as is, parsed on the GPU, then scanned (pipeline.cpp).
 void pipeline_submit_raw(speq_pipeline* pl, int32_t slot, uint64_t len1, uint64_t len2, uint64_t n, bool paired);
