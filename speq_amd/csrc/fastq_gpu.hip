@@ -270,7 +270,52 @@ __global__ void k_unpack_bases(const uint8_t* __restrict__ packed, uint64_t n, u
         }
     }
 }
+
+// Global-mode packing (pipeline_submit_packed3): 2 bits per base (A C G T) in u64 words of 32 bases, then one "bad"
+// bit per base (not A/C/G/T/U, or Phred <= cutoff) in u32 words. A bad base comes back as 'N' and a good one with the
+// largest phred42 quality: window validity (fm_scanner.cpp:162) is unchanged, and global mode reads nothing else.
+__global__ void k_unpack_bases3(const uint64_t* __restrict__ codes, const uint32_t* __restrict__ bad, uint64_t n,
+                                uint8_t* __restrict__ seq, uint8_t* __restrict__ qual) {
+    const uint64_t nw = (n + 31) / 32;
+    for (uint64_t w = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; w < nw; w += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t c = codes[w];
+        const uint32_t b = bad[w];
+        uint32_t so[8], qo[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const uint32_t cb = (uint32_t)(c >> (8 * i)) & 0xFFu;  // four 2-bit codes
+            const uint32_t c4 = (cb & 3u) | (((cb >> 2) & 3u) << 8) | (((cb >> 4) & 3u) << 16) | ((cb >> 6) << 24);
+            const uint32_t bb = (b >> (4 * i)) & 0xFu;
+            const uint32_t nm = ((bb * 0x00204081u) & 0x01010101u) * 0xFFu;  // 0xFF in every bad byte
+            const uint32_t letters = __builtin_amdgcn_perm(0u, 0x54474341u, c4);
+            so[i] = (letters & ~nm) | (0x4E4E4E4Eu & nm);
+            qo[i] = 0x4A4A4A4Au;  // 'J' = 33 + 41
+        }
+        const uint64_t a = w * 32;
+        if (a + 32 <= n) {
+            *reinterpret_cast<uint4*>(seq + a) = make_uint4(so[0], so[1], so[2], so[3]);
+            *reinterpret_cast<uint4*>(seq + a + 16) = make_uint4(so[4], so[5], so[6], so[7]);
+            *reinterpret_cast<uint4*>(qual + a) = make_uint4(qo[0], qo[1], qo[2], qo[3]);
+            *reinterpret_cast<uint4*>(qual + a + 16) = make_uint4(qo[4], qo[5], qo[6], qo[7]);
+        } else {
+            for (uint64_t i = a; i < n; ++i) {
+                seq[i] = (uint8_t)(so[(i - a) >> 2] >> (8 * ((i - a) & 3u)));
+                qual[i] = 0x4Au;
+            }
+        }
+    }
+}
 }  // namespace
+
+void launch_unpack_bases3(const uint64_t* d_codes, const uint32_t* d_bad, uint64_t n, uint8_t* d_seq, uint8_t* d_qual,
+                          void* stream) {
+    if (n == 0) return;
+    const uint64_t nw = (n + 31) / 32;
+    const uint32_t grid = (uint32_t)std::min<uint64_t>((nw + 255) / 256, 8192);
+    hipLaunchKernelGGL(k_unpack_bases3, dim3(grid), dim3(256), 0, static_cast<hipStream_t>(stream), d_codes, d_bad, n,
+                       d_seq, d_qual);
+    FHIP(hipGetLastError());
+}
 
 void launch_unpack_bases(const uint8_t* d_packed, uint64_t n, uint8_t* d_seq, uint8_t* d_qual, void* stream) {
     if (n == 0) return;

@@ -396,6 +396,75 @@ __attribute__((target("avx2"))) void pack_avx2(uint8_t* out, const uint8_t* seq,
 }
 }  // namespace
 
+namespace {
+// 2-bit code (bits 0-1) and bad flag (bit 7 set) of one base for pack_bases3
+inline void pack3_one(uint8_t sc, uint8_t qc, uint32_t cutoff, uint64_t& code, bool& bad) {
+    const uint32_t x = sc | 0x20u;
+    const bool ok = x == 'a' || x == 'c' || x == 'g' || x == 't' || x == 'u';
+    const uint32_t q = qc < 33u ? 0u : std::min<uint32_t>(qc - 33u, 41u);
+    code = ok ? (((x >> 1) ^ (x >> 2)) & 3u) : 0u;
+    bad = !ok || q <= cutoff;
+}
+
+void pack3_scalar(uint64_t* codes, uint32_t* bad, const uint8_t* seq, const uint8_t* qual, uint64_t n,
+                  uint32_t cutoff, uint64_t w0) {
+    for (uint64_t w = w0; w * 32 < n; ++w) {
+        uint64_t c = 0;
+        uint32_t b = 0;
+        for (uint32_t i = 0; i < 32; ++i) {
+            const uint64_t j = w * 32 + i;
+            uint64_t ci = 0;
+            bool bi = true;
+            if (j < n) pack3_one(seq[j], qual[j], cutoff, ci, bi);
+            c |= ci << (2 * i);
+            b |= (uint32_t)bi << i;
+        }
+        codes[w] = c;
+        bad[w] = b;
+    }
+}
+
+__attribute__((target("avx2,bmi2"))) void pack3_avx2(uint64_t* codes, uint32_t* bad, const uint8_t* seq,
+                                                     const uint8_t* qual, uint64_t n, uint32_t cutoff) {
+    const __m256i lc = _mm256_set1_epi8(0x20), q33 = _mm256_set1_epi8(33), q41 = _mm256_set1_epi8(41);
+    const __m256i A = _mm256_set1_epi8('a'), Cc = _mm256_set1_epi8('c'), Gg = _mm256_set1_epi8('g'),
+                  Tt = _mm256_set1_epi8('t'), Uu = _mm256_set1_epi8('u'), three = _mm256_set1_epi8(3);
+    const __m256i cut = _mm256_set1_epi8((char)std::min<uint32_t>(cutoff, 41u));
+    const bool all_bad = cutoff >= 41u;
+    uint64_t w = 0;
+    for (; (w + 1) * 32 <= n; ++w) {
+        const uint64_t i = w * 32;
+        const __m256i x = _mm256_or_si256(_mm256_loadu_si256(reinterpret_cast<const __m256i*>(seq + i)), lc);
+        const __m256i ok = _mm256_or_si256(
+            _mm256_or_si256(_mm256_cmpeq_epi8(x, A), _mm256_cmpeq_epi8(x, Cc)),
+            _mm256_or_si256(_mm256_or_si256(_mm256_cmpeq_epi8(x, Gg), _mm256_cmpeq_epi8(x, Tt)),
+                            _mm256_cmpeq_epi8(x, Uu)));
+        const __m256i code = _mm256_and_si256(
+            _mm256_and_si256(_mm256_xor_si256(_mm256_srli_epi16(x, 1), _mm256_srli_epi16(x, 2)), three), ok);
+        const __m256i q = _mm256_min_epu8(
+            _mm256_subs_epu8(_mm256_loadu_si256(reinterpret_cast<const __m256i*>(qual + i)), q33), q41);
+        // good <=> ok and q > cutoff (unsigned: max(q, cut) != cut)
+        const __m256i qgood = _mm256_xor_si256(_mm256_cmpeq_epi8(_mm256_max_epu8(q, cut), cut),
+                                               _mm256_set1_epi8(-1));
+        const uint32_t good = (uint32_t)_mm256_movemask_epi8(_mm256_and_si256(ok, qgood));
+        alignas(32) uint64_t cb[4];
+        _mm256_store_si256(reinterpret_cast<__m256i*>(cb), code);
+        uint64_t c = 0;
+        for (int t = 0; t < 4; ++t) c |= _pext_u64(cb[t], 0x0303030303030303ull) << (16 * t);
+        codes[w] = c;
+        bad[w] = all_bad ? ~0u : ~good;
+    }
+    pack3_scalar(codes, bad, seq, qual, n, cutoff, w);
+}
+}  // namespace
+
+void pack_bases3(uint64_t* codes, uint32_t* bad, const uint8_t* seq, const uint8_t* qual, uint64_t n,
+                 uint32_t cutoff) {
+    static const bool fast = __builtin_cpu_supports("avx2") && __builtin_cpu_supports("bmi2");
+    if (fast) pack3_avx2(codes, bad, seq, qual, n, cutoff);
+    else pack3_scalar(codes, bad, seq, qual, n, cutoff, 0);
+}
+
 void pack_bases(uint8_t* out, const uint8_t* seq, const uint8_t* qual, uint64_t n) {
     static const bool avx2 = __builtin_cpu_supports("avx2");
     if (avx2) {
@@ -405,7 +474,14 @@ void pack_bases(uint8_t* out, const uint8_t* seq, const uint8_t* qual, uint64_t 
     for (uint64_t i = 0; i < n; ++i) out[i] = pack_one(seq[i], qual[i]);
 }
 
+void pipeline_submit_packed_impl(speq_pipeline* pl, int32_t slot, uint64_t n_records, bool three);
 void pipeline_submit_packed(speq_pipeline* pl, int32_t slot, uint64_t n_records) {
+    pipeline_submit_packed_impl(pl, slot, n_records, false);
+}
+void pipeline_submit_packed3(speq_pipeline* pl, int32_t slot, uint64_t n_records) {
+    pipeline_submit_packed_impl(pl, slot, n_records, true);
+}
+void pipeline_submit_packed_impl(speq_pipeline* pl, int32_t slot, uint64_t n_records, bool three) {
     struct Release {
         speq_pipeline* pl;
         int32_t slot;
@@ -423,8 +499,9 @@ void pipeline_submit_packed(speq_pipeline* pl, int32_t slot, uint64_t n_records)
     if (n_records > s.cap_records) throw std::invalid_argument("pipeline_submit_packed: more records than capacity");
     if (pl->p.paired && (n_records & 1))
         throw std::invalid_argument("pipeline_submit_packed: paired scan needs an even record count");
-    const uint64_t bytes = s.h_off[n_records];
-    if (s.h_off[0] != 0 || bytes > s.cap_bytes) throw std::invalid_argument("pipeline_submit_packed: bad offsets");
+    const uint64_t bytes = s.h_off[n_records];  // bases
+    const uint64_t wire = three ? packed3_bytes(bytes) : bytes;
+    if (s.h_off[0] != 0 || wire > s.cap_bytes) throw std::invalid_argument("pipeline_submit_packed: bad offsets");
     DevScope g(pl->device);
     if (bytes > s.parse_bytes || n_records > s.parse_slots) {  // unpacked (seq, qual): the parse buffers
         const uint64_t pb = std::max({bytes, s.parse_bytes * 3 / 2, s.cap_bytes});
@@ -436,12 +513,18 @@ void pipeline_submit_packed(speq_pipeline* pl, int32_t slot, uint64_t n_records)
         s.parse_slots = ps;
     }
     std::lock_guard<std::mutex> lk(pl->submit_mu);
-    if (bytes) hip_ok(hipMemcpyAsync(s.d_seq, s.h_seq, bytes, hipMemcpyHostToDevice, pl->copy), "hipMemcpyAsync");
+    if (bytes) hip_ok(hipMemcpyAsync(s.d_seq, s.h_seq, wire, hipMemcpyHostToDevice, pl->copy), "hipMemcpyAsync");
     hip_ok(hipMemcpyAsync(s.d_off, s.h_off, (n_records + 1) * 8, hipMemcpyHostToDevice, pl->copy), "hipMemcpyAsync");
     hip_ok(hipEventRecord(s.copied, pl->copy), "hipEventRecord");
     hipStream_t cs = pl->lane();
     hip_ok(hipStreamWaitEvent(cs, s.copied, 0), "hipStreamWaitEvent");
-    launch_unpack_bases(s.d_seq, bytes, s.d_pseq, s.d_pqual, cs);
+    if (three) {
+        const uint64_t nw = (bytes + 31) / 32;
+        launch_unpack_bases3(reinterpret_cast<const uint64_t*>(s.d_seq),
+                             reinterpret_cast<const uint32_t*>(s.d_seq + nw * 8), bytes, s.d_pseq, s.d_pqual, cs);
+    } else {
+        launch_unpack_bases(s.d_seq, bytes, s.d_pseq, s.d_pqual, cs);
+    }
     launch_reads_scan(pl->d, s.d_pseq, s.d_pqual, s.d_off, n_records, &pl->p, pl->d_counts, pl->d_w,
                       pl->em ? pl->em->d_mult : nullptr, pl->em ? pl->em->d_hi : nullptr, cs);
     hip_ok(hipEventRecord(s.done, cs), "hipEventRecord");
@@ -578,7 +661,15 @@ void scan_host_pipelined(speq_device_index* d, const uint8_t* seq, const uint8_t
     if (offsets[n_reads] > offsets[0] && (!seq || !qual)) throw std::invalid_argument("speq_scan_reads: null read buffer");
     // 16 MiB batches, four filler threads: 4-32 MiB x 4-8 fillers all land at 32-34 GB/s of host bytes on the box
     // (profiles/r01/ab_host_batches.txt); 4 MiB loses to per-batch overheads.
-    const uint64_t BATCH_BYTES = 16ull << 20, BATCH_RECORDS = 1u << 16;
+    auto env_u = [](const char* name, uint64_t dflt) {  // A/B knobs (scripts/host_path_probe.py)
+        const char* v = std::getenv(name);
+        return v && *v ? std::strtoull(v, nullptr, 10) : dflt;
+    };
+    const char* hp = std::getenv("SPEQ_HOST_PACK");
+    const bool packed = !(hp && hp[0] == '0');
+    // packed batches: 8 MiB of reads, 12 fillers, 12 slots (profiles/r02/host_probe*.jsonl: cfg 2 host arrays
+    // 5.5 -> 3.3 ms against 16 MiB x 8 x 6); ASCII: 16 MiB x 4 x 6 (profiles/r01/ab_host_batches.txt)
+    const uint64_t BATCH_BYTES = env_u("SPEQ_HOST_BATCH_MB", packed ? 8 : 16) << 20, BATCH_RECORDS = 1u << 16;
     const uint64_t step = p->paired ? 2 : 1;
     std::vector<std::pair<uint64_t, uint64_t>> batches;
     uint64_t max_bytes = 1, max_recs = step;
@@ -590,12 +681,16 @@ void scan_host_pipelined(speq_device_index* d, const uint8_t* seq, const uint8_t
         max_recs = std::max(max_recs, r1 - r0);
         r0 = r1;
     }
-    // Reads cross PCIe packed, one byte per base instead of two (pack_bases; SPEQ_HOST_PACK=0: ASCII bases and
-    // qualities as given, for A/B), with eight filler threads packing batches into the pinned slots.
-    const char* hp = std::getenv("SPEQ_HOST_PACK");
-    const bool packed = !(hp && hp[0] == '0');
-    const uint32_t fillers = (uint32_t)std::min<size_t>(packed ? 8 : 4, batches.size());
-    std::unique_ptr<speq_pipeline, void (*)(speq_pipeline*)> guard(take_pipeline(d, p, em, max_bytes, max_recs, 6),
+    // Reads cross PCIe packed (SPEQ_HOST_PACK=0: ASCII bases and qualities as given, for A/B): one byte per base
+    // (pack_bases) in local mode, 3 bits per base (pack_bases3) in global mode; filler threads pack the batches
+    // straight into the pinned slots.
+    // global mode reads only "bad or not" of a quality: 3 bits per base (SPEQ_HOST_PACK=1: the byte format)
+    const bool three = packed && p->mode == SPEQ_MODE_GLOBAL && !(hp && hp[0] == '1');
+    const uint32_t fillers = (uint32_t)std::min<size_t>(env_u("SPEQ_HOST_FILLERS", packed ? 12 : 4), batches.size());
+    const uint32_t n_slots =
+        (uint32_t)std::min<uint64_t>(64, std::max<uint64_t>(2, env_u("SPEQ_HOST_SLOTS", packed ? 12 : 6)));
+    std::unique_ptr<speq_pipeline, void (*)(speq_pipeline*)> guard(take_pipeline(d, p, em, max_bytes, max_recs,
+                                                                                 n_slots),
                                                                    speq_pipeline_free);
     speq_pipeline* pl = guard.get();
     std::atomic<size_t> next{0};
@@ -622,8 +717,16 @@ void scan_host_pipelined(speq_device_index* d, const uint8_t* seq, const uint8_t
             }
             for (uint64_t i = r0; i <= r1; ++i) s.offsets[i - r0] = offsets[i] - base;
             if (packed) {
-                if (nb) pack_bases(s.seq, seq + base, qual + base, nb);
                 try {
+                    if (three) {
+                        const uint64_t nw = (nb + 31) / 32;
+                        if (nb)
+                            pack_bases3(reinterpret_cast<uint64_t*>(s.seq), reinterpret_cast<uint32_t*>(s.seq + nw * 8),
+                                        seq + base, qual + base, nb, p->phred_cutoff);
+                        pipeline_submit_packed3(pl, s.slot, r1 - r0);
+                        continue;
+                    }
+                    if (nb) pack_bases(s.seq, seq + base, qual + base, nb);
                     pipeline_submit_packed(pl, s.slot, r1 - r0);
                 } catch (const std::exception& e) {
                     std::lock_guard<std::mutex> lk(err_mu);

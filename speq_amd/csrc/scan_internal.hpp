@@ -33,6 +33,13 @@ void pack_bases(uint8_t* out, const uint8_t* seq, const uint8_t* qual, uint64_t 
 // Submits an acquired slot whose base buffer holds n_records PACKED reads (offsets as usual): half the bytes of
 // (seq, qual) cross PCIe, and the GPU unpacks them before the scan (pipeline.cpp).
 void pipeline_submit_packed(speq_pipeline* pl, int32_t slot, uint64_t n_records);
+// Global mode: 2-bit bases + one bad bit per base (not ACGTU, or Phred <= cutoff), 3 bits per base instead of 16
+// (fastq_gpu.hip unpacks, pipeline.cpp packs; the slot's base buffer holds the code words, then the bad words).
+void launch_unpack_bases3(const uint64_t* d_codes, const uint32_t* d_bad, uint64_t n, uint8_t* d_seq, uint8_t* d_qual,
+                          void* stream);
+void pack_bases3(uint64_t* codes, uint32_t* bad, const uint8_t* seq, const uint8_t* qual, uint64_t n, uint32_t cutoff);
+inline uint64_t packed3_bytes(uint64_t n) { return (n + 31) / 32 * 12; }
+void pipeline_submit_packed3(speq_pipeline* pl, int32_t slot, uint64_t n_records);
 // Submits an acquired pipeline slot whose host buffer holds RAW four-line FASTQ text (file 1's block, then file
 // 2's when paired, n records each): copied as is, parsed on the GPU, then scanned (pipeline.cpp).
 void pipeline_submit_raw(speq_pipeline* pl, int32_t slot, uint64_t len1, uint64_t len2, uint64_t n, bool paired);
