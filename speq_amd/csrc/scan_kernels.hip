@@ -103,8 +103,8 @@ __device__ __forceinline__ uint64_t kt_code(uint64_t key, uint32_t k) {
 // slot = ck << (64 - 2k) | payload with ck = plane0 | plane1 << k (the window's two bit planes, k bits each); payload = the
 // group id, or (1 << (pb - 1)) | m for a k-mer whose occurrences span >= 2 groups, m indexing kt_multi[] = {lo, hi}
 // (read by EM scans only); pb = 64 - 2k >= 18 bits. All-ones = empty (no valid payload is all ones). Any bucket count
-// nb (bucket = mulhi(hash, nb)), so the table is sized for a load of exactly 1/2: 4.6 MB at cfg 2 against 16 MB for
-// the 16-B-slot form, small enough to stay mostly in L2.
+// nb (bucket = mulhi(hash, nb)), so the table is sized for an exact load factor (kt_load8, 35 % by default: 7.3 MB at
+// cfg 2) against 16 MB for the 16-B-slot form, small enough to stay mostly in L2.
 constexpr uint32_t KT8_MAX_K = 23;
 __host__ __device__ __forceinline__ uint32_t kt8_bucket(uint64_t key64, uint32_t nb) {
     return (uint32_t)(((uint64_t)kt_hash(key64) * nb) >> 32);
@@ -1272,11 +1272,23 @@ speq_device_index::KmerTable build_ktab(speq_device_index* d, uint32_t k) {
     void* keys = nullptr;
     uint64_t* d_cum = nullptr;
     unsigned long long* d_cnt = nullptr;
+    void* tab = nullptr;       // compact-table build: freed here unless handed to the replica
+    uint2* multi = nullptr;
+    unsigned int* d_nm = nullptr;
     auto cleanup = [&] {
         (void)hipStreamSynchronize(d->stream);
         if (keys) (void)hipFree(keys);
         if (d_cum) (void)hipFree(d_cum);
         if (d_cnt) (void)hipFree(d_cnt);
+        if (tab) (void)hipFree(tab);
+        if (multi) (void)hipFree(multi);
+        if (d_nm) (void)hipFree(d_nm);
+        keys = nullptr;
+        d_cum = nullptr;
+        d_cnt = nullptr;
+        tab = nullptr;
+        multi = nullptr;
+        d_nm = nullptr;
     };
     try {
         unsigned long long distinct = 0;
@@ -1308,10 +1320,14 @@ speq_device_index::KmerTable build_ktab(speq_device_index* d, uint32_t k) {
         const uint32_t pbits = 64u - 2u * k;
         const uint64_t multi_cap = std::min<uint64_t>(distinct, (1ull << (pbits - 1u)) - 2u);
         const uint64_t nb8 = std::max<uint64_t>(1, (uint64_t)((double)distinct * 100.0 / (8.0 * d->kt_load8)) + 1);
-        if (d->kt_compact && KT_BSLOTS == 4 && k <= KT8_MAX_K && distinct > 0 && nb8 < (1ull << 32)) {
-            void* tab = nullptr;
-            uint2* multi = nullptr;
-            unsigned int* d_nm = nullptr;
+        // the fill writes the multi-group k-mers into a scratch array of the worst-case size (every distinct k-mer),
+        // copied to one of the exact size afterwards; the free-memory check covers the scratch
+        const bool try_compact = d->kt_compact && KT_BSLOTS == 4 && k <= KT8_MAX_K && distinct > 0 && nb8 < (1ull << 32);
+        if (try_compact && nb8 * 64 + std::max<uint64_t>(multi_cap, 1) * 8 > free_b / 10 * 9) {
+            cleanup();
+            return kt;  // kt.table == nullptr: LF steps
+        }
+        if (try_compact) {
             HIP_OK(hipMalloc(&tab, nb8 * 64));
             HIP_OK(hipMalloc(&multi, std::max<uint64_t>(multi_cap, 1) * 8));
             HIP_OK(hipMalloc(&d_nm, 4));
@@ -1327,19 +1343,28 @@ speq_device_index::KmerTable build_ktab(speq_device_index* d, uint32_t k) {
             unsigned int n_multi = 0;
             HIP_OK(hipMemcpyAsync(&n_multi, d_nm, 4, hipMemcpyDeviceToHost, d->stream));
             HIP_OK(hipStreamSynchronize(d->stream));
-            (void)hipFree(d_nm);
             if (n_multi <= multi_cap) {
+                uint2* exact = nullptr;
+                HIP_OK(hipMalloc(&exact, std::max<uint64_t>(n_multi, 1) * 8));
+                if (n_multi)
+                    HIP_OK(hipMemcpyAsync(exact, multi, (uint64_t)n_multi * 8, hipMemcpyDeviceToDevice, d->stream));
+                HIP_OK(hipStreamSynchronize(d->stream));
                 kt.compact = true;
                 kt.table = reinterpret_cast<uint4*>(d->track(tab));
-                kt.multi = d->track(multi);
+                kt.multi = d->track(exact);
                 kt.buckets = nb8;
-                kt.bytes = nb8 * 64 + (uint64_t)n_multi * 8;
+                kt.bytes = nb8 * 64 + std::max<uint64_t>(n_multi, 1) * 8;  // what the replica keeps
+                tab = nullptr;  // owned by the replica now
                 cleanup();
                 kt.build_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
                 return kt;
             }
             (void)hipFree(tab);
             (void)hipFree(multi);
+            (void)hipFree(d_nm);
+            tab = nullptr;
+            multi = nullptr;
+            d_nm = nullptr;
         }
         kt.buckets = next_pow2(std::max<uint64_t>(1, (distinct * d->kt_slots + KT_BSLOTS - 1) / KT_BSLOTS));
         kt.bytes = kt.buckets * 16 * KT_BSLOTS;

@@ -39,7 +39,8 @@ def test_key_set_is_the_distinct_reference_kmers(small, k):
     dev.tune(ax_scan=0)  # the k-mer table (the anchor-and-extend structures: tests/test_gpu_ax.py)
     info = dev.prepare(k)
     assert info["distinct_kmers"] == distinct_kmers(ref.records, k)
-    # 16-B slots at load <= 1/2, or (k <= 23) 8-B slots at load 1/2: >= 16 B per distinct k-mer either way
+    # 16-B slots at load <= 1/2, or (k <= 23) 8-B slots at load kt_load8 (35 % by default, ~23 B per k-mer):
+    # >= 16 B per distinct k-mer either way
     assert info["table_bytes"] >= 16 * info["distinct_kmers"]
 
 
@@ -172,8 +173,50 @@ def test_compact_table_equals_wide_table(paired):
             np.testing.assert_allclose(a[3], b[3], rtol=1e-12)
             assert a[4] == b[4]
             np.testing.assert_array_equal(a[5], b[5])
-    # at load 1/2 the compact table (16 B per k-mer + 8 B per multi-group k-mer) is smaller than the wide one (>= 32 B
+    # at kt_load8 = 50 % the compact table (16 B per k-mer + 8 B per multi-group k-mer) is smaller than the wide one (>= 32 B
     # per k-mer) for k <= 23; k = 24 uses the wide table either way
     for k in (11, 21, 23):
         assert res[("compact", k)][6] < res[("wide", k)][6]
     assert res[("compact", 24)][6] == res[("wide", 24)][6]
+
+
+@pytest.mark.parametrize("load8", [35, 90])
+def test_compact_table_poly_t_and_full_buckets(load8):
+    """The compact lookup relies on slots filling a bucket in order and on the all-T k-mer being the only key whose
+    bits can look like an empty slot's: poly-T (and poly-A) runs in the reference and in the reads, present and absent,
+    at the default load and at 90 % (many full buckets: lookups continue into the next bucket). Compact, wide and LF
+    steps must agree (k = 11, 21, 23)."""
+    rng = np.random.default_rng(5)
+    base = synth.make_reference(3, 2, 6_000)
+    recs = []
+    for i, r in enumerate(base.records):
+        r = bytearray(r)
+        if i % 2 == 0:  # poly-T / poly-A runs of 40 inside every other record (the rc texts get the complement)
+            for p in rng.integers(0, len(r) - 50, 4):
+                r[p:p + 40] = (b"T" if p % 2 else b"A") * 40
+        recs.append(bytes(r))
+    groups = list(base.groups)
+    idx = FmIndex.build(recs, groups, 3, prefix_q=8, pair_steps=True, triple_steps=True)
+    reads = synth.make_reads(base, 6_000, n_rate=0.001)
+    extra = [b"T" * 60, b"A" * 60, b"T" * 30 + b"ACGT" * 8, b"G" * 50, b"TTTTTTTTTTTTTTTTTTTTTTTC" * 3]
+    seqs = [reads.seq[int(reads.offsets[i]):int(reads.offsets[i + 1])].tobytes() for i in range(reads.n)] + extra
+    off = np.zeros(len(seqs) + 1, np.uint64)
+    off[1:] = np.cumsum([len(x) for x in seqs])
+    seq = b"".join(seqs)
+    qual = b"I" * len(seq)
+    res = {}
+    for mode in ("compact", "wide", "lf"):
+        dev = DeviceIndex(idx)
+        dev.tune(kt_compact=int(mode == "compact"), kmer_table=int(mode != "lf"), kt_load8=load8, ax_scan=0)
+        for k in (11, 21, 23):
+            r = dev.scan(seq, qual, off, k=k, local=True)
+            res[(mode, k)] = (r.total, r.ambiguous, r.unique.tolist(), r.weights)
+        dev.close()
+    for k in (11, 21, 23):
+        for other in ("wide", "lf"):
+            a, b = res[("compact", k)], res[(other, k)]
+            assert a[:3] == b[:3], (k, other)
+            np.testing.assert_allclose(a[3], b[3], rtol=1e-12)
+        T, amb, U, W = Oracle(recs, groups, 3, k).scan(np.frombuffer(seq, np.uint8), np.frombuffer(qual, np.uint8),
+                                                       off, local=True)
+        assert res[("compact", k)][:3] == (T, amb, U.tolist())
