@@ -362,17 +362,23 @@ constexpr uint32_t ax_wave_bytes() {
 
 #ifndef SPEQ_AX_PROBE  // timing probes (scripts/ax_probe.py A/B only; results are wrong): 1 staging only, 2 no phase 2,
                        // 3 nothing but the read offsets, 4 no counter flush at the end,
-                       // 5 staging alone without its global loads
+                       // 5 staging alone without its global loads, 6 staging alone without the counter flush
 #define SPEQ_AX_PROBE 0
 #endif
 #ifndef SPEQ_AX_SU  // staging: stream instructions per load batch (A/B knob)
 #define SPEQ_AX_SU 4
 #endif
-#ifndef SPEQ_AX_MIN_WAVES  // minimum waves per SIMD the register allocator must allow (A/B knob)
+#ifndef SPEQ_AX_MIN_WAVES  // minimum waves per SIMD the register allocator must allow, k <= 33 (A/B knob)
 #define SPEQ_AX_MIN_WAVES 4
 #endif
+#ifndef SPEQ_AX_MIN_WAVES4  // the same for 34 <= k <= 65 (four compare words)
+#define SPEQ_AX_MIN_WAVES4 4
+#endif
+#ifndef SPEQ_AX_MIN_WAVES6  // and 66 <= k <= 128 (six words): 3 waves, 168 VGPRs without most spills, win 12 % at
+#define SPEQ_AX_MIN_WAVES6 3  // k = 70 and lose 17 % at k = 21 (profiles/r02/ax_variants_probes.jsonl)
+#endif
 template <int MODE, bool PAIRED, bool LDS_HIST, bool EM, int NWC, int CW>
-__global__ __launch_bounds__(BLOCK_THREADS, SPEQ_AX_MIN_WAVES) void k_scan_ax(AxView A, UnitSrc src, unsigned long long* __restrict__ out_a,
+__global__ __launch_bounds__(BLOCK_THREADS, NWC >= 6 ? SPEQ_AX_MIN_WAVES6 : (NWC >= 4 ? SPEQ_AX_MIN_WAVES4 : SPEQ_AX_MIN_WAVES)) void k_scan_ax(AxView A, UnitSrc src, unsigned long long* __restrict__ out_a,
                                                            double* __restrict__ out_w) {
     using C = AxCls<CW>;
     constexpr uint32_t PER = C::PER;
@@ -658,7 +664,7 @@ __global__ __launch_bounds__(BLOCK_THREADS, SPEQ_AX_MIN_WAVES) void k_scan_ax(Ax
                 return u;
             };
 
-#if SPEQ_AX_PROBE == 1 || SPEQ_AX_PROBE == 5  // timing probe only (wrong results): staging alone
+#if SPEQ_AX_PROBE == 1 || SPEQ_AX_PROBE == 5 || SPEQ_AX_PROBE == 6  // timing probe only (wrong results): staging alone
             if (wend > 0u) continue;
 #endif
             // ---- phase 1: one read per lane, one memory round trip per iteration: a lane either probes the anchor
@@ -1034,7 +1040,7 @@ __global__ __launch_bounds__(BLOCK_THREADS, SPEQ_AX_MIN_WAVES) void k_scan_ax(Ax
         }
     }
 
-#if SPEQ_AX_PROBE == 4  // timing probe only (wrong results): no flush of the counters
+#if SPEQ_AX_PROBE == 4 || SPEQ_AX_PROBE == 6  // timing probe only (wrong results): no flush of the counters
     if (t_cnt != 0xFFFFFFFFu) return;
 #endif
     const unsigned long long tsum = wave_sum<unsigned long long>((unsigned long long)t_cnt);
