@@ -622,6 +622,12 @@ __global__ __launch_bounds__(BLOCK_THREADS, NWC >= 6 ? SPEQ_AX_MIN_WAVES6 : (NWC
 #pragma unroll
                 for (int i = 0; i < NWC; ++i) w[i] = funnel(raw[i], raw[i + 1], sh);
             };
+            auto vbits = [&](uint32_t b) -> uint64_t {  // this lane's valid-window bits b .. b + 63 (0 past the end)
+                const uint32_t w0 = b >> 6, s6 = b & 63u;
+                const uint64_t lo = w0 < AX_VWW ? vwl[w0 * 64u + lane] : 0ull;
+                const uint64_t hi = w0 + 1u < AX_VWW ? vwl[(w0 + 1u) * 64u + lane] : 0ull;
+                return funnel(lo, hi, s6);
+            };
             auto next_valid = [&](uint32_t j) -> uint32_t {  // first valid window >= j (or wend)
                 uint32_t res = wend;
 #pragma unroll
@@ -756,18 +762,22 @@ __global__ __launch_bounds__(BLOCK_THREADS, NWC >= 6 ? SPEQ_AX_MIN_WAVES6 : (NWC
                         uint32_t dend = (last_mm >= (int32_t)j && last_mm < (int32_t)(j + k)) ? (uint32_t)last_mm
                                                                                                : j + k - 1u;
                         dend = min(dend, wend - 1u);
-                        uint32_t cnt = 0;
-                        for (uint32_t w = j + 1; w <= dend; ++w)
-                            cnt += (uint32_t)((vwl[(w >> 6) * 64u + lane] >> (w & 63u)) & 1u);
+                        // the valid windows of (j, dend] as two 64-bit masks (dend - j <= k - 1 <= 127)
+                        const uint32_t span = dend - j;
+                        uint64_t dm0 = vbits(j + 1u), dm1 = span > 64u ? vbits(j + 65u) : 0ull;
+                        dm0 &= span >= 64u ? ~0ull : ((1ull << span) - 1ull);
+                        if (span > 64u) dm1 &= span - 64u >= 64u ? ~0ull : ((1ull << (span - 64u)) - 1ull);
+                        const uint32_t cnt = (uint32_t)__popcll(dm0) + (uint32_t)__popcll(dm1);
                         bool ok_def = true;
                         if (cnt) {
                             const uint32_t slot0 = atomicAdd(&defn[0], cnt);
                             ok_def = slot0 + cnt <= AX_DEF;
                             if (ok_def) {
                                 uint32_t sl = slot0;
-                                for (uint32_t w = j + 1; w <= dend; ++w)
-                                    if ((vwl[(w >> 6) * 64u + lane] >> (w & 63u)) & 1u)
-                                        defl[sl++] = (uint16_t)(lane | (w << 6));
+                                for (uint64_t t = dm0; t; t &= t - 1)
+                                    defl[sl++] = (uint16_t)(lane | ((j + 1u + (uint32_t)__builtin_ctzll(t)) << 6));
+                                for (uint64_t t = dm1; t; t &= t - 1)
+                                    defl[sl++] = (uint16_t)(lane | ((j + 65u + (uint32_t)__builtin_ctzll(t)) << 6));
                             } else {  // no room: the windows stay with this lane; void the slots reserved below the end
                                 for (uint32_t sl = slot0; sl < AX_DEF && sl < slot0 + cnt; ++sl) defl[sl] = AX_VOID;
                             }
