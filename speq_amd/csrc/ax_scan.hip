@@ -466,9 +466,17 @@ __global__ __launch_bounds__(BLOCK_THREADS, NWC >= 6 ? SPEQ_AX_MIN_WAVES6 : (NWC
         const uint64_t L = re - rb;
         const uint64_t W = L >= k ? L - k + 1 : 0;
         const uint32_t nseg = (uint32_t)((W + segw - 1) / segw);
-        uint32_t nseg_max = nseg;
-        for (uint32_t d = 32; d >= 1; d >>= 1) nseg_max = max(nseg_max, (uint32_t)__shfl_xor((int)nseg_max, (int)d));
-        nseg_max = __builtin_amdgcn_readfirstlane(nseg_max);
+        // the wave's largest segment count, bit by bit from the top (ballots: no shuffle address registers, which
+        // the compiler hoists out of the loops and spills)
+        uint32_t nseg_max = 0;
+        if (__ballot(nseg > 1u) == 0) {
+            nseg_max = __ballot(nseg != 0u) != 0 ? 1u : 0u;
+        } else {
+            for (int b = 31; b >= 0; --b) {  // greedy: set bit b when some lane reaches the candidate
+                const uint32_t cand = nseg_max | (1u << b);
+                if (__ballot(nseg >= cand) != 0) nseg_max = cand;
+            }
+        }
         int32_t af = -1, ad = 0;  // ambiguity state of this lane's read
         for (uint32_t seg = 0; seg < nseg_max; ++seg) {
 #if SPEQ_AX_PROBE == 3  // timing probe only (wrong results): read offsets, no staging
@@ -487,14 +495,16 @@ __global__ __launch_bounds__(BLOCK_THREADS, NWC >= 6 ? SPEQ_AX_MIN_WAVES6 : (NWC
             const uint64_t a16 = a & ~15ull;
             const uint32_t off0 = (uint32_t)(a - a16);
             const uint32_t nch = in_seg ? (off0 + sb + 15u) / 16u : 0u;
-            uint32_t incl = nch;  // inclusive prefix sum of the chunk counts
+            // exclusive prefix sum of the chunk counts (< 16) by bit planes: per bit, a ballot and a count of the lanes
+            // below this one (mbcnt)
+            static_assert(AX_CHUNKS < 16, "chunk counts in four bits");
+            uint32_t pre = 0, nch_tot = 0;
 #pragma unroll
-            for (uint32_t d = 1; d < 64u; d <<= 1) {
-                const uint32_t t = (uint32_t)__shfl_up((int)incl, d);
-                if (lane >= d) incl += t;
+            for (uint32_t b = 0; b < 4; ++b) {
+                const unsigned long long bb = __ballot((nch >> b) & 1u);
+                pre += __builtin_amdgcn_mbcnt_hi((uint32_t)(bb >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bb, 0u)) << b;
+                nch_tot += (uint32_t)__popcll(bb) << b;
             }
-            const uint32_t pre = incl - nch;
-            const uint32_t nch_tot = __builtin_amdgcn_readfirstlane(__shfl((int)incl, 63));
             const uint32_t sbase = 16u * pre + off0;        // stream position of the segment's first base
             const uint64_t gofs = a16 - 16ull * pre;        // byte offset of stream chunk c in this lane's frame: + 16 c
             const uint32_t qt = 33u + src.cutoff;  // Phred+33 byte <= qt  <=>  clamp(q, 0, 41) <= cutoff (cutoff < 41)
@@ -527,7 +537,7 @@ __global__ __launch_bounds__(BLOCK_THREADS, NWC >= 6 ? SPEQ_AX_MIN_WAVES6 : (NWC
                     const uint32_t qd[4] = {qv[u].x, qv[u].y, qv[u].z, qv[u].w};
                     uint32_t qprev = 0;
                     if (MODE == KM_LOCAL) {  // the byte before the chunk: the previous chunk's last quality
-                        const uint32_t up = (uint32_t)__shfl_up((int)qv[u].w, 1);
+                        const uint32_t up = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)qv[u].w, 0x138, 0xF, 0xF, false);
                         qprev = lane == 0 ? qcarry : up;
                         qcarry = __builtin_amdgcn_readlane(qv[u].w, 63);
                     }
@@ -1042,7 +1052,8 @@ __global__ __launch_bounds__(BLOCK_THREADS, NWC >= 6 ? SPEQ_AX_MIN_WAVES6 : (NWC
         }
         // ---- ambiguity of the unit (read, or mate pair in lanes 2i, 2i + 1)
         if (PAIRED) {
-            const int32_t of = __shfl_xor(af, 1), od = __shfl_xor(ad, 1);
+            const int32_t of = __builtin_amdgcn_mov_dpp(af, 0xB1, 0xF, 0xF, false);  // quad_perm [1,0,3,2]: the mate
+            const int32_t od = __builtin_amdgcn_mov_dpp(ad, 0xB1, 0xF, 0xF, false);
             const bool amb_pair = ad || od || (af >= 0 && of >= 0 && af != of);
             if (has && (lane & 1u) == 0u && amb_pair) ++amb;
         } else if (has && ad) {
@@ -1053,8 +1064,16 @@ __global__ __launch_bounds__(BLOCK_THREADS, NWC >= 6 ? SPEQ_AX_MIN_WAVES6 : (NWC
 #if SPEQ_AX_PROBE == 4 || SPEQ_AX_PROBE == 6  // timing probe only (wrong results): no flush of the counters
     if (t_cnt != 0xFFFFFFFFu) return;
 #endif
-    const unsigned long long tsum = wave_sum<unsigned long long>((unsigned long long)t_cnt);
-    const unsigned long long asum = wave_sum<unsigned long long>((unsigned long long)amb);
+    // wave sums of the window and ambiguity counters through two LDS words (no shuffle address registers)
+    if (lane == 0) {
+        defn[2] = 0;
+        defn[3] = 0;
+    }
+    wave_sync();
+    if (t_cnt) atomicAdd(&defn[2], t_cnt);
+    if (amb) atomicAdd(&defn[3], amb);
+    wave_sync();
+    const unsigned long long tsum = defn[2], asum = defn[3];
     if (lane == 0) {
         if (tsum) atomicAdd(&out_a[0], tsum);
         if (asum) atomicAdd(&out_a[1], asum);
