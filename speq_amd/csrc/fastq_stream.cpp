@@ -591,7 +591,119 @@ struct Sink {
         (void)s; (void)len1; (void)len2; (void)n; (void)paired;
         throw std::logic_error("this sink does not parse raw FASTQ");
     }
+    // records packed by pack_records (s.offsets filled; 3 bits per base when `three`, else one byte)
+    virtual void submit_packed(const speq_slot& s, uint64_t records, bool three) {
+        (void)s; (void)records; (void)three;
+        throw std::logic_error("this sink does not take packed records");
+    }
 };
+
+// Host packing of four-line FASTQ blocks (SPEQ_FASTQ_PACK=1; by default raw text goes to the GPU parser): 3 bits per
+// base in global mode, one byte per base in local mode (pipeline.cpp's formats), so the PCIe bytes per 150-bp record
+// drop from ~340 (raw text) to 56 or 150, at ~180 ns of host time per record.
+struct PackMode {
+    int kind = 0;         // 0 off, 1 one byte per base, 2 three bits per base
+    uint32_t cutoff = 30;
+};
+
+// every byte of [p, p + n) >= lo (unsigned)
+inline bool all_at_least(const char* p, size_t n, uint8_t lo) {
+    const __m128i l = _mm_set1_epi8((char)lo);
+    size_t i = 0;
+    for (; i + 16 <= n; i += 16) {
+        const __m128i x = _mm_loadu_si128(reinterpret_cast<const __m128i*>(p + i));
+        if (_mm_movemask_epi8(_mm_cmpeq_epi8(_mm_max_epu8(x, l), x)) != 0xFFFF) return false;
+    }
+    for (; i < n; ++i)
+        if ((uint8_t)p[i] < lo) return false;
+    return true;
+}
+
+// Newline offsets of [b, e) of d (absolute), appended to out; one SSE2 pass (movemask + bit scan).
+void newlines(const char* d, size_t b, size_t e, std::vector<uint32_t>& out) {
+    const __m128i nl = _mm_set1_epi8('\n');
+    size_t i = b;
+    for (; i + 16 <= e; i += 16) {
+        uint32_t m = (uint32_t)_mm_movemask_epi8(
+            _mm_cmpeq_epi8(_mm_loadu_si128(reinterpret_cast<const __m128i*>(d + i)), nl));
+        while (m) {
+            out.push_back((uint32_t)(i + (uint32_t)__builtin_ctz(m) - b));
+            m &= m - 1;
+        }
+    }
+    for (; i < e; ++i)
+        if (d[i] == '\n') out.push_back((uint32_t)(i - b));
+}
+
+// Packs n four-line records from [b1, e1) of d1 (and, paired, n from [b2, e2) of d2, interleaved as mates) into
+// slot s (offsets + packed bases). False when a record is not a clean four-line record or the records do not end
+// the range exactly (a header not opening with '@', a separator not opening with '+', base and quality lines of
+// different lengths, a base line holding anything below 'A' — blanks and digits the grammar drops —, a quality
+// line holding blanks): the caller then takes the general path, which parses such records by the grammar. The
+// lines come from one newline pass per block; wide loads may read up to 31 bytes past a line, never past the end
+// of the buffer (`lim`).
+bool pack_records(const char* d1, size_t b1, size_t e1, size_t lim1, const char* d2, size_t b2, size_t e2,
+                  size_t lim2, uint64_t n, bool paired, const PackMode& pm, speq_slot& s, uint64_t raw_bytes,
+                  uint64_t& bases) {
+    const bool three = pm.kind == 2;
+    const uint64_t nw_max = raw_bytes / 32 + 2;  // base words the block can need
+    uint64_t* codes = reinterpret_cast<uint64_t*>(s.seq);
+    uint32_t* bad_max = reinterpret_cast<uint32_t*>(s.seq + nw_max * 8);
+    if (three) std::memset(s.seq, 0, nw_max * 12);
+    thread_local std::vector<uint32_t> nl1, nl2;
+    nl1.clear();
+    nl2.clear();
+    if (e1 - b1 >= (1ull << 32) || (paired && e2 - b2 >= (1ull << 32))) return false;
+    newlines(d1, b1, e1, nl1);
+    if (paired) newlines(d2, b2, e2, nl2);
+    // an unterminated last line at the end of the input counts as terminated there
+    if (e1 > b1 && d1[e1 - 1] != '\n') {
+        if (e1 != lim1) return false;
+        nl1.push_back((uint32_t)(e1 - b1));
+    }
+    if (paired && e2 > b2 && d2[e2 - 1] != '\n') {
+        if (e2 != lim2) return false;
+        nl2.push_back((uint32_t)(e2 - b2));
+    }
+    if (nl1.size() != 4 * n || (paired && nl2.size() != 4 * n)) return false;
+    uint64_t at = 0, r = 0;
+    s.offsets[0] = 0;
+    auto one = [&](const char* d, size_t b, size_t lim, const std::vector<uint32_t>& nl, uint64_t i) -> bool {
+        const size_t h = i ? b + nl[4 * i - 1] + 1 : b;  // header line start
+        const size_t l0 = b + nl[4 * i], l1 = b + nl[4 * i + 1], l2 = b + nl[4 * i + 2], l3 = b + nl[4 * i + 3];
+        if (d[h] != '@' || d[l1 + 1] != '+' || d[l0 + 1] == '+') return false;
+        size_t hl = l0;
+        while (hl > h && d[hl - 1] == '\r') --hl;
+        if (hl <= h + 0) return false;  // empty header line (only '@' is fine: it is one byte)
+        size_t se = l1, qe = l3;
+        while (se > l0 + 1 && d[se - 1] == '\r') --se;
+        while (qe > l2 + 1 && d[qe - 1] == '\r') --qe;
+        const size_t L = se - (l0 + 1);
+        if (qe - (l2 + 1) != L) return false;
+        const char* sq = d + l0 + 1;
+        const char* qq = d + l2 + 1;
+        if (!all_at_least(sq, L, 'A') || !all_at_least(qq, L, 0x21)) return false;
+        const bool wide = l2 + 1 + L + 32 <= lim;  // a 32-byte load at the quality tail stays in the buffer
+        if (three)
+            speq::pack_bases3_append(codes, bad_max, at, reinterpret_cast<const uint8_t*>(sq),
+                                     reinterpret_cast<const uint8_t*>(qq), L, pm.cutoff, wide);
+        else
+            speq::pack_bases(s.seq + at, reinterpret_cast<const uint8_t*>(sq), reinterpret_cast<const uint8_t*>(qq), L);
+        at += L;
+        s.offsets[++r] = at;
+        return true;
+    };
+    for (uint64_t i = 0; i < n; ++i) {
+        if (!one(d1, b1, lim1, nl1, i)) return false;
+        if (paired && !one(d2, b2, lim2, nl2, i)) return false;
+    }
+    if (three) {  // the bad words follow the code words of the bases actually packed
+        const uint64_t nw = (at + 31) / 32;
+        std::memmove(s.seq + nw * 8, bad_max, nw * 4);
+    }
+    bases = at;
+    return true;
+}
 
 // Slots of one or more pipelines (one per GPU replica), dealt in turn: with equal GPUs every replica scans every
 // n-th block. The pipeline index travels in the slot id (slot * n + pipeline).
@@ -627,6 +739,10 @@ struct PipelineSink final : Sink {
     }
     void submit_raw(const speq_slot& s, uint64_t len1, uint64_t len2, uint64_t n, bool paired) override {
         speq::pipeline_submit_raw(of(s.slot), local(s.slot), len1, len2, n, paired);
+    }
+    void submit_packed(const speq_slot& s, uint64_t records, bool three) override {
+        if (three) speq::pipeline_submit_packed3(of(s.slot), local(s.slot), records);
+        else speq::pipeline_submit_packed(of(s.slot), local(s.slot), records);
     }
 };
 
@@ -763,7 +879,7 @@ void parallel_for(uint32_t threads, size_t n, F&& fn) {
 // both files, so any layout this does not fit fails there (or here) and the caller runs the sequential reader.
 // Files with different record counts also go to the sequential reader (its zip rule and read-ahead decide).
 StreamTotals run_paired_split(const std::shared_ptr<Buf>& m1, const std::shared_ptr<Buf>& m2, uint32_t threads,
-                              Sink& sink, ShardSel shard) {
+                              Sink& sink, ShardSel shard, PackMode pm) {
     const uint64_t BLOCK_RECORDS = 1u << 15, BLOCK_BYTES = 12ull << 20;
     const char* d1 = m1->data();
     const char* d2 = m2->data();
@@ -791,12 +907,32 @@ StreamTotals run_paired_split(const std::shared_ptr<Buf>& m1, const std::shared_
         if (r == r2[j]) return b2[j];
         return b2[j] + skip_lines(d2 + b2[j], b2[j + 1] - b2[j], 4 * (r - r2[j]));
     };
-    std::atomic<uint64_t> batches{0}, records{0};
+    std::atomic<uint64_t> batches{0}, records{0}, bases{0};
     parallel_for(threads, n1, [&](size_t i) {
         if (!shard.mine(i)) return;
         const size_t s2 = offset2(r1[i]), e2 = offset2(r1[i + 1]);
         const uint64_t l1 = b1[i + 1] - b1[i], l2 = e2 - s2, n = r1[i + 1] - r1[i];
         speq_slot s;
+        if (pm.kind) {  // packed on the host: both files' records, mates interleaved
+            sink.acquire(s, l1 + l2, 2 * n);
+            uint64_t nb = 0;
+            bool ok = false;
+            try {
+                ok = pack_records(d1, b1[i], b1[i + 1], m1->len, d2, s2, e2, m2->len, n, true, pm, s, l1 + l2, nb);
+            } catch (...) {
+                sink.submit(s, 0);
+                throw;
+            }
+            if (!ok) {
+                sink.submit(s, 0);
+                throw NotSimple();
+            }
+            sink.submit_packed(s, 2 * n, pm.kind == 2);
+            batches += 1;
+            records += 2 * n;
+            bases += nb;
+            return;
+        }
         sink.acquire_raw(s, l1 + l2);
         std::memcpy(s.seq, d1 + b1[i], l1);
         std::memcpy(s.seq + l1, d2 + s2, l2);
@@ -804,7 +940,7 @@ StreamTotals run_paired_split(const std::shared_ptr<Buf>& m1, const std::shared_
         batches += 1;
         records += 2 * n;
     });
-    return {records.load(), 0, batches.load()};
+    return {records.load(), bases.load(), batches.load()};
 }
 
 // Reader thread (cutting blocks of both files in step) + n_parsers parser threads feeding `sink`. With `split`, a
@@ -813,7 +949,7 @@ StreamTotals run_paired_split(const std::shared_ptr<Buf>& m1, const std::shared_
 // starts at byte 0, the chains join into exactly the records the sequential cutter finds. Throws NotSimple when a
 // block is not such a chain (the caller discards what was submitted and runs again without `split`).
 StreamTotals run_stream(const char* path1, const char* path2, uint32_t threads, Sink& sink, bool gpu_parse,
-                        bool split, ShardSel shard = {}) {
+                        bool split, ShardSel shard = {}, PackMode pm = {}) {
     const bool paired = path2 != nullptr;
     const uint32_t n_parsers = std::max<uint32_t>(1, std::min<uint32_t>(threads ? threads : 1, 64));
     const uint64_t BLOCK_RECORDS = 1u << 15, BLOCK_BYTES = 12ull << 20;  // pipeline slots hold SLOT_BYTES
@@ -824,7 +960,7 @@ StreamTotals run_stream(const char* path1, const char* path2, uint32_t threads, 
     if (paired) c2 = std::make_unique<Cutter>(path2, threads, !try_split);
     if (try_split && paired) {
         std::shared_ptr<Buf> m1 = c1.mapping(), m2 = c2->mapping();
-        if (m1 && m2) return run_paired_split(m1, m2, n_parsers, sink, shard);
+        if (m1 && m2) return run_paired_split(m1, m2, n_parsers, sink, shard, pm);
     }
     Shared sh;
     sh.max_q = n_parsers + 1;
@@ -904,6 +1040,36 @@ StreamTotals run_stream(const char* path1, const char* path2, uint32_t threads, 
                     sh.q.pop_front();
                     sh.cv_put.notify_one();
                 }
+                if (w.split && pm.kind) {
+                    // packed on the host: the record count from the newlines, then record by record (any record the
+                    // four-line packer cannot take makes the caller run the sequential cutter instead)
+                    const uint64_t l1 = w.b1.size();
+                    const bool eof = w.b1.end == w.b1.buf->len;
+                    uint64_t lines = count_nl(w.b1.data(), l1);
+                    if (eof && l1 && w.b1.data()[l1 - 1] != '\n') ++lines;
+                    if (lines == 0 || lines % 4 != 0) throw NotSimple();
+                    speq_slot s;
+                    sink.acquire(s, l1, lines / 4);
+                    uint64_t nb = 0;
+                    bool ok = false;
+                    try {
+                        ok = pack_records(w.b1.buf->data(), w.b1.begin, w.b1.end, w.b1.buf->len, nullptr, 0, 0, 0,
+                                          lines / 4, false, pm, s, l1, nb);
+                    } catch (...) {
+                        sink.submit(s, 0);
+                        throw;
+                    }
+                    if (!ok) {
+                        sink.submit(s, 0);
+                        throw NotSimple();
+                    }
+                    sink.submit_packed(s, lines / 4, pm.kind == 2);
+                    sh.records += lines / 4;
+                    sh.bases += nb;
+                    sh.batches += 1;
+                    if (sh.failed) return;
+                    continue;
+                }
                 if (w.split && gpu_parse) {
                     // raw text to HBM; the record count comes from the newlines counted during the copy, and the
                     // GPU checks every line group (a failure makes the caller run the sequential cutter instead)
@@ -935,6 +1101,31 @@ StreamTotals run_stream(const char* path1, const char* path2, uint32_t threads, 
                 }
                 speq_slot s;
                 const uint64_t recs = paired ? 2 * w.n : w.n;
+                if (pm.kind && w.b1.simple && w.n == w.b1.n && (!paired || (w.b2.simple && w.n == w.b2.n))) {
+                    // four-line records: packed on the host (falls through to the host parser when a record holds
+                    // blanks or digits the grammar drops)
+                    const uint64_t l1 = w.b1.size(), l2 = w.b2.size();
+                    sink.acquire(s, l1 + l2, recs);
+                    uint64_t nb = 0;
+                    bool ok = false;
+                    try {
+                        ok = pack_records(w.b1.buf->data(), w.b1.begin, w.b1.end, w.b1.buf->len,
+                                          paired ? w.b2.buf->data() : nullptr, w.b2.begin, w.b2.end,
+                                          paired ? w.b2.buf->len : 0, w.n, paired, pm, s, l1 + l2, nb);
+                    } catch (...) {
+                        sink.submit(s, 0);
+                        throw;
+                    }
+                    if (ok) {
+                        sink.submit_packed(s, recs, pm.kind == 2);
+                        sh.records += recs;
+                        sh.bases += nb;
+                        sh.batches += 1;
+                        if (sh.failed) return;
+                        continue;
+                    }
+                    sink.submit(s, 0);
+                }
                 if (gpu_parse && w.b1.simple && w.n == w.b1.n && (!paired || (w.b2.simple && w.n == w.b2.n))) {
                     // raw four-line text straight to HBM; records are split on the GPU (fastq_gpu.hip)
                     const uint64_t l1 = w.b1.size(), l2 = w.b2.size();
@@ -1038,11 +1229,20 @@ void scan_fastq_impl(speq_device_index* const* ds, speq_em* const* ems, uint32_t
     PipelineSink sink(pls);
     bool gpu_parse = true;
     for (uint32_t i = 0; i < n_dev; ++i) gpu_parse = gpu_parse && speq::device_fastq_gpu(ds[i]);
+    // SPEQ_FASTQ_PACK=1: four-line records packed on the host (3 bits per base in global mode, a byte in local mode)
+    // instead of raw text parsed on the GPU. Off by default: at 16 host threads the packer (~180 ns per 150-bp record)
+    // is slower than the PCIe transfer of the raw text it saves (cfg 2: 11.0 vs 9.9 ms, profiles/r02/stream_pack.jsonl)
+    PackMode pm;
+    {
+        const char* fp = std::getenv("SPEQ_FASTQ_PACK");
+        if (fp && fp[0] == '1') pm.kind = params->mode == SPEQ_MODE_GLOBAL ? 2 : 1;
+        pm.cutoff = params->phred_cutoff;
+    }
     std::vector<uint64_t> scratch(SPEQ_COUNTS_LEN(G));
     std::vector<double> wscratch(std::max<uint32_t>(G, 1));
     auto attempt = [&](bool split) {
         try {
-            StreamTotals t = run_stream(path1, path2, threads, sink, gpu_parse, split, shard);
+            StreamTotals t = run_stream(path1, path2, threads, sink, gpu_parse, split, shard, pm);
             // split blocks are parsed on the GPU unchecked by the host: any failed check means a layout the
             // parallel cut cannot handle (or a malformed file) -> sequential run, which reports real errors
             if (split && gpu_parse) {

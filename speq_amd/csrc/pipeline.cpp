@@ -458,6 +458,95 @@ __attribute__((target("avx2,bmi2"))) void pack3_avx2(uint64_t* codes, uint32_t* 
 }
 }  // namespace
 
+namespace {
+// one chunk of up to 32 bases: 2-bit codes (bases past n zero) and bad bits (past n zero)
+inline void pack3_chunk_scalar(const uint8_t* seq, const uint8_t* qual, uint32_t n, uint32_t cutoff, uint64_t& c,
+                               uint32_t& b) {
+    c = 0;
+    b = 0;
+    for (uint32_t i = 0; i < n; ++i) {
+        uint64_t ci = 0;
+        bool bi = true;
+        pack3_one(seq[i], qual[i], cutoff, ci, bi);
+        c |= ci << (2 * i);
+        b |= (uint32_t)bi << i;
+    }
+}
+
+__attribute__((target("avx2,bmi2"))) void pack3_append_avx2(uint64_t* codes, uint32_t* bad, uint64_t at,
+                                                            const uint8_t* seq, const uint8_t* qual, uint64_t n,
+                                                            uint32_t cutoff, bool wide) {
+    const __m256i lc = _mm256_set1_epi8(0x20), q33 = _mm256_set1_epi8(33), q41 = _mm256_set1_epi8(41);
+    const __m256i A = _mm256_set1_epi8('a'), Cc = _mm256_set1_epi8('c'), Gg = _mm256_set1_epi8('g'),
+                  Tt = _mm256_set1_epi8('t'), Uu = _mm256_set1_epi8('u'), three = _mm256_set1_epi8(3);
+    const __m256i cut = _mm256_set1_epi8((char)std::min<uint32_t>(cutoff, 41u));
+    const bool all_bad = cutoff >= 41u;
+    for (uint64_t i = 0; i < n; i += 32) {
+        const uint32_t m = (uint32_t)std::min<uint64_t>(32, n - i);
+        uint64_t c;
+        uint32_t b;
+        if (m == 32 || wide) {  // wide: 32-byte loads past the tail stay inside the caller's buffer
+            const __m256i x = _mm256_or_si256(_mm256_loadu_si256(reinterpret_cast<const __m256i*>(seq + i)), lc);
+            const __m256i ok = _mm256_or_si256(
+                _mm256_or_si256(_mm256_cmpeq_epi8(x, A), _mm256_cmpeq_epi8(x, Cc)),
+                _mm256_or_si256(_mm256_or_si256(_mm256_cmpeq_epi8(x, Gg), _mm256_cmpeq_epi8(x, Tt)),
+                                _mm256_cmpeq_epi8(x, Uu)));
+            const __m256i code = _mm256_and_si256(
+                _mm256_and_si256(_mm256_xor_si256(_mm256_srli_epi16(x, 1), _mm256_srli_epi16(x, 2)), three), ok);
+            const __m256i q = _mm256_min_epu8(
+                _mm256_subs_epu8(_mm256_loadu_si256(reinterpret_cast<const __m256i*>(qual + i)), q33), q41);
+            const __m256i qgood = _mm256_xor_si256(_mm256_cmpeq_epi8(_mm256_max_epu8(q, cut), cut),
+                                                   _mm256_set1_epi8(-1));
+            const uint32_t good = (uint32_t)_mm256_movemask_epi8(_mm256_and_si256(ok, qgood));
+            alignas(32) uint64_t cb[4];
+            _mm256_store_si256(reinterpret_cast<__m256i*>(cb), code);
+            c = 0;
+            for (int t = 0; t < 4; ++t) c |= _pext_u64(cb[t], 0x0303030303030303ull) << (16 * t);
+            b = all_bad ? ~0u : ~good;
+            if (m < 32) {
+                c &= (1ull << (2 * m)) - 1ull;
+                b &= (1u << m) - 1u;
+            }
+        } else {  // the record's tail: no reads past its last byte
+            pack3_chunk_scalar(seq + i, qual + i, m, cutoff, c, b);
+        }
+        const uint64_t o = at + i, w = o >> 5;
+        const uint32_t sh = (uint32_t)(o & 31u);
+        codes[w] |= c << (2 * sh);
+        bad[w] |= b << sh;
+        if (sh) {
+            codes[w + 1] |= c >> (64 - 2 * sh);
+            bad[w + 1] |= b >> (32 - sh);
+        }
+    }
+}
+
+void pack3_append_scalar(uint64_t* codes, uint32_t* bad, uint64_t at, const uint8_t* seq, const uint8_t* qual,
+                         uint64_t n, uint32_t cutoff) {
+    for (uint64_t i = 0; i < n; i += 32) {
+        const uint32_t m = (uint32_t)std::min<uint64_t>(32, n - i);
+        uint64_t c;
+        uint32_t b;
+        pack3_chunk_scalar(seq + i, qual + i, m, cutoff, c, b);
+        const uint64_t o = at + i, w = o >> 5;
+        const uint32_t sh = (uint32_t)(o & 31u);
+        codes[w] |= c << (2 * sh);
+        bad[w] |= b << sh;
+        if (sh) {
+            codes[w + 1] |= c >> (64 - 2 * sh);
+            bad[w + 1] |= b >> (32 - sh);
+        }
+    }
+}
+}  // namespace
+
+void pack_bases3_append(uint64_t* codes, uint32_t* bad, uint64_t at, const uint8_t* seq, const uint8_t* qual,
+                        uint64_t n, uint32_t cutoff, bool wide) {
+    static const bool fast = __builtin_cpu_supports("avx2") && __builtin_cpu_supports("bmi2");
+    if (fast) pack3_append_avx2(codes, bad, at, seq, qual, n, cutoff, wide);
+    else pack3_append_scalar(codes, bad, at, seq, qual, n, cutoff);
+}
+
 void pack_bases3(uint64_t* codes, uint32_t* bad, const uint8_t* seq, const uint8_t* qual, uint64_t n,
                  uint32_t cutoff) {
     static const bool fast = __builtin_cpu_supports("avx2") && __builtin_cpu_supports("bmi2");

@@ -38,6 +38,10 @@ void pipeline_submit_packed(speq_pipeline* pl, int32_t slot, uint64_t n_records)
 void launch_unpack_bases3(const uint64_t* d_codes, const uint32_t* d_bad, uint64_t n, uint8_t* d_seq, uint8_t* d_qual,
                           void* stream);
 void pack_bases3(uint64_t* codes, uint32_t* bad, const uint8_t* seq, const uint8_t* qual, uint64_t n, uint32_t cutoff);
+// ORs n bases into the 3-bit streams at base offset `at` (the words they touch must start zeroed): record by record.
+// wide: 32-byte loads may run up to 31 bytes past seq + n and qual + n (the caller's buffer continues there).
+void pack_bases3_append(uint64_t* codes, uint32_t* bad, uint64_t at, const uint8_t* seq, const uint8_t* qual,
+                        uint64_t n, uint32_t cutoff, bool wide = false);
 inline uint64_t packed3_bytes(uint64_t n) { return (n + 31) / 32 * 12; }
 void pipeline_submit_packed3(speq_pipeline* pl, int32_t slot, uint64_t n_records);
 // Submits an acquired pipeline slot whose host buffer holds RAW four-line FASTQ text (file 1's block, then file

@@ -70,9 +70,14 @@ def test_scan_fastq_matches_golden(tmp_path, name, gz):
             assert st["records"] == len(c.offsets) - 1
 
 
-@pytest.mark.parametrize("fmt", [dict(), dict(wrap=37, crlf=True, blank=True), dict(gz=True, wrap=60)])
+@pytest.mark.parametrize("fmt", [dict(), dict(wrap=37, crlf=True, blank=True), dict(gz=True, wrap=60),
+                                 dict(crlf=True), dict(gz=True)])
 @pytest.mark.parametrize("paired", [False, True])
-def test_scan_fastq_formats_match_in_memory(tmp_path, fmt, paired):
+@pytest.mark.parametrize("pack", ["0", "1"])
+def test_scan_fastq_formats_match_in_memory(tmp_path, monkeypatch, fmt, paired, pack):
+    """FASTQ streams (plain / gzip, four-line or wrapped / CRLF / blank lines) equal the in-memory scan, with the
+    records parsed on the GPU or (SPEQ_FASTQ_PACK=1) packed on the host; wrapped files take the general parser."""
+    monkeypatch.setenv("SPEQ_FASTQ_PACK", pack)
     ref = synth.make_reference(4, 2, 20_000, ref_n_rate=0.0005)
     n = 150_000 if not fmt else 40_000  # > one 131072-record block for the plain case
     reads = synth.make_reads(ref, n // (2 if paired else 1), paired=paired, n_rate=0.001, lowq_rate=0.005,
