@@ -365,6 +365,10 @@ constexpr uint32_t ax_wave_bytes() {
                        // 5 staging alone without its global loads, 6 staging alone without the counter flush
 #define SPEQ_AX_PROBE 0
 #endif
+#ifndef SPEQ_AX_WPB  // waves per workgroup of k_scan_ax (A/B knob)
+#define SPEQ_AX_WPB 4
+#endif
+constexpr uint32_t AX_WPB = SPEQ_AX_WPB, AX_THREADS = 64 * SPEQ_AX_WPB;
 #ifndef SPEQ_AX_SU  // staging: stream instructions per load batch (A/B knob)
 #define SPEQ_AX_SU 4
 #endif
@@ -378,7 +382,7 @@ constexpr uint32_t ax_wave_bytes() {
 #define SPEQ_AX_MIN_WAVES6 3  // k = 70 and lose 17 % at k = 21 (profiles/r02/ax_variants_probes.jsonl)
 #endif
 template <int MODE, bool PAIRED, bool LDS_HIST, bool EM, int NWC, int CW>
-__global__ __launch_bounds__(BLOCK_THREADS, NWC >= 6 ? SPEQ_AX_MIN_WAVES6 : (NWC >= 4 ? SPEQ_AX_MIN_WAVES4 : SPEQ_AX_MIN_WAVES)) void k_scan_ax(AxView A, UnitSrc src, unsigned long long* __restrict__ out_a,
+__global__ __launch_bounds__(AX_THREADS, NWC >= 6 ? SPEQ_AX_MIN_WAVES6 : (NWC >= 4 ? SPEQ_AX_MIN_WAVES4 : SPEQ_AX_MIN_WAVES)) void k_scan_ax(AxView A, UnitSrc src, unsigned long long* __restrict__ out_a,
                                                            double* __restrict__ out_w) {
     using C = AxCls<CW>;
     constexpr uint32_t PER = C::PER;
@@ -408,7 +412,7 @@ __global__ __launch_bounds__(BLOCK_THREADS, NWC >= 6 ? SPEQ_AX_MIN_WAVES6 : (NWC
     uint16_t* sbs = reinterpret_cast<uint16_t*>(ambd + 64);          // [64] stream base of each lane's segment
 
     if (MODE == KM_LOCAL)
-        for (uint32_t i = threadIdx.x; i < QLUT_LEN; i += BLOCK_THREADS) {
+        for (uint32_t i = threadIdx.x; i < QLUT_LEN; i += AX_THREADS) {
             const double lut = src.qlut[2 * i], inv = src.qlut[2 * i + 1];
             qtab[i] = make_double2(lut, inv);
             double x = 1.0;  // fm_scanner.cpp:454, k bases of quality i
@@ -416,7 +420,7 @@ __global__ __launch_bounds__(BLOCK_THREADS, NWC >= 6 ? SPEQ_AX_MIN_WAVES6 : (NWC
             wtab[i] = x;
         }
     if (LDS_HIST)
-        for (uint32_t i = threadIdx.x; i < hist_words; i += BLOCK_THREADS) hA[i] = 0ull;
+        for (uint32_t i = threadIdx.x; i < hist_words; i += AX_THREADS) hA[i] = 0ull;
     __syncthreads();
     unsigned long long* gU = out_a + 2;
 
@@ -430,8 +434,8 @@ __global__ __launch_bounds__(BLOCK_THREADS, NWC >= 6 ? SPEQ_AX_MIN_WAVES6 : (NWC
         __builtin_amdgcn_make_buffer_rsrc((void*)A.t2, (short)0, (int)(uint32_t)A.t2_bytes, 0x00020000);
     const __amdgpu_buffer_rsrc_t rs_filt =
         __builtin_amdgcn_make_buffer_rsrc((void*)A.filt, (short)0, (int)(uint32_t)(A.nf * 8u), 0x00020000);
-    const uint64_t NWV = (uint64_t)gridDim.x * WAVES_PER_BLOCK;
-    const uint64_t gw = (uint64_t)blockIdx.x * WAVES_PER_BLOCK + wid;
+    const uint64_t NWV = (uint64_t)gridDim.x * AX_WPB;
+    const uint64_t gw = (uint64_t)blockIdx.x * AX_WPB + wid;
     const uint64_t nu = PAIRED ? src.n_units / 2 : src.n_units;
     // groups of 64 reads (32 mate pairs), dealt to the waves round robin: the waves in flight sweep the read buffers
     // front to back together (a wave owning one contiguous range ran the staging loads at a third of the HBM rate)
@@ -1080,7 +1084,7 @@ __global__ __launch_bounds__(BLOCK_THREADS, NWC >= 6 ? SPEQ_AX_MIN_WAVES6 : (NWC
     }
     if (LDS_HIST) {
         __syncthreads();
-        for (uint32_t g = threadIdx.x; g < G; g += BLOCK_THREADS) {
+        for (uint32_t g = threadIdx.x; g < G; g += AX_THREADS) {
             const unsigned long long x = hA[g];
             if (x) atomicAdd(&gU[g], x);
             if (MODE == KM_LOCAL) {
@@ -1097,7 +1101,7 @@ void ax_launch_one(const AxView& A, const UnitSrc& src, uint32_t grid, size_t ld
     if (lds > 64 * 1024)  // dynamic LDS above 64 KiB must be allowed (occupancy caps pad it)
         HIP_OK(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_scan_ax<MODE, PAIRED, LDS, EM, NWC, CW>),
                                    hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-    hipLaunchKernelGGL((k_scan_ax<MODE, PAIRED, LDS, EM, NWC, CW>), dim3(grid), dim3(BLOCK_THREADS), lds, st, A, src, a,
+    hipLaunchKernelGGL((k_scan_ax<MODE, PAIRED, LDS, EM, NWC, CW>), dim3(grid), dim3(AX_THREADS), lds, st, A, src, a,
                        w);
 }
 
@@ -1253,9 +1257,9 @@ bool launch_ax(speq_device_index* d, int mode, bool paired, const UnitSrc& src, 
     const bool lds_hist = d->G <= LDS_HIST_MAX_G;
     const uint32_t hist_words = lds_hist ? (mode == KM_GLOBAL ? d->G : 2u * d->G) : 0u;
     const size_t lds = ((hist_words * 8u + 15u) & ~15u) + (mode == KM_LOCAL ? QTAB_BYTES : 0u) +
-                       (size_t)WAVES_PER_BLOCK * (mode == KM_LOCAL ? ax_wave_bytes<KM_LOCAL>() : ax_wave_bytes<KM_GLOBAL>());
+                       (size_t)AX_WPB * (mode == KM_LOCAL ? ax_wave_bytes<KM_LOCAL>() : ax_wave_bytes<KM_GLOBAL>());
     const uint64_t reads = src.n_units;
-    uint64_t blocks = (reads + 64 * WAVES_PER_BLOCK - 1) / (64 * WAVES_PER_BLOCK);
+    uint64_t blocks = (reads + 64 * AX_WPB - 1) / (64 * AX_WPB);
     blocks = std::max<uint64_t>(1, std::min<uint64_t>(blocks, d->grid_blocks_ax));
     size_t lds_launch = lds;
     if (d->blocks_per_cu_ax > 0) {
