@@ -1214,8 +1214,12 @@ void scan_fastq_impl(speq_device_index* const* ds, speq_em* const* ems, uint32_t
     const uint32_t G = speq::device_groups(ds[0]);
     const auto t0 = std::chrono::steady_clock::now();
     const uint32_t n_parsers = std::max<uint32_t>(1, std::min<uint32_t>(threads ? threads : 1, 64));
-    // one replica: parsers + 2 slots (up to 8); several: the same total spread over them, at least 3 each
-    const uint32_t want = std::min<uint32_t>(n_parsers, 6) + 2;
+    // one replica: parsers + 2 slots (up to SPEQ_STREAM_SLOTS_MAX, default 18: 9.5 -> 8.6 ms at cfg 2 with 16 parsers,
+    // profiles/r02/stream_slots.jsonl); several: the same total spread over
+    // them, at least 3 each
+    const char* sm = std::getenv("SPEQ_STREAM_SLOTS_MAX");
+    const uint32_t slots_max = sm && *sm ? (uint32_t)std::max(3l, std::min(64l, std::atol(sm))) : 18u;
+    const uint32_t want = std::min<uint32_t>(n_parsers + 2, slots_max);
     const uint32_t n_slots = n_dev == 1 ? want : std::max<uint32_t>(3, (want + n_dev - 1) / n_dev + 1);
     std::vector<std::unique_ptr<speq_pipeline, void (*)(speq_pipeline*)>> guards;
     std::vector<speq_pipeline*> pls;
