@@ -490,15 +490,30 @@ uint64_t copy_count_nl(char* dst, const char* src, size_t n) {
     const __m128i nl = _mm_set1_epi8('\n');
     uint64_t c = 0;
     size_t i = 0;
+    // non-temporal stores into the (16-B aligned) pinned slot when SPEQ_NT_COPY is not 0: the slot is only read by
+    // the DMA engine, and streaming stores skip the read-for-ownership of every destination line (host memory
+    // bandwidth is what bounds this path)
+    static const bool nt = [] {
+        const char* e = std::getenv("SPEQ_NT_COPY");
+        return !(e && e[0] == '0');
+    }();
+    const bool stream = nt && (reinterpret_cast<uintptr_t>(dst) & 15u) == 0;
     for (; i + 64 <= n; i += 64) {
         const __m128i a = _mm_loadu_si128(reinterpret_cast<const __m128i*>(src + i));
         const __m128i b = _mm_loadu_si128(reinterpret_cast<const __m128i*>(src + i + 16));
         const __m128i d = _mm_loadu_si128(reinterpret_cast<const __m128i*>(src + i + 32));
         const __m128i e = _mm_loadu_si128(reinterpret_cast<const __m128i*>(src + i + 48));
-        _mm_storeu_si128(reinterpret_cast<__m128i*>(dst + i), a);
-        _mm_storeu_si128(reinterpret_cast<__m128i*>(dst + i + 16), b);
-        _mm_storeu_si128(reinterpret_cast<__m128i*>(dst + i + 32), d);
-        _mm_storeu_si128(reinterpret_cast<__m128i*>(dst + i + 48), e);
+        if (stream) {
+            _mm_stream_si128(reinterpret_cast<__m128i*>(dst + i), a);
+            _mm_stream_si128(reinterpret_cast<__m128i*>(dst + i + 16), b);
+            _mm_stream_si128(reinterpret_cast<__m128i*>(dst + i + 32), d);
+            _mm_stream_si128(reinterpret_cast<__m128i*>(dst + i + 48), e);
+        } else {
+            _mm_storeu_si128(reinterpret_cast<__m128i*>(dst + i), a);
+            _mm_storeu_si128(reinterpret_cast<__m128i*>(dst + i + 16), b);
+            _mm_storeu_si128(reinterpret_cast<__m128i*>(dst + i + 32), d);
+            _mm_storeu_si128(reinterpret_cast<__m128i*>(dst + i + 48), e);
+        }
         const uint64_t m = (uint64_t)(uint32_t)_mm_movemask_epi8(_mm_cmpeq_epi8(a, nl)) |
                            (uint64_t)(uint32_t)_mm_movemask_epi8(_mm_cmpeq_epi8(b, nl)) << 16 |
                            (uint64_t)(uint32_t)_mm_movemask_epi8(_mm_cmpeq_epi8(d, nl)) << 32 |
@@ -506,6 +521,7 @@ uint64_t copy_count_nl(char* dst, const char* src, size_t n) {
         c += (uint64_t)__builtin_popcountll(m);
     }
     for (; i < n; ++i) c += (dst[i] = src[i]) == '\n';
+    if (stream) _mm_sfence();  // the streamed lines are globally visible before the slot is submitted
     return c;
 }
 

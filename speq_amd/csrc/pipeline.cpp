@@ -374,6 +374,12 @@ inline uint8_t pack_one(uint8_t sc, uint8_t qc) {
 }
 
 __attribute__((target("avx2"))) void pack_avx2(uint8_t* out, const uint8_t* seq, const uint8_t* qual, uint64_t n) {
+    // streaming stores into a 32-B aligned pinned slot (no read-for-ownership; SPEQ_NT_COPY=0 turns them off)
+    static const bool nt = [] {
+        const char* e = std::getenv("SPEQ_NT_COPY");
+        return !(e && e[0] == '0');
+    }();
+    const bool stream = nt && (reinterpret_cast<uintptr_t>(out) & 31u) == 0;
     const __m256i lc = _mm256_set1_epi8(0x20), q33 = _mm256_set1_epi8(33), q41 = _mm256_set1_epi8(41);
     const __m256i A = _mm256_set1_epi8('a'), Cc = _mm256_set1_epi8('c'), Gg = _mm256_set1_epi8('g'),
                   Tt = _mm256_set1_epi8('t'), Uu = _mm256_set1_epi8('u'), three = _mm256_set1_epi8(3),
@@ -390,9 +396,11 @@ __attribute__((target("avx2"))) void pack_avx2(uint8_t* out, const uint8_t* seq,
         const __m256i q = _mm256_min_epu8(
             _mm256_subs_epu8(_mm256_loadu_si256(reinterpret_cast<const __m256i*>(qual + i)), q33), q41);
         const __m256i v = _mm256_or_si256(code, _mm256_slli_epi16(q, 2));  // q <= 41: q << 2 stays in its byte
-        _mm256_storeu_si256(reinterpret_cast<__m256i*>(out + i), _mm256_blendv_epi8(nval, v, ok));
+        if (stream) _mm256_stream_si256(reinterpret_cast<__m256i*>(out + i), _mm256_blendv_epi8(nval, v, ok));
+        else _mm256_storeu_si256(reinterpret_cast<__m256i*>(out + i), _mm256_blendv_epi8(nval, v, ok));
     }
     for (; i < n; ++i) out[i] = pack_one(seq[i], qual[i]);
+    if (stream) _mm_sfence();
 }
 }  // namespace
 
