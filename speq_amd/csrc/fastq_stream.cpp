@@ -950,8 +950,9 @@ StreamTotals run_paired_split(const std::shared_ptr<Buf>& m1, const std::shared_
             return;
         }
         sink.acquire_raw(s, l1 + l2);
-        std::memcpy(s.seq, d1 + b1[i], l1);
-        std::memcpy(s.seq + l1, d2 + s2, l2);
+        // copies with streaming stores where the destination is 16-B aligned (no read-for-ownership)
+        (void)copy_count_nl(reinterpret_cast<char*>(s.seq), d1 + b1[i], l1);
+        (void)copy_count_nl(reinterpret_cast<char*>(s.seq) + l1, d2 + s2, l2);
         sink.submit_raw(s, l1, l2, n, true);
         batches += 1;
         records += 2 * n;
