@@ -9,6 +9,7 @@ import subprocess
 import numpy as np
 import pytest
 
+import cereal_dat
 from golden_io import CASES, Case
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -103,7 +104,10 @@ def test_scan_end_to_end(tmp_path, name, mode):
     lines = r.stderr.strip().split("\n")
     # first scan computes the .dat pass and prints U_ref / Tot_ref (fm_scanner.cpp:1572-1573)
     assert _parse_vec(lines[0]) == e["u_ref"] and _parse_vec(lines[1]) == e["tot_ref"]
-    assert (tmp_path / f"ref_{k}mer.dat").exists()
+    # the .dat holds cereal's bytes of {file_time_type of the .idx, U_ref, Tot_ref} (fm_scanner.cpp:1561-1571)
+    dat = (tmp_path / f"ref_{k}mer.dat").read_bytes()
+    stamp = cereal_dat.file_time_ns((tmp_path / "ref.idx").stat().st_mtime_ns)
+    assert dat == cereal_dat.encode(stamp, [int(x) for x in e["u_ref"]], [int(x) for x in e["tot_ref"]])
     g = e[mode]
     np.testing.assert_allclose(_parse_vec(lines[2]), g["percent"], rtol=1e-5)
     tl = [ln for ln in lines if "\t" in ln]
@@ -235,3 +239,42 @@ def test_scan_one_process_per_gpu_matches_one_process(tmp_path, paired):
     for line in one.stderr.splitlines():  # every result line of the one-process run, once, from rank 0
         assert line in two.stderr, line
     assert (tmp_path / "ref_21mer.dat").read_bytes() == one_dat  # written by rank 0 from the summed shards
+
+
+def test_cereal_dat_restatement_round_trips():
+    """The cereal restatement the .dat tests use: fixed layout (i64 stamp, u64 n, u64[n], u64 n, u64[n])."""
+    b = cereal_dat.encode(-5, [1, 2, 3], [4, 5, 6])
+    assert len(b) == 8 + 2 * (8 + 3 * 8) and b[:8] == (-5).to_bytes(8, "little", signed=True)
+    assert cereal_dat.decode(b) == (-5, [1, 2, 3], [4, 5, 6])
+    assert cereal_dat.file_time_ns(6437664000 * 10**9) == 0
+
+
+@pytest.mark.gpu
+def test_scan_reads_a_cereal_dat_and_recounts_a_stale_one(work):
+    """A .dat written by cereal (restated in tests/cereal_dat.py) with the .idx's file time is used as is: the
+    scan prints no U_ref/Tot_ref lines and its percentages follow the file's U_ref (here doubled, so every
+    percentage halves; fm_scanner.cpp:89-121, :1455-1474). A .dat with another stamp is recomputed and rewritten
+    (:97-107)."""
+    c = Case("tiny_single")
+    k = c.ks[0]
+    e = c.exp["by_k"][str(k)]
+    r = run(["index", "-r", "refs.fa", "-g", "groups.txt", "-x", "ref", "-o", "i.txt", "--prefix-q", "4"], work)
+    assert r.returncode == 0, r.stderr
+    args = ["scan", "-1", "reads_1.fq", "-x", "ref", "-k", str(k), "--phred-cutoff", str(c.cutoff), "-o", "p.txt",
+            "-f"]
+    stamp = cereal_dat.file_time_ns((work / "ref.idx").stat().st_mtime_ns)
+    u = [int(x) for x in e["u_ref"]]
+    t = [int(x) for x in e["tot_ref"]]
+    dat = work / f"ref_{k}mer.dat"
+    dat.write_bytes(cereal_dat.encode(stamp, [2 * x for x in u], t))
+    r = run(args, work)
+    assert r.returncode == 0, r.stderr
+    lines = r.stderr.strip().split("\n")
+    np.testing.assert_allclose(_parse_vec(lines[0]), np.asarray(e["local"]["percent"]) / 2, rtol=1e-5)
+    dat.write_bytes(cereal_dat.encode(stamp - 1, [2 * x for x in u], t))  # stale: recounted and rewritten
+    r = run(args, work)
+    assert r.returncode == 0, r.stderr
+    lines = r.stderr.strip().split("\n")
+    assert _parse_vec(lines[0]) == e["u_ref"] and _parse_vec(lines[1]) == e["tot_ref"]
+    np.testing.assert_allclose(_parse_vec(lines[2]), e["local"]["percent"], rtol=1e-5)
+    assert cereal_dat.decode(dat.read_bytes()) == (stamp, u, t)
