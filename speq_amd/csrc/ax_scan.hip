@@ -381,8 +381,20 @@ constexpr uint32_t AX_WPB = SPEQ_AX_WPB, AX_THREADS = 64 * SPEQ_AX_WPB;
 #ifndef SPEQ_AX_MIN_WAVES6  // and 66 <= k <= 128 (six words): 3 waves, 168 VGPRs without most spills, win 12 % at
 #define SPEQ_AX_MIN_WAVES6 3  // k = 70 and lose 17 % at k = 21 (profiles/r02/ax_variants_probes.jsonl)
 #endif
+#ifndef SPEQ_AX_MIN_WAVES_LOCAL  // local (Phred-weighted) mode, k <= 33: more live state than global mode
+#define SPEQ_AX_MIN_WAVES_LOCAL SPEQ_AX_MIN_WAVES
+#endif
+#ifndef SPEQ_AX_MIN_WAVES4_LOCAL  // local mode, 34 <= k <= 65
+#define SPEQ_AX_MIN_WAVES4_LOCAL SPEQ_AX_MIN_WAVES4
+#endif
+template <int MODE, int NWC>
+constexpr int ax_min_waves() {
+    return NWC >= 6 ? SPEQ_AX_MIN_WAVES6
+                    : (NWC >= 4 ? (MODE == KM_LOCAL ? SPEQ_AX_MIN_WAVES4_LOCAL : SPEQ_AX_MIN_WAVES4)
+                                : (MODE == KM_LOCAL ? SPEQ_AX_MIN_WAVES_LOCAL : SPEQ_AX_MIN_WAVES));
+}
 template <int MODE, bool PAIRED, bool LDS_HIST, bool EM, int NWC, int CW>
-__global__ __launch_bounds__(AX_THREADS, NWC >= 6 ? SPEQ_AX_MIN_WAVES6 : (NWC >= 4 ? SPEQ_AX_MIN_WAVES4 : SPEQ_AX_MIN_WAVES)) void k_scan_ax(AxView A, UnitSrc src, unsigned long long* __restrict__ out_a,
+__global__ __launch_bounds__(AX_THREADS, (ax_min_waves<MODE, NWC>())) void k_scan_ax(AxView A, UnitSrc src, unsigned long long* __restrict__ out_a,
                                                            double* __restrict__ out_w) {
     using C = AxCls<CW>;
     constexpr uint32_t PER = C::PER;
