@@ -381,11 +381,14 @@ constexpr uint32_t AX_WPB = SPEQ_AX_WPB, AX_THREADS = 64 * SPEQ_AX_WPB;
 #ifndef SPEQ_AX_MIN_WAVES6  // and 66 <= k <= 128 (six words): 3 waves, 168 VGPRs without most spills, win 12 % at
 #define SPEQ_AX_MIN_WAVES6 3  // k = 70 and lose 17 % at k = 21 (profiles/r02/ax_variants_probes.jsonl)
 #endif
-#ifndef SPEQ_AX_MIN_WAVES_LOCAL  // local (Phred-weighted) mode, k <= 33: more live state than global mode
-#define SPEQ_AX_MIN_WAVES_LOCAL SPEQ_AX_MIN_WAVES
+// local (Phred-weighted) mode holds more live state than global mode: at 4 waves it spilled 54-60 registers per lane
+// (k <= 65); 3 waves (168 VGPRs, 36 / 8 spills) win 5 % at k = 21, 3 % at k = 31 and 28 % at k = 45 (0.1 % errors;
+// 9-34 % at 0.5 %), 2 waves lose (profiles/r02/ax_variants_local_waves.jsonl)
+#ifndef SPEQ_AX_MIN_WAVES_LOCAL  // local mode, k <= 33
+#define SPEQ_AX_MIN_WAVES_LOCAL 3
 #endif
 #ifndef SPEQ_AX_MIN_WAVES4_LOCAL  // local mode, 34 <= k <= 65
-#define SPEQ_AX_MIN_WAVES4_LOCAL SPEQ_AX_MIN_WAVES4
+#define SPEQ_AX_MIN_WAVES4_LOCAL 3
 #endif
 template <int MODE, int NWC>
 constexpr int ax_min_waves() {
