@@ -390,9 +390,13 @@ constexpr uint32_t AX_WPB = SPEQ_AX_WPB, AX_THREADS = 64 * SPEQ_AX_WPB;
 #ifndef SPEQ_AX_MIN_WAVES4_LOCAL  // local mode, 34 <= k <= 65
 #define SPEQ_AX_MIN_WAVES4_LOCAL 3
 #endif
+#ifndef SPEQ_AX_MIN_WAVES6_LOCAL  // local mode, 66 <= k <= 128 (2 waves, no spills, lose 17-29 %:
+                                   // profiles/r02/ax_variants_local_k70_waves.jsonl)
+#define SPEQ_AX_MIN_WAVES6_LOCAL SPEQ_AX_MIN_WAVES6
+#endif
 template <int MODE, int NWC>
 constexpr int ax_min_waves() {
-    return NWC >= 6 ? SPEQ_AX_MIN_WAVES6
+    return NWC >= 6 ? (MODE == KM_LOCAL ? SPEQ_AX_MIN_WAVES6_LOCAL : SPEQ_AX_MIN_WAVES6)
                     : (NWC >= 4 ? (MODE == KM_LOCAL ? SPEQ_AX_MIN_WAVES4_LOCAL : SPEQ_AX_MIN_WAVES4)
                                 : (MODE == KM_LOCAL ? SPEQ_AX_MIN_WAVES_LOCAL : SPEQ_AX_MIN_WAVES));
 }
