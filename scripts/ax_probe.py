@@ -26,8 +26,11 @@ def main():
     ap.add_argument("--local", action="store_true")
     ap.add_argument("--paired", action="store_true")
     ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--variants", type=int, default=0, help="override the config's variant (group) count")
     a = ap.parse_args()
-    c = synth.CONFIGS[a.config]
+    c = dict(synth.CONFIGS[a.config])
+    if a.variants:
+        c["n_variants"] = a.variants
     ref = synth.make_reference(c["n_variants"], c["n_isolates"], c["length"])
     idx = FmIndex.build(ref.records, ref.groups, c["n_variants"], prefix_q=12, pair_steps=True, triple_steps=True,
                         gpu_device=0)

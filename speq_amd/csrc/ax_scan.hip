@@ -394,14 +394,17 @@ constexpr uint32_t AX_WPB = SPEQ_AX_WPB, AX_THREADS = 64 * SPEQ_AX_WPB;
                                    // profiles/r02/ax_variants_local_k70_waves.jsonl)
 #define SPEQ_AX_MIN_WAVES6_LOCAL SPEQ_AX_MIN_WAVES6
 #endif
-template <int MODE, int NWC>
+#ifndef SPEQ_AX_MIN_WAVES_CW2  // two-byte classes (> 253 groups; 0 = as for one-byte classes): their run loop holds
+#define SPEQ_AX_MIN_WAVES_CW2 3   // twice the class registers and spilled 91-104 per lane at 4 waves; 3 waves win 30-33 %
+#endif                            // at k = 21 / 31 global, 300 groups (profiles/r02/ax_variants_cw2_waves.jsonl)
+template <int MODE, int NWC, int CW>
 constexpr int ax_min_waves() {
-    return NWC >= 6 ? (MODE == KM_LOCAL ? SPEQ_AX_MIN_WAVES6_LOCAL : SPEQ_AX_MIN_WAVES6)
+    return (CW == 2 && SPEQ_AX_MIN_WAVES_CW2 > 0) ? SPEQ_AX_MIN_WAVES_CW2 : NWC >= 6 ? (MODE == KM_LOCAL ? SPEQ_AX_MIN_WAVES6_LOCAL : SPEQ_AX_MIN_WAVES6)
                     : (NWC >= 4 ? (MODE == KM_LOCAL ? SPEQ_AX_MIN_WAVES4_LOCAL : SPEQ_AX_MIN_WAVES4)
                                 : (MODE == KM_LOCAL ? SPEQ_AX_MIN_WAVES_LOCAL : SPEQ_AX_MIN_WAVES));
 }
 template <int MODE, bool PAIRED, bool LDS_HIST, bool EM, int NWC, int CW>
-__global__ __launch_bounds__(AX_THREADS, (ax_min_waves<MODE, NWC>())) void k_scan_ax(AxView A, UnitSrc src, unsigned long long* __restrict__ out_a,
+__global__ __launch_bounds__(AX_THREADS, (ax_min_waves<MODE, NWC, CW>())) void k_scan_ax(AxView A, UnitSrc src, unsigned long long* __restrict__ out_a,
                                                            double* __restrict__ out_w) {
     using C = AxCls<CW>;
     constexpr uint32_t PER = C::PER;

@@ -148,6 +148,19 @@ def test_many_groups_global_atomics():
     assert np.array_equal(u, ou) and np.array_equal(t, ot)
 
 
+@pytest.mark.parametrize("k", [21, 45, 70])
+def test_two_byte_classes_lds_tally(k):
+    """254 <= G <= 2048: two-byte anchor classes with the LDS tally (the kernel built for 3 waves/SIMD there)."""
+    G = 300
+    ref = synth.make_reference(G, 1, 400)
+    reads = synth.make_reads(ref, 4_000)
+    idx = FmIndex.build(ref.records, ref.groups, G, prefix_q=6, pair_steps=True, label_table=True)
+    dev = DeviceIndex(idx)
+    orc = Oracle(ref.records, ref.groups, G, k)
+    _check(dev, orc, reads, k)
+    _check(dev, orc, reads, k, local=True)
+
+
 def test_irregular_groupings():
     """Records assigned to groups out of order, one group spanning scattered records, single group."""
     ref = synth.make_reference(6, 1, 4_000)
