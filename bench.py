@@ -120,19 +120,36 @@ class Ctx:
         return float(t.item())
 
 
-def kernel_model(dev, k: int, table_on: bool, kmers: int, read_bytes: int, n_reads: int = 0) -> dict:
-    """The timed kernel and the bytes IT must move per k-mer window (its own roofline model).
+def ax_request_bytes(st: dict, k: int, n_reads: int, local: bool) -> dict:
+    """Bytes k_scan_ax REQUESTS per launch, from the work counters of its instrumented twin (speq_scan_reads_device_stats,
+    same scan, same results): every load the kernel issues, by kind, at the size it issues it (ax_scan.hip):
+      read offsets 8 B per read; staging 16 B of bases + 16 B of qualities per 16-base chunk;
+      anchor buckets 64 B per lookup (phase 1 and phase 2); run granules NG = NWC + 1 x 16 B per run iteration;
+      Bloom-filter words 8 B per deferred window; candidate granules NWC x 16 B per phase-2 verification;
+      local mode: single quality bytes."""
+    nwc = 3 if k <= 33 else (4 if k <= 65 else 6)
+    parts = {
+        "offsets": 8.0 * n_reads,
+        "staging": 32.0 * st["chunks"],
+        "anchor_buckets": 64.0 * (st["lookup_lanes"] + st["p2_probes"]),
+        "run_granules": 16.0 * (nwc + 1) * st["run_lanes"],
+        "filter": 8.0 * st["deferred"],
+        "verify_granules": 16.0 * nwc * st["p2_verify"],
+        "quality_bytes": float(st["qual_bytes"]) if local else 0.0,
+    }
+    return {"total": sum(parts.values()), "parts": parts}
 
-    Anchor-and-extend path (k_scan_ax): the read bytes (bases + qualities), one 4-B class per window, the 2-bit text
-    its runs compare (k - 1 + 32 bases per run of 32 windows) and at least one 64-B anchor bucket per read.
+
+def kernel_model(dev, k: int, table_on: bool, kmers: int, read_bytes: int, n_reads: int = 0) -> dict:
+    """The timed kernel and the bytes IT must move per k-mer window (its own roofline model), for the kernels whose
+    loads are a fixed function of the workload. k_scan_ax's are counted instead (ax_request_bytes).
+
     Table path (k_scan_kt): one 64-B table bucket per window + the read bytes (bases + qualities).
     LF-step path (k_scan): SURVEY.md 8(d)'s 2*k*64 B per window (k LF steps x 2 occ loads)."""
     rb = 2.0 * read_bytes / max(1, kmers)
     if dev.tuning("last_kernel") == 3:
-        per = rb + 4.0 + (k - 1 + 32) / 4.0 / 32.0 + 64.0 * n_reads / max(1, kmers)
-        return {"kernel": "k_scan_ax (anchor-and-extend scan, speq_amd/csrc/ax_scan.hip)", "bytes_per_kmer": per,
-                "model": "read bases + qualities, one 4-B class per window, the 2-bit text of each 32-window run "
-                         "((k - 1 + 32) / 4 B), one 64-B anchor bucket per read"}
+        return {"kernel": "k_scan_ax (anchor-and-extend scan, speq_amd/csrc/ax_scan.hip)", "bytes_per_kmer": None,
+                "model": "bytes the kernel requests, counted by its instrumented twin (ax_request_bytes)"}
     if table_on:
         return {"kernel": "k_scan_kt (pipelined k-mer-table scan, speq_amd/csrc/scan_kernels.hip)",
                 "bytes_per_kmer": 64.0 + rb,
@@ -142,21 +159,22 @@ def kernel_model(dev, k: int, table_on: bool, kmers: int, read_bytes: int, n_rea
             "model": "SURVEY.md 8(d): k LF steps x 2 occ-block loads x 64 B"}
 
 
-def traffic_lookup(cfg: int, k: int, mode: str, n_reads: int, kernel: str):
+def traffic_lookup(cfg: int, k: int, mode: str, n_reads: int, kernel: str) -> dict | None:
     """Measured fabric bytes per launch of this exact workload and kernel (rocprofv3 PMC passes summarised into
-    profiles/traffic.json by scripts/summarize_profile.py --traffic-key), or (None, None)."""
+    profiles/traffic.json by scripts/summarize_profile.py --traffic-key), or None."""
     prof = os.path.join(ROOT, "profiles", "traffic.json")
     if not os.path.exists(prof):
-        return None, None
+        return None
     try:
         tj = json.load(open(prof))
     except ValueError:
-        return None, None
+        return None
     key = f"cfg{cfg}_k{k}_{mode}_reads{n_reads}_{kernel}"
-    if key in tj:
-        src = tj[key]["source"]
-        return tj[key]["hbm_bytes_per_launch"], os.path.normpath(os.path.join("profiles", src))
-    return None, None
+    if key not in tj:
+        return None
+    e = dict(tj[key])
+    e["source"] = os.path.normpath(os.path.join("profiles", e["source"]))
+    return e
 
 
 KERNEL_TAG = {0: "lf", 1: "kt", 2: "kt", 3: "ax"}  # speq_device_get_tuning("last_kernel")
@@ -269,24 +287,50 @@ def run_workload(ctx: Ctx, cfg_no: int, k: int, n_reads: int, mode: str, steps: 
     total_kmers = kmers_per_step * ctx.world * steps
     value = total_kmers / elapsed
     avg_kernel_s = (kernel_ms / 1e3) / max(1, launches)
-    own_bytes = kmers_per_step * km["bytes_per_kmer"]
+    ax_stats = None
+    if hot_kernel == 3:
+        # one untimed launch of the instrumented twin: the same scan (checked equal), plus its work counters
+        d_counts.zero_()
+        if local:
+            d_w.zero_()
+        ax_stats = dev.scan_device_stats(d_seq.data_ptr(), d_qual.data_ptr(), d_off.data_ptr(), reads.n, k,
+                                         d_counts.data_ptr(), d_w.data_ptr(), paired=paired, local=local)
+        if not np.array_equal(d_counts.cpu().numpy(), counts):
+            raise RuntimeError("instrumented anchor-and-extend scan disagrees with the timed scan")
+        req = ax_request_bytes(ax_stats, k, reads.n, local)
+        own_bytes = req["total"]
+        km["bytes_per_kmer"] = own_bytes / kmers_per_step
+        km["bytes_parts"] = {key: round(v / kmers_per_step, 4) for key, v in req["parts"].items()}
+    else:
+        own_bytes = kmers_per_step * km["bytes_per_kmer"]
     own_gbs = own_bytes / avg_kernel_s / 1e9
     survey_gbs = kmers_per_step * 2 * k * OCC_ENTRY_BYTES / avg_kernel_s / 1e9
-    traffic, traffic_src = traffic_lookup(cfg_no, k, mode, n_reads, KERNEL_TAG.get(hot_kernel, "lf"))
+    tr = traffic_lookup(cfg_no, k, mode, n_reads, KERNEL_TAG.get(hot_kernel, "lf"))
+    traffic = tr["hbm_bytes_per_launch"] if tr else None
     roofline = {
         "bound": "hbm", "achieved": own_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": own_gbs / HBM_PEAK_GBS,
         "traffic": traffic,
         "kernel": km["kernel"], "bytes_per_kmer": round(km["bytes_per_kmer"], 3), "bytes_model": km["model"],
+        "bytes_per_kmer_by_kind": km.get("bytes_parts"), "own_bytes_per_launch": own_bytes,
         "avg_kernel_ms": avg_kernel_s * 1e3, "launches_timed": launches,
         # measured L2->fabric bytes per launch (rocprofv3 PMC, profiles/): what the kernel really draws from
-        # Infinity Cache + HBM, over this run's launch time, against the same 8 TB/s
+        # Infinity Cache + HBM, over this run's launch time, against the same 8 TB/s; split into reads, writes and
+        # the register-spill writes (Scratch_Size x lanes) inside them
+        "traffic_fetch": tr.get("fetch_bytes_per_launch") if tr else None,
+        "traffic_write": tr.get("write_bytes_per_launch") if tr else None,
+        "traffic_scratch_write": tr.get("scratch_write_bytes_per_launch") if tr else None,
         "traffic_GBps": (traffic / avg_kernel_s / 1e9) if traffic else None,
         "traffic_frac": (traffic / avg_kernel_s / 1e9 / HBM_PEAK_GBS) if traffic else None,
-        "traffic_source": traffic_src,
+        "useful_traffic_frac": ((traffic - (tr.get("scratch_write_bytes_per_launch") or 0.0)) / avg_kernel_s / 1e9
+                                / HBM_PEAK_GBS) if traffic else None,
+        "traffic_source": tr["source"] if tr else None,
+        "traffic_rocprof_kernel_ns": tr.get("kernel_steady_state_ns_rocprof") if tr else None,
         # SURVEY.md 8(d)'s fixed model (2*k*64 B per k-mer: k uncached LF steps) — not what this kernel moves
         "survey_model_bytes_per_kmer": 2 * k * OCC_ENTRY_BYTES,
         "survey_model_frac": survey_gbs / HBM_PEAK_GBS,
     }
+    if ax_stats is not None:
+        roofline["ax_work"] = ax_stats
 
     pcie = None
     if with_pcie:

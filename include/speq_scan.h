@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define SPEQ_ABI_VERSION 6
+#define SPEQ_ABI_VERSION 7
 
 enum {
     SPEQ_OK = 0,
@@ -140,6 +140,19 @@ int speq_scan_reads_device(speq_device_index* d, const uint8_t* d_seq, const uin
                            const uint64_t* d_offsets, uint64_t n_reads, const speq_scan_params* params,
                            uint64_t* d_counts, double* d_weights, void* stream);
 
+/* Diagnostic twin of speq_scan_reads_device (not the hot path; bench.py's roofline model): the same scan and
+ * results, run by an instrumented instantiation of the anchor-and-extend kernel that also counts the work it did.
+ * stats (host, u64[SPEQ_AX_STATS_N], overwritten; synchronous): [0] loop iterations per wave, [1] anchor-bucket loads
+ * (64 B each), [2] run granule loads (lanes; NWC + 1 16-B granules each), [3]/[4] iterations in which a wave issued
+ * bucket/granule loads, [5] windows classified by runs, [6] deferred windows, [7] deferred windows past the Bloom
+ * filter, [8] phase-2 bucket loads, [9] phase-2 granule loads (NWC 16-B granules each), [10] staged 16-base chunks
+ * (16 B of bases + 16 B of qualities), [11] staged read segments, [12] single quality bytes loaded, [13] windows
+ * tallied by runs. Fails with SPEQ_E_ARG when the scan would not use the anchor-and-extend kernel. */
+#define SPEQ_AX_STATS_N 14
+int speq_scan_reads_device_stats(speq_device_index* d, const uint8_t* d_seq, const uint8_t* d_qual,
+                                 const uint64_t* d_offsets, uint64_t n_reads, const speq_scan_params* params,
+                                 uint64_t* d_counts, double* d_weights, uint64_t* stats);
+
 /* Host-buffer convenience used by the CLI: stages the reads to HBM in batches, runs the kernel and
  * returns the totals (counts: u64[G+2]; weights: f64[G] or NULL). Synchronous. */
 int speq_scan_reads(speq_device_index* d, const uint8_t* seq, const uint8_t* qual, const uint64_t* offsets,
@@ -153,10 +166,25 @@ int speq_ref_unique(speq_device_index* d, uint32_t k, uint64_t* u_ref, uint64_t*
 int speq_ref_unique_device(speq_device_index* d, uint32_t k, uint64_t* d_u_ref, uint64_t* d_tot_ref,
                            void* stream);
 
-/* ---- multi-GPU: one RCCL all-reduce of the counter vector (replaces the future.get() sums,
- * fm_scanner.cpp:224-233).  comm is an ncclComm_t created with speq_comm_init. ---- */
+/* ---- multi-GPU: one all-reduce of the counter vector (replaces the future.get() sums, fm_scanner.cpp:224-233).
+ * A communicator (void* comm) runs over one of two transports: RCCL (ncclAllReduce over xGMI; one rank per GPU) or
+ * host sockets (loopback TCP: a reduce at rank 0 in rank order and a broadcast; ranks may share a GPU). Every
+ * speq_allreduce_* / speq_em_allreduce call below takes either. ---- */
+enum { SPEQ_COMM_AUTO = 0, SPEQ_COMM_RCCL = 1, SPEQ_COMM_HOST = 2 };
+/* RCCL communicator from an id that rank 0 made with speq_comm_unique_id and handed to the others out of band
+ * (bench.py: torch.distributed); binds to the calling thread's current GPU. */
 int speq_comm_unique_id(void* id_out /* 128 bytes */);
 int speq_comm_init(int nranks, int rank, const void* id /* 128 bytes */, void** comm_out);
+/* Rendezvous + communicator in one call (the CLI's one-process-per-GPU mode). Rank 0 listens on 127.0.0.1 and
+ * publishes {nonce, port} in the file rendezvous_path (replacing a stale one); the other ranks poll that file, connect
+ * and present the nonce (a stale file of a dead run is skipped: its port refuses or its nonce does not match), all
+ * within timeout_s. transport: SPEQ_COMM_RCCL, SPEQ_COMM_HOST, or SPEQ_COMM_AUTO = RCCL when every rank's `device`
+ * is a different GPU (PCI bus id), else host sockets (RCCL refuses two ranks on one GPU). The RCCL communicator is
+ * created on GPU `device` (set and restored around ncclCommInitRank); device may be -1 with SPEQ_COMM_HOST. */
+int speq_comm_connect(int nranks, int rank, int device, const char* rendezvous_path, int transport, int timeout_s,
+                      void** comm_out);
+/* SPEQ_COMM_RCCL or SPEQ_COMM_HOST (the transport a communicator runs on); SPEQ_E_ARG for NULL. */
+int speq_comm_transport(void* comm);
 int speq_comm_destroy(void* comm);
 int speq_allreduce_u64(void* comm, uint64_t* d_buf, uint64_t count, void* stream);
 int speq_allreduce_f64(void* comm, double* d_buf, uint64_t count, void* stream);
@@ -276,8 +304,8 @@ int speq_ref_unique_shard(speq_device_index* d, uint32_t k, uint32_t shard, uint
  * that starts a multi-group interval on any rank starts the same interval everywhere), enqueued on stream and
  * synchronized. Every rank then holds the whole job's histogram (speq_em_finalize / speq_em_step as usual). */
 int speq_em_allreduce(speq_em* em, void* comm, void* stream);
-/* In-place sum over the ranks of comm of `count` u64 (is_f64 = 0) or f64 (is_f64 = 1) words in HOST memory, staged
- * through GPU `device` (blocking): the CLI's counters, weights, .dat sums, statistics and status flags. */
+/* In-place sum over the ranks of comm of `count` u64 (is_f64 = 0) or f64 (is_f64 = 1) words in HOST memory (blocking;
+ * RCCL communicators stage it through GPU `device`): the CLI's counters, weights, .dat sums, statistics and flags. */
 int speq_allreduce_host(void* comm, int device, void* buf, uint64_t count, int is_f64);
 
 /* ---- groupings file (speq::file_to_map, /root/reference/src/file_to_map.cpp:20-119) ----

@@ -70,7 +70,14 @@ def main():
     if tkey and "fabric_read_bytes_per_launch" in out:
         tp = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "profiles", "traffic.json")
         tj = json.load(open(tp)) if os.path.exists(tp) else {}
+        scratch = None
+        if meta.get("Scratch_Size") not in (None, "") and meta.get("Grid_Size") not in (None, ""):
+            scratch = float(meta["Scratch_Size"]) * float(meta["Grid_Size"])  # spill bytes per lane x lanes
         tj[tkey] = {"hbm_bytes_per_launch": out["fabric_read_bytes_per_launch"] + out.get("fabric_write_bytes_per_launch", 0.0),
+                    "fetch_bytes_per_launch": out["fabric_read_bytes_per_launch"],
+                    "write_bytes_per_launch": out.get("fabric_write_bytes_per_launch"),
+                    "scratch_write_bytes_per_launch": scratch,
+                    "scratch_bytes_per_lane": meta.get("Scratch_Size"), "vgpr_count": meta.get("VGPR_Count"),
                     "note": "FETCH_SIZE+WRITE_SIZE (KiB x 1024) per scan launch; L2->fabric bytes incl. Infinity-Cache "
                             "hits (upper bound on HBM bytes)",
                     "source": os.path.relpath(os.path.join(dst, f"pmc_{tag}.json"), os.path.join(os.path.dirname(tp))),

@@ -70,12 +70,15 @@ SIGNATURES = {
     "speq_device_open": (C.c_int, [_P, C.c_int, C.POINTER(_P)]),
     "speq_device_close": (C.c_int, [_P]),
     "speq_scan_reads_device": (C.c_int, [_P, _P, _P, _P, C.c_uint64, C.POINTER(ScanParams), _P, _P, _P]),
+    "speq_scan_reads_device_stats": (C.c_int, [_P, _P, _P, _P, C.c_uint64, C.POINTER(ScanParams), _P, _P, _U64P]),
     "speq_scan_reads": (C.c_int, [_P, C.c_char_p, C.c_char_p, _U64P, C.c_uint64, C.POINTER(ScanParams),
                                   _U64P, _F64P]),
     "speq_ref_unique": (C.c_int, [_P, C.c_uint32, _U64P, _U64P]),
     "speq_ref_unique_device": (C.c_int, [_P, C.c_uint32, _P, _P, _P]),
     "speq_comm_unique_id": (C.c_int, [_P]),
     "speq_comm_init": (C.c_int, [C.c_int, C.c_int, _P, C.POINTER(_P)]),
+    "speq_comm_connect": (C.c_int, [C.c_int, C.c_int, C.c_int, C.c_char_p, C.c_int, C.c_int, C.POINTER(_P)]),
+    "speq_comm_transport": (C.c_int, [_P]),
     "speq_comm_destroy": (C.c_int, [_P]),
     "speq_allreduce_u64": (C.c_int, [_P, _P, C.c_uint64, _P]),
     "speq_allreduce_f64": (C.c_int, [_P, _P, C.c_uint64, _P]),
@@ -124,7 +127,7 @@ SIGNATURES = {
 }
 
 _lib = None
-ABI_VERSION = 6  # include/speq_scan.h SPEQ_ABI_VERSION (struct layouts above)
+ABI_VERSION = 7  # include/speq_scan.h SPEQ_ABI_VERSION (struct layouts above)
 
 
 def lib() -> C.CDLL:

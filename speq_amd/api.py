@@ -189,6 +189,21 @@ class DeviceIndex:
         check(lib().speq_scan_reads_device(self._h, d_seq, d_qual, d_offsets, n_reads, C.byref(p), d_counts,
                                            d_weights or None, stream or None))
 
+    AX_STATS_KEYS = ("wave_iters", "lookup_lanes", "run_lanes", "lookup_waves", "run_waves", "run_windows",
+                     "deferred", "filter_pass", "p2_probes", "p2_verify", "chunks", "segments", "qual_bytes",
+                     "run_tallied")
+
+    def scan_device_stats(self, d_seq: int, d_qual: int, d_offsets: int, n_reads: int, k: int, d_counts: int,
+                          d_weights: int = 0, phred_cutoff: int = 30, paired: bool = False,
+                          local: bool = False) -> dict:
+        """scan_device through the instrumented anchor-and-extend kernel (speq_scan_reads_device_stats, synchronous):
+        the same counters, plus the kernel's work counts by kind (keys AX_STATS_KEYS)."""
+        p = ScanParams(k, phred_cutoff, int(paired), SPEQ_MODE_LOCAL if local else SPEQ_MODE_GLOBAL)
+        st = np.zeros(len(self.AX_STATS_KEYS), dtype=np.uint64)
+        check(lib().speq_scan_reads_device_stats(self._h, d_seq, d_qual, d_offsets, n_reads, C.byref(p), d_counts,
+                                                 d_weights or None, _u64p(st)))
+        return {key: int(v) for key, v in zip(self.AX_STATS_KEYS, st)}
+
     def scan_fastq(self, path1: str, path2: Optional[str] = None, k: int = 21, phred_cutoff: int = 30,
                    local: bool = False, threads: int = 4, em: Optional["EmHistogram"] = None):
         """Streams FASTQ(.gz) file(s) through pinned slots to the GPU (speq_scan_fastq). Paired when path2 is given.
@@ -276,14 +291,16 @@ class DeviceIndex:
 
 
 class Comm:
-    """One RCCL communicator of a one-process-per-GPU job (speq_comm_* / speq_allreduce_*; ncclAllReduce over xGMI).
+    """One communicator of a one-process-per-GPU job (speq_comm_* / speq_allreduce_*): RCCL (ncclAllReduce over
+    xGMI) or host sockets when ranks share a GPU.
 
     Replaces the host `future.get()` sums of per-thread count vectors (/root/reference/src/fm_scanner.cpp:224-233):
-    every rank scans its own read shard and one all-reduce sums the G + 2 counters (and the G weights). Rank 0 makes
-    the 128-byte id with `Comm.unique_id()` and hands it to the other ranks out of band (bench.py broadcasts it with
-    torch.distributed; `speq scan` writes it to a rendezvous file)."""
+    every rank scans its own read shard and one all-reduce sums the G + 2 counters (and the G weights). Either rank 0
+    makes the 128-byte RCCL id with `Comm.unique_id()` and hands it to the other ranks out of band (bench.py broadcasts
+    it with torch.distributed), or `Comm.connect` runs the rendezvous through a file (as `speq scan` does)."""
 
     ID_BYTES = 128
+    AUTO, RCCL, HOST = 0, 1, 2
 
     @staticmethod
     def unique_id() -> bytes:
@@ -297,6 +314,27 @@ class Comm:
         h = C.c_void_p()
         check(lib().speq_comm_init(nranks, rank, C.create_string_buffer(uid, Comm.ID_BYTES), C.byref(h)))
         self._h, self.nranks, self.rank = h, nranks, rank
+
+    @classmethod
+    def connect(cls, nranks: int, rank: int, rendezvous: str, device: int = -1, transport: int = 0,
+                timeout_s: int = 120) -> "Comm":
+        """speq_comm_connect: file rendezvous at `rendezvous`; transport AUTO (RCCL when every rank has its own GPU),
+        RCCL or HOST (loopback sockets; device may be -1)."""
+        self = cls.__new__(cls)
+        h = C.c_void_p()
+        check(lib().speq_comm_connect(nranks, rank, device, rendezvous.encode(), transport, timeout_s, C.byref(h)))
+        self._h, self.nranks, self.rank = h, nranks, rank
+        return self
+
+    @property
+    def transport(self) -> int:
+        return lib().speq_comm_transport(self._h)
+
+    def allreduce_host(self, buf: np.ndarray, device: int = -1) -> None:
+        """In-place sum over the ranks of a host u64 or f64 array (speq_allreduce_host)."""
+        if buf.dtype not in (np.uint64, np.float64) or not buf.flags.c_contiguous:
+            raise TypeError("allreduce_host takes a contiguous uint64 or float64 array")
+        check(lib().speq_allreduce_host(self._h, device, buf.ctypes.data, buf.size, int(buf.dtype == np.float64)))
 
     def allreduce_u64(self, d_buf: int, count: int, stream: int = 0) -> None:
         """In-place sum of `count` u64 at device pointer d_buf, enqueued on `stream` (raw hipStream_t)."""
@@ -450,6 +488,21 @@ class Node:
 
     def em_histograms(self) -> list["EmHistogram"]:
         return [EmHistogram(d) for d in self.devices]
+
+    AX_STATS_KEYS = ("wave_iters", "lookup_lanes", "run_lanes", "lookup_waves", "run_waves", "run_windows",
+                     "deferred", "filter_pass", "p2_probes", "p2_verify", "chunks", "segments", "qual_bytes",
+                     "run_tallied")
+
+    def scan_device_stats(self, d_seq: int, d_qual: int, d_offsets: int, n_reads: int, k: int, d_counts: int,
+                          d_weights: int = 0, phred_cutoff: int = 30, paired: bool = False,
+                          local: bool = False) -> dict:
+        """scan_device through the instrumented anchor-and-extend kernel (speq_scan_reads_device_stats, synchronous):
+        the same counters, plus the kernel's work counts by kind (keys AX_STATS_KEYS)."""
+        p = ScanParams(k, phred_cutoff, int(paired), SPEQ_MODE_LOCAL if local else SPEQ_MODE_GLOBAL)
+        st = np.zeros(len(self.AX_STATS_KEYS), dtype=np.uint64)
+        check(lib().speq_scan_reads_device_stats(self._h, d_seq, d_qual, d_offsets, n_reads, C.byref(p), d_counts,
+                                                 d_weights or None, _u64p(st)))
+        return {key: int(v) for key, v in zip(self.AX_STATS_KEYS, st)}
 
     def scan_fastq(self, path1: str, path2: Optional[str] = None, k: int = 21, phred_cutoff: int = 30,
                    local: bool = False, threads: int = 4, ems: Optional[Sequence["EmHistogram"]] = None):

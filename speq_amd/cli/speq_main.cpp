@@ -411,11 +411,12 @@ struct PhaseClock {
 
 // ---- one process per GPU (RANK / WORLD_SIZE / LOCAL_RANK from a launcher such as `torchrun --no-python`) ----
 // Every rank opens its own replica on GPU $LOCAL_RANK, scans its share of the FASTQ blocks and of the reference
-// windows, and the sums are RCCL all-reduces (speq_allreduce_host / speq_em_allreduce): the reference's future.get()
+// windows, and the sums are all-reduces (speq_allreduce_host / speq_em_allreduce): the reference's future.get()
 // sums (fm_scanner.cpp:224-233) across processes. Rank 0 prints and writes everything; the others print nothing.
-// The RCCL id travels through a rendezvous file ($SPEQ_RENDEZVOUS, default /tmp/speq_rdzv_<parent pid>_<MASTER_PORT>:
-// the launcher is every rank's parent), written by rank 0 only after its index step, so `speq all` ranks also wait
-// for the index there.
+// The ranks meet through speq_comm_connect: rank 0 publishes {nonce, port} in a rendezvous file ($SPEQ_RENDEZVOUS,
+// default /tmp/speq_rdzv_<parent pid>_<MASTER_PORT>_<TORCHELASTIC_RUN_ID>: the launcher is every rank's parent) only
+// after its index step, so `speq all` ranks also wait for the index there. The transport is RCCL when the ranks are
+// on different GPUs, host sockets when they share one ($SPEQ_COMM = rccl | host forces it).
 struct Dist {
     int rank = 0, world = 1, device = 0;
     void* comm = nullptr;
@@ -438,42 +439,35 @@ Dist dist_from_env(const CmdArguments& a) {
     return dd;
 }
 
-void dist_connect(Dist& dd) {
-    std::string path;
-    if (const char* v = std::getenv("SPEQ_RENDEZVOUS"); v && *v) path = v;
-    else {
-        const char* port = std::getenv("MASTER_PORT");
-        const char* tmp = std::getenv("TMPDIR");
-        path = std::string(tmp && *tmp ? tmp : "/tmp") + "/speq_rdzv_" + std::to_string((long)getppid()) + "_" +
-               (port ? port : "0");
-    }
-    unsigned char id[128];
-    if (dd.rank == 0) {
-        ok(speq_comm_unique_id(id), "creating the RCCL id");
-        const std::string tmp = path + ".tmp." + std::to_string((long)getpid());
-        {
-            std::ofstream os(tmp, std::ios::binary | std::ios::trunc);
-            os.write(reinterpret_cast<const char*>(id), sizeof(id));
-            if (!os) throw CApiError("cannot write the rendezvous file " + tmp);
-        }
-        fs::rename(tmp, path);
-    } else {
-        const int limit_s = env_int("SPEQ_RENDEZVOUS_TIMEOUT", 600);
-        const auto t0 = std::chrono::steady_clock::now();
-        for (;;) {
-            std::ifstream is(path, std::ios::binary);
-            if (is.read(reinterpret_cast<char*>(id), sizeof(id))) break;
-            if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(limit_s))
-                throw CApiError("rank " + std::to_string(dd.rank) + ": no rendezvous file " + path + " after " +
-                                std::to_string(limit_s) + " s");
-            std::this_thread::sleep_for(std::chrono::milliseconds(20));
-        }
-    }
-    ok(speq_comm_init(dd.world, dd.rank, id, &dd.comm), "joining the RCCL communicator");
-    if (dd.rank == 0) {  // every rank has joined (ncclCommInitRank is collective): the file has been read
+std::string rendezvous_path() {
+    if (const char* v = std::getenv("SPEQ_RENDEZVOUS"); v && *v) return v;
+    const char* port = std::getenv("MASTER_PORT");
+    const char* run = std::getenv("TORCHELASTIC_RUN_ID");
+    const char* tmp = std::getenv("TMPDIR");
+    return std::string(tmp && *tmp ? tmp : "/tmp") + "/speq_rdzv_" + std::to_string((long)getppid()) + "_" +
+           (port ? port : "0") + "_" + (run && *run ? run : "none");
+}
+
+// Rank 0 of a one-process-per-GPU run clears a rendezvous file left by an earlier, crashed run before its (possibly
+// long) index step; the other ranks would skip it anyway (its nonce and port are dead).
+void dist_clear_stale(const Dist& dd) {
+    if (dd.on() && dd.rank == 0) {
         std::error_code ec;
-        fs::remove(path, ec);
+        fs::remove(rendezvous_path(), ec);
     }
+}
+
+void dist_connect(Dist& dd) {
+    int transport = SPEQ_COMM_AUTO;
+    if (const char* v = std::getenv("SPEQ_COMM"); v && *v) {
+        const std::string t(v);
+        if (t == "rccl") transport = SPEQ_COMM_RCCL;
+        else if (t == "host") transport = SPEQ_COMM_HOST;
+        else if (t != "auto") throw CApiError("SPEQ_COMM must be auto, rccl or host");
+    }
+    const int limit_s = env_int("SPEQ_RENDEZVOUS_TIMEOUT", 600);
+    ok(speq_comm_connect(dd.world, dd.rank, dd.device, rendezvous_path().c_str(), transport, limit_s, &dd.comm),
+       "joining the ranks");
 }
 
 // Sums u64 (or f64) words over the ranks, in place.
@@ -717,7 +711,9 @@ int main(int argc, char** argv) {
     if (!a.is_parsed) return 0;
     try {
         // one process per GPU: rank 0 alone builds the index; the others wait for it at the rendezvous in run_scan
-        const bool other_rank = a.is_scanner && dist_from_env(a).rank != 0;
+        const Dist dd = a.is_scanner ? dist_from_env(a) : Dist{};
+        dist_clear_stale(dd);
+        const bool other_rank = dd.rank != 0;
         if (a.is_indexer && !other_rank) run_index(a);
         if (a.is_scanner) run_scan(a);
     } catch (const std::exception& e) {

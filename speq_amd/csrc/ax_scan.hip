@@ -4,26 +4,32 @@
 // (/root/reference/src/fm_scanner.cpp:153-196 global, :426-471 local, :665-729 paired, :916-962 paired local).
 //
 // Why: consecutive windows of a read that matches the reference are consecutive positions of the reference text, and
-// whether a k-mer is unique to one group is a property of the k-mer, i.e. of ANY of its occurrences. So per k the
-// replica keeps the class of the k-mer that starts at every text position (`cls`, 1 byte per position when the
-// index has <= 253 groups, else 2: the group, MULTI, or SENT for a window that crosses a text end or holds an N), plus
-// a hash table of one representative position per distinct k-mer (`atab`). A lane takes one READ: it looks one window
-// up (the anchor: bucket -> fingerprint -> representative p), then compares the read with the 2-bit text at p, 64
-// windows at a time (one XOR per 32 bases), and reads the classes of the matched windows (64 bytes: four 16-B loads).
-// A mismatch (a SNP against the representative, or a sequencing error) ends the run and the next window is looked up
-// again. Every verdict is exact: a window is classified from cls[p'] only after its k bases were compared equal with
-// text[p', p' + k), and a window is absent only after its key's chain in the anchor table ran into an empty slot
-// without a verified fingerprint match (or its bits are missing from the table's blocked Bloom filter, which holds
-// every k-mer of the texts).
+// whether a k-mer is unique to one group is a property of the k-mer, i.e. of ANY of its occurrences. A k-mer that
+// occurs at text position p occurs in the group of p's text, so its class is one of four 2-bit codes relative to that
+// text: OWN (every occurrence is in the group of p's text), MULTI (occurrences in >= 2 groups), SENT (the window holds
+// an N inside one text) or END (the window crosses a text end). Per k the replica keeps
+//   * `gran`: per 32 text positions one 16-B granule {2-bit text of the 32 positions, class plane 0, class plane 1}
+//     — a run of 64 windows is NG consecutive 16-B loads of ONE array (text and classes together);
+//   * `atab`: a hash table of one representative position per distinct k-mer, each slot {position, 16-bit
+//     fingerprint, group of the position's text};
+//   * a blocked Bloom filter of the distinct k-mers.
+// A lane takes one READ: it looks one window up (the anchor: bucket -> fingerprint -> representative p and its
+// text's group), then compares the read with the text at p, 64 windows at a time (one XOR per 32 bases), and tallies
+// the matched OWN windows to the run's group. A mismatch (a SNP against the representative, or a sequencing error)
+// ends the run and the next window is looked up again; so does an END window (the run would leave p's text).
+// Every verdict is exact: a window is classified from its class at p' only after its k bases were compared equal
+// with text[p', p' + k) (SENT windows, whose text holds an N coded as A, are never classified from the text: they are
+// looked up), and a window is absent only after its key's chain in the anchor table ran into an empty slot without a
+// verified match (or its bits are missing from the Bloom filter, which holds every k-mer of the texts).
 //
-// Windows whose anchor lookup finds nothing (the k windows over a sequencing error) and windows that matched a text
-// position whose class is SENT are DEFERRED: the wave collects them in LDS and, after the per-read pass, tests them
-// against the Bloom filter (four per lane per round trip) and looks the survivors up one per lane, so one erroneous
-// read does not hold its wave for k lookups.
+// Windows whose anchor lookup finds nothing (the k windows over a sequencing error) and SENT windows are DEFERRED:
+// the wave collects them in LDS and, after the per-read pass, tests them against the Bloom filter (four per lane per
+// round trip) and looks the survivors up one per lane, so one erroneous read does not hold its wave for k lookups.
 //
-// What bounds it (profiles/r02): the per-CU vector-memory path, which serves the lanes' scattered 16-B loads one
-// cache line per lane; so the classes are bytes (a 64-window run is four loads, not sixteen), a load group is issued
-// only when some lane of the wave needs it, and one iteration costs one round trip.
+// What bounds it (profiles/r02, r03): the per-CU vector-memory path, which serves the lanes' scattered loads one cache
+// line per lane and instruction. So a run's text and classes come from one array (NG 16-B loads instead of NWC + 1
+// 8-B text loads and five class loads of r02), a load group is issued only when some lane of the wave needs it, and
+// one iteration costs one round trip.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -39,6 +45,7 @@
 #include "device_index.hpp"
 #include "scan_device.hpp"
 #include "scan_internal.hpp"
+#include "speq_scan.h"
 
 namespace {
 
@@ -48,35 +55,46 @@ constexpr uint32_t AX_MAX_K = 128;    // longest k the scan takes (AX_CAP - k + 
 constexpr uint32_t AX_CAP = 192;      // bases of a read a lane stages at once (longer reads: segments of AX_CAP bases)
 constexpr uint32_t AX_STREAM = AX_CAP + 16;  // staged bases incl. the 16-B alignment slack before the read
 constexpr uint32_t AX_CHUNKS = AX_STREAM / 16;
-constexpr uint32_t AX_RUN = 64;       // windows a lane classifies per iteration (one compare, 64 class bytes)
+constexpr uint32_t AX_RUN = 64;       // windows a lane classifies per iteration (one compare, two class words)
 constexpr uint32_t AX_VWW = 4;        // valid-window words per lane
 constexpr uint32_t AX_SCH = 64 * AX_CHUNKS;     // 16-base chunks of a wave's staged stream (every lane's segment)
 constexpr uint32_t AX_CSW = AX_SCH / 2 + 8;     // 2-bit code words (u64) of the stream, + read-past slack
 constexpr uint32_t AX_BSW = AX_SCH / 2 + 16;    // 1-bit-per-base words (u32) of the stream (bad / quality change)
-constexpr uint32_t AX_DEF = 1024;     // deferred-window entries per wave (u16: lane | window << 6)
+constexpr uint32_t AX_DEF = 896;      // deferred-window entries per wave (u16: lane | window << 6); 7.9 KB per wave: 5 blocks per CU
 constexpr uint32_t AX_F = 4;          // deferred windows a lane tests against the filter per round trip
 constexpr uint32_t AX_EMPTY = 0xFFFFFFFFu;
 constexpr uint16_t AX_VOID = 0xFFFFu;  // a deferred-list slot reserved by a lane that then kept its windows
 constexpr unsigned long long AX_SLOT_EMPTY = ~0ull;
 constexpr uint32_t AX_OOB = 0xFFFFFFF0u;  // buffer offset past every array (n < 2^30)
 constexpr uint32_t AX_FILTER_BITS = 16;   // Bloom filter bits per distinct k-mer (3 bits set per k-mer, one 64-bit word)
+constexpr uint32_t AX_MAX_G = 0xFFFFu;    // groups a slot's 16-bit group field holds
 typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+
+// class codes: plane 0 = bit 0, plane 1 = bit 1
+enum : uint32_t { AX_OWN = 0, AX_MULTI = 1, AX_SENT = 2, AX_END = 3 };
 
 static_assert(AX_STREAM % 16 == 0, "chunks of 16 bases");
 static_assert(AX_CAP < 1024, "deferred entries hold the window in 10 bits");
 
-// class values (CW bytes per text position): groups 0 .. G-1 < NONE; NONE is never stored
-template <int CW>
-struct AxCls {
-    static constexpr uint32_t SENT = CW == 1 ? 0xFFu : 0xFFFFu;
-    static constexpr uint32_t MULTI = SENT - 1u;
-    static constexpr uint32_t NONE = SENT - 2u;
-    static constexpr uint32_t MAX_G = NONE;
-    static constexpr uint32_t PER = 4 / CW;                                   // classes per dword
-    static constexpr uint32_t REP = CW == 1 ? 0x01010101u : 0x00010001u;      // broadcast factor
-    static constexpr uint32_t FLAGS = CW == 1 ? 0x80808080u : 0x80008000u;    // top bit of every element
-    static constexpr uint32_t LOW7 = CW == 1 ? 0x7F7F7F7Fu : 0x7FFF7FFFu;
+// per-launch work counters of the diagnostic (STATS) instantiation; bench.py turns them into the kernel's own bytes
+enum : uint32_t {
+    AXS_WAVE_ITERS = 0,  // phase-1 loop iterations (per wave)
+    AXS_LOOKUP_LANES,    // phase-1 lane-iterations that loaded an anchor bucket (64 B)
+    AXS_RUN_LANES,       // phase-1 lane-iterations that loaded a run's granules (NG x 16 B)
+    AXS_LOOKUP_WAVES,    // phase-1 iterations in which the wave issued the bucket loads
+    AXS_RUN_WAVES,       // ... the granule loads
+    AXS_RUN_WINDOWS,     // windows a run classified (tallied, multi or skipped as invalid)
+    AXS_DEFERRED,        // windows put on the deferred list
+    AXS_FILTER_PASS,     // deferred windows the Bloom filter could not rule out
+    AXS_P2_PROBES,       // phase-2 bucket loads (lanes)
+    AXS_P2_VERIFY,       // phase-2 granule loads of a candidate (lanes; NGV x 16 B)
+    AXS_CHUNKS,          // staged 16-base chunks (16 B of bases + 16 B of qualities each)
+    AXS_SEGMENTS,        // staged read segments
+    AXS_QBYTES,          // single quality bytes loaded (local mode)
+    AXS_RUN_TALLIED,     // windows tallied by runs
+    AXS_N
 };
+static_assert(AXS_N == SPEQ_AX_STATS_N, "speq_scan.h SPEQ_AX_STATS_N");
 
 __host__ __device__ __forceinline__ uint64_t ax_fmix(uint64_t x) {  // murmur3 fmix64 (a bijection)
     x ^= x >> 33;
@@ -106,6 +124,8 @@ __device__ __forceinline__ uint64_t ax_hash(const uint64_t (&w)[NW], uint32_t k)
 __host__ __device__ __forceinline__ uint32_t ax_bucket(uint64_t h, uint64_t nb) {
     return (uint32_t)(((h >> 32) * nb) >> 32);
 }
+// slot fingerprint: the hash's low 16 bits (the bucket comes from its high 32)
+__host__ __device__ __forceinline__ uint32_t ax_fp(uint64_t h) { return (uint32_t)h & 0xFFFFu; }
 // Bloom filter of the distinct k-mers: one 64-bit word per key, three bits in it
 __host__ __device__ __forceinline__ uint32_t ax_fword(uint64_t h, uint64_t nf) {
     return (uint32_t)((((h >> 24) & 0xFFFFFFFFull) * nf) >> 32);
@@ -117,15 +137,11 @@ __host__ __device__ __forceinline__ uint64_t ax_fbits(uint64_t h) {
 __device__ __forceinline__ uint64_t funnel(uint64_t lo, uint64_t hi, uint32_t sh) {  // bits [sh, sh + 64) of hi:lo
     return sh == 0u ? lo : ((lo >> sh) | (hi << (64u - sh)));
 }
+__device__ __forceinline__ uint64_t u64of(uint32_t lo, uint32_t hi) { return (uint64_t)lo | ((uint64_t)hi << 32); }
 
 // bytes of v that are zero -> 0x80 in that byte (exact: no borrow between bytes)
 __device__ __forceinline__ uint32_t zero_bytes(uint32_t v) {
     return ~(((v & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | v) & 0x80808080u;
-}
-// the same per element of a class dword
-template <int CW>
-__device__ __forceinline__ uint32_t zero_elems(uint32_t v) {
-    return ~(((v & AxCls<CW>::LOW7) + AxCls<CW>::LOW7) | v) & AxCls<CW>::FLAGS;
 }
 // the 0x80 flags of the four bytes -> bits 0..3
 __device__ __forceinline__ uint32_t flags4(uint32_t m) {
@@ -133,12 +149,6 @@ __device__ __forceinline__ uint32_t flags4(uint32_t m) {
     y |= y >> 7;
     y |= y >> 14;
     return y & 0xFu;
-}
-// bits 0 .. PER-1 of b -> the top bit of each element of a class dword
-template <int CW>
-__device__ __forceinline__ uint32_t spread(uint32_t b) {
-    if (CW == 1) return ((b * 0x00204081u) & 0x01010101u) << 7;
-    return ((b * 0x00008001u) & 0x00010001u) << 15;
 }
 
 // ---------------------------------------------------------------------------------------------------------------
@@ -215,16 +225,13 @@ __device__ int ax_search_text(const DevView& I, const Rsrc& R, const uint8_t* __
     return lo < hi ? classify(I, R, lo, hi) : -1;
 }
 
-// Pass A: the class of the k-mer at every text position, and one representative position per distinct k-mer (the
-// first to claim owner[lo] of its SA interval). Multi-group k-mers also record their interval: mlo[pos] = its start
-// and mhi[start] = its end (EM histograms).
-template <int CW>
+// Pass A: the class code of the k-mer at every text position (one byte per position, packed into granules by pass
+// B), and one representative position per distinct k-mer (the first to claim owner[lo] of its SA interval).
+// Multi-group k-mers also record their interval: mlo[pos] = its start and mhi[start] = its end (EM histograms).
 __global__ void k_ax_classify(DevView I, const uint8_t* __restrict__ text, const uint64_t* __restrict__ tbad,
-                              uint64_t n, uint32_t k, void* __restrict__ cls_v, uint32_t* __restrict__ mlo,
+                              uint64_t n, uint32_t k, uint8_t* __restrict__ codes, uint32_t* __restrict__ mlo,
                               uint32_t* __restrict__ mhi, uint32_t* __restrict__ owner,
                               unsigned long long* __restrict__ n_distinct) {
-    using T = typename std::conditional<CW == 1, uint8_t, uint16_t>::type;
-    T* cls = static_cast<T*>(cls_v);
     const Rsrc R = make_rsrc(I);
     unsigned long long claimed = 0;
     for (uint64_t pos = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; pos < n;
@@ -238,14 +245,16 @@ __global__ void k_ax_classify(DevView I, const uint8_t* __restrict__ text, const
             valid = ((tbad[w] >> sh) & m) == 0;
             b += span;
         }
-        if (!valid) {
-            cls[pos] = (T)AxCls<CW>::SENT;
+        if (!valid) {  // END when the window reaches a separator / the terminator / past n, else SENT (an N)
+            bool end = pos + k > n;
+            for (uint32_t i = 0; i < k && !end; ++i) end = text[pos + i] <= 1u;
+            codes[pos] = (uint8_t)(end ? AX_END : AX_SENT);
             continue;
         }
         uint32_t lo = 0, hi = 0;
         const int g = ax_search_text(I, R, text + pos, k, lo, hi);
-        // g == -1 cannot happen: the window occurs at pos
-        cls[pos] = (T)(g >= 0 ? (uint32_t)g : AxCls<CW>::MULTI);
+        // g == -1 cannot happen: the window occurs at pos; g >= 0 is the group of pos's text
+        codes[pos] = (uint8_t)(g >= 0 ? AX_OWN : AX_MULTI);
         if (g == -2) {
             mlo[pos] = lo;
             mhi[lo] = hi;
@@ -253,6 +262,28 @@ __global__ void k_ax_classify(DevView I, const uint8_t* __restrict__ text, const
         if (atomicCAS(&owner[lo], AX_EMPTY, (uint32_t)pos) == AX_EMPTY) ++claimed;
     }
     if (claimed) atomicAdd(n_distinct, claimed);
+}
+
+// Pass B: granule b = {t2 word b (positions 32b .. 32b + 31), class plane 0, class plane 1}; positions >= n are END.
+__global__ void k_ax_pack(const uint64_t* __restrict__ t2, uint64_t t2_words, const uint8_t* __restrict__ codes,
+                          uint64_t n, u32x4* __restrict__ gran, uint64_t n_gran) {
+    for (uint64_t b = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; b < n_gran;
+         b += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t t = b < t2_words ? t2[b] : 0ull;
+        uint32_t p0 = 0, p1 = 0;
+        for (uint32_t i = 0; i < 32; ++i) {
+            const uint64_t pos = 32 * b + i;
+            const uint32_t c = pos < n ? codes[pos] : AX_END;
+            p0 |= (c & 1u) << i;
+            p1 |= (c >> 1) << i;
+        }
+        u32x4 v;
+        v[0] = (uint32_t)t;
+        v[1] = (uint32_t)(t >> 32);
+        v[2] = p0;
+        v[3] = p1;
+        gran[b] = v;
+    }
 }
 
 // aligned little-endian 2-bit words of the text starting at base p
@@ -267,11 +298,13 @@ __device__ __forceinline__ void ax_text_words(const uint64_t* __restrict__ t2, u
     for (int i = 0; i < NW; ++i) w[i] = funnel(raw[i], raw[i + 1], sh);
 }
 
-// Pass B: every representative position inserts {fingerprint, position} into the anchor table (8 slots per 64-B
-// bucket, first empty slot in order, linear probing over buckets; no deletions) and sets its filter bits.
+// Pass C: every representative position inserts {position | (fingerprint << 16 | group of its text) << 32} into the
+// anchor table (8 slots per 64-B bucket, first empty slot in order, linear probing over buckets; no deletions) and
+// sets its filter bits.
 __global__ void k_ax_insert(const uint32_t* __restrict__ owner, uint64_t n, const uint64_t* __restrict__ t2, uint32_t k,
-                            unsigned long long* __restrict__ atab, uint64_t nb, unsigned long long* __restrict__ filt,
-                            uint64_t nf) {
+                            const uint64_t* __restrict__ text_start, const int32_t* __restrict__ text_group,
+                            uint32_t n_texts, unsigned long long* __restrict__ atab, uint64_t nb,
+                            unsigned long long* __restrict__ filt, uint64_t nf) {
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
         const uint32_t p = owner[i];
         if (p == AX_EMPTY) continue;
@@ -279,7 +312,14 @@ __global__ void k_ax_insert(const uint32_t* __restrict__ owner, uint64_t n, cons
         ax_text_words<4>(t2, p, w);
         const uint64_t h = ax_hash<4>(w, k);
         atomicOr(&filt[ax_fword(h, nf)], (unsigned long long)ax_fbits(h));
-        const unsigned long long v = ((unsigned long long)p << 32) | (uint32_t)h;
+        uint32_t lo = 0, hi = n_texts;  // the last text t with text_start[t] <= p
+        while (hi - lo > 1u) {
+            const uint32_t mid = (lo + hi) / 2u;
+            if (text_start[mid] <= p) lo = mid;
+            else hi = mid;
+        }
+        const uint32_t grp = (uint32_t)text_group[lo] & 0xFFFFu;
+        const unsigned long long v = ((unsigned long long)((ax_fp(h) << 16) | grp) << 32) | p;
         uint32_t b = ax_bucket(h, nb);
         for (bool placed = false; !placed; b = (b + 1u == nb) ? 0u : b + 1u)
             for (uint32_t j = 0; j < 8u && !placed; ++j)
@@ -292,25 +332,57 @@ __global__ void k_ax_insert(const uint32_t* __restrict__ owner, uint64_t n, cons
 // ---------------------------------------------------------------------------------------------------------------
 
 struct AxView {
-    const uint64_t* t2;        // 2-bit text
-    const void* cls;           // class per text position (CW bytes each, + padding)
+    const u32x4* gran;         // granules {2-bit text, class plane 0, class plane 1} per 32 text positions
     const uint32_t* mlo;       // SA interval start of the multi-group k-mer at a text position (EM)
     const uint32_t* mhi;       // its end, by interval start (EM)
     const unsigned long long* atab;
     const unsigned long long* filt;
+    unsigned long long* stats; // STATS instantiation only: AXS_N counters
     uint64_t nb;               // buckets
     uint64_t nf;               // filter words
     uint64_t n;                // text length
-    uint64_t t2_bytes;         // bytes of the 2-bit text (incl. padding)
-    uint64_t cls_bytes;        // bytes of cls (incl. padding)
+    uint64_t gran_bytes;       // bytes of gran (incl. END padding)
     uint32_t G;
 };
 
-// One probe of the anchor table from bucket *b, slot *s: the first slot >= *s whose fingerprint matches (position in
-// *p), or "absent" when an empty slot comes first; a full bucket without either moves to the next one. On a match
-// *s is that slot (a failed verification resumes at *s + 1). Phase 2 only (phase 1 resolves its buckets inline).
+// Resolves one anchor bucket (8 slots {pos, fp << 16 | group}) from slot `s` on: the first slot whose fingerprint
+// matches (candidate position p, its text's group g) before the first empty slot -> 1; an empty slot first -> 0
+// (absent); neither (a full bucket) -> 2 (continue in the next bucket).
+__device__ __forceinline__ uint32_t ax_resolve(const u32x4& v0, const u32x4& v1, const u32x4& v2, const u32x4& v3,
+                                               uint32_t fp, uint32_t s, uint32_t& slot, uint32_t& p, uint32_t& g) {
+    const uint32_t pos[8] = {v0[0], v0[2], v1[0], v1[2], v2[0], v2[2], v3[0], v3[2]};
+    const uint32_t fg[8] = {v0[1], v0[3], v1[1], v1[3], v2[1], v2[3], v3[1], v3[3]};
+    uint32_t mm = 0, me = 0;
+#pragma unroll
+    for (int t = 0; t < 8; ++t) {
+        const bool empty = pos[t] == AX_EMPTY;
+        me |= (empty ? 1u : 0u) << t;
+        mm |= ((!empty && (fg[t] >> 16) == fp) ? 1u : 0u) << t;
+    }
+    const uint32_t from = s >= 8u ? 0u : ((0xFFu << s) & 0xFFu);
+    mm &= from;
+    me &= from;
+    const uint32_t fm = mm ? (uint32_t)__builtin_ctz(mm) : 8u, fe = me ? (uint32_t)__builtin_ctz(me) : 8u;
+    if (fm < fe) {
+        uint32_t pp = pos[0], gg = fg[0];
+#pragma unroll
+        for (int t = 1; t < 8; ++t) {
+            pp = fm == (uint32_t)t ? pos[t] : pp;
+            gg = fm == (uint32_t)t ? fg[t] : gg;
+        }
+        p = pp;
+        g = gg & 0xFFFFu;
+        slot = fm;
+        return 1u;
+    }
+    return fe < 8u ? 0u : 2u;
+}
+
+// One probe chain of the anchor table from bucket b, slot s (phase 2): stops at the first fingerprint match (found:
+// p, g, s) or at an empty slot (absent); the caller verifies the candidate and resumes at s + 1 after a collision.
 __device__ __forceinline__ bool ax_probe(const AxView& A, const __amdgpu_buffer_rsrc_t& rs_atab, uint32_t fp,
-                                         uint32_t& b, uint32_t& s, uint32_t& p, bool active) {
+                                         uint32_t& b, uint32_t& s, uint32_t& p, uint32_t& g, bool active,
+                                         uint32_t& probes) {
     bool found = false, pending = active;
     while (__ballot(pending) != 0) {
         const uint32_t boff = pending ? b * 64u : AX_OOB;
@@ -319,28 +391,14 @@ __device__ __forceinline__ bool ax_probe(const AxView& A, const __amdgpu_buffer_
         const u32x4 v2 = __builtin_amdgcn_raw_buffer_load_b128(rs_atab, boff + 32u, 0, 0);
         const u32x4 v3 = __builtin_amdgcn_raw_buffer_load_b128(rs_atab, boff + 48u, 0, 0);
         if (pending) {
-            const uint32_t fps[8] = {v0[0], v0[2], v1[0], v1[2], v2[0], v2[2], v3[0], v3[2]};
-            const uint32_t pos[8] = {v0[1], v0[3], v1[1], v1[3], v2[1], v2[3], v3[1], v3[3]};
-            uint32_t mm = 0, me = 0;
-#pragma unroll
-            for (int t = 0; t < 8; ++t) {
-                const bool empty = pos[t] == AX_EMPTY;
-                me |= (empty ? 1u : 0u) << t;
-                mm |= ((!empty && fps[t] == fp) ? 1u : 0u) << t;
-            }
-            const uint32_t from = s >= 8u ? 0u : ((0xFFu << s) & 0xFFu);
-            mm &= from;
-            me &= from;
-            const uint32_t fm = mm ? (uint32_t)__builtin_ctz(mm) : 8u, fe = me ? (uint32_t)__builtin_ctz(me) : 8u;
-            if (fm < fe) {
-                s = fm;
-                uint32_t pp = pos[0];
-#pragma unroll
-                for (int t = 1; t < 8; ++t) pp = fm == (uint32_t)t ? pos[t] : pp;
-                p = pp;
+            ++probes;
+            uint32_t slot = 0;
+            const uint32_t r = ax_resolve(v0, v1, v2, v3, fp, s, slot, p, g);
+            if (r == 1u) {
+                s = slot;
                 found = true;
                 pending = false;
-            } else if (fe < 8u) {
+            } else if (r == 0u) {
                 pending = false;  // absent
             } else {
                 b = (b + 1u == (uint32_t)A.nb) ? 0u : b + 1u;
@@ -360,11 +418,6 @@ constexpr uint32_t ax_wave_bytes() {
            8u * 64u + 128u;
 }
 
-#ifndef SPEQ_AX_PROBE  // timing probes (scripts/ax_probe.py A/B only; results are wrong): 1 staging only, 2 no phase 2,
-                       // 3 nothing but the read offsets, 4 no counter flush at the end,
-                       // 5 staging alone without its global loads, 6 staging alone without the counter flush
-#define SPEQ_AX_PROBE 0
-#endif
 #ifndef SPEQ_AX_WPB  // waves per workgroup of k_scan_ax (A/B knob)
 #define SPEQ_AX_WPB 4
 #endif
@@ -375,40 +428,29 @@ constexpr uint32_t AX_WPB = SPEQ_AX_WPB, AX_THREADS = 64 * SPEQ_AX_WPB;
 #ifndef SPEQ_AX_MIN_WAVES  // minimum waves per SIMD the register allocator must allow, k <= 33 (A/B knob)
 #define SPEQ_AX_MIN_WAVES 4
 #endif
-#ifndef SPEQ_AX_MIN_WAVES4  // the same for 34 <= k <= 65 (four compare words)
+#ifndef SPEQ_AX_MIN_WAVES4  // the same for 34 <= k <= 65
 #define SPEQ_AX_MIN_WAVES4 4
 #endif
-#ifndef SPEQ_AX_MIN_WAVES6  // and 66 <= k <= 128 (six words): 3 waves, 168 VGPRs without most spills, win 12 % at
-#define SPEQ_AX_MIN_WAVES6 3  // k = 70 and lose 17 % at k = 21 (profiles/r02/ax_variants_probes.jsonl)
+#ifndef SPEQ_AX_MIN_WAVES6  // and 66 <= k <= 128
+#define SPEQ_AX_MIN_WAVES6 4
 #endif
-// local (Phred-weighted) mode holds more live state than global mode: at 4 waves it spilled 54-60 registers per lane
-// (k <= 65); 3 waves (168 VGPRs, 36 / 8 spills) win 5 % at k = 21, 3 % at k = 31 and 28 % at k = 45 (0.1 % errors;
-// 9-34 % at 0.5 %), 2 waves lose (profiles/r02/ax_variants_local_waves.jsonl)
-#ifndef SPEQ_AX_MIN_WAVES_LOCAL  // local mode, k <= 33
+#ifndef SPEQ_AX_MIN_WAVES_LOCAL  // local (Phred-weighted) mode, every k
 #define SPEQ_AX_MIN_WAVES_LOCAL 3
 #endif
-#ifndef SPEQ_AX_MIN_WAVES4_LOCAL  // local mode, 34 <= k <= 65
-#define SPEQ_AX_MIN_WAVES4_LOCAL 3
-#endif
-#ifndef SPEQ_AX_MIN_WAVES6_LOCAL  // local mode, 66 <= k <= 128 (2 waves, no spills, lose 17-29 %:
-                                   // profiles/r02/ax_variants_local_k70_waves.jsonl)
-#define SPEQ_AX_MIN_WAVES6_LOCAL SPEQ_AX_MIN_WAVES6
-#endif
-#ifndef SPEQ_AX_MIN_WAVES_CW2  // two-byte classes (> 253 groups; 0 = as for one-byte classes): their run loop holds
-#define SPEQ_AX_MIN_WAVES_CW2 3   // twice the class registers and spilled 91-104 per lane at 4 waves; 3 waves win 30-33 %
-#endif                            // at k = 21 / 31 global, 300 groups (profiles/r02/ax_variants_cw2_waves.jsonl)
-template <int MODE, int NWC, int CW>
+template <int MODE, int NWC>
 constexpr int ax_min_waves() {
-    return (CW == 2 && SPEQ_AX_MIN_WAVES_CW2 > 0) ? SPEQ_AX_MIN_WAVES_CW2 : NWC >= 6 ? (MODE == KM_LOCAL ? SPEQ_AX_MIN_WAVES6_LOCAL : SPEQ_AX_MIN_WAVES6)
-                    : (NWC >= 4 ? (MODE == KM_LOCAL ? SPEQ_AX_MIN_WAVES4_LOCAL : SPEQ_AX_MIN_WAVES4)
-                                : (MODE == KM_LOCAL ? SPEQ_AX_MIN_WAVES_LOCAL : SPEQ_AX_MIN_WAVES));
+    return MODE == KM_LOCAL ? SPEQ_AX_MIN_WAVES_LOCAL
+                            : (NWC >= 6 ? SPEQ_AX_MIN_WAVES6 : (NWC >= 4 ? SPEQ_AX_MIN_WAVES4 : SPEQ_AX_MIN_WAVES));
 }
-template <int MODE, bool PAIRED, bool LDS_HIST, bool EM, int NWC, int CW>
-__global__ __launch_bounds__(AX_THREADS, (ax_min_waves<MODE, NWC, CW>())) void k_scan_ax(AxView A, UnitSrc src, unsigned long long* __restrict__ out_a,
-                                                           double* __restrict__ out_w) {
-    using C = AxCls<CW>;
-    constexpr uint32_t PER = C::PER;
-    constexpr uint32_t RUNW = AX_RUN / PER;  // class dwords of one run
+
+// NWC = 2-bit words covering the k - 1 + AX_RUN bases of one compare: 3 (k <= 33), 4 (k <= 65), 6 (k <= 128);
+// a run loads NG = NWC + 1 granules, a phase-2 verification NGV + 1 = NWC (the k bases at any offset in a granule).
+template <int MODE, bool PAIRED, bool LDS_HIST, bool EM, int NWC, bool STATS>
+__global__ __launch_bounds__(AX_THREADS, (ax_min_waves<MODE, NWC>())) void k_scan_ax(AxView A, UnitSrc src,
+                                                                                   unsigned long long* __restrict__ out_a,
+                                                                                   double* __restrict__ out_w) {
+    constexpr int NG = NWC + 1;
+    constexpr int NGV = NWC - 1;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -448,12 +490,10 @@ __global__ __launch_bounds__(AX_THREADS, (ax_min_waves<MODE, NWC, CW>())) void k
 
     // every table is read through a buffer descriptor: 16-B loads need only dword alignment, and a lane that has
     // nothing to load gets an out-of-range offset, which issues no memory request
-    const __amdgpu_buffer_rsrc_t rs_cls =
-        __builtin_amdgcn_make_buffer_rsrc((void*)A.cls, (short)0, (int)(uint32_t)A.cls_bytes, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rs_gran =
+        __builtin_amdgcn_make_buffer_rsrc((void*)A.gran, (short)0, (int)(uint32_t)A.gran_bytes, 0x00020000);
     const __amdgpu_buffer_rsrc_t rs_atab =
         __builtin_amdgcn_make_buffer_rsrc((void*)A.atab, (short)0, (int)(uint32_t)(A.nb * 64u), 0x00020000);
-    const __amdgpu_buffer_rsrc_t rs_t2 =
-        __builtin_amdgcn_make_buffer_rsrc((void*)A.t2, (short)0, (int)(uint32_t)A.t2_bytes, 0x00020000);
     const __amdgpu_buffer_rsrc_t rs_filt =
         __builtin_amdgcn_make_buffer_rsrc((void*)A.filt, (short)0, (int)(uint32_t)(A.nf * 8u), 0x00020000);
     const uint64_t NWV = (uint64_t)gridDim.x * AX_WPB;
@@ -467,6 +507,9 @@ __global__ __launch_bounds__(AX_THREADS, (ax_min_waves<MODE, NWC, CW>())) void k
     const uint32_t cmpb = k - 1u + AX_RUN;  // bases compared per iteration
 
     uint32_t t_cnt = 0, amb = 0;
+    // diagnostic counters (STATS only; wave-level ones are counted by lane 0)
+    uint32_t s_iter = 0, s_lk = 0, s_rn = 0, s_lkw = 0, s_rnw = 0, s_rwin = 0, s_def = 0, s_fp = 0, s_p2 = 0,
+             s_p2v = 0, s_ch = 0, s_seg = 0, s_qb = 0, s_tal = 0;
 
     auto add_count = [&](uint32_t g, uint32_t cnt, double wsum) {
         if (LDS_HIST) {
@@ -476,12 +519,6 @@ __global__ __launch_bounds__(AX_THREADS, (ax_min_waves<MODE, NWC, CW>())) void k
             atomicAdd(&gU[g], (unsigned long long)cnt);
             if (MODE == KM_LOCAL) atomicAdd(&out_w[g], wsum);
         }
-    };
-    // one class from a text position (phase 2)
-    auto load_class = [&](uint32_t p, bool act) -> uint32_t {
-        const uint32_t by = p * (uint32_t)CW;
-        const uint32_t v = __builtin_amdgcn_raw_buffer_load_b32(rs_cls, act ? (by & ~3u) : AX_OOB, 0, 0);
-        return (v >> (8u * (by & 3u))) & C::SENT;
     };
 
     for (uint64_t grp = gw; grp < n_groups; grp += NWV) {
@@ -505,9 +542,6 @@ __global__ __launch_bounds__(AX_THREADS, (ax_min_waves<MODE, NWC, CW>())) void k
         }
         int32_t af = -1, ad = 0;  // ambiguity state of this lane's read
         for (uint32_t seg = 0; seg < nseg_max; ++seg) {
-#if SPEQ_AX_PROBE == 3  // timing probe only (wrong results): read offsets, no staging
-            if (nseg_max > 0u) continue;
-#endif
             // ---- stage segment `seg` (windows [s, s + wend) of each lane's read, bases [s, s + sb)) as ONE stream
             // of 16-base chunks: lane o's chunks are [pre_o, pre_o + nch_o), so its base b sits at stream position
             // 16 pre_o + b (b counted from the chunk-aligned a16). The wave decodes the stream 64 chunks per
@@ -531,6 +565,10 @@ __global__ __launch_bounds__(AX_THREADS, (ax_min_waves<MODE, NWC, CW>())) void k
                 pre += __builtin_amdgcn_mbcnt_hi((uint32_t)(bb >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bb, 0u)) << b;
                 nch_tot += (uint32_t)__popcll(bb) << b;
             }
+            if (STATS) {
+                s_ch += nch;
+                s_seg += in_seg ? 1u : 0u;
+            }
             const uint32_t sbase = 16u * pre + off0;        // stream position of the segment's first base
             const uint64_t gofs = a16 - 16ull * pre;        // byte offset of stream chunk c in this lane's frame: + 16 c
             const uint32_t qt = 33u + src.cutoff;  // Phred+33 byte <= qt  <=>  clamp(q, 0, 41) <= cutoff (cutoff < 41)
@@ -548,13 +586,8 @@ __global__ __launch_bounds__(AX_THREADS, (ax_min_waves<MODE, NWC, CW>())) void k
                     for (uint32_t d = 32; d >= 1; d >>= 1)
                         o = ((uint32_t)__shfl((int)pre, (int)(o + d)) <= c) ? o + d : o;
                     const uint64_t go = (uint64_t)__shfl((long long)gofs, (int)o) + 16ull * c;
-#if SPEQ_AX_PROBE == 5  // timing probe only (wrong results): staging without the global loads
-                    sv[u] = make_uint4((uint32_t)go, (uint32_t)go * 3u, (uint32_t)go * 5u, (uint32_t)go * 7u);
-                    qv[u] = make_uint4(0x49494949u ^ (uint32_t)go, 0x49494949u, 0x49494949u, 0x49494949u);
-#else
                     sv[u] = *reinterpret_cast<const uint4*>(src.seq + go);
                     qv[u] = *reinterpret_cast<const uint4*>(src.qual + go);
-#endif
                 }
 #pragma unroll
                 for (uint32_t u = 0; u < SU; ++u) {
@@ -690,6 +723,7 @@ __global__ __launch_bounds__(AX_THREADS, (ax_min_waves<MODE, NWC, CW>())) void k
                     const double2 t = qtab[q];
                     x = div_rn(x, t.x, t.y);  // == x / t.x
                 }
+                if (STATS) s_qb += k;
                 return x;
             };
             // quality-change bits of the stream over positions [x, x + len) all zero (local mode)
@@ -706,19 +740,16 @@ __global__ __launch_bounds__(AX_THREADS, (ax_min_waves<MODE, NWC, CW>())) void k
                 return u;
             };
 
-#if SPEQ_AX_PROBE == 1 || SPEQ_AX_PROBE == 5 || SPEQ_AX_PROBE == 6  // timing probe only (wrong results): staging alone
-            if (wend > 0u) continue;
-#endif
             // ---- phase 1: one read per lane, one memory round trip per iteration: a lane either probes the anchor
             // table (its candidate is compared in the next iteration) or extends a run by up to AX_RUN windows
             uint32_t j = 0;
             uint32_t st = wend > 0 ? 0u : 2u;  // 0: look window j up, 1: extend from text position p, 2: done
             bool verify = false;       // st 1: p came from the anchor table (window j itself not compared yet)
-            uint64_t p = 0;
+            uint32_t p = 0;            // text position of window j (st 1)
+            uint32_t gt = 0;           // group of p's text (st 1)
             int32_t last_mm = -1;      // base (relative to the segment) of the last observed mismatch
             uint32_t pb = 0, ps = 0;   // probe position of the current lookup (bucket, first slot)
             bool resume = false;       // continue the current lookup at (pb, ps): full bucket, or failed verification
-            uint32_t gcur = C::NONE;   // the group of this read's last counted run (the fast path's guess)
             for (;;) {
                 if (st == 0u) {
                     j = next_valid(j);
@@ -726,73 +757,60 @@ __global__ __launch_bounds__(AX_THREADS, (ax_min_waves<MODE, NWC, CW>())) void k
                 }
                 if (__ballot(st != 2u) == 0) break;
                 const bool lk = st == 0u, rn = st == 1u;
+                const bool any_lk = __ballot(lk) != 0, any_rn = __ballot(rn) != 0;
+                if (STATS) {
+                    s_iter += lane == 0 ? 1u : 0u;
+                    s_lkw += (lane == 0 && any_lk) ? 1u : 0u;
+                    s_rnw += (lane == 0 && any_rn) ? 1u : 0u;
+                    s_lk += lk ? 1u : 0u;
+                    s_rn += rn ? 1u : 0u;
+                }
                 uint64_t ra[NWC];
                 read_words(sbase + j, ra);
-                const uint64_t h = ax_hash<NWC>(ra, k);
-                if (lk && !resume) {
-                    pb = ax_bucket(h, A.nb);
-                    ps = 0;
-                }
-                // ---- this iteration's loads: a bucket (lookup lanes), text words + classes (run lanes), the quality
+                // ---- this iteration's loads: a bucket (lookup lanes), the run's granules (run lanes), the quality
                 // of window j (local mode); a group is issued only when some lane of the wave needs it
                 u32x4 q0 = {0u, 0u, 0u, 0u}, q1 = q0, q2 = q0, q3 = q0;
-                if (__ballot(lk) != 0) {
+                uint32_t fp = 0;
+                if (any_lk) {
+                    const uint64_t h = ax_hash<NWC>(ra, k);
+                    fp = ax_fp(h);
+                    if (lk && !resume) {
+                        pb = ax_bucket(h, A.nb);
+                        ps = 0;
+                    }
                     const uint32_t boff = lk ? pb * 64u : AX_OOB;
                     q0 = __builtin_amdgcn_raw_buffer_load_b128(rs_atab, boff, 0, 0);
                     q1 = __builtin_amdgcn_raw_buffer_load_b128(rs_atab, boff + 16u, 0, 0);
                     q2 = __builtin_amdgcn_raw_buffer_load_b128(rs_atab, boff + 32u, 0, 0);
                     q3 = __builtin_amdgcn_raw_buffer_load_b128(rs_atab, boff + 48u, 0, 0);
                 }
-                uint64_t traw[NWC + 1];
-                uint32_t craw[RUNW + 1];
+                u32x4 gr[NG];
+#pragma unroll
+                for (int i = 0; i < NG; ++i) gr[i] = q0;
                 uint32_t qj = 0;
-                const bool any_rn = __ballot(rn) != 0;
                 if (any_rn) {
-                    const uint32_t toff = rn ? (uint32_t)((p >> 5) * 8u) : AX_OOB;
+                    const uint32_t goff = rn ? (p >> 5) * 16u : AX_OOB;
 #pragma unroll
-                    for (int i = 0; i <= NWC; ++i) {
-                        const u32x2 v = __builtin_amdgcn_raw_buffer_load_b64(rs_t2, toff + 8u * (uint32_t)i, 0, 0);
-                        traw[i] = (uint64_t)v[0] | ((uint64_t)v[1] << 32);
+                    for (int i = 0; i < NG; ++i)
+                        gr[i] = __builtin_amdgcn_raw_buffer_load_b128(rs_gran, goff + 16u * (uint32_t)i, 0, 0);
+                    if (MODE == KM_LOCAL) {
+                        qj = src.qual[a + (rn ? j : 0u)];
+                        if (STATS) s_qb += rn ? 1u : 0u;
                     }
-                    const uint32_t cby = (uint32_t)(p * (uint32_t)CW);
-                    const uint32_t coff = rn ? (cby & ~3u) : AX_OOB;
-#pragma unroll
-                    for (uint32_t c = 0; c < RUNW / 4; ++c) {
-                        const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rs_cls, coff + 16u * c, 0, 0);
-                        craw[4 * c] = v[0];
-                        craw[4 * c + 1] = v[1];
-                        craw[4 * c + 2] = v[2];
-                        craw[4 * c + 3] = v[3];
-                    }
-                    craw[RUNW] = __builtin_amdgcn_raw_buffer_load_b32(rs_cls, coff + 4u * RUNW, 0, 0);
-                    if (MODE == KM_LOCAL) qj = src.qual[a + (rn ? j : 0u)];
                 }
 
                 // ---- lookup lanes: resolve the bucket
                 if (lk) {
-                    const uint32_t fps[8] = {q0[0], q0[2], q1[0], q1[2], q2[0], q2[2], q3[0], q3[2]};
-                    const uint32_t pos[8] = {q0[1], q0[3], q1[1], q1[3], q2[1], q2[3], q3[1], q3[3]};
-                    uint32_t mm = 0, me = 0;
-#pragma unroll
-                    for (int t = 0; t < 8; ++t) {
-                        const bool empty = pos[t] == AX_EMPTY;
-                        me |= (empty ? 1u : 0u) << t;
-                        mm |= ((!empty && fps[t] == (uint32_t)h) ? 1u : 0u) << t;
-                    }
-                    const uint32_t from = ps >= 8u ? 0u : ((0xFFu << ps) & 0xFFu);
-                    mm &= from;
-                    me &= from;
-                    const uint32_t fm = mm ? (uint32_t)__builtin_ctz(mm) : 8u, fe = me ? (uint32_t)__builtin_ctz(me) : 8u;
-                    if (fm < fe) {  // candidate: compared with the text in the next iteration
-                        uint32_t pp = pos[0];
-#pragma unroll
-                        for (int t = 1; t < 8; ++t) pp = fm == (uint32_t)t ? pos[t] : pp;
-                        p = pp;
-                        ps = fm;
+                    uint32_t slot = 0, cp = 0, cg = 0;
+                    const uint32_t res = ax_resolve(q0, q1, q2, q3, fp, ps, slot, cp, cg);
+                    if (res == 1u) {  // candidate: compared with the text in the next iteration
+                        p = cp;
+                        gt = cg;
+                        ps = slot;
                         st = 1u;
                         verify = true;
                         resume = false;
-                    } else if (fe < 8u) {
+                    } else if (res == 0u) {
                         // absent: defer the windows that share the mismatch (or the next k - 1), skip past them
                         resume = false;
                         uint32_t dend = (last_mm >= (int32_t)j && last_mm < (int32_t)(j + k)) ? (uint32_t)last_mm
@@ -814,6 +832,7 @@ __global__ __launch_bounds__(AX_THREADS, (ax_min_waves<MODE, NWC, CW>())) void k
                                     defl[sl++] = (uint16_t)(lane | ((j + 1u + (uint32_t)__builtin_ctzll(t)) << 6));
                                 for (uint64_t t = dm1; t; t &= t - 1)
                                     defl[sl++] = (uint16_t)(lane | ((j + 65u + (uint32_t)__builtin_ctzll(t)) << 6));
+                                if (STATS) s_def += cnt;
                             } else {  // no room: the windows stay with this lane; void the slots reserved below the end
                                 for (uint32_t sl = slot0; sl < AX_DEF && sl < slot0 + cnt; ++sl) defl[sl] = AX_VOID;
                             }
@@ -829,11 +848,12 @@ __global__ __launch_bounds__(AX_THREADS, (ax_min_waves<MODE, NWC, CW>())) void k
 
                 // ---- run lanes: compare read [j, j + cmpb) with text [p, p + cmpb), classify the matched windows
                 if (any_rn && rn) {
-                    const uint32_t sh = 2u * (uint32_t)(p & 31u);
+                    const uint32_t s5 = p & 31u, sh = 2u * s5;
                     uint32_t e = cmpb;
 #pragma unroll
                     for (int i = NWC - 1; i >= 0; --i) {
-                        uint64_t x = ra[i] ^ funnel(traw[i], traw[i + 1], sh);
+                        const uint64_t tw = funnel(u64of(gr[i][0], gr[i][1]), u64of(gr[i + 1][0], gr[i + 1][1]), sh);
+                        uint64_t x = ra[i] ^ tw;
                         const uint32_t b0 = 32u * (uint32_t)i;
                         if (cmpb <= b0) x = 0;
                         else if (cmpb < b0 + 32u) x &= (1ull << (2u * (cmpb - b0))) - 1ull;
@@ -847,57 +867,32 @@ __global__ __launch_bounds__(AX_THREADS, (ax_min_waves<MODE, NWC, CW>())) void k
                         uint32_t R = e - (k - 1u);  // e >= k - 1: a candidate matched k bases, a run k - 1
                         R = min(R, AX_RUN);
                         R = min(R, wend - j);
-                        uint64_t m;
-                        {
-                            const uint32_t w0 = j >> 6, s6 = j & 63u;
-                            const uint64_t lo = vwl[w0 * 64u + lane];
-                            const uint64_t hi = w0 + 1u < AX_VWW ? vwl[(w0 + 1u) * 64u + lane] : 0ull;
-                            m = funnel(lo, hi, s6) & (R >= 64u ? ~0ull : ((1ull << R) - 1ull));
+                        const uint64_t mR = R >= 64u ? ~0ull : ((1ull << R) - 1ull);
+                        const uint64_t m = vbits(j) & mR;  // the run's valid read windows
+                        // class planes of windows p .. p + 63 (bits s5 .. s5 + 63 of three granules' planes)
+                        const uint64_t P0 = funnel(u64of(gr[0][2], gr[1][2]), (uint64_t)gr[2][2], s5);
+                        const uint64_t P1 = funnel(u64of(gr[0][3], gr[1][3]), (uint64_t)gr[2][3], s5);
+                        // the run stops at the first END window (the text ends: the next windows belong to another
+                        // text, looked up again) or SENT window of a valid read window (an N in the text: looked up)
+                        const uint64_t stop = P1 & (P0 | m) & mR;
+                        const uint32_t d0 = stop ? (uint32_t)__builtin_ctzll(stop) : R;
+                        const uint64_t mRc = d0 >= 64u ? ~0ull : ((1ull << d0) - 1ull);
+                        const uint64_t own = ~P0 & ~P1 & m & mRc;
+                        const uint32_t cnt = (uint32_t)__popcll(own);
+                        if (STATS) {
+                            s_rwin += d0;
+                            s_tal += cnt;
                         }
-                        // the run's classes, aligned so that window d is element d
-                        const uint32_t ca = (uint32_t)(p * (uint32_t)CW) & 3u;
-                        uint32_t cw[RUNW];
-#pragma unroll
-                        for (uint32_t i = 0; i < RUNW; ++i) cw[i] = __builtin_amdgcn_alignbyte(craw[i + 1], craw[i], ca);
-                        // One group per run: g = this read's group so far (else the run's first window's, when single).
-                        // A branch-free pass finds d0, the first valid window that is neither g nor multi-group
-                        // (another group, or SENT); windows [0, d0) are tallied at once and the run is cut at d0, which
-                        // starts the next iteration (with that group as g, or deferred when SENT).
-                        const uint32_t c0 = cw[0] & C::SENT;
-                        const uint32_t g = gcur != C::NONE ? gcur : (c0 < G ? c0 : C::NONE);
-                        const uint32_t gr = g * C::REP, mr = C::MULTI * C::REP;
-                        uint32_t cnt = 0, fo = RUNW, fflags = 0;
-                        uint64_t gm = 0, mm = 0;  // bit d: window d is g (local mode) / multi-group (EM)
-#pragma unroll
-                        for (uint32_t i = 0; i < RUNW; ++i) {
-                            const uint32_t vm = spread<CW>((uint32_t)(m >> (PER * i)) & ((1u << PER) - 1u));
-                            const uint32_t eg = zero_elems<CW>(cw[i] ^ gr) & vm;
-                            const uint32_t em = zero_elems<CW>(cw[i] ^ mr) & vm;
-                            const uint32_t ot = vm & ~(eg | em);
-                            const bool before = fo == RUNW;
-                            const uint32_t below = ot ? ((ot & (0u - ot)) - 1u) : ~0u;  // elements before the first other
-                            cnt += before ? (uint32_t)__popc(eg & below) : 0u;
-                            if (MODE == KM_LOCAL)
-                                gm |= (uint64_t)(CW == 1 ? flags4(eg) : (((eg >> 15) & 1u) | ((eg >> 30) & 2u))) << (PER * i);
-                            if (EM)
-                                mm |= (uint64_t)(CW == 1 ? flags4(em) : (((em >> 15) & 1u) | ((em >> 30) & 2u))) << (PER * i);
-                            fflags = (before && ot) ? ot : fflags;
-                            fo = (before && ot) ? i : fo;
-                        }
-                        const uint32_t d0 = fo == RUNW ? AX_RUN : PER * fo + (uint32_t)__builtin_ctz(fflags) / (8u * CW);
-                        const bool cut = d0 < R;
-                        const uint32_t Rc = cut ? d0 : R;  // windows tallied in this iteration
-                        const uint64_t mRc = Rc >= 64u ? ~0ull : ((1ull << Rc) - 1ull);
                         if (cnt) {
                             double wsum = 0.0;
                             if (MODE == KM_LOCAL) {
-                                // one quality for the whole cut run when no base in (j, j + Rc - 1 + k) changes it
-                                if (chg_zero(sbase + j + 1u, Rc + k - 2u)) {
+                                // one quality for the whole cut run when no base in (j, j + d0 - 1 + k) changes it
+                                if (chg_zero(sbase + j + 1u, d0 + k - 2u)) {
                                     int q = (int)qj - 33;
                                     q = q < 0 ? 0 : (q > 41 ? 41 : q);
                                     wsum = (double)cnt * wtab[q];
                                 } else {
-                                    uint64_t todo = gm & mRc;
+                                    uint64_t todo = own;
                                     while (todo) {
                                         const uint32_t d = (uint32_t)__builtin_ctzll(todo);
                                         todo &= todo - 1;
@@ -906,16 +901,16 @@ __global__ __launch_bounds__(AX_THREADS, (ax_min_waves<MODE, NWC, CW>())) void k
                                         int q = (int)qb[0] - 33;
                                         q = q < 0 ? 0 : (q > 41 ? 41 : q);
                                         wsum += weight(qb, chg_zero(sbase + jj + 1u, k - 1u), (uint32_t)q);
+                                        if (STATS) s_qb += 1u;
                                     }
                                 }
                             }
-                            add_count(g, cnt, wsum);
-                            if (af < 0) af = (int32_t)g;
-                            else if ((int32_t)g != af) ad = 1;
-                            gcur = g;
+                            add_count(gt, cnt, wsum);
+                            if (af < 0) af = (int32_t)gt;
+                            else if ((int32_t)gt != af) ad = 1;
                         }
-                        if (EM) {  // multi-group windows of the cut run: the EM histogram
-                            uint64_t todo = mm & mRc;
+                        if (EM) {  // multi-group windows of the run: the EM histogram
+                            uint64_t todo = P0 & ~P1 & m & mRc;
                             while (todo) {
                                 const uint32_t d = (uint32_t)__builtin_ctzll(todo);
                                 todo &= todo - 1;
@@ -925,34 +920,31 @@ __global__ __launch_bounds__(AX_THREADS, (ax_min_waves<MODE, NWC, CW>())) void k
                             }
                         }
                         // next state
-                        if (cut) {
-                            uint32_t x = cw[0];
-#pragma unroll
-                            for (uint32_t i = 1; i < RUNW; ++i) x = (fo == i) ? cw[i] : x;
-                            const uint32_t cl = (x >> (8u * CW * (d0 % PER))) & C::SENT;
-                            uint32_t adv = d0;
-                            if (cl == C::SENT) {  // matched bases, but no valid text window there: looked up later
-                                if (defer_push(lane, j + d0)) {
-                                    adv = d0 + 1u;
-                                    st = 1u;
-                                } else {
-                                    st = 0u;  // the list is full: look that window up now
-                                    last_mm = -1;
-                                }
-                            } else {
-                                gcur = cl;  // another group: the next iteration tallies from d0 with it
+                        verify = false;
+                        if (d0 < R) {
+                            if ((P0 >> d0) & 1ull) {  // END: look the window up (its k-mer may occur elsewhere)
+                                j += d0;
+                                st = 0u;
+                                resume = false;
+                                last_mm = -1;
+                            } else if (defer_push(lane, j + d0)) {  // SENT: matched bases, but no valid text window
+                                if (STATS) s_def += 1u;
+                                j += d0 + 1u;
+                                p += d0 + 1u;
                                 st = 1u;
+                            } else {  // the list is full: look that window up now
+                                j += d0;
+                                st = 0u;
+                                resume = false;
+                                last_mm = -1;
                             }
-                            j += adv;
-                            p += adv;
-                            verify = false;
                         } else {
                             const bool mism = e < cmpb;  // the run ended at a mismatch (base j + e)
                             if (mism && R < wend - j) last_mm = (int32_t)(j + e);
                             j += R;
                             p += R;
-                            verify = false;
                             st = (mism || R == 0u) ? 0u : 1u;
+                            if (st == 0u) resume = false;
                         }
                         if (j >= wend) st = 2u;
                     }
@@ -965,11 +957,7 @@ __global__ __launch_bounds__(AX_THREADS, (ax_min_waves<MODE, NWC, CW>())) void k
             ambf[lane] = af;
             ambd[lane] = ad;
             wave_sync();
-#if SPEQ_AX_PROBE == 2  // timing probe only (wrong results): no deferred windows
-            const uint32_t n2 = 0;
-#else
             const uint32_t n2 = min(__builtin_amdgcn_readfirstlane(defn[0]), AX_DEF);
-#endif
             for (uint32_t base = 0; base < n2; base += 64u * AX_F) {
                 uint32_t ent[AX_F];
                 uint64_t hh[AX_F];
@@ -1002,6 +990,7 @@ __global__ __launch_bounds__(AX_THREADS, (ax_min_waves<MODE, NWC, CW>())) void k
                 wave_sync();
             }
             const uint32_t n3 = __builtin_amdgcn_readfirstlane(defn[1]);
+            if (STATS) s_fp += lane == 0 ? n3 : 0u;
             for (uint32_t base = 0; base < n3; base += 64) {
                 const uint32_t idx = base + lane;
                 const bool act = idx < n3;
@@ -1011,33 +1000,31 @@ __global__ __launch_bounds__(AX_THREADS, (ax_min_waves<MODE, NWC, CW>())) void k
                 uint64_t ra[NWC];
                 read_words(sbo + jj, ra);
                 const uint64_t h = ax_hash<NWC>(ra, k);
-                uint32_t b = act ? ax_bucket(h, A.nb) : 0u, sl = 0, pp = 0;
+                const uint32_t fp = ax_fp(h);
+                uint32_t b = act ? ax_bucket(h, A.nb) : 0u, sl = 0, pp = 0, pg = 0;
                 bool pend = act, found = false;
-                uint32_t cl = C::SENT;
+                uint32_t cl = AX_SENT;
                 while (__ballot(pend) != 0) {
-                    const bool c = ax_probe(A, rs_atab, (uint32_t)h, b, sl, pp, pend);
+                    const bool c = ax_probe(A, rs_atab, fp, b, sl, pp, pg, pend, s_p2);
                     const bool cand = pend && c;
-                    uint64_t tw[NWC];
+                    if (STATS) s_p2v += cand ? 1u : 0u;
+                    u32x4 gv[NGV + 1];
                     {
-                        const uint32_t toff = cand ? (pp >> 5) * 8u : AX_OOB;
-                        uint64_t raw[NWC + 1];
+                        const uint32_t goff = cand ? (pp >> 5) * 16u : AX_OOB;
 #pragma unroll
-                        for (int i = 0; i <= NWC; ++i) {
-                            const u32x2 v = __builtin_amdgcn_raw_buffer_load_b64(rs_t2, toff + 8u * (uint32_t)i, 0, 0);
-                            raw[i] = (uint64_t)v[0] | ((uint64_t)v[1] << 32);
-                        }
-#pragma unroll
-                        for (int i = 0; i < NWC; ++i) tw[i] = funnel(raw[i], raw[i + 1], 2u * (pp & 31u));
+                        for (int i = 0; i <= NGV; ++i)
+                            gv[i] = __builtin_amdgcn_raw_buffer_load_b128(rs_gran, goff + 16u * (uint32_t)i, 0, 0);
                     }
-                    const uint32_t cc = load_class(pp, cand);
                     if (pend) {
                         if (!c) {
                             pend = false;  // absent
                         } else {
+                            const uint32_t s5 = pp & 31u;
                             bool eq = true;
 #pragma unroll
-                            for (int i = 0; i < NWC; ++i) {
-                                uint64_t x = ra[i] ^ tw[i];
+                            for (int i = 0; i < NGV; ++i) {
+                                uint64_t x = ra[i] ^ funnel(u64of(gv[i][0], gv[i][1]), u64of(gv[i + 1][0], gv[i + 1][1]),
+                                                            2u * s5);
                                 const uint32_t b0 = 32u * (uint32_t)i;
                                 if (k <= b0) x = 0;
                                 else if (k < b0 + 32u) x &= (1ull << (2u * (k - b0))) - 1ull;
@@ -1045,7 +1032,7 @@ __global__ __launch_bounds__(AX_THREADS, (ax_min_waves<MODE, NWC, CW>())) void k
                             }
                             if (eq) {
                                 found = true;
-                                cl = cc;
+                                cl = ((gv[0][2] >> s5) & 1u) | (((gv[0][3] >> s5) & 1u) << 1);
                                 pend = false;
                             } else {
                                 ++sl;  // fingerprint collision: keep probing
@@ -1053,7 +1040,7 @@ __global__ __launch_bounds__(AX_THREADS, (ax_min_waves<MODE, NWC, CW>())) void k
                         }
                     }
                 }
-                if (found && cl < G) {
+                if (found && cl == AX_OWN) {
                     double wgt = 0.0;
                     if (MODE == KM_LOCAL) {
                         const uint8_t* qb = src.qual + rbase[o] + jj;
@@ -1061,11 +1048,12 @@ __global__ __launch_bounds__(AX_THREADS, (ax_min_waves<MODE, NWC, CW>())) void k
                         int q = (int)qb[0] - 33;
                         q = q < 0 ? 0 : (q > 41 ? 41 : q);
                         wgt = weight(qb, uni, (uint32_t)q);
+                        if (STATS) s_qb += 1u;
                     }
-                    add_count(cl, 1u, wgt);
-                    const int32_t old = atomicCAS(&ambf[o], -1, (int32_t)cl);
-                    if (old != -1 && old != (int32_t)cl) ambd[o] = 1;
-                } else if (EM && found && cl == C::MULTI) {
+                    add_count(pg, 1u, wgt);
+                    const int32_t old = atomicCAS(&ambf[o], -1, (int32_t)pg);
+                    if (old != -1 && old != (int32_t)pg) ambd[o] = 1;
+                } else if (EM && found && cl == AX_MULTI) {
                     const uint32_t lo = A.mlo[pp];
                     atomicAdd(&src.em_mult[lo], 1u);
                     src.em_hi[lo] = A.mhi[lo];
@@ -1087,9 +1075,6 @@ __global__ __launch_bounds__(AX_THREADS, (ax_min_waves<MODE, NWC, CW>())) void k
         }
     }
 
-#if SPEQ_AX_PROBE == 4 || SPEQ_AX_PROBE == 6  // timing probe only (wrong results): no flush of the counters
-    if (t_cnt != 0xFFFFFFFFu) return;
-#endif
     // wave sums of the window and ambiguity counters through two LDS words (no shuffle address registers)
     if (lane == 0) {
         defn[2] = 0;
@@ -1104,6 +1089,13 @@ __global__ __launch_bounds__(AX_THREADS, (ax_min_waves<MODE, NWC, CW>())) void k
         if (tsum) atomicAdd(&out_a[0], tsum);
         if (asum) atomicAdd(&out_a[1], asum);
     }
+    if (STATS) {
+        const uint32_t sv[AXS_N] = {s_iter, s_lk, s_rn, s_lkw, s_rnw, s_rwin, s_def, s_fp, s_p2, s_p2v, s_ch, s_seg,
+                                    s_qb, s_tal};
+#pragma unroll
+        for (uint32_t i = 0; i < AXS_N; ++i)
+            if (sv[i]) atomicAdd(&A.stats[i], (unsigned long long)sv[i]);
+    }
     if (LDS_HIST) {
         __syncthreads();
         for (uint32_t g = threadIdx.x; g < G; g += AX_THREADS) {
@@ -1117,38 +1109,39 @@ __global__ __launch_bounds__(AX_THREADS, (ax_min_waves<MODE, NWC, CW>())) void k
     }
 }
 
-template <int MODE, bool PAIRED, bool LDS, bool EM, int NWC, int CW>
+template <int MODE, bool PAIRED, bool LDS, bool EM, int NWC, bool STATS>
 void ax_launch_one(const AxView& A, const UnitSrc& src, uint32_t grid, size_t lds, hipStream_t st,
                    unsigned long long* a, double* w) {
     if (lds > 64 * 1024)  // dynamic LDS above 64 KiB must be allowed (occupancy caps pad it)
-        HIP_OK(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_scan_ax<MODE, PAIRED, LDS, EM, NWC, CW>),
+        HIP_OK(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_scan_ax<MODE, PAIRED, LDS, EM, NWC, STATS>),
                                    hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-    hipLaunchKernelGGL((k_scan_ax<MODE, PAIRED, LDS, EM, NWC, CW>), dim3(grid), dim3(AX_THREADS), lds, st, A, src, a,
-                       w);
+    hipLaunchKernelGGL((k_scan_ax<MODE, PAIRED, LDS, EM, NWC, STATS>), dim3(grid), dim3(AX_THREADS), lds, st, A, src,
+                       a, w);
 }
 
-// NWC = words covering the k - 1 + AX_RUN bases of one compare: 3 (k <= 33), 4 (k <= 65), 6 (k <= 128)
-template <int MODE, bool PAIRED, bool LDS, bool EM, int CW>
+// NWC by k: 3 (k <= 33), 4 (k <= 65), 6 (k <= 128)
+template <int MODE, bool PAIRED, bool LDS, bool EM, bool STATS>
 void ax_launch_nwc(uint32_t k, const AxView& A, const UnitSrc& src, uint32_t grid, size_t lds, hipStream_t st,
                    unsigned long long* a, double* w) {
-    if (k <= 33) ax_launch_one<MODE, PAIRED, LDS, EM, 3, CW>(A, src, grid, lds, st, a, w);
-    else if (k <= 65) ax_launch_one<MODE, PAIRED, LDS, EM, 4, CW>(A, src, grid, lds, st, a, w);
-    else ax_launch_one<MODE, PAIRED, LDS, EM, 6, CW>(A, src, grid, lds, st, a, w);
+    if (k <= 33) ax_launch_one<MODE, PAIRED, LDS, EM, 3, STATS>(A, src, grid, lds, st, a, w);
+    else if (k <= 65) ax_launch_one<MODE, PAIRED, LDS, EM, 4, STATS>(A, src, grid, lds, st, a, w);
+    else ax_launch_one<MODE, PAIRED, LDS, EM, 6, STATS>(A, src, grid, lds, st, a, w);
 }
 
 template <int MODE, bool PAIRED>
-void ax_launch_mode(uint32_t cw, bool lds_hist, uint32_t k, const AxView& A, const UnitSrc& src, uint32_t grid,
-                    size_t lds, hipStream_t st, unsigned long long* a, double* w) {
+void ax_launch_mode(bool lds_hist, uint32_t k, const AxView& A, const UnitSrc& src, uint32_t grid, size_t lds,
+                    hipStream_t st, unsigned long long* a, double* w) {
     const bool em = src.em_mult != nullptr;
-    if (cw == 1) {  // <= 253 groups: always the LDS histogram
-        if (em) ax_launch_nwc<MODE, PAIRED, true, true, 1>(k, A, src, grid, lds, st, a, w);
-        else ax_launch_nwc<MODE, PAIRED, true, false, 1>(k, A, src, grid, lds, st, a, w);
-    } else if (lds_hist) {
-        if (em) ax_launch_nwc<MODE, PAIRED, true, true, 2>(k, A, src, grid, lds, st, a, w);
-        else ax_launch_nwc<MODE, PAIRED, true, false, 2>(k, A, src, grid, lds, st, a, w);
+    if (A.stats != nullptr && lds_hist && !em) {
+        ax_launch_nwc<MODE, PAIRED, true, false, true>(k, A, src, grid, lds, st, a, w);
+        return;
+    }
+    if (lds_hist) {
+        if (em) ax_launch_nwc<MODE, PAIRED, true, true, false>(k, A, src, grid, lds, st, a, w);
+        else ax_launch_nwc<MODE, PAIRED, true, false, false>(k, A, src, grid, lds, st, a, w);
     } else {
-        if (em) ax_launch_nwc<MODE, PAIRED, false, true, 2>(k, A, src, grid, lds, st, a, w);
-        else ax_launch_nwc<MODE, PAIRED, false, false, 2>(k, A, src, grid, lds, st, a, w);
+        if (em) ax_launch_nwc<MODE, PAIRED, false, true, false>(k, A, src, grid, lds, st, a, w);
+        else ax_launch_nwc<MODE, PAIRED, false, false, false>(k, A, src, grid, lds, st, a, w);
     }
 }
 
@@ -1157,29 +1150,36 @@ void ax_launch_mode(uint32_t cw, bool lds_hist, uint32_t k, const AxView& A, con
 namespace speq {
 
 // Builds the per-k anchor structures of replica d (blocking, on its stream). Returns a table with ok == false when
-// k, the group count or the index is outside what the scan supports, or the structures would not fit the free HBM.
+// k, the group count or the index is outside what the scan supports (a structural limit: `transient` false), or
+// the structures would not fit the free HBM at this moment (`transient` true: ensure_ax tries again next time).
 AxTable build_ax(speq_device_index* d, uint32_t k) {
     DeviceGuard g(d->device);
     const auto t0 = std::chrono::steady_clock::now();
     AxTable ax;
     const uint64_t n = d->view.n;
-    if (k < 1 || k > AX_MAX_K || n >= (1ull << 30) || d->G > AxCls<2>::MAX_G) return ax;
-    ax.cw = d->G <= AxCls<1>::MAX_G ? 1u : 2u;
+    if (k < 1 || k > AX_MAX_K || n >= (1ull << 30) || d->G > AX_MAX_G) return ax;
     const uint64_t nw64 = (n + 63) / 64 + 4;
-    const uint64_t cls_bytes = ((n + 512) * ax.cw + 15) & ~15ull;
+    const uint64_t n_gran = (n + 255) / 32 + 2;  // a run from any p < n reads NG <= 7 granules: padded with END
+    const uint64_t gran_bytes = n_gran * 16;
     size_t free_b = 0, total_b = 0;
     HIP_OK(hipMemGetInfo(&free_b, &total_b));
-    // cls, mlo, mhi, owner, text2 + tbad, table + filter (bounds)
-    const uint64_t need = cls_bytes + (n + 64) * 4 * 3 + nw64 * 24 + n * 12;
-    if (need > free_b / 10 * 9) return ax;
+    // gran, codes, mlo, mhi, owner, text2 + tbad, table + filter (bounds)
+    const uint64_t need = gran_bytes + n + (n + 64) * 4 * 3 + nw64 * 24 + n * 12;
+    if (need > free_b / 10 * 9) {
+        ax.transient = true;
+        return ax;
+    }
     uint32_t* owner = nullptr;
+    uint8_t* codes = nullptr;
     unsigned long long* d_cnt = nullptr;
     std::vector<void*> mine;  // this table's allocations (tracked by the replica once the table is complete)
     auto cleanup = [&] {
         (void)hipStreamSynchronize(d->stream);
         if (owner) (void)hipFree(owner);
+        if (codes) (void)hipFree(codes);
         if (d_cnt) (void)hipFree(d_cnt);
         owner = nullptr;
+        codes = nullptr;
         d_cnt = nullptr;
     };
     auto alloc = [&](void** pp, uint64_t bytes) {
@@ -1197,22 +1197,22 @@ AxTable build_ax(speq_device_index* d, uint32_t k) {
                                nw64);
             HIP_OK(hipGetLastError());
         }
-        alloc(&ax.cls, cls_bytes);
+        alloc(&ax.gran, gran_bytes);
         alloc(reinterpret_cast<void**>(&ax.mlo), (n + 64) * 4);
         alloc(reinterpret_cast<void**>(&ax.mhi), (n + 64) * 4);
         HIP_OK(hipMalloc(&owner, (n + 1) * 4));
+        HIP_OK(hipMalloc(&codes, n + 64));
         HIP_OK(hipMalloc(&d_cnt, 8));
-        HIP_OK(hipMemsetAsync(ax.cls, 0xFF, cls_bytes, d->stream));
         HIP_OK(hipMemsetAsync(owner, 0xFF, (n + 1) * 4, d->stream));
         HIP_OK(hipMemsetAsync(d_cnt, 0, 8, d->stream));
         const DevView v = search_view(d, k);
         const uint32_t grid = (uint32_t)std::min<uint64_t>((n + 255) / 256, 16384);
-        if (ax.cw == 1)
-            hipLaunchKernelGGL(k_ax_classify<1>, dim3(grid), dim3(256), 0, d->stream, v, d->d_text, d->d_tbad, n, k,
-                               ax.cls, ax.mlo, ax.mhi, owner, d_cnt);
-        else
-            hipLaunchKernelGGL(k_ax_classify<2>, dim3(grid), dim3(256), 0, d->stream, v, d->d_text, d->d_tbad, n, k,
-                               ax.cls, ax.mlo, ax.mhi, owner, d_cnt);
+        hipLaunchKernelGGL(k_ax_classify, dim3(grid), dim3(256), 0, d->stream, v, d->d_text, d->d_tbad, n, k, codes,
+                           ax.mlo, ax.mhi, owner, d_cnt);
+        HIP_OK(hipGetLastError());
+        const uint32_t pgrid = (uint32_t)std::min<uint64_t>((n_gran + 255) / 256, 16384);
+        hipLaunchKernelGGL(k_ax_pack, dim3(pgrid), dim3(256), 0, d->stream, d->d_text2, 2 * nw64, codes, n,
+                           reinterpret_cast<u32x4*>(ax.gran), n_gran);
         HIP_OK(hipGetLastError());
         unsigned long long distinct = 0;
         HIP_OK(hipMemcpyAsync(&distinct, d_cnt, 8, hipMemcpyDeviceToHost, d->stream));
@@ -1230,13 +1230,13 @@ AxTable build_ax(speq_device_index* d, uint32_t k) {
         alloc(&ax.filt, ax.nf * 8);
         HIP_OK(hipMemsetAsync(ax.atab, 0xFF, ax.nb * 64, d->stream));
         HIP_OK(hipMemsetAsync(ax.filt, 0, ax.nf * 8, d->stream));
-        hipLaunchKernelGGL(k_ax_insert, dim3(grid), dim3(256), 0, d->stream, owner, n, d->d_text2, k,
-                           reinterpret_cast<unsigned long long*>(ax.atab), ax.nb,
+        hipLaunchKernelGGL(k_ax_insert, dim3(grid), dim3(256), 0, d->stream, owner, n, d->d_text2, k, d->d_text_start,
+                           d->d_text_group, d->n_texts, reinterpret_cast<unsigned long long*>(ax.atab), ax.nb,
                            reinterpret_cast<unsigned long long*>(ax.filt), ax.nf);
         HIP_OK(hipGetLastError());
         HIP_OK(hipStreamSynchronize(d->stream));
-        ax.cls_bytes = cls_bytes;
-        ax.bytes = ax.nb * 64 + ax.nf * 8 + cls_bytes + (n + 64) * 8;
+        ax.gran_bytes = gran_bytes;
+        ax.bytes = ax.nb * 64 + ax.nf * 8 + gran_bytes + (n + 64) * 8;
         ax.ok = true;
     } catch (...) {
         cleanup();
@@ -1253,28 +1253,32 @@ const AxTable* ensure_ax(speq_device_index* d, uint32_t k) {
     if (!d->ax_scan || k < 1 || k > AX_MAX_K) return nullptr;
     std::lock_guard<std::mutex> lk(d->ax_mu);
     auto it = d->axtabs.find(k);
+    if (it != d->axtabs.end() && !it->second.ok && it->second.transient) {
+        d->axtabs.erase(it);  // it did not fit the free HBM last time: try again
+        it = d->axtabs.end();
+    }
     if (it == d->axtabs.end()) it = d->axtabs.emplace(k, build_ax(d, k)).first;
     return it->second.ok ? &it->second : nullptr;
 }
 
 // Launches k_scan_ax for a read scan (mode 0 global, 1 local) when replica d has (or can build) the structures of
-// src.k; returns false when the caller must use another kernel.
+// src.k; returns false when the caller must use another kernel. With d->ax_stats set, the diagnostic instantiation
+// also adds its work counters there.
 bool launch_ax(speq_device_index* d, int mode, bool paired, const UnitSrc& src, hipStream_t st, unsigned long long* a,
                double* w) {
     const AxTable* ax = ensure_ax(d, src.k);
     if (!ax) return false;
     AxView A;
-    A.t2 = d->d_text2;
-    A.cls = ax->cls;
+    A.gran = reinterpret_cast<const u32x4*>(ax->gran);
     A.mlo = ax->mlo;
     A.mhi = ax->mhi;
     A.atab = reinterpret_cast<const unsigned long long*>(ax->atab);
     A.filt = reinterpret_cast<const unsigned long long*>(ax->filt);
+    A.stats = d->ax_stats;
     A.nb = ax->nb;
     A.nf = ax->nf;
     A.n = d->view.n;
-    A.t2_bytes = ((d->view.n + 63) / 64 + 4) * 16;
-    A.cls_bytes = ax->cls_bytes;
+    A.gran_bytes = ax->gran_bytes;
     A.G = d->G;
     const bool lds_hist = d->G <= LDS_HIST_MAX_G;
     const uint32_t hist_words = lds_hist ? (mode == KM_GLOBAL ? d->G : 2u * d->G) : 0u;
@@ -1290,11 +1294,11 @@ bool launch_ax(speq_device_index* d, int mode, bool paired, const UnitSrc& src, 
     }
     const uint32_t grid = (uint32_t)blocks;
     if (mode == KM_GLOBAL) {
-        if (paired) ax_launch_mode<KM_GLOBAL, true>(ax->cw, lds_hist, src.k, A, src, grid, lds_launch, st, a, w);
-        else ax_launch_mode<KM_GLOBAL, false>(ax->cw, lds_hist, src.k, A, src, grid, lds_launch, st, a, w);
+        if (paired) ax_launch_mode<KM_GLOBAL, true>(lds_hist, src.k, A, src, grid, lds_launch, st, a, w);
+        else ax_launch_mode<KM_GLOBAL, false>(lds_hist, src.k, A, src, grid, lds_launch, st, a, w);
     } else {
-        if (paired) ax_launch_mode<KM_LOCAL, true>(ax->cw, lds_hist, src.k, A, src, grid, lds_launch, st, a, w);
-        else ax_launch_mode<KM_LOCAL, false>(ax->cw, lds_hist, src.k, A, src, grid, lds_launch, st, a, w);
+        if (paired) ax_launch_mode<KM_LOCAL, true>(lds_hist, src.k, A, src, grid, lds_launch, st, a, w);
+        else ax_launch_mode<KM_LOCAL, false>(lds_hist, src.k, A, src, grid, lds_launch, st, a, w);
     }
     HIP_OK(hipGetLastError());
     return true;

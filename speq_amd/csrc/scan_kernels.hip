@@ -1684,6 +1684,36 @@ int speq_scan_reads_device(speq_device_index* d, const uint8_t* d_seq, const uin
     });
 }
 
+int speq_scan_reads_device_stats(speq_device_index* d, const uint8_t* d_seq, const uint8_t* d_qual,
+                                 const uint64_t* d_offsets, uint64_t n_reads, const speq_scan_params* p,
+                                 uint64_t* d_counts, double* d_weights, uint64_t* stats) {
+    return speq::guarded([&] {
+        if (!d || !stats) throw std::invalid_argument("speq_scan_reads_device_stats: null argument");
+        DeviceGuard g(d->device);
+        static std::mutex mu;  // one instrumented launch at a time (the replica's ax_stats is a single slot)
+        std::lock_guard<std::mutex> lk(mu);
+        unsigned long long* ds = nullptr;
+        HIP_OK(hipMalloc(&ds, SPEQ_AX_STATS_N * 8));
+        struct Release {
+            speq_device_index* d;
+            unsigned long long*& p;
+            ~Release() {
+                d->ax_stats = nullptr;
+                if (p) (void)hipFree(p);
+            }
+        } release{d, ds};
+        HIP_OK(hipMemsetAsync(ds, 0, SPEQ_AX_STATS_N * 8, d->stream));
+        HIP_OK(hipStreamSynchronize(d->stream));
+        d->ax_stats = ds;
+        scan_device_impl(d, d_seq, d_qual, d_offsets, n_reads, p, d_counts, d_weights, nullptr, nullptr, d->stream);
+        d->ax_stats = nullptr;
+        if (d->last_kernel != 3)
+            throw std::invalid_argument("speq_scan_reads_device_stats: the scan did not use the anchor-and-extend kernel");
+        HIP_OK(hipStreamSynchronize(d->stream));
+        HIP_OK(hipMemcpy(stats, ds, SPEQ_AX_STATS_N * 8, hipMemcpyDeviceToHost));
+    });
+}
+
 int speq_scan_reads(speq_device_index* d, const uint8_t* seq, const uint8_t* qual, const uint64_t* offsets,
                     uint64_t n_reads, const speq_scan_params* p, uint64_t* counts, double* weights) {
     return speq::guarded([&] { speq::scan_host_pipelined(d, seq, qual, offsets, n_reads, p, nullptr, counts, weights); });
@@ -1703,6 +1733,9 @@ int speq_em_create(const speq_index* idx, speq_device_index* d, speq_em** out) {
         HIP_OK(hipMalloc(&em->d_mult, em->n * 4));
         HIP_OK(hipMalloc(&em->d_hi, em->n * 4));
         HIP_OK(hipMemset(em->d_mult, 0, em->n * 4));
+        // interval ends are merged across ranks / replicas with a max (speq_em_allreduce, k_em_merge): a position this
+        // replica never wrote must hold 0, not whatever the allocation held
+        HIP_OK(hipMemset(em->d_hi, 0, em->n * 4));
         *out = em.release();
     });
 }
@@ -2099,6 +2132,7 @@ void em_clear(speq_em* em) {
     if (em->finalized) throw std::logic_error("speq: EM histogram already finalized");
     DeviceGuard g(em->dev->device);
     HIP_OK(hipMemset(em->d_mult, 0, em->n * 4));
+    HIP_OK(hipMemset(em->d_hi, 0, em->n * 4));
 }
 }  // namespace speq
 

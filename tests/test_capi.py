@@ -4,7 +4,7 @@ import re
 import subprocess
 
 from speq_amd import lib
-from speq_amd._lib import LIB_PATH, SIGNATURES
+from speq_amd._lib import ABI_VERSION, LIB_PATH, SIGNATURES
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
@@ -34,7 +34,7 @@ def test_python_binding_covers_header():
     L = lib()
     for name in declared():
         assert hasattr(L, name)
-    assert L.speq_abi_version() == 6
+    assert L.speq_abi_version() == ABI_VERSION
 
 
 def test_device_count_never_fails():

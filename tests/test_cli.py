@@ -196,9 +196,10 @@ def test_scan_sharded_over_replicas_matches_one_gpu(tmp_path, paired):
 @pytest.mark.parametrize("paired", [False, True])
 def test_scan_one_process_per_gpu_matches_one_process(tmp_path, paired):
     """`torchrun --no-python bin/speq scan ...` with WORLD_SIZE = 2: each rank scans its share of the FASTQ blocks
-    and of the .dat windows on GPU $LOCAL_RANK and the counters, weights, .dat sums and EM histograms are summed with
-    RCCL (speq_allreduce_host / speq_em_allreduce); rank 0 prints and writes exactly what one process prints. With
-    one visible GPU both ranks use GPU 0 (--device 0); if RCCL refuses two ranks on one GPU the test is skipped."""
+    and of the .dat windows on GPU $LOCAL_RANK and the counters, weights, .dat sums and EM histograms are summed
+    (speq_allreduce_host / speq_em_allreduce); rank 0 prints and writes exactly what one process prints. With one
+    visible GPU both ranks use GPU 0 (--device 0) and speq_comm_connect picks the host-socket transport (RCCL refuses
+    two ranks on one GPU); with two or more GPUs the ranks use RCCL."""
     import socket
     import sys
     from speq_amd import synth
@@ -231,9 +232,6 @@ def test_scan_one_process_per_gpu_matches_one_process(tmp_path, paired):
                           "--master-addr", "127.0.0.1", "--master-port", str(port), "--no-python", SPEQ] + base +
                          extra + ["-o", "two.txt", "-f"], cwd=tmp_path, capture_output=True, text=True, timeout=300,
                          env=env)
-    if two.returncode != 0 and not extra == [] and ("Duplicate GPU" in two.stderr or "ncclCommInitRank" in two.stderr
-                                                    or "joining the RCCL communicator" in two.stderr):
-        pytest.skip("RCCL refuses two ranks on one GPU: " + two.stderr[-300:])
     assert two.returncode == 0, two.stderr[-3000:]
     assert (tmp_path / "two.txt").read_text() == (tmp_path / "one.txt").read_text()
     for line in one.stderr.splitlines():  # every result line of the one-process run, once, from rank 0

@@ -77,3 +77,66 @@ def test_read_stream_is_shardable():
     ab = synth.make_reads(ref, 200)
     assert np.array_equal(np.concatenate([a.seq, b.seq]), ab.seq)
     assert np.array_equal(np.concatenate([a.qual, b.qual]), ab.qual)
+
+
+# ---- the product's own host-socket transport (speq_comm_connect, SPEQ_COMM_HOST): no GPU needed ----
+
+def _host_rank(rank, world, path, out, errs):
+    from speq_amd import Comm
+    try:
+        c = Comm.connect(world, rank, path, device=-1, transport=Comm.HOST, timeout_s=60)
+        assert c.transport == Comm.HOST
+        u = np.arange(5, dtype=np.uint64) * np.uint64(rank + 1)
+        f = np.array([0.1 * (rank + 1), 1e300, -2.5], dtype=np.float64)
+        c.allreduce_host(u)
+        c.allreduce_host(f)
+        out[rank] = (u.copy(), f.copy())
+        c.close()
+    except Exception as e:  # noqa: BLE001 - reported by the test thread
+        errs.append((rank, repr(e)))
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_host_transport_allreduce(tmp_path, world):
+    """speq_comm_connect over loopback sockets: every rank ends with the same sums, f64 added in rank order."""
+    import threading
+    path = str(tmp_path / "rdzv")
+    out, errs = {}, []
+    ts = [threading.Thread(target=_host_rank, args=(r, world, path, out, errs)) for r in range(world)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(120)
+    assert not errs, errs
+    su = sum(np.arange(5, dtype=np.uint64) * np.uint64(r + 1) for r in range(world))
+    fsum = np.array([0.1, 1e300, -2.5])
+    for r in range(1, world):
+        fsum = fsum + np.array([0.1 * (r + 1), 1e300, -2.5])
+    for r in range(world):
+        assert np.array_equal(out[r][0], su)
+        assert np.array_equal(out[r][1], fsum)  # bit-identical: rank 0 adds in rank order
+    assert not os.path.exists(path), "rank 0 removes the rendezvous file once every rank has joined"
+
+
+def test_host_transport_skips_a_stale_rendezvous(tmp_path):
+    """A rendezvous file left by a dead run (its port refuses) is skipped until rank 0 publishes a live one."""
+    import struct
+    import threading
+    import time
+    path = str(tmp_path / "rdzv")
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    dead_port = s.getsockname()[1]
+    s.close()
+    with open(path, "wb") as f:  # {magic "SPEQRDZ1", nonce, port}
+        f.write(struct.pack("<QQQ", 0x5350455152445A31, 12345, dead_port))
+    out, errs = {}, []
+    t1 = threading.Thread(target=_host_rank, args=(1, 2, path, out, errs))
+    t1.start()
+    time.sleep(0.5)  # rank 1 meets the stale file first
+    t0 = threading.Thread(target=_host_rank, args=(0, 2, path, out, errs))
+    t0.start()
+    t0.join(120)
+    t1.join(120)
+    assert not errs, errs
+    assert np.array_equal(out[0][0], out[1][0])

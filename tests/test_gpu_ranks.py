@@ -107,3 +107,50 @@ def test_em_histograms_of_shards_and_rccl_single_rank(setup):
     pct = np.linspace(5.0, 30.0, 6)
     cnt = [2] * 6
     np.testing.assert_allclose(merged.step(pct, cnt, U), em_all.step(pct, cnt, whole.unique), rtol=1e-12)
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_em_allreduce_over_host_transport(setup, tmp_path, world):
+    """The product's rank exchange with ranks sharing one GPU (speq_comm_connect picks host sockets): each rank
+    (a thread here) scans its FASTQ shard into its own histogram, speq_em_allreduce sums multiplicities and takes
+    the max of interval ends; positions a rank never wrote hold 0 (speq_em_create zeroes them, advisor finding), so
+    every rank ends with the one-scan histogram, and the counters summed by speq_allreduce_host equal one scan's."""
+    import threading
+    d, ref, dev = setup
+    p = str(d / "r.fq")
+    em_all = EmHistogram(dev)
+    whole, _ = dev.scan_fastq(p, k=21, em=em_all, threads=4)
+    em_all.finalize()
+    path = str(tmp_path / "rdzv")
+    res, errs = {}, []
+
+    def rank(r):
+        try:
+            c = Comm.connect(world, r, path, device=0, transport=Comm.AUTO, timeout_s=120)
+            assert c.transport == Comm.HOST  # every rank on GPU 0
+            em = EmHistogram(dev)
+            part, _ = dev.scan_fastq_shard(p, None, 21, r, world, cut=1, em=em)
+            counts = np.concatenate([[part.total, part.ambiguous], part.unique]).astype(np.uint64)
+            c.allreduce_host(counts, device=0)
+            em.allreduce(c)
+            c.close()
+            em.finalize()
+            pct = np.linspace(5.0, 30.0, 6)
+            res[r] = (counts, em.info(), em.step(pct, [2] * 6, counts[2:]))
+            em.close()
+        except Exception as e:  # noqa: BLE001 - reported below
+            errs.append((r, repr(e)))
+
+    ts = [threading.Thread(target=rank, args=(r,)) for r in range(world)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(300)
+    assert not errs, errs
+    pct = np.linspace(5.0, 30.0, 6)
+    ref_step = em_all.step(pct, [2] * 6, whole.unique)
+    for r in range(world):
+        counts, info, step = res[r]
+        assert counts.tolist() == [whole.total, whole.ambiguous] + whole.unique.tolist()
+        assert info == em_all.info()
+        np.testing.assert_allclose(step, ref_step, rtol=1e-12)
