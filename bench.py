@@ -124,17 +124,17 @@ def ax_request_bytes(st: dict, k: int, n_reads: int, local: bool) -> dict:
     """Bytes k_scan_ax REQUESTS per launch, from the work counters of its instrumented twin (speq_scan_reads_device_stats,
     same scan, same results): every load the kernel issues, by kind, at the size it issues it (ax_scan.hip):
       read offsets 8 B per read; staging 16 B of bases + 16 B of qualities per 16-base chunk;
-      anchor buckets 64 B per lookup (phase 1 and phase 2); run granules NG = NWC + 1 x 16 B per run iteration;
-      Bloom-filter words 8 B per deferred window; candidate granules NWC x 16 B per phase-2 verification;
+      anchor buckets 64 B per lookup (phase 1 and phase 2); run granules 16 B each (counted);
+      Bloom-filter words 8 B per deferred window; candidate granules ceil(k/32) + 1 x 16 B per phase-2 verification;
       local mode: single quality bytes."""
-    nwc = 3 if k <= 33 else (4 if k <= 65 else 6)
+    hw = (k + 31) // 32
     parts = {
         "offsets": 8.0 * n_reads,
         "staging": 32.0 * st["chunks"],
         "anchor_buckets": 64.0 * (st["lookup_lanes"] + st["p2_probes"]),
-        "run_granules": 16.0 * (nwc + 1) * st["run_lanes"],
+        "run_granules": 16.0 * st["run_granules"],
         "filter": 8.0 * st["deferred"],
-        "verify_granules": 16.0 * nwc * st["p2_verify"],
+        "verify_granules": 16.0 * (hw + 1) * st["p2_verify"],
         "quality_bytes": float(st["qual_bytes"]) if local else 0.0,
     }
     return {"total": sum(parts.values()), "parts": parts}
@@ -288,7 +288,7 @@ def run_workload(ctx: Ctx, cfg_no: int, k: int, n_reads: int, mode: str, steps: 
     value = total_kmers / elapsed
     avg_kernel_s = (kernel_ms / 1e3) / max(1, launches)
     ax_stats = None
-    if hot_kernel == 3:
+    if hot_kernel == 3 and not os.environ.get("SPEQ_BENCH_NO_STATS"):
         # one untimed launch of the instrumented twin: the same scan (checked equal), plus its work counters
         d_counts.zero_()
         if local:
@@ -301,8 +301,11 @@ def run_workload(ctx: Ctx, cfg_no: int, k: int, n_reads: int, mode: str, steps: 
         own_bytes = req["total"]
         km["bytes_per_kmer"] = own_bytes / kmers_per_step
         km["bytes_parts"] = {key: round(v / kmers_per_step, 4) for key, v in req["parts"].items()}
-    else:
+    elif km["bytes_per_kmer"] is not None:
         own_bytes = kmers_per_step * km["bytes_per_kmer"]
+    else:  # SPEQ_BENCH_NO_STATS (profiling passes: no instrumented launch among the profiled kernels)
+        own_bytes = 0.0
+        km["bytes_per_kmer"] = 0.0
     own_gbs = own_bytes / avg_kernel_s / 1e9
     survey_gbs = kmers_per_step * 2 * k * OCC_ENTRY_BYTES / avg_kernel_s / 1e9
     tr = traffic_lookup(cfg_no, k, mode, n_reads, KERNEL_TAG.get(hot_kernel, "lf"))

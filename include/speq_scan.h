@@ -143,12 +143,14 @@ int speq_scan_reads_device(speq_device_index* d, const uint8_t* d_seq, const uin
 /* Diagnostic twin of speq_scan_reads_device (not the hot path; bench.py's roofline model): the same scan and
  * results, run by an instrumented instantiation of the anchor-and-extend kernel that also counts the work it did.
  * stats (host, u64[SPEQ_AX_STATS_N], overwritten; synchronous): [0] loop iterations per wave, [1] anchor-bucket loads
- * (64 B each), [2] run granule loads (lanes; NWC + 1 16-B granules each), [3]/[4] iterations in which a wave issued
- * bucket/granule loads, [5] windows classified by runs, [6] deferred windows, [7] deferred windows past the Bloom
- * filter, [8] phase-2 bucket loads, [9] phase-2 granule loads (NWC 16-B granules each), [10] staged 16-base chunks
- * (16 B of bases + 16 B of qualities), [11] staged read segments, [12] single quality bytes loaded, [13] windows
- * tallied by runs. Fails with SPEQ_E_ARG when the scan would not use the anchor-and-extend kernel. */
-#define SPEQ_AX_STATS_N 14
+ * (64 B each), [2] run iterations (lanes), [3]/[4] iterations in which a wave issued bucket/granule loads, [5] windows
+ * classified by runs, [6] deferred windows, [7] deferred windows past the Bloom filter, [8] phase-2 bucket loads,
+ * [9] phase-2 candidate verifications (ceil(k / 32) + 1 16-B granules each), [10] staged 16-base chunks (16 B of
+ * bases + 16 B of qualities), [11] staged read segments, [12] single quality bytes loaded, [13] windows tallied by
+ * runs, [14] 16-B granules loaded by runs, [15] window ranges handed to idle lanes, [16..19] phase-1 wave iterations
+ * with 1-4, 5-16, 17-32, 33-64 busy lanes. Fails with SPEQ_E_ARG when the
+ * scan does not use that kernel. */
+#define SPEQ_AX_STATS_N 20
 int speq_scan_reads_device_stats(speq_device_index* d, const uint8_t* d_seq, const uint8_t* d_qual,
                                  const uint64_t* d_offsets, uint64_t n_reads, const speq_scan_params* params,
                                  uint64_t* d_counts, double* d_weights, uint64_t* stats);

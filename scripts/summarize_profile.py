@@ -42,7 +42,7 @@ def main():
             out["scan_steady_state_avg_ns"] = sum(tail) / len(tail)
     pmc = collections.defaultdict(list)
     meta = {}
-    for p in ("fetch", "write", "tcc", "sq", "sq2"):
+    for p in ("fetch", "write", "tcc", "sq", "sq2", "ta"):
         f = os.path.join(src, p, f"{p}_counter_collection.csv")
         if not os.path.exists(f):
             continue

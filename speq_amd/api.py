@@ -191,7 +191,7 @@ class DeviceIndex:
 
     AX_STATS_KEYS = ("wave_iters", "lookup_lanes", "run_lanes", "lookup_waves", "run_waves", "run_windows",
                      "deferred", "filter_pass", "p2_probes", "p2_verify", "chunks", "segments", "qual_bytes",
-                     "run_tallied")
+                     "run_tallied", "run_granules", "splits", "busy_1_4", "busy_5_16", "busy_17_32", "busy_33_64")
 
     def scan_device_stats(self, d_seq: int, d_qual: int, d_offsets: int, n_reads: int, k: int, d_counts: int,
                           d_weights: int = 0, phred_cutoff: int = 30, paired: bool = False,
@@ -488,21 +488,6 @@ class Node:
 
     def em_histograms(self) -> list["EmHistogram"]:
         return [EmHistogram(d) for d in self.devices]
-
-    AX_STATS_KEYS = ("wave_iters", "lookup_lanes", "run_lanes", "lookup_waves", "run_waves", "run_windows",
-                     "deferred", "filter_pass", "p2_probes", "p2_verify", "chunks", "segments", "qual_bytes",
-                     "run_tallied")
-
-    def scan_device_stats(self, d_seq: int, d_qual: int, d_offsets: int, n_reads: int, k: int, d_counts: int,
-                          d_weights: int = 0, phred_cutoff: int = 30, paired: bool = False,
-                          local: bool = False) -> dict:
-        """scan_device through the instrumented anchor-and-extend kernel (speq_scan_reads_device_stats, synchronous):
-        the same counters, plus the kernel's work counts by kind (keys AX_STATS_KEYS)."""
-        p = ScanParams(k, phred_cutoff, int(paired), SPEQ_MODE_LOCAL if local else SPEQ_MODE_GLOBAL)
-        st = np.zeros(len(self.AX_STATS_KEYS), dtype=np.uint64)
-        check(lib().speq_scan_reads_device_stats(self._h, d_seq, d_qual, d_offsets, n_reads, C.byref(p), d_counts,
-                                                 d_weights or None, _u64p(st)))
-        return {key: int(v) for key, v in zip(self.AX_STATS_KEYS, st)}
 
     def scan_fastq(self, path1: str, path2: Optional[str] = None, k: int = 21, phred_cutoff: int = 30,
                    local: bool = False, threads: int = 4, ems: Optional[Sequence["EmHistogram"]] = None):

@@ -9,7 +9,7 @@
 // text: OWN (every occurrence is in the group of p's text), MULTI (occurrences in >= 2 groups), SENT (the window holds
 // an N inside one text) or END (the window crosses a text end). Per k the replica keeps
 //   * `gran`: per 32 text positions one 16-B granule {2-bit text of the 32 positions, class plane 0, class plane 1}
-//     — a run of 64 windows is NG consecutive 16-B loads of ONE array (text and classes together);
+//     — a run over the rest of a read is up to six consecutive 16-B loads of ONE array (text and classes together);
 //   * `atab`: a hash table of one representative position per distinct k-mer, each slot {position, 16-bit
 //     fingerprint, group of the position's text};
 //   * a blocked Bloom filter of the distinct k-mers.
@@ -27,9 +27,10 @@
 // round trip) and looks the survivors up one per lane, so one erroneous read does not hold its wave for k lookups.
 //
 // What bounds it (profiles/r02, r03): the per-CU vector-memory path, which serves the lanes' scattered loads one cache
-// line per lane and instruction. So a run's text and classes come from one array (NG 16-B loads instead of NWC + 1
-// 8-B text loads and five class loads of r02), a load group is issued only when some lane of the wave needs it, and
-// one iteration costs one round trip.
+// line per lane and instruction. So a run's text and classes come from one array (at most six 16-B loads that cover
+// the rest of the read, where r02 loaded four 8-B text words and five class dwords per 64 windows), a clean read is
+// one lookup and one run, a load group is issued only when some lane of the wave needs it, and one iteration costs
+// one round trip.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -55,12 +56,20 @@ constexpr uint32_t AX_MAX_K = 128;    // longest k the scan takes (AX_CAP - k + 
 constexpr uint32_t AX_CAP = 192;      // bases of a read a lane stages at once (longer reads: segments of AX_CAP bases)
 constexpr uint32_t AX_STREAM = AX_CAP + 16;  // staged bases incl. the 16-B alignment slack before the read
 constexpr uint32_t AX_CHUNKS = AX_STREAM / 16;
-constexpr uint32_t AX_RUN = 64;       // windows a lane classifies per iteration (one compare, two class words)
-constexpr uint32_t AX_VWW = 4;        // valid-window words per lane
+constexpr uint32_t AX_CMP = 160;      // bases a run compares per iteration at most: a 150-bp read in one iteration
+constexpr uint32_t AX_CMPW = AX_CMP / 32;        // 2-bit words of one compare
+constexpr uint32_t AX_NGR = AX_CMPW + 1;         // granules that cover AX_CMP bases from any offset in the first
+constexpr uint32_t AX_CHK = 3;                   // 64-window class chunks of one run (<= AX_CMP - k + 1 windows)
+constexpr uint32_t AX_SPLIT = 16;     // a lane hands half of its window range to an idle lane when >= 2 x this is left
+#ifndef SPEQ_AX_SPLIT  // range hand-over to idle lanes (A/B knob: it adds lookups and VALU and did not shorten waves)
+#define SPEQ_AX_SPLIT 0
+#endif
+constexpr uint32_t AX_VWW = 3;        // valid-window words per lane (AX_CAP - k + 1 <= 192 windows)
 constexpr uint32_t AX_SCH = 64 * AX_CHUNKS;     // 16-base chunks of a wave's staged stream (every lane's segment)
 constexpr uint32_t AX_CSW = AX_SCH / 2 + 8;     // 2-bit code words (u64) of the stream, + read-past slack
 constexpr uint32_t AX_BSW = AX_SCH / 2 + 16;    // 1-bit-per-base words (u32) of the stream (bad / quality change)
-constexpr uint32_t AX_DEF = 896;      // deferred-window entries per wave (u16: lane | window << 6); 7.9 KB per wave: 5 blocks per CU
+constexpr uint32_t AX_DEF = 896;      // deferred-window entries per wave (u16: lane | window << 6); 7.9 KB per wave
+                                      // (5 blocks of 4 waves per CU)
 constexpr uint32_t AX_F = 4;          // deferred windows a lane tests against the filter per round trip
 constexpr uint32_t AX_EMPTY = 0xFFFFFFFFu;
 constexpr uint16_t AX_VOID = 0xFFFFu;  // a deferred-list slot reserved by a lane that then kept its windows
@@ -75,23 +84,30 @@ enum : uint32_t { AX_OWN = 0, AX_MULTI = 1, AX_SENT = 2, AX_END = 3 };
 
 static_assert(AX_STREAM % 16 == 0, "chunks of 16 bases");
 static_assert(AX_CAP < 1024, "deferred entries hold the window in 10 bits");
+static_assert(AX_CMP % 32 == 0 && AX_CMP <= AX_CAP && 64 * AX_CHK >= AX_CMP, "run geometry");
 
 // per-launch work counters of the diagnostic (STATS) instantiation; bench.py turns them into the kernel's own bytes
 enum : uint32_t {
     AXS_WAVE_ITERS = 0,  // phase-1 loop iterations (per wave)
     AXS_LOOKUP_LANES,    // phase-1 lane-iterations that loaded an anchor bucket (64 B)
-    AXS_RUN_LANES,       // phase-1 lane-iterations that loaded a run's granules (NG x 16 B)
+    AXS_RUN_LANES,       // phase-1 lane-iterations that loaded a run's granules
     AXS_LOOKUP_WAVES,    // phase-1 iterations in which the wave issued the bucket loads
     AXS_RUN_WAVES,       // ... the granule loads
     AXS_RUN_WINDOWS,     // windows a run classified (tallied, multi or skipped as invalid)
     AXS_DEFERRED,        // windows put on the deferred list
     AXS_FILTER_PASS,     // deferred windows the Bloom filter could not rule out
     AXS_P2_PROBES,       // phase-2 bucket loads (lanes)
-    AXS_P2_VERIFY,       // phase-2 granule loads of a candidate (lanes; NGV x 16 B)
+    AXS_P2_VERIFY,       // phase-2 verifications of a candidate (lanes; HW + 1 granules of 16 B)
     AXS_CHUNKS,          // staged 16-base chunks (16 B of bases + 16 B of qualities each)
     AXS_SEGMENTS,        // staged read segments
     AXS_QBYTES,          // single quality bytes loaded (local mode)
     AXS_RUN_TALLIED,     // windows tallied by runs
+    AXS_RUN_GRANULES,    // granules (16 B) loaded by phase-1 runs
+    AXS_SPLITS,          // window ranges handed from a busy lane to an idle one
+    AXS_BUSY_1_4,        // phase-1 wave iterations with 1-4 busy lanes
+    AXS_BUSY_5_16,       // ... 5-16
+    AXS_BUSY_17_32,      // ... 17-32
+    AXS_BUSY_33_64,      // ... 33-64
     AXS_N
 };
 static_assert(AXS_N == SPEQ_AX_STATS_N, "speq_scan.h SPEQ_AX_STATS_N");
@@ -412,10 +428,10 @@ __device__ __forceinline__ bool ax_probe(const AxView& A, const __amdgpu_buffer_
 template <int MODE>
 constexpr uint32_t ax_wave_bytes() {
     // codes | vw | (local: quality-change stream, rbase) | deferred list (u16; the bad-base stream before phase 1) |
-    // counters | ambiguity | stream base per lane (u16)
+    // counters | ambiguity | stream base per lane (u16) | task hand-over slots
     static_assert(2u * AX_DEF >= 4u * AX_BSW, "the bad-base stream lives in the deferred list");
     return 8u * AX_CSW + 8u * 64u * AX_VWW + (MODE == KM_LOCAL ? 4u * AX_BSW + 8u * 64u : 0u) + 2u * AX_DEF + 16u +
-           8u * 64u + 128u;
+           8u * 64u + 128u + 4u * 64u;
 }
 
 #ifndef SPEQ_AX_WPB  // waves per workgroup of k_scan_ax (A/B knob)
@@ -437,20 +453,18 @@ constexpr uint32_t AX_WPB = SPEQ_AX_WPB, AX_THREADS = 64 * SPEQ_AX_WPB;
 #ifndef SPEQ_AX_MIN_WAVES_LOCAL  // local (Phred-weighted) mode, every k
 #define SPEQ_AX_MIN_WAVES_LOCAL 3
 #endif
-template <int MODE, int NWC>
+template <int MODE, int HW>
 constexpr int ax_min_waves() {
     return MODE == KM_LOCAL ? SPEQ_AX_MIN_WAVES_LOCAL
-                            : (NWC >= 6 ? SPEQ_AX_MIN_WAVES6 : (NWC >= 4 ? SPEQ_AX_MIN_WAVES4 : SPEQ_AX_MIN_WAVES));
+                            : (HW >= 4 ? SPEQ_AX_MIN_WAVES6 : (HW >= 2 ? SPEQ_AX_MIN_WAVES4 : SPEQ_AX_MIN_WAVES));
 }
 
-// NWC = 2-bit words covering the k - 1 + AX_RUN bases of one compare: 3 (k <= 33), 4 (k <= 65), 6 (k <= 128);
-// a run loads NG = NWC + 1 granules, a phase-2 verification NGV + 1 = NWC (the k bases at any offset in a granule).
-template <int MODE, bool PAIRED, bool LDS_HIST, bool EM, int NWC, bool STATS>
-__global__ __launch_bounds__(AX_THREADS, (ax_min_waves<MODE, NWC>())) void k_scan_ax(AxView A, UnitSrc src,
-                                                                                   unsigned long long* __restrict__ out_a,
-                                                                                   double* __restrict__ out_w) {
-    constexpr int NG = NWC + 1;
-    constexpr int NGV = NWC - 1;
+// HW = 2-bit words of one k-mer (its hash): 1 (k <= 32), 2 (k <= 64), 4 (k <= 128); a phase-2 verification loads the
+// HW + 1 granules that cover k bases at any offset in the first.
+template <int MODE, bool PAIRED, bool LDS_HIST, bool EM, int HW, bool STATS>
+__global__ __launch_bounds__(AX_THREADS, (ax_min_waves<MODE, HW>())) void k_scan_ax(AxView A, UnitSrc src,
+                                                                                  unsigned long long* __restrict__ out_a,
+                                                                                  double* __restrict__ out_w) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -474,6 +488,7 @@ __global__ __launch_bounds__(AX_THREADS, (ax_min_waves<MODE, NWC>())) void k_sca
     int32_t* ambf = reinterpret_cast<int32_t*>(defn + 4);            // [64] first counted group
     int32_t* ambd = ambf + 64;                                       // [64] another group seen
     uint16_t* sbs = reinterpret_cast<uint16_t*>(ambd + 64);          // [64] stream base of each lane's segment
+    uint32_t* spl = reinterpret_cast<uint32_t*>(sbs + 64);           // [64] tasks handed to idle lanes
 
     if (MODE == KM_LOCAL)
         for (uint32_t i = threadIdx.x; i < QLUT_LEN; i += AX_THREADS) {
@@ -504,12 +519,12 @@ __global__ __launch_bounds__(AX_THREADS, (ax_min_waves<MODE, NWC>())) void k_sca
     const uint64_t r_end = PAIRED ? 2 * nu : nu;
     const uint64_t n_groups = (r_end + 63) / 64;
     const uint32_t segw = AX_CAP - k + 1u;  // windows per segment
-    const uint32_t cmpb = k - 1u + AX_RUN;  // bases compared per iteration
 
     uint32_t t_cnt = 0, amb = 0;
     // diagnostic counters (STATS only; wave-level ones are counted by lane 0)
     uint32_t s_iter = 0, s_lk = 0, s_rn = 0, s_lkw = 0, s_rnw = 0, s_rwin = 0, s_def = 0, s_fp = 0, s_p2 = 0,
-             s_p2v = 0, s_ch = 0, s_seg = 0, s_qb = 0, s_tal = 0;
+             s_p2v = 0, s_ch = 0, s_seg = 0, s_qb = 0, s_tal = 0, s_rg = 0, s_spl = 0, s_b4 = 0, s_b16 = 0, s_b32 = 0,
+             s_b64 = 0;
 
     auto add_count = [&](uint32_t g, uint32_t cnt, double wsum) {
         if (LDS_HIST) {
@@ -675,6 +690,8 @@ __global__ __launch_bounds__(AX_THREADS, (ax_min_waves<MODE, NWC>())) void k_sca
             }
             if (MODE == KM_LOCAL) rbase[lane] = a;
             sbs[lane] = (uint16_t)sbase;
+            ambf[lane] = af;  // the read's ambiguity state, updated by every lane that tallies windows of it
+            ambd[lane] = ad;
             wave_sync();  // the bad-base stream (in the deferred list) is read by every lane before the list is reset
             if (lane == 0) {
                 defn[0] = 0;
@@ -683,30 +700,26 @@ __global__ __launch_bounds__(AX_THREADS, (ax_min_waves<MODE, NWC>())) void k_sca
             wave_sync();
 
             // per-lane readers of the staged stream
-            auto read_words = [&](uint32_t base, uint64_t(&w)[NWC]) {  // NWC code words at stream position `base`
+            auto read_words = [&](uint32_t base, uint64_t(&w)[HW]) {  // HW code words at stream position `base`
                 const uint32_t idx = base >> 5, sh = 2u * (base & 31u);
-                uint64_t raw[NWC + 1];
+                uint64_t raw[HW + 1];
 #pragma unroll
-                for (int i = 0; i <= NWC; ++i) raw[i] = cs[min(idx + (uint32_t)i, AX_CSW - 1u)];
+                for (int i = 0; i <= HW; ++i) raw[i] = cs[min(idx + (uint32_t)i, AX_CSW - 1u)];
 #pragma unroll
-                for (int i = 0; i < NWC; ++i) w[i] = funnel(raw[i], raw[i + 1], sh);
+                for (int i = 0; i < HW; ++i) w[i] = funnel(raw[i], raw[i + 1], sh);
             };
-            auto vbits = [&](uint32_t b) -> uint64_t {  // this lane's valid-window bits b .. b + 63 (0 past the end)
-                const uint32_t w0 = b >> 6, s6 = b & 63u;
-                const uint64_t lo = w0 < AX_VWW ? vwl[w0 * 64u + lane] : 0ull;
-                const uint64_t hi = w0 + 1u < AX_VWW ? vwl[(w0 + 1u) * 64u + lane] : 0ull;
+            auto vbits = [&](uint32_t o, uint32_t b) -> uint64_t {  // read o's valid-window bits b .. b + 63 (0 past
+                const uint32_t w0 = b >> 6, s6 = b & 63u;                 // the end)
+                const uint64_t lo = w0 < AX_VWW ? vwl[w0 * 64u + o] : 0ull;
+                const uint64_t hi = w0 + 1u < AX_VWW ? vwl[(w0 + 1u) * 64u + o] : 0ull;
                 return funnel(lo, hi, s6);
             };
-            auto next_valid = [&](uint32_t j) -> uint32_t {  // first valid window >= j (or wend)
-                uint32_t res = wend;
-#pragma unroll
-                for (int i = (int)AX_VWW - 1; i >= 0; --i) {
-                    const uint32_t b0 = 64u * (uint32_t)i;
-                    uint64_t v = vwl[(uint32_t)i * 64u + lane];
-                    if (j > b0) v = (j - b0 >= 64u) ? 0ull : (v & (~0ull << (j - b0)));
-                    if (v) res = b0 + (uint32_t)__builtin_ctzll(v);
+            auto next_valid = [&](uint32_t o, uint32_t j, uint32_t end) -> uint32_t {  // first valid window of read o
+                for (uint32_t b = j; b < end; b += 64u) {                             // in [j, end), else end
+                    const uint64_t v = vbits(o, b);
+                    if (v) return min(b + (uint32_t)__builtin_ctzll(v), end);
                 }
-                return res;
+                return end;
             };
             auto defer_push = [&](uint32_t o, uint32_t jj) -> bool {
                 const uint32_t slot = atomicAdd(&defn[0], 1u);
@@ -740,8 +753,16 @@ __global__ __launch_bounds__(AX_THREADS, (ax_min_waves<MODE, NWC>())) void k_sca
                 return u;
             };
 
-            // ---- phase 1: one read per lane, one memory round trip per iteration: a lane either probes the anchor
-            // table (its candidate is compared in the next iteration) or extends a run by up to AX_RUN windows
+            // ---- phase 1: one task per lane (a window range [j, jend) of read o; first its own read), one memory
+            // round trip per iteration: a lane either probes the anchor table (its candidate is compared in the next
+            // iteration) or extends a run over the rest of its range (at most AX_CMP bases; a clean 150-bp read: one
+            // lookup and one run). A wave runs as long as its slowest lane, so a lane about to look a window up
+            // hands the second half of its range to an idle lane when there is one: the slow reads (mismatches
+            // against representatives of other variants, sequencing errors) are worked on by several lanes at once.
+            uint32_t o = lane;         // the read (lane of the wave that staged it) this lane works on
+            uint32_t jend = wend;      // end of this lane's window range
+            uint32_t tsb = sbase;      // read o's stream base
+            uint64_t ta = a;           // read o's first base in seq/qual (local mode)
             uint32_t j = 0;
             uint32_t st = wend > 0 ? 0u : 2u;  // 0: look window j up, 1: extend from text position p, 2: done
             bool verify = false;       // st 1: p came from the anchor table (window j itself not compared yet)
@@ -750,14 +771,62 @@ __global__ __launch_bounds__(AX_THREADS, (ax_min_waves<MODE, NWC>())) void k_sca
             int32_t last_mm = -1;      // base (relative to the segment) of the last observed mismatch
             uint32_t pb = 0, ps = 0;   // probe position of the current lookup (bucket, first slot)
             bool resume = false;       // continue the current lookup at (pb, ps): full bucket, or failed verification
+            bool run_phase = true;     // this wave iteration extends runs (else: looks windows up); starts with lookups
             for (;;) {
                 if (st == 0u) {
-                    j = next_valid(j);
-                    if (j >= wend) st = 2u;
+                    j = next_valid(o, j, jend);
+                    if (j >= jend) st = 2u;
                 }
-                if (__ballot(st != 2u) == 0) break;
-                const bool lk = st == 0u, rn = st == 1u;
-                const bool any_lk = __ballot(lk) != 0, any_rn = __ballot(rn) != 0;
+                const unsigned long long busy = __ballot(st != 2u);
+                if (busy == 0) break;
+                if (STATS && lane == 0) {
+                    const uint32_t nb = (uint32_t)__popcll(busy);
+                    s_b4 += nb <= 4u ? 1u : 0u;
+                    s_b16 += (nb > 4u && nb <= 16u) ? 1u : 0u;
+                    s_b32 += (nb > 16u && nb <= 32u) ? 1u : 0u;
+                    s_b64 += nb > 32u ? 1u : 0u;
+                }
+                if (SPEQ_AX_SPLIT && busy != ~0ull) {  // idle lanes: lanes about to look up with >= 2 AX_SPLIT windows left hand half over
+                    const unsigned long long idle = ~busy;
+                    const bool can = st == 0u && jend - j >= 2u * AX_SPLIT;
+                    const unsigned long long cm = __ballot(can);
+                    if (cm != 0) {
+                        const uint32_t n = min((uint32_t)__popcll(idle), (uint32_t)__popcll(cm));
+                        const uint32_t rc =
+                            __builtin_amdgcn_mbcnt_hi((uint32_t)(cm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)cm, 0u));
+                        const uint32_t ri = __builtin_amdgcn_mbcnt_hi((uint32_t)(idle >> 32),
+                                                                      __builtin_amdgcn_mbcnt_lo((uint32_t)idle, 0u));
+                        if (can && rc < n) {
+                            const uint32_t mid = j + (jend - j) / 2u;
+                            spl[rc] = o | (mid << 6) | (jend << 16);
+                            jend = mid;
+                        }
+                        wave_sync();
+                        if (st == 2u && ri < n) {
+                            const uint32_t t = spl[ri];
+                            o = t & 63u;
+                            j = (t >> 6) & 1023u;
+                            jend = t >> 16;
+                            tsb = sbs[o];
+                            if (MODE == KM_LOCAL) ta = rbase[o];
+                            st = 0u;
+                            verify = false;
+                            resume = false;
+                            last_mm = -1;
+                            j = next_valid(o, j, jend);
+                            if (j >= jend) st = 2u;
+                            if (STATS) s_spl += 1u;
+                        }
+                        wave_sync();
+                    }
+                }
+                // one kind of work per iteration, alternating (a lookup is followed by a run and a run by a lookup, so
+                // a lane rarely waits): the wave executes the lookup code or the run code, not both under exec masks
+                // (the kernel is bound by VALU issue, profiles/r03), and a kind no lane needs is skipped
+                const bool want_lk = __ballot(st == 0u) != 0, want_rn = __ballot(st == 1u) != 0;
+                run_phase = run_phase ? !want_lk : want_rn;
+                const bool lk = st == 0u && !run_phase, rn = st == 1u && run_phase;
+                const bool any_lk = !run_phase, any_rn = run_phase;
                 if (STATS) {
                     s_iter += lane == 0 ? 1u : 0u;
                     s_lkw += (lane == 0 && any_lk) ? 1u : 0u;
@@ -765,14 +834,14 @@ __global__ __launch_bounds__(AX_THREADS, (ax_min_waves<MODE, NWC>())) void k_sca
                     s_lk += lk ? 1u : 0u;
                     s_rn += rn ? 1u : 0u;
                 }
-                uint64_t ra[NWC];
-                read_words(sbase + j, ra);
                 // ---- this iteration's loads: a bucket (lookup lanes), the run's granules (run lanes), the quality
                 // of window j (local mode); a group is issued only when some lane of the wave needs it
                 u32x4 q0 = {0u, 0u, 0u, 0u}, q1 = q0, q2 = q0, q3 = q0;
                 uint32_t fp = 0;
                 if (any_lk) {
-                    const uint64_t h = ax_hash<NWC>(ra, k);
+                    uint64_t ra[HW];
+                    read_words(tsb + j, ra);
+                    const uint64_t h = ax_hash<HW>(ra, k);
                     fp = ax_fp(h);
                     if (lk && !resume) {
                         pb = ax_bucket(h, A.nb);
@@ -784,17 +853,22 @@ __global__ __launch_bounds__(AX_THREADS, (ax_min_waves<MODE, NWC>())) void k_sca
                     q2 = __builtin_amdgcn_raw_buffer_load_b128(rs_atab, boff + 32u, 0, 0);
                     q3 = __builtin_amdgcn_raw_buffer_load_b128(rs_atab, boff + 48u, 0, 0);
                 }
-                u32x4 gr[NG];
+                // a run compares the rest of the segment from window j (at most AX_CMP bases): the granules that
+                // cover it from p's granule on, the others with out-of-range offsets
+                const uint32_t cl = min(jend - j + k - 1u, AX_CMP);
+                u32x4 gr[AX_NGR];
 #pragma unroll
-                for (int i = 0; i < NG; ++i) gr[i] = q0;
+                for (uint32_t i = 0; i < AX_NGR; ++i) gr[i] = q0;
                 uint32_t qj = 0;
                 if (any_rn) {
-                    const uint32_t goff = rn ? (p >> 5) * 16u : AX_OOB;
+                    const uint32_t ng = rn ? ((p & 31u) + cl + 31u) >> 5 : 0u;
+                    const uint32_t goff = (p >> 5) * 16u;
 #pragma unroll
-                    for (int i = 0; i < NG; ++i)
-                        gr[i] = __builtin_amdgcn_raw_buffer_load_b128(rs_gran, goff + 16u * (uint32_t)i, 0, 0);
+                    for (uint32_t i = 0; i < AX_NGR; ++i)
+                        gr[i] = __builtin_amdgcn_raw_buffer_load_b128(rs_gran, i < ng ? goff + 16u * i : AX_OOB, 0, 0);
+                    if (STATS) s_rg += ng;
                     if (MODE == KM_LOCAL) {
-                        qj = src.qual[a + (rn ? j : 0u)];
+                        qj = src.qual[ta + (rn ? j : 0u)];
                         if (STATS) s_qb += rn ? 1u : 0u;
                     }
                 }
@@ -815,10 +889,10 @@ __global__ __launch_bounds__(AX_THREADS, (ax_min_waves<MODE, NWC>())) void k_sca
                         resume = false;
                         uint32_t dend = (last_mm >= (int32_t)j && last_mm < (int32_t)(j + k)) ? (uint32_t)last_mm
                                                                                                : j + k - 1u;
-                        dend = min(dend, wend - 1u);
+                        dend = min(dend, jend - 1u);
                         // the valid windows of (j, dend] as two 64-bit masks (dend - j <= k - 1 <= 127)
                         const uint32_t span = dend - j;
-                        uint64_t dm0 = vbits(j + 1u), dm1 = span > 64u ? vbits(j + 65u) : 0ull;
+                        uint64_t dm0 = vbits(o, j + 1u), dm1 = span > 64u ? vbits(o, j + 65u) : 0ull;
                         dm0 &= span >= 64u ? ~0ull : ((1ull << span) - 1ull);
                         if (span > 64u) dm1 &= span - 64u >= 64u ? ~0ull : ((1ull << (span - 64u)) - 1ull);
                         const uint32_t cnt = (uint32_t)__popcll(dm0) + (uint32_t)__popcll(dm1);
@@ -829,9 +903,9 @@ __global__ __launch_bounds__(AX_THREADS, (ax_min_waves<MODE, NWC>())) void k_sca
                             if (ok_def) {
                                 uint32_t sl = slot0;
                                 for (uint64_t t = dm0; t; t &= t - 1)
-                                    defl[sl++] = (uint16_t)(lane | ((j + 1u + (uint32_t)__builtin_ctzll(t)) << 6));
+                                    defl[sl++] = (uint16_t)(o | ((j + 1u + (uint32_t)__builtin_ctzll(t)) << 6));
                                 for (uint64_t t = dm1; t; t &= t - 1)
-                                    defl[sl++] = (uint16_t)(lane | ((j + 65u + (uint32_t)__builtin_ctzll(t)) << 6));
+                                    defl[sl++] = (uint16_t)(o | ((j + 65u + (uint32_t)__builtin_ctzll(t)) << 6));
                                 if (STATS) s_def += cnt;
                             } else {  // no room: the windows stay with this lane; void the slots reserved below the end
                                 for (uint32_t sl = slot0; sl < AX_DEF && sl < slot0 + cnt; ++sl) defl[sl] = AX_VOID;
@@ -846,18 +920,27 @@ __global__ __launch_bounds__(AX_THREADS, (ax_min_waves<MODE, NWC>())) void k_sca
                     }
                 }
 
-                // ---- run lanes: compare read [j, j + cmpb) with text [p, p + cmpb), classify the matched windows
+                // ---- run lanes: compare read [j, j + cl) with text [p, p + cl), classify the matched windows
                 if (any_rn && rn) {
                     const uint32_t s5 = p & 31u, sh = 2u * s5;
-                    uint32_t e = cmpb;
+                    uint32_t e = cl;  // first mismatching base (cl: none)
+                    {
+                        const uint32_t base = tsb + j, idx = base >> 5, rsh = 2u * (base & 31u);
+                        uint64_t cur = cs[min(idx, AX_CSW - 1u)];
 #pragma unroll
-                    for (int i = NWC - 1; i >= 0; --i) {
-                        const uint64_t tw = funnel(u64of(gr[i][0], gr[i][1]), u64of(gr[i + 1][0], gr[i + 1][1]), sh);
-                        uint64_t x = ra[i] ^ tw;
-                        const uint32_t b0 = 32u * (uint32_t)i;
-                        if (cmpb <= b0) x = 0;
-                        else if (cmpb < b0 + 32u) x &= (1ull << (2u * (cmpb - b0))) - 1ull;
-                        if (x) e = b0 + ((uint32_t)__builtin_ctzll(x) >> 1);
+                        for (uint32_t i = 0; i < AX_CMPW; ++i) {
+                            const uint64_t nxt = cs[min(idx + i + 1u, AX_CSW - 1u)];
+                            const uint64_t rw = funnel(cur, nxt, rsh);
+                            cur = nxt;
+                            const uint64_t tw =
+                                funnel(u64of(gr[i][0], gr[i][1]), u64of(gr[i + 1][0], gr[i + 1][1]), sh);
+                            uint64_t x = rw ^ tw;
+                            const uint32_t b0 = 32u * i;
+                            if (cl <= b0) x = 0;
+                            else if (cl < b0 + 32u) x &= (1ull << (2u * (cl - b0))) - 1ull;
+                            const uint32_t ei = b0 + ((uint32_t)__builtin_ctzll(x | (1ull << 63)) >> 1);
+                            e = (x != 0 && ei < e) ? ei : e;
+                        }
                     }
                     if (verify && e < k) {  // fingerprint collision: resume probing after that slot
                         st = 0u;
@@ -865,20 +948,45 @@ __global__ __launch_bounds__(AX_THREADS, (ax_min_waves<MODE, NWC>())) void k_sca
                         ++ps;
                     } else {
                         uint32_t R = e - (k - 1u);  // e >= k - 1: a candidate matched k bases, a run k - 1
-                        R = min(R, AX_RUN);
-                        R = min(R, wend - j);
-                        const uint64_t mR = R >= 64u ? ~0ull : ((1ull << R) - 1ull);
-                        const uint64_t m = vbits(j) & mR;  // the run's valid read windows
-                        // class planes of windows p .. p + 63 (bits s5 .. s5 + 63 of three granules' planes)
-                        const uint64_t P0 = funnel(u64of(gr[0][2], gr[1][2]), (uint64_t)gr[2][2], s5);
-                        const uint64_t P1 = funnel(u64of(gr[0][3], gr[1][3]), (uint64_t)gr[2][3], s5);
-                        // the run stops at the first END window (the text ends: the next windows belong to another
-                        // text, looked up again) or SENT window of a valid read window (an N in the text: looked up)
-                        const uint64_t stop = P1 & (P0 | m) & mR;
-                        const uint32_t d0 = stop ? (uint32_t)__builtin_ctzll(stop) : R;
-                        const uint64_t mRc = d0 >= 64u ? ~0ull : ((1ull << d0) - 1ull);
-                        const uint64_t own = ~P0 & ~P1 & m & mRc;
-                        const uint32_t cnt = (uint32_t)__popcll(own);
+                        R = min(R, jend - j);
+                        // the windows [0, R) in 64-window chunks: class planes of windows p + 64c .. (bits s5 + 64c ..
+                        // of the granules' planes). The run stops at the first END window (the text ends: the next
+                        // windows belong to another text, looked up again) or SENT window of a valid read window (an
+                        // N in the text: looked up); windows before it are tallied to the run's group
+                        uint32_t d0 = R, cnt = 0;
+                        bool cut = false, cut_end = false;
+                        uint64_t ownc[AX_CHK];
+#pragma unroll
+                        for (uint32_t c = 0; c < AX_CHK; ++c) {
+                            const uint32_t w0 = 64u * c;
+                            const uint64_t mRc = R <= w0 ? 0ull : (R - w0 >= 64u ? ~0ull : ((1ull << (R - w0)) - 1ull));
+                            const uint64_t hp0 = 2 * c + 2 < AX_NGR ? (uint64_t)gr[(2 * c + 2) % AX_NGR][2] : 0ull;
+                            const uint64_t hp1 = 2 * c + 2 < AX_NGR ? (uint64_t)gr[(2 * c + 2) % AX_NGR][3] : 0ull;
+                            const uint64_t P0 = funnel(u64of(gr[2 * c][2], gr[2 * c + 1][2]), hp0, s5);
+                            const uint64_t P1 = funnel(u64of(gr[2 * c][3], gr[2 * c + 1][3]), hp1, s5);
+                            const uint64_t m = vbits(o, j + w0) & mRc;  // the chunk's valid read windows in the run
+                            const uint64_t stop = P1 & (P0 | m) & mRc;
+                            const uint64_t below = cut ? 0ull : (stop ? ((stop & (0ull - stop)) - 1ull) : ~0ull);
+                            const uint64_t own = ~P0 & ~P1 & m & below;
+                            cnt += (uint32_t)__popcll(own);
+                            ownc[c] = own;
+                            if (EM) {  // multi-group windows of the run: the EM histogram
+                                uint64_t todo = P0 & ~P1 & m & below;
+                                while (todo) {
+                                    const uint32_t d = (uint32_t)__builtin_ctzll(todo);
+                                    todo &= todo - 1;
+                                    const uint32_t lo = A.mlo[p + w0 + d];
+                                    atomicAdd(&src.em_mult[lo], 1u);
+                                    src.em_hi[lo] = A.mhi[lo];
+                                }
+                            }
+                            if (!cut && stop) {
+                                const uint32_t t = (uint32_t)__builtin_ctzll(stop);
+                                d0 = w0 + t;
+                                cut_end = ((P0 >> t) & 1ull) != 0;
+                                cut = true;
+                            }
+                        }
                         if (STATS) {
                             s_rwin += d0;
                             s_tal += cnt;
@@ -887,47 +995,40 @@ __global__ __launch_bounds__(AX_THREADS, (ax_min_waves<MODE, NWC>())) void k_sca
                             double wsum = 0.0;
                             if (MODE == KM_LOCAL) {
                                 // one quality for the whole cut run when no base in (j, j + d0 - 1 + k) changes it
-                                if (chg_zero(sbase + j + 1u, d0 + k - 2u)) {
+                                if (chg_zero(tsb + j + 1u, d0 + k - 2u)) {
                                     int q = (int)qj - 33;
                                     q = q < 0 ? 0 : (q > 41 ? 41 : q);
                                     wsum = (double)cnt * wtab[q];
                                 } else {
-                                    uint64_t todo = own;
-                                    while (todo) {
-                                        const uint32_t d = (uint32_t)__builtin_ctzll(todo);
-                                        todo &= todo - 1;
-                                        const uint32_t jj = j + d;
-                                        const uint8_t* qb = src.qual + a + jj;
-                                        int q = (int)qb[0] - 33;
-                                        q = q < 0 ? 0 : (q > 41 ? 41 : q);
-                                        wsum += weight(qb, chg_zero(sbase + jj + 1u, k - 1u), (uint32_t)q);
-                                        if (STATS) s_qb += 1u;
+#pragma unroll
+                                    for (uint32_t c = 0; c < AX_CHK; ++c) {
+                                        uint64_t todo = ownc[c];
+                                        while (todo) {
+                                            const uint32_t d = 64u * c + (uint32_t)__builtin_ctzll(todo);
+                                            todo &= todo - 1;
+                                            const uint32_t jj = j + d;
+                                            const uint8_t* qb = src.qual + ta + jj;
+                                            int q = (int)qb[0] - 33;
+                                            q = q < 0 ? 0 : (q > 41 ? 41 : q);
+                                            wsum += weight(qb, chg_zero(tsb + jj + 1u, k - 1u), (uint32_t)q);
+                                            if (STATS) s_qb += 1u;
+                                        }
                                     }
                                 }
                             }
                             add_count(gt, cnt, wsum);
-                            if (af < 0) af = (int32_t)gt;
-                            else if ((int32_t)gt != af) ad = 1;
-                        }
-                        if (EM) {  // multi-group windows of the run: the EM histogram
-                            uint64_t todo = P0 & ~P1 & m & mRc;
-                            while (todo) {
-                                const uint32_t d = (uint32_t)__builtin_ctzll(todo);
-                                todo &= todo - 1;
-                                const uint32_t lo = A.mlo[p + d];
-                                atomicAdd(&src.em_mult[lo], 1u);
-                                src.em_hi[lo] = A.mhi[lo];
-                            }
+                            const int32_t old = atomicCAS(&ambf[o], -1, (int32_t)gt);
+                            if (old != -1 && old != (int32_t)gt) ambd[o] = 1;
                         }
                         // next state
                         verify = false;
                         if (d0 < R) {
-                            if ((P0 >> d0) & 1ull) {  // END: look the window up (its k-mer may occur elsewhere)
+                            if (cut_end) {  // END: look the window up (its k-mer may occur elsewhere)
                                 j += d0;
                                 st = 0u;
                                 resume = false;
                                 last_mm = -1;
-                            } else if (defer_push(lane, j + d0)) {  // SENT: matched bases, but no valid text window
+                            } else if (defer_push(o, j + d0)) {  // SENT: matched bases, but no valid text window
                                 if (STATS) s_def += 1u;
                                 j += d0 + 1u;
                                 p += d0 + 1u;
@@ -939,14 +1040,14 @@ __global__ __launch_bounds__(AX_THREADS, (ax_min_waves<MODE, NWC>())) void k_sca
                                 last_mm = -1;
                             }
                         } else {
-                            const bool mism = e < cmpb;  // the run ended at a mismatch (base j + e)
-                            if (mism && R < wend - j) last_mm = (int32_t)(j + e);
+                            const bool mism = e < cl;  // the run ended at a mismatch (base j + e)
+                            if (mism && R < jend - j) last_mm = (int32_t)(j + e);
                             j += R;
                             p += R;
                             st = (mism || R == 0u) ? 0u : 1u;
                             if (st == 0u) resume = false;
                         }
-                        if (j >= wend) st = 2u;
+                        if (j >= jend) st = 2u;
                     }
                 }
             }
@@ -954,8 +1055,6 @@ __global__ __launch_bounds__(AX_THREADS, (ax_min_waves<MODE, NWC>())) void k_sca
             // ---- phase 2: the deferred windows of the wave. (a) the Bloom filter, AX_F windows per lane per round
             // trip; the windows it cannot rule out are compacted to the front of the list; (b) those are looked up one
             // per lane (bucket -> fingerprint -> compare with the text -> class)
-            ambf[lane] = af;
-            ambd[lane] = ad;
             wave_sync();
             const uint32_t n2 = min(__builtin_amdgcn_readfirstlane(defn[0]), AX_DEF);
             for (uint32_t base = 0; base < n2; base += 64u * AX_F) {
@@ -968,9 +1067,9 @@ __global__ __launch_bounds__(AX_THREADS, (ax_min_waves<MODE, NWC>())) void k_sca
                     const uint16_t e16 = idx < n2 ? defl[idx] : AX_VOID;
                     ent[t] = e16 == AX_VOID ? AX_EMPTY : (uint32_t)e16;
                     const uint32_t o = ent[t] & 63u, jj = (ent[t] >> 6) & 1023u;
-                    uint64_t ra[NWC];
+                    uint64_t ra[HW];
                     read_words((uint32_t)sbs[o] + jj, ra);
-                    hh[t] = ax_hash<NWC>(ra, k);
+                    hh[t] = ax_hash<HW>(ra, k);
                 }
 #pragma unroll
                 for (uint32_t t = 0; t < AX_F; ++t) {
@@ -997,9 +1096,9 @@ __global__ __launch_bounds__(AX_THREADS, (ax_min_waves<MODE, NWC>())) void k_sca
                 const uint32_t ent = act ? (uint32_t)defl[idx] : 0u;
                 const uint32_t o = ent & 63u, jj = ent >> 6;
                 const uint32_t sbo = sbs[o];
-                uint64_t ra[NWC];
+                uint64_t ra[HW];
                 read_words(sbo + jj, ra);
-                const uint64_t h = ax_hash<NWC>(ra, k);
+                const uint64_t h = ax_hash<HW>(ra, k);
                 const uint32_t fp = ax_fp(h);
                 uint32_t b = act ? ax_bucket(h, A.nb) : 0u, sl = 0, pp = 0, pg = 0;
                 bool pend = act, found = false;
@@ -1008,11 +1107,11 @@ __global__ __launch_bounds__(AX_THREADS, (ax_min_waves<MODE, NWC>())) void k_sca
                     const bool c = ax_probe(A, rs_atab, fp, b, sl, pp, pg, pend, s_p2);
                     const bool cand = pend && c;
                     if (STATS) s_p2v += cand ? 1u : 0u;
-                    u32x4 gv[NGV + 1];
+                    u32x4 gv[HW + 1];
                     {
                         const uint32_t goff = cand ? (pp >> 5) * 16u : AX_OOB;
 #pragma unroll
-                        for (int i = 0; i <= NGV; ++i)
+                        for (int i = 0; i <= HW; ++i)
                             gv[i] = __builtin_amdgcn_raw_buffer_load_b128(rs_gran, goff + 16u * (uint32_t)i, 0, 0);
                     }
                     if (pend) {
@@ -1022,7 +1121,7 @@ __global__ __launch_bounds__(AX_THREADS, (ax_min_waves<MODE, NWC>())) void k_sca
                             const uint32_t s5 = pp & 31u;
                             bool eq = true;
 #pragma unroll
-                            for (int i = 0; i < NGV; ++i) {
+                            for (int i = 0; i < HW; ++i) {
                                 uint64_t x = ra[i] ^ funnel(u64of(gv[i][0], gv[i][1]), u64of(gv[i + 1][0], gv[i + 1][1]),
                                                             2u * s5);
                                 const uint32_t b0 = 32u * (uint32_t)i;
@@ -1091,7 +1190,7 @@ __global__ __launch_bounds__(AX_THREADS, (ax_min_waves<MODE, NWC>())) void k_sca
     }
     if (STATS) {
         const uint32_t sv[AXS_N] = {s_iter, s_lk, s_rn, s_lkw, s_rnw, s_rwin, s_def, s_fp, s_p2, s_p2v, s_ch, s_seg,
-                                    s_qb, s_tal};
+                                    s_qb, s_tal, s_rg, s_spl, s_b4, s_b16, s_b32, s_b64};
 #pragma unroll
         for (uint32_t i = 0; i < AXS_N; ++i)
             if (sv[i]) atomicAdd(&A.stats[i], (unsigned long long)sv[i]);
@@ -1109,23 +1208,23 @@ __global__ __launch_bounds__(AX_THREADS, (ax_min_waves<MODE, NWC>())) void k_sca
     }
 }
 
-template <int MODE, bool PAIRED, bool LDS, bool EM, int NWC, bool STATS>
+template <int MODE, bool PAIRED, bool LDS, bool EM, int HW, bool STATS>
 void ax_launch_one(const AxView& A, const UnitSrc& src, uint32_t grid, size_t lds, hipStream_t st,
                    unsigned long long* a, double* w) {
     if (lds > 64 * 1024)  // dynamic LDS above 64 KiB must be allowed (occupancy caps pad it)
-        HIP_OK(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_scan_ax<MODE, PAIRED, LDS, EM, NWC, STATS>),
+        HIP_OK(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_scan_ax<MODE, PAIRED, LDS, EM, HW, STATS>),
                                    hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-    hipLaunchKernelGGL((k_scan_ax<MODE, PAIRED, LDS, EM, NWC, STATS>), dim3(grid), dim3(AX_THREADS), lds, st, A, src,
+    hipLaunchKernelGGL((k_scan_ax<MODE, PAIRED, LDS, EM, HW, STATS>), dim3(grid), dim3(AX_THREADS), lds, st, A, src,
                        a, w);
 }
 
-// NWC by k: 3 (k <= 33), 4 (k <= 65), 6 (k <= 128)
+// HW by k: 1 (k <= 32), 2 (k <= 64), 4 (k <= 128)
 template <int MODE, bool PAIRED, bool LDS, bool EM, bool STATS>
 void ax_launch_nwc(uint32_t k, const AxView& A, const UnitSrc& src, uint32_t grid, size_t lds, hipStream_t st,
                    unsigned long long* a, double* w) {
-    if (k <= 33) ax_launch_one<MODE, PAIRED, LDS, EM, 3, STATS>(A, src, grid, lds, st, a, w);
-    else if (k <= 65) ax_launch_one<MODE, PAIRED, LDS, EM, 4, STATS>(A, src, grid, lds, st, a, w);
-    else ax_launch_one<MODE, PAIRED, LDS, EM, 6, STATS>(A, src, grid, lds, st, a, w);
+    if (k <= 32) ax_launch_one<MODE, PAIRED, LDS, EM, 1, STATS>(A, src, grid, lds, st, a, w);
+    else if (k <= 64) ax_launch_one<MODE, PAIRED, LDS, EM, 2, STATS>(A, src, grid, lds, st, a, w);
+    else ax_launch_one<MODE, PAIRED, LDS, EM, 4, STATS>(A, src, grid, lds, st, a, w);
 }
 
 template <int MODE, bool PAIRED>
@@ -1159,7 +1258,7 @@ AxTable build_ax(speq_device_index* d, uint32_t k) {
     const uint64_t n = d->view.n;
     if (k < 1 || k > AX_MAX_K || n >= (1ull << 30) || d->G > AX_MAX_G) return ax;
     const uint64_t nw64 = (n + 63) / 64 + 4;
-    const uint64_t n_gran = (n + 255) / 32 + 2;  // a run from any p < n reads NG <= 7 granules: padded with END
+    const uint64_t n_gran = (n + 255) / 32 + 2;  // a run from any p < n reads <= AX_NGR granules: padded with END
     const uint64_t gran_bytes = n_gran * 16;
     size_t free_b = 0, total_b = 0;
     HIP_OK(hipMemGetInfo(&free_b, &total_b));
