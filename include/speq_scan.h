@@ -147,7 +147,7 @@ int speq_scan_reads_device(speq_device_index* d, const uint8_t* d_seq, const uin
  * classified by runs, [6] deferred windows, [7] deferred windows past the Bloom filter, [8] phase-2 bucket loads,
  * [9] phase-2 candidate verifications (ceil(k / 32) + 1 16-B granules each), [10] staged 16-base chunks (16 B of
  * bases + 16 B of qualities), [11] staged read segments, [12] single quality bytes loaded, [13] windows tallied by
- * runs, [14] 16-B granules loaded by runs, [15] window ranges handed to idle lanes, [16..19] phase-1 wave iterations
+ * runs, [14] 16-B granules loaded by runs, [15] lane refills (per wave), [16..19] phase-1 wave iterations
  * with 1-4, 5-16, 17-32, 33-64 busy lanes. Fails with SPEQ_E_ARG when the
  * scan does not use that kernel. */
 #define SPEQ_AX_STATS_N 20

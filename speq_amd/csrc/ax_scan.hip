@@ -60,14 +60,7 @@ constexpr uint32_t AX_CMP = 160;      // bases a run compares per iteration at m
 constexpr uint32_t AX_CMPW = AX_CMP / 32;        // 2-bit words of one compare
 constexpr uint32_t AX_NGR = AX_CMPW + 1;         // granules that cover AX_CMP bases from any offset in the first
 constexpr uint32_t AX_CHK = 3;                   // 64-window class chunks of one run (<= AX_CMP - k + 1 windows)
-constexpr uint32_t AX_SPLIT = 16;     // a lane hands half of its window range to an idle lane when >= 2 x this is left
-#ifndef SPEQ_AX_SPLIT  // range hand-over to idle lanes (A/B knob: it adds lookups and VALU and did not shorten waves)
-#define SPEQ_AX_SPLIT 0
-#endif
-constexpr uint32_t AX_VWW = 3;        // valid-window words per lane (AX_CAP - k + 1 <= 192 windows)
-constexpr uint32_t AX_SCH = 64 * AX_CHUNKS;     // 16-base chunks of a wave's staged stream (every lane's segment)
-constexpr uint32_t AX_CSW = AX_SCH / 2 + 8;     // 2-bit code words (u64) of the stream, + read-past slack
-constexpr uint32_t AX_BSW = AX_SCH / 2 + 16;    // 1-bit-per-base words (u32) of the stream (bad / quality change)
+constexpr uint32_t AX_VWW = 4;        // valid-window words per lane (>= AX_CAP - k + 1 windows; 16 B per staged chunk)
 constexpr uint32_t AX_DEF = 896;      // deferred-window entries per wave (u16: lane | window << 6); 7.9 KB per wave
                                       // (5 blocks of 4 waves per CU)
 constexpr uint32_t AX_F = 4;          // deferred windows a lane tests against the filter per round trip
@@ -103,7 +96,7 @@ enum : uint32_t {
     AXS_QBYTES,          // single quality bytes loaded (local mode)
     AXS_RUN_TALLIED,     // windows tallied by runs
     AXS_RUN_GRANULES,    // granules (16 B) loaded by phase-1 runs
-    AXS_SPLITS,          // window ranges handed from a busy lane to an idle one
+    AXS_REFILLS,         // refills (staging of the next pieces of idle lanes; per wave)
     AXS_BUSY_1_4,        // phase-1 wave iterations with 1-4 busy lanes
     AXS_BUSY_5_16,       // ... 5-16
     AXS_BUSY_17_32,      // ... 17-32
@@ -425,13 +418,20 @@ __device__ __forceinline__ bool ax_probe(const AxView& A, const __amdgpu_buffer_
     return found;
 }
 
+// LDS of one wave (persistent lanes). Every lane owns a slot holding the read piece it works on; slot arrays are
+// transposed ([word][lane]), so lanes reading their own slots at different offsets never share a bank.
+//   codes  u32 [AX_CHUNKS][64]  2-bit bases of the piece from its 16-B-aligned start (slot position 0 = a16)
+//   vw     u64 [AX_VWW][64]     valid-window bits, read-relative (window j of the piece at bit j); while staging, the
+//                               bad-base bits of the refilling lanes, chunk c in 16 bits of the lane's own word c / 4
+//   chg    u16 [AX_CHUNKS][64]  (local) quality-change bits per slot position
+//   rbase  u64 [64]             (local) offset of the piece's first base in seq/qual
+//   off0s  u8 [64]              the piece's first base in its slot (a - a16)
+//   defl   u16 [AX_DEF]         deferred windows (lane | window << 6), defn u32[4] counters, ambf/ambd i32[64]
 template <int MODE>
 constexpr uint32_t ax_wave_bytes() {
-    // codes | vw | (local: quality-change stream, rbase) | deferred list (u16; the bad-base stream before phase 1) |
-    // counters | ambiguity | stream base per lane (u16) | task hand-over slots
-    static_assert(2u * AX_DEF >= 4u * AX_BSW, "the bad-base stream lives in the deferred list");
-    return 8u * AX_CSW + 8u * 64u * AX_VWW + (MODE == KM_LOCAL ? 4u * AX_BSW + 8u * 64u : 0u) + 2u * AX_DEF + 16u +
-           8u * 64u + 128u + 4u * 64u;
+    static_assert(8u * AX_VWW >= 2u * AX_CHUNKS, "the bad-base bits of a staged piece live in its valid-window words");
+    return 4u * AX_CHUNKS * 64u + 8u * AX_VWW * 64u + (MODE == KM_LOCAL ? 2u * AX_CHUNKS * 64u + 8u * 64u : 0u) +
+           64u + 2u * AX_DEF + 16u + 8u * 64u;
 }
 
 #ifndef SPEQ_AX_WPB  // waves per workgroup of k_scan_ax (A/B knob)
@@ -439,19 +439,25 @@ constexpr uint32_t ax_wave_bytes() {
 #endif
 constexpr uint32_t AX_WPB = SPEQ_AX_WPB, AX_THREADS = 64 * SPEQ_AX_WPB;
 #ifndef SPEQ_AX_SU  // staging: stream instructions per load batch (A/B knob)
-#define SPEQ_AX_SU 4
+#define SPEQ_AX_SU 2
 #endif
-#ifndef SPEQ_AX_MIN_WAVES  // minimum waves per SIMD the register allocator must allow, k <= 33 (A/B knob)
+#ifndef SPEQ_AX_MIN_WAVES  // minimum waves per SIMD the register allocator must allow, k <= 32 (A/B knob)
 #define SPEQ_AX_MIN_WAVES 4
 #endif
-#ifndef SPEQ_AX_MIN_WAVES4  // the same for 34 <= k <= 65
+#ifndef SPEQ_AX_MIN_WAVES4  // the same for 33 <= k <= 64
 #define SPEQ_AX_MIN_WAVES4 4
 #endif
-#ifndef SPEQ_AX_MIN_WAVES6  // and 66 <= k <= 128
+#ifndef SPEQ_AX_MIN_WAVES6  // and 65 <= k <= 128
 #define SPEQ_AX_MIN_WAVES6 4
 #endif
 #ifndef SPEQ_AX_MIN_WAVES_LOCAL  // local (Phred-weighted) mode, every k
 #define SPEQ_AX_MIN_WAVES_LOCAL 3
+#endif
+#ifndef SPEQ_AX_REFILL  // idle lanes that trigger a refill (staging of their next pieces) while others still run
+#define SPEQ_AX_REFILL 16
+#endif
+#ifndef SPEQ_AX_BLOCKED  // idle lanes waiting for their deferred windows that trigger the deferred-window pass
+#define SPEQ_AX_BLOCKED 16
 #endif
 template <int MODE, int HW>
 constexpr int ax_min_waves() {
@@ -459,8 +465,24 @@ constexpr int ax_min_waves() {
                             : (HW >= 4 ? SPEQ_AX_MIN_WAVES6 : (HW >= 2 ? SPEQ_AX_MIN_WAVES4 : SPEQ_AX_MIN_WAVES));
 }
 
+__device__ __forceinline__ uint32_t alignbit(uint32_t hi, uint32_t lo, uint32_t s) {  // ({hi, lo} >> (s & 31))[31:0]
+    return __builtin_amdgcn_alignbit(hi, lo, s);
+}
+__device__ __forceinline__ uint32_t lanes_below(unsigned long long m) {  // set bits of m below this lane
+    return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+
 // HW = 2-bit words of one k-mer (its hash): 1 (k <= 32), 2 (k <= 64), 4 (k <= 128); a phase-2 verification loads the
 // HW + 1 granules that cover k bases at any offset in the first.
+//
+// Persistent lanes: a wave takes the units (reads, or mate pairs) of its groups of 64 in order; every lane works on
+// one unit at a time, piece by piece (a read segment of at most AX_CAP bases; a pair's mates one after the other),
+// and takes the next unit from the wave's pool when it is done. A lane's chain of dependent round trips depends on
+// its read (one lookup and one run for a clean read; one more of each per mismatch against the representative's text
+// or per sequencing error), so lanes that finish early are refilled in batches (SPEQ_AX_REFILL lanes at a time:
+// coalesced staging of their next pieces) instead of idling until the wave's slowest read is done. Deferred windows
+// (phase 2) are resolved by the whole wave when SPEQ_AX_BLOCKED finished lanes wait for theirs (their slots hold the
+// bases the deferred entries refer to) or when the list fills up.
 template <int MODE, bool PAIRED, bool LDS_HIST, bool EM, int HW, bool STATS>
 __global__ __launch_bounds__(AX_THREADS, (ax_min_waves<MODE, HW>())) void k_scan_ax(AxView A, UnitSrc src,
                                                                                   unsigned long long* __restrict__ out_a,
@@ -478,17 +500,16 @@ __global__ __launch_bounds__(AX_THREADS, (ax_min_waves<MODE, HW>())) void k_scan
     const uint32_t qtab_bytes = MODE == KM_LOCAL ? QTAB_BYTES : 0u;
     constexpr uint32_t WAVE_BYTES = ax_wave_bytes<MODE>();
     unsigned char* wb = smem + hist_bytes + qtab_bytes + wid * WAVE_BYTES;
-    uint64_t* cs = reinterpret_cast<uint64_t*>(wb);                 // [AX_CSW] 2-bit codes of the wave's stream
-    uint64_t* vwl = cs + AX_CSW;                                     // [AX_VWW][64] valid windows per lane
-    uint32_t* cgs = reinterpret_cast<uint32_t*>(vwl + AX_VWW * 64u); // [AX_BSW] quality-change bits (local)
-    uint64_t* rbase = reinterpret_cast<uint64_t*>(cgs + (MODE == KM_LOCAL ? AX_BSW : 0u));  // [64] (local)
-    uint16_t* defl = reinterpret_cast<uint16_t*>(rbase + (MODE == KM_LOCAL ? 64u : 0u));  // [AX_DEF]
-    uint32_t* bss = reinterpret_cast<uint32_t*>(defl);               // [AX_BSW] bad-base bits (staging only)
-    uint32_t* defn = reinterpret_cast<uint32_t*>(defl + AX_DEF);     // [4]: entries, survivors
-    int32_t* ambf = reinterpret_cast<int32_t*>(defn + 4);            // [64] first counted group
-    int32_t* ambd = ambf + 64;                                       // [64] another group seen
-    uint16_t* sbs = reinterpret_cast<uint16_t*>(ambd + 64);          // [64] stream base of each lane's segment
-    uint32_t* spl = reinterpret_cast<uint32_t*>(sbs + 64);           // [64] tasks handed to idle lanes
+    uint32_t* codes = reinterpret_cast<uint32_t*>(wb);                       // [AX_CHUNKS][64]
+    uint64_t* vw = reinterpret_cast<uint64_t*>(codes + AX_CHUNKS * 64u);     // [AX_VWW][64]
+    uint16_t* bad16 = reinterpret_cast<uint16_t*>(vw);                       // staging: see bad_at
+    uint16_t* chg = reinterpret_cast<uint16_t*>(vw + AX_VWW * 64u);          // [AX_CHUNKS][64] (local)
+    uint64_t* rbase = reinterpret_cast<uint64_t*>(chg + (MODE == KM_LOCAL ? AX_CHUNKS * 64u : 0u));  // [64] (local)
+    uint8_t* off0s = reinterpret_cast<uint8_t*>(rbase + (MODE == KM_LOCAL ? 64u : 0u));              // [64]
+    uint16_t* defl = reinterpret_cast<uint16_t*>(off0s + 64);                // [AX_DEF]
+    uint32_t* defn = reinterpret_cast<uint32_t*>(defl + AX_DEF);             // [4]: entries, survivors, sums
+    int32_t* ambf = reinterpret_cast<int32_t*>(defn + 4);                    // [64] first counted group
+    int32_t* ambd = ambf + 64;                                               // [64] another group seen
 
     if (MODE == KM_LOCAL)
         for (uint32_t i = threadIdx.x; i < QLUT_LEN; i += AX_THREADS) {
@@ -500,6 +521,7 @@ __global__ __launch_bounds__(AX_THREADS, (ax_min_waves<MODE, HW>())) void k_scan
         }
     if (LDS_HIST)
         for (uint32_t i = threadIdx.x; i < hist_words; i += AX_THREADS) hA[i] = 0ull;
+    if (lane == 0) defn[0] = defn[1] = 0u;
     __syncthreads();
     unsigned long long* gU = out_a + 2;
 
@@ -513,12 +535,12 @@ __global__ __launch_bounds__(AX_THREADS, (ax_min_waves<MODE, HW>())) void k_scan
         __builtin_amdgcn_make_buffer_rsrc((void*)A.filt, (short)0, (int)(uint32_t)(A.nf * 8u), 0x00020000);
     const uint64_t NWV = (uint64_t)gridDim.x * AX_WPB;
     const uint64_t gw = (uint64_t)blockIdx.x * AX_WPB + wid;
-    const uint64_t nu = PAIRED ? src.n_units / 2 : src.n_units;
-    // groups of 64 reads (32 mate pairs), dealt to the waves round robin: the waves in flight sweep the read buffers
-    // front to back together (a wave owning one contiguous range ran the staging loads at a third of the HBM rate)
-    const uint64_t r_end = PAIRED ? 2 * nu : nu;
-    const uint64_t n_groups = (r_end + 63) / 64;
+    const uint64_t nu = PAIRED ? src.n_units / 2 : src.n_units;  // units: reads, or mate pairs
+    const uint64_t n_groups = (nu + 63) / 64;
     const uint32_t segw = AX_CAP - k + 1u;  // windows per segment
+    const uint32_t qt = 33u + src.cutoff;   // Phred+33 byte <= qt  <=>  clamp(q, 0, 41) <= cutoff (cutoff < 41)
+    const uint32_t qt4 = (qt > 0x7Fu ? 0x7Fu : qt) * 0x01010101u;
+    const uint32_t allbad = src.cutoff >= 41u ? 0x80808080u : 0u;  // every window fails the quality filter
 
     uint32_t t_cnt = 0, amb = 0;
     // diagnostic counters (STATS only; wave-level ones are counted by lane 0)
@@ -535,528 +557,111 @@ __global__ __launch_bounds__(AX_THREADS, (ax_min_waves<MODE, HW>())) void k_scan
             if (MODE == KM_LOCAL) atomicAdd(&out_w[g], wsum);
         }
     };
-
-    for (uint64_t grp = gw; grp < n_groups; grp += NWV) {
-        const uint64_t r0 = grp * 64;
-        const uint64_t r = r0 + lane;
-        const bool has = r < r_end;
-        const uint64_t rb = has ? src.off[r] : 0, re = has ? src.off[r + 1] : 0;
-        const uint64_t L = re - rb;
-        const uint64_t W = L >= k ? L - k + 1 : 0;
-        const uint32_t nseg = (uint32_t)((W + segw - 1) / segw);
-        // the wave's largest segment count, bit by bit from the top (ballots: no shuffle address registers, which
-        // the compiler hoists out of the loops and spills)
-        uint32_t nseg_max = 0;
-        if (__ballot(nseg > 1u) == 0) {
-            nseg_max = __ballot(nseg != 0u) != 0 ? 1u : 0u;
-        } else {
-            for (int b = 31; b >= 0; --b) {  // greedy: set bit b when some lane reaches the candidate
-                const uint32_t cand = nseg_max | (1u << b);
-                if (__ballot(nseg >= cand) != 0) nseg_max = cand;
-            }
+    // 32 bases (64 bits) of slot o from slot position pos
+    auto slot64 = [&](uint32_t o, uint32_t pos) -> uint64_t {
+        const uint32_t d = pos >> 4, sh = 2u * (pos & 15u);
+        const uint32_t w0 = d < AX_CHUNKS ? codes[d * 64u + o] : 0u;
+        const uint32_t w1 = d + 1u < AX_CHUNKS ? codes[(d + 1u) * 64u + o] : 0u;
+        const uint32_t w2 = d + 2u < AX_CHUNKS ? codes[(d + 2u) * 64u + o] : 0u;
+        return u64of(alignbit(w1, w0, sh), alignbit(w2, w1, sh));
+    };
+    auto read_words = [&](uint32_t o, uint32_t pos, uint64_t(&w)[HW]) {  // HW code words of slot o at pos
+#pragma unroll
+        for (int i = 0; i < HW; ++i) w[i] = slot64(o, pos + 32u * (uint32_t)i);
+    };
+    auto vbits = [&](uint32_t o, uint32_t b) -> uint64_t {  // read o's valid-window bits b .. b + 63 (0 past the end)
+        const uint32_t w0 = b >> 6, s6 = b & 63u;
+        const uint64_t lo = w0 < AX_VWW ? vw[w0 * 64u + o] : 0ull;
+        const uint64_t hi = w0 + 1u < AX_VWW ? vw[(w0 + 1u) * 64u + o] : 0ull;
+        return funnel(lo, hi, s6);
+    };
+    auto next_valid = [&](uint32_t o, uint32_t j, uint32_t end) -> uint32_t {  // first valid window of read o in
+        for (uint32_t b = j; b < end; b += 64u) {                             // [j, end), else end
+            const uint64_t v = vbits(o, b);
+            if (v) return min(b + (uint32_t)__builtin_ctzll(v), end);
         }
-        int32_t af = -1, ad = 0;  // ambiguity state of this lane's read
-        for (uint32_t seg = 0; seg < nseg_max; ++seg) {
-            // ---- stage segment `seg` (windows [s, s + wend) of each lane's read, bases [s, s + sb)) as ONE stream
-            // of 16-base chunks: lane o's chunks are [pre_o, pre_o + nch_o), so its base b sits at stream position
-            // 16 pre_o + b (b counted from the chunk-aligned a16). The wave decodes the stream 64 chunks per
-            // instruction, each lane a whole chunk found by a binary search over the lanes' chunk offsets: the 16-B
-            // loads of one instruction cover a few consecutive reads (coalesced) instead of 64 reads 150 B apart.
-            const bool in_seg = seg < nseg;
-            const uint64_t s = (uint64_t)seg * segw;
-            const uint32_t sb = in_seg ? (uint32_t)(L - s < AX_CAP ? L - s : AX_CAP) : 0u;
-            const uint32_t wend = in_seg ? (uint32_t)(W - s < segw ? W - s : segw) : 0u;
-            const uint64_t a = rb + s;                       // first base (offset into seq/qual)
-            const uint64_t a16 = a & ~15ull;
-            const uint32_t off0 = (uint32_t)(a - a16);
-            const uint32_t nch = in_seg ? (off0 + sb + 15u) / 16u : 0u;
-            // exclusive prefix sum of the chunk counts (< 16) by bit planes: per bit, a ballot and a count of the lanes
-            // below this one (mbcnt)
-            static_assert(AX_CHUNKS < 16, "chunk counts in four bits");
-            uint32_t pre = 0, nch_tot = 0;
-#pragma unroll
-            for (uint32_t b = 0; b < 4; ++b) {
-                const unsigned long long bb = __ballot((nch >> b) & 1u);
-                pre += __builtin_amdgcn_mbcnt_hi((uint32_t)(bb >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bb, 0u)) << b;
-                nch_tot += (uint32_t)__popcll(bb) << b;
-            }
-            if (STATS) {
-                s_ch += nch;
-                s_seg += in_seg ? 1u : 0u;
-            }
-            const uint32_t sbase = 16u * pre + off0;        // stream position of the segment's first base
-            const uint64_t gofs = a16 - 16ull * pre;        // byte offset of stream chunk c in this lane's frame: + 16 c
-            const uint32_t qt = 33u + src.cutoff;  // Phred+33 byte <= qt  <=>  clamp(q, 0, 41) <= cutoff (cutoff < 41)
-            const uint32_t qt4 = (qt > 0x7Fu ? 0x7Fu : qt) * 0x01010101u;
-            const uint32_t allbad = src.cutoff >= 41u ? 0x80808080u : 0u;  // every window fails the quality filter
-            uint32_t qcarry = 0;  // local: last quality dword of the previous instruction's lane 63
-            constexpr uint32_t SU = SPEQ_AX_SU;  // stream instructions whose loads are in flight together
-            for (uint32_t c0 = 0; c0 < nch_tot; c0 += 64u * SU) {
-                uint4 sv[SU], qv[SU];
-#pragma unroll
-                for (uint32_t u = 0; u < SU; ++u) {
-                    const uint32_t c = min(c0 + 64u * u + lane, nch_tot - 1u);
-                    uint32_t o = 0;  // the lane whose segment holds chunk c: the last o with pre_o <= c
-#pragma unroll
-                    for (uint32_t d = 32; d >= 1; d >>= 1)
-                        o = ((uint32_t)__shfl((int)pre, (int)(o + d)) <= c) ? o + d : o;
-                    const uint64_t go = (uint64_t)__shfl((long long)gofs, (int)o) + 16ull * c;
-                    sv[u] = *reinterpret_cast<const uint4*>(src.seq + go);
-                    qv[u] = *reinterpret_cast<const uint4*>(src.qual + go);
-                }
-#pragma unroll
-                for (uint32_t u = 0; u < SU; ++u) {
-                    const uint32_t c = c0 + 64u * u + lane;
-                    const uint32_t sd[4] = {sv[u].x, sv[u].y, sv[u].z, sv[u].w};
-                    const uint32_t qd[4] = {qv[u].x, qv[u].y, qv[u].z, qv[u].w};
-                    uint32_t qprev = 0;
-                    if (MODE == KM_LOCAL) {  // the byte before the chunk: the previous chunk's last quality
-                        const uint32_t up = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)qv[u].w, 0x138, 0xF, 0xF, false);
-                        qprev = lane == 0 ? qcarry : up;
-                        qcarry = __builtin_amdgcn_readlane(qv[u].w, 63);
-                    }
-                    uint32_t codes = 0, bad = 0, chg = 0;
-#pragma unroll
-                    for (int i = 0; i < 4; ++i) {
-                        const uint32_t x = sd[i] | 0x20202020u;  // lower case
-                        const uint32_t c4 = ((x >> 1) ^ (x >> 2)) & 0x03030303u;  // a c g t/u -> 0 1 2 3
-                        codes |= ((c4 | (c4 >> 6) | (c4 >> 12) | (c4 >> 18)) & 0xFFu) << (8 * i);
-                        const uint32_t canon = __builtin_amdgcn_perm(0u, 0x74676361u, c4);  // the letter of that code
-                        const uint32_t okb = zero_bytes(x ^ canon) | zero_bytes(x ^ 0x75757575u);  // ACGT or U
-                        const uint32_t y = qd[i];
-                        const uint32_t badq = (((0x80808080u | qt4) - (y & 0x7F7F7F7Fu)) & ~y & 0x80808080u) | allbad;
-                        bad |= flags4((~okb & 0x80808080u) | badq) << (4 * i);
-                        if (MODE == KM_LOCAL) {
-                            const uint32_t prev = (y << 8) | (qprev >> 24);
-                            chg |= flags4(~zero_bytes(y ^ prev) & 0x80808080u) << (4 * i);
-                            qprev = y;
-                        }
-                    }
-                    if (c < nch_tot) {
-                        reinterpret_cast<uint32_t*>(cs)[c] = codes;
-                        reinterpret_cast<uint16_t*>(bss)[c] = (uint16_t)bad;
-                        if (MODE == KM_LOCAL) reinterpret_cast<uint16_t*>(cgs)[c] = (uint16_t)chg;
-                    }
-                }
-            }
-            wave_sync();
-            // this lane's bad-base bits (256 from a16; chunks past its segment are bad)
-            uint64_t badw[4];
-            {
-                const uint32_t d0 = pre >> 1, sh = 16u * (pre & 1u);
-                uint32_t bw[9];
-#pragma unroll
-                for (int i = 0; i < 9; ++i) bw[i] = bss[min(d0 + (uint32_t)i, AX_BSW - 1u)];
-#pragma unroll
-                for (int i = 0; i < 4; ++i) {
-                    const uint64_t lo = (uint64_t)bw[2 * i] | ((uint64_t)bw[2 * i + 1] << 32);
-                    const uint64_t hi = (uint64_t)bw[2 * i + 2];
-                    uint64_t v = sh ? ((lo >> sh) | (hi << (64u - sh))) : lo;
-                    const uint32_t b0 = 64u * (uint32_t)i, nb = 16u * nch;  // bits of this lane's chunks
-                    if (nb <= b0) v = ~0ull;
-                    else if (nb < b0 + 64u) v |= ~0ull << (nb - b0);
-                    badw[i] = v;
-                }
-            }
-            // valid windows: AND of k consecutive "good" bits (doubling), then shifted to the read's first base
-            uint64_t ok[4] = {~badw[0], ~badw[1], ~badw[2], ~badw[3]};
-            for (uint32_t len = 1; len < k;) {
-                const uint32_t sft = min(len, k - len);
-                const uint32_t ws = sft >> 6, bs = sft & 63u;
-                uint64_t nx[4];
-#pragma unroll
-                for (int i = 0; i < 4; ++i) {
-                    uint64_t lo = 0ull, hi = 0ull;  // ok[i + ws], ok[i + ws + 1] (zero past the end), no indexing
-#pragma unroll
-                    for (int t = 0; t < 4; ++t) {
-                        lo = (uint32_t)(t - i) == ws ? ok[t] : lo;
-                        hi = (uint32_t)(t - i) == ws + 1u ? ok[t] : hi;
-                    }
-                    nx[i] = ok[i] & funnel(lo, hi, bs);
-                }
-#pragma unroll
-                for (int i = 0; i < 4; ++i) ok[i] = nx[i];
-                len += sft;
-            }
-#pragma unroll
-            for (uint32_t i = 0; i < AX_VWW; ++i) {
-                const uint64_t lo = i < 4 ? ok[i] : 0ull, hi = i + 1 < 4 ? ok[i + 1] : 0ull;
-                uint64_t v = funnel(lo, hi, off0);
-                const uint32_t bit0 = 64u * i;
-                if (wend <= bit0) v = 0;
-                else if (wend < bit0 + 64u) v &= (1ull << (wend - bit0)) - 1ull;
-                vwl[i * 64u + lane] = v;
-                t_cnt += (uint32_t)__popcll(v);
-            }
-            if (MODE == KM_LOCAL) rbase[lane] = a;
-            sbs[lane] = (uint16_t)sbase;
-            ambf[lane] = af;  // the read's ambiguity state, updated by every lane that tallies windows of it
-            ambd[lane] = ad;
-            wave_sync();  // the bad-base stream (in the deferred list) is read by every lane before the list is reset
-            if (lane == 0) {
-                defn[0] = 0;
-                defn[1] = 0;
-            }
-            wave_sync();
+        return end;
+    };
+    // Phred weight of a window whose first quality byte is at qbase (fm_scanner.cpp:454)
+    auto weight = [&](const uint8_t* qbase, bool uniform, uint32_t qcur) -> double {
+        if (uniform) return wtab[qcur];
+        double x = 1.0;
+        for (uint32_t i = 0; i < k; ++i) {
+            int q = (int)qbase[i] - 33;
+            q = q < 0 ? 0 : (q > 41 ? 41 : q);
+            const double2 t = qtab[q];
+            x = div_rn(x, t.x, t.y);  // == x / t.x
+        }
+        if (STATS) s_qb += k;
+        return x;
+    };
+    // quality-change bits of slot o over slot positions [x, x + len) all zero (local mode)
+    auto chg_zero = [&](uint32_t o, uint32_t x, uint32_t len) -> bool {
+        uint32_t left = len;
+        bool u = true;
+        while (left) {
+            const uint32_t w = x >> 4, sh = x & 15u, span = min(16u - sh, left);
+            const uint32_t mk = (1u << span) - 1u;
+            u = u && (w >= AX_CHUNKS || (((uint32_t)chg[w * 64u + o] >> sh) & mk) == 0);
+            x += span;
+            left -= span;
+        }
+        return u;
+    };
 
-            // per-lane readers of the staged stream
-            auto read_words = [&](uint32_t base, uint64_t(&w)[HW]) {  // HW code words at stream position `base`
-                const uint32_t idx = base >> 5, sh = 2u * (base & 31u);
-                uint64_t raw[HW + 1];
-#pragma unroll
-                for (int i = 0; i <= HW; ++i) raw[i] = cs[min(idx + (uint32_t)i, AX_CSW - 1u)];
-#pragma unroll
-                for (int i = 0; i < HW; ++i) w[i] = funnel(raw[i], raw[i + 1], sh);
-            };
-            auto vbits = [&](uint32_t o, uint32_t b) -> uint64_t {  // read o's valid-window bits b .. b + 63 (0 past
-                const uint32_t w0 = b >> 6, s6 = b & 63u;                 // the end)
-                const uint64_t lo = w0 < AX_VWW ? vwl[w0 * 64u + o] : 0ull;
-                const uint64_t hi = w0 + 1u < AX_VWW ? vwl[(w0 + 1u) * 64u + o] : 0ull;
-                return funnel(lo, hi, s6);
-            };
-            auto next_valid = [&](uint32_t o, uint32_t j, uint32_t end) -> uint32_t {  // first valid window of read o
-                for (uint32_t b = j; b < end; b += 64u) {                             // in [j, end), else end
-                    const uint64_t v = vbits(o, b);
-                    if (v) return min(b + (uint32_t)__builtin_ctzll(v), end);
-                }
-                return end;
-            };
-            auto defer_push = [&](uint32_t o, uint32_t jj) -> bool {
-                const uint32_t slot = atomicAdd(&defn[0], 1u);
-                if (slot < AX_DEF) defl[slot] = (uint16_t)(o | (jj << 6));
-                return slot < AX_DEF;
-            };
-            // Phred weight of a window whose first quality byte is at qbase (fm_scanner.cpp:454)
-            auto weight = [&](const uint8_t* qbase, bool uniform, uint32_t qcur) -> double {
-                if (uniform) return wtab[qcur];
-                double x = 1.0;
-                for (uint32_t i = 0; i < k; ++i) {
-                    int q = (int)qbase[i] - 33;
-                    q = q < 0 ? 0 : (q > 41 ? 41 : q);
-                    const double2 t = qtab[q];
-                    x = div_rn(x, t.x, t.y);  // == x / t.x
-                }
-                if (STATS) s_qb += k;
-                return x;
-            };
-            // quality-change bits of the stream over positions [x, x + len) all zero (local mode)
-            auto chg_zero = [&](uint32_t x, uint32_t len) -> bool {
-                uint32_t left = len;
-                bool u = true;
-                while (left) {
-                    const uint32_t w = x >> 5, sh = x & 31u, span = min(32u - sh, left);
-                    const uint32_t mk = span == 32u ? ~0u : ((1u << span) - 1u);
-                    u = u && (w >= AX_BSW || ((cgs[w] >> sh) & mk) == 0);
-                    x += span;
-                    left -= span;
-                }
-                return u;
-            };
+    // ---- the lane's unit and piece
+    bool has_unit = false;     // working on a unit (until it is finalized)
+    bool last_piece = true;    // the current piece is the unit's last
+    uint64_t rd = 0;           // current read (index into off)
+    uint32_t mate = 0, seg = 0, nseg = 0;
+    uint64_t rb = 0, L = 0, W = 0;  // current read: first base, length, windows
+    int32_t af = -1, ad = 0;   // ambiguity state of the unit
+    bool hasdef = false;       // deferred windows of this lane's piece are in the wave's list
+    // ---- the wave's pool: units of groups gw, gw + NWV, ... (uniform)
+    uint64_t pool = 0;         // units taken so far (flat index over the wave's groups)
+    const uint64_t my_groups = gw < n_groups ? (n_groups - gw + NWV - 1) / NWV : 0;
+    const uint64_t pool_n = my_groups * 64;
+    auto pool_unit = [&](uint64_t flat) -> uint64_t {  // the unit of flat pool index `flat`, or nu (none)
+        const uint64_t u = (gw + (flat >> 6) * NWV) * 64 + (flat & 63u);
+        return (flat < pool_n && u < nu) ? u : nu;
+    };
+    // ---- phase-1 state of the current piece
+    uint32_t wend = 0;         // windows of the piece
+    uint32_t off0 = 0;         // first base of the piece in the slot
+    uint64_t ta = 0;           // first base of the piece in seq/qual (local mode)
+    uint32_t j = 0;
+    uint32_t st = 2u;          // 0: look window j up, 1: extend from text position p, 2: idle
+    bool verify = false;       // st 1: p came from the anchor table (window j itself not compared yet)
+    uint32_t p = 0;            // text position of window j (st 1)
+    uint32_t gt = 0;           // group of p's text (st 1)
+    int32_t last_mm = -1;      // base (relative to the piece) of the last observed mismatch
+    uint32_t pb = 0, ps = 0;   // probe position of the current lookup (bucket, first slot)
+    bool resume = false;       // continue the current lookup at (pb, ps): full bucket, or failed verification
+    bool run_phase = true;     // this wave iteration extends runs (else: looks windows up)
 
-            // ---- phase 1: one task per lane (a window range [j, jend) of read o; first its own read), one memory
-            // round trip per iteration: a lane either probes the anchor table (its candidate is compared in the next
-            // iteration) or extends a run over the rest of its range (at most AX_CMP bases; a clean 150-bp read: one
-            // lookup and one run). A wave runs as long as its slowest lane, so a lane about to look a window up
-            // hands the second half of its range to an idle lane when there is one: the slow reads (mismatches
-            // against representatives of other variants, sequencing errors) are worked on by several lanes at once.
-            uint32_t o = lane;         // the read (lane of the wave that staged it) this lane works on
-            uint32_t jend = wend;      // end of this lane's window range
-            uint32_t tsb = sbase;      // read o's stream base
-            uint64_t ta = a;           // read o's first base in seq/qual (local mode)
-            uint32_t j = 0;
-            uint32_t st = wend > 0 ? 0u : 2u;  // 0: look window j up, 1: extend from text position p, 2: done
-            bool verify = false;       // st 1: p came from the anchor table (window j itself not compared yet)
-            uint32_t p = 0;            // text position of window j (st 1)
-            uint32_t gt = 0;           // group of p's text (st 1)
-            int32_t last_mm = -1;      // base (relative to the segment) of the last observed mismatch
-            uint32_t pb = 0, ps = 0;   // probe position of the current lookup (bucket, first slot)
-            bool resume = false;       // continue the current lookup at (pb, ps): full bucket, or failed verification
-            bool run_phase = true;     // this wave iteration extends runs (else: looks windows up); starts with lookups
-            for (;;) {
-                if (st == 0u) {
-                    j = next_valid(o, j, jend);
-                    if (j >= jend) st = 2u;
-                }
-                const unsigned long long busy = __ballot(st != 2u);
-                if (busy == 0) break;
-                if (STATS && lane == 0) {
-                    const uint32_t nb = (uint32_t)__popcll(busy);
-                    s_b4 += nb <= 4u ? 1u : 0u;
-                    s_b16 += (nb > 4u && nb <= 16u) ? 1u : 0u;
-                    s_b32 += (nb > 16u && nb <= 32u) ? 1u : 0u;
-                    s_b64 += nb > 32u ? 1u : 0u;
-                }
-                if (SPEQ_AX_SPLIT && busy != ~0ull) {  // idle lanes: lanes about to look up with >= 2 AX_SPLIT windows left hand half over
-                    const unsigned long long idle = ~busy;
-                    const bool can = st == 0u && jend - j >= 2u * AX_SPLIT;
-                    const unsigned long long cm = __ballot(can);
-                    if (cm != 0) {
-                        const uint32_t n = min((uint32_t)__popcll(idle), (uint32_t)__popcll(cm));
-                        const uint32_t rc =
-                            __builtin_amdgcn_mbcnt_hi((uint32_t)(cm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)cm, 0u));
-                        const uint32_t ri = __builtin_amdgcn_mbcnt_hi((uint32_t)(idle >> 32),
-                                                                      __builtin_amdgcn_mbcnt_lo((uint32_t)idle, 0u));
-                        if (can && rc < n) {
-                            const uint32_t mid = j + (jend - j) / 2u;
-                            spl[rc] = o | (mid << 6) | (jend << 16);
-                            jend = mid;
-                        }
-                        wave_sync();
-                        if (st == 2u && ri < n) {
-                            const uint32_t t = spl[ri];
-                            o = t & 63u;
-                            j = (t >> 6) & 1023u;
-                            jend = t >> 16;
-                            tsb = sbs[o];
-                            if (MODE == KM_LOCAL) ta = rbase[o];
-                            st = 0u;
-                            verify = false;
-                            resume = false;
-                            last_mm = -1;
-                            j = next_valid(o, j, jend);
-                            if (j >= jend) st = 2u;
-                            if (STATS) s_spl += 1u;
-                        }
-                        wave_sync();
-                    }
-                }
-                // one kind of work per iteration, alternating (a lookup is followed by a run and a run by a lookup, so
-                // a lane rarely waits): the wave executes the lookup code or the run code, not both under exec masks
-                // (the kernel is bound by VALU issue, profiles/r03), and a kind no lane needs is skipped
-                const bool want_lk = __ballot(st == 0u) != 0, want_rn = __ballot(st == 1u) != 0;
-                run_phase = run_phase ? !want_lk : want_rn;
-                const bool lk = st == 0u && !run_phase, rn = st == 1u && run_phase;
-                const bool any_lk = !run_phase, any_rn = run_phase;
-                if (STATS) {
-                    s_iter += lane == 0 ? 1u : 0u;
-                    s_lkw += (lane == 0 && any_lk) ? 1u : 0u;
-                    s_rnw += (lane == 0 && any_rn) ? 1u : 0u;
-                    s_lk += lk ? 1u : 0u;
-                    s_rn += rn ? 1u : 0u;
-                }
-                // ---- this iteration's loads: a bucket (lookup lanes), the run's granules (run lanes), the quality
-                // of window j (local mode); a group is issued only when some lane of the wave needs it
-                u32x4 q0 = {0u, 0u, 0u, 0u}, q1 = q0, q2 = q0, q3 = q0;
-                uint32_t fp = 0;
-                if (any_lk) {
-                    uint64_t ra[HW];
-                    read_words(tsb + j, ra);
-                    const uint64_t h = ax_hash<HW>(ra, k);
-                    fp = ax_fp(h);
-                    if (lk && !resume) {
-                        pb = ax_bucket(h, A.nb);
-                        ps = 0;
-                    }
-                    const uint32_t boff = lk ? pb * 64u : AX_OOB;
-                    q0 = __builtin_amdgcn_raw_buffer_load_b128(rs_atab, boff, 0, 0);
-                    q1 = __builtin_amdgcn_raw_buffer_load_b128(rs_atab, boff + 16u, 0, 0);
-                    q2 = __builtin_amdgcn_raw_buffer_load_b128(rs_atab, boff + 32u, 0, 0);
-                    q3 = __builtin_amdgcn_raw_buffer_load_b128(rs_atab, boff + 48u, 0, 0);
-                }
-                // a run compares the rest of the segment from window j (at most AX_CMP bases): the granules that
-                // cover it from p's granule on, the others with out-of-range offsets
-                const uint32_t cl = min(jend - j + k - 1u, AX_CMP);
-                u32x4 gr[AX_NGR];
-#pragma unroll
-                for (uint32_t i = 0; i < AX_NGR; ++i) gr[i] = q0;
-                uint32_t qj = 0;
-                if (any_rn) {
-                    const uint32_t ng = rn ? ((p & 31u) + cl + 31u) >> 5 : 0u;
-                    const uint32_t goff = (p >> 5) * 16u;
-#pragma unroll
-                    for (uint32_t i = 0; i < AX_NGR; ++i)
-                        gr[i] = __builtin_amdgcn_raw_buffer_load_b128(rs_gran, i < ng ? goff + 16u * i : AX_OOB, 0, 0);
-                    if (STATS) s_rg += ng;
-                    if (MODE == KM_LOCAL) {
-                        qj = src.qual[ta + (rn ? j : 0u)];
-                        if (STATS) s_qb += rn ? 1u : 0u;
-                    }
-                }
+    auto start_read = [&](uint64_t r) {
+        rd = r;
+        rb = src.off[r];
+        L = src.off[r + 1] - rb;
+        W = L >= k ? L - k + 1 : 0;
+        nseg = W ? (uint32_t)((W + segw - 1) / segw) : 1u;
+        seg = 0;
+    };
 
-                // ---- lookup lanes: resolve the bucket
-                if (lk) {
-                    uint32_t slot = 0, cp = 0, cg = 0;
-                    const uint32_t res = ax_resolve(q0, q1, q2, q3, fp, ps, slot, cp, cg);
-                    if (res == 1u) {  // candidate: compared with the text in the next iteration
-                        p = cp;
-                        gt = cg;
-                        ps = slot;
-                        st = 1u;
-                        verify = true;
-                        resume = false;
-                    } else if (res == 0u) {
-                        // absent: defer the windows that share the mismatch (or the next k - 1), skip past them
-                        resume = false;
-                        uint32_t dend = (last_mm >= (int32_t)j && last_mm < (int32_t)(j + k)) ? (uint32_t)last_mm
-                                                                                               : j + k - 1u;
-                        dend = min(dend, jend - 1u);
-                        // the valid windows of (j, dend] as two 64-bit masks (dend - j <= k - 1 <= 127)
-                        const uint32_t span = dend - j;
-                        uint64_t dm0 = vbits(o, j + 1u), dm1 = span > 64u ? vbits(o, j + 65u) : 0ull;
-                        dm0 &= span >= 64u ? ~0ull : ((1ull << span) - 1ull);
-                        if (span > 64u) dm1 &= span - 64u >= 64u ? ~0ull : ((1ull << (span - 64u)) - 1ull);
-                        const uint32_t cnt = (uint32_t)__popcll(dm0) + (uint32_t)__popcll(dm1);
-                        bool ok_def = true;
-                        if (cnt) {
-                            const uint32_t slot0 = atomicAdd(&defn[0], cnt);
-                            ok_def = slot0 + cnt <= AX_DEF;
-                            if (ok_def) {
-                                uint32_t sl = slot0;
-                                for (uint64_t t = dm0; t; t &= t - 1)
-                                    defl[sl++] = (uint16_t)(o | ((j + 1u + (uint32_t)__builtin_ctzll(t)) << 6));
-                                for (uint64_t t = dm1; t; t &= t - 1)
-                                    defl[sl++] = (uint16_t)(o | ((j + 65u + (uint32_t)__builtin_ctzll(t)) << 6));
-                                if (STATS) s_def += cnt;
-                            } else {  // no room: the windows stay with this lane; void the slots reserved below the end
-                                for (uint32_t sl = slot0; sl < AX_DEF && sl < slot0 + cnt; ++sl) defl[sl] = AX_VOID;
-                            }
-                        }
-                        j = ok_def ? dend + 1u : j + 1u;
-                        last_mm = -1;
-                    } else {  // full bucket without the key or an empty slot: the next bucket
-                        pb = pb + 1u == (uint32_t)A.nb ? 0u : pb + 1u;
-                        ps = 0;
-                        resume = true;
-                    }
-                }
-
-                // ---- run lanes: compare read [j, j + cl) with text [p, p + cl), classify the matched windows
-                if (any_rn && rn) {
-                    const uint32_t s5 = p & 31u, sh = 2u * s5;
-                    uint32_t e = cl;  // first mismatching base (cl: none)
-                    {
-                        const uint32_t base = tsb + j, idx = base >> 5, rsh = 2u * (base & 31u);
-                        uint64_t cur = cs[min(idx, AX_CSW - 1u)];
-#pragma unroll
-                        for (uint32_t i = 0; i < AX_CMPW; ++i) {
-                            const uint64_t nxt = cs[min(idx + i + 1u, AX_CSW - 1u)];
-                            const uint64_t rw = funnel(cur, nxt, rsh);
-                            cur = nxt;
-                            const uint64_t tw =
-                                funnel(u64of(gr[i][0], gr[i][1]), u64of(gr[i + 1][0], gr[i + 1][1]), sh);
-                            uint64_t x = rw ^ tw;
-                            const uint32_t b0 = 32u * i;
-                            if (cl <= b0) x = 0;
-                            else if (cl < b0 + 32u) x &= (1ull << (2u * (cl - b0))) - 1ull;
-                            const uint32_t ei = b0 + ((uint32_t)__builtin_ctzll(x | (1ull << 63)) >> 1);
-                            e = (x != 0 && ei < e) ? ei : e;
-                        }
-                    }
-                    if (verify && e < k) {  // fingerprint collision: resume probing after that slot
-                        st = 0u;
-                        resume = true;
-                        ++ps;
-                    } else {
-                        uint32_t R = e - (k - 1u);  // e >= k - 1: a candidate matched k bases, a run k - 1
-                        R = min(R, jend - j);
-                        // the windows [0, R) in 64-window chunks: class planes of windows p + 64c .. (bits s5 + 64c ..
-                        // of the granules' planes). The run stops at the first END window (the text ends: the next
-                        // windows belong to another text, looked up again) or SENT window of a valid read window (an
-                        // N in the text: looked up); windows before it are tallied to the run's group
-                        uint32_t d0 = R, cnt = 0;
-                        bool cut = false, cut_end = false;
-                        uint64_t ownc[AX_CHK];
-#pragma unroll
-                        for (uint32_t c = 0; c < AX_CHK; ++c) {
-                            const uint32_t w0 = 64u * c;
-                            const uint64_t mRc = R <= w0 ? 0ull : (R - w0 >= 64u ? ~0ull : ((1ull << (R - w0)) - 1ull));
-                            const uint64_t hp0 = 2 * c + 2 < AX_NGR ? (uint64_t)gr[(2 * c + 2) % AX_NGR][2] : 0ull;
-                            const uint64_t hp1 = 2 * c + 2 < AX_NGR ? (uint64_t)gr[(2 * c + 2) % AX_NGR][3] : 0ull;
-                            const uint64_t P0 = funnel(u64of(gr[2 * c][2], gr[2 * c + 1][2]), hp0, s5);
-                            const uint64_t P1 = funnel(u64of(gr[2 * c][3], gr[2 * c + 1][3]), hp1, s5);
-                            const uint64_t m = vbits(o, j + w0) & mRc;  // the chunk's valid read windows in the run
-                            const uint64_t stop = P1 & (P0 | m) & mRc;
-                            const uint64_t below = cut ? 0ull : (stop ? ((stop & (0ull - stop)) - 1ull) : ~0ull);
-                            const uint64_t own = ~P0 & ~P1 & m & below;
-                            cnt += (uint32_t)__popcll(own);
-                            ownc[c] = own;
-                            if (EM) {  // multi-group windows of the run: the EM histogram
-                                uint64_t todo = P0 & ~P1 & m & below;
-                                while (todo) {
-                                    const uint32_t d = (uint32_t)__builtin_ctzll(todo);
-                                    todo &= todo - 1;
-                                    const uint32_t lo = A.mlo[p + w0 + d];
-                                    atomicAdd(&src.em_mult[lo], 1u);
-                                    src.em_hi[lo] = A.mhi[lo];
-                                }
-                            }
-                            if (!cut && stop) {
-                                const uint32_t t = (uint32_t)__builtin_ctzll(stop);
-                                d0 = w0 + t;
-                                cut_end = ((P0 >> t) & 1ull) != 0;
-                                cut = true;
-                            }
-                        }
-                        if (STATS) {
-                            s_rwin += d0;
-                            s_tal += cnt;
-                        }
-                        if (cnt) {
-                            double wsum = 0.0;
-                            if (MODE == KM_LOCAL) {
-                                // one quality for the whole cut run when no base in (j, j + d0 - 1 + k) changes it
-                                if (chg_zero(tsb + j + 1u, d0 + k - 2u)) {
-                                    int q = (int)qj - 33;
-                                    q = q < 0 ? 0 : (q > 41 ? 41 : q);
-                                    wsum = (double)cnt * wtab[q];
-                                } else {
-#pragma unroll
-                                    for (uint32_t c = 0; c < AX_CHK; ++c) {
-                                        uint64_t todo = ownc[c];
-                                        while (todo) {
-                                            const uint32_t d = 64u * c + (uint32_t)__builtin_ctzll(todo);
-                                            todo &= todo - 1;
-                                            const uint32_t jj = j + d;
-                                            const uint8_t* qb = src.qual + ta + jj;
-                                            int q = (int)qb[0] - 33;
-                                            q = q < 0 ? 0 : (q > 41 ? 41 : q);
-                                            wsum += weight(qb, chg_zero(tsb + jj + 1u, k - 1u), (uint32_t)q);
-                                            if (STATS) s_qb += 1u;
-                                        }
-                                    }
-                                }
-                            }
-                            add_count(gt, cnt, wsum);
-                            const int32_t old = atomicCAS(&ambf[o], -1, (int32_t)gt);
-                            if (old != -1 && old != (int32_t)gt) ambd[o] = 1;
-                        }
-                        // next state
-                        verify = false;
-                        if (d0 < R) {
-                            if (cut_end) {  // END: look the window up (its k-mer may occur elsewhere)
-                                j += d0;
-                                st = 0u;
-                                resume = false;
-                                last_mm = -1;
-                            } else if (defer_push(o, j + d0)) {  // SENT: matched bases, but no valid text window
-                                if (STATS) s_def += 1u;
-                                j += d0 + 1u;
-                                p += d0 + 1u;
-                                st = 1u;
-                            } else {  // the list is full: look that window up now
-                                j += d0;
-                                st = 0u;
-                                resume = false;
-                                last_mm = -1;
-                            }
-                        } else {
-                            const bool mism = e < cl;  // the run ended at a mismatch (base j + e)
-                            if (mism && R < jend - j) last_mm = (int32_t)(j + e);
-                            j += R;
-                            p += R;
-                            st = (mism || R == 0u) ? 0u : 1u;
-                            if (st == 0u) resume = false;
-                        }
-                        if (j >= jend) st = 2u;
-                    }
-                }
-            }
-
+    for (;;) {
+        // ================= housekeeping (wave-uniform decisions) =================
+        const unsigned long long idle = __ballot(st == 2u);
+        const unsigned long long blk = __ballot(st == 2u && hasdef);
+        const unsigned long long busy = ~idle;
+        const uint32_t n_def = __builtin_amdgcn_readfirstlane(defn[0]);
+        if (blk != 0 && ((uint32_t)__popcll(blk) >= SPEQ_AX_BLOCKED || busy == 0 || n_def + 256u > AX_DEF)) {
             // ---- phase 2: the deferred windows of the wave. (a) the Bloom filter, AX_F windows per lane per round
-            // trip; the windows it cannot rule out are compacted to the front of the list; (b) those are looked up one
-            // per lane (bucket -> fingerprint -> compare with the text -> class)
+            // trip; the windows it cannot rule out are compacted to the front of the list; (b) those are looked up
+            // one per lane (bucket -> fingerprint -> compare with the text -> class)
+            ambf[lane] = af;
+            ambd[lane] = ad;
             wave_sync();
-            const uint32_t n2 = min(__builtin_amdgcn_readfirstlane(defn[0]), AX_DEF);
+            const uint32_t n2 = min(n_def, AX_DEF);
             for (uint32_t base = 0; base < n2; base += 64u * AX_F) {
                 uint32_t ent[AX_F];
                 uint64_t hh[AX_F];
@@ -1068,7 +673,7 @@ __global__ __launch_bounds__(AX_THREADS, (ax_min_waves<MODE, HW>())) void k_scan
                     ent[t] = e16 == AX_VOID ? AX_EMPTY : (uint32_t)e16;
                     const uint32_t o = ent[t] & 63u, jj = (ent[t] >> 6) & 1023u;
                     uint64_t ra[HW];
-                    read_words((uint32_t)sbs[o] + jj, ra);
+                    read_words(o, (uint32_t)off0s[o] + jj, ra);
                     hh[t] = ax_hash<HW>(ra, k);
                 }
 #pragma unroll
@@ -1095,9 +700,9 @@ __global__ __launch_bounds__(AX_THREADS, (ax_min_waves<MODE, HW>())) void k_scan
                 const bool act = idx < n3;
                 const uint32_t ent = act ? (uint32_t)defl[idx] : 0u;
                 const uint32_t o = ent & 63u, jj = ent >> 6;
-                const uint32_t sbo = sbs[o];
+                const uint32_t so = (uint32_t)off0s[o] + jj;  // the window's slot position
                 uint64_t ra[HW];
-                read_words(sbo + jj, ra);
+                read_words(o, so, ra);
                 const uint64_t h = ax_hash<HW>(ra, k);
                 const uint32_t fp = ax_fp(h);
                 uint32_t b = act ? ax_bucket(h, A.nb) : 0u, sl = 0, pp = 0, pg = 0;
@@ -1143,7 +748,7 @@ __global__ __launch_bounds__(AX_THREADS, (ax_min_waves<MODE, HW>())) void k_scan
                     double wgt = 0.0;
                     if (MODE == KM_LOCAL) {
                         const uint8_t* qb = src.qual + rbase[o] + jj;
-                        const bool uni = chg_zero(sbo + jj + 1u, k - 1u);
+                        const bool uni = chg_zero(o, so + 1u, k - 1u);
                         int q = (int)qb[0] - 33;
                         q = q < 0 ? 0 : (q > 41 ? 41 : q);
                         wgt = weight(qb, uni, (uint32_t)q);
@@ -1161,18 +766,447 @@ __global__ __launch_bounds__(AX_THREADS, (ax_min_waves<MODE, HW>())) void k_scan
             wave_sync();
             af = ambf[lane];
             ad = ambd[lane];
+            hasdef = false;
+            if (lane == 0) defn[0] = defn[1] = 0u;
             wave_sync();
+            continue;
         }
-        // ---- ambiguity of the unit (read, or mate pair in lanes 2i, 2i + 1)
-        if (PAIRED) {
-            const int32_t of = __builtin_amdgcn_mov_dpp(af, 0xB1, 0xF, 0xF, false);  // quad_perm [1,0,3,2]: the mate
-            const int32_t od = __builtin_amdgcn_mov_dpp(ad, 0xB1, 0xF, 0xF, false);
-            const bool amb_pair = ad || od || (af >= 0 && of >= 0 && af != of);
-            if (has && (lane & 1u) == 0u && amb_pair) ++amb;
-        } else if (has && ad) {
-            ++amb;
+        // lanes that can start a piece now: idle, no deferred windows pending, and a next piece of their unit or
+        // a unit left in the pool
+        const bool ready = st == 2u && !hasdef;
+        const bool more_pool = pool < pool_n;
+        const bool wants = ready && ((has_unit && !last_piece) || more_pool);
+        const unsigned long long want = __ballot(wants);
+        if (want == 0 && busy == 0) {
+            if (blk == 0) break;  // (blk != 0 with busy == 0 ran phase 2 above)
+        }
+        if (want != 0 && ((uint32_t)__popcll(want) >= SPEQ_AX_REFILL || busy == 0)) {
+            // ================= refill: next pieces of the wanting lanes, staged together =================
+            if (STATS) s_spl += lane == 0 ? 1u : 0u;
+            if (wants && has_unit && last_piece) {  // the unit is complete: its ambiguity (fm_scanner.cpp:183-190)
+                if (ad) ++amb;
+                has_unit = false;
+                af = -1;
+                ad = 0;
+            }
+            // units from the pool for the lanes without one, in lane order
+            const unsigned long long tk = __ballot(wants && !has_unit);
+            uint64_t newu = nu;
+            if (wants && !has_unit) newu = pool_unit(pool + lanes_below(tk));
+            pool += (uint64_t)__popcll(tk);
+            bool stg = false;
+            if (wants) {
+                if (!has_unit) {
+                    if (newu < nu) {
+                        has_unit = true;
+                        mate = 0;
+                        start_read(PAIRED ? 2 * newu : newu);
+                        stg = true;
+                    }
+                } else if (seg + 1u < nseg) {
+                    ++seg;
+                    stg = true;
+                } else {  // PAIRED: the second mate
+                    mate = 1;
+                    start_read(rd + 1);
+                    stg = true;
+                }
+            }
+            // the piece: bases [s, s + sb), windows [s, s + wend) of read rd
+            const uint64_t s = (uint64_t)seg * segw;
+            const uint32_t sb = stg && W ? (uint32_t)(L - s < AX_CAP ? L - s : AX_CAP) : 0u;
+            const uint32_t nwend = stg && W ? (uint32_t)(W - s < segw ? W - s : segw) : 0u;
+            const uint64_t a = rb + s;
+            const uint64_t a16 = a & ~15ull;
+            const uint32_t noff0 = (uint32_t)(a - a16);
+            const uint32_t nch = sb ? (noff0 + sb + 15u) / 16u : 0u;
+            if (stg) {
+                last_piece = seg + 1u >= nseg && (!PAIRED || mate == 1u);
+                wend = nwend;
+                off0 = noff0;
+                ta = a;
+                off0s[lane] = (uint8_t)noff0;
+                if (MODE == KM_LOCAL) rbase[lane] = a;
+                if (STATS) {
+                    s_ch += nch;
+                    s_seg += 1u;
+                }
+            }
+            // ---- coalesced staging: the refilling lanes' chunks laid end to end (lane o's at [pre_o, pre_o + nch_o));
+            // every lane of the wave decodes whole chunks, found by a binary search over the lanes' chunk ranges
+            static_assert(AX_CHUNKS < 16, "chunk counts in four bits");
+            uint32_t pre = 0, nch_tot = 0;
+#pragma unroll
+            for (uint32_t bb = 0; bb < 4; ++bb) {
+                const unsigned long long m = __ballot((nch >> bb) & 1u);
+                pre += lanes_below(m) << bb;
+                nch_tot += (uint32_t)__popcll(m) << bb;
+            }
+            const uint32_t endc = pre + nch;
+            uint32_t qcarry = 0;  // local: last quality dword of the previous instruction's lane 63
+            constexpr uint32_t SU = SPEQ_AX_SU;  // stream instructions whose loads are in flight together
+            for (uint32_t c0 = 0; c0 < nch_tot; c0 += 64u * SU) {
+                uint4 sv[SU], qv[SU];
+                uint32_t own[SU], ci[SU];
+#pragma unroll
+                for (uint32_t u = 0; u < SU; ++u) {
+                    const uint32_t c = min(c0 + 64u * u + lane, nch_tot - 1u);
+                    uint32_t o = 0;  // the first lane whose chunk range ends after c
+#pragma unroll
+                    for (uint32_t d = 32; d >= 1; d >>= 1)
+                        o = ((uint32_t)__shfl((int)endc, (int)(o + d - 1u)) <= c) ? o + d : o;
+                    own[u] = o;
+                    ci[u] = c - (uint32_t)__shfl((int)pre, (int)o);
+                    const uint64_t go = (uint64_t)__shfl((long long)a16, (int)o) + 16ull * ci[u];
+                    sv[u] = *reinterpret_cast<const uint4*>(src.seq + go);
+                    qv[u] = *reinterpret_cast<const uint4*>(src.qual + go);
+                }
+#pragma unroll
+                for (uint32_t u = 0; u < SU; ++u) {
+                    const uint32_t c = c0 + 64u * u + lane;
+                    const uint32_t sd[4] = {sv[u].x, sv[u].y, sv[u].z, sv[u].w};
+                    const uint32_t qd[4] = {qv[u].x, qv[u].y, qv[u].z, qv[u].w};
+                    uint32_t cw = 0, bad = 0, chb = 0;
+                    // local mode: the quality byte before the chunk (a chunk's change bit 0 compares with it; the
+                    // piece's first base never reads its change bit)
+                    uint32_t qprev = 0;
+                    if (MODE == KM_LOCAL) {  // the previous chunk's last quality (the previous lane's, or the carry)
+                        const uint32_t up = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)qv[u].w, 0x138, 0xF, 0xF, false);
+                        qprev = lane == 0 ? qcarry : up;
+                        qcarry = __builtin_amdgcn_readlane(qv[u].w, 63);
+                    }
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) {
+                        const uint32_t x = sd[i] | 0x20202020u;  // lower case
+                        const uint32_t c4 = ((x >> 1) ^ (x >> 2)) & 0x03030303u;  // a c g t/u -> 0 1 2 3
+                        cw |= ((c4 | (c4 >> 6) | (c4 >> 12) | (c4 >> 18)) & 0xFFu) << (8 * i);
+                        const uint32_t canon = __builtin_amdgcn_perm(0u, 0x74676361u, c4);  // the letter of that code
+                        const uint32_t okb = zero_bytes(x ^ canon) | zero_bytes(x ^ 0x75757575u);  // ACGT or U
+                        const uint32_t y = qd[i];
+                        const uint32_t badq = (((0x80808080u | qt4) - (y & 0x7F7F7F7Fu)) & ~y & 0x80808080u) | allbad;
+                        bad |= flags4((~okb & 0x80808080u) | badq) << (4 * i);
+                        if (MODE == KM_LOCAL) {
+                            const uint32_t prev = (y << 8) | (qprev >> 24);
+                            chb |= flags4(~zero_bytes(y ^ prev) & 0x80808080u) << (4 * i);
+                            qprev = y;
+                        }
+                    }
+                    if (c < nch_tot) {
+                        codes[ci[u] * 64u + own[u]] = cw;
+                        bad16[((ci[u] >> 2) * 64u + own[u]) * 4u + (ci[u] & 3u)] = (uint16_t)bad;
+                        if (MODE == KM_LOCAL) chg[ci[u] * 64u + own[u]] = (uint16_t)chb;
+                    }
+                }
+            }
+            wave_sync();
+            if (stg) {
+                // this lane's bad-base bits (16 per chunk from a16; chunks past its piece are bad)
+                uint64_t ok[4];
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    uint64_t v = vw[(uint32_t)i * 64u + lane];  // chunks 4i .. 4i + 3, 16 bits each
+                    const uint32_t b0 = 64u * (uint32_t)i, nb = 16u * nch;
+                    if (nb <= b0) v = ~0ull;
+                    else if (nb < b0 + 64u) v |= ~0ull << (nb - b0);
+                    ok[i] = ~v;
+                }
+                // valid windows: AND of k consecutive "good" bits (doubling), then shifted to the read's first base
+                for (uint32_t len = 1; len < k;) {
+                    const uint32_t sft = min(len, k - len);
+                    const uint32_t ws = sft >> 6, bs = sft & 63u;
+                    uint64_t nx[4];
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) {
+                        uint64_t lo = 0ull, hi = 0ull;  // ok[i + ws], ok[i + ws + 1] (zero past the end), no indexing
+#pragma unroll
+                        for (int t = 0; t < 4; ++t) {
+                            lo = (uint32_t)(t - i) == ws ? ok[t] : lo;
+                            hi = (uint32_t)(t - i) == ws + 1u ? ok[t] : hi;
+                        }
+                        nx[i] = ok[i] & funnel(lo, hi, bs);
+                    }
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) ok[i] = nx[i];
+                    len += sft;
+                }
+                uint64_t vv[AX_VWW];
+#pragma unroll
+                for (uint32_t i = 0; i < AX_VWW; ++i) {
+                    const uint64_t lo = ok[i], hi = i + 1 < 4 ? ok[i + 1] : 0ull;
+                    uint64_t v = funnel(lo, hi, off0);
+                    const uint32_t bit0 = 64u * i;
+                    if (wend <= bit0) v = 0;
+                    else if (wend < bit0 + 64u) v &= (1ull << (wend - bit0)) - 1ull;
+                    vv[i] = v;
+                    t_cnt += (uint32_t)__popcll(v);
+                }
+                wave_sync();  // (own slot only; keeps the bad-bit reads before the overwrite below)
+#pragma unroll
+                for (uint32_t i = 0; i < AX_VWW; ++i) vw[i * 64u + lane] = vv[i];
+                j = 0;
+                st = wend > 0 ? 0u : 2u;
+                verify = false;
+                resume = false;
+                last_mm = -1;
+            } else {
+                wave_sync();
+            }
+            wave_sync();
+            continue;  // re-evaluate (lanes whose piece has no window are idle again)
+        }
+        if (busy == 0) continue;  // blocked lanes only: phase 2 runs next time round
+
+        // ================= phase 1: one memory round trip per iteration =================
+        // a lane either probes the anchor table (its candidate is compared in the next iteration) or extends a run
+        // over the rest of its piece (at most AX_CMP bases; a clean 150-bp read: one lookup and one run). One kind
+        // of work per iteration, alternating (a lookup is followed by a run and a run by a lookup, so a lane rarely
+        // waits): the wave executes the lookup code or the run code, not both under exec masks (the kernel is bound
+        // by VALU issue, profiles/r03), and a kind no lane needs is skipped.
+        if (st == 0u) {
+            j = next_valid(lane, j, wend);
+            if (j >= wend) st = 2u;
+        }
+        const unsigned long long busy1 = __ballot(st != 2u);
+        if (busy1 == 0) continue;
+        if (STATS && lane == 0) {
+            const uint32_t nb = (uint32_t)__popcll(busy1);
+            s_b4 += nb <= 4u ? 1u : 0u;
+            s_b16 += (nb > 4u && nb <= 16u) ? 1u : 0u;
+            s_b32 += (nb > 16u && nb <= 32u) ? 1u : 0u;
+            s_b64 += nb > 32u ? 1u : 0u;
+        }
+        const bool want_lk = __ballot(st == 0u) != 0, want_rn = __ballot(st == 1u) != 0;
+        run_phase = run_phase ? !want_lk : want_rn;
+        const bool lk = st == 0u && !run_phase, rn = st == 1u && run_phase;
+        if (STATS) {
+            s_iter += lane == 0 ? 1u : 0u;
+            s_lkw += (lane == 0 && !run_phase) ? 1u : 0u;
+            s_rnw += (lane == 0 && run_phase) ? 1u : 0u;
+            s_lk += lk ? 1u : 0u;
+            s_rn += rn ? 1u : 0u;
+        }
+        if (!run_phase) {
+            // ---- lookup: hash window j -> bucket (8 slots {pos, fp | group}); resolve
+            uint64_t ra[HW];
+            read_words(lane, off0 + j, ra);
+            const uint64_t h = ax_hash<HW>(ra, k);
+            const uint32_t fp = ax_fp(h);
+            if (lk && !resume) {
+                pb = ax_bucket(h, A.nb);
+                ps = 0;
+            }
+            const uint32_t boff = lk ? pb * 64u : AX_OOB;
+            const u32x4 q0 = __builtin_amdgcn_raw_buffer_load_b128(rs_atab, boff, 0, 0);
+            const u32x4 q1 = __builtin_amdgcn_raw_buffer_load_b128(rs_atab, boff + 16u, 0, 0);
+            const u32x4 q2 = __builtin_amdgcn_raw_buffer_load_b128(rs_atab, boff + 32u, 0, 0);
+            const u32x4 q3 = __builtin_amdgcn_raw_buffer_load_b128(rs_atab, boff + 48u, 0, 0);
+            if (lk) {
+                uint32_t slot = 0, cp = 0, cg = 0;
+                const uint32_t res = ax_resolve(q0, q1, q2, q3, fp, ps, slot, cp, cg);
+                if (res == 1u) {  // candidate: compared with the text in the next iteration
+                    p = cp;
+                    gt = cg;
+                    ps = slot;
+                    st = 1u;
+                    verify = true;
+                    resume = false;
+                } else if (res == 0u) {
+                    // absent: defer the windows that share the mismatch (or the next k - 1), skip past them
+                    resume = false;
+                    uint32_t dend = (last_mm >= (int32_t)j && last_mm < (int32_t)(j + k)) ? (uint32_t)last_mm
+                                                                                           : j + k - 1u;
+                    dend = min(dend, wend - 1u);
+                    // the valid windows of (j, dend] as two 64-bit masks (dend - j <= k - 1 <= 127)
+                    const uint32_t span = dend - j;
+                    uint64_t dm0 = vbits(lane, j + 1u), dm1 = span > 64u ? vbits(lane, j + 65u) : 0ull;
+                    dm0 &= span >= 64u ? ~0ull : ((1ull << span) - 1ull);
+                    if (span > 64u) dm1 &= span - 64u >= 64u ? ~0ull : ((1ull << (span - 64u)) - 1ull);
+                    const uint32_t cnt = (uint32_t)__popcll(dm0) + (uint32_t)__popcll(dm1);
+                    bool ok_def = true;
+                    if (cnt) {
+                        const uint32_t slot0 = atomicAdd(&defn[0], cnt);
+                        ok_def = slot0 + cnt <= AX_DEF;
+                        if (ok_def) {
+                            uint32_t sl = slot0;
+                            for (uint64_t t = dm0; t; t &= t - 1)
+                                defl[sl++] = (uint16_t)(lane | ((j + 1u + (uint32_t)__builtin_ctzll(t)) << 6));
+                            for (uint64_t t = dm1; t; t &= t - 1)
+                                defl[sl++] = (uint16_t)(lane | ((j + 65u + (uint32_t)__builtin_ctzll(t)) << 6));
+                            hasdef = true;
+                            if (STATS) s_def += cnt;
+                        } else {  // no room: the windows stay with this lane; void the slots reserved below the end
+                            for (uint32_t sl = slot0; sl < AX_DEF && sl < slot0 + cnt; ++sl) defl[sl] = AX_VOID;
+                        }
+                    }
+                    j = ok_def ? dend + 1u : j + 1u;
+                    last_mm = -1;
+                } else {  // full bucket without the key or an empty slot: the next bucket
+                    pb = pb + 1u == (uint32_t)A.nb ? 0u : pb + 1u;
+                    ps = 0;
+                    resume = true;
+                }
+            }
+        } else {
+            // ---- run: compare read [j, j + cl) with text [p, p + cl) (cl = the rest of the piece, at most AX_CMP
+            // bases: the granules that cover it from p's granule on, the others with out-of-range offsets), then
+            // classify the matched windows
+            const uint32_t cl = min(wend - j + k - 1u, AX_CMP);
+            const uint32_t ng = rn ? ((p & 31u) + cl + 31u) >> 5 : 0u;
+            const uint32_t goff = (p >> 5) * 16u;
+            u32x4 gr[AX_NGR];
+#pragma unroll
+            for (uint32_t i = 0; i < AX_NGR; ++i)
+                gr[i] = __builtin_amdgcn_raw_buffer_load_b128(rs_gran, i < ng ? goff + 16u * i : AX_OOB, 0, 0);
+            if (STATS) s_rg += ng;
+            uint32_t qj = 0;
+            if (MODE == KM_LOCAL) {
+                qj = src.qual[ta + (rn ? j : 0u)];
+                if (STATS) s_qb += rn ? 1u : 0u;
+            }
+            // the read's 16-base dwords from slot position off0 + j
+            const uint32_t rpos = off0 + j, rd0 = rpos >> 4, rsh = 2u * (rpos & 15u);
+            uint32_t rw[AX_CMPW * 2 + 1];
+#pragma unroll
+            for (uint32_t i = 0; i <= 2 * AX_CMPW; ++i) {
+                const uint32_t d = rd0 + i;
+                rw[i] = d < AX_CHUNKS ? codes[d * 64u + lane] : 0u;
+            }
+            if (rn) {
+                const uint32_t s5 = p & 31u, q16 = s5 >> 4, tsh = 2u * (s5 & 15u);
+                uint32_t e = cl;  // first mismatching base (cl: none)
+#pragma unroll
+                for (int i = 2 * (int)AX_CMPW - 1; i >= 0; --i) {
+                    // text dwords T[m] = gr[m / 2][m % 2]; aligned: bases 16 i .. 16 i + 15 from p
+                    const uint32_t m0 = (uint32_t)i, m1 = (uint32_t)i + 1u, m2 = (uint32_t)i + 2u;
+                    const uint32_t t0 = gr[m0 / 2][m0 % 2], t1 = gr[m1 / 2][m1 % 2];
+                    const uint32_t t2 = m2 / 2 < AX_NGR ? gr[(m2 / 2) % AX_NGR][m2 % 2] : 0u;
+                    const uint32_t tlo = q16 ? t1 : t0, thi = q16 ? t2 : t1;
+                    const uint32_t td = alignbit(thi, tlo, tsh);
+                    const uint32_t rdw = alignbit(rw[i + 1], rw[i], rsh);
+                    uint32_t x = td ^ rdw;
+                    const uint32_t b0 = 16u * (uint32_t)i;
+                    if (cl <= b0) x = 0;
+                    else if (cl < b0 + 16u) x &= (1u << (2u * (cl - b0))) - 1u;
+                    e = x ? b0 + ((uint32_t)__builtin_ctz(x) >> 1) : e;
+                }
+                if (verify && e < k) {  // fingerprint collision: resume probing after that slot
+                    st = 0u;
+                    resume = true;
+                    ++ps;
+                } else {
+                    uint32_t R = e - (k - 1u);  // e >= k - 1: a candidate matched k bases, a run k - 1
+                    R = min(R, wend - j);
+                    // the windows [0, R) in 32-window chunks: class planes of windows p + 32c .. (bits s5 + 32c ..
+                    // of the granules' planes). The run stops at the first END window (the text ends: the next
+                    // windows belong to another text, looked up again) or SENT window of a valid read window (an N
+                    // in the text: looked up); windows before it are tallied to the run's group.
+                    uint32_t d0 = R, cnt = 0;
+                    bool cut = false, cut_end = false;
+                    uint32_t ownc[AX_CMPW];
+                    const uint64_t v0 = vbits(lane, j), v1 = vbits(lane, j + 64u), v2 = vbits(lane, j + 128u);
+                    const uint32_t vm[AX_CMPW] = {(uint32_t)v0, (uint32_t)(v0 >> 32), (uint32_t)v1,
+                                                  (uint32_t)(v1 >> 32), (uint32_t)v2};
+                    static_assert(AX_CMPW == 5, "five 32-window chunks");
+#pragma unroll
+                    for (uint32_t c = 0; c < AX_CMPW; ++c) {
+                        const uint32_t w0 = 32u * c;
+                        const uint32_t mR = R <= w0 ? 0u : (R - w0 >= 32u ? ~0u : ((1u << (R - w0)) - 1u));
+                        const uint32_t P0 = alignbit(gr[c + 1][2], gr[c][2], s5);
+                        const uint32_t P1 = alignbit(gr[c + 1][3], gr[c][3], s5);
+                        const uint32_t m = vm[c] & mR;  // the chunk's valid read windows in the run
+                        const uint32_t stop = P1 & (P0 | m) & mR;
+                        const uint32_t below = cut ? 0u : (stop ? ((stop & (0u - stop)) - 1u) : ~0u);
+                        const uint32_t ow = ~(P0 | P1) & m & below;
+                        cnt += (uint32_t)__popc(ow);
+                        ownc[c] = ow;
+                        if (EM) {  // multi-group windows of the run: the EM histogram
+                            uint32_t todo = P0 & ~P1 & m & below;
+                            while (todo) {
+                                const uint32_t d = (uint32_t)__builtin_ctz(todo);
+                                todo &= todo - 1;
+                                const uint32_t lo = A.mlo[p + w0 + d];
+                                atomicAdd(&src.em_mult[lo], 1u);
+                                src.em_hi[lo] = A.mhi[lo];
+                            }
+                        }
+                        if (!cut && stop) {
+                            const uint32_t t = (uint32_t)__builtin_ctz(stop);
+                            d0 = w0 + t;
+                            cut_end = ((P0 >> t) & 1u) != 0;
+                            cut = true;
+                        }
+                    }
+                    if (STATS) {
+                        s_rwin += d0;
+                        s_tal += cnt;
+                    }
+                    if (cnt) {
+                        double wsum = 0.0;
+                        if (MODE == KM_LOCAL) {
+                            // one quality for the whole cut run when no base in (j, j + d0 - 1 + k) changes it
+                            if (chg_zero(lane, rpos + 1u, d0 + k - 2u)) {
+                                int q = (int)qj - 33;
+                                q = q < 0 ? 0 : (q > 41 ? 41 : q);
+                                wsum = (double)cnt * wtab[q];
+                            } else {
+#pragma unroll
+                                for (uint32_t c = 0; c < AX_CMPW; ++c) {
+                                    uint32_t todo = ownc[c];
+                                    while (todo) {
+                                        const uint32_t d = 32u * c + (uint32_t)__builtin_ctz(todo);
+                                        todo &= todo - 1;
+                                        const uint32_t jj = j + d;
+                                        const uint8_t* qb = src.qual + ta + jj;
+                                        int q = (int)qb[0] - 33;
+                                        q = q < 0 ? 0 : (q > 41 ? 41 : q);
+                                        wsum += weight(qb, chg_zero(lane, off0 + jj + 1u, k - 1u), (uint32_t)q);
+                                        if (STATS) s_qb += 1u;
+                                    }
+                                }
+                            }
+                        }
+                        add_count(gt, cnt, wsum);
+                        if (af < 0) af = (int32_t)gt;
+                        else if ((int32_t)gt != af) ad = 1;
+                    }
+                    // next state
+                    verify = false;
+                    if (d0 < R) {
+                        if (cut_end) {  // END: look the window up (its k-mer may occur elsewhere)
+                            j += d0;
+                            st = 0u;
+                            resume = false;
+                            last_mm = -1;
+                        } else {  // SENT: matched bases, but no valid text window: deferred (or looked up now)
+                            const uint32_t slot = atomicAdd(&defn[0], 1u);
+                            if (slot < AX_DEF) {
+                                defl[slot] = (uint16_t)(lane | ((j + d0) << 6));
+                                hasdef = true;
+                                if (STATS) s_def += 1u;
+                                j += d0 + 1u;
+                                p += d0 + 1u;
+                                st = 1u;
+                            } else {
+                                j += d0;
+                                st = 0u;
+                                resume = false;
+                                last_mm = -1;
+                            }
+                        }
+                    } else {
+                        const bool mism = e < cl;  // the run ended at a mismatch (base j + e)
+                        if (mism && R < wend - j) last_mm = (int32_t)(j + e);
+                        j += R;
+                        p += R;
+                        st = (mism || R == 0u) ? 0u : 1u;
+                        if (st == 0u) resume = false;
+                    }
+                    if (j >= wend) st = 2u;
+                }
+            }
         }
     }
+    if (has_unit && ad) ++amb;  // the wave's last units
 
     // wave sums of the window and ambiguity counters through two LDS words (no shuffle address registers)
     if (lane == 0) {
@@ -1210,10 +1244,28 @@ __global__ __launch_bounds__(AX_THREADS, (ax_min_waves<MODE, HW>())) void k_scan
 
 template <int MODE, bool PAIRED, bool LDS, bool EM, int HW, bool STATS>
 void ax_launch_one(const AxView& A, const UnitSrc& src, uint32_t grid, size_t lds, hipStream_t st,
-                   unsigned long long* a, double* w) {
+                   unsigned long long* a, double* w, uint32_t n_cus) {
     if (lds > 64 * 1024)  // dynamic LDS above 64 KiB must be allowed (occupancy caps pad it)
         HIP_OK(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_scan_ax<MODE, PAIRED, LDS, EM, HW, STATS>),
                                    hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    // persistent waves: at most the blocks that are resident at once (each wave then takes several groups of units
+    // and refills its lanes from them)
+    static std::mutex mu;
+    static size_t cached_lds = 0;
+    static int cached_blocks = 0;
+    int per_cu = 0;
+    {
+        std::lock_guard<std::mutex> lk(mu);
+        if (cached_lds != lds || cached_blocks == 0) {
+            int nb = 0;
+            HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(
+                &nb, reinterpret_cast<const void*>(&k_scan_ax<MODE, PAIRED, LDS, EM, HW, STATS>), AX_THREADS, lds));
+            cached_lds = lds;
+            cached_blocks = std::max(nb, 1);
+        }
+        per_cu = cached_blocks;
+    }
+    grid = std::min<uint32_t>(grid, (uint32_t)per_cu * n_cus);
     hipLaunchKernelGGL((k_scan_ax<MODE, PAIRED, LDS, EM, HW, STATS>), dim3(grid), dim3(AX_THREADS), lds, st, A, src,
                        a, w);
 }
@@ -1221,26 +1273,26 @@ void ax_launch_one(const AxView& A, const UnitSrc& src, uint32_t grid, size_t ld
 // HW by k: 1 (k <= 32), 2 (k <= 64), 4 (k <= 128)
 template <int MODE, bool PAIRED, bool LDS, bool EM, bool STATS>
 void ax_launch_nwc(uint32_t k, const AxView& A, const UnitSrc& src, uint32_t grid, size_t lds, hipStream_t st,
-                   unsigned long long* a, double* w) {
-    if (k <= 32) ax_launch_one<MODE, PAIRED, LDS, EM, 1, STATS>(A, src, grid, lds, st, a, w);
-    else if (k <= 64) ax_launch_one<MODE, PAIRED, LDS, EM, 2, STATS>(A, src, grid, lds, st, a, w);
-    else ax_launch_one<MODE, PAIRED, LDS, EM, 4, STATS>(A, src, grid, lds, st, a, w);
+                   unsigned long long* a, double* w, uint32_t n_cus) {
+    if (k <= 32) ax_launch_one<MODE, PAIRED, LDS, EM, 1, STATS>(A, src, grid, lds, st, a, w, n_cus);
+    else if (k <= 64) ax_launch_one<MODE, PAIRED, LDS, EM, 2, STATS>(A, src, grid, lds, st, a, w, n_cus);
+    else ax_launch_one<MODE, PAIRED, LDS, EM, 4, STATS>(A, src, grid, lds, st, a, w, n_cus);
 }
 
 template <int MODE, bool PAIRED>
 void ax_launch_mode(bool lds_hist, uint32_t k, const AxView& A, const UnitSrc& src, uint32_t grid, size_t lds,
-                    hipStream_t st, unsigned long long* a, double* w) {
+                    hipStream_t st, unsigned long long* a, double* w, uint32_t n_cus) {
     const bool em = src.em_mult != nullptr;
     if (A.stats != nullptr && lds_hist && !em) {
-        ax_launch_nwc<MODE, PAIRED, true, false, true>(k, A, src, grid, lds, st, a, w);
+        ax_launch_nwc<MODE, PAIRED, true, false, true>(k, A, src, grid, lds, st, a, w, n_cus);
         return;
     }
     if (lds_hist) {
-        if (em) ax_launch_nwc<MODE, PAIRED, true, true, false>(k, A, src, grid, lds, st, a, w);
-        else ax_launch_nwc<MODE, PAIRED, true, false, false>(k, A, src, grid, lds, st, a, w);
+        if (em) ax_launch_nwc<MODE, PAIRED, true, true, false>(k, A, src, grid, lds, st, a, w, n_cus);
+        else ax_launch_nwc<MODE, PAIRED, true, false, false>(k, A, src, grid, lds, st, a, w, n_cus);
     } else {
-        if (em) ax_launch_nwc<MODE, PAIRED, false, true, false>(k, A, src, grid, lds, st, a, w);
-        else ax_launch_nwc<MODE, PAIRED, false, false, false>(k, A, src, grid, lds, st, a, w);
+        if (em) ax_launch_nwc<MODE, PAIRED, false, true, false>(k, A, src, grid, lds, st, a, w, n_cus);
+        else ax_launch_nwc<MODE, PAIRED, false, false, false>(k, A, src, grid, lds, st, a, w, n_cus);
     }
 }
 
@@ -1393,11 +1445,11 @@ bool launch_ax(speq_device_index* d, int mode, bool paired, const UnitSrc& src, 
     }
     const uint32_t grid = (uint32_t)blocks;
     if (mode == KM_GLOBAL) {
-        if (paired) ax_launch_mode<KM_GLOBAL, true>(lds_hist, src.k, A, src, grid, lds_launch, st, a, w);
-        else ax_launch_mode<KM_GLOBAL, false>(lds_hist, src.k, A, src, grid, lds_launch, st, a, w);
+        if (paired) ax_launch_mode<KM_GLOBAL, true>(lds_hist, src.k, A, src, grid, lds_launch, st, a, w, d->n_cus);
+        else ax_launch_mode<KM_GLOBAL, false>(lds_hist, src.k, A, src, grid, lds_launch, st, a, w, d->n_cus);
     } else {
-        if (paired) ax_launch_mode<KM_LOCAL, true>(lds_hist, src.k, A, src, grid, lds_launch, st, a, w);
-        else ax_launch_mode<KM_LOCAL, false>(lds_hist, src.k, A, src, grid, lds_launch, st, a, w);
+        if (paired) ax_launch_mode<KM_LOCAL, true>(lds_hist, src.k, A, src, grid, lds_launch, st, a, w, d->n_cus);
+        else ax_launch_mode<KM_LOCAL, false>(lds_hist, src.k, A, src, grid, lds_launch, st, a, w, d->n_cus);
     }
     HIP_OK(hipGetLastError());
     return true;
