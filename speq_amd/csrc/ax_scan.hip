@@ -441,14 +441,14 @@ constexpr uint32_t AX_WPB = SPEQ_AX_WPB, AX_THREADS = 64 * SPEQ_AX_WPB;
 #ifndef SPEQ_AX_SU  // staging: stream instructions per load batch (A/B knob)
 #define SPEQ_AX_SU 2
 #endif
-#ifndef SPEQ_AX_MIN_WAVES  // minimum waves per SIMD the register allocator must allow, k <= 32 (A/B knob)
-#define SPEQ_AX_MIN_WAVES 4
+#ifndef SPEQ_AX_MIN_WAVES  // minimum waves per SIMD the register allocator must allow, k <= 32 (A/B knob): 5 (96
+#define SPEQ_AX_MIN_WAVES 5   // VGPRs, no spills; LDS fits 5 blocks) is 16 % faster than 4 (profiles/r03/ax_variants_w5)
 #endif
 #ifndef SPEQ_AX_MIN_WAVES4  // the same for 33 <= k <= 64
-#define SPEQ_AX_MIN_WAVES4 4
+#define SPEQ_AX_MIN_WAVES4 5
 #endif
 #ifndef SPEQ_AX_MIN_WAVES6  // and 65 <= k <= 128
-#define SPEQ_AX_MIN_WAVES6 4
+#define SPEQ_AX_MIN_WAVES6 4  // (at 5: 8-24 B of spills per lane)
 #endif
 #ifndef SPEQ_AX_MIN_WAVES_LOCAL  // local (Phred-weighted) mode, every k
 #define SPEQ_AX_MIN_WAVES_LOCAL 3
@@ -459,10 +459,13 @@ constexpr uint32_t AX_WPB = SPEQ_AX_WPB, AX_THREADS = 64 * SPEQ_AX_WPB;
 #ifndef SPEQ_AX_BLOCKED  // idle lanes waiting for their deferred windows that trigger the deferred-window pass
 #define SPEQ_AX_BLOCKED 16
 #endif
-template <int MODE, int HW>
+// EM scans and the instrumented twin hold more live state: 4 waves (no spills)
+template <int MODE, int HW, bool EM, bool STATS>
 constexpr int ax_min_waves() {
     return MODE == KM_LOCAL ? SPEQ_AX_MIN_WAVES_LOCAL
-                            : (HW >= 4 ? SPEQ_AX_MIN_WAVES6 : (HW >= 2 ? SPEQ_AX_MIN_WAVES4 : SPEQ_AX_MIN_WAVES));
+                            : ((EM || STATS) ? 4
+                                             : (HW >= 4 ? SPEQ_AX_MIN_WAVES6
+                                                        : (HW >= 2 ? SPEQ_AX_MIN_WAVES4 : SPEQ_AX_MIN_WAVES)));
 }
 
 __device__ __forceinline__ uint32_t alignbit(uint32_t hi, uint32_t lo, uint32_t s) {  // ({hi, lo} >> (s & 31))[31:0]
@@ -484,7 +487,7 @@ __device__ __forceinline__ uint32_t lanes_below(unsigned long long m) {  // set 
 // (phase 2) are resolved by the whole wave when SPEQ_AX_BLOCKED finished lanes wait for theirs (their slots hold the
 // bases the deferred entries refer to) or when the list fills up.
 template <int MODE, bool PAIRED, bool LDS_HIST, bool EM, int HW, bool STATS>
-__global__ __launch_bounds__(AX_THREADS, (ax_min_waves<MODE, HW>())) void k_scan_ax(AxView A, UnitSrc src,
+__global__ __launch_bounds__(AX_THREADS, (ax_min_waves<MODE, HW, EM, STATS>())) void k_scan_ax(AxView A, UnitSrc src,
                                                                                   unsigned long long* __restrict__ out_a,
                                                                                   double* __restrict__ out_w) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -536,7 +539,6 @@ __global__ __launch_bounds__(AX_THREADS, (ax_min_waves<MODE, HW>())) void k_scan
     const uint64_t NWV = (uint64_t)gridDim.x * AX_WPB;
     const uint64_t gw = (uint64_t)blockIdx.x * AX_WPB + wid;
     const uint64_t nu = PAIRED ? src.n_units / 2 : src.n_units;  // units: reads, or mate pairs
-    const uint64_t n_groups = (nu + 63) / 64;
     const uint32_t segw = AX_CAP - k + 1u;  // windows per segment
     const uint32_t qt = 33u + src.cutoff;   // Phred+33 byte <= qt  <=>  clamp(q, 0, 41) <= cutoff (cutoff < 41)
     const uint32_t qt4 = (qt > 0x7Fu ? 0x7Fu : qt) * 0x01010101u;
@@ -617,14 +619,11 @@ __global__ __launch_bounds__(AX_THREADS, (ax_min_waves<MODE, HW>())) void k_scan
     uint64_t rb = 0, L = 0, W = 0;  // current read: first base, length, windows
     int32_t af = -1, ad = 0;   // ambiguity state of the unit
     bool hasdef = false;       // deferred windows of this lane's piece are in the wave's list
-    // ---- the wave's pool: units of groups gw, gw + NWV, ... (uniform)
-    uint64_t pool = 0;         // units taken so far (flat index over the wave's groups)
-    const uint64_t my_groups = gw < n_groups ? (n_groups - gw + NWV - 1) / NWV : 0;
-    const uint64_t pool_n = my_groups * 64;
-    auto pool_unit = [&](uint64_t flat) -> uint64_t {  // the unit of flat pool index `flat`, or nu (none)
-        const uint64_t u = (gw + (flat >> 6) * NWV) * 64 + (flat & 63u);
-        return (flat < pool_n && u < nu) ? u : nu;
-    };
+    // ---- the wave's pool (uniform): an equal share of the units, [nu w / NWV, nu (w + 1) / NWV) — contiguous
+    // reads (coalesced staging), and every wave gets the same number of units so the waves finish together (a
+    // launch-wide counter handing out groups was slower: one contended atomic address)
+    uint64_t cur = (nu * gw) / NWV;            // next unit
+    const uint64_t cur_end = (nu * (gw + 1)) / NWV;
     // ---- phase-1 state of the current piece
     uint32_t wend = 0;         // windows of the piece
     uint32_t off0 = 0;         // first base of the piece in the slot
@@ -774,7 +773,7 @@ __global__ __launch_bounds__(AX_THREADS, (ax_min_waves<MODE, HW>())) void k_scan
         // lanes that can start a piece now: idle, no deferred windows pending, and a next piece of their unit or
         // a unit left in the pool
         const bool ready = st == 2u && !hasdef;
-        const bool more_pool = pool < pool_n;
+        const bool more_pool = cur < cur_end;
         const bool wants = ready && ((has_unit && !last_piece) || more_pool);
         const unsigned long long want = __ballot(wants);
         if (want == 0 && busy == 0) {
@@ -792,8 +791,9 @@ __global__ __launch_bounds__(AX_THREADS, (ax_min_waves<MODE, HW>())) void k_scan
             // units from the pool for the lanes without one, in lane order
             const unsigned long long tk = __ballot(wants && !has_unit);
             uint64_t newu = nu;
-            if (wants && !has_unit) newu = pool_unit(pool + lanes_below(tk));
-            pool += (uint64_t)__popcll(tk);
+            const uint32_t rank = lanes_below(tk);
+            if (wants && !has_unit && cur + rank < cur_end) newu = cur + rank;
+            cur = min(cur + (uint64_t)__popcll(tk), cur_end);
             bool stg = false;
             if (wants) {
                 if (!has_unit) {
@@ -1085,8 +1085,8 @@ __global__ __launch_bounds__(AX_THREADS, (ax_min_waves<MODE, HW>())) void k_scan
                     const uint32_t rdw = alignbit(rw[i + 1], rw[i], rsh);
                     uint32_t x = td ^ rdw;
                     const uint32_t b0 = 16u * (uint32_t)i;
-                    if (cl <= b0) x = 0;
-                    else if (cl < b0 + 16u) x &= (1u << (2u * (cl - b0))) - 1u;
+                    const uint32_t nb = cl > b0 ? min(cl - b0, 16u) : 0u;  // bases of this dword in the compare
+                    x &= nb >= 16u ? ~0u : ((1u << (2u * nb)) - 1u);
                     e = x ? b0 + ((uint32_t)__builtin_ctz(x) >> 1) : e;
                 }
                 if (verify && e < k) {  // fingerprint collision: resume probing after that slot
@@ -1102,38 +1102,76 @@ __global__ __launch_bounds__(AX_THREADS, (ax_min_waves<MODE, HW>())) void k_scan
                     // in the text: looked up); windows before it are tallied to the run's group.
                     uint32_t d0 = R, cnt = 0;
                     bool cut = false, cut_end = false;
-                    uint32_t ownc[AX_CMPW];
-                    const uint64_t v0 = vbits(lane, j), v1 = vbits(lane, j + 64u), v2 = vbits(lane, j + 128u);
-                    const uint32_t vm[AX_CMPW] = {(uint32_t)v0, (uint32_t)(v0 >> 32), (uint32_t)v1,
-                                                  (uint32_t)(v1 >> 32), (uint32_t)v2};
+                    uint32_t ownc[AX_CMPW] = {0u, 0u, 0u, 0u, 0u};
                     static_assert(AX_CMPW == 5, "five 32-window chunks");
+                    // the lane's valid-window bits j .. j + 159 as 32-bit chunks (dwords of its vw column)
+                    uint32_t vm[AX_CMPW];
+                    {
+                        const uint32_t* vw32 = reinterpret_cast<const uint32_t*>(vw);
+                        const uint32_t d = j >> 5, vs = j & 31u;
+                        uint32_t vd[AX_CMPW + 1];
 #pragma unroll
-                    for (uint32_t c = 0; c < AX_CMPW; ++c) {
-                        const uint32_t w0 = 32u * c;
-                        const uint32_t mR = R <= w0 ? 0u : (R - w0 >= 32u ? ~0u : ((1u << (R - w0)) - 1u));
-                        const uint32_t P0 = alignbit(gr[c + 1][2], gr[c][2], s5);
-                        const uint32_t P1 = alignbit(gr[c + 1][3], gr[c][3], s5);
-                        const uint32_t m = vm[c] & mR;  // the chunk's valid read windows in the run
-                        const uint32_t stop = P1 & (P0 | m) & mR;
-                        const uint32_t below = cut ? 0u : (stop ? ((stop & (0u - stop)) - 1u) : ~0u);
-                        const uint32_t ow = ~(P0 | P1) & m & below;
-                        cnt += (uint32_t)__popc(ow);
-                        ownc[c] = ow;
-                        if (EM) {  // multi-group windows of the run: the EM histogram
-                            uint32_t todo = P0 & ~P1 & m & below;
-                            while (todo) {
-                                const uint32_t d = (uint32_t)__builtin_ctz(todo);
-                                todo &= todo - 1;
-                                const uint32_t lo = A.mlo[p + w0 + d];
-                                atomicAdd(&src.em_mult[lo], 1u);
-                                src.em_hi[lo] = A.mhi[lo];
-                            }
+                        for (uint32_t i = 0; i <= AX_CMPW; ++i) {
+                            const uint32_t di = d + i;
+                            vd[i] = di < 2u * AX_VWW ? vw32[((di >> 1) * 64u + lane) * 2u + (di & 1u)] : 0u;
                         }
-                        if (!cut && stop) {
-                            const uint32_t t = (uint32_t)__builtin_ctz(stop);
-                            d0 = w0 + t;
-                            cut_end = ((P0 >> t) & 1u) != 0;
-                            cut = true;
+#pragma unroll
+                        for (uint32_t i = 0; i < AX_CMPW; ++i) vm[i] = alignbit(vd[i + 1], vd[i], vs);
+                    }
+                    // windows of chunk c in the run (none past R)
+                    auto run_mask = [&](uint32_t c) -> uint32_t {
+                        const uint32_t w0 = 32u * c;
+                        return R <= w0 ? 0u : (R - w0 >= 32u ? ~0u : ((1u << (R - w0)) - 1u));
+                    };
+                    // common case first: no END / SENT window in the run (no stop): the tally is one popcount per
+                    // chunk; runs with a stop (rare) are recounted below with the windows before it only
+                    uint32_t anystop = 0;
+                    if (!EM) {
+#pragma unroll
+                        for (uint32_t c = 0; c < AX_CMPW; ++c) {
+                            if (c > 0 && __ballot(R > 32u * c) == 0) break;
+                            const uint32_t mR = run_mask(c);
+                            const uint32_t P0 = alignbit(gr[c + 1][2], gr[c][2], s5);
+                            const uint32_t P1 = alignbit(gr[c + 1][3], gr[c][3], s5);
+                            const uint32_t m = vm[c] & mR;
+                            anystop |= P1 & (P0 | m) & mR;
+                            const uint32_t ow = ~(P0 | P1) & m;
+                            cnt += (uint32_t)__popc(ow);
+                            ownc[c] = ow;
+                        }
+                    }
+                    if (EM || __ballot(anystop != 0) != 0) {
+                        if (EM || anystop != 0) {
+                            cnt = 0;
+#pragma unroll
+                            for (uint32_t c = 0; c < AX_CMPW; ++c) {
+                                const uint32_t w0 = 32u * c;
+                                const uint32_t mR = run_mask(c);
+                                const uint32_t P0 = alignbit(gr[c + 1][2], gr[c][2], s5);
+                                const uint32_t P1 = alignbit(gr[c + 1][3], gr[c][3], s5);
+                                const uint32_t m = vm[c] & mR;  // the chunk's valid read windows in the run
+                                const uint32_t stop = P1 & (P0 | m) & mR;
+                                const uint32_t below = cut ? 0u : (stop ? ((stop & (0u - stop)) - 1u) : ~0u);
+                                const uint32_t ow = ~(P0 | P1) & m & below;
+                                cnt += (uint32_t)__popc(ow);
+                                ownc[c] = ow;
+                                if (EM) {  // multi-group windows of the run: the EM histogram
+                                    uint32_t todo = P0 & ~P1 & m & below;
+                                    while (todo) {
+                                        const uint32_t d = (uint32_t)__builtin_ctz(todo);
+                                        todo &= todo - 1;
+                                        const uint32_t lo = A.mlo[p + w0 + d];
+                                        atomicAdd(&src.em_mult[lo], 1u);
+                                        src.em_hi[lo] = A.mhi[lo];
+                                    }
+                                }
+                                if (!cut && stop) {
+                                    const uint32_t t = (uint32_t)__builtin_ctz(stop);
+                                    d0 = w0 + t;
+                                    cut_end = ((P0 >> t) & 1u) != 0;
+                                    cut = true;
+                                }
+                            }
                         }
                     }
                     if (STATS) {
