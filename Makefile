@@ -32,7 +32,7 @@ all: $(LIB) $(CLI) oracle $(SYNTH)
 # synthetic-input generator for bench.py / tests (makes inputs, computes no counts)
 $(SYNTH): tools/synth_gen.c
 	@mkdir -p tools/build
-	$(CC) -O2 -fopenmp -fPIC -shared -Wall -Wextra -o $@ $<
+	$(CC) -O2 -fopenmp -fPIC -shared -Wall -Wextra -o $@ $< -lm
 
 $(OBJDIR)/%.o: speq_amd/csrc/%.hip $(HDRS)
 	@mkdir -p $(OBJDIR)

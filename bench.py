@@ -7,7 +7,13 @@ counters (N > 1). Default workload = BASELINE config 2 (10 variants x 50 kb, 1M 
 mode) -> `value`. The same run also measures, as secondary lines in the same JSON object:
   * "local_mode": config 2 in the reference's default Phred-weighted mode (fixed_accuracy 0, arg_parse.h:23);
   * "k31": BASELINE config 3 (50 variants x 3 isolates, k = 31) at its full 10 M reads per GPU — at N = 8 the
-    per-rank shard of config 4 (100 M reads over 8 GPUs, 12.5 M each).
+    per-rank shard of config 4 (100 M reads over 8 GPUs, 12.5 M each);
+  * "k70_reference_defaults": config 2's reads at the reference CLI's defaults (k = 70, Phred-weighted);
+  * "local_varq" (N = 1): config 2, Phred-weighted, with Illumina-like per-base qualities (synth "variable");
+  * "cfg5_paired" / "cfg5_paired_local": BASELINE config 5's index (200 variants x 5 isolates), paired 2 x 150 bp,
+    k = 31, on a per-GPU sample of the config's pairs (--cfg5-pairs);
+  * "fastq_e2e" (N = 1): the drop-in input path, speq_scan_fastq on config 2's reads written as a FASTQ file on
+    local disk (file bytes/s and k-mers/s, page cache warm).
 Weak scaling: every rank scans its own shard of the deterministic read stream.
 
 Launch: python bench.py [--gpus 1 --steps K --warmup W]; for N > 1 the driver uses torch.distributed.run.
@@ -53,6 +59,8 @@ def parse_args():
                    help="skip timing the LF-step kernel beside the table kernel")
     p.add_argument("--no-extra", action="store_true", help="skip the local-mode and k=31 secondary lines")
     p.add_argument("--k31-reads", type=int, default=0, help="reads per GPU of the k=31 line (0 = config 3/4)")
+    p.add_argument("--cfg5-pairs", type=int, default=4_000_000, help="pairs per GPU of the config-5 lines (0: skip)")
+    p.add_argument("--no-fastq", action="store_true", help="skip the FASTQ end-to-end line")
     p.add_argument("--cpu-seconds", type=float, default=15.0, help="target CPU-baseline sample duration")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-pcie", action="store_true", help="skip the PCIe-inclusive host-buffer measurement")
@@ -181,9 +189,11 @@ KERNEL_TAG = {0: "lf", 1: "kt", 2: "kt", 3: "ax"}  # speq_device_get_tuning("las
 
 
 def run_workload(ctx: Ctx, cfg_no: int, k: int, n_reads: int, mode: str, steps: int, warmup: int,
-                 with_lf: bool, with_pcie: bool, with_cpu: bool, cpu_seconds: float, prepared=None) -> dict:
+                 with_lf: bool, with_pcie: bool, with_cpu: bool, cpu_seconds: float, prepared=None,
+                 qual_profile: str = "q40") -> dict:
     """Builds the index of BASELINE config `cfg_no` (or reuses `prepared`), stages this rank's reads in HBM, times
-    `steps` scans and returns the measurement (plus the objects for reuse)."""
+    `steps` scans and returns the measurement (plus the objects for reuse). qual_profile: synth.QUALITY_PROFILES
+    (the reads of `prepared` are regenerated with it when they differ)."""
     torch, a = ctx.torch, ctx.a
     from speq_amd import DeviceIndex, FmIndex, synth
 
@@ -204,12 +214,13 @@ def run_workload(ctx: Ctx, cfg_no: int, k: int, n_reads: int, mode: str, steps: 
         for kv in a.tune:
             key, val = kv.split("=")
             dev.tune(**{key: int(val)})
-        reads = synth.make_reads(ref, n_reads, start_index=ctx.rank * n_reads, paired=paired)
-        d_seq = torch.from_numpy(reads.seq).to(ctx.dev_t)
-        d_qual = torch.from_numpy(reads.qual).to(ctx.dev_t)
-        d_off = torch.from_numpy(reads.offsets.astype(np.int64)).to(ctx.dev_t)
-        prepared = dict(ref=ref, idx=idx, dev=dev, reads=reads, d_seq=d_seq, d_qual=d_qual, d_off=d_off,
-                        build_s=build_s)
+        prepared = dict(ref=ref, idx=idx, dev=dev, build_s=build_s, qual_profile=None)
+    if prepared.get("qual_profile") != qual_profile:
+        reads = synth.make_reads(prepared["ref"], n_reads, start_index=ctx.rank * n_reads, paired=paired)
+        reads = synth.apply_quality_profile(reads, qual_profile)
+        prepared.update(reads=reads, qual_profile=qual_profile, d_seq=torch.from_numpy(reads.seq).to(ctx.dev_t),
+                        d_qual=torch.from_numpy(reads.qual).to(ctx.dev_t),
+                        d_off=torch.from_numpy(reads.offsets.astype(np.int64)).to(ctx.dev_t))
     ref, idx, dev, reads = prepared["ref"], prepared["idx"], prepared["dev"], prepared["reads"]
     d_seq, d_qual, d_off = prepared["d_seq"], prepared["d_qual"], prepared["d_off"]
     ktab = dev.prepare(k)  # per-k index structure (like the .dat cache): built once, outside the timed region
@@ -358,7 +369,9 @@ def run_workload(ctx: Ctx, cfg_no: int, k: int, n_reads: int, mode: str, steps: 
     out = {
         "value": value, "ms_per_step": elapsed / steps * 1e3, "k": k, "mode": mode,
         "workload": f"BASELINE config {cfg_no}: {c['n_variants']} variants x {c['n_isolates']} isolates x "
-                    f"{c['length']} bp, {n_reads} x 150 bp {'pairs' if paired else 'reads'} per GPU, k={k}, {mode}",
+                    f"{c['length']} bp, {n_reads} x 150 bp {'pairs' if paired else 'reads'} per GPU, k={k}, {mode}"
+                    + (f", qualities '{qual_profile}' ({synth.QUALITY_PROFILES[qual_profile]})"
+                       if qual_profile != "q40" else ""),
         "reads_per_gpu": n_reads, "kmers_per_step_per_gpu": kmers_per_step, "paired": paired,
         "index_build_s": round(prepared["build_s"], 3), "fm_text_len": int(idx.info().n),
         "kmer_table": {"on": table_on, "distinct_kmers": ktab["distinct_kmers"], "bytes": ktab["table_bytes"],
@@ -397,6 +410,24 @@ def main():
         extra["k70_reference_defaults"], _ = run_workload(ctx, 2, 70, n_reads, "local", a.steps, a.warmup,
                                                           with_lf=False, with_pcie=False, with_cpu=False,
                                                           cpu_seconds=0, prepared=prep)
+        if ctx.world == 1:
+            if not a.no_fastq:  # the drop-in input path before the reads are re-generated below
+                extra["fastq_e2e"] = fastq_e2e(ctx, prep, k)
+            # the reference's default (Phred-weighted) mode on reads whose qualities vary base by base
+            extra["local_varq"], _ = run_workload(ctx, 2, k, n_reads, "local", a.steps, a.warmup, with_lf=False,
+                                                  with_pcie=False, with_cpu=False, cpu_seconds=0, prepared=prep,
+                                                  qual_profile="variable")
+        if a.cfg5_pairs:
+            # BASELINE config 5 (the north_star's scaling config): paired, k = 31, on a per-GPU sample of its pairs
+            extra["cfg5_paired"], p5 = run_workload(ctx, 5, 31, a.cfg5_pairs, "global", max(3, a.steps // 4),
+                                                    max(1, a.warmup // 2), with_lf=False, with_pcie=False,
+                                                    with_cpu=False, cpu_seconds=0)
+            extra["cfg5_paired"]["note"] = (f"config 5 lists 500 M pairs (a node's job); each GPU scans a "
+                                            f"{a.cfg5_pairs}-pair shard of the same deterministic pair stream")
+            extra["cfg5_paired_local"], _ = run_workload(ctx, 5, 31, a.cfg5_pairs, "local", max(3, a.steps // 4),
+                                                         max(1, a.warmup // 2), with_lf=False, with_pcie=False,
+                                                         with_cpu=False, cpu_seconds=0, prepared=p5)
+            p5["dev"].close()
 
     if ctx.rank == 0:
         out = {
@@ -438,6 +469,56 @@ def main():
         ctx.comm.close()
     if ctx.world > 1:
         ctx.dist.destroy_process_group()
+
+
+def write_fastq(path: str, reads) -> int:
+    """Writes equal-length reads as four-line FASTQ records (@r<9-digit index>), vectorised; returns the bytes."""
+    lens = np.diff(reads.offsets)
+    L = int(lens[0]) if len(lens) else 0
+    if not len(lens) or np.any(lens != L):
+        raise ValueError("write_fastq: equal-length reads only")
+    n = len(lens)
+    head = np.frombuffer(b"@r", dtype=np.uint8)
+    digits = (np.arange(n, dtype=np.int64)[:, None] // (10 ** np.arange(8, -1, -1))[None, :]) % 10 + ord("0")
+    rec = np.empty((n, 2 + 9 + 1 + L + 3 + L + 1), dtype=np.uint8)
+    rec[:, 0:2] = head
+    rec[:, 2:11] = digits.astype(np.uint8)
+    rec[:, 11] = ord("\n")
+    rec[:, 12:12 + L] = reads.seq.reshape(n, L)
+    rec[:, 12 + L:15 + L] = np.frombuffer(b"\n+\n", dtype=np.uint8)
+    rec[:, 15 + L:15 + 2 * L] = reads.qual.reshape(n, L)
+    rec[:, 15 + 2 * L] = ord("\n")
+    rec.tofile(path)
+    return rec.size
+
+
+def fastq_e2e(ctx: Ctx, prep: dict, k: int) -> dict:
+    """The drop-in input path (speq_scan_fastq: reader thread + parser threads -> pinned slots -> H2D || scan) on the
+    workload's reads written as one FASTQ file on local disk; best of 3 passes with the page cache warm. Checked
+    against the HBM-resident scan of the same reads."""
+    import tempfile
+    reads, dev = prep["reads"], prep["dev"]
+    threads = host_cpu_info()["threads"]
+    with tempfile.TemporaryDirectory(dir=os.environ.get("TMPDIR", "/tmp")) as td:
+        path = os.path.join(td, "reads.fq")
+        nbytes = write_fastq(path, reads)
+        ref_res = dev.scan(reads.seq.tobytes(), reads.qual.tobytes(), reads.offsets, k=k)
+        best, res = None, None
+        for _ in range(3):
+            t0 = time.perf_counter()
+            res, st = dev.scan_fastq(path, k=k, threads=threads)
+            dt = time.perf_counter() - t0
+            best = dt if best is None else min(best, dt)
+        if (res.total, res.ambiguous, res.unique.tolist()) != (ref_res.total, ref_res.ambiguous,
+                                                              ref_res.unique.tolist()):
+            raise RuntimeError("FASTQ scan disagrees with the in-memory scan")
+    lens = np.diff(reads.offsets).astype(np.int64)
+    kmers = int(np.maximum(lens - k + 1, 0).sum())
+    return {"value": kmers / best, "unit": "k-mers/s", "file_GB_per_s": nbytes / best / 1e9, "seconds": best,
+            "file_bytes": nbytes, "threads": threads, "k": k,
+            "path": "speq_scan_fastq: plain FASTQ on local disk (page cache warm), parallel record-aligned cut, "
+                    "raw text to pinned slots -> H2D (copy stream) || GPU record parsing + k_scan_ax",
+            "workload": f"{reads.n} x 150 bp reads of BASELINE config 2, global mode"}
 
 
 def cpu_baseline(ref, reads, k, G, target_s, local, paired=False, idx=None):

@@ -9,7 +9,8 @@ line of variant v is ``V<v>(<n_iso>): <first>-<last>``.
 
 Reads: variant drawn with weight (v + 1) (seed 2), isolate uniform, start uniform in [0, len - L], strand 50/50
 (reverse complement), 0.1 % substitution errors (seed 3), quality all 'I' (Q40). Parity fixtures add N bases,
-low-quality bases and short reads on request.
+low-quality bases and short reads on request. `apply_quality_profile` replaces the qualities with an Illumina-like
+profile (QUALITY_PROFILES) for the Phred-weighted scans.
 """
 from __future__ import annotations
 
@@ -198,6 +199,65 @@ def _make_reads_chunk(ref: Reference, n_reads: int, read_len: int, start_index: 
     return Reads(np.ascontiguousarray(seq_flat), np.ascontiguousarray(qual_flat), off, tv)
 
 
+QUALITY_PROFILES = {
+    "q40": "every base 'I' (Q40): every window's Phred weight is the same (the synthetic default)",
+    "binned": "NovaSeq-style 4-bin qualities {2, 12, 23, 37} in runs (per-read Markov chain, more low bins towards "
+              "the 3' end): windows that pass a cutoff of 30 are all Q37",
+    "variable": "HiSeq-style per-base qualities: 40 - 4 pos / L + uniform noise in [-3, 3], plus 2-4 % dips to Q12-29 "
+                "(more towards the 3' end), clipped to [2, 41]: passing windows mix many quality values",
+}
+
+
+def apply_quality_profile(reads: Reads, profile: str, seed: int = 7) -> Reads:
+    """Reads with the qualities of an Illumina-like profile (QUALITY_PROFILES); bases unchanged. Deterministic."""
+    if profile == "q40":
+        return reads
+    if profile not in QUALITY_PROFILES:
+        raise ValueError(f"unknown quality profile {profile!r} (one of {sorted(QUALITY_PROFILES)})")
+    n = len(reads.qual)
+    lens = np.diff(reads.offsets).astype(np.int64)
+    starts = reads.offsets[:-1].astype(np.int64)
+    pos = np.arange(n, dtype=np.int64) - np.repeat(starts, lens)
+    frac = pos.astype(np.float64) / np.maximum(1, np.repeat(lens, lens)).astype(np.float64)
+    L = _synth_lib()
+    if profile == "variable" and L is not None and n:
+        q = np.empty(n, dtype=np.uint8)
+        off = np.ascontiguousarray(reads.offsets, dtype=np.uint64)
+        L.synth_quality_variable(off.ctypes.data, len(off) - 1, seed, q.ctypes.data)
+        return Reads(reads.seq, q, reads.offsets, reads.variant)
+    if profile == "variable":
+        r = rand_u64(seed, 0, n)  # one draw per base: noise (low bits), dip (bits 11-63), dip value (bits 40-)
+        q = 40.0 - 4.0 * frac + ((r % np.uint64(7)).astype(np.float64) - 3.0)
+        dip = (r >> np.uint64(11)).astype(np.float64) * (1.0 / (1 << 53)) < 0.02 + 0.02 * frac
+        q[dip] = 12.0 + ((r[dip] >> np.uint64(40)) % np.uint64(18)).astype(np.float64)
+        q = np.clip(np.rint(q), 2, 41).astype(np.uint8)
+    else:  # binned: a Markov chain over the bins along each read
+        bins = np.array([37, 23, 12, 2], dtype=np.uint8)
+        u = rand_unit(seed, 0, n)
+        state = np.zeros(n, dtype=np.int8)
+        first = pos == 0
+        # leave Q37 with probability 0.03 + 0.05 pos / L (to 23 / 12 / 2 as 6 : 3 : 1), come back with 0.45
+        leave = 0.03 + 0.05 * frac
+        order = np.argsort(pos, kind="stable")  # position-major: every read's previous base comes first
+        sp = pos[order]
+        bounds = np.searchsorted(sp, np.arange(sp[-1] + 2 if n else 1))
+        prev = np.zeros(len(lens), dtype=np.int8)
+        read_of = np.repeat(np.arange(len(lens)), lens)[order]
+        for t in range(len(bounds) - 1):
+            sl = order[bounds[t]:bounds[t + 1]]
+            rs = read_of[bounds[t]:bounds[t + 1]]
+            uu, lv = u[sl], leave[sl]
+            cur = prev[rs]
+            nxt = np.where(cur == 0,
+                           np.where(uu < lv * 0.6, 1, np.where(uu < lv * 0.9, 2, np.where(uu < lv, 3, 0))),
+                           np.where(uu < 0.45, 0, cur))
+            nxt[first[sl]] = np.where(uu[first[sl]] < 0.02, 1, 0)
+            state[sl] = nxt
+            prev[rs] = nxt
+        q = bins[state]
+    return Reads(reads.seq, (q + 33).astype(np.uint8), reads.offsets, reads.variant)
+
+
 _SYNTH_LIB = None
 _SYNTH_PATH = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools", "build",
                            "libsynth_gen.so")
@@ -214,6 +274,8 @@ def _synth_lib():
         L.synth_reads.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint64, C.c_uint64, C.c_uint32, C.c_uint64,
                                   C.c_double, C.c_double, C.c_double, C.c_double, C.c_int, C.c_uint32, C.c_void_p,
                                   C.c_void_p, C.c_void_p, C.c_void_p]
+        L.synth_quality_variable.restype = C.c_int
+        L.synth_quality_variable.argtypes = [C.c_void_p, C.c_uint64, C.c_uint64, C.c_void_p]
         _SYNTH_LIB = L
     return _SYNTH_LIB
 

@@ -8,6 +8,7 @@
  *   2: eight draws per fragment (variant, isolate, start, strand, shorten?, short length)
  *   3: substitution-error test per base, 4: substitution choice, 5: N test, 6: low-quality test
  */
+#include <math.h>
 #include <stddef.h>
 #include <stdint.h>
 #include <string.h>
@@ -98,6 +99,28 @@ int synth_reads(const uint8_t* genomes, uint32_t V, uint32_t I, uint64_t Lg, uin
             }
             lens[rec] = len;
             var[rec] = (int32_t)vv;
+        }
+    }
+    return 0;
+}
+
+/* The "variable" quality profile of speq_amd/synth.py (apply_quality_profile; the numpy version is the fallback and
+ * computes the same bytes): base i of a record at position pos of a record of length L gets, from r = stream `seed`
+ * value i, q = 40 - 4 pos / L + (r % 7 - 3), or a dip to 12 + (r >> 40) % 18 when unit(r) < 0.02 + 0.02 pos / L;
+ * rint, clipped to [2, 41], written as Phred+33. */
+int synth_quality_variable(const uint64_t* offsets, uint64_t n_rec, uint64_t seed, uint8_t* qual) {
+#pragma omp parallel for schedule(static)
+    for (uint64_t rec = 0; rec < n_rec; ++rec) {
+        const uint64_t a = offsets[rec], L = offsets[rec + 1] - a;
+        for (uint64_t pos = 0; pos < L; ++pos) {
+            const uint64_t i = a + pos;
+            const uint64_t r = rnd(seed, i);
+            const double frac = (double)pos / (double)(L ? L : 1);
+            double q = 40.0 - 4.0 * frac + ((double)(r % 7ull) - 3.0);
+            if (unit(r) < 0.02 + 0.02 * frac) q = 12.0 + (double)((r >> 40) % 18ull);
+            q = rint(q);
+            q = q < 2.0 ? 2.0 : (q > 41.0 ? 41.0 : q);
+            qual[i] = (uint8_t)((int)q + 33);
         }
     }
     return 0;
