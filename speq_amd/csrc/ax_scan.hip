@@ -427,11 +427,14 @@ __device__ __forceinline__ bool ax_probe(const AxView& A, const __amdgpu_buffer_
 //   rbase  u64 [64]             (local) offset of the piece's first base in seq/qual
 //   off0s  u8 [64]              the piece's first base in its slot (a - a16)
 //   defl   u16 [AX_DEF]         deferred windows (lane | window << 6), defn u32[4] counters, ambf/ambd i32[64]
+//   wl     u32 [AX_WL]          (local) weight work list: 8-window blocks of runs with varying qualities
+//                               (lane | block << 6 | window mask << 11); wlm u32 [64] the lane's run (group | j << 16)
+constexpr uint32_t AX_WL = 256;  // 64 lanes x 4 blocks per pass
 template <int MODE>
 constexpr uint32_t ax_wave_bytes() {
     static_assert(8u * AX_VWW >= 2u * AX_CHUNKS, "the bad-base bits of a staged piece live in its valid-window words");
     return 4u * AX_CHUNKS * 64u + 8u * AX_VWW * 64u + (MODE == KM_LOCAL ? 2u * AX_CHUNKS * 64u + 8u * 64u : 0u) +
-           64u + 2u * AX_DEF + 16u + 8u * 64u;
+           64u + 2u * AX_DEF + 16u + 8u * 64u + (MODE == KM_LOCAL ? 4u * AX_WL + 4u * 64u : 0u);
 }
 
 #ifndef SPEQ_AX_WPB  // waves per workgroup of k_scan_ax (A/B knob)
@@ -513,6 +516,8 @@ __global__ __launch_bounds__(AX_THREADS, (ax_min_waves<MODE, HW, EM, STATS>())) 
     uint32_t* defn = reinterpret_cast<uint32_t*>(defl + AX_DEF);             // [4]: entries, survivors, sums
     int32_t* ambf = reinterpret_cast<int32_t*>(defn + 4);                    // [64] first counted group
     int32_t* ambd = ambf + 64;                                               // [64] another group seen
+    uint32_t* wl = reinterpret_cast<uint32_t*>(ambd + 64);                   // [AX_WL] (local)
+    uint32_t* wlm = wl + AX_WL;                                              // [64] (local)
 
     if (MODE == KM_LOCAL)
         for (uint32_t i = threadIdx.x; i < QLUT_LEN; i += AX_THREADS) {
@@ -553,11 +558,15 @@ __global__ __launch_bounds__(AX_THREADS, (ax_min_waves<MODE, HW, EM, STATS>())) 
     auto add_count = [&](uint32_t g, uint32_t cnt, double wsum) {
         if (LDS_HIST) {
             atomicAdd(&hA[g], (unsigned long long)cnt);
-            if (MODE == KM_LOCAL) atomicAdd(&hW[g], wsum);
+            if (MODE == KM_LOCAL && wsum != 0.0) atomicAdd(&hW[g], wsum);
         } else {
             atomicAdd(&gU[g], (unsigned long long)cnt);
-            if (MODE == KM_LOCAL) atomicAdd(&out_w[g], wsum);
+            if (MODE == KM_LOCAL && wsum != 0.0) atomicAdd(&out_w[g], wsum);
         }
+    };
+    auto add_weight = [&](uint32_t g, double w) {
+        if (LDS_HIST) atomicAdd(&hW[g], w);
+        else atomicAdd(&out_w[g], w);
     };
     // 32 bases (64 bits) of slot o from slot position pos
     auto slot64 = [&](uint32_t o, uint32_t pos) -> uint64_t {
@@ -584,18 +593,78 @@ __global__ __launch_bounds__(AX_THREADS, (ax_min_waves<MODE, HW, EM, STATS>())) 
         }
         return end;
     };
-    // Phred weight of a window whose first quality byte is at qbase (fm_scanner.cpp:454)
-    auto weight = [&](const uint8_t* qbase, bool uniform, uint32_t qcur) -> double {
-        if (uniform) return wtab[qcur];
+    // Phred weight of the window whose first quality byte is src.qual[qo]. fm_scanner.cpp:454 divides 1 by the lut
+    // values of its k qualities in turn: a window of one quality takes that quotient from wtab (bit-exact); any
+    // other window is the product of the k reciprocals qtab[q].y = fl(1 / lut[q]), within 3 k 2^-53 of the
+    // reference's quotient (relative). Qualities are read as the aligned dwords that hold them.
+    auto weight = [&](uint64_t qo, bool uniform) -> double {
+        const uintptr_t ad = reinterpret_cast<uintptr_t>(src.qual + qo);
+        const uint32_t* wp = reinterpret_cast<const uint32_t*>(ad & ~(uintptr_t)3);
+        const uint32_t sh = (uint32_t)ad & 3u;
+        auto qof = [](uint32_t byte) -> uint32_t {
+            const int q = (int)byte - 33;
+            return q < 0 ? 0u : (q > 41 ? 41u : (uint32_t)q);
+        };
+        if (uniform) {
+            if (STATS) s_qb += 1u;
+            return wtab[qof((wp[0] >> (8u * sh)) & 0xFFu)];
+        }
+        const uint32_t nd = (sh + k + 3u) >> 2;
         double x = 1.0;
-        for (uint32_t i = 0; i < k; ++i) {
-            int q = (int)qbase[i] - 33;
-            q = q < 0 ? 0 : (q > 41 ? 41 : q);
-            const double2 t = qtab[q];
-            x = div_rn(x, t.x, t.y);  // == x / t.x
+        for (uint32_t t = 0; t < nd; ++t) {
+            const uint32_t w = wp[t];
+#pragma unroll
+            for (uint32_t b = 0; b < 4u; ++b) {
+                const uint32_t idx = 4u * t + b;  // the window's base idx - sh
+                const double f = qtab[qof((w >> (8u * b)) & 0xFFu)].y;
+                x = (idx >= sh && idx < sh + k) ? x * f : x;
+            }
         }
         if (STATS) s_qb += k;
         return x;
+    };
+    // the summed weights of the windows t (bits of mask, t < 8) of a block whose first window's first quality byte is
+    // src.qual[qo] (k >= 8): every window t is L_t M R_t with M the product of the reciprocals of bytes 7 .. k - 1
+    // (shared by the 8 windows), L_t of bytes t .. 6 and R_t of bytes k .. k + t - 1, so k + 21 products weigh 8
+    // windows instead of 8 k. Any product tree over k factors rounds k - 1 times: the bound of weight() holds.
+    // Only the dwords that hold a byte of a window in the mask are read (none past the read's last quality byte).
+    auto weight8 = [&](uint64_t qo, uint32_t mask) -> double {
+        const uintptr_t ad = reinterpret_cast<uintptr_t>(src.qual + qo);
+        const uint32_t* wp = reinterpret_cast<const uint32_t*>(ad & ~(uintptr_t)3);
+        const uint32_t sh = (uint32_t)ad & 3u;
+        auto qinv = [&](uint32_t byte) -> double {
+            const int q = (int)(byte & 0xFFu) - 33;
+            return qtab[q < 0 ? 0 : (q > 41 ? 41 : q)].y;
+        };
+        const uint32_t tmax = 31u - (uint32_t)__builtin_clz(mask);  // the last window of the block to weigh
+        const uint32_t a0 = wp[0], a1 = wp[1], a2 = sh >= 2u ? wp[2] : 0u;
+        const uint32_t l03 = __builtin_amdgcn_alignbyte(a1, a0, sh), l47 = __builtin_amdgcn_alignbyte(a2, a1, sh);
+        const uint32_t rs = sh + k, rsh = rs & 3u, rlast = rsh + tmax;  // right bytes k .. k + tmax - 1
+        const uint32_t* rp = wp + (rs >> 2);
+        const uint32_t c0 = tmax >= 1u ? rp[0] : 0u, c1 = rlast > 4u ? rp[1] : 0u, c2 = rlast > 8u ? rp[2] : 0u;
+        const uint32_t r03 = __builtin_amdgcn_alignbyte(c1, c0, rsh), r47 = __builtin_amdgcn_alignbyte(c2, c1, rsh);
+        double M = 1.0;
+        for (uint32_t t = (sh + 7u) >> 2; t <= (sh + k - 1u) >> 2; ++t) {
+            const uint32_t w = wp[t];
+#pragma unroll
+            for (uint32_t b = 0; b < 4u; ++b) {
+                const uint32_t idx = 4u * t + b;
+                const double f = qinv(w >> (8u * b));
+                M = (idx >= sh + 7u && idx < sh + k) ? M * f : M;
+            }
+        }
+        double L[8];
+        L[7] = 1.0;
+#pragma unroll
+        for (int t = 6; t >= 0; --t) L[t] = qinv((t < 4 ? l03 : l47) >> (8 * (t & 3))) * L[t + 1];
+        double MR = M, sum = 0.0;
+#pragma unroll
+        for (uint32_t t = 0; t < 8u; ++t) {
+            sum += ((mask >> t) & 1u) ? L[t] * MR : 0.0;
+            if (t < 7u) MR *= qinv((t < 4u ? r03 : r47) >> (8u * (t & 3u)));
+        }
+        if (STATS) s_qb += k + tmax;
+        return sum;
     };
     // quality-change bits of slot o over slot positions [x, x + len) all zero (local mode)
     auto chg_zero = [&](uint32_t o, uint32_t x, uint32_t len) -> bool {
@@ -745,14 +814,7 @@ __global__ __launch_bounds__(AX_THREADS, (ax_min_waves<MODE, HW, EM, STATS>())) 
                 }
                 if (found && cl == AX_OWN) {
                     double wgt = 0.0;
-                    if (MODE == KM_LOCAL) {
-                        const uint8_t* qb = src.qual + rbase[o] + jj;
-                        const bool uni = chg_zero(o, so + 1u, k - 1u);
-                        int q = (int)qb[0] - 33;
-                        q = q < 0 ? 0 : (q > 41 ? 41 : q);
-                        wgt = weight(qb, uni, (uint32_t)q);
-                        if (STATS) s_qb += 1u;
-                    }
+                    if (MODE == KM_LOCAL) wgt = weight(rbase[o] + jj, chg_zero(o, so + 1u, k - 1u));
                     add_count(pg, 1u, wgt);
                     const int32_t old = atomicCAS(&ambf[o], -1, (int32_t)pg);
                     if (old != -1 && old != (int32_t)pg) ambd[o] = 1;
@@ -1071,6 +1133,12 @@ __global__ __launch_bounds__(AX_THREADS, (ax_min_waves<MODE, HW, EM, STATS>())) 
                 const uint32_t d = rd0 + i;
                 rw[i] = d < AX_CHUNKS ? codes[d * 64u + lane] : 0u;
             }
+            // a run's own windows (chunk c: windows j + 32 c ..); with varying qualities (local mode), weighed by
+            // the whole wave after the run (wl_pend; run group wl_g, first window wl_j)
+            uint32_t ownc[AX_CMPW] = {0u, 0u, 0u, 0u, 0u};
+            static_assert(AX_CMPW == 5, "five 32-window chunks");
+            bool wl_pend = false;
+            uint32_t wl_g = 0, wl_j = 0;
             if (rn) {
                 const uint32_t s5 = p & 31u, q16 = s5 >> 4, tsh = 2u * (s5 & 15u);
                 uint32_t e = cl;  // first mismatching base (cl: none)
@@ -1102,8 +1170,6 @@ __global__ __launch_bounds__(AX_THREADS, (ax_min_waves<MODE, HW, EM, STATS>())) 
                     // in the text: looked up); windows before it are tallied to the run's group.
                     uint32_t d0 = R, cnt = 0;
                     bool cut = false, cut_end = false;
-                    uint32_t ownc[AX_CMPW] = {0u, 0u, 0u, 0u, 0u};
-                    static_assert(AX_CMPW == 5, "five 32-window chunks");
                     // the lane's valid-window bits j .. j + 159 as 32-bit chunks (dwords of its vw column)
                     uint32_t vm[AX_CMPW];
                     {
@@ -1187,20 +1253,9 @@ __global__ __launch_bounds__(AX_THREADS, (ax_min_waves<MODE, HW, EM, STATS>())) 
                                 q = q < 0 ? 0 : (q > 41 ? 41 : q);
                                 wsum = (double)cnt * wtab[q];
                             } else {
-#pragma unroll
-                                for (uint32_t c = 0; c < AX_CMPW; ++c) {
-                                    uint32_t todo = ownc[c];
-                                    while (todo) {
-                                        const uint32_t d = 32u * c + (uint32_t)__builtin_ctz(todo);
-                                        todo &= todo - 1;
-                                        const uint32_t jj = j + d;
-                                        const uint8_t* qb = src.qual + ta + jj;
-                                        int q = (int)qb[0] - 33;
-                                        q = q < 0 ? 0 : (q > 41 ? 41 : q);
-                                        wsum += weight(qb, chg_zero(lane, off0 + jj + 1u, k - 1u), (uint32_t)q);
-                                        if (STATS) s_qb += 1u;
-                                    }
-                                }
+                                wl_pend = true;
+                                wl_g = gt;
+                                wl_j = j;
                             }
                         }
                         add_count(gt, cnt, wsum);
@@ -1240,6 +1295,57 @@ __global__ __launch_bounds__(AX_THREADS, (ax_min_waves<MODE, HW, EM, STATS>())) 
                         if (st == 0u) resume = false;
                     }
                     if (j >= wend) st = 2u;
+                }
+            }
+            if (MODE == KM_LOCAL && __ballot(wl_pend) != 0) {
+                // runs with varying qualities: their own windows in 8-window blocks (20 per run), weighed by the
+                // whole wave, at most 4 blocks of every lane per pass (a lane sums a block's windows, one atomic)
+                uint32_t nzb = 0;
+                if (wl_pend) {
+#pragma unroll
+                    for (uint32_t c = 0; c < AX_CMPW; ++c)
+#pragma unroll
+                        for (uint32_t b = 0; b < 4u; ++b)
+                            nzb |= (((ownc[c] >> (8u * b)) & 0xFFu) != 0u ? 1u : 0u) << (4u * c + b);
+                    wlm[lane] = wl_g | (wl_j << 16);
+                }
+                while (__ballot(nzb != 0u) != 0) {
+                    const uint32_t take = min((uint32_t)__popc(nzb), 4u);
+                    uint32_t pre = 0, tot = 0;
+#pragma unroll
+                    for (uint32_t b = 0; b < 3u; ++b) {
+                        const unsigned long long m = __ballot(((take >> b) & 1u) != 0u);
+                        pre += lanes_below(m) << b;
+                        tot += (uint32_t)__popcll(m) << b;
+                    }
+                    for (uint32_t t = 0; t < take; ++t) {
+                        const uint32_t blk = (uint32_t)__builtin_ctz(nzb);
+                        nzb &= nzb - 1u;
+                        const uint32_t c = blk >> 2;
+                        const uint32_t oc = c == 0u ? ownc[0] : (c == 1u ? ownc[1] : (c == 2u ? ownc[2] : (c == 3u ? ownc[3] : ownc[4])));
+                        wl[pre + t] = lane | (blk << 6) | (((oc >> (8u * (blk & 3u))) & 0xFFu) << 11);
+                    }
+                    wave_sync();
+                    for (uint32_t b0 = 0; b0 < tot; b0 += 64u) {
+                        if (b0 + lane < tot) {
+                            const uint32_t en = wl[b0 + lane];
+                            const uint32_t o = en & 63u, meta = wlm[o];
+                            const uint32_t jb = (meta >> 16) + 8u * ((en >> 6) & 31u);
+                            const uint64_t qo = rbase[o];
+                            double s = 0.0;
+                            if (k >= 8u) {
+                                s = weight8(qo + jb, en >> 11);
+                            } else {
+                                const uint32_t so = (uint32_t)off0s[o];
+                                for (uint32_t m = en >> 11; m; m &= m - 1u) {
+                                    const uint32_t jj = jb + (uint32_t)__builtin_ctz(m);
+                                    s += weight(qo + jj, chg_zero(o, so + jj + 1u, k - 1u));
+                                }
+                            }
+                            add_weight(meta & 0xFFFFu, s);
+                        }
+                    }
+                    wave_sync();
                 }
             }
         }

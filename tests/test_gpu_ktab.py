@@ -115,14 +115,17 @@ def test_launch_knobs_keep_results(small, ilp_kt, kt_slots):
 
 
 def test_phred_weight_of_one_window_is_bit_exact(small):
-    """A read of exactly k bases that occurs in one group: W[g] is that window's weight, which must equal the
-    reference's left-to-right divisions w = w / (1 - 1/10^(q/10)) (fm_scanner.cpp:454) to the last bit."""
+    """A read of exactly k bases that occurs in one group: W[g] is that window's weight, the reference's
+    left-to-right divisions w = w / (1 - 1/10^(q/10)) (fm_scanner.cpp:454). The k-mer-table kernel divides the same
+    way (bit-exact); the anchor kernel takes one-quality windows from its quotient table (bit-exact) and multiplies
+    the k reciprocals of any other window: |w - w_ref| <= 3 k 2^-53 w."""
     ref, idx = small
     rng = np.random.default_rng(11)
     devs = [DeviceIndex(idx), DeviceIndex(idx)]
     devs[1].tune(ax_scan=0)  # both read-scan kernels
     k = 31
     checked = 0
+    tol = 3 * k * 2.0 ** -53
     for _ in range(150):
         r = int(rng.integers(0, len(ref.records)))
         rec = ref.records[r]
@@ -133,7 +136,7 @@ def test_phred_weight_of_one_window_is_bit_exact(small):
         # varied qualities, or one quality for the whole window (weight from the per-block uniform-q table)
         q = rng.integers(31, 42, size=k) if checked % 2 else np.full(k, int(rng.integers(31, 42)))
         qual = bytes((q + 33).astype(np.uint8))
-        for dev in devs:
+        for dev, exact in zip(devs, (checked % 2 == 0, True)):
             res = dev.scan(seq, qual, np.array([0, k], dtype=np.uint64), k=k, local=True)
             if res.unique.sum() != 1:
                 break  # the window is shared by several groups
@@ -141,7 +144,10 @@ def test_phred_weight_of_one_window_is_bit_exact(small):
             for x in q:
                 w = w / (1.0 - 1.0 / (10.0 ** (float(x) / 10.0)))
             g = int(np.argmax(res.unique))
-            assert res.weights[g] == w, (res.weights[g], w)
+            if exact:
+                assert res.weights[g] == w, (res.weights[g], w)
+            else:
+                assert abs(res.weights[g] - w) <= tol * w, (res.weights[g], w)
         else:
             checked += 1
     assert checked > 50
