@@ -430,11 +430,15 @@ __device__ __forceinline__ bool ax_probe(const AxView& A, const __amdgpu_buffer_
 //   wl     u32 [AX_WL]          (local) weight work list: 8-window blocks of runs with varying qualities
 //                               (lane | block << 6 | window mask << 11); wlm u32 [64] the lane's run (group | j << 16)
 constexpr uint32_t AX_WL = 256;  // 64 lanes x 4 blocks per pass
+#ifndef SPEQ_AX_SU_MAX  // staging batch sizes the owner map holds (A/B knob)
+#define SPEQ_AX_SU_MAX 2
+#endif
+constexpr uint32_t AX_OWNB = 64u * SPEQ_AX_SU_MAX;  // bytes of the staging owner map (64 x SPEQ_AX_SU)
 template <int MODE>
 constexpr uint32_t ax_wave_bytes() {
     static_assert(8u * AX_VWW >= 2u * AX_CHUNKS, "the bad-base bits of a staged piece live in its valid-window words");
     return 4u * AX_CHUNKS * 64u + 8u * AX_VWW * 64u + (MODE == KM_LOCAL ? 2u * AX_CHUNKS * 64u + 8u * 64u : 0u) +
-           64u + 2u * AX_DEF + 16u + 8u * 64u + (MODE == KM_LOCAL ? 4u * AX_WL + 4u * 64u : 0u);
+           64u + 2u * AX_DEF + 16u + 8u * 64u + (MODE == KM_LOCAL ? 4u * AX_WL + 4u * 64u : 0u) + AX_OWNB;
 }
 
 #ifndef SPEQ_AX_WPB  // waves per workgroup of k_scan_ax (A/B knob)
@@ -461,6 +465,11 @@ constexpr uint32_t AX_WPB = SPEQ_AX_WPB, AX_THREADS = 64 * SPEQ_AX_WPB;
 #endif
 #ifndef SPEQ_AX_BLOCKED  // idle lanes waiting for their deferred windows that trigger the deferred-window pass
 #define SPEQ_AX_BLOCKED 16
+#endif
+#ifndef SPEQ_AX_PROBE  // timing probes (wrong counts; make axvariant only): 1 staging only, 2 no deferred-window pass,
+                       // 3 staging loads only (no decode), 5 as 3 without the valid-window bits, 6 / 7 as 3 without the
+                       // doubling steps / the bad-bit reads
+#define SPEQ_AX_PROBE 0
 #endif
 // EM scans and the instrumented twin hold more live state: 4 waves (no spills)
 template <int MODE, int HW, bool EM, bool STATS>
@@ -518,6 +527,7 @@ __global__ __launch_bounds__(AX_THREADS, (ax_min_waves<MODE, HW, EM, STATS>())) 
     int32_t* ambd = ambf + 64;                                               // [64] another group seen
     uint32_t* wl = reinterpret_cast<uint32_t*>(ambd + 64);                   // [AX_WL] (local)
     uint32_t* wlm = wl + AX_WL;                                              // [64] (local)
+    uint8_t* ownb = reinterpret_cast<uint8_t*>(MODE == KM_LOCAL ? wlm + 64 : wl);  // [AX_OWNB] staging owner map
 
     if (MODE == KM_LOCAL)
         for (uint32_t i = threadIdx.x; i < QLUT_LEN; i += AX_THREADS) {
@@ -690,8 +700,9 @@ __global__ __launch_bounds__(AX_THREADS, (ax_min_waves<MODE, HW, EM, STATS>())) 
     bool hasdef = false;       // deferred windows of this lane's piece are in the wave's list
     // ---- the wave's pool (uniform): an equal share of the units, [nu w / NWV, nu (w + 1) / NWV) — contiguous
     // reads (coalesced staging), and every wave gets the same number of units so the waves finish together (a
-    // launch-wide counter handing out groups was slower: one contended atomic address)
-    uint64_t cur = (nu * gw) / NWV;            // next unit
+    // launch-wide counter handing out groups was slower: one contended atomic address; so were groups of 64-256 units
+    // dealt round robin, profiles/r03/ax_variants_owner_group.jsonl)
+    uint64_t cur = (nu * gw) / NWV;  // next unit
     const uint64_t cur_end = (nu * (gw + 1)) / NWV;
     // ---- phase-1 state of the current piece
     uint32_t wend = 0;         // windows of the piece
@@ -721,6 +732,7 @@ __global__ __launch_bounds__(AX_THREADS, (ax_min_waves<MODE, HW, EM, STATS>())) 
         const unsigned long long idle = __ballot(st == 2u);
         const unsigned long long blk = __ballot(st == 2u && hasdef);
         const unsigned long long busy = ~idle;
+        if (SPEQ_AX_PROBE == 2 && lane == 0) defn[0] = 0u;  // probe: deferred windows are dropped
         const uint32_t n_def = __builtin_amdgcn_readfirstlane(defn[0]);
         if (blk != 0 && ((uint32_t)__popcll(blk) >= SPEQ_AX_BLOCKED || busy == 0 || n_def + 256u > AX_DEF)) {
             // ---- phase 2: the deferred windows of the wave. (a) the Bloom filter, AX_F windows per lane per round
@@ -854,8 +866,9 @@ __global__ __launch_bounds__(AX_THREADS, (ax_min_waves<MODE, HW, EM, STATS>())) 
             const unsigned long long tk = __ballot(wants && !has_unit);
             uint64_t newu = nu;
             const uint32_t rank = lanes_below(tk);
+            const uint64_t taken = (uint64_t)__popcll(tk);
             if (wants && !has_unit && cur + rank < cur_end) newu = cur + rank;
-            cur = min(cur + (uint64_t)__popcll(tk), cur_end);
+            cur = min(cur + taken, cur_end);
             bool stg = false;
             if (wants) {
                 if (!has_unit) {
@@ -895,7 +908,8 @@ __global__ __launch_bounds__(AX_THREADS, (ax_min_waves<MODE, HW, EM, STATS>())) 
                 }
             }
             // ---- coalesced staging: the refilling lanes' chunks laid end to end (lane o's at [pre_o, pre_o + nch_o));
-            // every lane of the wave decodes whole chunks, found by a binary search over the lanes' chunk ranges
+            // every lane of the wave decodes whole chunks, SU x 64 chunks per batch (software-pipelining the batches,
+            // the next one's loads in flight while one is decoded, spilled 128 B per lane and was slower)
             static_assert(AX_CHUNKS < 16, "chunk counts in four bits");
             uint32_t pre = 0, nch_tot = 0;
 #pragma unroll
@@ -904,28 +918,53 @@ __global__ __launch_bounds__(AX_THREADS, (ax_min_waves<MODE, HW, EM, STATS>())) 
                 pre += lanes_below(m) << bb;
                 nch_tot += (uint32_t)__popcll(m) << bb;
             }
-            const uint32_t endc = pre + nch;
             uint32_t qcarry = 0;  // local: last quality dword of the previous instruction's lane 63
-            constexpr uint32_t SU = SPEQ_AX_SU;  // stream instructions whose loads are in flight together
-            for (uint32_t c0 = 0; c0 < nch_tot; c0 += 64u * SU) {
-                uint4 sv[SU], qv[SU];
-                uint32_t own[SU], ci[SU];
+            uint32_t ocarry = 0;  // owner mark of the last chunk of the previous 64
+            constexpr uint32_t SU = SPEQ_AX_SU;  // stream instructions of one batch
+            static_assert(64u * SU <= AX_OWNB, "owner map of one batch");
+            // owners and loads of the batch from chunk c0: every refilling lane marks the first chunk of its range in
+            // a byte map (lane + 1); a prefix max over the lanes (DPP; owners grow with the chunk index) spreads the
+            // mark over the range, and the last owner carries into the next 64 chunks
+            auto issue = [&](uint32_t c0, uint4(&sv)[SU], uint4(&qv)[SU], uint32_t(&own)[SU], uint32_t(&ci)[SU]) {
+#pragma unroll
+                for (uint32_t u = 0; u < SU; ++u) ownb[64u * u + lane] = 0;
+                if (nch != 0u && pre >= c0 && pre < c0 + 64u * SU) ownb[pre - c0] = (uint8_t)(lane + 1u);
+                wave_sync();
+                uint32_t mk[SU];
+#pragma unroll
+                for (uint32_t u = 0; u < SU; ++u) mk[u] = ownb[64u * u + lane];
 #pragma unroll
                 for (uint32_t u = 0; u < SU; ++u) {
                     const uint32_t c = min(c0 + 64u * u + lane, nch_tot - 1u);
-                    uint32_t o = 0;  // the first lane whose chunk range ends after c
-#pragma unroll
-                    for (uint32_t d = 32; d >= 1; d >>= 1)
-                        o = ((uint32_t)__shfl((int)endc, (int)(o + d - 1u)) <= c) ? o + d : o;
+                    uint32_t m = mk[u];
+                    m = max(m, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)m, 0x111, 0xF, 0xF, false));  // row_shr:1
+                    m = max(m, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)m, 0x112, 0xF, 0xF, false));  // row_shr:2
+                    m = max(m, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)m, 0x114, 0xF, 0xF, false));  // row_shr:4
+                    m = max(m, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)m, 0x118, 0xF, 0xF, false));  // row_shr:8
+                    m = max(m, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)m, 0x142, 0xA, 0xF, false));  // row_bcast:15
+                    m = max(m, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)m, 0x143, 0xC, 0xF, false));  // row_bcast:31
+                    m = max(m, ocarry);
+                    ocarry = (uint32_t)__builtin_amdgcn_readlane((int)m, 63);
+                    const uint32_t o = m - 1u;
                     own[u] = o;
                     ci[u] = c - (uint32_t)__shfl((int)pre, (int)o);
                     const uint64_t go = (uint64_t)__shfl((long long)a16, (int)o) + 16ull * ci[u];
                     sv[u] = *reinterpret_cast<const uint4*>(src.seq + go);
                     qv[u] = *reinterpret_cast<const uint4*>(src.qual + go);
                 }
+            };
+            // decodes the batch from chunk c0 into the owners' slots: 2-bit codes, bad-base bits, quality changes
+            auto decode = [&](uint32_t c0, const uint4(&sv)[SU], const uint4(&qv)[SU], const uint32_t(&own)[SU],
+                              const uint32_t(&ci)[SU]) {
 #pragma unroll
                 for (uint32_t u = 0; u < SU; ++u) {
                     const uint32_t c = c0 + 64u * u + lane;
+                    if (SPEQ_AX_PROBE == 3 || SPEQ_AX_PROBE >= 5) {  // probe: the loads only
+                        if (c < nch_tot)
+                            codes[ci[u] * 64u + own[u]] = sv[u].x ^ sv[u].y ^ sv[u].z ^ sv[u].w ^ qv[u].x ^ qv[u].y ^
+                                                          qv[u].z ^ qv[u].w;
+                        continue;
+                    }
                     const uint32_t sd[4] = {sv[u].x, sv[u].y, sv[u].z, sv[u].w};
                     const uint32_t qd[4] = {qv[u].x, qv[u].y, qv[u].z, qv[u].w};
                     uint32_t cw = 0, bad = 0, chb = 0;
@@ -959,54 +998,64 @@ __global__ __launch_bounds__(AX_THREADS, (ax_min_waves<MODE, HW, EM, STATS>())) 
                         if (MODE == KM_LOCAL) chg[ci[u] * 64u + own[u]] = (uint16_t)chb;
                     }
                 }
+            };
+            for (uint32_t c0 = 0; c0 < nch_tot; c0 += 64u * SU) {
+                uint4 sv[SU], qv[SU];
+                uint32_t own[SU], ci[SU];
+                issue(c0, sv, qv, own, ci);
+                decode(c0, sv, qv, own, ci);
             }
             wave_sync();
-            if (stg) {
-                // this lane's bad-base bits (16 per chunk from a16; chunks past its piece are bad)
-                uint64_t ok[4];
+            if (SPEQ_AX_PROBE == 5 && stg) {  // probe: no valid-window bits either
+                st = 2u;
+            } else if (stg) {
+                // this lane's good-base bits, 16 per chunk from a16 (chunks past its piece are bad), as 8 dwords
+                uint32_t ok[8];
+                {
+                    const uint32_t* vw32 = reinterpret_cast<const uint32_t*>(vw);
+                    const uint32_t nb = 16u * nch;
 #pragma unroll
-                for (int i = 0; i < 4; ++i) {
-                    uint64_t v = vw[(uint32_t)i * 64u + lane];  // chunks 4i .. 4i + 3, 16 bits each
-                    const uint32_t b0 = 64u * (uint32_t)i, nb = 16u * nch;
-                    if (nb <= b0) v = ~0ull;
-                    else if (nb < b0 + 64u) v |= ~0ull << (nb - b0);
-                    ok[i] = ~v;
-                }
-                // valid windows: AND of k consecutive "good" bits (doubling), then shifted to the read's first base
-                for (uint32_t len = 1; len < k;) {
-                    const uint32_t sft = min(len, k - len);
-                    const uint32_t ws = sft >> 6, bs = sft & 63u;
-                    uint64_t nx[4];
-#pragma unroll
-                    for (int i = 0; i < 4; ++i) {
-                        uint64_t lo = 0ull, hi = 0ull;  // ok[i + ws], ok[i + ws + 1] (zero past the end), no indexing
-#pragma unroll
-                        for (int t = 0; t < 4; ++t) {
-                            lo = (uint32_t)(t - i) == ws ? ok[t] : lo;
-                            hi = (uint32_t)(t - i) == ws + 1u ? ok[t] : hi;
-                        }
-                        nx[i] = ok[i] & funnel(lo, hi, bs);
+                    for (uint32_t d = 0; d < 8u; ++d) {
+                        const uint32_t b0 = 32u * d;  // dword d: chunks 2d, 2d + 1 (word d / 2 of the lane's column)
+                        uint32_t v = SPEQ_AX_PROBE == 7 ? 0u : vw32[((d >> 1) * 64u + lane) * 2u + (d & 1u)];
+                        v |= nb <= b0 ? ~0u : (nb < b0 + 32u ? ~0u << (nb - b0) : 0u);
+                        ok[d] = ~v;
                     }
+                }
+                // valid windows: AND of k consecutive good bits (doubling: shifts of at most 64 bits, one funnel
+                // shift per dword), then aligned to the piece's first base
+                for (uint32_t len = SPEQ_AX_PROBE == 6 ? k : 1u; len < k;) {
+                    const uint32_t sft = min(len, k - len);  // 1 .. 64
+                    const uint32_t dw = sft >> 5, bs = sft & 31u;
+                    if (dw == 0u) {
 #pragma unroll
-                    for (int i = 0; i < 4; ++i) ok[i] = nx[i];
+                        for (uint32_t d = 0; d < 8u; ++d) ok[d] &= alignbit(d + 1u < 8u ? ok[d + 1] : 0u, ok[d], bs);
+                    } else if (dw == 1u) {
+#pragma unroll
+                        for (uint32_t d = 0; d < 8u; ++d)
+                            ok[d] &= alignbit(d + 2u < 8u ? ok[d + 2] : 0u, d + 1u < 8u ? ok[d + 1] : 0u, bs);
+                    } else {  // sft == 64
+#pragma unroll
+                        for (uint32_t d = 0; d < 8u; ++d) ok[d] &= d + 2u < 8u ? ok[d + 2] : 0u;
+                    }
                     len += sft;
                 }
-                uint64_t vv[AX_VWW];
+                // valid-window bits of the piece (window j at bit j): the good-window dwords from slot position
+                // off0 (< 16, so dword d + {0, 1}), none past wend
+                wave_sync();  // (own column only; keeps the bad-bit reads before the overwrite below)
+                {
+                    uint32_t* vw32 = reinterpret_cast<uint32_t*>(vw);
 #pragma unroll
-                for (uint32_t i = 0; i < AX_VWW; ++i) {
-                    const uint64_t lo = ok[i], hi = i + 1 < 4 ? ok[i + 1] : 0ull;
-                    uint64_t v = funnel(lo, hi, off0);
-                    const uint32_t bit0 = 64u * i;
-                    if (wend <= bit0) v = 0;
-                    else if (wend < bit0 + 64u) v &= (1ull << (wend - bit0)) - 1ull;
-                    vv[i] = v;
-                    t_cnt += (uint32_t)__popcll(v);
+                    for (uint32_t d = 0; d < 2u * AX_VWW; ++d) {
+                        uint32_t v = alignbit(d + 1u < 8u ? ok[d + 1] : 0u, ok[d], off0);
+                        const uint32_t bit0 = 32u * d;
+                        v = wend <= bit0 ? 0u : (wend < bit0 + 32u ? v & ((1u << (wend - bit0)) - 1u) : v);
+                        t_cnt += (uint32_t)__popc(v);
+                        vw32[((d >> 1) * 64u + lane) * 2u + (d & 1u)] = v;
+                    }
                 }
-                wave_sync();  // (own slot only; keeps the bad-bit reads before the overwrite below)
-#pragma unroll
-                for (uint32_t i = 0; i < AX_VWW; ++i) vw[i * 64u + lane] = vv[i];
                 j = 0;
-                st = wend > 0 ? 0u : 2u;
+                st = (wend > 0 && SPEQ_AX_PROBE != 1 && SPEQ_AX_PROBE != 3 && SPEQ_AX_PROBE < 6) ? 0u : 2u;
                 verify = false;
                 resume = false;
                 last_mm = -1;
@@ -1094,7 +1143,7 @@ __global__ __launch_bounds__(AX_THREADS, (ax_min_waves<MODE, HW, EM, STATS>())) 
                                 defl[sl++] = (uint16_t)(lane | ((j + 1u + (uint32_t)__builtin_ctzll(t)) << 6));
                             for (uint64_t t = dm1; t; t &= t - 1)
                                 defl[sl++] = (uint16_t)(lane | ((j + 65u + (uint32_t)__builtin_ctzll(t)) << 6));
-                            hasdef = true;
+                            hasdef = SPEQ_AX_PROBE != 2;
                             if (STATS) s_def += cnt;
                         } else {  // no room: the windows stay with this lane; void the slots reserved below the end
                             for (uint32_t sl = slot0; sl < AX_DEF && sl < slot0 + cnt; ++sl) defl[sl] = AX_VOID;
@@ -1274,7 +1323,7 @@ __global__ __launch_bounds__(AX_THREADS, (ax_min_waves<MODE, HW, EM, STATS>())) 
                             const uint32_t slot = atomicAdd(&defn[0], 1u);
                             if (slot < AX_DEF) {
                                 defl[slot] = (uint16_t)(lane | ((j + d0) << 6));
-                                hasdef = true;
+                                hasdef = SPEQ_AX_PROBE != 2;
                                 if (STATS) s_def += 1u;
                                 j += d0 + 1u;
                                 p += d0 + 1u;
