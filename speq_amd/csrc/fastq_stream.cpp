@@ -338,7 +338,9 @@ struct Buf {
     size_t cap = 0, len = 0;
     void* map = nullptr;
     size_t map_len = 0;
-    ~Buf() {
+    bool registered = false;  // page-locked for direct DMA (SPEQ_FASTQ_DIRECT=2); every copy from it has completed
+    ~Buf() {                  // before the last block releases it (run_stream drains the copies first)
+        if (registered) speq::host_unregister(map);
         if (map) ::munmap(map, map_len);
     }
     char* data() const { return ptr; }
@@ -603,10 +605,14 @@ struct Sink {
     virtual void acquire_raw(speq_slot& s, uint64_t bytes) { acquire(s, bytes, 1); }
     virtual void submit(const speq_slot& s, uint64_t records) = 0;  // records == 0 releases the slot
     // raw four-line FASTQ text (file 1's block, then file 2's) in s.seq, n records per file
-    virtual void submit_raw(const speq_slot& s, uint64_t len1, uint64_t len2, uint64_t n, bool paired) {
-        (void)s; (void)len1; (void)len2; (void)n; (void)paired;
+    // host1 / host2 non-null: the blocks are copied from there (the file's mapping), not from s.seq
+    virtual void submit_raw(const speq_slot& s, uint64_t len1, uint64_t len2, uint64_t n, bool paired,
+                            const char* host1 = nullptr, const char* host2 = nullptr) {
+        (void)s; (void)len1; (void)len2; (void)n; (void)paired; (void)host1; (void)host2;
         throw std::logic_error("this sink does not parse raw FASTQ");
     }
+    // waits until every H2D copy issued so far has completed (before a registered mapping is released)
+    virtual void drain_copies() {}
     // records packed by pack_records (s.offsets filled; 3 bits per base when `three`, else one byte)
     virtual void submit_packed(const speq_slot& s, uint64_t records, bool three) {
         (void)s; (void)records; (void)three;
@@ -753,8 +759,13 @@ struct PipelineSink final : Sink {
     void submit(const speq_slot& s, uint64_t records) override {
         check_rc(speq_pipeline_submit(of(s.slot), local(s.slot), records));
     }
-    void submit_raw(const speq_slot& s, uint64_t len1, uint64_t len2, uint64_t n, bool paired) override {
-        speq::pipeline_submit_raw(of(s.slot), local(s.slot), len1, len2, n, paired);
+    void submit_raw(const speq_slot& s, uint64_t len1, uint64_t len2, uint64_t n, bool paired, const char* host1,
+                    const char* host2) override {
+        speq::pipeline_submit_raw(of(s.slot), local(s.slot), len1, len2, n, paired,
+                                  reinterpret_cast<const uint8_t*>(host1), reinterpret_cast<const uint8_t*>(host2));
+    }
+    void drain_copies() override {
+        for (speq_pipeline* pl : pls) speq::pipeline_sync_copies(pl);
     }
     void submit_packed(const speq_slot& s, uint64_t records, bool three) override {
         if (three) speq::pipeline_submit_packed3(of(s.slot), local(s.slot), records);
@@ -895,7 +906,7 @@ void parallel_for(uint32_t threads, size_t n, F&& fn) {
 // both files, so any layout this does not fit fails there (or here) and the caller runs the sequential reader.
 // Files with different record counts also go to the sequential reader (its zip rule and read-ahead decide).
 StreamTotals run_paired_split(const std::shared_ptr<Buf>& m1, const std::shared_ptr<Buf>& m2, uint32_t threads,
-                              Sink& sink, ShardSel shard, PackMode pm) {
+                              Sink& sink, ShardSel shard, PackMode pm, int direct) {
     const uint64_t BLOCK_RECORDS = 1u << 15, BLOCK_BYTES = 12ull << 20;
     const char* d1 = m1->data();
     const char* d2 = m2->data();
@@ -950,10 +961,14 @@ StreamTotals run_paired_split(const std::shared_ptr<Buf>& m1, const std::shared_
             return;
         }
         sink.acquire_raw(s, l1 + l2);
-        // copies with streaming stores where the destination is 16-B aligned (no read-for-ownership)
-        (void)copy_count_nl(reinterpret_cast<char*>(s.seq), d1 + b1[i], l1);
-        (void)copy_count_nl(reinterpret_cast<char*>(s.seq) + l1, d2 + s2, l2);
-        sink.submit_raw(s, l1, l2, n, true);
+        if (direct) {  // H2D straight from the mappings (the record counts came from the newline pass above)
+            sink.submit_raw(s, l1, l2, n, true, d1 + b1[i], d2 + s2);
+        } else {
+            // copies with streaming stores where the destination is 16-B aligned (no read-for-ownership)
+            (void)copy_count_nl(reinterpret_cast<char*>(s.seq), d1 + b1[i], l1);
+            (void)copy_count_nl(reinterpret_cast<char*>(s.seq) + l1, d2 + s2, l2);
+            sink.submit_raw(s, l1, l2, n, true);
+        }
         batches += 1;
         records += 2 * n;
     });
@@ -966,7 +981,7 @@ StreamTotals run_paired_split(const std::shared_ptr<Buf>& m1, const std::shared_
 // starts at byte 0, the chains join into exactly the records the sequential cutter finds. Throws NotSimple when a
 // block is not such a chain (the caller discards what was submitted and runs again without `split`).
 StreamTotals run_stream(const char* path1, const char* path2, uint32_t threads, Sink& sink, bool gpu_parse,
-                        bool split, ShardSel shard = {}, PackMode pm = {}) {
+                        bool split, ShardSel shard = {}, PackMode pm = {}, int direct = 0) {
     const bool paired = path2 != nullptr;
     const uint32_t n_parsers = std::max<uint32_t>(1, std::min<uint32_t>(threads ? threads : 1, 64));
     const uint64_t BLOCK_RECORDS = 1u << 15, BLOCK_BYTES = 12ull << 20;  // pipeline slots hold SLOT_BYTES
@@ -975,13 +990,28 @@ StreamTotals run_stream(const char* path1, const char* path2, uint32_t threads, 
     Cutter c1(path1, threads, !try_split);
     std::unique_ptr<Cutter> c2;
     if (paired) c2 = std::make_unique<Cutter>(path2, threads, !try_split);
+    // direct 2: the mappings are page-locked (one registration each) and copied by DMA straight from the page
+    // cache; every copy completes before they are released (drain, which runs before the cutters go)
+    auto reg = [&](const std::shared_ptr<Buf>& m) {
+        if (direct == 2 && m && !m->registered && m->map) m->registered = speq::host_register_readonly(m->map, m->map_len);
+    };
+    struct Drain {
+        Sink& s;
+        bool on;
+        ~Drain() {
+            if (on) try { s.drain_copies(); } catch (...) {}
+        }
+    } drain{sink, direct != 0};
     if (try_split && paired) {
         std::shared_ptr<Buf> m1 = c1.mapping(), m2 = c2->mapping();
-        if (m1 && m2) return run_paired_split(m1, m2, n_parsers, sink, shard, pm);
+        reg(m1);
+        reg(m2);
+        if (m1 && m2) return run_paired_split(m1, m2, n_parsers, sink, shard, pm, direct);
     }
     Shared sh;
     sh.max_q = n_parsers + 1;
     const std::shared_ptr<Buf> map = split && !paired ? c1.mapping() : nullptr;
+    if (gpu_parse) reg(map);
     auto push = [&](Work&& w) {
         std::unique_lock<std::mutex> lk(sh.mu);
         sh.cv_put.wait(lk, [&] { return sh.q.size() < sh.max_q || sh.failed; });
@@ -1094,13 +1124,15 @@ StreamTotals run_stream(const char* path1, const char* path2, uint32_t threads, 
                     const bool eof = w.b1.end == w.b1.buf->len;
                     speq_slot s;
                     sink.acquire_raw(s, l1);
-                    uint64_t lines = copy_count_nl(reinterpret_cast<char*>(s.seq), w.b1.data(), l1);
+                    // direct: one read-only newline pass over the mapping, then H2D from the mapping itself
+                    uint64_t lines = direct ? count_nl(w.b1.data(), l1)
+                                            : copy_count_nl(reinterpret_cast<char*>(s.seq), w.b1.data(), l1);
                     if (eof && l1 && w.b1.data()[l1 - 1] != '\n') ++lines;
                     if (lines == 0 || lines % 4 != 0) {
                         sink.submit(s, 0);
                         throw NotSimple();
                     }
-                    sink.submit_raw(s, l1, 0, lines / 4, false);
+                    sink.submit_raw(s, l1, 0, lines / 4, false, direct ? w.b1.data() : nullptr);
                     sh.records += lines / 4;
                     sh.batches += 1;
                     if (sh.failed) return;
@@ -1259,11 +1291,19 @@ void scan_fastq_impl(speq_device_index* const* ds, speq_em* const* ems, uint32_t
         if (fp && fp[0] == '1') pm.kind = params->mode == SPEQ_MODE_GLOBAL ? 2 : 1;
         pm.cutoff = params->phred_cutoff;
     }
+    // SPEQ_FASTQ_DIRECT (A/B knob, default 0 = copy into the pinned slots): raw blocks of a mapped file go to the GPU
+    // straight from the page-cache mapping, the parsers only counting newlines — 1: hipMemcpyAsync from the pageable
+    // mapping; 2: the mapping page-locked once (hipHostRegister, read-only) and copied by DMA.
+    int direct = 0;
+    {
+        const char* e = std::getenv("SPEQ_FASTQ_DIRECT");
+        if (e && (e[0] == '1' || e[0] == '2')) direct = e[0] - '0';
+    }
     std::vector<uint64_t> scratch(SPEQ_COUNTS_LEN(G));
     std::vector<double> wscratch(std::max<uint32_t>(G, 1));
     auto attempt = [&](bool split) {
         try {
-            StreamTotals t = run_stream(path1, path2, threads, sink, gpu_parse, split, shard, pm);
+            StreamTotals t = run_stream(path1, path2, threads, sink, gpu_parse, split, shard, pm, direct);
             // split blocks are parsed on the GPU unchecked by the host: any failed check means a layout the
             // parallel cut cannot handle (or a malformed file) -> sequential run, which reports real errors
             if (split && gpu_parse) {

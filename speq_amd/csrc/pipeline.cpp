@@ -311,7 +311,8 @@ int speq_pipeline_submit(speq_pipeline* pl, int32_t slot, uint64_t n_records) {
 }  // extern "C"
 
 namespace speq {
-void pipeline_submit_raw(speq_pipeline* pl, int32_t slot, uint64_t len1, uint64_t len2, uint64_t n, bool paired) {
+void pipeline_submit_raw(speq_pipeline* pl, int32_t slot, uint64_t len1, uint64_t len2, uint64_t n, bool paired,
+                         const uint8_t* host1, const uint8_t* host2) {
     struct Release {
         speq_pipeline* pl;
         int32_t slot;
@@ -349,7 +350,12 @@ void pipeline_submit_raw(speq_pipeline* pl, int32_t slot, uint64_t len1, uint64_
         s.scratch_bytes = sb;
     }
     std::lock_guard<std::mutex> lk(pl->submit_mu);
-    hip_ok(hipMemcpyAsync(s.d_seq, s.h_seq, len1 + len2, hipMemcpyHostToDevice, pl->copy), "hipMemcpyAsync");
+    if (host1) {  // straight from the file's mapping (pageable: staged by the runtime, no slot copy on this thread)
+        hip_ok(hipMemcpyAsync(s.d_seq, host1, len1, hipMemcpyHostToDevice, pl->copy), "hipMemcpyAsync");
+        if (len2) hip_ok(hipMemcpyAsync(s.d_seq + len1, host2, len2, hipMemcpyHostToDevice, pl->copy), "hipMemcpyAsync");
+    } else {
+        hip_ok(hipMemcpyAsync(s.d_seq, s.h_seq, len1 + len2, hipMemcpyHostToDevice, pl->copy), "hipMemcpyAsync");
+    }
     hip_ok(hipEventRecord(s.copied, pl->copy), "hipEventRecord");
     hipStream_t cs = pl->lane();
     hip_ok(hipStreamWaitEvent(cs, s.copied, 0), "hipStreamWaitEvent");
@@ -359,6 +365,15 @@ void pipeline_submit_raw(speq_pipeline* pl, int32_t slot, uint64_t len1, uint64_
                       pl->em ? pl->em->d_mult : nullptr, pl->em ? pl->em->d_hi : nullptr, cs);
     hip_ok(hipEventRecord(s.done, cs), "hipEventRecord");
     s.pending = true;
+}
+
+bool host_register_readonly(void* p, size_t n) {
+    return hipHostRegister(p, n, hipHostRegisterReadOnly) == hipSuccess;
+}
+void host_unregister(void* p) { (void)hipHostUnregister(p); }
+void pipeline_sync_copies(speq_pipeline* pl) {
+    DevScope g(pl->device);
+    hip_ok(hipStreamSynchronize(pl->copy), "hipStreamSynchronize");
 }
 
 // Host packer of the one-byte-per-base format (launch_unpack_bases): dna5 (A C G T, U as T, any case; everything else

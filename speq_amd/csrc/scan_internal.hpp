@@ -46,7 +46,16 @@ inline uint64_t packed3_bytes(uint64_t n) { return (n + 31) / 32 * 12; }
 void pipeline_submit_packed3(speq_pipeline* pl, int32_t slot, uint64_t n_records);
 // Submits an acquired pipeline slot whose host buffer holds RAW four-line FASTQ text (file 1's block, then file
 // 2's when paired, n records each): copied as is, parsed on the GPU, then scanned (pipeline.cpp).
-void pipeline_submit_raw(speq_pipeline* pl, int32_t slot, uint64_t len1, uint64_t len2, uint64_t n, bool paired);
+// host1 / host2: copy the two blocks from these (pageable) host addresses instead of the slot's pinned buffer — the
+// page-cache mapping of the file (SPEQ_FASTQ_DIRECT); the copy has left them when this returns (the runtime stages
+// pageable sources before hipMemcpyAsync returns).
+void pipeline_submit_raw(speq_pipeline* pl, int32_t slot, uint64_t len1, uint64_t len2, uint64_t n, bool paired,
+                         const uint8_t* host1 = nullptr, const uint8_t* host2 = nullptr);
+// Page-locks [p, p + n) of a read-only file mapping for direct DMA (hipHostRegister, read-only flag); false when the
+// runtime refuses. host_unregister undoes it; pipeline_sync_copies waits for every H2D copy issued on pl so far.
+bool host_register_readonly(void* p, size_t n);
+void host_unregister(void* p);
+void pipeline_sync_copies(speq_pipeline* pl);
 // Acquires a slot for raw FASTQ text of up to `bytes` (no quality buffer; submit it with pipeline_submit_raw or
 // release it with speq_pipeline_submit(pl, slot, 0)); *text receives the pinned host buffer.
 int32_t pipeline_acquire_raw(speq_pipeline* pl, uint64_t bytes, uint8_t** text);
