@@ -27,6 +27,7 @@ def main():
     ap.add_argument("--paired", action="store_true")
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--variants", type=int, default=0, help="override the config's variant (group) count")
+    ap.add_argument("--qual", default="q40", help="quality profile (speq_amd.synth.QUALITY_PROFILES)")
     a = ap.parse_args()
     c = dict(synth.CONFIGS[a.config])
     if a.variants:
@@ -41,6 +42,8 @@ def main():
     G = c["n_variants"]
     for err in [float(x) for x in a.err.split(",")]:
         reads = synth.make_reads(ref, a.reads, err_rate=err, paired=a.paired)
+        if a.qual != "q40":
+            reads = synth.apply_quality_profile(reads, a.qual)
         d_seq = torch.from_numpy(reads.seq).cuda()
         d_qual = torch.from_numpy(reads.qual).cuda()
         d_off = torch.from_numpy(reads.offsets.astype(np.int64)).cuda()
@@ -64,7 +67,7 @@ def main():
                     best = ms if best is None else min(best, ms)
             print(json.dumps({"err": err, "k": k, "ms": round(best, 4), "Gkmers_s": round(kmers / best / 1e6, 1),
                               "kernel": dev.tuning("last_kernel"), "T": int(cnt[0]), "amb": int(cnt[1]),
-                              "tune": a.tune, "local": a.local, "table_bytes": info["table_bytes"]}), flush=True)
+                              "tune": a.tune, "local": a.local, "qual": a.qual, "table_bytes": info["table_bytes"]}), flush=True)
 
 
 if __name__ == "__main__":
