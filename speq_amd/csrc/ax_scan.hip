@@ -61,8 +61,15 @@ constexpr uint32_t AX_CMPW = AX_CMP / 32;        // 2-bit words of one compare
 constexpr uint32_t AX_NGR = AX_CMPW + 1;         // granules that cover AX_CMP bases from any offset in the first
 constexpr uint32_t AX_CHK = 3;                   // 64-window class chunks of one run (<= AX_CMP - k + 1 windows)
 constexpr uint32_t AX_VWW = 4;        // valid-window words per lane (>= AX_CAP - k + 1 windows; 16 B per staged chunk)
-constexpr uint32_t AX_DEF = 896;      // deferred-window entries per wave (u16: lane | window << 6); 7.9 KB per wave
-                                      // (5 blocks of 4 waves per CU)
+#ifndef SPEQ_AX_DEF_LOCAL  // deferred-window entries per wave in local mode (A/B knob)
+#define SPEQ_AX_DEF_LOCAL 448
+#endif
+// deferred-window entries per wave (u16: lane | window << 6): global mode 896 (7.9 KB per wave: 5 blocks of 4 waves
+// per CU); local mode 448, so that its 9.7 KB per wave fit 4 blocks per CU (up to 77 groups)
+template <int MODE>
+constexpr uint32_t ax_def() {
+    return MODE == KM_LOCAL ? SPEQ_AX_DEF_LOCAL : 896u;
+}
 constexpr uint32_t AX_F = 4;          // deferred windows a lane tests against the filter per round trip
 constexpr uint32_t AX_EMPTY = 0xFFFFFFFFu;
 constexpr uint16_t AX_VOID = 0xFFFFu;  // a deferred-list slot reserved by a lane that then kept its windows
@@ -424,12 +431,16 @@ __device__ __forceinline__ bool ax_probe(const AxView& A, const __amdgpu_buffer_
 //   vw     u64 [AX_VWW][64]     valid-window bits, read-relative (window j of the piece at bit j); while staging, the
 //                               bad-base bits of the refilling lanes, chunk c in 16 bits of the lane's own word c / 4
 //   chg    u16 [AX_CHUNKS][64]  (local) quality-change bits per slot position
-//   rbase  u64 [64]             (local) offset of the piece's first base in seq/qual
+//   rbase  u32 [64]             (local) offset of the piece's first base in seq/qual, from the wave's first unit's
 //   off0s  u8 [64]              the piece's first base in its slot (a - a16)
-//   defl   u16 [AX_DEF]         deferred windows (lane | window << 6), defn u32[4] counters, ambf/ambd i32[64]
+//   defl   u16 [ax_def]         deferred windows (lane | window << 6), defn u32[4] counters, ambf/ambd i32[64]
 //   wl     u32 [AX_WL]          (local) weight work list: 8-window blocks of runs with varying qualities
 //                               (lane | block << 6 | window mask << 11); wlm u32 [64] the lane's run (group | j << 16)
-constexpr uint32_t AX_WL = 256;  // 64 lanes x 4 blocks per pass
+#ifndef SPEQ_AX_WL  // weight work-list entries per wave (A/B knob): 64 lanes x AX_WL / 64 blocks per pass
+#define SPEQ_AX_WL 128
+#endif
+constexpr uint32_t AX_WL = SPEQ_AX_WL, AX_WL_TAKE = AX_WL / 64u;
+static_assert(AX_WL % 64u == 0 && AX_WL_TAKE >= 1u && AX_WL_TAKE <= 7u, "work list: 1-7 blocks per lane per pass");
 #ifndef SPEQ_AX_SU_MAX  // staging batch sizes the owner map holds (A/B knob)
 #define SPEQ_AX_SU_MAX 2
 #endif
@@ -437,8 +448,8 @@ constexpr uint32_t AX_OWNB = 64u * SPEQ_AX_SU_MAX;  // bytes of the staging owne
 template <int MODE>
 constexpr uint32_t ax_wave_bytes() {
     static_assert(8u * AX_VWW >= 2u * AX_CHUNKS, "the bad-base bits of a staged piece live in its valid-window words");
-    return 4u * AX_CHUNKS * 64u + 8u * AX_VWW * 64u + (MODE == KM_LOCAL ? 2u * AX_CHUNKS * 64u + 8u * 64u : 0u) +
-           64u + 2u * AX_DEF + 16u + 8u * 64u + (MODE == KM_LOCAL ? 4u * AX_WL + 4u * 64u : 0u) + AX_OWNB;
+    return 4u * AX_CHUNKS * 64u + 8u * AX_VWW * 64u + (MODE == KM_LOCAL ? 2u * AX_CHUNKS * 64u + 4u * 64u : 0u) +
+           64u + 2u * ax_def<MODE>() + 16u + 8u * 64u + (MODE == KM_LOCAL ? 4u * AX_WL + 4u * 64u : 0u) + AX_OWNB;
 }
 
 #ifndef SPEQ_AX_WPB  // waves per workgroup of k_scan_ax (A/B knob)
@@ -519,9 +530,10 @@ __global__ __launch_bounds__(AX_THREADS, (ax_min_waves<MODE, HW, EM, STATS>())) 
     uint64_t* vw = reinterpret_cast<uint64_t*>(codes + AX_CHUNKS * 64u);     // [AX_VWW][64]
     uint16_t* bad16 = reinterpret_cast<uint16_t*>(vw);                       // staging: see bad_at
     uint16_t* chg = reinterpret_cast<uint16_t*>(vw + AX_VWW * 64u);          // [AX_CHUNKS][64] (local)
-    uint64_t* rbase = reinterpret_cast<uint64_t*>(chg + (MODE == KM_LOCAL ? AX_CHUNKS * 64u : 0u));  // [64] (local)
+    uint32_t* rbase = reinterpret_cast<uint32_t*>(chg + (MODE == KM_LOCAL ? AX_CHUNKS * 64u : 0u));  // [64] (local)
     uint8_t* off0s = reinterpret_cast<uint8_t*>(rbase + (MODE == KM_LOCAL ? 64u : 0u));              // [64]
     uint16_t* defl = reinterpret_cast<uint16_t*>(off0s + 64);                // [AX_DEF]
+    constexpr uint32_t AX_DEF = ax_def<MODE>();
     uint32_t* defn = reinterpret_cast<uint32_t*>(defl + AX_DEF);             // [4]: entries, survivors, sums
     int32_t* ambf = reinterpret_cast<int32_t*>(defn + 4);                    // [64] first counted group
     int32_t* ambd = ambf + 64;                                               // [64] another group seen
@@ -704,6 +716,7 @@ __global__ __launch_bounds__(AX_THREADS, (ax_min_waves<MODE, HW, EM, STATS>())) 
     // dealt round robin, profiles/r03/ax_variants_owner_group.jsonl)
     uint64_t cur = (nu * gw) / NWV;  // next unit
     const uint64_t cur_end = (nu * (gw + 1)) / NWV;
+    const uint64_t wbase = MODE == KM_LOCAL ? src.off[PAIRED ? 2 * cur : cur] : 0;  // rbase origin (local)
     // ---- phase-1 state of the current piece
     uint32_t wend = 0;         // windows of the piece
     uint32_t off0 = 0;         // first base of the piece in the slot
@@ -826,7 +839,7 @@ __global__ __launch_bounds__(AX_THREADS, (ax_min_waves<MODE, HW, EM, STATS>())) 
                 }
                 if (found && cl == AX_OWN) {
                     double wgt = 0.0;
-                    if (MODE == KM_LOCAL) wgt = weight(rbase[o] + jj, chg_zero(o, so + 1u, k - 1u));
+                    if (MODE == KM_LOCAL) wgt = weight(wbase + rbase[o] + jj, chg_zero(o, so + 1u, k - 1u));
                     add_count(pg, 1u, wgt);
                     const int32_t old = atomicCAS(&ambf[o], -1, (int32_t)pg);
                     if (old != -1 && old != (int32_t)pg) ambd[o] = 1;
@@ -901,7 +914,7 @@ __global__ __launch_bounds__(AX_THREADS, (ax_min_waves<MODE, HW, EM, STATS>())) 
                 off0 = noff0;
                 ta = a;
                 off0s[lane] = (uint8_t)noff0;
-                if (MODE == KM_LOCAL) rbase[lane] = a;
+                if (MODE == KM_LOCAL) rbase[lane] = (uint32_t)(a - wbase);
                 if (STATS) {
                     s_ch += nch;
                     s_seg += 1u;
@@ -1359,7 +1372,7 @@ __global__ __launch_bounds__(AX_THREADS, (ax_min_waves<MODE, HW, EM, STATS>())) 
                     wlm[lane] = wl_g | (wl_j << 16);
                 }
                 while (__ballot(nzb != 0u) != 0) {
-                    const uint32_t take = min((uint32_t)__popc(nzb), 4u);
+                    const uint32_t take = min((uint32_t)__popc(nzb), AX_WL_TAKE);
                     uint32_t pre = 0, tot = 0;
 #pragma unroll
                     for (uint32_t b = 0; b < 3u; ++b) {
@@ -1380,7 +1393,7 @@ __global__ __launch_bounds__(AX_THREADS, (ax_min_waves<MODE, HW, EM, STATS>())) 
                             const uint32_t en = wl[b0 + lane];
                             const uint32_t o = en & 63u, meta = wlm[o];
                             const uint32_t jb = (meta >> 16) + 8u * ((en >> 6) & 31u);
-                            const uint64_t qo = rbase[o];
+                            const uint64_t qo = wbase + rbase[o];
                             double s = 0.0;
                             if (k >= 8u) {
                                 s = weight8(qo + jb, en >> 11);
