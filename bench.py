@@ -48,6 +48,7 @@ def parse_args():
     p.add_argument("--pair-steps", type=int, default=1)
     p.add_argument("--label-table", default="auto", help="auto|0|1 (auto: only for >= 4 M-symbol indexes)")
     p.add_argument("--mode", choices=["global", "local"], default="global")
+    p.add_argument("--qual", default="q40", help="quality profile of the headline reads (speq_amd.synth.QUALITY_PROFILES)")
     p.add_argument("--ilp", type=int, default=0, help="windows per lane of the LF-step kernel (1|2; 0 = default)")
     p.add_argument("--gpu-build", type=int, default=1, help="build the index on the GPU (1) or host SA-IS (0)")
     p.add_argument("--triple-steps", type=int, default=1, help="three-symbol occ planes (1) or not (0)")
@@ -167,7 +168,7 @@ def kernel_model(dev, k: int, table_on: bool, kmers: int, read_bytes: int, n_rea
             "model": "SURVEY.md 8(d): k LF steps x 2 occ-block loads x 64 B"}
 
 
-def traffic_lookup(cfg: int, k: int, mode: str, n_reads: int, kernel: str) -> dict | None:
+def traffic_lookup(cfg: int, k: int, mode: str, n_reads: int, kernel: str, qual_profile: str = "q40") -> dict | None:
     """Measured fabric bytes per launch of this exact workload and kernel (rocprofv3 PMC passes summarised into
     profiles/traffic.json by scripts/summarize_profile.py --traffic-key), or None."""
     prof = os.path.join(ROOT, "profiles", "traffic.json")
@@ -177,7 +178,7 @@ def traffic_lookup(cfg: int, k: int, mode: str, n_reads: int, kernel: str) -> di
         tj = json.load(open(prof))
     except ValueError:
         return None
-    key = f"cfg{cfg}_k{k}_{mode}_reads{n_reads}_{kernel}"
+    key = f"cfg{cfg}_k{k}_{mode}_reads{n_reads}_{kernel}" + ("" if qual_profile == "q40" else f"_{qual_profile}")
     if key not in tj:
         return None
     e = dict(tj[key])
@@ -319,7 +320,7 @@ def run_workload(ctx: Ctx, cfg_no: int, k: int, n_reads: int, mode: str, steps: 
         km["bytes_per_kmer"] = 0.0
     own_gbs = own_bytes / avg_kernel_s / 1e9
     survey_gbs = kmers_per_step * 2 * k * OCC_ENTRY_BYTES / avg_kernel_s / 1e9
-    tr = traffic_lookup(cfg_no, k, mode, n_reads, KERNEL_TAG.get(hot_kernel, "lf"))
+    tr = traffic_lookup(cfg_no, k, mode, n_reads, KERNEL_TAG.get(hot_kernel, "lf"), qual_profile)
     traffic = tr["hbm_bytes_per_launch"] if tr else None
     roofline = {
         "bound": "hbm", "achieved": own_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": own_gbs / HBM_PEAK_GBS,
@@ -392,10 +393,11 @@ def main():
     k = a.k or c["k"]
     n_reads = a.reads or (c["n_reads"] if a.config <= 3 else c["n_reads"] // 8)
     head, prep = run_workload(ctx, a.config, k, n_reads, a.mode, a.steps, a.warmup, with_lf=not a.no_lf_compare,
-                              with_pcie=not a.no_pcie, with_cpu=not a.no_cpu_baseline, cpu_seconds=a.cpu_seconds)
+                              with_pcie=not a.no_pcie, with_cpu=not a.no_cpu_baseline, cpu_seconds=a.cpu_seconds,
+                              qual_profile=a.qual)
     dev = prep["dev"]
     extra = {}
-    if not a.no_extra and a.config == 2 and not a.k and not a.reads:
+    if not a.no_extra and a.config == 2 and not a.k and not a.reads and a.qual == "q40":
         other = "local" if a.mode == "global" else "global"
         extra[f"{other}_mode"], _ = run_workload(ctx, 2, k, n_reads, other, a.steps, a.warmup, with_lf=False,
                                                  with_pcie=False, with_cpu=False, cpu_seconds=0, prepared=prep)
