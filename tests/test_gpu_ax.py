@@ -110,9 +110,43 @@ def test_random_and_error_heavy_reads_overflow_the_deferred_list(small):
     seq = np.concatenate([rnd, noisy.seq, clean.seq])
     qual = np.full(seq.size, ord("I"), dtype=np.uint8)
     off = np.arange(0, seq.size + 1, L, dtype=np.uint64)
-    for k in (11, 21, 31, 45):
+    for k in (11, 21, 31, 45, 70, 100):
         for local in (False, True):
             check(dev, Oracle(ref.records, ref.groups, 4, k), seq, qual, off, k, local=local)
+
+
+def test_speculative_left_runs_at_text_starts():
+    """k > 64: a window found absent with no known mismatch (a read's first window over an error) leaves the windows
+    after it pending, and a hit on the window past them is compared from the pending windows on, against the text
+    shifted back from the anchor. Reads from the first bases of short records whose k-mers the other
+    records share put anchors near text starts (the shifted text would cross a text end: the fallback), and one to
+    three errors in the first 90 bases give absent windows after absent windows (pending windows deferred first)
+    and pending windows at the end of a read."""
+    ref = synth.make_reference(6, 3, 400)
+    idx = FmIndex.build(ref.records, ref.groups, 6, prefix_q=8, pair_steps=True, triple_steps=True)
+    dev = DeviceIndex(idx)
+    rng = np.random.default_rng(11)
+    comp = np.frombuffer(bytes.maketrans(b"ACGT", b"TGCA"), dtype=np.uint8)
+    parts = []
+    for i in range(6_000):
+        rec = np.frombuffer(ref.records[int(rng.integers(len(ref.records)))], dtype=np.uint8)
+        L = int(rng.choice([150, 150, 100, 75]))
+        s0 = int(rng.integers(0, 8)) if i % 2 else int(rng.integers(0, rec.size - L + 1))
+        r = rec[s0:s0 + L].copy()
+        if i % 3 == 0:
+            r = comp[r[::-1]]
+        for _ in range(int(rng.integers(1, 4))):
+            pos = int(rng.integers(0, min(90, L)))
+            r[pos] = np.frombuffer(b"ACGT", dtype=np.uint8)[(np.searchsorted(np.frombuffer(b"ACGT", dtype=np.uint8),
+                                                                            r[pos]) + 1 + int(rng.integers(3))) % 4]
+        parts.append(r)
+    seq = np.concatenate(parts)
+    off = np.concatenate([[0], np.cumsum([p.size for p in parts])]).astype(np.uint64)
+    qual = np.full(seq.size, ord("I"), dtype=np.uint8)
+    qual[rng.random(seq.size) < 0.01] = ord("#")  # a few low-quality bases: invalid windows between anchors
+    for k in (65, 70, 97, 128):
+        for local in (False, True):
+            check(dev, Oracle(ref.records, ref.groups, 6, k), seq, qual, off, k, local=local)
 
 
 @pytest.mark.parametrize("k", [11, 21, 23, 31])
