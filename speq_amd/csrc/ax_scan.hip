@@ -477,9 +477,6 @@ constexpr uint32_t AX_WPB = SPEQ_AX_WPB, AX_THREADS = 64 * SPEQ_AX_WPB;
 #ifndef SPEQ_AX_BLOCKED  // idle lanes waiting for their deferred windows that trigger the deferred-window pass
 #define SPEQ_AX_BLOCKED 16
 #endif
-#ifndef SPEQ_AX_SPEC_HW  // speculative left runs after an absent lookup whose mismatch is unknown, for HW >= this
-#define SPEQ_AX_SPEC_HW 4  // (k > 64 by default; 8 = off). A/B knob
-#endif
 #ifndef SPEQ_AX_PROBE  // timing probes (wrong counts; make axvariant only): 1 staging only, 2 no deferred-window pass,
                        // 3 staging loads only (no decode), 5 as 3 without the valid-window bits, 6 / 7 as 3 without the
                        // doubling steps / the bad-bit reads
@@ -733,39 +730,6 @@ __global__ __launch_bounds__(AX_THREADS, (ax_min_waves<MODE, HW, EM, STATS>())) 
     uint32_t pb = 0, ps = 0;   // probe position of the current lookup (bucket, first slot)
     bool resume = false;       // continue the current lookup at (pb, ps): full bucket, or failed verification
     bool run_phase = true;     // this wave iteration extends runs (else: looks windows up)
-    // Speculative left runs (SPEC): window j_f absent with no known mismatch (a read's first window over a sequencing
-    // error) used to defer the k - 1 windows after it, of which those right of the error are present (Bloom filter
-    // passes, one phase-2 lookup each: ~k/2 per such read). Instead the lane keeps them pending (sp = j_f + 1),
-    // looks up the first window past them, and on a hit compares the read from sp against the text shifted back to
-    // sp (ps = AX_PS_SPEC): the first mismatch e (the error) defers only the windows [sp, sp + e] that hold it, and
-    // the rest continues as a run from sp + e + 1 (ps = AX_PS_FRESH: its first k bases are not compared yet).
-    constexpr bool SPEC = HW >= SPEQ_AX_SPEC_HW && !EM;
-    constexpr uint32_t AX_PS_SPEC = 16u, AX_PS_FRESH = 17u;
-    uint32_t sp = 0;  // 1 + ... : the pending windows are [sp, sp + k - 2]; 0 none
-
-    // defers the valid windows of [lo, hi] (hi - lo <= 127; hi < lo: none) of this lane's piece to the wave's list;
-    // false when the list has no room (nothing deferred, the reserved slots voided)
-    auto defer_range = [&](uint32_t lo, uint32_t hi) -> bool {
-        if (hi + 1u <= lo) return true;
-        const uint32_t span = hi + 1u - lo;
-        uint64_t dm0 = vbits(lane, lo), dm1 = span > 64u ? vbits(lane, lo + 64u) : 0ull;
-        dm0 &= span >= 64u ? ~0ull : ((1ull << span) - 1ull);
-        if (span > 64u) dm1 &= span - 64u >= 64u ? ~0ull : ((1ull << (span - 64u)) - 1ull);
-        const uint32_t cnt = (uint32_t)__popcll(dm0) + (uint32_t)__popcll(dm1);
-        if (cnt == 0u) return true;
-        const uint32_t slot0 = atomicAdd(&defn[0], cnt);
-        if (slot0 + cnt > AX_DEF) {  // no room: void the slots reserved below the end
-            for (uint32_t sl = slot0; sl < AX_DEF && sl < slot0 + cnt; ++sl) defl[sl] = AX_VOID;
-            return false;
-        }
-        uint32_t sl = slot0;
-        for (uint64_t t = dm0; t; t &= t - 1) defl[sl++] = (uint16_t)(lane | ((lo + (uint32_t)__builtin_ctzll(t)) << 6));
-        for (uint64_t t = dm1; t; t &= t - 1)
-            defl[sl++] = (uint16_t)(lane | ((lo + 64u + (uint32_t)__builtin_ctzll(t)) << 6));
-        hasdef = SPEQ_AX_PROBE != 2;
-        if (STATS) s_def += cnt;
-        return true;
-    };
 
     auto start_read = [&](uint64_t r) {
         rd = r;
@@ -1104,7 +1068,6 @@ __global__ __launch_bounds__(AX_THREADS, (ax_min_waves<MODE, HW, EM, STATS>())) 
                     }
                 }
                 j = 0;
-                sp = 0;
                 st = (wend > 0 && SPEQ_AX_PROBE != 1 && SPEQ_AX_PROBE != 3 && SPEQ_AX_PROBE < 6) ? 0u : 2u;
                 verify = false;
                 resume = false;
@@ -1125,14 +1088,6 @@ __global__ __launch_bounds__(AX_THREADS, (ax_min_waves<MODE, HW, EM, STATS>())) 
         // by VALU issue, profiles/r03), and a kind no lane needs is skipped.
         if (st == 0u) {
             j = next_valid(lane, j, wend);
-            if (SPEC && sp != 0u && j >= wend) {  // no window left to anchor the pending ones: defer them
-                if (defer_range(sp, min(sp + k - 2u, wend - 1u))) {
-                    sp = 0;
-                } else {  // no room: look them up one by one
-                    j = next_valid(lane, sp, wend);
-                    sp = 0;
-                }
-            }
             if (j >= wend) st = 2u;
         }
         const unsigned long long busy1 = __ballot(st != 2u);
@@ -1179,53 +1134,36 @@ __global__ __launch_bounds__(AX_THREADS, (ax_min_waves<MODE, HW, EM, STATS>())) 
                     st = 1u;
                     verify = true;
                     resume = false;
-                    if (SPEC && sp != 0u) {  // pending windows [sp, j): the run starts there, text shifted back
-                        const uint32_t back = j - sp;
-                        if (cp >= back && back < 128u) {
-                            p = cp - back;
-                            j = sp;
-                            ps = AX_PS_SPEC;
-                            pb = back;  // (no probe to resume from a speculative run)
-                        } else if (!defer_range(sp, min(sp + k - 2u, j - 1u))) {  // (text start) defer them
-                            j = next_valid(lane, sp, wend);  // no room: look them up one by one
-                            st = 0u;
-                        }
-                        sp = 0;
-                    }
-                } else if (SPEC && res == 0u && !(last_mm >= (int32_t)j && last_mm < (int32_t)(j + k)) &&
-                           j + k < wend) {
-                    // absent, mismatch unknown: the next k - 1 windows stay pending, the window after them is
-                    // looked up (earlier pending windows are deferred first)
-                    resume = false;
-                    if (sp != 0u && !defer_range(sp, sp + k - 2u)) {
-                        j = next_valid(lane, sp, wend);  // no room: look them up one by one
-                        sp = 0;
-                    } else {
-                        sp = j + 1u;
-                        j += k;
-                    }
-                    last_mm = -1;
                 } else if (res == 0u) {
                     // absent: defer the windows that share the mismatch (or the next k - 1), skip past them
                     resume = false;
-                    bool pend_ok = true;
-                    if (SPEC && sp != 0u) {  // pending windows first (no room: looked up one by one)
-                        pend_ok = defer_range(sp, min(sp + k - 2u, j - 1u));
-                        if (!pend_ok) {
-                            j = next_valid(lane, sp, wend);
-                            last_mm = -1;
+                    uint32_t dend = (last_mm >= (int32_t)j && last_mm < (int32_t)(j + k)) ? (uint32_t)last_mm
+                                                                                           : j + k - 1u;
+                    dend = min(dend, wend - 1u);
+                    // the valid windows of (j, dend] as two 64-bit masks (dend - j <= k - 1 <= 127)
+                    const uint32_t span = dend - j;
+                    uint64_t dm0 = vbits(lane, j + 1u), dm1 = span > 64u ? vbits(lane, j + 65u) : 0ull;
+                    dm0 &= span >= 64u ? ~0ull : ((1ull << span) - 1ull);
+                    if (span > 64u) dm1 &= span - 64u >= 64u ? ~0ull : ((1ull << (span - 64u)) - 1ull);
+                    const uint32_t cnt = (uint32_t)__popcll(dm0) + (uint32_t)__popcll(dm1);
+                    bool ok_def = true;
+                    if (cnt) {
+                        const uint32_t slot0 = atomicAdd(&defn[0], cnt);
+                        ok_def = slot0 + cnt <= AX_DEF;
+                        if (ok_def) {
+                            uint32_t sl = slot0;
+                            for (uint64_t t = dm0; t; t &= t - 1)
+                                defl[sl++] = (uint16_t)(lane | ((j + 1u + (uint32_t)__builtin_ctzll(t)) << 6));
+                            for (uint64_t t = dm1; t; t &= t - 1)
+                                defl[sl++] = (uint16_t)(lane | ((j + 65u + (uint32_t)__builtin_ctzll(t)) << 6));
+                            hasdef = SPEQ_AX_PROBE != 2;
+                            if (STATS) s_def += cnt;
+                        } else {  // no room: the windows stay with this lane; void the slots reserved below the end
+                            for (uint32_t sl = slot0; sl < AX_DEF && sl < slot0 + cnt; ++sl) defl[sl] = AX_VOID;
                         }
-                        sp = 0;
                     }
-                    if (pend_ok) {
-                        uint32_t dend = (last_mm >= (int32_t)j && last_mm < (int32_t)(j + k)) ? (uint32_t)last_mm
-                                                                                               : j + k - 1u;
-                        dend = min(dend, wend - 1u);
-                        // the valid windows of (j, dend] (no room: they stay with this lane, the next one is
-                        // looked up)
-                        j = defer_range(j + 1u, dend) ? dend + 1u : j + 1u;
-                        last_mm = -1;
-                    }
+                    j = ok_def ? dend + 1u : j + 1u;
+                    last_mm = -1;
                 } else {  // full bucket without the key or an empty slot: the next bucket
                     pb = pb + 1u == (uint32_t)A.nb ? 0u : pb + 1u;
                     ps = 0;
@@ -1281,56 +1219,10 @@ __global__ __launch_bounds__(AX_THREADS, (ax_min_waves<MODE, HW, EM, STATS>())) 
                     x &= nb >= 16u ? ~0u : ((1u << (2u * nb)) - 1u);
                     e = x ? b0 + ((uint32_t)__builtin_ctz(x) >> 1) : e;
                 }
-                // a speculative left run must stay in the text of its anchor: no END window (a text end) among the
-                // windows [0, pb) before the anchored one, else the pending windows are deferred and the anchored
-                // window is compared from its own position next iteration
-                bool sep = false;
-                if (SPEC && ps == AX_PS_SPEC) {
-#pragma unroll
-                    for (uint32_t c = 0; c < 4u; ++c) {
-                        const uint32_t w0 = 32u * c;
-                        const uint32_t P0 = alignbit(gr[c + 1][2], gr[c][2], s5);
-                        const uint32_t P1 = alignbit(gr[c + 1][3], gr[c][3], s5);
-                        const uint32_t m = pb <= w0 ? 0u : (pb - w0 >= 32u ? ~0u : ((1u << (pb - w0)) - 1u));
-                        sep = sep || (P0 & P1 & m) != 0u;
-                    }
-                }
-                if (sep) {
-                    if (defer_range(j, j + pb - 1u)) {
-                        j += pb;
-                        p += pb;
-                        ps = AX_PS_FRESH;  // (verify stays set)
-                    } else {  // no room: look them up one by one
-                        st = 0u;
-                        resume = false;
-                        ps = 0;
-                    }
-                    last_mm = -1;
-                } else if (verify && e < k) {
-                    if (SPEC && ps == AX_PS_SPEC) {
-                        // speculative left run: the windows [j, j + e] hold its first mismatch (the read's error):
-                        // deferred; the run continues after it, its first k bases still to compare
-                        if (defer_range(j, j + e)) {
-                            j += e + 1u;
-                            p += e + 1u;
-                            ps = AX_PS_FRESH;
-                            st = j < wend ? 1u : 2u;
-                        } else {  // no room: look them up one by one
-                            st = 0u;
-                            resume = false;
-                            ps = 0;
-                        }
-                        last_mm = -1;
-                    } else if (SPEC && ps == AX_PS_FRESH) {  // no match from here: look window j up
-                        st = 0u;
-                        resume = false;
-                        ps = 0;
-                        last_mm = (int32_t)(j + e);
-                    } else {  // fingerprint collision: resume probing after that slot
-                        st = 0u;
-                        resume = true;
-                        ++ps;
-                    }
+                if (verify && e < k) {  // fingerprint collision: resume probing after that slot
+                    st = 0u;
+                    resume = true;
+                    ++ps;
                 } else {
                     uint32_t R = e - (k - 1u);  // e >= k - 1: a candidate matched k bases, a run k - 1
                     R = min(R, wend - j);

@@ -115,13 +115,12 @@ def test_random_and_error_heavy_reads_overflow_the_deferred_list(small):
             check(dev, Oracle(ref.records, ref.groups, 4, k), seq, qual, off, k, local=local)
 
 
-def test_speculative_left_runs_at_text_starts():
-    """k > 64: a window found absent with no known mismatch (a read's first window over an error) leaves the windows
-    after it pending, and a hit on the window past them is compared from the pending windows on, against the text
-    shifted back from the anchor. Reads from the first bases of short records whose k-mers the other
-    records share put anchors near text starts (the shifted text would cross a text end: the fallback), and one to
-    three errors in the first 90 bases give absent windows after absent windows (pending windows deferred first)
-    and pending windows at the end of a read."""
+def test_errors_in_first_windows_near_text_starts():
+    """k > 64, reads with one to three errors in their first 90 bases: absent windows with no known mismatch (every
+    window after them deferred), absent windows after absent windows, and deferred windows at the end of a read;
+    reads from the first bases of short records whose k-mers the other records share put anchors near text starts
+    (runs that must stop at a text end). Round 3 tried speculative left runs on exactly these reads (DESIGN.md §4e,
+    commit dee1ce1); the test stays as a guard of the deferral paths."""
     ref = synth.make_reference(6, 3, 400)
     idx = FmIndex.build(ref.records, ref.groups, 6, prefix_q=8, pair_steps=True, triple_steps=True)
     dev = DeviceIndex(idx)
