@@ -477,6 +477,9 @@ constexpr uint32_t AX_WPB = SPEQ_AX_WPB, AX_THREADS = 64 * SPEQ_AX_WPB;
 #ifndef SPEQ_AX_BLOCKED  // idle lanes waiting for their deferred windows that trigger the deferred-window pass
 #define SPEQ_AX_BLOCKED 16
 #endif
+#ifndef SPEQ_AX_MICRO  // 1: the run's compare is not masked per dword (its first mismatch is clamped to the compared
+#define SPEQ_AX_MICRO 1   // length instead) and the deferred-list length is read only when phase 2 may run (A/B knob)
+#endif
 #ifndef SPEQ_AX_PROBE  // timing probes (wrong counts; make axvariant only): 1 staging only, 2 no deferred-window pass,
                        // 3 staging loads only (no decode), 5 as 3 without the valid-window bits, 6 / 7 as 3 without the
                        // doubling steps / the bad-bit reads
@@ -746,8 +749,10 @@ __global__ __launch_bounds__(AX_THREADS, (ax_min_waves<MODE, HW, EM, STATS>())) 
         const unsigned long long blk = __ballot(st == 2u && hasdef);
         const unsigned long long busy = ~idle;
         if (SPEQ_AX_PROBE == 2 && lane == 0) defn[0] = 0u;  // probe: deferred windows are dropped
-        const uint32_t n_def = __builtin_amdgcn_readfirstlane(defn[0]);
-        if (blk != 0 && ((uint32_t)__popcll(blk) >= SPEQ_AX_BLOCKED || busy == 0 || n_def + 256u > AX_DEF)) {
+        const bool p2 = blk != 0 && ((uint32_t)__popcll(blk) >= SPEQ_AX_BLOCKED || busy == 0 ||
+                                     __builtin_amdgcn_readfirstlane(defn[0]) + 256u > AX_DEF);
+        const uint32_t n_def = (SPEQ_AX_MICRO && !p2) ? 0u : __builtin_amdgcn_readfirstlane(defn[0]);
+        if (p2) {
             // ---- phase 2: the deferred windows of the wave. (a) the Bloom filter, AX_F windows per lane per round
             // trip; the windows it cannot rule out are compacted to the front of the list; (b) those are looked up
             // one per lane (bucket -> fingerprint -> compare with the text -> class)
@@ -1215,10 +1220,15 @@ __global__ __launch_bounds__(AX_THREADS, (ax_min_waves<MODE, HW, EM, STATS>())) 
                     const uint32_t rdw = alignbit(rw[i + 1], rw[i], rsh);
                     uint32_t x = td ^ rdw;
                     const uint32_t b0 = 16u * (uint32_t)i;
-                    const uint32_t nb = cl > b0 ? min(cl - b0, 16u) : 0u;  // bases of this dword in the compare
-                    x &= nb >= 16u ? ~0u : ((1u << (2u * nb)) - 1u);
+                    if (!SPEQ_AX_MICRO) {
+                        const uint32_t nb = cl > b0 ? min(cl - b0, 16u) : 0u;  // bases of this dword in the compare
+                        x &= nb >= 16u ? ~0u : ((1u << (2u * nb)) - 1u);
+                    }
                     e = x ? b0 + ((uint32_t)__builtin_ctz(x) >> 1) : e;
                 }
+                // (MICRO) bases past cl compare whatever lies there (zeros past the staged chunks and the loaded
+                // granules): a mismatch among them only matters as "none before cl"
+                if (SPEQ_AX_MICRO) e = min(e, cl);
                 if (verify && e < k) {  // fingerprint collision: resume probing after that slot
                     st = 0u;
                     resume = true;
