@@ -764,14 +764,21 @@ __global__ __launch_bounds__(AX_THREADS, (ax_min_waves<MODE, HW, EM, STATS>())) 
                 uint32_t ent[AX_F];
                 uint64_t hh[AX_F];
                 uint64_t fw[AX_F];
+                // in stages over the AX_F entries (entries, then their slot offsets, then their bases), so each stage's
+                // LDS reads are in flight together instead of one dependent chain per entry
+                uint32_t so[AX_F];
 #pragma unroll
                 for (uint32_t t = 0; t < AX_F; ++t) {
                     const uint32_t idx = base + 64u * t + lane;
-                    const uint16_t e16 = idx < n2 ? defl[idx] : AX_VOID;
-                    ent[t] = e16 == AX_VOID ? AX_EMPTY : (uint32_t)e16;
-                    const uint32_t o = ent[t] & 63u, jj = (ent[t] >> 6) & 1023u;
+                    const uint16_t e16 = defl[min(idx, AX_DEF - 1u)];
+                    ent[t] = (idx < n2 && e16 != AX_VOID) ? (uint32_t)e16 : AX_EMPTY;
+                }
+#pragma unroll
+                for (uint32_t t = 0; t < AX_F; ++t) so[t] = (uint32_t)off0s[ent[t] & 63u] + ((ent[t] >> 6) & 1023u);
+#pragma unroll
+                for (uint32_t t = 0; t < AX_F; ++t) {
                     uint64_t ra[HW];
-                    read_words(o, (uint32_t)off0s[o] + jj, ra);
+                    read_words(ent[t] & 63u, so[t], ra);
                     hh[t] = ax_hash<HW>(ra, k);
                 }
 #pragma unroll
