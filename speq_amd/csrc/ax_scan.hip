@@ -719,7 +719,9 @@ __global__ __launch_bounds__(AX_THREADS, (ax_min_waves<MODE, HW, EM, STATS>())) 
     // dealt round robin, profiles/r03/ax_variants_owner_group.jsonl)
     uint64_t cur = (nu * gw) / NWV;  // next unit
     const uint64_t cur_end = (nu * (gw + 1)) / NWV;
-    const uint64_t wbase = MODE == KM_LOCAL ? src.off[PAIRED ? 2 * cur : cur] : 0;  // rbase origin (local)
+    // rbase origin (local mode): the bases of the wave's share of units, from here, are addressed with 32 bits — a share
+    // of nu / (5,120 waves) units spans far less than 4 GiB unless single reads are gigabases long
+    const uint64_t wbase = MODE == KM_LOCAL ? src.off[PAIRED ? 2 * cur : cur] : 0;
     // ---- phase-1 state of the current piece
     uint32_t wend = 0;         // windows of the piece
     uint32_t off0 = 0;         // first base of the piece in the slot
