@@ -480,6 +480,12 @@ constexpr uint32_t AX_WPB = SPEQ_AX_WPB, AX_THREADS = 64 * SPEQ_AX_WPB;
 #ifndef SPEQ_AX_MICRO  // 1: the run's compare is not masked per dword (its first mismatch is clamped to the compared
 #define SPEQ_AX_MICRO 1   // length instead) and the deferred-list length is read only when phase 2 may run (A/B knob)
 #endif
+#ifndef SPEQ_AX_LAZYNV  // 1: a lane looking a window up advances to its next valid window only in lookup iterations
+#define SPEQ_AX_LAZYNV 1   // (0: at the top of every iteration, run iterations included). A/B knob
+#endif
+#ifndef SPEQ_AX_SPECRW  // 1: with LAZYNV, a lookup reads its window's code words together with the valid bits
+#define SPEQ_AX_SPECRW 1
+#endif
 #ifndef SPEQ_AX_PROBE  // timing probes (wrong counts; make axvariant only): 1 staging only, 2 no deferred-window pass,
                        // 3 staging loads only (no decode), 5 as 3 without the valid-window bits, 6 / 7 as 3 without the
                        // doubling steps / the bad-bit reads
@@ -1100,7 +1106,9 @@ __global__ __launch_bounds__(AX_THREADS, (ax_min_waves<MODE, HW, EM, STATS>())) 
         // of work per iteration, alternating (a lookup is followed by a run and a run by a lookup, so a lane rarely
         // waits): the wave executes the lookup code or the run code, not both under exec masks (the kernel is bound
         // by VALU issue, profiles/r03), and a kind no lane needs is skipped.
-        if (st == 0u) {
+        // (LAZYNV) the next valid window of a lane waiting to look one up is found in the lookup iteration itself, so
+        // a run iteration does not wait for those lanes' LDS reads; such a lane may count as busy one iteration longer
+        if (!SPEQ_AX_LAZYNV && st == 0u) {
             j = next_valid(lane, j, wend);
             if (j >= wend) st = 2u;
         }
@@ -1115,6 +1123,18 @@ __global__ __launch_bounds__(AX_THREADS, (ax_min_waves<MODE, HW, EM, STATS>())) 
         }
         const bool want_lk = __ballot(st == 0u) != 0, want_rn = __ballot(st == 1u) != 0;
         run_phase = run_phase ? !want_lk : want_rn;
+        // (LAZYNV) lookup iterations: the window's code words are read together with its valid bits (the same
+        // window unless it is not valid, then read again), one LDS round trip before the bucket load instead of two
+        // (single-end k <= 32 only: elsewhere the words held across the valid-bit search spill)
+        constexpr bool SPEC_RW = SPEQ_AX_SPECRW && HW == 1 && !PAIRED;
+        uint64_t ra[HW];
+        if (SPEQ_AX_LAZYNV && !run_phase && st == 0u) {
+            const uint32_t j0 = j;
+            if (SPEC_RW) read_words(lane, off0 + j0, ra);
+            j = next_valid(lane, j0, wend);
+            if (j >= wend) st = 2u;
+            else if (SPEC_RW && j != j0) read_words(lane, off0 + j, ra);
+        }
         const bool lk = st == 0u && !run_phase, rn = st == 1u && run_phase;
         if (STATS) {
             s_iter += lane == 0 ? 1u : 0u;
@@ -1125,8 +1145,7 @@ __global__ __launch_bounds__(AX_THREADS, (ax_min_waves<MODE, HW, EM, STATS>())) 
         }
         if (!run_phase) {
             // ---- lookup: hash window j -> bucket (8 slots {pos, fp | group}); resolve
-            uint64_t ra[HW];
-            read_words(lane, off0 + j, ra);
+            if (!SPEQ_AX_LAZYNV || !SPEC_RW) read_words(lane, off0 + j, ra);
             const uint64_t h = ax_hash<HW>(ra, k);
             const uint32_t fp = ax_fp(h);
             if (lk && !resume) {
