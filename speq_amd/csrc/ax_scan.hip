@@ -486,6 +486,9 @@ constexpr uint32_t AX_WPB = SPEQ_AX_WPB, AX_THREADS = 64 * SPEQ_AX_WPB;
 #ifndef SPEQ_AX_SPECRW  // 1: with LAZYNV, a lookup reads its window's code words together with the valid bits
 #define SPEQ_AX_SPECRW 1
 #endif
+#ifndef SPEQ_AX_REFILL_SYNC  // 1: the refill ends with wave-level LDS fences after the valid-window bits (A/B knob;
+#define SPEQ_AX_REFILL_SYNC 0   // 0: none — every lane writes and then reads only its own column of them)
+#endif
 #ifndef SPEQ_AX_PROBE  // timing probes (wrong counts; make axvariant only): 1 staging only, 2 no deferred-window pass,
                        // 3 staging loads only (no decode), 5 as 3 without the valid-window bits, 6 / 7 as 3 without the
                        // doubling steps / the bad-bit reads
@@ -1075,7 +1078,7 @@ __global__ __launch_bounds__(AX_THREADS, (ax_min_waves<MODE, HW, EM, STATS>())) 
                 }
                 // valid-window bits of the piece (window j at bit j): the good-window dwords from slot position
                 // off0 (< 16, so dword d + {0, 1}), none past wend
-                wave_sync();  // (own column only; keeps the bad-bit reads before the overwrite below)
+                if (SPEQ_AX_REFILL_SYNC) wave_sync();  // (own column: the lane's reads precede its writes anyway)
                 {
                     uint32_t* vw32 = reinterpret_cast<uint32_t*>(vw);
 #pragma unroll
@@ -1092,10 +1095,12 @@ __global__ __launch_bounds__(AX_THREADS, (ax_min_waves<MODE, HW, EM, STATS>())) 
                 verify = false;
                 resume = false;
                 last_mm = -1;
-            } else {
+            } else if (SPEQ_AX_REFILL_SYNC) {
                 wave_sync();
             }
-            wave_sync();
+            // the slots' code words were fenced after the decode (phase 2 reads other lanes' slots); the valid-window
+            // bits are read by their own lane only
+            if (SPEQ_AX_REFILL_SYNC) wave_sync();
             continue;  // re-evaluate (lanes whose piece has no window are idle again)
         }
         if (busy == 0) continue;  // blocked lanes only: phase 2 runs next time round
