@@ -4,27 +4,33 @@
 One "step" = one pass of the hot path (exact search of every k-mer window + unique-to-one-group tally) over this
 rank's batch of synthetic 150-bp reads already resident in HBM, followed by the RCCL all-reduce of the G+2
 counters (N > 1). Default workload = BASELINE config 2 (10 variants x 50 kb, 1M reads per GPU, k = 21, global
-mode) -> `value`. The same run also measures, as secondary lines in the same JSON object:
+mode) -> `value`. The same run also measures secondary lines (compact objects under "lines" in the JSON):
   * "local_mode": config 2 in the reference's default Phred-weighted mode (fixed_accuracy 0, arg_parse.h:23);
   * "k31": BASELINE config 3 (50 variants x 3 isolates, k = 31) at its full 10 M reads per GPU — at N = 8 the
     per-rank shard of config 4 (100 M reads over 8 GPUs, 12.5 M each);
+  * "cli_e2e" (N = 1): `bin/speq index` + `bin/speq scan` processes on config 3's 10 M reads written as FASTQ
+    (reference defaults but k = 31: Phred-weighted, .dat pass, EM loop; src/main.cpp:25-31 -> fm_scanner.cpp:309-545);
   * "k70_reference_defaults": config 2's reads at the reference CLI's defaults (k = 70, Phred-weighted);
+  * "k70_err05": the same at 0.5 % sequencing errors (the upper end of Illumina error rates);
   * "local_varq" (N = 1): config 2, Phred-weighted, with Illumina-like per-base qualities (synth "variable");
   * "cfg5_paired" / "cfg5_paired_local": BASELINE config 5's index (200 variants x 5 isolates), paired 2 x 150 bp,
     k = 31, on a per-GPU sample of the config's pairs (--cfg5-pairs);
-  * "fastq_e2e" (N = 1): the drop-in input path, speq_scan_fastq on config 2's reads written as a FASTQ file on
-    local disk (file bytes/s and k-mers/s, page cache warm).
+  * "fastq_e2e" (N = 1): speq_scan_fastq on config 2's reads written as a FASTQ file (page cache warm).
 Weak scaling: every rank scans its own shard of the deterministic read stream.
 
+stdout: ONE compact JSON line on rank 0 (< 8 KB; `compact_result`); the full per-line detail (work counters, U
+vectors, paths) goes to --detail (default profiles/r04/bench_detail_n<N>.json).
 Launch: python bench.py [--gpus 1 --steps K --warmup W]; for N > 1 the driver uses torch.distributed.run.
-Prints ONE JSON line on rank 0.
 """
 from __future__ import annotations
 
 import argparse
+import hashlib
 import json
 import os
+import subprocess
 import sys
+import tempfile
 import time
 
 import numpy as np
@@ -34,9 +40,10 @@ sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-level parameters)
 OCC_ENTRY_BYTES = 64   # algorithmic bytes per k-mer = k LF steps x 2 occ loads x 64 B
+LINE_LIMIT = 8000      # bytes of the stdout line (the driver parsed 9.3 KB in round 2, not 22.8 KB in round 3)
 
 
-def parse_args():
+def parse_args(argv=None):
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=20)
@@ -44,6 +51,7 @@ def parse_args():
     p.add_argument("--config", type=int, default=2, help="BASELINE.json config number (1-5) of the headline")
     p.add_argument("--reads", type=int, default=0, help="override reads per GPU")
     p.add_argument("--k", type=int, default=0, help="override k")
+    p.add_argument("--err", type=float, default=0.001, help="substitution error rate of the headline reads")
     p.add_argument("--prefix-q", type=int, default=12)
     p.add_argument("--pair-steps", type=int, default=1)
     p.add_argument("--label-table", default="auto", help="auto|0|1 (auto: only for >= 4 M-symbol indexes)")
@@ -58,14 +66,16 @@ def parse_args():
                    help="extra launch tuning key=value (speq_device_set_tuning), e.g. ilp_kt=2; repeatable")
     p.add_argument("--no-lf-compare", action="store_true",
                    help="skip timing the LF-step kernel beside the table kernel")
-    p.add_argument("--no-extra", action="store_true", help="skip the local-mode and k=31 secondary lines")
+    p.add_argument("--no-extra", action="store_true", help="skip the secondary lines")
+    p.add_argument("--only", default="", help="comma-separated secondary lines to run (default: all)")
     p.add_argument("--k31-reads", type=int, default=0, help="reads per GPU of the k=31 line (0 = config 3/4)")
     p.add_argument("--cfg5-pairs", type=int, default=4_000_000, help="pairs per GPU of the config-5 lines (0: skip)")
-    p.add_argument("--no-fastq", action="store_true", help="skip the FASTQ end-to-end line")
-    p.add_argument("--cpu-seconds", type=float, default=15.0, help="target CPU-baseline sample duration")
+    p.add_argument("--no-fastq", action="store_true", help="skip the FASTQ end-to-end lines (fastq_e2e, cli_e2e)")
+    p.add_argument("--cpu-seconds", type=float, default=15.0, help="target CPU-baseline sample duration (headline)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-pcie", action="store_true", help="skip the PCIe-inclusive host-buffer measurement")
-    return p.parse_args()
+    p.add_argument("--detail", default="", help="full-detail JSON path (default profiles/r04/bench_detail_n<N>.json)")
+    return p.parse_args(argv)
 
 
 def host_cpu_info() -> dict:
@@ -130,8 +140,8 @@ class Ctx:
 
 
 def ax_request_bytes(st: dict, k: int, n_reads: int, local: bool) -> dict:
-    """Bytes k_scan_ax REQUESTS per launch, from the work counters of its instrumented twin (speq_scan_reads_device_stats,
-    same scan, same results): every load the kernel issues, by kind, at the size it issues it (ax_scan.hip):
+    """Bytes k_scan_ax REQUESTS per launch (L1/L2 requests, not fabric bytes), from the work counters of its
+    instrumented twin (speq_scan_reads_device_stats, same scan, same results), by kind at the size it issues it:
       read offsets 8 B per read; staging 16 B of bases + 16 B of qualities per 16-base chunk;
       anchor buckets 64 B per lookup (phase 1 and phase 2); run granules 16 B each (counted);
       Bloom-filter words 8 B per deferred window; candidate granules ceil(k/32) + 1 x 16 B per phase-2 verification;
@@ -149,52 +159,72 @@ def ax_request_bytes(st: dict, k: int, n_reads: int, local: bool) -> dict:
     return {"total": sum(parts.values()), "parts": parts}
 
 
-def kernel_model(dev, k: int, table_on: bool, kmers: int, read_bytes: int, n_reads: int = 0) -> dict:
-    """The timed kernel and the bytes IT must move per k-mer window (its own roofline model), for the kernels whose
-    loads are a fixed function of the workload. k_scan_ax's are counted instead (ax_request_bytes).
-
-    Table path (k_scan_kt): one 64-B table bucket per window + the read bytes (bases + qualities).
-    LF-step path (k_scan): SURVEY.md 8(d)'s 2*k*64 B per window (k LF steps x 2 occ loads)."""
-    rb = 2.0 * read_bytes / max(1, kmers)
-    if dev.tuning("last_kernel") == 3:
-        return {"kernel": "k_scan_ax (anchor-and-extend scan, speq_amd/csrc/ax_scan.hip)", "bytes_per_kmer": None,
-                "model": "bytes the kernel requests, counted by its instrumented twin (ax_request_bytes)"}
-    if table_on:
-        return {"kernel": "k_scan_kt (pipelined k-mer-table scan, speq_amd/csrc/scan_kernels.hip)",
-                "bytes_per_kmer": 64.0 + rb,
-                "model": "one 64-B table bucket per window + the read's bases and qualities"}
-    return {"kernel": "k_scan<..., KT = false> (LF-step scan, speq_amd/csrc/scan_kernels.hip)",
-            "bytes_per_kmer": float(2 * k * OCC_ENTRY_BYTES),
-            "model": "SURVEY.md 8(d): k LF steps x 2 occ-block loads x 64 B"}
+def workload_key(cfg: int, k: int, mode: str, n_reads: int, kernel: str, qual_profile: str = "q40",
+                 err: float = 0.001) -> str:
+    """profiles/traffic.json key of one workload + kernel (scripts/summarize_profile.py --traffic-key)."""
+    return (f"cfg{cfg}_k{k}_{mode}_reads{n_reads}_{kernel}" + ("" if qual_profile == "q40" else f"_{qual_profile}")
+            + ("" if abs(err - 0.001) < 1e-12 else f"_err{err:g}"))
 
 
-def traffic_lookup(cfg: int, k: int, mode: str, n_reads: int, kernel: str, qual_profile: str = "q40") -> dict | None:
-    """Measured fabric bytes per launch of this exact workload and kernel (rocprofv3 PMC passes summarised into
-    profiles/traffic.json by scripts/summarize_profile.py --traffic-key), or None."""
+def traffic_lookup(key: str) -> dict | None:
+    """Measured FABRIC bytes per launch of this exact workload and kernel, or None. Only round-4 entries count: they
+    carry `fabric_bytes_per_launch`, computed from the L2's memory-side request counters with the request sizes
+    calibrated on gfx950 (scripts/calibrate_counters.sh); earlier entries were raw FETCH_SIZE."""
     prof = os.path.join(ROOT, "profiles", "traffic.json")
-    if not os.path.exists(prof):
-        return None
     try:
         tj = json.load(open(prof))
-    except ValueError:
+    except (OSError, ValueError):
         return None
-    key = f"cfg{cfg}_k{k}_{mode}_reads{n_reads}_{kernel}" + ("" if qual_profile == "q40" else f"_{qual_profile}")
-    if key not in tj:
+    e = tj.get(key)
+    if not e or "fabric_bytes_per_launch" not in e:
         return None
-    e = dict(tj[key])
+    e = dict(e)
     e["source"] = os.path.normpath(os.path.join("profiles", e["source"]))
     return e
 
 
+def roofline_of(key: str, avg_kernel_s: float, request_bytes: float | None, compulsory_bytes: float, k: int,
+                kmers: int) -> dict:
+    """The roofline object of one line. frac = fabric bytes per launch (PMC, calibrated; profiles/traffic.json) ÷ the
+    launch's mean duration (HIP events, this run) ÷ 8 TB/s. Beside it: l2_request_frac (bytes the kernel requests,
+    mostly L2 hits), compulsory_frac (the read stream that must cross the fabric once: bases + qualities + offsets)
+    and survey_model_frac (SURVEY §8(d)'s 2·k·64 B per k-mer: k uncached LF steps, not what this kernel does)."""
+    tr = traffic_lookup(key)
+    t = max(avg_kernel_s, 1e-12)
+    gbs = lambda b: b / t / 1e9  # noqa: E731
+    if tr:
+        traffic, basis, source = tr["fabric_bytes_per_launch"], "fabric", tr["source"]
+    else:
+        traffic, basis, source = None, "compulsory", "no PMC profile of this workload: compulsory read bytes"
+    achieved = gbs(traffic if traffic is not None else compulsory_bytes)
+    return {
+        "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
+        "traffic": traffic, "traffic_frac": (gbs(traffic) / HBM_PEAK_GBS) if traffic is not None else None,
+        "frac_basis": basis, "traffic_source": source, "avg_kernel_ms": t * 1e3,
+        "traffic_rocprof_kernel_ms": (tr.get("kernel_steady_state_ns_rocprof") or 0) / 1e6 if tr else None,
+        "l2_hit_rate": tr.get("l2_hit_rate") if tr else None,
+        "l2_request_frac": (gbs(request_bytes) / HBM_PEAK_GBS) if request_bytes else None,
+        "compulsory_frac": gbs(compulsory_bytes) / HBM_PEAK_GBS,
+        "survey_model_frac": gbs(kmers * 2 * k * OCC_ENTRY_BYTES) / HBM_PEAK_GBS,
+        "kernel": None,
+    }
+
+
 KERNEL_TAG = {0: "lf", 1: "kt", 2: "kt", 3: "ax"}  # speq_device_get_tuning("last_kernel")
+KERNEL_NAME = {0: "k_scan<KT=false> (LF steps)", 1: "k_scan<KT> (k-mer table)", 2: "k_scan_kt (k-mer table)",
+               3: "k_scan_ax (anchor-and-extend)"}
+
+
+def u_sha1(u) -> str:
+    return hashlib.sha1(np.asarray(u, dtype=np.int64).tobytes()).hexdigest()[:16]
 
 
 def run_workload(ctx: Ctx, cfg_no: int, k: int, n_reads: int, mode: str, steps: int, warmup: int,
                  with_lf: bool, with_pcie: bool, with_cpu: bool, cpu_seconds: float, prepared=None,
-                 qual_profile: str = "q40") -> dict:
+                 qual_profile: str = "q40", err: float = 0.001, cpu_extra_ports: bool = False) -> dict:
     """Builds the index of BASELINE config `cfg_no` (or reuses `prepared`), stages this rank's reads in HBM, times
-    `steps` scans and returns the measurement (plus the objects for reuse). qual_profile: synth.QUALITY_PROFILES
-    (the reads of `prepared` are regenerated with it when they differ)."""
+    `steps` scans and returns the measurement (plus the objects for reuse). qual_profile: synth.QUALITY_PROFILES;
+    err: substitution rate (the reads of `prepared` are regenerated when either differs)."""
     torch, a = ctx.torch, ctx.a
     from speq_amd import DeviceIndex, FmIndex, synth
 
@@ -215,11 +245,14 @@ def run_workload(ctx: Ctx, cfg_no: int, k: int, n_reads: int, mode: str, steps: 
         for kv in a.tune:
             key, val = kv.split("=")
             dev.tune(**{key: int(val)})
-        prepared = dict(ref=ref, idx=idx, dev=dev, build_s=build_s, qual_profile=None)
-    if prepared.get("qual_profile") != qual_profile:
-        reads = synth.make_reads(prepared["ref"], n_reads, start_index=ctx.rank * n_reads, paired=paired)
+        prepared = dict(ref=ref, idx=idx, dev=dev, build_s=build_s, reads_key=None, cfg=cfg_no)
+    if prepared.get("reads_key") != (qual_profile, err, n_reads):
+        prepared.update(d_seq=None, d_qual=None, d_off=None)
+        reads = synth.make_reads(prepared["ref"], n_reads, start_index=ctx.rank * n_reads, paired=paired,
+                                 err_rate=err)
         reads = synth.apply_quality_profile(reads, qual_profile)
-        prepared.update(reads=reads, qual_profile=qual_profile, d_seq=torch.from_numpy(reads.seq).to(ctx.dev_t),
+        prepared.update(reads=reads, reads_key=(qual_profile, err, n_reads),
+                        d_seq=torch.from_numpy(reads.seq).to(ctx.dev_t),
                         d_qual=torch.from_numpy(reads.qual).to(ctx.dev_t),
                         d_off=torch.from_numpy(reads.offsets.astype(np.int64)).to(ctx.dev_t))
     ref, idx, dev, reads = prepared["ref"], prepared["idx"], prepared["dev"], prepared["reads"]
@@ -267,11 +300,9 @@ def run_workload(ctx: Ctx, cfg_no: int, k: int, n_reads: int, mode: str, steps: 
     weights = d_w.cpu().numpy() if local else None
     table_on = bool(ktab["table_bytes"])
     hot_kernel = dev.tuning("last_kernel")
-    km = kernel_model(dev, k, table_on, kmers_per_step, read_bytes, reads.n)
 
-    lf = None
-    prev = None
-    if with_lf and a.kmer_table and table_on and dev.tuning("last_kernel") == 3:
+    lf = prev = None
+    if with_lf and a.kmer_table and table_on and hot_kernel == 3:
         # the previous hot path (k-mer-table kernel for k <= 31, else LF steps) on the same reads
         dev.tune(ax_scan=0)
         pv_el, pv_ms, pv_n = timed_run(steps, 1)
@@ -281,9 +312,7 @@ def run_workload(ctx: Ctx, cfg_no: int, k: int, n_reads: int, mode: str, steps: 
         if not np.array_equal(pv_counts, counts):
             raise RuntimeError("k-mer-table scan disagrees with the anchor-and-extend scan")
         prev = {"value": kmers_per_step * ctx.world * steps / pv_el, "unit": "k-mers/s",
-                "avg_kernel_ms": pv_ms / max(1, pv_n),
-                "path": {0: "k_scan (LF steps)", 1: "k_scan<KT> (k-mer table)",
-                         2: "k_scan_kt (pipelined k-mer-table scan, round-1 hot path)"}.get(kind, str(kind))}
+                "avg_kernel_ms": pv_ms / max(1, pv_n), "path": KERNEL_NAME.get(kind, str(kind))}
     if with_lf and a.kmer_table and table_on:
         dev.tune(kmer_table=0, ax_scan=0)
         lf_el, lf_ms, lf_n = timed_run(steps, 1)
@@ -293,13 +322,12 @@ def run_workload(ctx: Ctx, cfg_no: int, k: int, n_reads: int, mode: str, steps: 
             raise RuntimeError("LF-step scan disagrees with the hot path")
         lf = {"value": kmers_per_step * ctx.world * steps / lf_el, "unit": "k-mers/s",
               "avg_kernel_ms": lf_ms / max(1, lf_n),
-              "achieved_GBps": kmers_per_step * 2 * k * OCC_ENTRY_BYTES / (lf_ms / 1e3 / max(1, lf_n)) / 1e9,
               "path": "k_scan<..., KT = false>: q-mer table + three-base LF steps + label-run classification"}
 
     total_kmers = kmers_per_step * ctx.world * steps
     value = total_kmers / elapsed
     avg_kernel_s = (kernel_ms / 1e3) / max(1, launches)
-    ax_stats = None
+    ax_stats = req = None
     if hot_kernel == 3 and not os.environ.get("SPEQ_BENCH_NO_STATS"):
         # one untimed launch of the instrumented twin: the same scan (checked equal), plus its work counters
         d_counts.zero_()
@@ -310,42 +338,11 @@ def run_workload(ctx: Ctx, cfg_no: int, k: int, n_reads: int, mode: str, steps: 
         if not np.array_equal(d_counts.cpu().numpy(), counts):
             raise RuntimeError("instrumented anchor-and-extend scan disagrees with the timed scan")
         req = ax_request_bytes(ax_stats, k, reads.n, local)
-        own_bytes = req["total"]
-        km["bytes_per_kmer"] = own_bytes / kmers_per_step
-        km["bytes_parts"] = {key: round(v / kmers_per_step, 4) for key, v in req["parts"].items()}
-    elif km["bytes_per_kmer"] is not None:
-        own_bytes = kmers_per_step * km["bytes_per_kmer"]
-    else:  # SPEQ_BENCH_NO_STATS (profiling passes: no instrumented launch among the profiled kernels)
-        own_bytes = 0.0
-        km["bytes_per_kmer"] = 0.0
-    own_gbs = own_bytes / avg_kernel_s / 1e9
-    survey_gbs = kmers_per_step * 2 * k * OCC_ENTRY_BYTES / avg_kernel_s / 1e9
-    tr = traffic_lookup(cfg_no, k, mode, n_reads, KERNEL_TAG.get(hot_kernel, "lf"), qual_profile)
-    traffic = tr["hbm_bytes_per_launch"] if tr else None
-    roofline = {
-        "bound": "hbm", "achieved": own_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": own_gbs / HBM_PEAK_GBS,
-        "traffic": traffic,
-        "kernel": km["kernel"], "bytes_per_kmer": round(km["bytes_per_kmer"], 3), "bytes_model": km["model"],
-        "bytes_per_kmer_by_kind": km.get("bytes_parts"), "own_bytes_per_launch": own_bytes,
-        "avg_kernel_ms": avg_kernel_s * 1e3, "launches_timed": launches,
-        # measured L2->fabric bytes per launch (rocprofv3 PMC, profiles/): what the kernel really draws from
-        # Infinity Cache + HBM, over this run's launch time, against the same 8 TB/s; split into reads, writes and
-        # the register-spill writes (Scratch_Size x lanes) inside them
-        "traffic_fetch": tr.get("fetch_bytes_per_launch") if tr else None,
-        "traffic_write": tr.get("write_bytes_per_launch") if tr else None,
-        "traffic_scratch_write": tr.get("scratch_write_bytes_per_launch") if tr else None,
-        "traffic_GBps": (traffic / avg_kernel_s / 1e9) if traffic else None,
-        "traffic_frac": (traffic / avg_kernel_s / 1e9 / HBM_PEAK_GBS) if traffic else None,
-        "useful_traffic_frac": ((traffic - (tr.get("scratch_write_bytes_per_launch") or 0.0)) / avg_kernel_s / 1e9
-                                / HBM_PEAK_GBS) if traffic else None,
-        "traffic_source": tr["source"] if tr else None,
-        "traffic_rocprof_kernel_ns": tr.get("kernel_steady_state_ns_rocprof") if tr else None,
-        # SURVEY.md 8(d)'s fixed model (2*k*64 B per k-mer: k uncached LF steps) — not what this kernel moves
-        "survey_model_bytes_per_kmer": 2 * k * OCC_ENTRY_BYTES,
-        "survey_model_frac": survey_gbs / HBM_PEAK_GBS,
-    }
-    if ax_stats is not None:
-        roofline["ax_work"] = ax_stats
+    compulsory = 2.0 * read_bytes + 8.0 * (reads.n + 1)  # bases + qualities + read offsets
+    key = workload_key(cfg_no, k, mode, n_reads, KERNEL_TAG.get(hot_kernel, "lf"), qual_profile, err)
+    roofline = roofline_of(key, avg_kernel_s, req["total"] if req else None, compulsory, k, kmers_per_step)
+    roofline["kernel"] = KERNEL_NAME.get(hot_kernel, str(hot_kernel))
+    roofline["launches_timed"] = launches
 
     pcie = None
     if with_pcie:
@@ -365,23 +362,80 @@ def run_workload(ctx: Ctx, cfg_no: int, k: int, n_reads: int, mode: str, steps: 
 
     cpu = None
     if with_cpu and ctx.rank == 0 and ctx.world == 1:
-        cpu = cpu_baseline(ref, reads, k, G, cpu_seconds, local, paired, idx)
+        cpu = cpu_baseline(prepared, reads, k, G, cpu_seconds, local, paired, extra_ports=cpu_extra_ports)
 
+    check = {"T": int(counts[0]), "ambiguous": int(counts[1]), "U_sha1": u_sha1(counts[2:]),
+             **({"W_sum": float(weights.sum())} if weights is not None else {})}
     out = {
-        "value": value, "ms_per_step": elapsed / steps * 1e3, "k": k, "mode": mode,
+        "value": value, "ms_per_step": elapsed / steps * 1e3, "avg_kernel_ms": avg_kernel_s * 1e3, "k": k,
+        "mode": mode,
         "workload": f"BASELINE config {cfg_no}: {c['n_variants']} variants x {c['n_isolates']} isolates x "
                     f"{c['length']} bp, {n_reads} x 150 bp {'pairs' if paired else 'reads'} per GPU, k={k}, {mode}"
-                    + (f", qualities '{qual_profile}' ({synth.QUALITY_PROFILES[qual_profile]})"
-                       if qual_profile != "q40" else ""),
+                    + (f", qualities '{qual_profile}'" if qual_profile != "q40" else "")
+                    + (f", {err * 100:g} % substitutions" if abs(err - 0.001) > 1e-12 else ""),
         "reads_per_gpu": n_reads, "kmers_per_step_per_gpu": kmers_per_step, "paired": paired,
         "index_build_s": round(prepared["build_s"], 3), "fm_text_len": int(idx.info().n),
         "kmer_table": {"on": table_on, "distinct_kmers": ktab["distinct_kmers"], "bytes": ktab["table_bytes"],
                        "build_s": round(ktab["build_ms"] / 1e3, 4)},
-        "roofline": roofline, "cpu_baseline": cpu, "lf_steps": lf, "kmer_table_kernel": prev, "pcie_inclusive": pcie,
-        "check": {"T": int(counts[0]), "ambiguous": int(counts[1]), "U": [int(x) for x in counts[2:]],
-                  **({"W_sum": float(weights.sum())} if weights is not None else {})},
+        "roofline": roofline, "traffic_key": key, "cpu_baseline": cpu, "lf_steps": lf, "kmer_table_kernel": prev,
+        "pcie_inclusive": pcie, "check": check,
+        "detail": {"U": [int(x) for x in counts[2:]], "W": weights.tolist() if weights is not None else None,
+                   "ax_work": ax_stats, "request_bytes_by_kind": req["parts"] if req else None},
     }
     return out, prepared
+
+
+def compact_cpu(cpu: dict | None) -> dict | None:
+    if not cpu:
+        return None
+    return {k: cpu[k] for k in ("value", "unit", "cores", "kind", "sample", "checked") if k in cpu}
+
+
+def compact_line(r: dict) -> dict:
+    """One secondary line in the stdout JSON: rate, times, roofline fractions and the result check (no vectors)."""
+    rf = r.get("roofline") or {}
+    out = {"value": r["value"]}
+    for key in ("ms_per_step", "avg_kernel_ms", "seconds", "unit"):
+        if key in r:
+            out[key] = r[key]
+    if rf:
+        out.update(frac=rf.get("frac"), traffic_frac=rf.get("traffic_frac"), l2_request_frac=rf.get("l2_request_frac"),
+                   frac_basis=rf.get("frac_basis"))
+    if "check" in r:
+        out["check"] = {k: v for k, v in r["check"].items() if k != "U"}
+    if r.get("cpu_baseline"):
+        out["cpu_baseline"] = {k: r["cpu_baseline"][k] for k in ("value", "cores", "kind", "checked")
+                               if k in r["cpu_baseline"]}
+    return out
+
+
+def compact_result(head: dict, lines: dict, meta: dict) -> dict:
+    """The ONE stdout JSON line (BASELINE keys + roofline + cpu_baseline + compact secondary lines), < LINE_LIMIT
+    bytes; everything else goes to the detail file."""
+    rf = dict(head["roofline"])
+    roof = {k: rf.get(k) for k in ("bound", "achieved", "peak", "unit", "frac", "traffic", "traffic_frac",
+                                   "frac_basis", "avg_kernel_ms", "traffic_source", "traffic_rocprof_kernel_ms",
+                                   "l2_hit_rate", "l2_request_frac", "compulsory_frac", "survey_model_frac",
+                                   "kernel")}
+    out = {
+        "metric": meta["metric"], "value": head["value"], "unit": "k-mers/s", "n_gpus": meta["n_gpus"],
+        "steps": meta["steps"], "warmup": meta["warmup"], "ms_per_step": head["ms_per_step"],
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u32",
+        "data": "synthetic (splitmix64 references/reads, SURVEY.md §8(d))",
+        "config": meta["config"],
+        "roofline": roof,
+        "cpu_baseline": compact_cpu(head.get("cpu_baseline")),
+        "check": head["check"],
+        "lines": {name: compact_line(r) for name, r in lines.items() if r},
+        "detail_file": meta.get("detail_file"),
+    }
+    s = json.dumps(out)
+    if len(s) > LINE_LIMIT:  # never let the line outgrow what the driver parses: drop the optional fields first
+        for r in out["lines"].values():
+            for key in ("l2_request_frac", "frac_basis", "unit"):
+                r.pop(key, None)
+        out["config"].pop("kmer_table", None)
+    return out
 
 
 def main():
@@ -394,78 +448,85 @@ def main():
     n_reads = a.reads or (c["n_reads"] if a.config <= 3 else c["n_reads"] // 8)
     head, prep = run_workload(ctx, a.config, k, n_reads, a.mode, a.steps, a.warmup, with_lf=not a.no_lf_compare,
                               with_pcie=not a.no_pcie, with_cpu=not a.no_cpu_baseline, cpu_seconds=a.cpu_seconds,
-                              qual_profile=a.qual)
+                              qual_profile=a.qual, err=a.err, cpu_extra_ports=True)
     dev = prep["dev"]
-    extra = {}
-    if not a.no_extra and a.config == 2 and not a.k and not a.reads and a.qual == "q40":
+    lines = {}
+    only = set(x for x in a.only.split(",") if x)
+    want = lambda name: not only or name in only  # noqa: E731
+    cpu_on = not a.no_cpu_baseline
+    short_cpu = max(4.0, a.cpu_seconds / 2)
+    if not a.no_extra and a.config == 2 and not a.k and not a.reads and a.qual == "q40" and a.err == 0.001:
         other = "local" if a.mode == "global" else "global"
-        extra[f"{other}_mode"], _ = run_workload(ctx, 2, k, n_reads, other, a.steps, a.warmup, with_lf=False,
-                                                 with_pcie=False, with_cpu=False, cpu_seconds=0, prepared=prep)
-        n31 = a.k31_reads or (10_000_000 if ctx.world == 1 else synth.CONFIGS[4]["n_reads"] // 8)
-        extra["k31"], p31 = run_workload(ctx, 3, 31, n31, "global", max(3, a.steps // 4), max(1, a.warmup // 2),
-                                         with_lf=False, with_pcie=False, with_cpu=not a.no_cpu_baseline,
-                                         cpu_seconds=a.cpu_seconds)
-        extra["k31"]["note"] = ("config 3 (10 M reads on one GPU); with 8 ranks each scans config 4's 12.5 M-read "
-                                "shard of the same index")
-        p31["dev"].close()
+        if want(f"{other}_mode"):
+            lines[f"{other}_mode"], _ = run_workload(ctx, 2, k, n_reads, other, a.steps, a.warmup, with_lf=False,
+                                                     with_pcie=False, with_cpu=False, cpu_seconds=0, prepared=prep)
+        if want("k31") or want("cli_e2e"):
+            n31 = a.k31_reads or (10_000_000 if ctx.world == 1 else synth.CONFIGS[4]["n_reads"] // 8)
+            lines["k31"], p31 = run_workload(ctx, 3, 31, n31, "global", max(3, a.steps // 4), max(1, a.warmup // 2),
+                                             with_lf=False, with_pcie=False, with_cpu=cpu_on, cpu_seconds=short_cpu)
+            lines["k31"]["note"] = ("config 3 (10 M reads on one GPU); with 8 ranks each scans config 4's 12.5 M-read "
+                                    "shard of the same index")
+            if ctx.world == 1 and not a.no_fastq and want("cli_e2e"):
+                lines["cli_e2e"] = cli_e2e(p31, 31, lines["k31"]["check"])
+            p31["dev"].close()
+            del p31
         # the reference CLI's defaults: k = 70 (include/arg_parse.h:21), Phred-weighted local mode (:23)
-        extra["k70_reference_defaults"], _ = run_workload(ctx, 2, 70, n_reads, "local", a.steps, a.warmup,
-                                                          with_lf=False, with_pcie=False, with_cpu=False,
-                                                          cpu_seconds=0, prepared=prep)
+        if want("k70_reference_defaults"):
+            lines["k70_reference_defaults"], _ = run_workload(ctx, 2, 70, n_reads, "local", a.steps, a.warmup,
+                                                              with_lf=False, with_pcie=False, with_cpu=cpu_on,
+                                                              cpu_seconds=short_cpu, prepared=prep)
+        if want("k70_err05"):
+            lines["k70_err05"], _ = run_workload(ctx, 2, 70, n_reads, "local", a.steps, a.warmup, with_lf=False,
+                                                 with_pcie=False, with_cpu=False, cpu_seconds=0, prepared=prep,
+                                                 err=0.005)
         if ctx.world == 1:
-            if not a.no_fastq:  # the drop-in input path before the reads are re-generated below
-                extra["fastq_e2e"] = fastq_e2e(ctx, prep, k)
+            if not a.no_fastq and want("fastq_e2e"):
+                lines["fastq_e2e"] = fastq_e2e(ctx, prep, k)
             # the reference's default (Phred-weighted) mode on reads whose qualities vary base by base
-            extra["local_varq"], _ = run_workload(ctx, 2, k, n_reads, "local", a.steps, a.warmup, with_lf=False,
-                                                  with_pcie=False, with_cpu=False, cpu_seconds=0, prepared=prep,
-                                                  qual_profile="variable")
-        if a.cfg5_pairs:
+            if want("local_varq"):
+                lines["local_varq"], _ = run_workload(ctx, 2, k, n_reads, "local", a.steps, a.warmup, with_lf=False,
+                                                      with_pcie=False, with_cpu=False, cpu_seconds=0, prepared=prep,
+                                                      qual_profile="variable")
+        if a.cfg5_pairs and (want("cfg5_paired") or want("cfg5_paired_local")):
             # BASELINE config 5 (the north_star's scaling config): paired, k = 31, on a per-GPU sample of its pairs
-            extra["cfg5_paired"], p5 = run_workload(ctx, 5, 31, a.cfg5_pairs, "global", max(3, a.steps // 4),
+            lines["cfg5_paired"], p5 = run_workload(ctx, 5, 31, a.cfg5_pairs, "global", max(3, a.steps // 4),
                                                     max(1, a.warmup // 2), with_lf=False, with_pcie=False,
-                                                    with_cpu=False, cpu_seconds=0)
-            extra["cfg5_paired"]["note"] = (f"config 5 lists 500 M pairs (a node's job); each GPU scans a "
+                                                    with_cpu=cpu_on, cpu_seconds=short_cpu)
+            lines["cfg5_paired"]["note"] = (f"config 5 lists 500 M pairs (a node's job); each GPU scans a "
                                             f"{a.cfg5_pairs}-pair shard of the same deterministic pair stream")
-            extra["cfg5_paired_local"], _ = run_workload(ctx, 5, 31, a.cfg5_pairs, "local", max(3, a.steps // 4),
-                                                         max(1, a.warmup // 2), with_lf=False, with_pcie=False,
-                                                         with_cpu=False, cpu_seconds=0, prepared=p5)
+            if want("cfg5_paired_local"):
+                lines["cfg5_paired_local"], _ = run_workload(ctx, 5, 31, a.cfg5_pairs, "local", max(3, a.steps // 4),
+                                                             max(1, a.warmup // 2), with_lf=False, with_pcie=False,
+                                                             with_cpu=False, cpu_seconds=0, prepared=p5)
             p5["dev"].close()
 
     if ctx.rank == 0:
-        out = {
-            "metric": "k-mers scanned/sec (whole node) at k=%d, 150 bp reads" % k,
-            "value": head["value"],
-            "unit": "k-mers/s",
-            "n_gpus": ctx.world,
-            "steps": a.steps,
-            "warmup": a.warmup,
-            "ms_per_step": head["ms_per_step"],
-            "higher_is_better": True,
-            "scaling": "weak",
-            "vs_baseline": None,
-            "dtype": "u32",
-            "data": "synthetic (splitmix64 references/reads, SURVEY.md §8(d))",
-            "config": {
-                "workload": head["workload"],
-                "k": k, "reads_per_gpu": n_reads, "paired": head["paired"], "mode": a.mode,
-                "prefix_q": a.prefix_q, "pair_steps": a.pair_steps, "triple_steps": a.triple_steps,
-                "label_table": int(prep["idx"].info().label_table),
-                "blocks_per_cu": dev.tuning("blocks_per_cu"), "grid_blocks": dev.tuning("grid_blocks"),
-                "kmers_per_step_per_gpu": head["kmers_per_step_per_gpu"],
-                "parallelism": f"dp{ctx.world} (reads sharded, index replicated)",
-                "collective": ("speq_allreduce_u64/_f64 (C ABI; RCCL ncclAllReduce of the G + 2 counters per step)"
-                               if ctx.comm is not None else "none (one GPU)"),
-                "index_build_s": head["index_build_s"], "index_builder": "gpu" if a.gpu_build else "host",
-                "fm_text_len": head["fm_text_len"], "kmer_table": head["kmer_table"],
-            },
-            "roofline": head["roofline"],
-            "cpu_baseline": head["cpu_baseline"],
-            "lf_steps": head["lf_steps"],
-            "kmer_table_kernel": head["kmer_table_kernel"],
-            "pcie_inclusive": head["pcie_inclusive"],
-            "check": head["check"],
-            **extra,
+        detail_path = a.detail or os.path.join(ROOT, "profiles", "r04", f"bench_detail_n{ctx.world}.json")
+        config = {
+            "workload": head["workload"],
+            "k": k, "reads_per_gpu": n_reads, "paired": head["paired"], "mode": a.mode,
+            "parallelism": f"dp{ctx.world} (reads sharded, index replicated)",
+            "collective": ("speq_allreduce_u64/_f64 (C ABI; RCCL ncclAllReduce of the G + 2 counters per step)"
+                           if ctx.comm is not None else "none (one GPU)"),
+            "index_build_s": head["index_build_s"], "index_builder": "gpu" if a.gpu_build else "host",
+            "fm_text_len": head["fm_text_len"],
+            "kmer_table": {"bytes": head["kmer_table"]["bytes"], "build_s": head["kmer_table"]["build_s"]},
         }
+        meta = {"metric": "k-mers scanned/sec (whole node) at k=%d, 150 bp reads" % k, "n_gpus": ctx.world,
+                "steps": a.steps, "warmup": a.warmup, "config": config,
+                "detail_file": os.path.relpath(detail_path, ROOT) if detail_path.startswith(ROOT) else detail_path}
+        out = compact_result(head, lines, meta)
+        try:
+            os.makedirs(os.path.dirname(detail_path), exist_ok=True)
+            with open(detail_path, "w") as f:
+                json.dump({"compact": out, "head": head, "lines": lines,
+                           "tuning": {"blocks_per_cu": dev.tuning("blocks_per_cu"),
+                                      "grid_blocks": dev.tuning("grid_blocks"), "prefix_q": a.prefix_q,
+                                      "pair_steps": a.pair_steps, "triple_steps": a.triple_steps,
+                                      "label_table": int(prep["idx"].info().label_table)},
+                           "host": host_cpu_info()}, f, indent=1, default=str)
+        except OSError as e:
+            out["detail_file"] = f"not written: {e}"
         print(json.dumps(out), flush=True)
     if ctx.comm is not None:
         ctx.comm.close()
@@ -473,32 +534,37 @@ def main():
         ctx.dist.destroy_process_group()
 
 
-def write_fastq(path: str, reads) -> int:
-    """Writes equal-length reads as four-line FASTQ records (@r<9-digit index>), vectorised; returns the bytes."""
+def write_fastq(path: str, reads, chunk: int = 1_000_000) -> int:
+    """Writes equal-length reads as four-line FASTQ records (@r<9-digit index>), vectorised in chunks; returns the
+    bytes."""
     lens = np.diff(reads.offsets)
     L = int(lens[0]) if len(lens) else 0
     if not len(lens) or np.any(lens != L):
         raise ValueError("write_fastq: equal-length reads only")
     n = len(lens)
-    head = np.frombuffer(b"@r", dtype=np.uint8)
-    digits = (np.arange(n, dtype=np.int64)[:, None] // (10 ** np.arange(8, -1, -1))[None, :]) % 10 + ord("0")
-    rec = np.empty((n, 2 + 9 + 1 + L + 3 + L + 1), dtype=np.uint8)
-    rec[:, 0:2] = head
-    rec[:, 2:11] = digits.astype(np.uint8)
-    rec[:, 11] = ord("\n")
-    rec[:, 12:12 + L] = reads.seq.reshape(n, L)
-    rec[:, 12 + L:15 + L] = np.frombuffer(b"\n+\n", dtype=np.uint8)
-    rec[:, 15 + L:15 + 2 * L] = reads.qual.reshape(n, L)
-    rec[:, 15 + 2 * L] = ord("\n")
-    rec.tofile(path)
-    return rec.size
+    total = 0
+    with open(path, "wb") as f:
+        for r0 in range(0, n, chunk):
+            m = min(chunk, n - r0)
+            digits = ((np.arange(r0, r0 + m, dtype=np.int64)[:, None] // (10 ** np.arange(8, -1, -1))[None, :]) % 10
+                      + ord("0"))
+            rec = np.empty((m, 2 + 9 + 1 + L + 3 + L + 1), dtype=np.uint8)
+            rec[:, 0:2] = np.frombuffer(b"@r", dtype=np.uint8)
+            rec[:, 2:11] = digits.astype(np.uint8)
+            rec[:, 11] = ord("\n")
+            rec[:, 12:12 + L] = reads.seq[r0 * L:(r0 + m) * L].reshape(m, L)
+            rec[:, 12 + L:15 + L] = np.frombuffer(b"\n+\n", dtype=np.uint8)
+            rec[:, 15 + L:15 + 2 * L] = reads.qual[r0 * L:(r0 + m) * L].reshape(m, L)
+            rec[:, 15 + 2 * L] = ord("\n")
+            rec.tofile(f)
+            total += rec.size
+    return total
 
 
 def fastq_e2e(ctx: Ctx, prep: dict, k: int) -> dict:
     """The drop-in input path (speq_scan_fastq: reader thread + parser threads -> pinned slots -> H2D || scan) on the
     workload's reads written as one FASTQ file on local disk; best of 3 passes with the page cache warm. Checked
     against the HBM-resident scan of the same reads."""
-    import tempfile
     reads, dev = prep["reads"], prep["dev"]
     threads = host_cpu_info()["threads"]
     with tempfile.TemporaryDirectory(dir=os.environ.get("TMPDIR", "/tmp")) as td:
@@ -518,25 +584,96 @@ def fastq_e2e(ctx: Ctx, prep: dict, k: int) -> dict:
     kmers = int(np.maximum(lens - k + 1, 0).sum())
     return {"value": kmers / best, "unit": "k-mers/s", "file_GB_per_s": nbytes / best / 1e9, "seconds": best,
             "file_bytes": nbytes, "threads": threads, "k": k,
+            "check": {"T": int(res.total), "ambiguous": int(res.ambiguous), "U_sha1": u_sha1(res.unique)},
             "path": "speq_scan_fastq: plain FASTQ on local disk (page cache warm), parallel record-aligned cut, "
                     "raw text to pinned slots -> H2D (copy stream) || GPU record parsing + k_scan_ax",
             "workload": f"{reads.n} x 150 bp reads of BASELINE config 2, global mode"}
 
 
-def cpu_baseline(ref, reads, k, G, target_s, local, paired=False, idx=None):
-    """CPU baselines on this host's cores over a bounded sample of the same reads (rank 0, N = 1 only).
+def cli_e2e(prep: dict, k: int, check: dict) -> dict:
+    """The user-visible path end to end (SURVEY §8(d) secondary metric): `bin/speq index` then `bin/speq scan` as
+    processes on files — config 3's references + groupings, its 10 M reads as one FASTQ on local disk — at the
+    reference's defaults (Phred-weighted, phred cutoff 30; src/main.cpp:25-31 -> fm_scanner.cpp:309-545) with
+    k = 31: FASTQ stream + scan, the .dat pass (first scan only), unique_to_percent and the EM loop. T and the
+    ambiguous count on stderr are checked against the HBM-resident scan of the same reads (`check`)."""
+    ref, reads = prep["ref"], prep["reads"]
+    threads = host_cpu_info()["threads"]
+    speq = os.path.join(ROOT, "bin", "speq")
+    work = tempfile.mkdtemp(prefix="speq_cli_", dir=os.environ.get("TMPDIR", "/tmp"))
+    env = dict(os.environ, SPEQ_CLI_TIMING="1")
+    res = {"unit": "k-mers/s", "threads": threads, "k": k}
+    try:
+        with open(os.path.join(work, "refs.fa"), "w") as f:
+            f.write(ref.fasta_text())
+        with open(os.path.join(work, "groups.txt"), "w") as f:
+            f.write(ref.groupings_text())
+        t0 = time.perf_counter()
+        fq_bytes = write_fastq(os.path.join(work, "r1.fq"), reads)
+        res["fastq_write_s"] = round(time.perf_counter() - t0, 2)
+        lens = np.diff(reads.offsets).astype(np.int64)
+        kmers = int(np.maximum(lens - k + 1, 0).sum())
+
+        def run(args):
+            t0 = time.perf_counter()
+            p = subprocess.run([speq] + args, cwd=work, capture_output=True, text=True, env=env, timeout=300)
+            dt = time.perf_counter() - t0
+            if p.returncode != 0:
+                raise RuntimeError(f"speq {args[0]} failed ({p.returncode}): {p.stderr[-400:]}")
+            phases = {}
+            for ln in p.stderr.splitlines():
+                if ln.startswith("speq: ") and ln.endswith(" s"):
+                    name, sec = ln[6:-2].rsplit(None, 1)
+                    try:
+                        phases[name.strip()] = float(sec)
+                    except ValueError:
+                        pass
+            return dt, p.stderr, phases
+
+        res["index_s"], _, res["index_phases"] = run(["index", "-r", "refs.fa", "-g", "groups.txt", "-x", "ref",
+                                                      "-t", str(threads)])
+        scan = ["scan", "-1", "r1.fq", "-x", "ref", "-k", str(k), "-t", str(threads), "-o", "out.txt"]
+        res["first_scan_s"], _, res["first_scan_phases"] = run(scan)  # + the .dat pass (new index)
+        dt, err, phases = run(scan)  # .dat cached (the reference's steady state: fm_scanner.cpp:79-135)
+        tl = [ln for ln in err.splitlines() if ln.count("\t") == 1 and ln.replace("\t", "").isdigit()]
+        T, amb = (int(x) for x in tl[0].split("\t"))
+        if (T, amb) != (check["T"], check["ambiguous"]):
+            raise RuntimeError(f"speq scan stderr T/ambiguous {(T, amb)} != HBM-resident scan "
+                               f"{(check['T'], check['ambiguous'])}")
+        res.update(value=kmers / dt, seconds=dt, phases=phases, kmers=kmers, fastq_bytes=fq_bytes,
+                   em_iterations=err.count("Percent of each group"),
+                   check={"T": T, "ambiguous": amb, "matches_hbm_scan": True},
+                   path="bin/speq scan process: index load || HIP init, FASTQ stream (parallel cut, GPU parsing) + "
+                        "k_scan_ax, cached .dat, unique_to_percent, EM loop over the interval histogram, -o write",
+                   workload=f"BASELINE config 3 references, {reads.n} x 150 bp reads (FASTQ on local disk), k={k}, "
+                            f"Phred-weighted (reference default mode)")
+    finally:
+        subprocess.run(["rm", "-rf", work])
+    return res
+
+
+_SEQAN_LIKE = {}
+
+
+def cpu_baseline(prep, reads, k, G, target_s, local, paired=False, extra_ports=False):
+    """CPU baseline on this host's cores over a bounded sample of the same reads (rank 0, N = 1 only).
 
     value: oracle/seqan_like.c — the reference's ALGORITHM restated (backward search on a wavelet structure, locate of
     every hit through SA samples every 16 rows, sorted hit lists, first-hit rule), the SURVEY.md 8(d) stand-in for
-    the SeqAn3 binary, which cannot be built here (8(c)). "hash_port" beside it: oracle/kmer_oracle.c, a hash-map
-    restatement of the same semantics (no FM-index, no locate) — an upper bound for any CPU port."""
+    the SeqAn3 binary, which cannot be built here (8(c)). Its counts on the sample are checked against the GPU scan of
+    the same sample (`checked`). extra_ports (headline): also oracle/kmer_oracle.c (hash map, no FM-index) and
+    oracle/fm_cpu.c (this build's label-run search on host cores)."""
     from oracle.oracle import Oracle, SeqanLike
+    ref, idx, dev = prep["ref"], prep["idx"], prep["dev"]
     hw = host_cpu_info()
     threads = hw["threads"]
     t0 = time.perf_counter()
-    sl = SeqanLike(ref.records, ref.groups, G)
+    cfg = prep.get("cfg")
+    sl = _SEQAN_LIKE.get(cfg)
+    if sl is None:
+        # the product index's suffix array of the same text spares the stand-in its O(n log n) doubling sort
+        # (minutes at config 5); a suffix array is unique (tests/test_seqan_like.py checks the two builds agree)
+        sl = _SEQAN_LIKE[cfg] = SeqanLike(ref.records, ref.groups, G, sa=idx.array("sa", np.uint32))
     sl_build = time.perf_counter() - t0
-    orc = Oracle(ref.records, ref.groups, G, k)
     units = reads.n // 2 if paired else reads.n
 
     def timed(fn, target):
@@ -545,47 +682,57 @@ def cpu_baseline(ref, reads, k, G, target_s, local, paired=False, idx=None):
             b = int(reads.offsets[nr])
             t0 = time.perf_counter()
             for _ in range(reps):
-                fn(reads.seq[:b], reads.qual[:b], reads.offsets[:nr + 1])
-            return time.perf_counter() - t0
+                r = fn(reads.seq[:b], reads.qual[:b], reads.offsets[:nr + 1])
+            return time.perf_counter() - t0, r
 
-        n = min(units, 2_000)
-        t = run(n)
+        n = min(units, 500)
+        t, r = run(n)
         while t < target / 2 and n < units:  # grow the sample first, repeat passes only over the whole shard
             n = int(min(units, n * min(8.0, 1.2 * target / max(t, 1e-3))))
-            t = run(n)
+            t, r = run(n)
         reps = 1
         if t < target / 2:
             reps = max(1, int(target / max(t, 1e-3)))
-            t = run(n, reps)
+            t, r = run(n, reps)
         nr = 2 * n if paired else n
         lens = np.diff(reads.offsets[:nr + 1]).astype(np.int64)
         km = int(np.maximum(lens - k + 1, 0).sum()) * reps
-        return km / t, n, reps, km, t
+        return km / t, n, reps, km, t, r
 
-    v, n, reps, km, t = timed(lambda s, q, o: sl.scan(s, q, o, k=k, paired=paired, local=local, threads=threads),
-                              target_s)
-    hv, hn, hreps, hkm, ht = timed(lambda s, q, o: orc.scan(s, q, o, paired=paired, local=local, threads=threads),
-                                   target_s / 3)
-    lr = None
-    if idx is not None and k <= 32 and not local:  # the build's own algorithm on CPU cores (oracle/fm_cpu.c)
-        from oracle.oracle import FmCpu
-        fc = FmCpu(idx)
-        lv, ln, lreps, lkm, lt = timed(lambda s, q, o: fc.scan(s, q, o, k=k, paired=paired, threads=threads),
-                                       target_s / 3)
-        lr = {"value": lv, "unit": "k-mers/s", "cores": threads,
-              "sample": f"first {ln} x {lreps} passes ({lkm} k-mers, {lt:.1f} s), oracle/fm_cpu.c (this build's "
-                        f"label-run FM-index search on host cores, same index arrays as the GPU)"}
+    v, n, reps, km, t, r = timed(lambda s, q, o: sl.scan(s, q, o, k=k, paired=paired, local=local, threads=threads),
+                                 target_s)
+    # the same sample through the product (host buffers -> GPU): the baseline computed the same answer
+    nr = 2 * n if paired else n
+    b = int(reads.offsets[nr])
+    g = dev.scan(reads.seq[:b].tobytes(), reads.qual[:b].tobytes(), reads.offsets[:nr + 1], k=k, paired=paired,
+                 local=local)
+    checked = (r[0], r[1], r[2].tolist()) == (g.total, g.ambiguous, g.unique.tolist())
+    if checked and local:
+        checked = bool(np.allclose(r[3], g.weights, rtol=1e-9, atol=0))
+    if not checked:
+        raise RuntimeError("CPU baseline (seqan_like) disagrees with the GPU scan on its sample")
     unit = "pairs" if paired else "reads"
-    return {"value": v, "unit": "k-mers/s", "cores": threads, "kind": "port",
-            "sample": f"first {n} {unit} of the same workload x {reps} passes ({km} k-mers, {t:.1f} s) through "
-                      f"oracle/seqan_like.c: the reference algorithm (wavelet backward search + SA-sample-16 locate "
-                      f"of every hit + sorted hit list + first-hit rule; index build {sl_build:.1f} s not timed); "
-                      f"the SeqAn3 binary cannot be built here (SURVEY.md 8(c))",
-            "host": hw,
-            "label_run_port": lr,
-            "hash_port": {"value": hv, "unit": "k-mers/s", "cores": threads,
-                          "sample": f"first {hn} {unit} x {hreps} passes ({hkm} k-mers, {ht:.1f} s), "
-                                    f"oracle/kmer_oracle.c (hash map k-mer -> group label: no FM-index, no locate)"}}
+    out = {"value": v, "unit": "k-mers/s", "cores": threads, "kind": "port", "checked": True,
+           "sample": f"first {n} {unit} x {reps} ({km} k-mers, {t:.1f} s), oracle/seqan_like.c (wavelet backward "
+                     f"search + SA-sample-16 locate of every hit + first-hit rule), {threads} threads",
+           "host": hw, "index_build_s_untimed": round(sl_build, 1)}
+    if extra_ports:
+        orc = Oracle(ref.records, ref.groups, G, k)
+        hv, hn, hreps, hkm, ht, _ = timed(lambda s, q, o: orc.scan(s, q, o, paired=paired, local=local,
+                                                                   threads=threads), target_s / 3)
+        out["hash_port"] = {"value": hv, "unit": "k-mers/s", "cores": threads,
+                            "sample": f"first {hn} {unit} x {hreps} passes ({hkm} k-mers, {ht:.1f} s), "
+                                      f"oracle/kmer_oracle.c (hash map k-mer -> group label: no FM-index, no locate)"}
+        if k <= 32 and not local:  # the build's own algorithm on CPU cores (oracle/fm_cpu.c)
+            from oracle.oracle import FmCpu
+            fc = FmCpu(idx)
+            lv, ln, lreps, lkm, lt, _ = timed(lambda s, q, o: fc.scan(s, q, o, k=k, paired=paired, threads=threads),
+                                              target_s / 3)
+            out["label_run_port"] = {"value": lv, "unit": "k-mers/s", "cores": threads,
+                                     "sample": f"first {ln} x {lreps} passes ({lkm} k-mers, {lt:.1f} s), "
+                                               f"oracle/fm_cpu.c (this build's label-run FM-index search on host "
+                                               f"cores, same index arrays as the GPU)"}
+    return out
 
 
 if __name__ == "__main__":

@@ -45,6 +45,11 @@ def lib() -> C.CDLL:
         L.oracle_ref_unique.argtypes = [P, U64P, U64P]
         L.sl_build.restype = P
         L.sl_build.argtypes = [C.c_char_p, U64P, C.c_uint32, C.POINTER(C.c_int32), C.c_uint32]
+        L.sl_build_sa.restype = P
+        L.sl_build_sa.argtypes = [C.c_char_p, U64P, C.c_uint32, C.POINTER(C.c_int32), C.c_uint32,
+                                  C.POINTER(C.c_uint32)]
+        L.sl_sample.restype = C.c_uint32
+        L.sl_sample.argtypes = [P, C.c_uint32]
         L.sl_free.argtypes = [P]
         L.sl_count.restype = C.c_int64
         L.sl_count.argtypes = [P, C.c_char_p, C.c_uint32]
@@ -136,13 +141,24 @@ class SeqanLike:
     every hit through SA samples (every 16 rows), sorted hit list, first-hit group rule. k is chosen per scan, as
     with the reference's index."""
 
-    def __init__(self, records: Sequence[bytes], groups: Sequence[int], n_groups: int):
+    def __init__(self, records: Sequence[bytes], groups: Sequence[int], n_groups: int, sa=None):
+        """sa: optional suffix array of the same text (t_0 $ t_1 $ ... #, codes # $ A C G T N = 0..6), e.g. the
+        product index's (FmIndex.array("sa")): a suffix array is unique, so it only skips this file's own O(n log n)
+        sort (bench.py's config-5 baseline; the scan, which is what is timed, is this file's code alone)."""
         bs = [bytes(r) for r in records]
         off = np.zeros(len(bs) + 1, dtype=np.uint64)
         off[1:] = np.cumsum([len(b) for b in bs])
         g = np.asarray(groups, dtype=np.int32)
         self.G = n_groups
-        self._h = lib().sl_build(b"".join(bs), _u64p(off), len(bs), g.ctypes.data_as(C.POINTER(C.c_int32)), n_groups)
+        if sa is None:
+            self._h = lib().sl_build(b"".join(bs), _u64p(off), len(bs), g.ctypes.data_as(C.POINTER(C.c_int32)),
+                                     n_groups)
+        else:
+            sa = np.ascontiguousarray(sa, dtype=np.uint32)
+            if len(sa) != int(off[-1]) * 2 + 2 * len(bs) + 1:
+                raise ValueError("SeqanLike: suffix array length does not match the text")
+            self._h = lib().sl_build_sa(b"".join(bs), _u64p(off), len(bs), g.ctypes.data_as(C.POINTER(C.c_int32)),
+                                        n_groups, sa.ctypes.data_as(C.POINTER(C.c_uint32)))
         if not self._h:
             raise ValueError("sl_build failed")
 
@@ -152,6 +168,10 @@ class SeqanLike:
 
     def count(self, kmer: bytes) -> int:
         return int(lib().sl_count(self._h, kmer, len(kmer)))
+
+    def sample(self, j: int) -> int:
+        """SA[16 j] of this structure (0xFFFFFFFF past the end)."""
+        return int(lib().sl_sample(self._h, j))
 
     def which(self, kmer: bytes) -> int:
         return int(lib().sl_which(self._h, kmer, len(kmer)))

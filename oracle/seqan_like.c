@@ -148,8 +148,11 @@ void sl_free(sl_t* s) {
     free(s);
 }
 
-sl_t* sl_build(const char* seq, const uint64_t* rec_off, uint32_t n_records, const int32_t* group_of_rec,
-               uint32_t n_groups) {
+/* Builds the stand-in index. given_sa (may be NULL): the suffix array of the same text computed elsewhere — a suffix
+ * array is unique, so it only saves the O(n log n) doubling here (bench.py's config-5 CPU baseline, where the build
+ * is not timed); NULL sorts with build_sa. tests/test_seqan_like.py checks both give the same structure. */
+sl_t* sl_build_sa(const char* seq, const uint64_t* rec_off, uint32_t n_records, const int32_t* group_of_rec,
+                  uint32_t n_groups, const uint32_t* given_sa) {
     if (n_records == 0) return NULL;
     uint64_t total = 1;
     for (uint32_t r = 0; r < n_records; ++r) total += 2 * (rec_off[r + 1] - rec_off[r] + 1);
@@ -175,7 +178,13 @@ sl_t* sl_build(const char* seq, const uint64_t* rec_off, uint32_t n_records, con
     }
     s->text_start[s->n_texts] = p;
     t[p] = S_TERM;
-    uint32_t* sa = build_sa(t, n);
+    uint32_t* sa = NULL;
+    if (given_sa) {
+        sa = (uint32_t*)malloc(sizeof(uint32_t) * n);
+        memcpy(sa, given_sa, sizeof(uint32_t) * n);
+    } else {
+        sa = build_sa(t, n);
+    }
     uint8_t* bwt = (uint8_t*)malloc(n);
     uint32_t cnt[SIGMA] = {0};
     for (uint32_t i = 0; i < n; ++i) {
@@ -215,6 +224,14 @@ sl_t* sl_build(const char* seq, const uint64_t* rec_off, uint32_t n_records, con
     for (int c = 0; c < SIGMA; ++c) s->base[c] = wm_map(s, (uint8_t)c, 0);
     return s;
 }
+
+sl_t* sl_build(const char* seq, const uint64_t* rec_off, uint32_t n_records, const int32_t* group_of_rec,
+               uint32_t n_groups) {
+    return sl_build_sa(seq, rec_off, n_records, group_of_rec, n_groups, NULL);
+}
+
+/* SA[16 j] samples (tests: the given-SA build equals the own build) */
+uint32_t sl_sample(const sl_t* s, uint32_t j) { return j * SAMPLE < s->n ? s->samples[j] : 0xFFFFFFFFu; }
 
 /* Backward search of k symbols (codes); returns the SA interval [lo, hi). */
 static inline void search(const sl_t* s, const uint8_t* q, uint32_t k, uint32_t* lo_out, uint32_t* hi_out) {

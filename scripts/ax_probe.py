@@ -28,6 +28,8 @@ def main():
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--variants", type=int, default=0, help="override the config's variant (group) count")
     ap.add_argument("--qual", default="q40", help="quality profile (speq_amd.synth.QUALITY_PROFILES)")
+    ap.add_argument("--stats", action="store_true",
+                    help="also run the instrumented twin once: work counters + per-section clock shares")
     a = ap.parse_args()
     c = dict(synth.CONFIGS[a.config])
     if a.variants:
@@ -65,9 +67,21 @@ def main():
                 ms, n = dev.timing_read()
                 if it > 0:
                     best = ms if best is None else min(best, ms)
-            print(json.dumps({"err": err, "k": k, "ms": round(best, 4), "Gkmers_s": round(kmers / best / 1e6, 1),
-                              "kernel": dev.tuning("last_kernel"), "T": int(cnt[0]), "amb": int(cnt[1]),
-                              "tune": a.tune, "local": a.local, "qual": a.qual, "table_bytes": info["table_bytes"]}), flush=True)
+            rec = {"err": err, "k": k, "ms": round(best, 4), "Gkmers_s": round(kmers / best / 1e6, 1),
+                   "kernel": dev.tuning("last_kernel"), "T": int(cnt[0]), "amb": int(cnt[1]),
+                   "tune": a.tune, "local": a.local, "qual": a.qual, "table_bytes": info["table_bytes"]}
+            if a.stats and rec["kernel"] == 3:
+                c0 = cnt.cpu().numpy().copy()
+                cnt.zero_()
+                w.zero_()
+                st = dev.scan_device_stats(d_seq.data_ptr(), d_qual.data_ptr(), d_off.data_ptr(), reads.n, k,
+                                           cnt.data_ptr(), w.data_ptr(), local=a.local, paired=a.paired)
+                rec["stats_equal"] = bool((cnt.cpu().numpy() == c0).all())
+                tot = max(1, st["cyc_total"])
+                rec["cycle_share"] = {s_: round(st[f"cyc_{s_}"] / tot, 3) for s_ in ("refill", "lookup", "run", "phase2")}
+                rec["work"] = {k_: v for k_, v in st.items() if not k_.startswith("cyc_")}
+                rec["cyc"] = {k_: v for k_, v in st.items() if k_.startswith("cyc_")}
+            print(json.dumps(rec), flush=True)
 
 
 if __name__ == "__main__":

@@ -5,11 +5,12 @@ Usage: python scripts/summarize_profile.py gpurun_out/prof profiles/r01 [--tag c
            [--traffic-key cfg2_k21_global_reads1000000_ax]
 --traffic-key also records the launch's fabric bytes in profiles/traffic.json under that key, where bench.py looks
 them up (cfg<N>_k<k>_<mode>_reads<reads per GPU>_<ax|kt|lf>) for the `traffic` field of its roofline.
-HBM/fabric bytes follow MI355X_MICROARCH.md §HBM: FETCH_SIZE and WRITE_SIZE are in KiB and derive from the L2's
-memory-side request counters (TCC_EA0_RDREQ x 64 B); Infinity-Cache hits are counted, not excluded, so they are an
-upper bound on HBM bytes for an index that stays MALL-resident. (The documented x2 correction applies to wide
-coalesced 16 B/lane streams; this kernel's traffic is 16-B random gathers, for which FETCH_SIZE == RDREQ x 64 B
-exactly — checked below — so no correction is applied.)
+Fabric bytes (round 4): TCC_EA0_RDREQ x 128 B + WRITE_SIZE, per profiles/r04/counter_calibration.json
+(scripts/calibrate_counters.sh): on gfx950 TCC_BUBBLE and TCC_EA0_RDREQ_32B read 0, so FETCH_SIZE = RDREQ x 64 B,
+while one RDREQ is issued per 128-B line filled from the fabric for the 16-B/lane stream (exact: FETCH_SIZE reports
+half of a known 2 GiB read, MI355X_MICROARCH.md §HBM) and for 16/64/128-B random gathers (one request per line).
+FETCH_SIZE (RDREQ x 64 B) is kept as the lower bound. Infinity-Cache hits are counted (L2 -> fabric requests), so
+these are upper bounds on HBM bytes for an index that stays MALL-resident.
 """
 import collections
 import csv
@@ -42,7 +43,7 @@ def main():
             out["scan_steady_state_avg_ns"] = sum(tail) / len(tail)
     pmc = collections.defaultdict(list)
     meta = {}
-    for p in ("fetch", "write", "tcc", "sq", "sq2", "ta"):
+    for p in ("fetch", "write", "tcc", "sq", "sq2", "ta", "req"):
         f = os.path.join(src, p, f"{p}_counter_collection.csv")
         if not os.path.exists(f):
             continue
@@ -65,9 +66,30 @@ def main():
     if "TCC_HIT_sum" in means:
         h, m = means["TCC_HIT_sum"], means.get("TCC_MISS_sum", 0.0)
         out["l2_hit_rate"] = h / max(1.0, h + m)
+    if "TCC_EA0_RDREQ_sum" in means:  # calibrated: 128 B per request (profiles/r04/counter_calibration.json)
+        out["fabric_read_bytes_calibrated"] = means["TCC_EA0_RDREQ_sum"] * 128.0
+        out["fabric_read_bytes_lower_bound"] = means["TCC_EA0_RDREQ_sum"] * 64.0
+        if "TCC_BUBBLE_sum" in means:
+            out["tcc_bubble"] = means["TCC_BUBBLE_sum"]
+            out["tcc_rdreq_32b"] = means.get("TCC_EA0_RDREQ_32B_sum")
     json.dump(out, open(os.path.join(dst, f"pmc_{tag}.json"), "w"), indent=1)
     print(json.dumps(out, indent=1))
-    if tkey and "fabric_read_bytes_per_launch" in out:
+    if tkey and "fabric_read_bytes_calibrated" in out:
+        tp = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "profiles", "traffic.json")
+        tj = json.load(open(tp)) if os.path.exists(tp) else {}
+        wr = out.get("fabric_write_bytes_per_launch", 0.0)
+        tj[tkey] = {"fabric_bytes_per_launch": out["fabric_read_bytes_calibrated"] + wr,
+                    "fabric_read_bytes_per_launch": out["fabric_read_bytes_calibrated"],
+                    "fabric_bytes_lower_bound": out["fabric_read_bytes_lower_bound"] + wr,
+                    "write_bytes_per_launch": out.get("fabric_write_bytes_per_launch"),
+                    "method": "TCC_EA0_RDREQ x 128 B + WRITE_SIZE (profiles/r04/counter_calibration.json); lower "
+                              "bound RDREQ x 64 B (= FETCH_SIZE)",
+                    "source": os.path.relpath(os.path.join(dst, f"pmc_{tag}.json"), os.path.join(os.path.dirname(tp))),
+                    "l2_hit_rate": out.get("l2_hit_rate"),
+                    "scratch_bytes_per_lane": meta.get("Scratch_Size"), "vgpr_count": meta.get("VGPR_Count"),
+                    "kernel_steady_state_ns_rocprof": out.get("scan_steady_state_avg_ns")}
+        json.dump(tj, open(tp, "w"), indent=1)
+    elif tkey and "fabric_read_bytes_per_launch" in out:
         tp = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "profiles", "traffic.json")
         tj = json.load(open(tp)) if os.path.exists(tp) else {}
         scratch = None

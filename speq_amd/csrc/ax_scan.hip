@@ -108,6 +108,11 @@ enum : uint32_t {
     AXS_BUSY_5_16,       // ... 5-16
     AXS_BUSY_17_32,      // ... 17-32
     AXS_BUSY_33_64,      // ... 33-64
+    AXS_CYC_REFILL,      // shader-clock cycles (s_memtime, summed over waves): refills
+    AXS_CYC_LOOKUP,      // ... phase-1 lookup iterations
+    AXS_CYC_RUN,         // ... phase-1 run iterations
+    AXS_CYC_P2,          // ... phase 2 (deferred windows)
+    AXS_CYC_TOTAL,       // ... the whole loop
     AXS_N
 };
 static_assert(AXS_N == SPEQ_AX_STATS_N, "speq_scan.h SPEQ_AX_STATS_N");
@@ -243,10 +248,8 @@ __device__ int ax_search_text(const DevView& I, const Rsrc& R, const uint8_t* __
 
 // Pass A: the class code of the k-mer at every text position (one byte per position, packed into granules by pass
 // B), and one representative position per distinct k-mer (the first to claim owner[lo] of its SA interval).
-// Multi-group k-mers also record their interval: mlo[pos] = its start and mhi[start] = its end (EM histograms).
 __global__ void k_ax_classify(DevView I, const uint8_t* __restrict__ text, const uint64_t* __restrict__ tbad,
-                              uint64_t n, uint32_t k, uint8_t* __restrict__ codes, uint32_t* __restrict__ mlo,
-                              uint32_t* __restrict__ mhi, uint32_t* __restrict__ owner,
+                              uint64_t n, uint32_t k, uint8_t* __restrict__ codes, uint32_t* __restrict__ owner,
                               unsigned long long* __restrict__ n_distinct) {
     const Rsrc R = make_rsrc(I);
     unsigned long long claimed = 0;
@@ -271,13 +274,26 @@ __global__ void k_ax_classify(DevView I, const uint8_t* __restrict__ text, const
         const int g = ax_search_text(I, R, text + pos, k, lo, hi);
         // g == -1 cannot happen: the window occurs at pos; g >= 0 is the group of pos's text
         codes[pos] = (uint8_t)(g >= 0 ? AX_OWN : AX_MULTI);
-        if (g == -2) {
-            mlo[pos] = lo;
-            mhi[lo] = hi;
-        }
         if (atomicCAS(&owner[lo], AX_EMPTY, (uint32_t)pos) == AX_EMPTY) ++claimed;
     }
     if (claimed) atomicAdd(n_distinct, claimed);
+}
+
+// EM scans only (built on the first EM scan of k): every text position whose k-mer is MULTI (granule class planes)
+// records its SA interval, mlo[pos] = its start and mhi[start] = its end, for the EM histogram of the scan.
+__global__ void k_ax_em_intervals(DevView I, const uint8_t* __restrict__ text, const u32x4* __restrict__ gran,
+                                  uint64_t n, uint32_t k, uint32_t* __restrict__ mlo, uint32_t* __restrict__ mhi) {
+    const Rsrc R = make_rsrc(I);
+    for (uint64_t pos = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; pos < n;
+         pos += (uint64_t)gridDim.x * blockDim.x) {
+        const u32x4 gv = gran[pos >> 5];
+        const uint32_t b = (uint32_t)pos & 31u;
+        if ((((gv[2] >> b) & 1u) | (((gv[3] >> b) & 1u) << 1)) != AX_MULTI) continue;
+        uint32_t lo = 0, hi = 0;
+        ax_search_text(I, R, text + pos, k, lo, hi);  // a MULTI window is all ACGT and occurs at pos
+        mlo[pos] = lo;
+        mhi[lo] = hi;
+    }
 }
 
 // Pass B: granule b = {t2 word b (positions 32b .. 32b + 31), class plane 0, class plane 1}; positions >= n are END.
@@ -431,7 +447,6 @@ __device__ __forceinline__ bool ax_probe(const AxView& A, const __amdgpu_buffer_
 //   vw     u64 [AX_VWW][64]     valid-window bits, read-relative (window j of the piece at bit j); while staging, the
 //                               bad-base bits of the refilling lanes, chunk c in 16 bits of the lane's own word c / 4
 //   chg    u16 [AX_CHUNKS][64]  (local) quality-change bits per slot position
-//   rbase  u32 [64]             (local) offset of the piece's first base in seq/qual, from the wave's first unit's
 //   off0s  u8 [64]              the piece's first base in its slot (a - a16)
 //   defl   u16 [ax_def]         deferred windows (lane | window << 6), defn u32[4] counters, ambf/ambd i32[64]
 //   wl     u32 [AX_WL]          (local) weight work list: 8-window blocks of runs with varying qualities
@@ -448,7 +463,7 @@ constexpr uint32_t AX_OWNB = 64u * SPEQ_AX_SU_MAX;  // bytes of the staging owne
 template <int MODE>
 constexpr uint32_t ax_wave_bytes() {
     static_assert(8u * AX_VWW >= 2u * AX_CHUNKS, "the bad-base bits of a staged piece live in its valid-window words");
-    return 4u * AX_CHUNKS * 64u + 8u * AX_VWW * 64u + (MODE == KM_LOCAL ? 2u * AX_CHUNKS * 64u + 4u * 64u : 0u) +
+    return 4u * AX_CHUNKS * 64u + 8u * AX_VWW * 64u + (MODE == KM_LOCAL ? 2u * AX_CHUNKS * 64u : 0u) +
            64u + 2u * ax_def<MODE>() + 16u + 8u * 64u + (MODE == KM_LOCAL ? 4u * AX_WL + 4u * 64u : 0u) + AX_OWNB;
 }
 
@@ -542,8 +557,7 @@ __global__ __launch_bounds__(AX_THREADS, (ax_min_waves<MODE, HW, EM, STATS>())) 
     uint64_t* vw = reinterpret_cast<uint64_t*>(codes + AX_CHUNKS * 64u);     // [AX_VWW][64]
     uint16_t* bad16 = reinterpret_cast<uint16_t*>(vw);                       // staging: see bad_at
     uint16_t* chg = reinterpret_cast<uint16_t*>(vw + AX_VWW * 64u);          // [AX_CHUNKS][64] (local)
-    uint32_t* rbase = reinterpret_cast<uint32_t*>(chg + (MODE == KM_LOCAL ? AX_CHUNKS * 64u : 0u));  // [64] (local)
-    uint8_t* off0s = reinterpret_cast<uint8_t*>(rbase + (MODE == KM_LOCAL ? 64u : 0u));              // [64]
+    uint8_t* off0s = reinterpret_cast<uint8_t*>(chg + (MODE == KM_LOCAL ? AX_CHUNKS * 64u : 0u));   // [64]
     uint16_t* defl = reinterpret_cast<uint16_t*>(off0s + 64);                // [AX_DEF]
     constexpr uint32_t AX_DEF = ax_def<MODE>();
     uint32_t* defn = reinterpret_cast<uint32_t*>(defl + AX_DEF);             // [4]: entries, survivors, sums
@@ -588,6 +602,8 @@ __global__ __launch_bounds__(AX_THREADS, (ax_min_waves<MODE, HW, EM, STATS>())) 
     uint32_t s_iter = 0, s_lk = 0, s_rn = 0, s_lkw = 0, s_rnw = 0, s_rwin = 0, s_def = 0, s_fp = 0, s_p2 = 0,
              s_p2v = 0, s_ch = 0, s_seg = 0, s_qb = 0, s_tal = 0, s_rg = 0, s_spl = 0, s_b4 = 0, s_b16 = 0, s_b32 = 0,
              s_b64 = 0;
+    // section clocks (STATS only; wave-uniform, kept by every lane, reported by lane 0)
+    uint64_t c_ref = 0, c_lk = 0, c_rn = 0, c_p2 = 0, c_t0 = STATS ? clock64() : 0ull, c_s = 0;
 
     auto add_count = [&](uint32_t g, uint32_t cnt, double wsum) {
         if (LDS_HIST) {
@@ -728,13 +744,10 @@ __global__ __launch_bounds__(AX_THREADS, (ax_min_waves<MODE, HW, EM, STATS>())) 
     // dealt round robin, profiles/r03/ax_variants_owner_group.jsonl)
     uint64_t cur = (nu * gw) / NWV;  // next unit
     const uint64_t cur_end = (nu * (gw + 1)) / NWV;
-    // rbase origin (local mode): the bases of the wave's share of units, from here, are addressed with 32 bits — a share
-    // of nu / (5,120 waves) units spans far less than 4 GiB unless single reads are gigabases long
-    const uint64_t wbase = MODE == KM_LOCAL ? src.off[PAIRED ? 2 * cur : cur] : 0;
     // ---- phase-1 state of the current piece
     uint32_t wend = 0;         // windows of the piece
     uint32_t off0 = 0;         // first base of the piece in the slot
-    uint64_t ta = 0;           // first base of the piece in seq/qual (local mode)
+    uint64_t ta = 0;           // first base of the piece in seq/qual (local mode; other lanes read it by a shuffle)
     uint32_t j = 0;
     uint32_t st = 2u;          // 0: look window j up, 1: extend from text position p, 2: idle
     bool verify = false;       // st 1: p came from the anchor table (window j itself not compared yet)
@@ -763,6 +776,7 @@ __global__ __launch_bounds__(AX_THREADS, (ax_min_waves<MODE, HW, EM, STATS>())) 
         const bool p2 = blk != 0 && ((uint32_t)__popcll(blk) >= SPEQ_AX_BLOCKED || busy == 0 ||
                                      __builtin_amdgcn_readfirstlane(defn[0]) + 256u > AX_DEF);
         const uint32_t n_def = (SPEQ_AX_MICRO && !p2) ? 0u : __builtin_amdgcn_readfirstlane(defn[0]);
+        if (STATS) c_s = clock64();
         if (p2) {
             // ---- phase 2: the deferred windows of the wave. (a) the Bloom filter, AX_F windows per lane per round
             // trip; the windows it cannot rule out are compacted to the front of the list; (b) those are looked up
@@ -817,6 +831,8 @@ __global__ __launch_bounds__(AX_THREADS, (ax_min_waves<MODE, HW, EM, STATS>())) 
                 const uint32_t ent = act ? (uint32_t)defl[idx] : 0u;
                 const uint32_t o = ent & 63u, jj = ent >> 6;
                 const uint32_t so = (uint32_t)off0s[o] + jj;  // the window's slot position
+                // local mode: the first base of lane o's piece (every lane active here: a full-wave shuffle)
+                const uint64_t tao = MODE == KM_LOCAL ? (uint64_t)__shfl((long long)ta, (int)o) : 0ull;
                 uint64_t ra[HW];
                 read_words(o, so, ra);
                 const uint64_t h = ax_hash<HW>(ra, k);
@@ -862,7 +878,7 @@ __global__ __launch_bounds__(AX_THREADS, (ax_min_waves<MODE, HW, EM, STATS>())) 
                 }
                 if (found && cl == AX_OWN) {
                     double wgt = 0.0;
-                    if (MODE == KM_LOCAL) wgt = weight(wbase + rbase[o] + jj, chg_zero(o, so + 1u, k - 1u));
+                    if (MODE == KM_LOCAL) wgt = weight(tao + jj, chg_zero(o, so + 1u, k - 1u));
                     add_count(pg, 1u, wgt);
                     const int32_t old = atomicCAS(&ambf[o], -1, (int32_t)pg);
                     if (old != -1 && old != (int32_t)pg) ambd[o] = 1;
@@ -878,6 +894,7 @@ __global__ __launch_bounds__(AX_THREADS, (ax_min_waves<MODE, HW, EM, STATS>())) 
             hasdef = false;
             if (lane == 0) defn[0] = defn[1] = 0u;
             wave_sync();
+            if (STATS) c_p2 += clock64() - c_s;
             continue;
         }
         // lanes that can start a piece now: idle, no deferred windows pending, and a next piece of their unit or
@@ -937,7 +954,6 @@ __global__ __launch_bounds__(AX_THREADS, (ax_min_waves<MODE, HW, EM, STATS>())) 
                 off0 = noff0;
                 ta = a;
                 off0s[lane] = (uint8_t)noff0;
-                if (MODE == KM_LOCAL) rbase[lane] = (uint32_t)(a - wbase);
                 if (STATS) {
                     s_ch += nch;
                     s_seg += 1u;
@@ -1101,6 +1117,7 @@ __global__ __launch_bounds__(AX_THREADS, (ax_min_waves<MODE, HW, EM, STATS>())) 
             // the slots' code words were fenced after the decode (phase 2 reads other lanes' slots); the valid-window
             // bits are read by their own lane only
             if (SPEQ_AX_REFILL_SYNC) wave_sync();
+            if (STATS) c_ref += clock64() - c_s;
             continue;  // re-evaluate (lanes whose piece has no window are idle again)
         }
         if (busy == 0) continue;  // blocked lanes only: phase 2 runs next time round
@@ -1432,11 +1449,12 @@ __global__ __launch_bounds__(AX_THREADS, (ax_min_waves<MODE, HW, EM, STATS>())) 
                     }
                     wave_sync();
                     for (uint32_t b0 = 0; b0 < tot; b0 += 64u) {
+                        // the entry's lane o and the first base of o's piece (a full-wave shuffle, before the branch)
+                        const uint32_t en = wl[min(b0 + lane, AX_WL - 1u)];
+                        const uint64_t qo = (uint64_t)__shfl((long long)ta, (int)(en & 63u));
                         if (b0 + lane < tot) {
-                            const uint32_t en = wl[b0 + lane];
                             const uint32_t o = en & 63u, meta = wlm[o];
                             const uint32_t jb = (meta >> 16) + 8u * ((en >> 6) & 31u);
-                            const uint64_t qo = wbase + rbase[o];
                             double s = 0.0;
                             if (k >= 8u) {
                                 s = weight8(qo + jb, en >> 11);
@@ -1454,7 +1472,12 @@ __global__ __launch_bounds__(AX_THREADS, (ax_min_waves<MODE, HW, EM, STATS>())) 
                 }
             }
         }
+        if (STATS) {
+            if (run_phase) c_rn += clock64() - c_s;
+            else c_lk += clock64() - c_s;
+        }
     }
+    const uint64_t c_tot = STATS ? clock64() - c_t0 : 0ull;
     if (has_unit && ad) ++amb;  // the wave's last units
 
     // wave sums of the window and ambiguity counters through two LDS words (no shuffle address registers)
@@ -1472,8 +1495,10 @@ __global__ __launch_bounds__(AX_THREADS, (ax_min_waves<MODE, HW, EM, STATS>())) 
         if (asum) atomicAdd(&out_a[1], asum);
     }
     if (STATS) {
-        const uint32_t sv[AXS_N] = {s_iter, s_lk, s_rn, s_lkw, s_rnw, s_rwin, s_def, s_fp, s_p2, s_p2v, s_ch, s_seg,
-                                    s_qb, s_tal, s_rg, s_spl, s_b4, s_b16, s_b32, s_b64};
+        const uint64_t sv[AXS_N] = {s_iter, s_lk, s_rn, s_lkw, s_rnw, s_rwin, s_def, s_fp, s_p2, s_p2v, s_ch, s_seg,
+                                    s_qb, s_tal, s_rg, s_spl, s_b4, s_b16, s_b32, s_b64,
+                                    lane == 0 ? c_ref : 0ull, lane == 0 ? c_lk : 0ull, lane == 0 ? c_rn : 0ull,
+                                    lane == 0 ? c_p2 : 0ull, lane == 0 ? c_tot : 0ull};
 #pragma unroll
         for (uint32_t i = 0; i < AXS_N; ++i)
             if (sv[i]) atomicAdd(&A.stats[i], (unsigned long long)sv[i]);
@@ -1563,8 +1588,8 @@ AxTable build_ax(speq_device_index* d, uint32_t k) {
     const uint64_t gran_bytes = n_gran * 16;
     size_t free_b = 0, total_b = 0;
     HIP_OK(hipMemGetInfo(&free_b, &total_b));
-    // gran, codes, mlo, mhi, owner, text2 + tbad, table + filter (bounds)
-    const uint64_t need = gran_bytes + n + (n + 64) * 4 * 3 + nw64 * 24 + n * 12;
+    // gran, codes, owner, text2 + tbad, table + filter (bounds); the EM-only mlo / mhi come later (ensure_ax_em)
+    const uint64_t need = gran_bytes + n + (n + 64) * 4 + nw64 * 24 + n * 12;
     if (need > free_b / 10 * 9) {
         ax.transient = true;
         return ax;
@@ -1598,8 +1623,6 @@ AxTable build_ax(speq_device_index* d, uint32_t k) {
             HIP_OK(hipGetLastError());
         }
         alloc(&ax.gran, gran_bytes);
-        alloc(reinterpret_cast<void**>(&ax.mlo), (n + 64) * 4);
-        alloc(reinterpret_cast<void**>(&ax.mhi), (n + 64) * 4);
         HIP_OK(hipMalloc(&owner, (n + 1) * 4));
         HIP_OK(hipMalloc(&codes, n + 64));
         HIP_OK(hipMalloc(&d_cnt, 8));
@@ -1608,7 +1631,7 @@ AxTable build_ax(speq_device_index* d, uint32_t k) {
         const DevView v = search_view(d, k);
         const uint32_t grid = (uint32_t)std::min<uint64_t>((n + 255) / 256, 16384);
         hipLaunchKernelGGL(k_ax_classify, dim3(grid), dim3(256), 0, d->stream, v, d->d_text, d->d_tbad, n, k, codes,
-                           ax.mlo, ax.mhi, owner, d_cnt);
+                           owner, d_cnt);
         HIP_OK(hipGetLastError());
         const uint32_t pgrid = (uint32_t)std::min<uint64_t>((n_gran + 255) / 256, 16384);
         hipLaunchKernelGGL(k_ax_pack, dim3(pgrid), dim3(256), 0, d->stream, d->d_text2, 2 * nw64, codes, n,
@@ -1636,7 +1659,7 @@ AxTable build_ax(speq_device_index* d, uint32_t k) {
         HIP_OK(hipGetLastError());
         HIP_OK(hipStreamSynchronize(d->stream));
         ax.gran_bytes = gran_bytes;
-        ax.bytes = ax.nb * 64 + ax.nf * 8 + gran_bytes + (n + 64) * 8;
+        ax.bytes = ax.nb * 64 + ax.nf * 8 + gran_bytes;
         ax.ok = true;
     } catch (...) {
         cleanup();
@@ -1661,20 +1684,53 @@ const AxTable* ensure_ax(speq_device_index* d, uint32_t k) {
     return it->second.ok ? &it->second : nullptr;
 }
 
+// The EM-only arrays of table ax (k): allocated and filled on the first EM scan of k (8 B per text position: 1.6 GB
+// at config 5, which plain scans never read). Returns false when they do not fit the free HBM.
+static bool ensure_ax_em(speq_device_index* d, AxTable* ax, uint32_t k) {
+    std::lock_guard<std::mutex> lk(d->ax_mu);
+    if (ax->mlo) return true;
+    DeviceGuard g(d->device);
+    const uint64_t n = d->view.n;
+    size_t free_b = 0, total_b = 0;
+    HIP_OK(hipMemGetInfo(&free_b, &total_b));
+    if ((n + 64) * 8 > free_b / 10 * 9) return false;
+    uint32_t* mlo = nullptr;
+    uint32_t* mhi = nullptr;
+    HIP_OK(hipMalloc(&mlo, (n + 64) * 4));
+    if (hipMalloc(&mhi, (n + 64) * 4) != hipSuccess) {
+        (void)hipFree(mlo);
+        throw DeviceError("ensure_ax_em: hipMalloc failed");
+    }
+    const DevView v = search_view(d, k);
+    const uint32_t grid = (uint32_t)std::min<uint64_t>((n + 255) / 256, 16384);
+    hipLaunchKernelGGL(k_ax_em_intervals, dim3(grid), dim3(256), 0, d->stream, v, d->d_text,
+                       reinterpret_cast<const u32x4*>(ax->gran), n, k, mlo, mhi);
+    HIP_OK(hipGetLastError());
+    HIP_OK(hipStreamSynchronize(d->stream));
+    d->track(mlo);
+    d->track(mhi);
+    ax->mhi = mhi;
+    ax->mlo = mlo;  // last: the unlocked check in launch_ax reads it
+    ax->bytes += (n + 64) * 8;
+    return true;
+}
+
 // Launches k_scan_ax for a read scan (mode 0 global, 1 local) when replica d has (or can build) the structures of
-// src.k; returns false when the caller must use another kernel. With d->ax_stats set, the diagnostic instantiation
-// also adds its work counters there.
+// src.k; returns false when the caller must use another kernel. With src.ax_stats set (speq_scan_reads_device_stats:
+// a per-call buffer, so concurrent ordinary scans of the replica never see it), the diagnostic instantiation also adds
+// its work counters there.
 bool launch_ax(speq_device_index* d, int mode, bool paired, const UnitSrc& src, hipStream_t st, unsigned long long* a,
                double* w) {
-    const AxTable* ax = ensure_ax(d, src.k);
+    AxTable* ax = const_cast<AxTable*>(ensure_ax(d, src.k));
     if (!ax) return false;
+    if (src.em_mult != nullptr && !ensure_ax_em(d, ax, src.k)) return false;  // EM: the other kernels take it
     AxView A;
     A.gran = reinterpret_cast<const u32x4*>(ax->gran);
     A.mlo = ax->mlo;
     A.mhi = ax->mhi;
     A.atab = reinterpret_cast<const unsigned long long*>(ax->atab);
     A.filt = reinterpret_cast<const unsigned long long*>(ax->filt);
-    A.stats = d->ax_stats;
+    A.stats = src.ax_stats;
     A.nb = ax->nb;
     A.nf = ax->nf;
     A.n = d->view.n;

@@ -14,6 +14,7 @@
 // or Python process never maps it (linking it cost every process start the load and registration of its code).
 #include <arpa/inet.h>
 #include <dlfcn.h>
+#include <fcntl.h>
 #include <hip/hip_runtime.h>
 #include <netinet/in.h>
 #include <netinet/tcp.h>
@@ -224,14 +225,17 @@ int speq_comm_connect(int nranks, int rank, int device, const char* rendezvous_p
             ::getsockname(ls, reinterpret_cast<sockaddr*>(&addr), &alen);
             const uint64_t nonce = std::random_device{}() ^ ((uint64_t)std::random_device{}() << 32) ^
                                    (uint64_t)std::chrono::steady_clock::now().time_since_epoch().count();
-            {  // publish {magic, nonce, port} atomically
+            {  // publish {magic, nonce, port} atomically, readable by this user only (the nonce is the credential)
                 const std::string tmp = path + ".tmp." + std::to_string((long)::getpid());
-                std::ofstream os(tmp, std::ios::binary | std::ios::trunc);
+                (void)::unlink(tmp.c_str());
+                const int tfd = ::open(tmp.c_str(), O_WRONLY | O_CREAT | O_EXCL | O_CLOEXEC, 0600);
                 const uint64_t rec[3] = {RDZV_MAGIC, nonce, (uint64_t)ntohs(addr.sin_port)};
-                os.write(reinterpret_cast<const char*>(rec), sizeof(rec));
-                os.close();
-                if (!os || std::rename(tmp.c_str(), path.c_str()) != 0)
+                bool ok_w = tfd >= 0 && ::write(tfd, rec, sizeof(rec)) == (ssize_t)sizeof(rec);
+                if (tfd >= 0) ok_w = (::close(tfd) == 0) && ok_w;
+                if (!ok_w || std::rename(tmp.c_str(), path.c_str()) != 0) {
+                    (void)::unlink(tmp.c_str());
                     throw speq::DeviceError("speq_comm_connect: cannot write the rendezvous file " + path);
+                }
             }
             std::vector<std::string> buses(nranks);
             buses[0] = my_bus;
@@ -307,6 +311,12 @@ int speq_comm_connect(int nranks, int rank, int device, const char* rendezvous_p
                     continue;
                 }
                 try {
+                    // rank 0's reply must arrive before the deadline too (a listener that never answers)
+                    const auto left = std::chrono::duration_cast<std::chrono::microseconds>(
+                        deadline - std::chrono::steady_clock::now()).count();
+                    timeval tv{(time_t)(std::max<long long>(left, 1000) / 1000000),
+                               (suseconds_t)(std::max<long long>(left, 1000) % 1000000)};
+                    ::setsockopt(fd, SOL_SOCKET, SO_RCVTIMEO, &tv, sizeof(tv));
                     send_u64(fd, HELLO_MAGIC);
                     send_u64(fd, rec[1]);
                     send_u64(fd, (uint64_t)rank);
@@ -315,6 +325,8 @@ int speq_comm_connect(int nranks, int rank, int device, const char* rendezvous_p
                     set_nodelay(fd);
                     chosen = (int)recv_u64(fd);  // a listener of another run closes on our nonce: retry
                     recv_all(fd, uid, sizeof(uid));
+                    timeval none{0, 0};
+                    ::setsockopt(fd, SOL_SOCKET, SO_RCVTIMEO, &none, sizeof(none));
                 } catch (const std::exception&) {
                     ::close(fd);
                     std::this_thread::sleep_for(std::chrono::milliseconds(50));
@@ -471,8 +483,11 @@ int speq_em_allreduce(speq_em* em, void* comm, void* stream) {
                 send_u64(fd, v.size());
                 if (!v.empty()) send_all(fd, v.data(), v.size() * 4);
             };
-            auto recv_vec = [&](int fd) {
-                std::vector<uint32_t> v(recv_u64(fd));
+            auto recv_vec = [&](int fd) {  // {position, multiplicity, end} triples, at most one per position
+                const uint64_t len = recv_u64(fd);
+                if (len % 3 != 0 || len > 3 * em->n)
+                    throw speq::DeviceError("speq_em_allreduce: a peer sent a malformed histogram length");
+                std::vector<uint32_t> v(len);
                 if (!v.empty()) recv_all(fd, v.data(), v.size() * 4);
                 return v;
             };

@@ -16,8 +16,8 @@ namespace speq {
 // Per-k structures of the anchor-and-extend scan (ax_scan.hip).
 struct AxTable {
     void* gran = nullptr;      // per 32 text positions {2-bit text, class plane 0, class plane 1} (see ax_scan.hip)
-    uint32_t* mlo = nullptr;   // SA interval start of the multi-group k-mer at a text position (EM)
-    uint32_t* mhi = nullptr;   // SA interval end of each multi-group k-mer, indexed by its interval start (EM)
+    uint32_t* mlo = nullptr;   // SA interval start of the multi-group k-mer at a text position (EM scans only: built
+    uint32_t* mhi = nullptr;   // on the first EM scan of k, ensure_ax_em) / its end, indexed by its interval start
     void* atab = nullptr;      // anchor table: 64-B buckets of 8 {representative position, fingerprint, group} slots
     void* filt = nullptr;      // blocked Bloom filter of the distinct k-mers (one 64-bit word per k-mer, 3 bits)
     uint64_t nb = 0;           // buckets
@@ -96,7 +96,6 @@ struct speq_device_index {
     uint32_t blocks_per_cu_ax = 0;  // tuning "blocks_per_cu_ax" (0: as many as registers/LDS allow)
     std::mutex ax_mu;
     std::map<uint32_t, speq::AxTable> axtabs;
-    unsigned long long* ax_stats = nullptr;  // diagnostic: set for one launch by speq_scan_reads_device_stats
     std::mutex events_mu;  // launches may come from several host threads (pipelines, concurrent scans)
     std::vector<std::pair<hipEvent_t, hipEvent_t>> events;
     double timed_ms = 0.0;

@@ -68,6 +68,7 @@ struct UnitSrc {
     uint32_t k;
     uint32_t cutoff;
     uint32_t buf_bytes;       // per-wave staging buffer (bases)
+    unsigned long long* ax_stats;  // diagnostic (speq_scan_reads_device_stats): k_scan_ax's work counters, else null
 };
 
 // Per-wave LDS: bases [buf_bytes] | qualities [buf_bytes] (local mode) | bad-mask words | N-mask words |

@@ -1458,13 +1458,15 @@ void launch_t(const speq_device_index* d, const UnitSrc& src, uint32_t grid, siz
     else launch_v<MODE, PAIRED, LDS, false>(d, v, src, grid, lds, st, a, b, w);
 }
 
-void launch_scan(speq_device_index* d, int mode, bool paired, const UnitSrc& src, uint64_t work_units,
-                 hipStream_t st, unsigned long long* a, unsigned long long* b, double* w) {
+// returns the kernel it launched (speq_device_get_tuning "last_kernel" codes: 0 LF steps, 1/2 k-mer table, 3 ax)
+int launch_scan(speq_device_index* d, int mode, bool paired, const UnitSrc& src, uint64_t work_units,
+                hipStream_t st, unsigned long long* a, unsigned long long* b, double* w) {
     // read scans: the anchor-and-extend kernel when the replica has (or can build) its structures for k (ax_scan.hip)
     if (mode != KM_REF && speq::launch_ax(d, mode, paired, src, st, a, w)) {
         d->last_kernel = 3;
-        return;
+        return 3;
     }
+    if (src.ax_stats) return -1;  // the diagnostic twin exists for k_scan_ax only: launch nothing
     const speq_device_index::KmerTable* kt = ensure_ktab(d, src.k);
     const bool lds_hist = d->G <= LDS_HIST_MAX_G;
     const uint32_t hist_words = lds_hist ? ((mode == KM_GLOBAL) ? d->G : 2u * d->G) : 0u;
@@ -1492,6 +1494,7 @@ void launch_scan(speq_device_index* d, int mode, bool paired, const UnitSrc& src
     else { if (paired) SPEQ_DISPATCH(KM_LOCAL, true); else SPEQ_DISPATCH(KM_LOCAL, false); }
 #undef SPEQ_DISPATCH
     HIP_OK(hipGetLastError());
+    return kt ? ((d->ilp_kt <= 2 && d->kt_pipeline) || kt->compact ? 2 : 1) : 0;
 }
 
 }  // namespace
@@ -1501,9 +1504,10 @@ DevView search_view(const speq_device_index* d, uint32_t k) { return scan_view(d
 }  // namespace speq
 
 // ---- scan implementations shared by the plain and the EM-histogram entry points ----
-static void scan_device_impl(speq_device_index* d, const uint8_t* d_seq, const uint8_t* d_qual, const uint64_t* d_offsets,
+// returns the kernel it launched (launch_scan), -1 with ax_stats when k_scan_ax cannot take the scan (nothing launched)
+static int scan_device_impl(speq_device_index* d, const uint8_t* d_seq, const uint8_t* d_qual, const uint64_t* d_offsets,
                       uint64_t n_reads, const speq_scan_params* p, uint64_t* d_counts, double* d_weights,
-                      uint32_t* em_mult, uint32_t* em_hi, hipStream_t st) {
+                      uint32_t* em_mult, uint32_t* em_hi, hipStream_t st, unsigned long long* ax_stats = nullptr) {
     if (!d || !p || !d_counts) throw std::invalid_argument("speq_scan_reads_device: null argument");
     if (p->k < 1 || p->k > MAX_K) throw std::invalid_argument("speq_scan_reads_device: k must be in [1, 4096]");
     if (p->mode != SPEQ_MODE_GLOBAL && p->mode != SPEQ_MODE_LOCAL)
@@ -1511,7 +1515,7 @@ static void scan_device_impl(speq_device_index* d, const uint8_t* d_seq, const u
     if (p->mode == SPEQ_MODE_LOCAL && !d_weights)
         throw std::invalid_argument("speq_scan_reads_device: local mode needs a weights buffer");
     if (p->paired && (n_reads & 1)) throw std::invalid_argument("speq_scan_reads_device: paired scan needs an even record count");
-    if (n_reads == 0) return;
+    if (n_reads == 0) return ax_stats ? -1 : 0;
     if (!d_seq || !d_qual || !d_offsets) throw std::invalid_argument("speq_scan_reads_device: null read buffer");
     DeviceGuard g(d->device);
     UnitSrc src{};
@@ -1526,6 +1530,7 @@ static void scan_device_impl(speq_device_index* d, const uint8_t* d_seq, const u
     src.k = p->k;
     src.cutoff = p->phred_cutoff;
     src.buf_bytes = staging_bytes(p->k, std::max({d->ilp, d->ilp_local, d->ilp_kt ? d->ilp_kt : 2u}));
+    src.ax_stats = ax_stats;
     const int mode = p->mode == SPEQ_MODE_LOCAL ? KM_LOCAL : KM_GLOBAL;
     hipEvent_t e0 = nullptr, e1 = nullptr;
     if (d->timing) {
@@ -1533,13 +1538,14 @@ static void scan_device_impl(speq_device_index* d, const uint8_t* d_seq, const u
         HIP_OK(hipEventCreate(&e1));
         HIP_OK(hipEventRecord(e0, st));
     }
-    launch_scan(d, mode, p->paired != 0, src, p->paired ? n_reads / 2 : n_reads, st,
-                reinterpret_cast<unsigned long long*>(d_counts), nullptr, d_weights);
+    const int kernel = launch_scan(d, mode, p->paired != 0, src, p->paired ? n_reads / 2 : n_reads, st,
+                                   reinterpret_cast<unsigned long long*>(d_counts), nullptr, d_weights);
     if (d->timing) {
         HIP_OK(hipEventRecord(e1, st));
         std::lock_guard<std::mutex> lk(d->events_mu);
         d->events.emplace_back(e0, e1);
     }
+    return kernel;
 }
 
 
@@ -1690,24 +1696,21 @@ int speq_scan_reads_device_stats(speq_device_index* d, const uint8_t* d_seq, con
     return speq::guarded([&] {
         if (!d || !stats) throw std::invalid_argument("speq_scan_reads_device_stats: null argument");
         DeviceGuard g(d->device);
-        static std::mutex mu;  // one instrumented launch at a time (the replica's ax_stats is a single slot)
-        std::lock_guard<std::mutex> lk(mu);
+        // the counters' buffer travels with this launch only (UnitSrc::ax_stats), so ordinary scans of the same
+        // replica from other threads never run the instrumented kernel
         unsigned long long* ds = nullptr;
         HIP_OK(hipMalloc(&ds, SPEQ_AX_STATS_N * 8));
         struct Release {
-            speq_device_index* d;
             unsigned long long*& p;
             ~Release() {
-                d->ax_stats = nullptr;
                 if (p) (void)hipFree(p);
             }
-        } release{d, ds};
+        } release{ds};
         HIP_OK(hipMemsetAsync(ds, 0, SPEQ_AX_STATS_N * 8, d->stream));
         HIP_OK(hipStreamSynchronize(d->stream));
-        d->ax_stats = ds;
-        scan_device_impl(d, d_seq, d_qual, d_offsets, n_reads, p, d_counts, d_weights, nullptr, nullptr, d->stream);
-        d->ax_stats = nullptr;
-        if (d->last_kernel != 3)
+        const int kernel =
+            scan_device_impl(d, d_seq, d_qual, d_offsets, n_reads, p, d_counts, d_weights, nullptr, nullptr, d->stream, ds);
+        if (kernel != 3)
             throw std::invalid_argument("speq_scan_reads_device_stats: the scan did not use the anchor-and-extend kernel");
         HIP_OK(hipStreamSynchronize(d->stream));
         HIP_OK(hipMemcpy(stats, ds, SPEQ_AX_STATS_N * 8, hipMemcpyDeviceToHost));

@@ -1,0 +1,94 @@
+"""CPU: bench.py's stdout line stays driver-parseable (round 3's 22.8 KB line was not parsed: BENCH_r03 `parsed: null`).
+
+The line builder runs on canned results as large as the real ones (20-entry work counters, 200-entry U and W vectors
+per line, ten secondary lines); the line must stay under 8 KB and carry the BASELINE keys, `roofline` and
+`cpu_baseline`, while the vectors and counters go to the detail file only."""
+import json
+import os
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import bench  # noqa: E402
+
+
+def _line(G=200, local=True):
+    ax = {k: 123456789 for k in ("wave_iters", "lookup_lanes", "run_lanes", "lookup_waves", "run_waves",
+                                 "run_windows", "deferred", "filter_pass", "p2_probes", "p2_verify", "chunks",
+                                 "segments", "qual_bytes", "run_tallied", "run_granules", "refills", "busy_1_4",
+                                 "busy_5_16", "busy_17_32", "busy_33_64")}
+    rf = bench.roofline_of("no-such-key", 0.25e-3, 7.6e8, 3.08e8, 21, 130_000_000)
+    rf["kernel"] = bench.KERNEL_NAME[3]
+    cpu = {"value": 1.1e7, "unit": "k-mers/s", "cores": 16, "kind": "port", "checked": True,
+           "sample": "x" * 180, "host": {"cpu_model": "AMD EPYC 9575F 64-Core Processor", "rule": "y" * 80},
+           "hash_port": {"value": 3.3e8, "sample": "z" * 150}, "label_run_port": {"value": 1e9, "sample": "w" * 150}}
+    return {"value": 5.1e11, "ms_per_step": 0.2561234, "avg_kernel_ms": 0.2481234, "k": 21, "mode": "local",
+            "workload": "w" * 160, "roofline": rf, "cpu_baseline": cpu,
+            "check": {"T": 130000000, "ambiguous": 3633, "U_sha1": "0123456789abcdef", "W_sum": 1.23456789e8},
+            "detail": {"U": [10 ** 8] * G, "W": [1.234567891234e7] * G if local else None, "ax_work": ax}}
+
+
+def test_compact_line_is_small_and_complete():
+    head = _line()
+    lines = {name: _line() for name in ("local_mode", "k31", "cli_e2e", "k70_reference_defaults", "k70_err05",
+                                        "fastq_e2e", "local_varq", "cfg5_paired", "cfg5_paired_local", "extra")}
+    meta = {"metric": "k-mers scanned/sec (whole node) at k=21, 150 bp reads", "n_gpus": 8, "steps": 20,
+            "warmup": 2, "detail_file": "profiles/r04/bench_detail_n8.json",
+            "config": {"workload": "v" * 160, "k": 21, "reads_per_gpu": 1000000, "paired": False, "mode": "global",
+                       "parallelism": "dp8 (reads sharded, index replicated)", "collective": "c" * 100,
+                       "index_build_s": 0.2, "index_builder": "gpu", "fm_text_len": 1000021,
+                       "kmer_table": {"bytes": 15733384, "build_s": 0.004}}}
+    out = bench.compact_result(head, lines, meta)
+    s = json.dumps(out)
+    assert len(s) < bench.LINE_LIMIT, len(s)
+    for key in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better",
+                "scaling", "vs_baseline", "dtype", "data", "config"):
+        assert key in out
+    assert out["roofline"]["frac"] is not None and out["roofline"]["bound"] == "hbm"
+    assert {"achieved", "peak", "unit", "frac", "traffic", "avg_kernel_ms", "traffic_source"} <= set(out["roofline"])
+    assert out["cpu_baseline"]["cores"] == 16 and out["cpu_baseline"]["kind"] == "port"
+    assert "ax_work" not in s and "hash_port" not in s  # detail only
+    for r in out["lines"].values():
+        assert {"value", "avg_kernel_ms", "frac", "traffic_frac", "check"} <= set(r)
+        assert "U" not in r["check"]
+
+
+def test_roofline_uses_calibrated_fabric_bytes(tmp_path, monkeypatch):
+    prof = tmp_path / "profiles"
+    prof.mkdir()
+    key = bench.workload_key(2, 21, "global", 1_000_000, "ax")
+    assert key == "cfg2_k21_global_reads1000000_ax"
+    assert bench.workload_key(2, 70, "local", 1_000_000, "ax", err=0.005) == "cfg2_k70_local_reads1000000_ax_err0.005"
+    (prof / "traffic.json").write_text(json.dumps({
+        key: {"fabric_bytes_per_launch": 4.0e8, "source": "r04/pmc_x.json", "l2_hit_rate": 0.6},
+        "old": {"hbm_bytes_per_launch": 2.5e8, "source": "r03/pmc_y.json"}}))
+    monkeypatch.setattr(bench, "ROOT", str(tmp_path))
+    rf = bench.roofline_of(key, 0.25e-3, 7.6e8, 3.08e8, 21, 130_000_000)
+    assert rf["frac_basis"] == "fabric" and rf["traffic"] == 4.0e8
+    assert rf["frac"] == pytest.approx(4.0e8 / 0.25e-3 / 1e9 / 8000.0)
+    assert rf["traffic_frac"] == pytest.approx(rf["frac"])
+    assert rf["l2_request_frac"] == pytest.approx(7.6e8 / 0.25e-3 / 1e9 / 8000.0)
+    # an uncalibrated (pre-round-4) entry is not used: the compulsory read bytes are the basis then
+    rf2 = bench.roofline_of("old", 0.25e-3, None, 3.08e8, 21, 130_000_000)
+    assert rf2["frac_basis"] == "compulsory" and rf2["traffic"] is None
+    assert rf2["frac"] == pytest.approx(3.08e8 / 0.25e-3 / 1e9 / 8000.0)
+
+
+def test_write_fastq_round_trip(tmp_path):
+    import numpy as np
+
+    from speq_amd import synth
+    ref = synth.make_reference(2, 1, 2000)
+    reads = synth.make_reads(ref, 2500)
+    p = tmp_path / "r.fq"
+    n = bench.write_fastq(str(p), reads, chunk=1000)
+    data = p.read_bytes()
+    assert len(data) == n
+    lines = data.split(b"\n")
+    assert lines[0] == b"@r000000000" and lines[4 * 2499] == b"@r000002499"
+    seq = b"".join(lines[1::4][:2500])
+    assert seq == reads.seq.tobytes()
+    assert b"".join(lines[3::4][:2500]) == reads.qual.tobytes()
+    assert np.all(np.diff(reads.offsets) == 150)

@@ -231,3 +231,33 @@ def test_device_buffers_and_grid_knobs(small):
         torch.cuda.synchronize()
         c = cnt.cpu().numpy()
         assert (int(c[0]), int(c[1]), c[2:].tolist()) == (T, amb, U.tolist()), (grid, bpc)
+
+
+@pytest.mark.parametrize("k", [12, 21, 31, 70])
+@pytest.mark.parametrize("paired", [False, True])
+def test_varying_quality_weights_within_the_documented_bound(k, paired):
+    """Phred-weighted scans of reads whose qualities vary base by base (the anchor kernel's non-uniform path: k
+    reciprocal products, or the shared-middle 8-window blocks) against the reference's left-to-right divisions
+    (fm_scanner.cpp:454, restated in oracle/kmer_oracle.c) at the bound DESIGN.md §4e documents rather than 1e-10:
+    each window within 3k·2^-53 (relative), and each group's sum of n_g windows within another (n_g + 1)·2^-53 for
+    the different summation order, so |W_gpu - W_ref| <= (3k + 2 n_g + 2)·2^-53 · W_ref. Few hundred reads keep n_g
+    small enough for the bound to see a single mis-weighted window (one wrong quality byte moves W by ~1e-5)."""
+    ref = synth.make_reference(24, 1, 4_000)
+    idx = FmIndex.build(ref.records, ref.groups, 24, prefix_q=8, pair_steps=True, triple_steps=True)
+    dev = DeviceIndex(idx)
+    orc = Oracle(ref.records, ref.groups, 24, k)
+    reads = synth.make_reads(ref, 200, err_rate=0.002, paired=paired)
+    rng = np.random.default_rng(k + 7 * paired)
+    # qualities 31..41 changing at almost every base, 1 % at Q20 (below the cutoff 30: they split runs)
+    q = rng.integers(31, 42, size=len(reads.qual)).astype(np.uint8)
+    q[rng.random(len(q)) < 0.01] = 20
+    qual = (q + 33).astype(np.uint8)
+    got = dev.scan(reads.seq.tobytes(), qual.tobytes(), reads.offsets, k=k, paired=paired, local=True)
+    T, amb, U, W = orc.scan(reads.seq, qual, reads.offsets, paired=paired, local=True)
+    assert (got.total, got.ambiguous, got.unique.tolist()) == (T, amb, U.tolist())
+    assert dev.tuning("last_kernel") == 3
+    u = 2.0 ** -53
+    for g in range(24):
+        tol = (3 * k + 2 * int(U[g]) + 2) * u * W[g]
+        assert abs(got.weights[g] - W[g]) <= tol, (g, got.weights[g], W[g], tol)
+    assert int(U.sum()) > 2000  # enough windows counted for the bound to mean something

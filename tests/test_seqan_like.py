@@ -81,3 +81,23 @@ def test_label_run_cpu_path_equals_hash_oracle(steps, paired):
             a = fc.scan(reads.seq, reads.qual, reads.offsets, k=k, paired=paired, threads=4)
             b = orc.scan(reads.seq, reads.qual, reads.offsets, paired=paired, threads=4)
             assert a[:2] == b[:2] and a[2].tolist() == b[2].tolist(), (q, k)
+
+
+def test_seqan_like_from_product_suffix_array_is_the_same_structure():
+    """bench.py's config-5 CPU baseline hands the product index's suffix array to the stand-in (its own doubling sort
+    takes minutes at 200 M symbols): a suffix array is unique, so the structure — SA samples and scan results — must
+    be identical to the stand-in's own build."""
+    from speq_amd import FmIndex
+    ref = synth.make_reference(4, 2, 3000, ref_n_rate=0.002)
+    own = SeqanLike(ref.records, ref.groups, 4)
+    idx = FmIndex.build(ref.records, ref.groups, 4, prefix_q=4)
+    given = SeqanLike(ref.records, ref.groups, 4, sa=idx.array("sa", np.uint32))
+    assert own.n == given.n
+    assert all(own.sample(j) == given.sample(j) for j in range(own.n // 16 + 1))
+    reads = synth.make_reads(ref, 300, err_rate=0.01, n_rate=0.005, lowq_rate=0.01)
+    for k in (15, 31):
+        a = own.scan(reads.seq, reads.qual, reads.offsets, k=k)
+        b = given.scan(reads.seq, reads.qual, reads.offsets, k=k)
+        assert (a[0], a[1], a[2].tolist()) == (b[0], b[1], b[2].tolist())
+    with pytest.raises(ValueError):
+        SeqanLike(ref.records, ref.groups, 4, sa=idx.array("sa", np.uint32)[:-1])
