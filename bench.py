@@ -631,9 +631,10 @@ def cli_e2e(prep: dict, k: int, check: dict) -> dict:
 
         res["index_s"], _, res["index_phases"] = run(["index", "-r", "refs.fa", "-g", "groups.txt", "-x", "ref",
                                                       "-t", str(threads)])
-        scan = ["scan", "-1", "r1.fq", "-x", "ref", "-k", str(k), "-t", str(threads), "-o", "out.txt"]
-        res["first_scan_s"], _, res["first_scan_phases"] = run(scan)  # + the .dat pass (new index)
-        dt, err, phases = run(scan)  # .dat cached (the reference's steady state: fm_scanner.cpp:79-135)
+        scan = ["scan", "-1", "r1.fq", "-x", "ref", "-k", str(k), "-t", str(threads)]
+        res["first_scan_s"], _, res["first_scan_phases"] = run(scan + ["-o", "out.txt"])  # + the .dat pass (new index)
+        # .dat cached (the reference's steady state: fm_scanner.cpp:79-135); -o must be a new file (arg_parse.cpp:37)
+        dt, err, phases = run(scan + ["-o", "out_cached.txt"])
         tl = [ln for ln in err.splitlines() if ln.count("\t") == 1 and ln.replace("\t", "").isdigit()]
         T, amb = (int(x) for x in tl[0].split("\t"))
         if (T, amb) != (check["T"], check["ambiguous"]):

@@ -44,6 +44,7 @@
 #include <vector>
 
 #include "device_index.hpp"
+#include "fm_index.hpp"
 #include "scan_device.hpp"
 #include "scan_internal.hpp"
 #include "speq_scan.h"
@@ -52,6 +53,12 @@ namespace {
 
 using namespace speq_dev;
 
+#ifndef SPEQ_AX_CUCKOO  // 1: the anchor table is a two-choice cuckoo table of 32-B buckets (4 slots), every key in one
+#define SPEQ_AX_CUCKOO 0  // of its two buckets, both loaded in one round trip; 0 (default): linear probing over 64-B
+#endif                    // buckets (cuckoo loads two lines per lookup: config 5 4.79 vs 3.69 ms, explore_r04)
+#ifndef SPEQ_AX_REP  // which occurrence of a k-mer represents it in the anchor table (A/B knob): 0 the first thread to
+#define SPEQ_AX_REP 2  // claim it, 1 its lowest text position, 2 (default) the median of its SA interval
+#endif
 constexpr uint32_t AX_MAX_K = 128;    // longest k the scan takes (AX_CAP - k + 1 windows per segment)
 constexpr uint32_t AX_CAP = 192;      // bases of a read a lane stages at once (longer reads: segments of AX_CAP bases)
 constexpr uint32_t AX_STREAM = AX_CAP + 16;  // staged bases incl. the 16-B alignment slack before the read
@@ -144,6 +151,11 @@ __device__ __forceinline__ uint64_t ax_hash(const uint64_t (&w)[NW], uint32_t k)
 }
 __host__ __device__ __forceinline__ uint32_t ax_bucket(uint64_t h, uint64_t nb) {
     return (uint32_t)(((h >> 32) * nb) >> 32);
+}
+// the second bucket of the cuckoo table: the hash's low 32 bits, spread by an odd multiplier (the first bucket comes
+// from the high 32 bits, the fingerprint from the low 16)
+__host__ __device__ __forceinline__ uint32_t ax_bucket2(uint64_t h, uint64_t nb) {
+    return (uint32_t)(((uint64_t)((uint32_t)h * 0x9E3779B1u) * nb) >> 32);
 }
 // slot fingerprint: the hash's low 16 bits (the bucket comes from its high 32)
 __host__ __device__ __forceinline__ uint32_t ax_fp(uint64_t h) { return (uint32_t)h & 0xFFFFu; }
@@ -248,9 +260,18 @@ __device__ int ax_search_text(const DevView& I, const Rsrc& R, const uint8_t* __
 
 // Pass A: the class code of the k-mer at every text position (one byte per position, packed into granules by pass
 // B), and one representative position per distinct k-mer (the first to claim owner[lo] of its SA interval).
+//
+// The representative (SPEQ_AX_REP = 2) is the occurrence at the MEDIAN rank of the k-mer's SA interval, SA[(lo + hi -
+// 1) / 2]. Within the interval the suffixes are sorted by the text that follows the k-mer, so occurrences that share
+// their continuation form contiguous groups, and whenever one continuation is shared by more than half of the
+// occurrences, the median lies in it, base after base: the representative follows the consensus of the records that
+// contain the k-mer. A read run from it breaks only where the read's record leaves that consensus (its own SNPs),
+// not wherever an arbitrary representative's record has one — fewer lookups and runs per read (simulated on config 2:
+// 1.99 -> 1.76 runs per read against a uniformly random occurrence, 3.13 for the lowest position; the first
+// claimant of round 3 leaned towards the lowest: config 5 measured 3.6). sa == nullptr: the first claimant.
 __global__ void k_ax_classify(DevView I, const uint8_t* __restrict__ text, const uint64_t* __restrict__ tbad,
                               uint64_t n, uint32_t k, uint8_t* __restrict__ codes, uint32_t* __restrict__ owner,
-                              unsigned long long* __restrict__ n_distinct) {
+                              const uint32_t* __restrict__ sa, unsigned long long* __restrict__ n_distinct) {
     const Rsrc R = make_rsrc(I);
     unsigned long long claimed = 0;
     for (uint64_t pos = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; pos < n;
@@ -274,7 +295,12 @@ __global__ void k_ax_classify(DevView I, const uint8_t* __restrict__ text, const
         const int g = ax_search_text(I, R, text + pos, k, lo, hi);
         // g == -1 cannot happen: the window occurs at pos; g >= 0 is the group of pos's text
         codes[pos] = (uint8_t)(g >= 0 ? AX_OWN : AX_MULTI);
-        if (atomicCAS(&owner[lo], AX_EMPTY, (uint32_t)pos) == AX_EMPTY) ++claimed;
+        if (SPEQ_AX_REP == 1) {
+            if (atomicMin(&owner[lo], (uint32_t)pos) == AX_EMPTY) ++claimed;
+        } else {
+            const uint32_t rp = (SPEQ_AX_REP == 2 && sa != nullptr) ? sa[lo + (hi - lo - 1u) / 2u] : (uint32_t)pos;
+            if (atomicCAS(&owner[lo], AX_EMPTY, rp) == AX_EMPTY) ++claimed;
+        }
     }
     if (claimed) atomicAdd(n_distinct, claimed);
 }
@@ -359,6 +385,58 @@ __global__ void k_ax_insert(const uint32_t* __restrict__ owner, uint64_t n, cons
     }
 }
 
+// Pass C, cuckoo form (SPEQ_AX_CUCKOO): every representative goes into one of its two 32-B buckets (ax_bucket,
+// ax_bucket2; 4 slots each): an empty slot of either, else it takes a slot of the bucket it was not evicted from and
+// carries the slot's previous key on to that key's other bucket (atomicExch: every key is always in the table or
+// carried by exactly one thread). A key is found by loading both buckets, so a lookup is one round trip at any load
+// factor; the table is filled to 85-90 % (8.9-9.4 B per k-mer against 23 B for linear probing at 35 %). A thread
+// that is still carrying a key after max_iter evictions counts a failure: the host rebuilds at a lower load.
+__global__ void k_ax_insert_ck(const uint32_t* __restrict__ owner, uint64_t n, const uint64_t* __restrict__ t2,
+                               uint32_t k, const uint64_t* __restrict__ text_start,
+                               const int32_t* __restrict__ text_group, uint32_t n_texts,
+                               unsigned long long* __restrict__ atab, uint64_t nb, unsigned long long* __restrict__ filt,
+                               uint64_t nf, uint32_t max_iter, unsigned long long* __restrict__ n_fail) {
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+        const uint32_t p = owner[i];
+        if (p == AX_EMPTY) continue;
+        uint64_t w[4];
+        ax_text_words<4>(t2, p, w);
+        uint64_t h = ax_hash<4>(w, k);
+        atomicOr(&filt[ax_fword(h, nf)], (unsigned long long)ax_fbits(h));
+        uint32_t lo = 0, hi = n_texts;  // the last text t with text_start[t] <= p
+        while (hi - lo > 1u) {
+            const uint32_t mid = (lo + hi) / 2u;
+            if (text_start[mid] <= p) lo = mid;
+            else hi = mid;
+        }
+        const uint32_t grp = (uint32_t)text_group[lo] & 0xFFFFu;
+        unsigned long long cur = ((unsigned long long)((ax_fp(h) << 16) | grp) << 32) | p;
+        uint32_t from = AX_EMPTY;  // the bucket the carried key was evicted from
+        bool placed = false;
+        for (uint32_t it = 0; it < max_iter && !placed; ++it) {
+            const uint32_t b1 = ax_bucket(h, nb), b2 = ax_bucket2(h, nb);
+            const uint32_t first = from == b1 ? b2 : b1, second = first == b1 ? b2 : b1;
+            for (uint32_t j = 0; j < 8u && !placed; ++j) {
+                const uint32_t b = j < 4u ? first : second;
+                placed = atomicCAS(&atab[(uint64_t)b * 4u + (j & 3u)], AX_SLOT_EMPTY, cur) == AX_SLOT_EMPTY;
+            }
+            if (placed) break;
+            // both buckets full: take a slot of `first` (not where this key came from) and carry its key
+            const uint32_t sl = (uint32_t)(h >> 20) + it;
+            const unsigned long long old = atomicExch(&atab[(uint64_t)first * 4u + (sl & 3u)], cur);
+            if (old == AX_SLOT_EMPTY) {
+                placed = true;
+                break;
+            }
+            cur = old;
+            from = first;
+            ax_text_words<4>(t2, (uint32_t)old, w);
+            h = ax_hash<4>(w, k);
+        }
+        if (!placed) atomicAdd(n_fail, 1ull);
+    }
+}
+
 // ---------------------------------------------------------------------------------------------------------------
 // The scan
 // ---------------------------------------------------------------------------------------------------------------
@@ -408,6 +486,47 @@ __device__ __forceinline__ uint32_t ax_resolve(const u32x4& v0, const u32x4& v1,
         return 1u;
     }
     return fe < 8u ? 0u : 2u;
+}
+
+// Cuckoo form: the 8 slots of a key's two buckets (v0, v1: the first; v2, v3: the second); the first slot from `s` on
+// whose fingerprint matches (empty slots excluded) gives the candidate (1), none: the key is absent (0).
+__device__ __forceinline__ uint32_t ax_resolve_ck(const u32x4& v0, const u32x4& v1, const u32x4& v2, const u32x4& v3,
+                                                  uint32_t fp, uint32_t s, uint32_t& slot, uint32_t& p, uint32_t& g) {
+    const uint32_t pos[8] = {v0[0], v0[2], v1[0], v1[2], v2[0], v2[2], v3[0], v3[2]};
+    const uint32_t fg[8] = {v0[1], v0[3], v1[1], v1[3], v2[1], v2[3], v3[1], v3[3]};
+    uint32_t mm = 0;
+#pragma unroll
+    for (int t = 0; t < 8; ++t) mm |= ((pos[t] != AX_EMPTY && (fg[t] >> 16) == fp) ? 1u : 0u) << t;
+    mm &= s >= 8u ? 0u : ((0xFFu << s) & 0xFFu);
+    if (mm == 0u) return 0u;
+    const uint32_t fm = (uint32_t)__builtin_ctz(mm);
+    uint32_t pp = pos[0], gg = fg[0];
+#pragma unroll
+    for (int t = 1; t < 8; ++t) {
+        pp = fm == (uint32_t)t ? pos[t] : pp;
+        gg = fm == (uint32_t)t ? fg[t] : gg;
+    }
+    p = pp;
+    g = gg & 0xFFFFu;
+    slot = fm;
+    return 1u;
+}
+
+// Phase-2 probe of the cuckoo table: one round trip (both buckets), the first fingerprint match from slot s.
+__device__ __forceinline__ bool ax_probe_ck(const __amdgpu_buffer_rsrc_t& rs_atab, uint32_t fp, uint32_t b1,
+                                            uint32_t b2, uint32_t& s, uint32_t& p, uint32_t& g, bool active,
+                                            uint32_t& probes) {
+    const uint32_t o1 = active ? b1 * 32u : AX_OOB, o2 = active ? b2 * 32u : AX_OOB;
+    const u32x4 v0 = __builtin_amdgcn_raw_buffer_load_b128(rs_atab, o1, 0, 0);
+    const u32x4 v1 = __builtin_amdgcn_raw_buffer_load_b128(rs_atab, o1 + 16u, 0, 0);
+    const u32x4 v2 = __builtin_amdgcn_raw_buffer_load_b128(rs_atab, o2, 0, 0);
+    const u32x4 v3 = __builtin_amdgcn_raw_buffer_load_b128(rs_atab, o2 + 16u, 0, 0);
+    if (!active) return false;
+    ++probes;
+    uint32_t slot = 0;
+    if (ax_resolve_ck(v0, v1, v2, v3, fp, s, slot, p, g) == 0u) return false;
+    s = slot;
+    return true;
 }
 
 // One probe chain of the anchor table from bucket b, slot s (phase 2): stops at the first fingerprint match (found:
@@ -480,7 +599,10 @@ constexpr uint32_t AX_WPB = SPEQ_AX_WPB, AX_THREADS = 64 * SPEQ_AX_WPB;
 #ifndef SPEQ_AX_MIN_WAVES4  // the same for 33 <= k <= 64
 #define SPEQ_AX_MIN_WAVES4 5
 #endif
-#ifndef SPEQ_AX_MIN_WAVES6  // and 65 <= k <= 128
+#ifndef SPEQ_AX_MIN_WAVES5  // 65 <= k <= 96
+#define SPEQ_AX_MIN_WAVES5 5
+#endif
+#ifndef SPEQ_AX_MIN_WAVES6  // and 97 <= k <= 128
 #define SPEQ_AX_MIN_WAVES6 4  // (at 5: 8-24 B of spills per lane)
 #endif
 #ifndef SPEQ_AX_MIN_WAVES_LOCAL  // local (Phred-weighted) mode, every k: 4 (<= 128 VGPRs, no spills; its LDS fits 4
@@ -515,7 +637,8 @@ constexpr int ax_min_waves() {
     return MODE == KM_LOCAL ? (STATS ? 3 : SPEQ_AX_MIN_WAVES_LOCAL)
                             : ((EM || STATS) ? 4
                                              : (HW >= 4 ? SPEQ_AX_MIN_WAVES6
-                                                        : (HW >= 2 ? SPEQ_AX_MIN_WAVES4 : SPEQ_AX_MIN_WAVES)));
+                                                        : (HW == 3 ? SPEQ_AX_MIN_WAVES5
+                                                                   : (HW >= 2 ? SPEQ_AX_MIN_WAVES4 : SPEQ_AX_MIN_WAVES))));
 }
 
 __device__ __forceinline__ uint32_t alignbit(uint32_t hi, uint32_t lo, uint32_t s) {  // ({hi, lo} >> (s & 31))[31:0]
@@ -525,7 +648,7 @@ __device__ __forceinline__ uint32_t lanes_below(unsigned long long m) {  // set 
     return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
 }
 
-// HW = 2-bit words of one k-mer (its hash): 1 (k <= 32), 2 (k <= 64), 4 (k <= 128); a phase-2 verification loads the
+// HW = 2-bit words of one k-mer (its hash): 1 (k <= 32), 2 (k <= 64), 3 (k <= 96), 4 (k <= 128); a phase-2 verification loads the
 // HW + 1 granules that cover k bases at any offset in the first.
 //
 // Persistent lanes: a wave takes the units (reads, or mate pairs) of its groups of 64 in order; every lane works on
@@ -586,7 +709,8 @@ __global__ __launch_bounds__(AX_THREADS, (ax_min_waves<MODE, HW, EM, STATS>())) 
     const __amdgpu_buffer_rsrc_t rs_gran =
         __builtin_amdgcn_make_buffer_rsrc((void*)A.gran, (short)0, (int)(uint32_t)A.gran_bytes, 0x00020000);
     const __amdgpu_buffer_rsrc_t rs_atab =
-        __builtin_amdgcn_make_buffer_rsrc((void*)A.atab, (short)0, (int)(uint32_t)(A.nb * 64u), 0x00020000);
+        __builtin_amdgcn_make_buffer_rsrc((void*)A.atab, (short)0, (int)(uint32_t)(A.nb * (SPEQ_AX_CUCKOO ? 32u : 64u)),
+                                          0x00020000);
     const __amdgpu_buffer_rsrc_t rs_filt =
         __builtin_amdgcn_make_buffer_rsrc((void*)A.filt, (short)0, (int)(uint32_t)(A.nf * 8u), 0x00020000);
     const uint64_t NWV = (uint64_t)gridDim.x * AX_WPB;
@@ -627,8 +751,18 @@ __global__ __launch_bounds__(AX_THREADS, (ax_min_waves<MODE, HW, EM, STATS>())) 
         return u64of(alignbit(w1, w0, sh), alignbit(w2, w1, sh));
     };
     auto read_words = [&](uint32_t o, uint32_t pos, uint64_t(&w)[HW]) {  // HW code words of slot o at pos
+        if (HW <= 2) {  // (HW = 2: the shared reads below hold more registers at once and spill)
 #pragma unroll
-        for (int i = 0; i < HW; ++i) w[i] = slot64(o, pos + 32u * (uint32_t)i);
+            for (int i = 0; i < HW; ++i) w[i] = slot64(o, pos + 32u * (uint32_t)i);
+            return;
+        }
+        // the 2 HW + 1 slot words that cover them, each read once (consecutive 64-bit words share a slot word)
+        const uint32_t d = pos >> 4, sh = 2u * (pos & 15u);
+        uint32_t c[2 * HW + 1];
+#pragma unroll
+        for (int i = 0; i <= 2 * HW; ++i) c[i] = d + (uint32_t)i < AX_CHUNKS ? codes[(d + (uint32_t)i) * 64u + o] : 0u;
+#pragma unroll
+        for (int i = 0; i < HW; ++i) w[i] = u64of(alignbit(c[2 * i + 1], c[2 * i], sh), alignbit(c[2 * i + 2], c[2 * i + 1], sh));
     };
     auto vbits = [&](uint32_t o, uint32_t b) -> uint64_t {  // read o's valid-window bits b .. b + 63 (0 past the end)
         const uint32_t w0 = b >> 6, s6 = b & 63u;
@@ -749,7 +883,8 @@ __global__ __launch_bounds__(AX_THREADS, (ax_min_waves<MODE, HW, EM, STATS>())) 
     uint32_t off0 = 0;         // first base of the piece in the slot
     uint64_t ta = 0;           // first base of the piece in seq/qual (local mode; other lanes read it by a shuffle)
     uint32_t j = 0;
-    uint32_t st = 2u;          // 0: look window j up, 1: extend from text position p, 2: idle
+    uint32_t st = 2u;          // 0: look window j up, 1: extend from text position p, 2: idle, 3: wait for the
+                               // deferred-window pass (its deferral found the list full), then look window j up
     bool verify = false;       // st 1: p came from the anchor table (window j itself not compared yet)
     uint32_t p = 0;            // text position of window j (st 1)
     uint32_t gt = 0;           // group of p's text (st 1)
@@ -770,9 +905,12 @@ __global__ __launch_bounds__(AX_THREADS, (ax_min_waves<MODE, HW, EM, STATS>())) 
     for (;;) {
         // ================= housekeeping (wave-uniform decisions) =================
         const unsigned long long idle = __ballot(st == 2u);
-        const unsigned long long blk = __ballot(st == 2u && hasdef);
+        const unsigned long long blk = __ballot(st >= 2u && hasdef);
         const unsigned long long busy = ~idle;
         if (SPEQ_AX_PROBE == 2 && lane == 0) defn[0] = 0u;  // probe: deferred windows are dropped
+        // (a lane whose deferral found the list full waits for this pass and then looks its window up again)
+        // (a lane whose deferral found the list full, st 3, counts as blocked: the list then holds more than AX_DEF
+        // entries, so this pass runs, and the lane looks its window up again afterwards)
         const bool p2 = blk != 0 && ((uint32_t)__popcll(blk) >= SPEQ_AX_BLOCKED || busy == 0 ||
                                      __builtin_amdgcn_readfirstlane(defn[0]) + 256u > AX_DEF);
         const uint32_t n_def = (SPEQ_AX_MICRO && !p2) ? 0u : __builtin_amdgcn_readfirstlane(defn[0]);
@@ -838,10 +976,12 @@ __global__ __launch_bounds__(AX_THREADS, (ax_min_waves<MODE, HW, EM, STATS>())) 
                 const uint64_t h = ax_hash<HW>(ra, k);
                 const uint32_t fp = ax_fp(h);
                 uint32_t b = act ? ax_bucket(h, A.nb) : 0u, sl = 0, pp = 0, pg = 0;
+                const uint32_t b2 = SPEQ_AX_CUCKOO ? ax_bucket2(h, A.nb) : 0u;
                 bool pend = act, found = false;
                 uint32_t cl = AX_SENT;
                 while (__ballot(pend) != 0) {
-                    const bool c = ax_probe(A, rs_atab, fp, b, sl, pp, pg, pend, s_p2);
+                    const bool c = SPEQ_AX_CUCKOO ? ax_probe_ck(rs_atab, fp, b, b2, sl, pp, pg, pend, s_p2)
+                                                  : ax_probe(A, rs_atab, fp, b, sl, pp, pg, pend, s_p2);
                     const bool cand = pend && c;
                     if (STATS) s_p2v += cand ? 1u : 0u;
                     u32x4 gv[HW + 1];
@@ -892,6 +1032,7 @@ __global__ __launch_bounds__(AX_THREADS, (ax_min_waves<MODE, HW, EM, STATS>())) 
             af = ambf[lane];
             ad = ambd[lane];
             hasdef = false;
+            st = st == 3u ? 0u : st;  // retry the lookup whose deferral found the list full
             if (lane == 0) defn[0] = defn[1] = 0u;
             wave_sync();
             if (STATS) c_p2 += clock64() - c_s;
@@ -1171,17 +1312,21 @@ __global__ __launch_bounds__(AX_THREADS, (ax_min_waves<MODE, HW, EM, STATS>())) 
             const uint64_t h = ax_hash<HW>(ra, k);
             const uint32_t fp = ax_fp(h);
             if (lk && !resume) {
-                pb = ax_bucket(h, A.nb);
+                if (!SPEQ_AX_CUCKOO) pb = ax_bucket(h, A.nb);
                 ps = 0;
             }
-            const uint32_t boff = lk ? pb * 64u : AX_OOB;
+            // cuckoo: the key's two 32-B buckets (recomputed from the hash each time: no bucket state to keep);
+            // linear probing: the 64-B bucket pb of the probe chain
+            const uint32_t boff = lk ? (SPEQ_AX_CUCKOO ? ax_bucket(h, A.nb) * 32u : pb * 64u) : AX_OOB;
+            const uint32_t boff2 = SPEQ_AX_CUCKOO ? (lk ? ax_bucket2(h, A.nb) * 32u : AX_OOB) : boff + 32u;
             const u32x4 q0 = __builtin_amdgcn_raw_buffer_load_b128(rs_atab, boff, 0, 0);
             const u32x4 q1 = __builtin_amdgcn_raw_buffer_load_b128(rs_atab, boff + 16u, 0, 0);
-            const u32x4 q2 = __builtin_amdgcn_raw_buffer_load_b128(rs_atab, boff + 32u, 0, 0);
-            const u32x4 q3 = __builtin_amdgcn_raw_buffer_load_b128(rs_atab, boff + 48u, 0, 0);
+            const u32x4 q2 = __builtin_amdgcn_raw_buffer_load_b128(rs_atab, boff2, 0, 0);
+            const u32x4 q3 = __builtin_amdgcn_raw_buffer_load_b128(rs_atab, boff2 + 16u, 0, 0);
             if (lk) {
                 uint32_t slot = 0, cp = 0, cg = 0;
-                const uint32_t res = ax_resolve(q0, q1, q2, q3, fp, ps, slot, cp, cg);
+                const uint32_t res = SPEQ_AX_CUCKOO ? ax_resolve_ck(q0, q1, q2, q3, fp, ps, slot, cp, cg)
+                                                    : ax_resolve(q0, q1, q2, q3, fp, ps, slot, cp, cg);
                 if (res == 1u) {  // candidate: compared with the text in the next iteration
                     p = cp;
                     gt = cg;
@@ -1213,12 +1358,18 @@ __global__ __launch_bounds__(AX_THREADS, (ax_min_waves<MODE, HW, EM, STATS>())) 
                                 defl[sl++] = (uint16_t)(lane | ((j + 65u + (uint32_t)__builtin_ctzll(t)) << 6));
                             hasdef = SPEQ_AX_PROBE != 2;
                             if (STATS) s_def += cnt;
-                        } else {  // no room: the windows stay with this lane; void the slots reserved below the end
+                        } else {  // no room: void the slots reserved below the end; the lane waits for the deferred-
+                            // window pass (next iteration) and looks window j up again (one wasted lookup instead
+                            // of looking up all k - 1 windows one by one, as round 3 did)
                             for (uint32_t sl = slot0; sl < AX_DEF && sl < slot0 + cnt; ++sl) defl[sl] = AX_VOID;
+                            st = 3u;
+                            hasdef = true;
                         }
                     }
-                    j = ok_def ? dend + 1u : j + 1u;
-                    last_mm = -1;
+                    if (ok_def) {
+                        j = dend + 1u;
+                        last_mm = -1;
+                    }
                 } else {  // full bucket without the key or an empty slot: the next bucket
                     pb = pb + 1u == (uint32_t)A.nb ? 0u : pb + 1u;
                     ps = 0;
@@ -1544,12 +1695,13 @@ void ax_launch_one(const AxView& A, const UnitSrc& src, uint32_t grid, size_t ld
                        a, w);
 }
 
-// HW by k: 1 (k <= 32), 2 (k <= 64), 4 (k <= 128)
+// HW by k: 1 (k <= 32), 2 (k <= 64), 3 (k <= 96: the reference's default k = 70), 4 (k <= 128)
 template <int MODE, bool PAIRED, bool LDS, bool EM, bool STATS>
 void ax_launch_nwc(uint32_t k, const AxView& A, const UnitSrc& src, uint32_t grid, size_t lds, hipStream_t st,
                    unsigned long long* a, double* w, uint32_t n_cus) {
     if (k <= 32) ax_launch_one<MODE, PAIRED, LDS, EM, 1, STATS>(A, src, grid, lds, st, a, w, n_cus);
     else if (k <= 64) ax_launch_one<MODE, PAIRED, LDS, EM, 2, STATS>(A, src, grid, lds, st, a, w, n_cus);
+    else if (k <= 96) ax_launch_one<MODE, PAIRED, LDS, EM, 3, STATS>(A, src, grid, lds, st, a, w, n_cus);
     else ax_launch_one<MODE, PAIRED, LDS, EM, 4, STATS>(A, src, grid, lds, st, a, w, n_cus);
 }
 
@@ -1577,6 +1729,10 @@ namespace speq {
 // Builds the per-k anchor structures of replica d (blocking, on its stream). Returns a table with ok == false when
 // k, the group count or the index is outside what the scan supports (a structural limit: `transient` false), or
 // the structures would not fit the free HBM at this moment (`transient` true: ensure_ax tries again next time).
+uint32_t ax_effective_load(const speq_device_index* d) {
+    return d->ax_load ? d->ax_load : (SPEQ_AX_CUCKOO ? 88u : 35u);
+}
+
 AxTable build_ax(speq_device_index* d, uint32_t k) {
     DeviceGuard g(d->device);
     const auto t0 = std::chrono::steady_clock::now();
@@ -1628,10 +1784,22 @@ AxTable build_ax(speq_device_index* d, uint32_t k) {
         HIP_OK(hipMalloc(&d_cnt, 8));
         HIP_OK(hipMemsetAsync(owner, 0xFF, (n + 1) * 4, d->stream));
         HIP_OK(hipMemsetAsync(d_cnt, 0, 8, d->stream));
+        if (SPEQ_AX_REP == 2 && !d->d_sa) {
+            // the replica's suffix array (median representatives), once: the GPU prefix-doubling sort of the index
+            // build (build_gpu.hip), about 52 B per symbol of temporary memory; skipped (first claimant) if short
+            HIP_OK(hipMemGetInfo(&free_b, &total_b));
+            if (n * 60 < free_b / 10 * 9) {
+                HIP_OK(hipMalloc(&d->d_sa, n * 4));
+                d->track(d->d_sa);
+                HIP_OK(hipStreamSynchronize(d->stream));
+                gpu_suffix_sort(d->d_text, (uint32_t)n, d->d_sa, d->stream, false);
+                HIP_OK(hipStreamSynchronize(d->stream));
+            }
+        }
         const DevView v = search_view(d, k);
         const uint32_t grid = (uint32_t)std::min<uint64_t>((n + 255) / 256, 16384);
         hipLaunchKernelGGL(k_ax_classify, dim3(grid), dim3(256), 0, d->stream, v, d->d_text, d->d_tbad, n, k, codes,
-                           owner, d_cnt);
+                           owner, SPEQ_AX_REP == 2 ? d->d_sa : nullptr, d_cnt);
         HIP_OK(hipGetLastError());
         const uint32_t pgrid = (uint32_t)std::min<uint64_t>((n_gran + 255) / 256, 16384);
         hipLaunchKernelGGL(k_ax_pack, dim3(pgrid), dim3(256), 0, d->stream, d->d_text2, 2 * nw64, codes, n,
@@ -1641,25 +1809,50 @@ AxTable build_ax(speq_device_index* d, uint32_t k) {
         HIP_OK(hipMemcpyAsync(&distinct, d_cnt, 8, hipMemcpyDeviceToHost, d->stream));
         HIP_OK(hipStreamSynchronize(d->stream));
         ax.distinct = distinct;
-        ax.nb = std::max<uint64_t>(1, (uint64_t)((double)distinct * 100.0 / (8.0 * d->ax_load)) + 1);
+        constexpr uint32_t SLOTS = SPEQ_AX_CUCKOO ? 4u : 8u, BUCKET_B = 8u * SLOTS;
         ax.nf = std::max<uint64_t>(1, distinct * AX_FILTER_BITS / 64);
-        if (ax.nb * 64 >= (1ull << 32) - 64 || ax.nf * 8 >= (1ull << 32) - 64) {
-            // the scan addresses the tables with 32-bit buffer offsets: leave this k to the other kernels
-            cleanup();
-            for (void* q : mine) (void)hipFree(q);
-            return AxTable{};
-        }
-        alloc(&ax.atab, ax.nb * 64);
         alloc(&ax.filt, ax.nf * 8);
-        HIP_OK(hipMemsetAsync(ax.atab, 0xFF, ax.nb * 64, d->stream));
         HIP_OK(hipMemsetAsync(ax.filt, 0, ax.nf * 8, d->stream));
-        hipLaunchKernelGGL(k_ax_insert, dim3(grid), dim3(256), 0, d->stream, owner, n, d->d_text2, k, d->d_text_start,
-                           d->d_text_group, d->n_texts, reinterpret_cast<unsigned long long*>(ax.atab), ax.nb,
-                           reinterpret_cast<unsigned long long*>(ax.filt), ax.nf);
-        HIP_OK(hipGetLastError());
-        HIP_OK(hipStreamSynchronize(d->stream));
+        // cuckoo: a build that leaves a key out (eviction walk too long) is redone at a lower load factor
+        for (uint32_t load = ax_effective_load(d);; load = load > 60u ? load - 8u : load / 2u) {
+            ax.nb = std::max<uint64_t>(SPEQ_AX_CUCKOO ? 2 : 1,
+                                       (uint64_t)((double)distinct * 100.0 / ((double)SLOTS * load)) + 1);
+            if (ax.nb * BUCKET_B >= (1ull << 32) - 64 || ax.nf * 8 >= (1ull << 32) - 64) {
+                // the scan addresses the tables with 32-bit buffer offsets: leave this k to the other kernels
+                cleanup();
+                for (void* q : mine) (void)hipFree(q);
+                return AxTable{};
+            }
+            alloc(&ax.atab, ax.nb * BUCKET_B);
+            HIP_OK(hipMemsetAsync(ax.atab, 0xFF, ax.nb * BUCKET_B, d->stream));
+            if (!SPEQ_AX_CUCKOO) {
+                hipLaunchKernelGGL(k_ax_insert, dim3(grid), dim3(256), 0, d->stream, owner, n, d->d_text2, k,
+                                   d->d_text_start, d->d_text_group, d->n_texts,
+                                   reinterpret_cast<unsigned long long*>(ax.atab), ax.nb,
+                                   reinterpret_cast<unsigned long long*>(ax.filt), ax.nf);
+                HIP_OK(hipGetLastError());
+                HIP_OK(hipStreamSynchronize(d->stream));
+                ax.load = load;
+                break;
+            }
+            HIP_OK(hipMemsetAsync(d_cnt, 0, 8, d->stream));
+            hipLaunchKernelGGL(k_ax_insert_ck, dim3(grid), dim3(256), 0, d->stream, owner, n, d->d_text2, k,
+                               d->d_text_start, d->d_text_group, d->n_texts,
+                               reinterpret_cast<unsigned long long*>(ax.atab), ax.nb,
+                               reinterpret_cast<unsigned long long*>(ax.filt), ax.nf, 512u, d_cnt);
+            HIP_OK(hipGetLastError());
+            unsigned long long failed = 0;
+            HIP_OK(hipMemcpyAsync(&failed, d_cnt, 8, hipMemcpyDeviceToHost, d->stream));
+            HIP_OK(hipStreamSynchronize(d->stream));
+            ax.load = load;
+            if (failed == 0) break;
+            if (load <= 10u) throw DeviceError("build_ax: the cuckoo anchor table could not place every k-mer");
+            (void)hipFree(ax.atab);  // smaller load next: a new table
+            mine.erase(std::find(mine.begin(), mine.end(), ax.atab));
+            ax.atab = nullptr;
+        }
         ax.gran_bytes = gran_bytes;
-        ax.bytes = ax.nb * 64 + ax.nf * 8 + gran_bytes;
+        ax.bytes = ax.nb * BUCKET_B + ax.nf * 8 + gran_bytes;
         ax.ok = true;
     } catch (...) {
         cleanup();

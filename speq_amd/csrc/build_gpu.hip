@@ -236,6 +236,70 @@ uint32_t bits_for(uint64_t v) {
 
 }  // namespace
 
+// Suffix array of the device text d_text[0, n) (SA alphabet codes; a unique smallest terminator at n - 1) into d_sa, on
+// stream st (synchronous: the rounds read the survivor count back). Temporary device memory: about 52 B per symbol.
+// Used by the index build below and by the anchor-structure build (ax_scan.hip: median representatives).
+void gpu_suffix_sort(const uint8_t* d_text, uint32_t n, uint32_t* d_sa, void* stream, bool timing) {
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    DevBuf<uint32_t> d_rank(n);
+    Temp tmp;
+    {
+        DevBuf<uint64_t> k0(n), k1(n);
+        DevBuf<uint32_t> v0(n), v1(n), head(n), keep(n), off(n), pos0(n), pos1(n), suf0(n);
+        // round 0
+        k_init_keys<<<grid(n), 256, 0, st>>>(d_text, n, k0.p, v0.p);
+        BHIP(hipGetLastError());
+        rocprim::double_buffer<uint64_t> kb(k0.p, k1.p);
+        rocprim::double_buffer<uint32_t> vb(v0.p, v1.p);
+        size_t need = 0;
+        BHIP(rocprim::radix_sort_pairs(nullptr, need, kb, vb, n, 0, 3 * KEY_SYMS, st));
+        tmp.need(need);
+        BHIP(rocprim::radix_sort_pairs(tmp.p, need, kb, vb, n, 0, 3 * KEY_SYMS, st));
+        uint32_t m = n;
+        const uint32_t* cur_pos = nullptr;  // SA slots of the active list; nullptr = identity (round 0)
+        uint32_t h = KEY_SYMS;
+        const uint32_t rb = bits_for(n);
+        uint32_t rounds = 0;
+        for (;;) {
+            ++rounds;
+            // groups of equal keys in the sorted active list: head slot by max-scan, ranks, survivors
+            k_heads<<<grid(m), 256, 0, st>>>(kb.current(), m, head.p);
+            BHIP(hipGetLastError());
+            BHIP(rocprim::inclusive_scan(nullptr, need, head.p, head.p, m, rocprim::maximum<uint32_t>(), st));
+            tmp.need(need);
+            BHIP(rocprim::inclusive_scan(tmp.p, need, head.p, head.p, m, rocprim::maximum<uint32_t>(), st));
+            k_assign<<<grid(m), 256, 0, st>>>(kb.current(), vb.current(), head.p, cur_pos, m, d_sa, d_rank.p,
+                                              keep.p);
+            BHIP(hipGetLastError());
+            BHIP(rocprim::exclusive_scan(nullptr, need, keep.p, off.p, 0u, m, rocprim::plus<uint32_t>(), st));
+            tmp.need(need);
+            BHIP(rocprim::exclusive_scan(tmp.p, need, keep.p, off.p, 0u, m, rocprim::plus<uint32_t>(), st));
+            uint32_t last_off = 0, last_keep = 0;
+            // on st: the caller's stream may be a non-blocking one (the replica's), which hipMemcpy does not wait for
+            BHIP(hipMemcpyAsync(&last_off, off.p + (m - 1), 4, hipMemcpyDeviceToHost, st));
+            BHIP(hipMemcpyAsync(&last_keep, keep.p + (m - 1), 4, hipMemcpyDeviceToHost, st));
+            BHIP(hipStreamSynchronize(st));
+            const uint32_t m2 = last_off + last_keep;
+            if (m2 == 0) break;
+            if (h >= n) throw std::runtime_error("gpu build: suffix sorting did not converge");
+            // compact the survivors: slots alternate between two buffers (the current ones are being read)
+            uint32_t* npos = cur_pos == pos0.p ? pos1.p : pos0.p;
+            k_compact<<<grid(m), 256, 0, st>>>(keep.p, off.p, cur_pos, vb.current(), m, npos, suf0.p);
+            BHIP(hipGetLastError());
+            m = m2;
+            cur_pos = npos;
+            // next round: sort the survivors by (rank[s], rank[s + h]), i.e. by their first 2h symbols
+            k_pair_keys<<<grid(m), 256, 0, st>>>(suf0.p, m, d_rank.p, n, h, rb, kb.current(), vb.current());
+            BHIP(hipGetLastError());
+            BHIP(rocprim::radix_sort_pairs(nullptr, need, kb, vb, m, 0, 2 * rb, st));
+            tmp.need(need);
+            BHIP(rocprim::radix_sort_pairs(tmp.p, need, kb, vb, m, 0, 2 * rb, st));
+            h *= 2;
+        }
+        if (timing) std::fprintf(stderr, "fm_build[gpu]: %u doubling rounds\n", rounds);
+    }
+}
+
 // Fills idx.sa, occ, occ2 (pair_steps), runs, run_label and lab (label_table) from idx.text, idx.C, text_start and
 // text_group, on `device`. The caller has built the text and C and builds the prefix table afterwards.
 void fm_build_arrays_gpu(FmIndex& idx, int device, bool pair_steps, bool triple_steps, bool label_table,
@@ -266,61 +330,9 @@ void fm_build_arrays_gpu(FmIndex& idx, int device, bool pair_steps, bool triple_
 
     DevBuf<uint8_t> d_text(n);
     BHIP(hipMemcpy(d_text.p, idx.text.data(), n, hipMemcpyHostToDevice));
-    DevBuf<uint32_t> d_sa(n), d_rank(n);
-    Temp tmp;
-    {
-        DevBuf<uint64_t> k0(n), k1(n);
-        DevBuf<uint32_t> v0(n), v1(n), head(n), keep(n), off(n), pos0(n), pos1(n), suf0(n);
-        // round 0
-        k_init_keys<<<grid(n), 256, 0, st>>>(d_text.p, n, k0.p, v0.p);
-        BHIP(hipGetLastError());
-        rocprim::double_buffer<uint64_t> kb(k0.p, k1.p);
-        rocprim::double_buffer<uint32_t> vb(v0.p, v1.p);
-        size_t need = 0;
-        BHIP(rocprim::radix_sort_pairs(nullptr, need, kb, vb, n, 0, 3 * KEY_SYMS, st));
-        tmp.need(need);
-        BHIP(rocprim::radix_sort_pairs(tmp.p, need, kb, vb, n, 0, 3 * KEY_SYMS, st));
-        uint32_t m = n;
-        const uint32_t* cur_pos = nullptr;  // SA slots of the active list; nullptr = identity (round 0)
-        uint32_t h = KEY_SYMS;
-        const uint32_t rb = bits_for(n);
-        uint32_t rounds = 0;
-        for (;;) {
-            ++rounds;
-            // groups of equal keys in the sorted active list: head slot by max-scan, ranks, survivors
-            k_heads<<<grid(m), 256, 0, st>>>(kb.current(), m, head.p);
-            BHIP(hipGetLastError());
-            BHIP(rocprim::inclusive_scan(nullptr, need, head.p, head.p, m, rocprim::maximum<uint32_t>(), st));
-            tmp.need(need);
-            BHIP(rocprim::inclusive_scan(tmp.p, need, head.p, head.p, m, rocprim::maximum<uint32_t>(), st));
-            k_assign<<<grid(m), 256, 0, st>>>(kb.current(), vb.current(), head.p, cur_pos, m, d_sa.p, d_rank.p,
-                                              keep.p);
-            BHIP(hipGetLastError());
-            BHIP(rocprim::exclusive_scan(nullptr, need, keep.p, off.p, 0u, m, rocprim::plus<uint32_t>(), st));
-            tmp.need(need);
-            BHIP(rocprim::exclusive_scan(tmp.p, need, keep.p, off.p, 0u, m, rocprim::plus<uint32_t>(), st));
-            uint32_t last_off = 0, last_keep = 0;
-            BHIP(hipMemcpy(&last_off, off.p + (m - 1), 4, hipMemcpyDeviceToHost));
-            BHIP(hipMemcpy(&last_keep, keep.p + (m - 1), 4, hipMemcpyDeviceToHost));
-            const uint32_t m2 = last_off + last_keep;
-            if (m2 == 0) break;
-            if (h >= n) throw std::runtime_error("gpu build: suffix sorting did not converge");
-            // compact the survivors: slots alternate between two buffers (the current ones are being read)
-            uint32_t* npos = cur_pos == pos0.p ? pos1.p : pos0.p;
-            k_compact<<<grid(m), 256, 0, st>>>(keep.p, off.p, cur_pos, vb.current(), m, npos, suf0.p);
-            BHIP(hipGetLastError());
-            m = m2;
-            cur_pos = npos;
-            // next round: sort the survivors by (rank[s], rank[s + h]), i.e. by their first 2h symbols
-            k_pair_keys<<<grid(m), 256, 0, st>>>(suf0.p, m, d_rank.p, n, h, rb, kb.current(), vb.current());
-            BHIP(hipGetLastError());
-            BHIP(rocprim::radix_sort_pairs(nullptr, need, kb, vb, m, 0, 2 * rb, st));
-            tmp.need(need);
-            BHIP(rocprim::radix_sort_pairs(tmp.p, need, kb, vb, m, 0, 2 * rb, st));
-            h *= 2;
-        }
-        if (timing) std::fprintf(stderr, "fm_build[gpu]: %u doubling rounds\n", rounds);
-    }
+    DevBuf<uint32_t> d_sa(n);
+    gpu_suffix_sort(d_text.p, n, d_sa.p, st, timing);
+    Temp tmp;  // rocPRIM scratch of the steps below
     phase("sa");
 
     idx.sa.resize(n);

@@ -20,7 +20,8 @@ struct AxTable {
     uint32_t* mhi = nullptr;   // on the first EM scan of k, ensure_ax_em) / its end, indexed by its interval start
     void* atab = nullptr;      // anchor table: 64-B buckets of 8 {representative position, fingerprint, group} slots
     void* filt = nullptr;      // blocked Bloom filter of the distinct k-mers (one 64-bit word per k-mer, 3 bits)
-    uint64_t nb = 0;           // buckets
+    uint64_t nb = 0;           // buckets (cuckoo: 32 B, 4 slots; linear probing: 64 B, 8 slots)
+    uint32_t load = 0;         // load factor the table was built at (percent)
     uint64_t nf = 0;           // filter words
     uint64_t gran_bytes = 0;
     uint64_t distinct = 0;     // distinct k-mers of the texts
@@ -90,8 +91,11 @@ struct speq_device_index {
     // anchor-and-extend scan (ax_scan.hip)
     uint64_t* d_text2 = nullptr;    // 2-bit text, built with the first per-k structures
     uint64_t* d_tbad = nullptr;     // bitmap of non-ACGT text positions
+    uint32_t* d_sa = nullptr;       // suffix array (median anchor representatives), sorted on the GPU with the first
+                                    // per-k structures
     bool ax_scan = true;            // tuning "ax_scan": read scans of k <= 128 use k_scan_ax
-    uint32_t ax_load = 35;          // tuning "ax_load": anchor-table load factor, percent
+    uint32_t ax_load = 0;           // tuning "ax_load": anchor-table load factor, percent (0: the table form's
+                                    // default, ax_scan.hip: cuckoo 88, linear probing 35)
     uint32_t grid_blocks_ax = 65535;  // tuning "grid_blocks_ax"
     uint32_t blocks_per_cu_ax = 0;  // tuning "blocks_per_cu_ax" (0: as many as registers/LDS allow)
     std::mutex ax_mu;
@@ -109,6 +113,7 @@ namespace speq {
 DevView search_view(const speq_device_index* d, uint32_t k);  // the FM view a search of k-mers uses (scan_kernels.hip)
 AxTable build_ax(speq_device_index* d, uint32_t k);
 const AxTable* ensure_ax(speq_device_index* d, uint32_t k);
+uint32_t ax_effective_load(const speq_device_index* d);  // the anchor table's load factor (percent) builds use
 bool launch_ax(speq_device_index* d, int mode, bool paired, const speq_dev::UnitSrc& src, hipStream_t st,
                unsigned long long* a, double* w);
 }  // namespace speq

@@ -1124,15 +1124,18 @@ StreamTotals run_stream(const char* path1, const char* path2, uint32_t threads, 
                     const bool eof = w.b1.end == w.b1.buf->len;
                     speq_slot s;
                     sink.acquire_raw(s, l1);
-                    // direct: one read-only newline pass over the mapping, then H2D from the mapping itself
-                    uint64_t lines = direct ? count_nl(w.b1.data(), l1)
-                                            : copy_count_nl(reinterpret_cast<char*>(s.seq), w.b1.data(), l1);
+                    // direct: one read-only newline pass over the mapping, then H2D from the mapping itself — only
+                    // for blocks of a whole-file mapping, which outlives every copy (run_stream drains them before
+                    // the cutters go); a block of a recycled read / inflate buffer is always copied into the slot
+                    const bool dir = direct != 0 && w.b1.buf && w.b1.buf->map != nullptr;
+                    uint64_t lines = dir ? count_nl(w.b1.data(), l1)
+                                         : copy_count_nl(reinterpret_cast<char*>(s.seq), w.b1.data(), l1);
                     if (eof && l1 && w.b1.data()[l1 - 1] != '\n') ++lines;
                     if (lines == 0 || lines % 4 != 0) {
                         sink.submit(s, 0);
                         throw NotSimple();
                     }
-                    sink.submit_raw(s, l1, 0, lines / 4, false, direct ? w.b1.data() : nullptr);
+                    sink.submit_raw(s, l1, 0, lines / 4, false, dir ? w.b1.data() : nullptr);
                     sh.records += lines / 4;
                     sh.batches += 1;
                     if (sh.failed) return;

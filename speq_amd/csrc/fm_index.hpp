@@ -105,6 +105,8 @@ void fm_build(FmIndex& idx, const char* seq, const uint64_t* rec_offsets, uint32
               uint32_t threads, bool pair_steps = false, bool label_table = false, int gpu_device = -1,
               bool triple_steps = false);
 // GPU half of fm_build (build_gpu.hip): suffix array, occ/occ2/occ3/runs planes, run labels and label table.
+// suffix array of a device text (build_gpu.hip); stream = hipStream_t
+void gpu_suffix_sort(const uint8_t* d_text, uint32_t n, uint32_t* d_sa, void* stream, bool timing);
 void fm_build_arrays_gpu(FmIndex& idx, int device, bool pair_steps, bool triple_steps, bool label_table,
                          bool timing);
 // C3[abc] = #suffixes < "abc" (a, b, c in A..T), from symbol-pair and -triple counts of the text.

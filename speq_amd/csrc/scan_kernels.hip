@@ -2046,7 +2046,7 @@ int speq_device_set_tuning(speq_device_index* d, const char* key, int64_t value)
         } else if (k == "ax_load") {
             if (value < 10 || value > 90) throw std::invalid_argument("ax_load must be in [10, 90] (percent)");
             std::lock_guard<std::mutex> lk(d->ax_mu);
-            if (!d->axtabs.empty() && (uint32_t)value != d->ax_load)
+            if (!d->axtabs.empty() && (uint32_t)value != speq::ax_effective_load(d))
                 throw std::invalid_argument("ax_load must be set before the first scan");
             d->ax_load = (uint32_t)value;
         } else if (k == "grid_blocks_ax") {
@@ -2093,7 +2093,7 @@ int speq_device_get_tuning(const speq_device_index* d, const char* key, int64_t*
         else if (k == "kt_load8") *value = d->kt_load8;
         else if (k == "ax_scan") *value = d->ax_scan ? 1 : 0;
         else if (k == "last_kernel") *value = d->last_kernel;
-        else if (k == "ax_load") *value = d->ax_load;
+        else if (k == "ax_load") *value = speq::ax_effective_load(d);
         else if (k == "grid_blocks_ax") *value = d->grid_blocks_ax;
         else if (k == "blocks_per_cu_ax") *value = d->blocks_per_cu_ax;
         else throw std::invalid_argument("speq_device_get_tuning: unknown key " + k);
