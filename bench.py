@@ -475,10 +475,6 @@ def main():
             lines["k70_reference_defaults"], _ = run_workload(ctx, 2, 70, n_reads, "local", a.steps, a.warmup,
                                                               with_lf=False, with_pcie=False, with_cpu=cpu_on,
                                                               cpu_seconds=short_cpu, prepared=prep)
-        if want("k70_err05"):
-            lines["k70_err05"], _ = run_workload(ctx, 2, 70, n_reads, "local", a.steps, a.warmup, with_lf=False,
-                                                 with_pcie=False, with_cpu=False, cpu_seconds=0, prepared=prep,
-                                                 err=0.005)
         if ctx.world == 1:
             if not a.no_fastq and want("fastq_e2e"):
                 lines["fastq_e2e"] = fastq_e2e(ctx, prep, k)
@@ -487,6 +483,10 @@ def main():
                 lines["local_varq"], _ = run_workload(ctx, 2, k, n_reads, "local", a.steps, a.warmup, with_lf=False,
                                                       with_pcie=False, with_cpu=False, cpu_seconds=0, prepared=prep,
                                                       qual_profile="variable")
+        if want("k70_err05"):  # (after the lines that reuse config 2's 0.1 %-error reads)
+            lines["k70_err05"], _ = run_workload(ctx, 2, 70, n_reads, "local", a.steps, a.warmup, with_lf=False,
+                                                 with_pcie=False, with_cpu=False, cpu_seconds=0, prepared=prep,
+                                                 err=0.005)
         if a.cfg5_pairs and (want("cfg5_paired") or want("cfg5_paired_local")):
             # BASELINE config 5 (the north_star's scaling config): paired, k = 31, on a per-GPU sample of its pairs
             lines["cfg5_paired"], p5 = run_workload(ctx, 5, 31, a.cfg5_pairs, "global", max(3, a.steps // 4),

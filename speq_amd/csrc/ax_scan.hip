@@ -626,6 +626,15 @@ constexpr uint32_t AX_WPB = SPEQ_AX_WPB, AX_THREADS = 64 * SPEQ_AX_WPB;
 #ifndef SPEQ_AX_REFILL_SYNC  // 1: the refill ends with wave-level LDS fences after the valid-window bits (A/B knob;
 #define SPEQ_AX_REFILL_SYNC 0   // 0: none — every lane writes and then reads only its own column of them)
 #endif
+#ifndef SPEQ_AX_SPEC_HW  // speculative left runs after an absent lookup whose mismatch is unknown, for HW >= this
+#define SPEQ_AX_SPEC_HW 3  // (k > 64 by default; 8 = off), Phred-weighted scans only (A/B knob): k = 70 local -5 % at
+#endif                     // 0.1 % errors, -14 % at 0.5 %; global mode +6 % (8 B of spills; profiles/r04/ab_*)
+#ifndef SPEQ_AX_SPEC_GLOBAL  // 1: speculative left runs in global mode too
+#define SPEQ_AX_SPEC_GLOBAL 0
+#endif
+#ifndef SPEQ_AX_OFFPF  // 1: single-end refills take the new reads' offsets from a window prefetched during the previous
+#define SPEQ_AX_OFFPF 0   // refill (one dependent round trip less per refill, but 12 B of spills at k <= 32: config 2
+#endif                    // 0.2243 vs 0.2162 ms, profiles/r04/ab_*); 0 (default): load them when needed (A/B knob)
 #ifndef SPEQ_AX_PROBE  // timing probes (wrong counts; make axvariant only): 1 staging only, 2 no deferred-window pass,
                        // 3 staging loads only (no decode), 5 as 3 without the valid-window bits, 6 / 7 as 3 without the
                        // doubling steps / the bad-bit reads
@@ -867,9 +876,10 @@ __global__ __launch_bounds__(AX_THREADS, (ax_min_waves<MODE, HW, EM, STATS>())) 
     // ---- the lane's unit and piece
     bool has_unit = false;     // working on a unit (until it is finalized)
     bool last_piece = true;    // the current piece is the unit's last
-    uint64_t rd = 0;           // current read (index into off)
+    uint32_t rd = 0;           // current read (index into off; launch_ax keeps n_units < 2^32)
     uint32_t mate = 0, seg = 0, nseg = 0;
-    uint64_t rb = 0, L = 0, W = 0;  // current read: first base, length, windows
+    uint64_t rb = 0;           // current read: first base
+    uint32_t L = 0, W = 0;     // its length (< 2^32: a read in HBM with its qualities) and windows
     int32_t af = -1, ad = 0;   // ambiguity state of the unit
     bool hasdef = false;       // deferred windows of this lane's piece are in the wave's list
     // ---- the wave's pool (uniform): an equal share of the units, [nu w / NWV, nu (w + 1) / NWV) — contiguous
@@ -892,15 +902,58 @@ __global__ __launch_bounds__(AX_THREADS, (ax_min_waves<MODE, HW, EM, STATS>())) 
     uint32_t pb = 0, ps = 0;   // probe position of the current lookup (bucket, first slot)
     bool resume = false;       // continue the current lookup at (pb, ps): full bucket, or failed verification
     bool run_phase = true;     // this wave iteration extends runs (else: looks windows up)
+    // Speculative left runs (SPEC, k > 64): a window absent with no known mismatch (the read's first windows over a
+    // sequencing error) used to defer the k - 1 windows after it, of which those right of the error are present
+    // (each then passes the Bloom filter and costs a phase-2 lookup: ~k/2 per such read, the bulk of the deferred-
+    // window pass at k = 70). Instead the lane keeps them pending (sp), looks up the window past them, and on a hit
+    // runs from sp against the text shifted back by the pending windows (ps = AX_PS_SPEC): the first mismatch e (the
+    // error, which lies in the window before sp) defers only the windows [sp, sp + e] that hold it, and the rest
+    // goes on as a run whose first k bases are still to be compared (ps = AX_PS_FRESH). A speculative run must stay in
+    // its anchor's text: an END window among the pending ones defers them instead.
+    constexpr bool SPEC = HW >= SPEQ_AX_SPEC_HW && !EM && (MODE == KM_LOCAL || SPEQ_AX_SPEC_GLOBAL);
+    constexpr uint32_t AX_PS_SPEC = 16u, AX_PS_FRESH = 17u;
+    uint32_t sp = 0;  // pending windows [sp, sp + k - 2] of the piece; 0: none
+    // defers the valid windows of [lo, hi] (hi - lo <= 127; hi < lo: none) of this lane's piece; when the list has
+    // no room: the reserved slots are voided, the lane waits for the deferred-window pass (st 3) and false
+    auto defer_range = [&](uint32_t lo, uint32_t hi) -> bool {
+        if (hi + 1u <= lo) return true;
+        const uint32_t span = hi + 1u - lo;
+        uint64_t dm0 = vbits(lane, lo), dm1 = span > 64u ? vbits(lane, lo + 64u) : 0ull;
+        dm0 &= span >= 64u ? ~0ull : ((1ull << span) - 1ull);
+        if (span > 64u) dm1 &= span - 64u >= 64u ? ~0ull : ((1ull << (span - 64u)) - 1ull);
+        const uint32_t cnt = (uint32_t)__popcll(dm0) + (uint32_t)__popcll(dm1);
+        if (cnt == 0u) return true;
+        const uint32_t slot0 = atomicAdd(&defn[0], cnt);
+        if (slot0 + cnt > AX_DEF) {
+            for (uint32_t sl = slot0; sl < AX_DEF && sl < slot0 + cnt; ++sl) defl[sl] = AX_VOID;
+            st = 3u;
+            hasdef = true;
+            return false;
+        }
+        uint32_t sl = slot0;
+        for (uint64_t t = dm0; t; t &= t - 1) defl[sl++] = (uint16_t)(lane | ((lo + (uint32_t)__builtin_ctzll(t)) << 6));
+        for (uint64_t t = dm1; t; t &= t - 1)
+            defl[sl++] = (uint16_t)(lane | ((lo + 64u + (uint32_t)__builtin_ctzll(t)) << 6));
+        hasdef = SPEQ_AX_PROBE != 2;
+        if (STATS) s_def += cnt;
+        return true;
+    };
 
-    auto start_read = [&](uint64_t r) {
-        rd = r;
-        rb = src.off[r];
-        L = src.off[r + 1] - rb;
+    auto start_read_at = [&](uint64_t r, uint64_t b, uint64_t e) {  // read r spans [b, e) of seq / qual
+        rd = (uint32_t)r;
+        rb = b;
+        L = (uint32_t)(e - b);
         W = L >= k ? L - k + 1 : 0;
         nseg = W ? (uint32_t)((W + segw - 1) / segw) : 1u;
         seg = 0;
     };
+    auto start_read = [&](uint64_t r) { start_read_at(r, src.off[r], src.off[r + 1]); };
+    // (OFFPF) the prefetched window of read offsets, relative to the wave's first read (a wave whose reads span
+    // 4 GiB or more loads its offsets directly: pf_ok false)
+    constexpr bool OFFPF = SPEQ_AX_OFFPF && !PAIRED;
+    const uint64_t wbase = OFFPF ? src.off[cur] : 0;
+    const bool pf_ok = OFFPF && src.off[cur_end] - wbase < (1ull << 32);
+    uint32_t pf = (pf_ok && cur + lane <= nu) ? (uint32_t)(src.off[cur + lane] - wbase) : 0u;
 
     for (;;) {
         // ================= housekeeping (wave-uniform decisions) =================
@@ -1062,6 +1115,19 @@ __global__ __launch_bounds__(AX_THREADS, (ax_min_waves<MODE, HW, EM, STATS>())) 
             const uint32_t rank = lanes_below(tk);
             const uint64_t taken = (uint64_t)__popcll(tk);
             if (wants && !has_unit && cur + rank < cur_end) newu = cur + rank;
+            // (OFFPF, single-end) the new units' bounds come from the wave's prefetched window of read offsets (lane
+            // i: off[cur + i] - wbase, loaded during the previous refill's staging), so the staging loads below do not
+            // wait behind a round trip for the offsets; the window then moves on by `taken` units, its top lanes
+            // loading the next offsets (consumed at the next refill)
+            uint32_t pf_s = 0, pf_e = 0;
+            const bool pf_use = OFFPF && pf_ok && taken < 64u;
+            if (OFFPF && pf_ok) {
+                pf_s = (uint32_t)__shfl((int)pf, (int)min(rank, 63u));
+                pf_e = (uint32_t)__shfl((int)pf, (int)min(rank + 1u, 63u));
+                const uint32_t shifted = (uint32_t)__shfl((int)pf, (int)((lane + (uint32_t)taken) & 63u));
+                const uint64_t idx = cur + taken + lane;
+                pf = lane + taken < 64u ? shifted : (idx <= nu ? (uint32_t)(src.off[idx] - wbase) : 0u);
+            }
             cur = min(cur + taken, cur_end);
             bool stg = false;
             if (wants) {
@@ -1069,7 +1135,8 @@ __global__ __launch_bounds__(AX_THREADS, (ax_min_waves<MODE, HW, EM, STATS>())) 
                     if (newu < nu) {
                         has_unit = true;
                         mate = 0;
-                        start_read(PAIRED ? 2 * newu : newu);
+                        if (pf_use) start_read_at(newu, wbase + pf_s, wbase + pf_e);
+                        else start_read(PAIRED ? 2 * newu : newu);
                         stg = true;
                     }
                 } else if (seg + 1u < nseg) {
@@ -1084,7 +1151,7 @@ __global__ __launch_bounds__(AX_THREADS, (ax_min_waves<MODE, HW, EM, STATS>())) 
             // the piece: bases [s, s + sb), windows [s, s + wend) of read rd
             const uint64_t s = (uint64_t)seg * segw;
             const uint32_t sb = stg && W ? (uint32_t)(L - s < AX_CAP ? L - s : AX_CAP) : 0u;
-            const uint32_t nwend = stg && W ? (uint32_t)(W - s < segw ? W - s : segw) : 0u;
+            const uint32_t nwend = stg && W ? (uint32_t)(W - s < segw ? W - s : segw) : 0u;  // (s < W here)
             const uint64_t a = rb + s;
             const uint64_t a16 = a & ~15ull;
             const uint32_t noff0 = (uint32_t)(a - a16);
@@ -1248,6 +1315,7 @@ __global__ __launch_bounds__(AX_THREADS, (ax_min_waves<MODE, HW, EM, STATS>())) 
                     }
                 }
                 j = 0;
+                if (SPEC) sp = 0;
                 st = (wend > 0 && SPEQ_AX_PROBE != 1 && SPEQ_AX_PROBE != 3 && SPEQ_AX_PROBE < 6) ? 0u : 2u;
                 verify = false;
                 resume = false;
@@ -1295,7 +1363,9 @@ __global__ __launch_bounds__(AX_THREADS, (ax_min_waves<MODE, HW, EM, STATS>())) 
             const uint32_t j0 = j;
             if (SPEC_RW) read_words(lane, off0 + j0, ra);
             j = next_valid(lane, j0, wend);
-            if (j >= wend) st = 2u;
+            if (SPEC && sp != 0u && j >= wend && defer_range(sp, min(sp + k - 2u, wend - 1u)))
+                sp = 0;  // no window left to anchor the pending ones (no room: st 3, kept)
+            if (j >= wend && st == 0u) st = 2u;
             else if (SPEC_RW && j != j0) read_words(lane, off0 + j, ra);
         }
         const bool lk = st == 0u && !run_phase, rn = st == 1u && run_phase;
@@ -1334,41 +1404,39 @@ __global__ __launch_bounds__(AX_THREADS, (ax_min_waves<MODE, HW, EM, STATS>())) 
                     st = 1u;
                     verify = true;
                     resume = false;
-                } else if (res == 0u) {
-                    // absent: defer the windows that share the mismatch (or the next k - 1), skip past them
-                    resume = false;
-                    uint32_t dend = (last_mm >= (int32_t)j && last_mm < (int32_t)(j + k)) ? (uint32_t)last_mm
-                                                                                           : j + k - 1u;
-                    dend = min(dend, wend - 1u);
-                    // the valid windows of (j, dend] as two 64-bit masks (dend - j <= k - 1 <= 127)
-                    const uint32_t span = dend - j;
-                    uint64_t dm0 = vbits(lane, j + 1u), dm1 = span > 64u ? vbits(lane, j + 65u) : 0ull;
-                    dm0 &= span >= 64u ? ~0ull : ((1ull << span) - 1ull);
-                    if (span > 64u) dm1 &= span - 64u >= 64u ? ~0ull : ((1ull << (span - 64u)) - 1ull);
-                    const uint32_t cnt = (uint32_t)__popcll(dm0) + (uint32_t)__popcll(dm1);
-                    bool ok_def = true;
-                    if (cnt) {
-                        const uint32_t slot0 = atomicAdd(&defn[0], cnt);
-                        ok_def = slot0 + cnt <= AX_DEF;
-                        if (ok_def) {
-                            uint32_t sl = slot0;
-                            for (uint64_t t = dm0; t; t &= t - 1)
-                                defl[sl++] = (uint16_t)(lane | ((j + 1u + (uint32_t)__builtin_ctzll(t)) << 6));
-                            for (uint64_t t = dm1; t; t &= t - 1)
-                                defl[sl++] = (uint16_t)(lane | ((j + 65u + (uint32_t)__builtin_ctzll(t)) << 6));
-                            hasdef = SPEQ_AX_PROBE != 2;
-                            if (STATS) s_def += cnt;
-                        } else {  // no room: void the slots reserved below the end; the lane waits for the deferred-
-                            // window pass (next iteration) and looks window j up again (one wasted lookup instead
-                            // of looking up all k - 1 windows one by one, as round 3 did)
-                            for (uint32_t sl = slot0; sl < AX_DEF && sl < slot0 + cnt; ++sl) defl[sl] = AX_VOID;
-                            st = 3u;
-                            hasdef = true;
-                        }
+                    if (SPEC && sp != 0u) {  // pending windows [sp, j): the run starts there, text shifted back
+                        const uint32_t back = j - sp;
+                        if (cp >= back) {
+                            p = cp - back;
+                            j = sp;
+                            ps = AX_PS_SPEC;
+                            pb = back;  // (no probe to resume from a speculative run)
+                            sp = 0;
+                        } else if (defer_range(sp, j - 1u)) {  // (the text's start) defer them
+                            sp = 0;
+                        }  // (no room: st 3, the lookup is redone after the deferred-window pass)
                     }
-                    if (ok_def) {
-                        j = dend + 1u;
-                        last_mm = -1;
+                } else if (res == 0u) {
+                    // absent: defer the windows that share the mismatch (or the next k - 1), skip past them; (SPEC)
+                    // mismatch unknown: keep the next k - 1 windows pending and look up the one after them
+                    resume = false;
+                    const bool known = last_mm >= (int32_t)j && last_mm < (int32_t)(j + k);
+                    if (SPEC && !known && j + k < wend) {
+                        if (sp == 0u || defer_range(sp, sp + k - 2u)) {  // (an earlier pending range first)
+                            sp = j + 1u;
+                            j += k;
+                            last_mm = -1;
+                        }
+                    } else if (!SPEC || sp == 0u || defer_range(sp, min(sp + k - 2u, j - 1u))) {
+                        if (SPEC) sp = 0;
+                        uint32_t dend = known ? (uint32_t)last_mm : j + k - 1u;
+                        dend = min(dend, wend - 1u);
+                        // (no room: the lane waits for the deferred-window pass, st 3, and looks window j up again
+                        // afterwards — one wasted lookup instead of looking up all k - 1 windows one by one)
+                        if (defer_range(j + 1u, dend)) {
+                            j = dend + 1u;
+                            last_mm = -1;
+                        }
                     }
                 } else {  // full bucket without the key or an empty slot: the next bucket
                     pb = pb + 1u == (uint32_t)A.nb ? 0u : pb + 1u;
@@ -1430,7 +1498,48 @@ __global__ __launch_bounds__(AX_THREADS, (ax_min_waves<MODE, HW, EM, STATS>())) 
                 // (MICRO) bases past cl compare whatever lies there (zeros past the staged chunks and the loaded
                 // granules): a mismatch among them only matters as "none before cl"
                 if (SPEQ_AX_MICRO) e = min(e, cl);
-                if (verify && e < k) {  // fingerprint collision: resume probing after that slot
+                // (SPEC) a speculative run must stay in its anchor's text: an END window (a text end) among the pending
+                // windows [0, pb) defers them, and the anchored window is compared from its own position next
+                bool sep = false;
+                if (SPEC && ps == AX_PS_SPEC) {
+#pragma unroll
+                    for (uint32_t c = 0; c < 4u; ++c) {
+                        const uint32_t w0 = 32u * c;
+                        const uint32_t P0 = alignbit(gr[c + 1][2], gr[c][2], s5);
+                        const uint32_t P1 = alignbit(gr[c + 1][3], gr[c][3], s5);
+                        const uint32_t m = pb <= w0 ? 0u : (pb - w0 >= 32u ? ~0u : ((1u << (pb - w0)) - 1u));
+                        sep = sep || (P0 & P1 & m) != 0u;
+                    }
+                }
+                if (SPEC && sep) {
+                    if (defer_range(j, j + pb - 1u)) {
+                        j += pb;
+                        p += pb;
+                        ps = AX_PS_FRESH;  // (verify stays set)
+                    } else {
+                        ps = 0;  // no room (st 3): window j is looked up after the deferred-window pass
+                        resume = false;
+                    }
+                    last_mm = -1;
+                } else if (SPEC && verify && e < k && ps == AX_PS_SPEC) {
+                    // the windows [j, j + e] hold the speculative run's first mismatch (the read's error): deferred;
+                    // the run goes on after it, its first k bases still to be compared
+                    if (defer_range(j, j + e)) {
+                        j += e + 1u;
+                        p += e + 1u;
+                        ps = AX_PS_FRESH;
+                        st = j < wend ? 1u : 2u;
+                    } else {
+                        ps = 0;
+                        resume = false;
+                    }
+                    last_mm = -1;
+                } else if (SPEC && verify && e < k && ps == AX_PS_FRESH) {  // no match from here: look window j up
+                    st = 0u;
+                    resume = false;
+                    ps = 0;
+                    last_mm = (int32_t)(j + e);
+                } else if (verify && e < k) {  // fingerprint collision: resume probing after that slot
                     st = 0u;
                     resume = true;
                     ++ps;
@@ -1914,6 +2023,7 @@ static bool ensure_ax_em(speq_device_index* d, AxTable* ax, uint32_t k) {
 // its work counters there.
 bool launch_ax(speq_device_index* d, int mode, bool paired, const UnitSrc& src, hipStream_t st, unsigned long long* a,
                double* w) {
+    if (src.n_units >= (1ull << 32)) return false;  // 32-bit read indices in the kernel: the other kernels take it
     AxTable* ax = const_cast<AxTable*>(ensure_ax(d, src.k));
     if (!ax) return false;
     if (src.em_mult != nullptr && !ensure_ax_em(d, ax, src.k)) return false;  // EM: the other kernels take it
