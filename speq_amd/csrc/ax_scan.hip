@@ -120,6 +120,7 @@ enum : uint32_t {
     AXS_CYC_RUN,         // ... phase-1 run iterations
     AXS_CYC_P2,          // ... phase 2 (deferred windows)
     AXS_CYC_TOTAL,       // ... the whole loop
+    AXS_P2_PASSES,       // deferred-window passes (per wave)
     AXS_N
 };
 static_assert(AXS_N == SPEQ_AX_STATS_N, "speq_scan.h SPEQ_AX_STATS_N");
@@ -583,7 +584,7 @@ template <int MODE>
 constexpr uint32_t ax_wave_bytes() {
     static_assert(8u * AX_VWW >= 2u * AX_CHUNKS, "the bad-base bits of a staged piece live in its valid-window words");
     return 4u * AX_CHUNKS * 64u + 8u * AX_VWW * 64u + (MODE == KM_LOCAL ? 2u * AX_CHUNKS * 64u : 0u) +
-           64u + 2u * ax_def<MODE>() + 16u + 8u * 64u + (MODE == KM_LOCAL ? 4u * AX_WL + 4u * 64u : 0u) + AX_OWNB;
+           64u + 2u * ax_def<MODE>() + 24u + 8u * 64u + (MODE == KM_LOCAL ? 4u * AX_WL + 4u * 64u : 0u) + AX_OWNB;
 }
 
 #ifndef SPEQ_AX_WPB  // waves per workgroup of k_scan_ax (A/B knob)
@@ -692,8 +693,11 @@ __global__ __launch_bounds__(AX_THREADS, (ax_min_waves<MODE, HW, EM, STATS>())) 
     uint8_t* off0s = reinterpret_cast<uint8_t*>(chg + (MODE == KM_LOCAL ? AX_CHUNKS * 64u : 0u));   // [64]
     uint16_t* defl = reinterpret_cast<uint16_t*>(off0s + 64);                // [AX_DEF]
     constexpr uint32_t AX_DEF = ax_def<MODE>();
-    uint32_t* defn = reinterpret_cast<uint32_t*>(defl + AX_DEF);             // [4]: entries, survivors, sums
-    int32_t* ambf = reinterpret_cast<int32_t*>(defn + 4);                    // [64] first counted group
+    uint32_t* defn = reinterpret_cast<uint32_t*>(defl + AX_DEF);             // [2]: entries, survivors
+    // the wave's sums of passing windows (T) and ambiguous units, u64 (8-B aligned: every array before is a multiple
+    // of 8 B), added to by the lanes' LDS atomics as they go (no per-lane registers held for them)
+    unsigned long long* wsum = reinterpret_cast<unsigned long long*>(defn + 2);  // [2]
+    int32_t* ambf = reinterpret_cast<int32_t*>(defn + 6);                    // [64] first counted group
     int32_t* ambd = ambf + 64;                                               // [64] another group seen
     uint32_t* wl = reinterpret_cast<uint32_t*>(ambd + 64);                   // [AX_WL] (local)
     uint32_t* wlm = wl + AX_WL;                                              // [64] (local)
@@ -709,7 +713,10 @@ __global__ __launch_bounds__(AX_THREADS, (ax_min_waves<MODE, HW, EM, STATS>())) 
         }
     if (LDS_HIST)
         for (uint32_t i = threadIdx.x; i < hist_words; i += AX_THREADS) hA[i] = 0ull;
-    if (lane == 0) defn[0] = defn[1] = 0u;
+    if (lane == 0) {
+        defn[0] = defn[1] = 0u;
+        wsum[0] = wsum[1] = 0ull;
+    }
     __syncthreads();
     unsigned long long* gU = out_a + 2;
 
@@ -730,11 +737,10 @@ __global__ __launch_bounds__(AX_THREADS, (ax_min_waves<MODE, HW, EM, STATS>())) 
     const uint32_t qt4 = (qt > 0x7Fu ? 0x7Fu : qt) * 0x01010101u;
     const uint32_t allbad = src.cutoff >= 41u ? 0x80808080u : 0u;  // every window fails the quality filter
 
-    uint32_t t_cnt = 0, amb = 0;
     // diagnostic counters (STATS only; wave-level ones are counted by lane 0)
     uint32_t s_iter = 0, s_lk = 0, s_rn = 0, s_lkw = 0, s_rnw = 0, s_rwin = 0, s_def = 0, s_fp = 0, s_p2 = 0,
              s_p2v = 0, s_ch = 0, s_seg = 0, s_qb = 0, s_tal = 0, s_rg = 0, s_spl = 0, s_b4 = 0, s_b16 = 0, s_b32 = 0,
-             s_b64 = 0;
+             s_b64 = 0, s_p2n = 0;
     // section clocks (STATS only; wave-uniform, kept by every lane, reported by lane 0)
     uint64_t c_ref = 0, c_lk = 0, c_rn = 0, c_p2 = 0, c_t0 = STATS ? clock64() : 0ull, c_s = 0;
 
@@ -1088,7 +1094,10 @@ __global__ __launch_bounds__(AX_THREADS, (ax_min_waves<MODE, HW, EM, STATS>())) 
             st = st == 3u ? 0u : st;  // retry the lookup whose deferral found the list full
             if (lane == 0) defn[0] = defn[1] = 0u;
             wave_sync();
-            if (STATS) c_p2 += clock64() - c_s;
+            if (STATS) {
+                c_p2 += clock64() - c_s;
+                s_p2n += lane == 0 ? 1u : 0u;
+            }
             continue;
         }
         // lanes that can start a piece now: idle, no deferred windows pending, and a next piece of their unit or
@@ -1104,7 +1113,7 @@ __global__ __launch_bounds__(AX_THREADS, (ax_min_waves<MODE, HW, EM, STATS>())) 
             // ================= refill: next pieces of the wanting lanes, staged together =================
             if (STATS) s_spl += lane == 0 ? 1u : 0u;
             if (wants && has_unit && last_piece) {  // the unit is complete: its ambiguity (fm_scanner.cpp:183-190)
-                if (ad) ++amb;
+                if (ad) atomicAdd(&wsum[1], 1ull);
                 has_unit = false;
                 af = -1;
                 ad = 0;
@@ -1305,14 +1314,16 @@ __global__ __launch_bounds__(AX_THREADS, (ax_min_waves<MODE, HW, EM, STATS>())) 
                 if (SPEQ_AX_REFILL_SYNC) wave_sync();  // (own column: the lane's reads precede its writes anyway)
                 {
                     uint32_t* vw32 = reinterpret_cast<uint32_t*>(vw);
+                    uint32_t tc = 0;  // T (fm_scanner.cpp:164): the piece's passing windows
 #pragma unroll
                     for (uint32_t d = 0; d < 2u * AX_VWW; ++d) {
                         uint32_t v = alignbit(d + 1u < 8u ? ok[d + 1] : 0u, ok[d], off0);
                         const uint32_t bit0 = 32u * d;
                         v = wend <= bit0 ? 0u : (wend < bit0 + 32u ? v & ((1u << (wend - bit0)) - 1u) : v);
-                        t_cnt += (uint32_t)__popc(v);
+                        tc += (uint32_t)__popc(v);
                         vw32[((d >> 1) * 64u + lane) * 2u + (d & 1u)] = v;
                     }
+                    if (tc) atomicAdd(&wsum[0], (unsigned long long)tc);
                 }
                 j = 0;
                 if (SPEC) sp = 0;
@@ -1738,18 +1749,9 @@ __global__ __launch_bounds__(AX_THREADS, (ax_min_waves<MODE, HW, EM, STATS>())) 
         }
     }
     const uint64_t c_tot = STATS ? clock64() - c_t0 : 0ull;
-    if (has_unit && ad) ++amb;  // the wave's last units
-
-    // wave sums of the window and ambiguity counters through two LDS words (no shuffle address registers)
-    if (lane == 0) {
-        defn[2] = 0;
-        defn[3] = 0;
-    }
+    if (has_unit && ad) atomicAdd(&wsum[1], 1ull);  // the wave's last units
     wave_sync();
-    if (t_cnt) atomicAdd(&defn[2], t_cnt);
-    if (amb) atomicAdd(&defn[3], amb);
-    wave_sync();
-    const unsigned long long tsum = defn[2], asum = defn[3];
+    const unsigned long long tsum = wsum[0], asum = wsum[1];
     if (lane == 0) {
         if (tsum) atomicAdd(&out_a[0], tsum);
         if (asum) atomicAdd(&out_a[1], asum);
@@ -1758,7 +1760,7 @@ __global__ __launch_bounds__(AX_THREADS, (ax_min_waves<MODE, HW, EM, STATS>())) 
         const uint64_t sv[AXS_N] = {s_iter, s_lk, s_rn, s_lkw, s_rnw, s_rwin, s_def, s_fp, s_p2, s_p2v, s_ch, s_seg,
                                     s_qb, s_tal, s_rg, s_spl, s_b4, s_b16, s_b32, s_b64,
                                     lane == 0 ? c_ref : 0ull, lane == 0 ? c_lk : 0ull, lane == 0 ? c_rn : 0ull,
-                                    lane == 0 ? c_p2 : 0ull, lane == 0 ? c_tot : 0ull};
+                                    lane == 0 ? c_p2 : 0ull, lane == 0 ? c_tot : 0ull, s_p2n};
 #pragma unroll
         for (uint32_t i = 0; i < AXS_N; ++i)
             if (sv[i]) atomicAdd(&A.stats[i], (unsigned long long)sv[i]);
