@@ -150,8 +150,10 @@ int speq_scan_reads_device(speq_device_index* d, const uint8_t* d_seq, const uin
  * runs, [14] 16-B granules loaded by runs, [15] lane refills (per wave), [16..19] phase-1 wave iterations
  * with 1-4, 5-16, 17-32, 33-64 busy lanes, [20..24] shader-clock cycles (s_memtime) summed over waves: in refills
  * (staging), phase-1 lookup iterations, phase-1 run iterations, phase 2 (deferred windows), and the whole loop,
- * [25] deferred-window passes (per wave). Fails with SPEQ_E_ARG when the scan does not use that kernel. */
-#define SPEQ_AX_STATS_N 26
+ * [25] deferred-window passes (per wave), [26] cycles of the Bloom-filter part of phase 2, [27] phase-2 probe rounds
+ * of the filter's survivors (per wave), [28] / [29] cycles of refills before their staging loads / in their staging
+ * batches. Fails with SPEQ_E_ARG when the scan does not use that kernel. */
+#define SPEQ_AX_STATS_N 30
 int speq_scan_reads_device_stats(speq_device_index* d, const uint8_t* d_seq, const uint8_t* d_qual,
                                  const uint64_t* d_offsets, uint64_t n_reads, const speq_scan_params* params,
                                  uint64_t* d_counts, double* d_weights, uint64_t* stats);

@@ -71,12 +71,16 @@ constexpr uint32_t AX_VWW = 4;        // valid-window words per lane (>= AX_CAP 
 #ifndef SPEQ_AX_DEF_LOCAL  // deferred-window entries per wave in local mode (A/B knob)
 #define SPEQ_AX_DEF_LOCAL 448
 #endif
+#ifndef SPEQ_AX_DEF_GLOBAL  // the same in global mode (A/B knob; a multiple of 4)
+#define SPEQ_AX_DEF_GLOBAL 896
+#endif
 // deferred-window entries per wave (u16: lane | window << 6): global mode 896 (7.9 KB per wave: 5 blocks of 4 waves
 // per CU); local mode 448, so that its 9.7 KB per wave fit 4 blocks per CU (up to 77 groups)
 template <int MODE>
 constexpr uint32_t ax_def() {
-    return MODE == KM_LOCAL ? SPEQ_AX_DEF_LOCAL : 896u;
+    return MODE == KM_LOCAL ? SPEQ_AX_DEF_LOCAL : SPEQ_AX_DEF_GLOBAL;
 }
+static_assert(SPEQ_AX_DEF_GLOBAL % 4 == 0 && SPEQ_AX_DEF_LOCAL % 4 == 0, "u64 counters after the deferred list");
 constexpr uint32_t AX_F = 4;          // deferred windows a lane tests against the filter per round trip
 constexpr uint32_t AX_EMPTY = 0xFFFFFFFFu;
 constexpr uint16_t AX_VOID = 0xFFFFu;  // a deferred-list slot reserved by a lane that then kept its windows
@@ -121,6 +125,10 @@ enum : uint32_t {
     AXS_CYC_P2,          // ... phase 2 (deferred windows)
     AXS_CYC_TOTAL,       // ... the whole loop
     AXS_P2_PASSES,       // deferred-window passes (per wave)
+    AXS_CYC_P2_FILTER,   // ... the Bloom-filter part of phase 2
+    AXS_P2_ROUNDS,       // phase-2 probe rounds of the survivors (per wave; a round is bucket + granule loads)
+    AXS_CYC_REF_PRE,     // cycles of refills before the staging loads (unit hand-out, read offsets, chunk prefix sums)
+    AXS_CYC_REF_STAGE,   // ... their staging batches (loads + decode)
     AXS_N
 };
 static_assert(AXS_N == SPEQ_AX_STATS_N, "speq_scan.h SPEQ_AX_STATS_N");
@@ -636,6 +644,9 @@ constexpr uint32_t AX_WPB = SPEQ_AX_WPB, AX_THREADS = 64 * SPEQ_AX_WPB;
 #ifndef SPEQ_AX_OFFPF  // 1: single-end refills take the new reads' offsets from a window prefetched during the previous
 #define SPEQ_AX_OFFPF 0   // refill (one dependent round trip less per refill, but 12 B of spills at k <= 32: config 2
 #endif                    // 0.2243 vs 0.2162 ms, profiles/r04/ab_*); 0 (default): load them when needed (A/B knob)
+#ifndef SPEQ_AX_P2_MARGIN  // the deferred-window pass also runs when fewer than this many list entries are free
+#define SPEQ_AX_P2_MARGIN 256u  // (A/B knob; a deferral that finds the list full waits for the pass: lane state 3)
+#endif
 #ifndef SPEQ_AX_PROBE  // timing probes (wrong counts; make axvariant only): 1 staging only, 2 no deferred-window pass,
                        // 3 staging loads only (no decode), 5 as 3 without the valid-window bits, 6 / 7 as 3 without the
                        // doubling steps / the bad-bit reads
@@ -740,9 +751,9 @@ __global__ __launch_bounds__(AX_THREADS, (ax_min_waves<MODE, HW, EM, STATS>())) 
     // diagnostic counters (STATS only; wave-level ones are counted by lane 0)
     uint32_t s_iter = 0, s_lk = 0, s_rn = 0, s_lkw = 0, s_rnw = 0, s_rwin = 0, s_def = 0, s_fp = 0, s_p2 = 0,
              s_p2v = 0, s_ch = 0, s_seg = 0, s_qb = 0, s_tal = 0, s_rg = 0, s_spl = 0, s_b4 = 0, s_b16 = 0, s_b32 = 0,
-             s_b64 = 0, s_p2n = 0;
+             s_b64 = 0, s_p2n = 0, s_p2r = 0;
     // section clocks (STATS only; wave-uniform, kept by every lane, reported by lane 0)
-    uint64_t c_ref = 0, c_lk = 0, c_rn = 0, c_p2 = 0, c_t0 = STATS ? clock64() : 0ull, c_s = 0;
+    uint64_t c_ref = 0, c_lk = 0, c_rn = 0, c_p2 = 0, c_p2f = 0, c_rpre = 0, c_rstg = 0, c_t0 = STATS ? clock64() : 0ull, c_s = 0;
 
     auto add_count = [&](uint32_t g, uint32_t cnt, double wsum) {
         if (LDS_HIST) {
@@ -971,7 +982,7 @@ __global__ __launch_bounds__(AX_THREADS, (ax_min_waves<MODE, HW, EM, STATS>())) 
         // (a lane whose deferral found the list full, st 3, counts as blocked: the list then holds more than AX_DEF
         // entries, so this pass runs, and the lane looks its window up again afterwards)
         const bool p2 = blk != 0 && ((uint32_t)__popcll(blk) >= SPEQ_AX_BLOCKED || busy == 0 ||
-                                     __builtin_amdgcn_readfirstlane(defn[0]) + 256u > AX_DEF);
+                                     __builtin_amdgcn_readfirstlane(defn[0]) + SPEQ_AX_P2_MARGIN > AX_DEF);
         const uint32_t n_def = (SPEQ_AX_MICRO && !p2) ? 0u : __builtin_amdgcn_readfirstlane(defn[0]);
         if (STATS) c_s = clock64();
         if (p2) {
@@ -1021,7 +1032,10 @@ __global__ __launch_bounds__(AX_THREADS, (ax_min_waves<MODE, HW, EM, STATS>())) 
                 wave_sync();
             }
             const uint32_t n3 = __builtin_amdgcn_readfirstlane(defn[1]);
-            if (STATS) s_fp += lane == 0 ? n3 : 0u;
+            if (STATS) {
+                s_fp += lane == 0 ? n3 : 0u;
+                c_p2f += clock64() - c_s;
+            }
             for (uint32_t base = 0; base < n3; base += 64) {
                 const uint32_t idx = base + lane;
                 const bool act = idx < n3;
@@ -1039,6 +1053,7 @@ __global__ __launch_bounds__(AX_THREADS, (ax_min_waves<MODE, HW, EM, STATS>())) 
                 bool pend = act, found = false;
                 uint32_t cl = AX_SENT;
                 while (__ballot(pend) != 0) {
+                    if (STATS) s_p2r += lane == 0 ? 1u : 0u;
                     const bool c = SPEQ_AX_CUCKOO ? ax_probe_ck(rs_atab, fp, b, b2, sl, pp, pg, pend, s_p2)
                                                   : ax_probe(A, rs_atab, fp, b, sl, pp, pg, pend, s_p2);
                     const bool cand = pend && c;
@@ -1268,6 +1283,11 @@ __global__ __launch_bounds__(AX_THREADS, (ax_min_waves<MODE, HW, EM, STATS>())) 
                     }
                 }
             };
+            uint64_t c_b = 0;
+            if (STATS) {
+                c_b = clock64();
+                c_rpre += c_b - c_s;
+            }
             for (uint32_t c0 = 0; c0 < nch_tot; c0 += 64u * SU) {
                 uint4 sv[SU], qv[SU];
                 uint32_t own[SU], ci[SU];
@@ -1275,6 +1295,7 @@ __global__ __launch_bounds__(AX_THREADS, (ax_min_waves<MODE, HW, EM, STATS>())) 
                 decode(c0, sv, qv, own, ci);
             }
             wave_sync();
+            if (STATS) c_rstg += clock64() - c_b;
             if (SPEQ_AX_PROBE == 5 && stg) {  // probe: no valid-window bits either
                 st = 2u;
             } else if (stg) {
@@ -1760,7 +1781,9 @@ __global__ __launch_bounds__(AX_THREADS, (ax_min_waves<MODE, HW, EM, STATS>())) 
         const uint64_t sv[AXS_N] = {s_iter, s_lk, s_rn, s_lkw, s_rnw, s_rwin, s_def, s_fp, s_p2, s_p2v, s_ch, s_seg,
                                     s_qb, s_tal, s_rg, s_spl, s_b4, s_b16, s_b32, s_b64,
                                     lane == 0 ? c_ref : 0ull, lane == 0 ? c_lk : 0ull, lane == 0 ? c_rn : 0ull,
-                                    lane == 0 ? c_p2 : 0ull, lane == 0 ? c_tot : 0ull, s_p2n};
+                                    lane == 0 ? c_p2 : 0ull, lane == 0 ? c_tot : 0ull, s_p2n,
+                                    lane == 0 ? c_p2f : 0ull, s_p2r, lane == 0 ? c_rpre : 0ull,
+                                    lane == 0 ? c_rstg : 0ull};
 #pragma unroll
         for (uint32_t i = 0; i < AXS_N; ++i)
             if (sv[i]) atomicAdd(&A.stats[i], (unsigned long long)sv[i]);
