@@ -152,8 +152,9 @@ int speq_scan_reads_device(speq_device_index* d, const uint8_t* d_seq, const uin
  * (staging), phase-1 lookup iterations, phase-1 run iterations, phase 2 (deferred windows), and the whole loop,
  * [25] deferred-window passes (per wave), [26] cycles of the Bloom-filter part of phase 2, [27] phase-2 probe rounds
  * of the filter's survivors (per wave), [28] / [29] cycles of refills before their staging loads / in their staging
- * batches. Fails with SPEQ_E_ARG when the scan does not use that kernel. */
-#define SPEQ_AX_STATS_N 30
+ * batches, [30] the longest wave's loop cycles (a maximum), [31] waves, [32..36] loop cycles summed over the waves of
+ * blocks 0-255, 256-511, 512-767, 768-1023 and 1024 on. Fails with SPEQ_E_ARG when the scan does not use that kernel. */
+#define SPEQ_AX_STATS_N 37
 int speq_scan_reads_device_stats(speq_device_index* d, const uint8_t* d_seq, const uint8_t* d_qual,
                                  const uint64_t* d_offsets, uint64_t n_reads, const speq_scan_params* params,
                                  uint64_t* d_counts, double* d_weights, uint64_t* stats);

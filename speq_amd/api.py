@@ -193,7 +193,8 @@ class DeviceIndex:
                      "deferred", "filter_pass", "p2_probes", "p2_verify", "chunks", "segments", "qual_bytes",
                      "run_tallied", "run_granules", "refills", "busy_1_4", "busy_5_16", "busy_17_32", "busy_33_64",
                      "cyc_refill", "cyc_lookup", "cyc_run", "cyc_phase2", "cyc_total", "p2_passes",
-                     "cyc_p2_filter", "p2_rounds", "cyc_ref_pre", "cyc_ref_stage")
+                     "cyc_p2_filter", "p2_rounds", "cyc_ref_pre", "cyc_ref_stage", "cyc_wave_max", "waves",
+                     "cyc_gen0", "cyc_gen1", "cyc_gen2", "cyc_gen3", "cyc_gen4")
 
     def scan_device_stats(self, d_seq: int, d_qual: int, d_offsets: int, n_reads: int, k: int, d_counts: int,
                           d_weights: int = 0, phred_cutoff: int = 30, paired: bool = False,

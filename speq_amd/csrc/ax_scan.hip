@@ -129,6 +129,13 @@ enum : uint32_t {
     AXS_P2_ROUNDS,       // phase-2 probe rounds of the survivors (per wave; a round is bucket + granule loads)
     AXS_CYC_REF_PRE,     // cycles of refills before the staging loads (unit hand-out, read offsets, chunk prefix sums)
     AXS_CYC_REF_STAGE,   // ... their staging batches (loads + decode)
+    AXS_CYC_WAVE_MAX,    // the longest wave's loop cycles (max, not a sum: with AXS_CYC_TOTAL / waves, the imbalance)
+    AXS_WAVES,           // waves
+    AXS_CYC_GEN0,        // loop cycles summed over the waves of blocks 0-255 (dispatched first: the oldest waves of
+    AXS_CYC_GEN1,        // their SIMDs), 256-511, 512-767, 768-1023, and 1024 on
+    AXS_CYC_GEN2,
+    AXS_CYC_GEN3,
+    AXS_CYC_GEN4,
     AXS_N
 };
 static_assert(AXS_N == SPEQ_AX_STATS_N, "speq_scan.h SPEQ_AX_STATS_N");
@@ -462,6 +469,8 @@ struct AxView {
     uint64_t n;                // text length
     uint64_t gran_bytes;       // bytes of gran (incl. END padding)
     uint32_t G;
+    unsigned long long* tail;  // the launch's tail counters {units handed out, waves done} (SPEQ_AX_TAIL), zero at entry
+    uint64_t tail_base;        // first unit of the dynamic tail (units before it: the waves' static pools)
 };
 
 // Resolves one anchor bucket (8 slots {pos, fp << 16 | group}) from slot `s` on: the first slot whose fingerprint
@@ -644,6 +653,19 @@ constexpr uint32_t AX_WPB = SPEQ_AX_WPB, AX_THREADS = 64 * SPEQ_AX_WPB;
 #ifndef SPEQ_AX_OFFPF  // 1: single-end refills take the new reads' offsets from a window prefetched during the previous
 #define SPEQ_AX_OFFPF 0   // refill (one dependent round trip less per refill, but 12 B of spills at k <= 32: config 2
 #endif                    // 0.2243 vs 0.2162 ms, profiles/r04/ab_*); 0 (default): load them when needed (A/B knob)
+#ifndef SPEQ_AX_TAIL  // percent of a launch's units handed out at run time, SPEQ_AX_GRAB at a time, to the waves that
+#define SPEQ_AX_TAIL 0  // have finished their static pools (0: every unit in the static pools). A/B knob
+#endif
+#ifndef SPEQ_AX_GRAB
+#define SPEQ_AX_GRAB 32u
+#endif
+constexpr uint32_t AX_TAIL_XCD = 8;  // tail shares (one per XCD of an MI355X)
+#ifndef SPEQ_AX_PRIO  // 1: waves set their issue priority by the share of their pool still to do (A/B knob)
+#define SPEQ_AX_PRIO 1
+#endif
+#ifndef SPEQ_AX_PRIO_MIN
+#define SPEQ_AX_PRIO_MIN 384u
+#endif
 #ifndef SPEQ_AX_P2_MARGIN  // the deferred-window pass also runs when fewer than this many list entries are free
 #define SPEQ_AX_P2_MARGIN 256u  // (A/B knob; a deferral that finds the list full waits for the pass: lane state 3)
 #endif
@@ -903,8 +925,19 @@ __global__ __launch_bounds__(AX_THREADS, (ax_min_waves<MODE, HW, EM, STATS>())) 
     // reads (coalesced staging), and every wave gets the same number of units so the waves finish together (a
     // launch-wide counter handing out groups was slower: one contended atomic address; so were groups of 64-256 units
     // dealt round robin, profiles/r03/ax_variants_owner_group.jsonl)
-    uint64_t cur = (nu * gw) / NWV;  // next unit
-    const uint64_t cur_end = (nu * (gw + 1)) / NWV;
+    // (TAIL) the static pools cover the units before A.tail_base; the rest go, SPEQ_AX_GRAB at a time, to whichever
+    // wave has run out (the waves of a SIMD progress at different rates: issue goes to the oldest first)
+    const uint64_t nst = SPEQ_AX_TAIL ? A.tail_base : nu;
+    uint64_t cur = (nst * gw) / NWV;  // next unit
+    uint64_t cur_end = (nst * (gw + 1)) / NWV;
+    bool tail_done = SPEQ_AX_TAIL == 0;
+    const uint64_t pool_n = cur_end - cur;  // (PRIO) units of the static pool
+    // (PRIO) on for pools of SPEQ_AX_PRIO_MIN units or more (a priority step every few refills) and for k > 64; off for
+    // the small pools of light scans, which it slows (config 2 k = 21 +3.5 %: their refills then come in step)
+    const bool prio_on = pool_n >= SPEQ_AX_PRIO_MIN || HW >= 3;
+    const uint32_t nxq = min(AX_TAIL_XCD, gridDim.x);  // tail shares (every share has blocks)
+    const uint32_t xq = blockIdx.x % nxq;                // the XCD share of the tail: [tq0, tq1)
+    const uint64_t tq0 = nst + ((nu - nst) * xq) / nxq, tq1 = nst + ((nu - nst) * (xq + 1u)) / nxq;
     // ---- phase-1 state of the current piece
     uint32_t wend = 0;         // windows of the piece
     uint32_t off0 = 0;         // first base of the piece in the slot
@@ -968,6 +1001,7 @@ __global__ __launch_bounds__(AX_THREADS, (ax_min_waves<MODE, HW, EM, STATS>())) 
     // (OFFPF) the prefetched window of read offsets, relative to the wave's first read (a wave whose reads span
     // 4 GiB or more loads its offsets directly: pf_ok false)
     constexpr bool OFFPF = SPEQ_AX_OFFPF && !PAIRED;
+    static_assert(!(SPEQ_AX_OFFPF && SPEQ_AX_TAIL), "the offset window assumes one contiguous pool");
     const uint64_t wbase = OFFPF ? src.off[cur] : 0;
     const bool pf_ok = OFFPF && src.off[cur_end] - wbase < (1ull << 32);
     uint32_t pf = (pf_ok && cur + lane <= nu) ? (uint32_t)(src.off[cur + lane] - wbase) : 0u;
@@ -1118,6 +1152,19 @@ __global__ __launch_bounds__(AX_THREADS, (ax_min_waves<MODE, HW, EM, STATS>())) 
         // lanes that can start a piece now: idle, no deferred windows pending, and a next piece of their unit or
         // a unit left in the pool
         const bool ready = st == 2u && !hasdef;
+        if (SPEQ_AX_TAIL && cur >= cur_end && !tail_done && __ballot(ready && !(has_unit && !last_piece)) != 0) {
+            // the next units of the tail (one atomic per SPEQ_AX_GRAB units; at the end of the launch only), from the
+            // share of the wave's XCD (blocks go to the XCDs in turn): one counter per XCD, on its own cache line
+            unsigned long long t0 = 0;
+            if (lane == 0) t0 = atomicAdd(&A.tail[16u * xq], (unsigned long long)SPEQ_AX_GRAB);
+            const uint64_t g0 = tq0 + (uint64_t)__shfl((long long)t0, 0);
+            if (g0 < tq1) {
+                cur = g0;
+                cur_end = min(g0 + (uint64_t)SPEQ_AX_GRAB, tq1);
+            } else {
+                tail_done = true;
+            }
+        }
         const bool more_pool = cur < cur_end;
         const bool wants = ready && ((has_unit && !last_piece) || more_pool);
         const unsigned long long want = __ballot(wants);
@@ -1153,6 +1200,16 @@ __global__ __launch_bounds__(AX_THREADS, (ax_min_waves<MODE, HW, EM, STATS>())) 
                 pf = lane + taken < 64u ? shifted : (idx <= nu ? (uint32_t)(src.off[idx] - wbase) : 0u);
             }
             cur = min(cur + taken, cur_end);
+            if (SPEQ_AX_PRIO && prio_on) {
+                // issue priority by the share of the pool still to do: the SIMD's arbiter favours the oldest wave at
+                // equal priority, so without this the waves dispatched first finish in a third of the time of the
+                // last ones and the SIMD runs the end of the launch with few waves (profiles/r04/stats_gen.jsonl)
+                const uint32_t q = (uint32_t)(((cur_end - cur) * 4u) / (pool_n + 1u));
+                if (q >= 3u) __builtin_amdgcn_s_setprio(3);
+                else if (q == 2u) __builtin_amdgcn_s_setprio(2);
+                else if (q == 1u) __builtin_amdgcn_s_setprio(1);
+                else __builtin_amdgcn_s_setprio(0);
+            }
             bool stg = false;
             if (wants) {
                 if (!has_unit) {
@@ -1770,6 +1827,14 @@ __global__ __launch_bounds__(AX_THREADS, (ax_min_waves<MODE, HW, EM, STATS>())) 
         }
     }
     const uint64_t c_tot = STATS ? clock64() - c_t0 : 0ull;
+    if (SPEQ_AX_TAIL && lane == 0) {  // the XCD share's last wave out resets its counters for the next launch
+        const uint64_t nwx = (uint64_t)AX_WPB * ((gridDim.x - xq + nxq - 1u) / nxq);
+        __threadfence();
+        if (atomicAdd(&A.tail[16u * xq + 1u], 1ull) == nwx - 1) {
+            atomicExch(&A.tail[16u * xq], 0ull);
+            atomicExch(&A.tail[16u * xq + 1u], 0ull);
+        }
+    }
     if (has_unit && ad) atomicAdd(&wsum[1], 1ull);  // the wave's last units
     wave_sync();
     const unsigned long long tsum = wsum[0], asum = wsum[1];
@@ -1783,10 +1848,15 @@ __global__ __launch_bounds__(AX_THREADS, (ax_min_waves<MODE, HW, EM, STATS>())) 
                                     lane == 0 ? c_ref : 0ull, lane == 0 ? c_lk : 0ull, lane == 0 ? c_rn : 0ull,
                                     lane == 0 ? c_p2 : 0ull, lane == 0 ? c_tot : 0ull, s_p2n,
                                     lane == 0 ? c_p2f : 0ull, s_p2r, lane == 0 ? c_rpre : 0ull,
-                                    lane == 0 ? c_rstg : 0ull};
+                                    lane == 0 ? c_rstg : 0ull, 0ull, lane == 0 ? 1ull : 0ull, 0ull, 0ull, 0ull, 0ull,
+                                    0ull};
 #pragma unroll
         for (uint32_t i = 0; i < AXS_N; ++i)
             if (sv[i]) atomicAdd(&A.stats[i], (unsigned long long)sv[i]);
+        if (lane == 0) {
+            atomicMax(&A.stats[AXS_CYC_WAVE_MAX], (unsigned long long)c_tot);
+            atomicAdd(&A.stats[AXS_CYC_GEN0 + min(blockIdx.x / 256u, 4u)], (unsigned long long)c_tot);
+        }
     }
     if (LDS_HIST) {
         __syncthreads();
@@ -2046,6 +2116,19 @@ static bool ensure_ax_em(speq_device_index* d, AxTable* ax, uint32_t k) {
 // src.k; returns false when the caller must use another kernel. With src.ax_stats set (speq_scan_reads_device_stats:
 // a per-call buffer, so concurrent ordinary scans of the replica never see it), the diagnostic instantiation also adds
 // its work counters there.
+// The tail counters of the next launch: one of AX_TAIL_SLOTS sets of AX_TAIL_XCD {handed out, waves done} pairs
+// (128 B apart), in turn (launches on different streams may run together; each leaves its set at zero).
+constexpr uint32_t AX_TAIL_SLOTS = 256;
+unsigned long long* ax_tail_slot(speq_device_index* d) {
+    std::lock_guard<std::mutex> lk(d->ax_mu);
+    if (!d->d_ax_tail) {
+        HIP_OK(hipMalloc(&d->d_ax_tail, AX_TAIL_SLOTS * AX_TAIL_XCD * 128u));
+        d->track(d->d_ax_tail);
+        HIP_OK(hipMemset(d->d_ax_tail, 0, AX_TAIL_SLOTS * AX_TAIL_XCD * 128u));
+    }
+    return d->d_ax_tail + 16u * AX_TAIL_XCD * (d->ax_tail_next++ % AX_TAIL_SLOTS);
+}
+
 bool launch_ax(speq_device_index* d, int mode, bool paired, const UnitSrc& src, hipStream_t st, unsigned long long* a,
                double* w) {
     if (src.n_units >= (1ull << 32)) return false;  // 32-bit read indices in the kernel: the other kernels take it
@@ -2064,6 +2147,13 @@ bool launch_ax(speq_device_index* d, int mode, bool paired, const UnitSrc& src, 
     A.n = d->view.n;
     A.gran_bytes = ax->gran_bytes;
     A.G = d->G;
+    A.tail = nullptr;
+    A.tail_base = 0;
+    if (SPEQ_AX_TAIL) {
+        const uint64_t units = paired ? src.n_units / 2 : src.n_units;
+        A.tail = ax_tail_slot(d);
+        A.tail_base = units - units * SPEQ_AX_TAIL / 100u;
+    }
     const bool lds_hist = d->G <= LDS_HIST_MAX_G;
     const uint32_t hist_words = lds_hist ? (mode == KM_GLOBAL ? d->G : 2u * d->G) : 0u;
     const size_t lds = ((hist_words * 8u + 15u) & ~15u) + (mode == KM_LOCAL ? QTAB_BYTES : 0u) +

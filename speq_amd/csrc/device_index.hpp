@@ -100,6 +100,8 @@ struct speq_device_index {
     uint32_t blocks_per_cu_ax = 0;  // tuning "blocks_per_cu_ax" (0: as many as registers/LDS allow)
     std::mutex ax_mu;
     std::map<uint32_t, speq::AxTable> axtabs;
+    unsigned long long* d_ax_tail = nullptr;  // k_scan_ax tail counters (ax_tail_slot), allocated on first use
+    uint32_t ax_tail_next = 0;
     std::mutex events_mu;  // launches may come from several host threads (pipelines, concurrent scans)
     std::vector<std::pair<hipEvent_t, hipEvent_t>> events;
     double timed_ms = 0.0;
