@@ -663,6 +663,9 @@ constexpr uint32_t AX_TAIL_XCD = 8;  // tail shares (one per XCD of an MI355X)
 #ifndef SPEQ_AX_PRIO  // 1: waves set their issue priority by the share of their pool still to do (A/B knob)
 #define SPEQ_AX_PRIO 1
 #endif
+#ifndef SPEQ_AX_GENW  // pools weighted by dispatch generation where PRIO is off (0: equal pools). A/B knob
+#define SPEQ_AX_GENW 0
+#endif
 #ifndef SPEQ_AX_PRIO_MIN
 #define SPEQ_AX_PRIO_MIN 384u
 #endif
@@ -935,6 +938,20 @@ __global__ __launch_bounds__(AX_THREADS, (ax_min_waves<MODE, HW, EM, STATS>())) 
     // (PRIO) on for pools of SPEQ_AX_PRIO_MIN units or more (a priority step every few refills) and for k > 64; off for
     // the small pools of light scans, which it slows (config 2 k = 21 +3.5 %: their refills then come in step)
     const bool prio_on = pool_n >= SPEQ_AX_PRIO_MIN || HW >= 3;
+    if (SPEQ_AX_GENW && !prio_on) {
+        // (GENW) pools weighted by dispatch generation (blocks 0-255 first, ...: the older waves of a SIMD, which the
+        // arbiter favours, take more units): weight 10 + GENW per generation younger than the last, in tenths
+        const uint32_t ng = (gridDim.x + 255u) / 256u;
+        auto pre = [&](uint64_t w) -> uint64_t {  // summed weights of the waves before wave w
+            const uint64_t g = w / (256u * AX_WPB), in = w - g * 256u * AX_WPB;
+            // generations before g are full (256 blocks); weight of generation x: 10 + GENW (ng - 1 - x)
+            const uint64_t full = 256u * AX_WPB * (10u * g + (uint64_t)SPEQ_AX_GENW * (g * (ng - 1u) - g * (g - 1u) / 2u));
+            return full + in * (10u + (uint64_t)SPEQ_AX_GENW * (ng - 1u - g));
+        };
+        const uint64_t wt = pre(NWV);
+        cur = (nst * pre(gw)) / wt;
+        cur_end = (nst * pre(gw + 1u)) / wt;
+    }
     const uint32_t nxq = min(AX_TAIL_XCD, gridDim.x);  // tail shares (every share has blocks)
     const uint32_t xq = blockIdx.x % nxq;                // the XCD share of the tail: [tq0, tq1)
     const uint64_t tq0 = nst + ((nu - nst) * xq) / nxq, tq1 = nst + ((nu - nst) * (xq + 1u)) / nxq;
