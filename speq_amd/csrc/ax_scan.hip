@@ -2184,12 +2184,13 @@ bool launch_ax(speq_device_index* d, int mode, bool paired, const UnitSrc& src, 
         if (pad > lds_launch) lds_launch = pad & ~(size_t)15;
     }
     const uint32_t grid = (uint32_t)blocks;
+    const uint32_t slots = d->n_cus * d->ax_generations;  // (the grid cap: resident blocks per CU x slots)
     if (mode == KM_GLOBAL) {
-        if (paired) ax_launch_mode<KM_GLOBAL, true>(lds_hist, src.k, A, src, grid, lds_launch, st, a, w, d->n_cus);
-        else ax_launch_mode<KM_GLOBAL, false>(lds_hist, src.k, A, src, grid, lds_launch, st, a, w, d->n_cus);
+        if (paired) ax_launch_mode<KM_GLOBAL, true>(lds_hist, src.k, A, src, grid, lds_launch, st, a, w, slots);
+        else ax_launch_mode<KM_GLOBAL, false>(lds_hist, src.k, A, src, grid, lds_launch, st, a, w, slots);
     } else {
-        if (paired) ax_launch_mode<KM_LOCAL, true>(lds_hist, src.k, A, src, grid, lds_launch, st, a, w, d->n_cus);
-        else ax_launch_mode<KM_LOCAL, false>(lds_hist, src.k, A, src, grid, lds_launch, st, a, w, d->n_cus);
+        if (paired) ax_launch_mode<KM_LOCAL, true>(lds_hist, src.k, A, src, grid, lds_launch, st, a, w, slots);
+        else ax_launch_mode<KM_LOCAL, false>(lds_hist, src.k, A, src, grid, lds_launch, st, a, w, slots);
     }
     HIP_OK(hipGetLastError());
     return true;

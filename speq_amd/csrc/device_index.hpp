@@ -98,6 +98,8 @@ struct speq_device_index {
                                     // default, ax_scan.hip: cuckoo 88, linear probing 35)
     uint32_t grid_blocks_ax = 65535;  // tuning "grid_blocks_ax"
     uint32_t blocks_per_cu_ax = 0;  // tuning "blocks_per_cu_ax" (0: as many as registers/LDS allow)
+    uint32_t ax_generations = 1;    // tuning "ax_generations": grid = this many times the resident blocks (1: one
+                                    // persistent generation; more: smaller pools, freed slots refilled by new blocks)
     std::mutex ax_mu;
     std::map<uint32_t, speq::AxTable> axtabs;
     unsigned long long* d_ax_tail = nullptr;  // k_scan_ax tail counters (ax_tail_slot), allocated on first use

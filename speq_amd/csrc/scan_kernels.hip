@@ -2055,6 +2055,9 @@ int speq_device_set_tuning(speq_device_index* d, const char* key, int64_t value)
         } else if (k == "blocks_per_cu_ax") {
             if (value < 0 || value > 8) throw std::invalid_argument("blocks_per_cu_ax must be in [0, 8]");
             d->blocks_per_cu_ax = (uint32_t)value;
+        } else if (k == "ax_generations") {
+            if (value < 1 || value > 16) throw std::invalid_argument("ax_generations must be in [1, 16]");
+            d->ax_generations = (uint32_t)value;
         } else if (k == "kmer_table") {
             if (value != 0 && value != 1) throw std::invalid_argument("kmer_table must be 0 or 1");
             d->kmer_table = value != 0;
@@ -2096,6 +2099,7 @@ int speq_device_get_tuning(const speq_device_index* d, const char* key, int64_t*
         else if (k == "ax_load") *value = speq::ax_effective_load(d);
         else if (k == "grid_blocks_ax") *value = d->grid_blocks_ax;
         else if (k == "blocks_per_cu_ax") *value = d->blocks_per_cu_ax;
+        else if (k == "ax_generations") *value = d->ax_generations;
         else throw std::invalid_argument("speq_device_get_tuning: unknown key " + k);
     });
 }
