@@ -666,6 +666,9 @@ constexpr uint32_t AX_TAIL_XCD = 8;  // tail shares (one per XCD of an MI355X)
 #ifndef SPEQ_AX_GENW  // pools weighted by dispatch generation where PRIO is off (0: equal pools). A/B knob
 #define SPEQ_AX_GENW 0
 #endif
+#ifndef SPEQ_AX_PRIO_LEVELS  // priority levels used (2..4: the pool split into that many parts, the last at 0)
+#define SPEQ_AX_PRIO_LEVELS 4u
+#endif
 #ifndef SPEQ_AX_PRIO_MIN
 #define SPEQ_AX_PRIO_MIN 384u
 #endif
@@ -1221,7 +1224,7 @@ __global__ __launch_bounds__(AX_THREADS, (ax_min_waves<MODE, HW, EM, STATS>())) 
                 // issue priority by the share of the pool still to do: the SIMD's arbiter favours the oldest wave at
                 // equal priority, so without this the waves dispatched first finish in a third of the time of the
                 // last ones and the SIMD runs the end of the launch with few waves (profiles/r04/stats_gen.jsonl)
-                const uint32_t q = (uint32_t)(((cur_end - cur) * 4u) / (pool_n + 1u));
+                const uint32_t q = (uint32_t)(((cur_end - cur) * SPEQ_AX_PRIO_LEVELS) / (pool_n + 1u));
                 if (q >= 3u) __builtin_amdgcn_s_setprio(3);
                 else if (q == 2u) __builtin_amdgcn_s_setprio(2);
                 else if (q == 1u) __builtin_amdgcn_s_setprio(1);
