@@ -179,6 +179,23 @@ __host__ __device__ __forceinline__ uint32_t ax_fp(uint64_t h) { return (uint32_
 __host__ __device__ __forceinline__ uint32_t ax_fword(uint64_t h, uint64_t nf) {
     return (uint32_t)((((h >> 24) & 0xFFFFFFFFull) * nf) >> 32);
 }
+// (minimizer-keyed filter, k <= 32: `fm` = m > 0) the filter word of a k-mer lies in the 128-B line of its minimizer —
+// the least 32-bit hash over its m-mers — and within the line by the k-mer's own hash: consecutive k-mers of a read
+// mostly share their minimizer (about (k - m + 2) / 2 in a row), so the deferred windows around a sequencing error,
+// which sit next to each other in the deferred list and so in adjacent lanes of one load, share one cache line
+// instead of one line each. w0: the k-mer's 2-bit codes, base i at bits 2i (bases past k ignored). nf: a multiple of 16.
+__host__ __device__ __forceinline__ uint32_t ax_fword_min(uint64_t h, uint64_t w0, uint32_t k, uint32_t m, uint64_t nf) {
+    const uint64_t km = k >= 32u ? w0 : (w0 & ((1ull << (2u * k)) - 1ull));
+    const uint64_t mk = (1ull << (2u * m)) - 1ull;  // (m < 32)
+    uint32_t best = 0xFFFFFFFFu;
+    for (uint32_t j = 0; j + m <= k; ++j) {
+        const uint64_t x = ((km >> (2u * j)) & mk) * 0x9E3779B97F4A7C15ull;
+        const uint32_t hv = (uint32_t)(x >> 32) ^ (uint32_t)(x >> 13);
+        best = hv < best ? hv : best;
+    }
+    const uint64_t line = ((uint64_t)best * (nf >> 4)) >> 32;
+    return (uint32_t)(line * 16u + ((h >> 20) & 15u));
+}
 __host__ __device__ __forceinline__ uint64_t ax_fbits(uint64_t h) {
     return (1ull << (h & 63u)) | (1ull << ((h >> 6) & 63u)) | (1ull << ((h >> 12) & 63u));
 }
@@ -378,14 +395,15 @@ __device__ __forceinline__ void ax_text_words(const uint64_t* __restrict__ t2, u
 __global__ void k_ax_insert(const uint32_t* __restrict__ owner, uint64_t n, const uint64_t* __restrict__ t2, uint32_t k,
                             const uint64_t* __restrict__ text_start, const int32_t* __restrict__ text_group,
                             uint32_t n_texts, unsigned long long* __restrict__ atab, uint64_t nb,
-                            unsigned long long* __restrict__ filt, uint64_t nf) {
+                            unsigned long long* __restrict__ filt, uint64_t nf, uint32_t fm) {
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
         const uint32_t p = owner[i];
         if (p == AX_EMPTY) continue;
         uint64_t w[4];
         ax_text_words<4>(t2, p, w);
         const uint64_t h = ax_hash<4>(w, k);
-        atomicOr(&filt[ax_fword(h, nf)], (unsigned long long)ax_fbits(h));
+        const uint32_t fw = fm ? ax_fword_min(h, w[0], k, fm, nf) : ax_fword(h, nf);
+        atomicOr(&filt[fw], (unsigned long long)ax_fbits(h));
         uint32_t lo = 0, hi = n_texts;  // the last text t with text_start[t] <= p
         while (hi - lo > 1u) {
             const uint32_t mid = (lo + hi) / 2u;
@@ -469,6 +487,7 @@ struct AxView {
     uint64_t n;                // text length
     uint64_t gran_bytes;       // bytes of gran (incl. END padding)
     uint32_t G;
+    uint32_t fmin;             // minimizer length of a minimizer-keyed filter (ax_fword_min), 0: plain filter
     unsigned long long* tail;  // the launch's tail counters {units handed out, waves done} (SPEQ_AX_TAIL), zero at entry
     uint64_t tail_base;        // first unit of the dynamic tail (units before it: the waves' static pools)
 };
@@ -665,6 +684,12 @@ constexpr uint32_t AX_TAIL_XCD = 8;  // tail shares (one per XCD of an MI355X)
 #endif
 #ifndef SPEQ_AX_GENW  // pools weighted by dispatch generation where PRIO is off (0: equal pools). A/B knob
 #define SPEQ_AX_GENW 0
+#endif
+#ifndef SPEQ_AX_FMIN  // 1: minimizer-keyed Bloom filter for k = 24..32 when it is at least SPEQ_AX_FMIN_BYTES (config 5
+#define SPEQ_AX_FMIN 1   // -3.1 %; forced on L2-sized filters it loses 14-36 %: profiles/r04/ab_fmin.jsonl)
+#endif
+#ifndef SPEQ_AX_FMIN_BYTES
+#define SPEQ_AX_FMIN_BYTES (8u << 20)
 #endif
 #ifndef SPEQ_AX_PRIO_LEVELS  // priority levels used (2..4: the pool split into that many parts, the last at 0)
 #define SPEQ_AX_PRIO_LEVELS 4u
@@ -1051,6 +1076,7 @@ __global__ __launch_bounds__(AX_THREADS, (ax_min_waves<MODE, HW, EM, STATS>())) 
                 uint32_t ent[AX_F];
                 uint64_t hh[AX_F];
                 uint64_t fw[AX_F];
+                uint64_t kw[AX_F];  // (minimizer-keyed filter) the entries' first code words
                 // in stages over the AX_F entries (entries, then their slot offsets, then their bases), so each stage's
                 // LDS reads are in flight together instead of one dependent chain per entry
                 uint32_t so[AX_F];
@@ -1067,10 +1093,13 @@ __global__ __launch_bounds__(AX_THREADS, (ax_min_waves<MODE, HW, EM, STATS>())) 
                     uint64_t ra[HW];
                     read_words(ent[t] & 63u, so[t], ra);
                     hh[t] = ax_hash<HW>(ra, k);
+                    kw[t] = ra[0];
                 }
 #pragma unroll
                 for (uint32_t t = 0; t < AX_F; ++t) {
-                    const uint32_t foff = ent[t] != AX_EMPTY ? ax_fword(hh[t], A.nf) * 8u : AX_OOB;
+                    const uint32_t fwi = (HW == 1 && A.fmin) ? ax_fword_min(hh[t], kw[t], k, A.fmin, A.nf)
+                                                             : ax_fword(hh[t], A.nf);
+                    const uint32_t foff = ent[t] != AX_EMPTY ? fwi * 8u : AX_OOB;
                     const u32x2 v = __builtin_amdgcn_raw_buffer_load_b64(rs_filt, foff, 0, 0);
                     fw[t] = (uint64_t)v[0] | ((uint64_t)v[1] << 32);
                 }
@@ -2034,7 +2063,12 @@ AxTable build_ax(speq_device_index* d, uint32_t k) {
         HIP_OK(hipStreamSynchronize(d->stream));
         ax.distinct = distinct;
         constexpr uint32_t SLOTS = SPEQ_AX_CUCKOO ? 4u : 8u, BUCKET_B = 8u * SLOTS;
+        // minimizer-keyed filter (ax_fword_min) for k = 24..32 when the filter outgrows an XCD's L2 share
+        // (SPEQ_AX_FMIN; the cuckoo form keeps the plain filter)
+        ax.fmin = (SPEQ_AX_FMIN && !SPEQ_AX_CUCKOO && k >= 24u && k <= 32u &&
+                   distinct * AX_FILTER_BITS / 8 >= (uint64_t)SPEQ_AX_FMIN_BYTES) ? 16u : 0u;
         ax.nf = std::max<uint64_t>(1, distinct * AX_FILTER_BITS / 64);
+        if (ax.fmin) ax.nf = (ax.nf + 15u) & ~(uint64_t)15u;
         alloc(&ax.filt, ax.nf * 8);
         HIP_OK(hipMemsetAsync(ax.filt, 0, ax.nf * 8, d->stream));
         // cuckoo: a build that leaves a key out (eviction walk too long) is redone at a lower load factor
@@ -2053,7 +2087,7 @@ AxTable build_ax(speq_device_index* d, uint32_t k) {
                 hipLaunchKernelGGL(k_ax_insert, dim3(grid), dim3(256), 0, d->stream, owner, n, d->d_text2, k,
                                    d->d_text_start, d->d_text_group, d->n_texts,
                                    reinterpret_cast<unsigned long long*>(ax.atab), ax.nb,
-                                   reinterpret_cast<unsigned long long*>(ax.filt), ax.nf);
+                                   reinterpret_cast<unsigned long long*>(ax.filt), ax.nf, ax.fmin);
                 HIP_OK(hipGetLastError());
                 HIP_OK(hipStreamSynchronize(d->stream));
                 ax.load = load;
@@ -2164,6 +2198,7 @@ bool launch_ax(speq_device_index* d, int mode, bool paired, const UnitSrc& src, 
     A.stats = src.ax_stats;
     A.nb = ax->nb;
     A.nf = ax->nf;
+    A.fmin = ax->fmin;
     A.n = d->view.n;
     A.gran_bytes = ax->gran_bytes;
     A.G = d->G;

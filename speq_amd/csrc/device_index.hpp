@@ -22,6 +22,7 @@ struct AxTable {
     void* filt = nullptr;      // blocked Bloom filter of the distinct k-mers (one 64-bit word per k-mer, 3 bits)
     uint64_t nb = 0;           // buckets (cuckoo: 32 B, 4 slots; linear probing: 64 B, 8 slots)
     uint32_t load = 0;         // load factor the table was built at (percent)
+    uint32_t fmin = 0;         // minimizer length of a minimizer-keyed filter (ax_scan.hip ax_fword_min), 0: plain
     uint64_t nf = 0;           // filter words
     uint64_t gran_bytes = 0;
     uint64_t distinct = 0;     // distinct k-mers of the texts
