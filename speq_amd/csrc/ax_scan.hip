@@ -685,9 +685,9 @@ constexpr uint32_t AX_TAIL_XCD = 8;  // tail shares (one per XCD of an MI355X)
 #ifndef SPEQ_AX_GENW  // pools weighted by dispatch generation where PRIO is off (0: equal pools). A/B knob
 #define SPEQ_AX_GENW 0
 #endif
-#ifndef SPEQ_AX_FMIN  // 1: minimizer-keyed Bloom filter for k = 24..32 when it is at least SPEQ_AX_FMIN_BYTES (config 5
-#define SPEQ_AX_FMIN 1   // -3.1 %; forced on L2-sized filters it loses 14-36 %: profiles/r04/ab_fmin.jsonl)
-#endif
+#ifndef SPEQ_AX_FMIN  // 1: minimizer-keyed Bloom filter for k = 24..32 when it is at least SPEQ_AX_FMIN_BYTES (A/B knob:
+#define SPEQ_AX_FMIN 0   // config 5 -3.1 % in the probe, but neutral in the bench and +7 % in local mode; forced on
+#endif                   // L2-sized filters it loses 14-36 %: profiles/r04/ab_fmin.jsonl, bench_default_s5.log)
 #ifndef SPEQ_AX_FMIN_BYTES
 #define SPEQ_AX_FMIN_BYTES (8u << 20)
 #endif
@@ -1093,12 +1093,12 @@ __global__ __launch_bounds__(AX_THREADS, (ax_min_waves<MODE, HW, EM, STATS>())) 
                     uint64_t ra[HW];
                     read_words(ent[t] & 63u, so[t], ra);
                     hh[t] = ax_hash<HW>(ra, k);
-                    kw[t] = ra[0];
+                    kw[t] = SPEQ_AX_FMIN ? ra[0] : 0ull;
                 }
 #pragma unroll
                 for (uint32_t t = 0; t < AX_F; ++t) {
-                    const uint32_t fwi = (HW == 1 && A.fmin) ? ax_fword_min(hh[t], kw[t], k, A.fmin, A.nf)
-                                                             : ax_fword(hh[t], A.nf);
+                    const uint32_t fwi = (SPEQ_AX_FMIN && HW == 1 && A.fmin)
+                                             ? ax_fword_min(hh[t], kw[t], k, A.fmin, A.nf) : ax_fword(hh[t], A.nf);
                     const uint32_t foff = ent[t] != AX_EMPTY ? fwi * 8u : AX_OOB;
                     const u32x2 v = __builtin_amdgcn_raw_buffer_load_b64(rs_filt, foff, 0, 0);
                     fw[t] = (uint64_t)v[0] | ((uint64_t)v[1] << 32);
