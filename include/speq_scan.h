@@ -352,7 +352,11 @@ void speq_groupings_free(speq_groupings* g);
  *                  "blocks_per_cu_kt": blocks_per_cu of table scans (default 0: no cap);
  * "stream_lanes" : compute streams of a pipeline created afterwards (speq_pipeline_create, speq_scan_fastq, host
  *                  scans), 1..8 (default 3): consecutive batches are parsed and scanned on them in turn, so the
- *                  short launches of different batches overlap on the CUs. */
+ *                  short launches of different batches overlap on the CUs;
+ * anchor-and-extend scans (k <= 128): "ax_scan" 1 (default) / 0 (other kernels), "ax_load" anchor-table load factor in
+ *                  percent for tables built afterwards, "grid_blocks_ax" grid cap, "blocks_per_cu_ax" resident blocks
+ *                  per CU (0: as registers/LDS allow), "ax_generations" grid = 1..16 times the resident blocks
+ *                  (default 1: one persistent generation); "last_kernel" (read only) the kernel of the last scan. */
 int speq_device_set_tuning(speq_device_index* d, const char* key, int64_t value);
 int speq_device_get_tuning(const speq_device_index* d, const char* key, int64_t* value);
 

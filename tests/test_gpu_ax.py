@@ -233,6 +233,29 @@ def test_device_buffers_and_grid_knobs(small):
         assert (int(c[0]), int(c[1]), c[2:].tolist()) == (T, amb, U.tolist()), (grid, bpc)
 
 
+def test_grid_generations_give_identical_counts(small):
+    """Tuning ax_generations (grid = n x the resident blocks, blocks dispatched as slots free up) and the one-block-per-
+    CU cap change only which wave scans which reads: the counts of every setting equal the default's."""
+    import torch
+    ref, idx = small
+    reads = synth.make_reads(ref, 150_000, err_rate=0.002)
+    d_seq = torch.from_numpy(reads.seq).cuda()
+    d_qual = torch.from_numpy(reads.qual).cuda()
+    d_off = torch.from_numpy(reads.offsets.astype(np.int64)).cuda()
+    dev = DeviceIndex(idx)
+    got = []
+    for bpc, gens in ((0, 1), (1, 1), (1, 2), (1, 3), (0, 4)):
+        dev.tune(blocks_per_cu_ax=bpc, ax_generations=gens)
+        assert dev.tuning("ax_generations") == gens
+        cnt = torch.zeros(6, dtype=torch.int64, device="cuda")
+        dev.scan_device(d_seq.data_ptr(), d_qual.data_ptr(), d_off.data_ptr(), reads.n, 31, cnt.data_ptr())
+        torch.cuda.synchronize()
+        got.append(cnt.cpu().numpy().tolist())
+    assert all(g == got[0] for g in got), got
+    with pytest.raises(Exception):
+        dev.tune(ax_generations=0)
+
+
 @pytest.mark.parametrize("k", [12, 21, 31, 70])
 @pytest.mark.parametrize("paired", [False, True])
 def test_varying_quality_weights_within_the_documented_bound(k, paired):
