@@ -19,8 +19,9 @@ mode) -> `value`. The same run also measures secondary lines (compact objects un
 Weak scaling: every rank scans its own shard of the deterministic read stream.
 
 stdout: ONE compact JSON line on rank 0 (< 8 KB; `compact_result`); the full per-line detail (work counters, U
-vectors, paths) goes to --detail (default profiles/r04/bench_detail_n<N>.json).
-Launch: python bench.py [--gpus 1 --steps K --warmup W]; for N > 1 the driver uses torch.distributed.run.
+vectors, paths) goes to --detail (default profiles/r05/bench_detail_n<N>.json).
+Launch: python bench.py [--gpus N --steps K --warmup W]. N > 1 under torch.distributed.run (WORLD_SIZE must equal N),
+or without a launcher: bench.py then starts torch.distributed.run over N local ranks itself (launch_plan).
 """
 from __future__ import annotations
 
@@ -45,7 +46,11 @@ LINE_LIMIT = 8000      # bytes of the stdout line (the driver parsed 9.3 KB in r
 
 def parse_args(argv=None):
     p = argparse.ArgumentParser()
-    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--gpus", type=int, default=1,
+                   help="ranks (one process per GPU); N > 1 without a launcher starts torch.distributed.run itself")
+    p.add_argument("--transport", default=os.environ.get("SPEQ_BENCH_TRANSPORT", "auto"),
+                   help="N > 1 collective: rccl (one GPU per rank), host (gloo + host sockets; ranks may share a "
+                        "GPU), auto (rccl when every rank has its own GPU)")
     p.add_argument("--steps", type=int, default=20)
     p.add_argument("--warmup", type=int, default=2)
     p.add_argument("--config", type=int, default=2, help="BASELINE.json config number (1-5) of the headline")
@@ -74,7 +79,7 @@ def parse_args(argv=None):
     p.add_argument("--cpu-seconds", type=float, default=15.0, help="target CPU-baseline sample duration (headline)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-pcie", action="store_true", help="skip the PCIe-inclusive host-buffer measurement")
-    p.add_argument("--detail", default="", help="full-detail JSON path (default profiles/r04/bench_detail_n<N>.json)")
+    p.add_argument("--detail", default="", help="full-detail JSON path (default profiles/r05/bench_detail_n<N>.json)")
     return p.parse_args(argv)
 
 
@@ -105,6 +110,54 @@ def cpu_model() -> str:
     return "unknown"
 
 
+class LaunchError(RuntimeError):
+    pass
+
+
+def launch_plan(gpus: int, env) -> str:
+    """What `python bench.py --gpus N` does in this process (decided before anything touches a GPU):
+      "relaunch": N > 1 and no launcher around us (WORLD_SIZE unset) -> start N ranks under torch.distributed.run
+                  as a child process and exit with its status;
+      "run":      this process is one rank of a launcher whose WORLD_SIZE equals --gpus, or the only process (N = 1).
+    A launcher whose WORLD_SIZE differs from --gpus is an error (the line would report the wrong n_gpus)."""
+    if gpus < 1:
+        raise LaunchError(f"--gpus {gpus}: at least one GPU")
+    ws = env.get("WORLD_SIZE")
+    if ws is None or ws == "":
+        return "relaunch" if gpus > 1 else "run"
+    if int(ws) != gpus:
+        raise LaunchError(f"WORLD_SIZE={ws} from the launcher but --gpus {gpus}: they must agree")
+    return "run"
+
+
+def pick_transport(requested: str, world: int, n_devices: int) -> str:
+    """The ranks' collective transport. "rccl": ncclAllReduce over xGMI, one rank per GPU (the product path the
+    driver's 8-GPU run measures); "host": torch.distributed over gloo plus the product's host-socket transport
+    (speq_comm_connect, SPEQ_COMM_HOST), so N ranks can share fewer GPUs (RCCL refuses two ranks on one GPU).
+    "auto": rccl when every rank has its own GPU, else host."""
+    if requested not in ("auto", "rccl", "host"):
+        raise LaunchError(f"--transport {requested}: auto, rccl or host")
+    if world <= 1:
+        return "none"
+    if requested == "auto":
+        return "rccl" if n_devices >= world else "host"
+    return requested
+
+
+def free_port() -> int:
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def relaunch_cmd(gpus: int, argv: list, port: int) -> list:
+    """torch.distributed.run over N local ranks (rendezvous on 127.0.0.1), each running this file with the same
+    arguments; WORLD_SIZE then equals --gpus in every rank."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={gpus}",
+            "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + list(argv)
+
+
 class Ctx:
     def __init__(self, a):
         import torch
@@ -113,29 +166,44 @@ class Ctx:
         self.world = int(os.environ.get("WORLD_SIZE", "1"))
         self.rank = int(os.environ.get("RANK", "0"))
         self.local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-        if self.world > 1:
-            dist.init_process_group("nccl", device_id=torch.device(f"cuda:{self.local_rank}"))
-        torch.cuda.set_device(self.local_rank)
-        self.dev_t = torch.device(f"cuda:{self.local_rank}")
+        n_dev = self.n_dev = torch.cuda.device_count()
+        self.transport = pick_transport(a.transport, self.world, n_dev)
+        # ranks beyond the visible GPUs share them round-robin (host transport only: RCCL needs one GPU per rank)
+        self.device = self.local_rank % max(1, n_dev)
+        if self.transport == "rccl":
+            dist.init_process_group("nccl", device_id=torch.device(f"cuda:{self.device}"))
+        elif self.transport == "host":
+            dist.init_process_group("gloo")
+        torch.cuda.set_device(self.device)
+        self.dev_t = torch.device(f"cuda:{self.device}")
         self.comm = None
-        if self.world > 1:
+        from speq_amd import Comm
+        if self.transport == "rccl":
             # the product's own collective (C ABI speq_allreduce_*, ncclAllReduce over xGMI): rank 0's 128-byte
             # RCCL id reaches the other ranks through torch.distributed, which keeps only the barrier and timing
-            from speq_amd import Comm
             uid = torch.zeros(Comm.ID_BYTES, dtype=torch.uint8, device=self.dev_t)
             if self.rank == 0:
                 uid.copy_(torch.frombuffer(bytearray(Comm.unique_id()), dtype=torch.uint8))
             dist.broadcast(uid, 0)
             self.comm = Comm(self.world, self.rank, bytes(uid.cpu().numpy().tobytes()))
+        elif self.transport == "host":
+            # the same C ABI calls (speq_allreduce_u64/_f64 on the device counters) over the product's host-socket
+            # transport; the rendezvous file is keyed by this launch (torch.distributed.run's port and run id)
+            rdzv = os.path.join(os.environ.get("TMPDIR", "/tmp"),
+                                "speq_bench_rdzv_%s_%s" % (os.environ.get("MASTER_PORT", "0"),
+                                                           os.environ.get("TORCHELASTIC_RUN_ID", "none")))
+            self.comm = Comm.connect(self.world, self.rank, rdzv, device=self.device, transport=Comm.HOST)
 
     def barrier(self):
         if self.world > 1:
             self.dist.barrier()
 
     def allreduce_max(self, x: float) -> float:
-        t = self.torch.tensor([x], dtype=self.torch.float64, device=self.dev_t)
-        if self.world > 1:
-            self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
+        if self.world <= 1:
+            return float(x)
+        dev = self.dev_t if self.transport == "rccl" else "cpu"
+        t = self.torch.tensor([x], dtype=self.torch.float64, device=dev)
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
         return float(t.item())
 
 
@@ -235,10 +303,10 @@ def run_workload(ctx: Ctx, cfg_no: int, k: int, n_reads: int, mode: str, steps: 
         t0 = time.time()
         idx = FmIndex.build(ref.records, ref.groups, G, prefix_q=a.prefix_q, pair_steps=bool(a.pair_steps),
                             label_table="auto" if a.label_table == "auto" else bool(int(a.label_table)),
-                            threads=16, gpu_device=ctx.local_rank if a.gpu_build else None,
+                            threads=16, gpu_device=ctx.device if a.gpu_build else None,
                             triple_steps=bool(a.triple_steps))
         build_s = time.time() - t0
-        dev = DeviceIndex(idx, ctx.local_rank)
+        dev = DeviceIndex(idx, ctx.device)
         if a.ilp:
             dev.tune(ilp=a.ilp)
         dev.tune(kmer_table=a.kmer_table)
@@ -354,15 +422,21 @@ def run_workload(ctx: Ctx, cfg_no: int, k: int, n_reads: int, mode: str, steps: 
             r = dev.scan(seq_b, qual_b, reads.offsets, k=k, paired=paired, local=local)
             dt = time.perf_counter() - t0
             best = dt if best is None else min(best, dt)
-        if r.total != int(counts[0]) and ctx.world == 1:
-            raise RuntimeError("host-buffer scan disagrees with the HBM-resident scan")
+        if ctx.world == 1:  # (at N > 1 the timed counters are the all-reduced sums of every rank)
+            same = (r.total, r.ambiguous, r.unique.tolist()) == (int(counts[0]), int(counts[1]),
+                                                                  [int(x) for x in counts[2:]])
+            if same and local:
+                same = bool(np.allclose(r.weights, weights, rtol=1e-10, atol=0))
+            if not same:
+                raise RuntimeError("host-buffer scan disagrees with the HBM-resident scan (T, ambiguous, U, W)")
         pcie = {"value": kmers_per_step / best, "unit": "k-mers/s", "per_gpu": True,
                 "path": "speq_scan_reads: pageable host arrays -> pinned slots -> H2D (copy stream) || scan",
                 "host_GB_per_s": 2 * len(seq_b) / best / 1e9}
 
     cpu = None
     if with_cpu and ctx.rank == 0 and ctx.world == 1:
-        cpu = cpu_baseline(prepared, reads, k, G, cpu_seconds, local, paired, extra_ports=cpu_extra_ports)
+        cpu = cpu_baseline(prepared, reads, k, G, cpu_seconds, local, paired, extra_ports=cpu_extra_ports,
+                           timed=(counts, weights))
 
     check = {"T": int(counts[0]), "ambiguous": int(counts[1]), "U_sha1": u_sha1(counts[2:]),
              **({"W_sum": float(weights.sum())} if weights is not None else {})}
@@ -388,7 +462,7 @@ def run_workload(ctx: Ctx, cfg_no: int, k: int, n_reads: int, mode: str, steps: 
 def compact_cpu(cpu: dict | None) -> dict | None:
     if not cpu:
         return None
-    return {k: cpu[k] for k in ("value", "unit", "cores", "kind", "sample", "checked") if k in cpu}
+    return {k: cpu[k] for k in ("value", "unit", "cores", "kind", "sample", "checked", "checked_timed") if k in cpu}
 
 
 def compact_line(r: dict) -> dict:
@@ -404,7 +478,7 @@ def compact_line(r: dict) -> dict:
     if "check" in r:
         out["check"] = {k: v for k, v in r["check"].items() if k != "U"}
     if r.get("cpu_baseline"):
-        out["cpu_baseline"] = {k: r["cpu_baseline"][k] for k in ("value", "cores", "kind", "checked")
+        out["cpu_baseline"] = {k: r["cpu_baseline"][k] for k in ("value", "cores", "kind", "checked", "checked_timed")
                                if k in r["cpu_baseline"]}
     return out
 
@@ -438,8 +512,17 @@ def compact_result(head: dict, lines: dict, meta: dict) -> dict:
     return out
 
 
-def main():
-    a = parse_args()
+def main(argv=None):
+    argv = sys.argv[1:] if argv is None else argv
+    a = parse_args(argv)
+    try:
+        plan = launch_plan(a.gpus, os.environ)
+    except LaunchError as e:
+        print(f"bench.py: {e}", file=sys.stderr, flush=True)
+        sys.exit(2)
+    if plan == "relaunch":
+        # nothing has touched a GPU in this process: start the N ranks as a child and exit with its status
+        sys.exit(subprocess.call(relaunch_cmd(a.gpus, argv, free_port())))
     ctx = Ctx(a)
     from speq_amd import synth
 
@@ -501,13 +584,15 @@ def main():
             p5["dev"].close()
 
     if ctx.rank == 0:
-        detail_path = a.detail or os.path.join(ROOT, "profiles", "r04", f"bench_detail_n{ctx.world}.json")
+        detail_path = a.detail or os.path.join(ROOT, "profiles", "r05", f"bench_detail_n{ctx.world}.json")
         config = {
             "workload": head["workload"],
             "k": k, "reads_per_gpu": n_reads, "paired": head["paired"], "mode": a.mode,
             "parallelism": f"dp{ctx.world} (reads sharded, index replicated)",
-            "collective": ("speq_allreduce_u64/_f64 (C ABI; RCCL ncclAllReduce of the G + 2 counters per step)"
-                           if ctx.comm is not None else "none (one GPU)"),
+            "collective": {"rccl": "speq_allreduce_u64/_f64 (C ABI; RCCL ncclAllReduce of the G + 2 counters per step)",
+                           "host": "speq_allreduce_u64/_f64 (C ABI; host-socket transport, ranks share GPUs)",
+                           "none": "none (one GPU)"}[ctx.transport],
+            "gpus_visible": ctx.n_dev, "ranks_per_gpu": -(-ctx.world // max(1, min(ctx.world, ctx.n_dev))),
             "index_build_s": head["index_build_s"], "index_builder": "gpu" if a.gpu_build else "host",
             "fm_text_len": head["fm_text_len"],
             "kmer_table": {"bytes": head["kmer_table"]["bytes"], "build_s": head["kmer_table"]["build_s"]},
@@ -655,14 +740,16 @@ def cli_e2e(prep: dict, k: int, check: dict) -> dict:
 _SEQAN_LIKE = {}
 
 
-def cpu_baseline(prep, reads, k, G, target_s, local, paired=False, extra_ports=False):
+def cpu_baseline(prep, reads, k, G, target_s, local, paired=False, extra_ports=False, timed=None):
     """CPU baseline on this host's cores over a bounded sample of the same reads (rank 0, N = 1 only).
 
     value: oracle/seqan_like.c — the reference's ALGORITHM restated (backward search on a wavelet structure, locate of
     every hit through SA samples every 16 rows, sorted hit lists, first-hit rule), the SURVEY.md 8(d) stand-in for
     the SeqAn3 binary, which cannot be built here (8(c)). Its counts on the sample are checked against the GPU scan of
-    the same sample (`checked`). extra_ports (headline): also oracle/kmer_oracle.c (hash map, no FM-index) and
-    oracle/fm_cpu.c (this build's label-run search on host cores)."""
+    the same sample (`checked`); when the sample is the whole shard, also against the TIMED scan's own counters
+    (`timed` = (counts, weights) of speq_scan_reads_device: T, ambiguous, every U[g], W; `checked_timed`).
+    extra_ports (headline): also oracle/kmer_oracle.c (hash map, no FM-index) and oracle/fm_cpu.c (this build's
+    label-run search on host cores)."""
     from oracle.oracle import Oracle, SeqanLike
     ref, idx, dev = prep["ref"], prep["idx"], prep["dev"]
     hw = host_cpu_info()
@@ -712,8 +799,18 @@ def cpu_baseline(prep, reads, k, G, target_s, local, paired=False, extra_ports=F
         checked = bool(np.allclose(r[3], g.weights, rtol=1e-9, atol=0))
     if not checked:
         raise RuntimeError("CPU baseline (seqan_like) disagrees with the GPU scan on its sample")
+    checked_timed = None
+    if timed is not None and n == units:
+        tc, tw = timed
+        checked_timed = (r[0], r[1], r[2].tolist()) == (int(tc[0]), int(tc[1]), [int(x) for x in tc[2:]])
+        if checked_timed and local:
+            checked_timed = bool(np.allclose(r[3], tw, rtol=1e-9, atol=0))
+        if not checked_timed:
+            raise RuntimeError("CPU baseline (seqan_like) over the whole shard disagrees with the timed "
+                               "speq_scan_reads_device counters")
     unit = "pairs" if paired else "reads"
     out = {"value": v, "unit": "k-mers/s", "cores": threads, "kind": "port", "checked": True,
+           "checked_timed": checked_timed,
            "sample": f"first {n} {unit} x {reps} ({km} k-mers, {t:.1f} s), oracle/seqan_like.c (wavelet backward "
                      f"search + SA-sample-16 locate of every hit + first-hit rule), {threads} threads",
            "host": hw, "index_build_s_untimed": round(sl_build, 1)}

@@ -92,3 +92,45 @@ def test_write_fastq_round_trip(tmp_path):
     assert seq == reads.seq.tobytes()
     assert b"".join(lines[3::4][:2500]) == reads.qual.tobytes()
     assert np.all(np.diff(reads.offsets) == 150)
+
+
+# ---- bench.py --gpus N: who launches the ranks (decided before anything touches a GPU) ----
+
+def test_launch_plan():
+    assert bench.launch_plan(1, {}) == "run"
+    assert bench.launch_plan(8, {}) == "relaunch"  # `python bench.py --gpus 8` starts its own 8 ranks
+    assert bench.launch_plan(2, {"WORLD_SIZE": ""}) == "relaunch"
+    assert bench.launch_plan(8, {"WORLD_SIZE": "8", "RANK": "3"}) == "run"  # a rank of the driver's launcher
+    assert bench.launch_plan(1, {"WORLD_SIZE": "1"}) == "run"
+    for gpus, ws in ((1, "8"), (8, "4"), (2, "1")):
+        with pytest.raises(bench.LaunchError):
+            bench.launch_plan(gpus, {"WORLD_SIZE": ws})
+    with pytest.raises(bench.LaunchError):
+        bench.launch_plan(0, {})
+
+
+def test_pick_transport():
+    assert bench.pick_transport("auto", 1, 1) == "none"
+    assert bench.pick_transport("auto", 8, 8) == "rccl"   # the driver's 8-GPU node: one rank per GPU
+    assert bench.pick_transport("auto", 2, 1) == "host"   # two ranks on the one-GPU box
+    assert bench.pick_transport("host", 8, 8) == "host"
+    assert bench.pick_transport("rccl", 2, 1) == "rccl"   # forced (RCCL will refuse to share the GPU)
+    with pytest.raises(bench.LaunchError):
+        bench.pick_transport("mpi", 2, 2)
+
+
+def test_relaunch_cmd_keeps_the_arguments():
+    cmd = bench.relaunch_cmd(4, ["--gpus", "4", "--steps", "5"], 29555)
+    assert cmd[1:3] == ["-m", "torch.distributed.run"]
+    assert "--nproc-per-node=4" in cmd and "--master-addr=127.0.0.1" in cmd and "--master-port=29555" in cmd
+    assert cmd[-5:] == [os.path.join(ROOT, "bench.py"), "--gpus", "4", "--steps", "5"]
+
+
+def test_world_size_mismatch_exits_nonzero():
+    """A launcher with WORLD_SIZE != --gpus: bench.py refuses before importing torch (no GPU needed)."""
+    import subprocess
+    env = dict(os.environ, WORLD_SIZE="2", RANK="0", LOCAL_RANK="0")
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "8"], env=env,
+                       capture_output=True, text=True, timeout=60)
+    assert p.returncode == 2, (p.returncode, p.stderr[-500:])
+    assert "WORLD_SIZE=2" in p.stderr and p.stdout == ""

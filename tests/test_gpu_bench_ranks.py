@@ -1,0 +1,60 @@
+"""GPU: `python bench.py --gpus 2` on the one-GPU box — the bench's N > 1 path end to end.
+
+Without a launcher bench.py starts torch.distributed.run over two local ranks itself (launch_plan "relaunch"). Both
+ranks share the one GPU, so the transport is "host" (torch.distributed over gloo for the barrier and the
+max-over-ranks timing; the product's speq_allreduce_u64 over its host-socket transport for the counters — the same
+C ABI call the 8-GPU run makes over RCCL). Each rank scans its own shard of the deterministic read stream
+(make_reads(start_index = rank * n)); the line's check must equal ONE process scanning both shards, and n_gpus must
+say 2. Reference reduction replaced: /root/reference/src/fm_scanner.cpp:224-233."""
+import json
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+from speq_amd import DeviceIndex, FmIndex, synth
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import bench  # noqa: E402
+
+READS = 100_000
+
+
+def test_bench_two_ranks_on_one_gpu(tmp_path):
+    detail = tmp_path / "detail.json"
+    cmd = [sys.executable, "-u", os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "3", "--warmup", "1",
+           "--reads", str(READS), "--no-extra", "--no-cpu-baseline", "--no-pcie", "--no-lf-compare",
+           "--detail", str(detail)]
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env["SPEQ_BENCH_NO_STATS"] = "1"
+    p = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=300, cwd=str(tmp_path))
+    assert p.returncode == 0, p.stderr[-3000:]
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, p.stdout[-2000:]  # rank 0 alone prints
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 2 and out["scaling"] == "weak"
+    assert "host-socket" in out["config"]["collective"]
+    assert out["config"]["parallelism"].startswith("dp2")
+
+    # one process, both shards (reads 0 .. 2n-1 of the same stream), same index options as the bench
+    c = synth.CONFIGS[2]
+    ref = synth.make_reference(c["n_variants"], c["n_isolates"], c["length"])
+    idx = FmIndex.build(ref.records, ref.groups, c["n_variants"], prefix_q=12, pair_steps=True, label_table="auto",
+                        threads=16, gpu_device=0, triple_steps=True)
+    dev = DeviceIndex(idx, 0)
+    try:
+        reads = synth.make_reads(ref, 2 * READS, err_rate=0.001)
+        r = dev.scan(reads.seq.tobytes(), reads.qual.tobytes(), reads.offsets, k=21)
+    finally:
+        dev.close()
+    assert out["check"]["T"] == r.total
+    assert out["check"]["ambiguous"] == r.ambiguous
+    assert out["check"]["U_sha1"] == bench.u_sha1(r.unique)
+    kmers = int(np.maximum(np.diff(reads.offsets).astype(np.int64) - 21 + 1, 0).sum())
+    # value = all ranks' k-mers / max-over-ranks time
+    assert out["value"] == pytest.approx(kmers * 3 / (out["ms_per_step"] * 3 / 1e3), rel=1e-6)
