@@ -37,6 +37,7 @@
 #include <chrono>
 #include <climits>
 #include <cstdint>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <stdexcept>
@@ -53,12 +54,12 @@ namespace {
 
 using namespace speq_dev;
 
-#ifndef SPEQ_AX_CUCKOO  // 1: the anchor table is a two-choice cuckoo table of 32-B buckets (4 slots), every key in one
-#define SPEQ_AX_CUCKOO 0  // of its two buckets, both loaded in one round trip; 0 (default): linear probing over 64-B
-#endif                    // buckets (cuckoo loads two lines per lookup: config 5 4.79 vs 3.69 ms, explore_r04)
-#ifndef SPEQ_AX_REP  // which occurrence of a k-mer represents it in the anchor table (A/B knob): 0 the first thread to
-#define SPEQ_AX_REP 2  // claim it, 1 its lowest text position, 2 (default) the median of its SA interval
-#endif
+// Compile-time knobs (A/B only; every one is run through the parity tests forced to a non-default value by
+// tests/test_gpu_ax_knobs.py over `make axknobs` builds): SPEQ_AX_DEF_LOCAL, SPEQ_AX_DEF_GLOBAL, SPEQ_AX_WL,
+// SPEQ_AX_WPB, SPEQ_AX_SU, SPEQ_AX_MIN_WAVES, SPEQ_AX_MIN_WAVES_LOCAL, SPEQ_AX_REFILL, SPEQ_AX_BLOCKED,
+// SPEQ_AX_SPEC_HW, SPEQ_AX_PRIO, SPEQ_AX_PRIO_MIN, SPEQ_AX_P2_MARGIN. Measured losers of rounds 3-4 (a cuckoo anchor
+// table, lowest / first-claimant representatives, a dynamic tail, generation-weighted pools, offset prefetch,
+// speculative runs in global mode, a minimizer-keyed filter) were removed; DESIGN.md §4f keeps their numbers.
 constexpr uint32_t AX_MAX_K = 128;    // longest k the scan takes (AX_CAP - k + 1 windows per segment)
 constexpr uint32_t AX_CAP = 192;      // bases of a read a lane stages at once (longer reads: segments of AX_CAP bases)
 constexpr uint32_t AX_STREAM = AX_CAP + 16;  // staged bases incl. the 16-B alignment slack before the read
@@ -168,33 +169,11 @@ __device__ __forceinline__ uint64_t ax_hash(const uint64_t (&w)[NW], uint32_t k)
 __host__ __device__ __forceinline__ uint32_t ax_bucket(uint64_t h, uint64_t nb) {
     return (uint32_t)(((h >> 32) * nb) >> 32);
 }
-// the second bucket of the cuckoo table: the hash's low 32 bits, spread by an odd multiplier (the first bucket comes
-// from the high 32 bits, the fingerprint from the low 16)
-__host__ __device__ __forceinline__ uint32_t ax_bucket2(uint64_t h, uint64_t nb) {
-    return (uint32_t)(((uint64_t)((uint32_t)h * 0x9E3779B1u) * nb) >> 32);
-}
 // slot fingerprint: the hash's low 16 bits (the bucket comes from its high 32)
 __host__ __device__ __forceinline__ uint32_t ax_fp(uint64_t h) { return (uint32_t)h & 0xFFFFu; }
 // Bloom filter of the distinct k-mers: one 64-bit word per key, three bits in it
 __host__ __device__ __forceinline__ uint32_t ax_fword(uint64_t h, uint64_t nf) {
     return (uint32_t)((((h >> 24) & 0xFFFFFFFFull) * nf) >> 32);
-}
-// (minimizer-keyed filter, k <= 32: `fm` = m > 0) the filter word of a k-mer lies in the 128-B line of its minimizer —
-// the least 32-bit hash over its m-mers — and within the line by the k-mer's own hash: consecutive k-mers of a read
-// mostly share their minimizer (about (k - m + 2) / 2 in a row), so the deferred windows around a sequencing error,
-// which sit next to each other in the deferred list and so in adjacent lanes of one load, share one cache line
-// instead of one line each. w0: the k-mer's 2-bit codes, base i at bits 2i (bases past k ignored). nf: a multiple of 16.
-__host__ __device__ __forceinline__ uint32_t ax_fword_min(uint64_t h, uint64_t w0, uint32_t k, uint32_t m, uint64_t nf) {
-    const uint64_t km = k >= 32u ? w0 : (w0 & ((1ull << (2u * k)) - 1ull));
-    const uint64_t mk = (1ull << (2u * m)) - 1ull;  // (m < 32)
-    uint32_t best = 0xFFFFFFFFu;
-    for (uint32_t j = 0; j + m <= k; ++j) {
-        const uint64_t x = ((km >> (2u * j)) & mk) * 0x9E3779B97F4A7C15ull;
-        const uint32_t hv = (uint32_t)(x >> 32) ^ (uint32_t)(x >> 13);
-        best = hv < best ? hv : best;
-    }
-    const uint64_t line = ((uint64_t)best * (nf >> 4)) >> 32;
-    return (uint32_t)(line * 16u + ((h >> 20) & 15u));
 }
 __host__ __device__ __forceinline__ uint64_t ax_fbits(uint64_t h) {
     return (1ull << (h & 63u)) | (1ull << ((h >> 6) & 63u)) | (1ull << ((h >> 12) & 63u));
@@ -294,14 +273,15 @@ __device__ int ax_search_text(const DevView& I, const Rsrc& R, const uint8_t* __
 // Pass A: the class code of the k-mer at every text position (one byte per position, packed into granules by pass
 // B), and one representative position per distinct k-mer (the first to claim owner[lo] of its SA interval).
 //
-// The representative (SPEQ_AX_REP = 2) is the occurrence at the MEDIAN rank of the k-mer's SA interval, SA[(lo + hi -
+// The representative is the occurrence at the MEDIAN rank of the k-mer's SA interval, SA[(lo + hi -
 // 1) / 2]. Within the interval the suffixes are sorted by the text that follows the k-mer, so occurrences that share
 // their continuation form contiguous groups, and whenever one continuation is shared by more than half of the
 // occurrences, the median lies in it, base after base: the representative follows the consensus of the records that
 // contain the k-mer. A read run from it breaks only where the read's record leaves that consensus (its own SNPs),
 // not wherever an arbitrary representative's record has one — fewer lookups and runs per read (simulated on config 2:
 // 1.99 -> 1.76 runs per read against a uniformly random occurrence, 3.13 for the lowest position; the first
-// claimant of round 3 leaned towards the lowest: config 5 measured 3.6). sa == nullptr: the first claimant.
+// claimant of round 3 leaned towards the lowest: config 5 measured 3.6). sa == nullptr (the replica's suffix array did
+// not fit the free HBM): the first thread to claim the interval.
 __global__ void k_ax_classify(DevView I, const uint8_t* __restrict__ text, const uint64_t* __restrict__ tbad,
                               uint64_t n, uint32_t k, uint8_t* __restrict__ codes, uint32_t* __restrict__ owner,
                               const uint32_t* __restrict__ sa, unsigned long long* __restrict__ n_distinct) {
@@ -328,12 +308,8 @@ __global__ void k_ax_classify(DevView I, const uint8_t* __restrict__ text, const
         const int g = ax_search_text(I, R, text + pos, k, lo, hi);
         // g == -1 cannot happen: the window occurs at pos; g >= 0 is the group of pos's text
         codes[pos] = (uint8_t)(g >= 0 ? AX_OWN : AX_MULTI);
-        if (SPEQ_AX_REP == 1) {
-            if (atomicMin(&owner[lo], (uint32_t)pos) == AX_EMPTY) ++claimed;
-        } else {
-            const uint32_t rp = (SPEQ_AX_REP == 2 && sa != nullptr) ? sa[lo + (hi - lo - 1u) / 2u] : (uint32_t)pos;
-            if (atomicCAS(&owner[lo], AX_EMPTY, rp) == AX_EMPTY) ++claimed;
-        }
+        const uint32_t rp = sa != nullptr ? sa[lo + (hi - lo - 1u) / 2u] : (uint32_t)pos;
+        if (atomicCAS(&owner[lo], AX_EMPTY, rp) == AX_EMPTY) ++claimed;
     }
     if (claimed) atomicAdd(n_distinct, claimed);
 }
@@ -395,15 +371,14 @@ __device__ __forceinline__ void ax_text_words(const uint64_t* __restrict__ t2, u
 __global__ void k_ax_insert(const uint32_t* __restrict__ owner, uint64_t n, const uint64_t* __restrict__ t2, uint32_t k,
                             const uint64_t* __restrict__ text_start, const int32_t* __restrict__ text_group,
                             uint32_t n_texts, unsigned long long* __restrict__ atab, uint64_t nb,
-                            unsigned long long* __restrict__ filt, uint64_t nf, uint32_t fm) {
+                            unsigned long long* __restrict__ filt, uint64_t nf) {
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
         const uint32_t p = owner[i];
         if (p == AX_EMPTY) continue;
         uint64_t w[4];
         ax_text_words<4>(t2, p, w);
         const uint64_t h = ax_hash<4>(w, k);
-        const uint32_t fw = fm ? ax_fword_min(h, w[0], k, fm, nf) : ax_fword(h, nf);
-        atomicOr(&filt[fw], (unsigned long long)ax_fbits(h));
+        atomicOr(&filt[ax_fword(h, nf)], (unsigned long long)ax_fbits(h));
         uint32_t lo = 0, hi = n_texts;  // the last text t with text_start[t] <= p
         while (hi - lo > 1u) {
             const uint32_t mid = (lo + hi) / 2u;
@@ -416,58 +391,6 @@ __global__ void k_ax_insert(const uint32_t* __restrict__ owner, uint64_t n, cons
         for (bool placed = false; !placed; b = (b + 1u == nb) ? 0u : b + 1u)
             for (uint32_t j = 0; j < 8u && !placed; ++j)
                 placed = atomicCAS(&atab[(uint64_t)b * 8u + j], AX_SLOT_EMPTY, v) == AX_SLOT_EMPTY;
-    }
-}
-
-// Pass C, cuckoo form (SPEQ_AX_CUCKOO): every representative goes into one of its two 32-B buckets (ax_bucket,
-// ax_bucket2; 4 slots each): an empty slot of either, else it takes a slot of the bucket it was not evicted from and
-// carries the slot's previous key on to that key's other bucket (atomicExch: every key is always in the table or
-// carried by exactly one thread). A key is found by loading both buckets, so a lookup is one round trip at any load
-// factor; the table is filled to 85-90 % (8.9-9.4 B per k-mer against 23 B for linear probing at 35 %). A thread
-// that is still carrying a key after max_iter evictions counts a failure: the host rebuilds at a lower load.
-__global__ void k_ax_insert_ck(const uint32_t* __restrict__ owner, uint64_t n, const uint64_t* __restrict__ t2,
-                               uint32_t k, const uint64_t* __restrict__ text_start,
-                               const int32_t* __restrict__ text_group, uint32_t n_texts,
-                               unsigned long long* __restrict__ atab, uint64_t nb, unsigned long long* __restrict__ filt,
-                               uint64_t nf, uint32_t max_iter, unsigned long long* __restrict__ n_fail) {
-    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
-        const uint32_t p = owner[i];
-        if (p == AX_EMPTY) continue;
-        uint64_t w[4];
-        ax_text_words<4>(t2, p, w);
-        uint64_t h = ax_hash<4>(w, k);
-        atomicOr(&filt[ax_fword(h, nf)], (unsigned long long)ax_fbits(h));
-        uint32_t lo = 0, hi = n_texts;  // the last text t with text_start[t] <= p
-        while (hi - lo > 1u) {
-            const uint32_t mid = (lo + hi) / 2u;
-            if (text_start[mid] <= p) lo = mid;
-            else hi = mid;
-        }
-        const uint32_t grp = (uint32_t)text_group[lo] & 0xFFFFu;
-        unsigned long long cur = ((unsigned long long)((ax_fp(h) << 16) | grp) << 32) | p;
-        uint32_t from = AX_EMPTY;  // the bucket the carried key was evicted from
-        bool placed = false;
-        for (uint32_t it = 0; it < max_iter && !placed; ++it) {
-            const uint32_t b1 = ax_bucket(h, nb), b2 = ax_bucket2(h, nb);
-            const uint32_t first = from == b1 ? b2 : b1, second = first == b1 ? b2 : b1;
-            for (uint32_t j = 0; j < 8u && !placed; ++j) {
-                const uint32_t b = j < 4u ? first : second;
-                placed = atomicCAS(&atab[(uint64_t)b * 4u + (j & 3u)], AX_SLOT_EMPTY, cur) == AX_SLOT_EMPTY;
-            }
-            if (placed) break;
-            // both buckets full: take a slot of `first` (not where this key came from) and carry its key
-            const uint32_t sl = (uint32_t)(h >> 20) + it;
-            const unsigned long long old = atomicExch(&atab[(uint64_t)first * 4u + (sl & 3u)], cur);
-            if (old == AX_SLOT_EMPTY) {
-                placed = true;
-                break;
-            }
-            cur = old;
-            from = first;
-            ax_text_words<4>(t2, (uint32_t)old, w);
-            h = ax_hash<4>(w, k);
-        }
-        if (!placed) atomicAdd(n_fail, 1ull);
     }
 }
 
@@ -487,9 +410,6 @@ struct AxView {
     uint64_t n;                // text length
     uint64_t gran_bytes;       // bytes of gran (incl. END padding)
     uint32_t G;
-    uint32_t fmin;             // minimizer length of a minimizer-keyed filter (ax_fword_min), 0: plain filter
-    unsigned long long* tail;  // the launch's tail counters {units handed out, waves done} (SPEQ_AX_TAIL), zero at entry
-    uint64_t tail_base;        // first unit of the dynamic tail (units before it: the waves' static pools)
 };
 
 // Resolves one anchor bucket (8 slots {pos, fp << 16 | group}) from slot `s` on: the first slot whose fingerprint
@@ -523,47 +443,6 @@ __device__ __forceinline__ uint32_t ax_resolve(const u32x4& v0, const u32x4& v1,
         return 1u;
     }
     return fe < 8u ? 0u : 2u;
-}
-
-// Cuckoo form: the 8 slots of a key's two buckets (v0, v1: the first; v2, v3: the second); the first slot from `s` on
-// whose fingerprint matches (empty slots excluded) gives the candidate (1), none: the key is absent (0).
-__device__ __forceinline__ uint32_t ax_resolve_ck(const u32x4& v0, const u32x4& v1, const u32x4& v2, const u32x4& v3,
-                                                  uint32_t fp, uint32_t s, uint32_t& slot, uint32_t& p, uint32_t& g) {
-    const uint32_t pos[8] = {v0[0], v0[2], v1[0], v1[2], v2[0], v2[2], v3[0], v3[2]};
-    const uint32_t fg[8] = {v0[1], v0[3], v1[1], v1[3], v2[1], v2[3], v3[1], v3[3]};
-    uint32_t mm = 0;
-#pragma unroll
-    for (int t = 0; t < 8; ++t) mm |= ((pos[t] != AX_EMPTY && (fg[t] >> 16) == fp) ? 1u : 0u) << t;
-    mm &= s >= 8u ? 0u : ((0xFFu << s) & 0xFFu);
-    if (mm == 0u) return 0u;
-    const uint32_t fm = (uint32_t)__builtin_ctz(mm);
-    uint32_t pp = pos[0], gg = fg[0];
-#pragma unroll
-    for (int t = 1; t < 8; ++t) {
-        pp = fm == (uint32_t)t ? pos[t] : pp;
-        gg = fm == (uint32_t)t ? fg[t] : gg;
-    }
-    p = pp;
-    g = gg & 0xFFFFu;
-    slot = fm;
-    return 1u;
-}
-
-// Phase-2 probe of the cuckoo table: one round trip (both buckets), the first fingerprint match from slot s.
-__device__ __forceinline__ bool ax_probe_ck(const __amdgpu_buffer_rsrc_t& rs_atab, uint32_t fp, uint32_t b1,
-                                            uint32_t b2, uint32_t& s, uint32_t& p, uint32_t& g, bool active,
-                                            uint32_t& probes) {
-    const uint32_t o1 = active ? b1 * 32u : AX_OOB, o2 = active ? b2 * 32u : AX_OOB;
-    const u32x4 v0 = __builtin_amdgcn_raw_buffer_load_b128(rs_atab, o1, 0, 0);
-    const u32x4 v1 = __builtin_amdgcn_raw_buffer_load_b128(rs_atab, o1 + 16u, 0, 0);
-    const u32x4 v2 = __builtin_amdgcn_raw_buffer_load_b128(rs_atab, o2, 0, 0);
-    const u32x4 v3 = __builtin_amdgcn_raw_buffer_load_b128(rs_atab, o2 + 16u, 0, 0);
-    if (!active) return false;
-    ++probes;
-    uint32_t slot = 0;
-    if (ax_resolve_ck(v0, v1, v2, v3, fp, s, slot, p, g) == 0u) return false;
-    s = slot;
-    return true;
 }
 
 // One probe chain of the anchor table from bucket b, slot s (phase 2): stops at the first fingerprint match (found:
@@ -612,10 +491,10 @@ __device__ __forceinline__ bool ax_probe(const AxView& A, const __amdgpu_buffer_
 #endif
 constexpr uint32_t AX_WL = SPEQ_AX_WL, AX_WL_TAKE = AX_WL / 64u;
 static_assert(AX_WL % 64u == 0 && AX_WL_TAKE >= 1u && AX_WL_TAKE <= 7u, "work list: 1-7 blocks per lane per pass");
-#ifndef SPEQ_AX_SU_MAX  // staging batch sizes the owner map holds (A/B knob)
-#define SPEQ_AX_SU_MAX 2
+#ifndef SPEQ_AX_SU  // staging: stream instructions per load batch (A/B knob; 3 at 5 waves spills 20-36 B per lane)
+#define SPEQ_AX_SU 2
 #endif
-constexpr uint32_t AX_OWNB = 64u * SPEQ_AX_SU_MAX;  // bytes of the staging owner map (64 x SPEQ_AX_SU)
+constexpr uint32_t AX_OWNB = 64u * SPEQ_AX_SU;  // bytes of the staging owner map (64 x SPEQ_AX_SU)
 template <int MODE>
 constexpr uint32_t ax_wave_bytes() {
     static_assert(8u * AX_VWW >= 2u * AX_CHUNKS, "the bad-base bits of a staged piece live in its valid-window words");
@@ -627,21 +506,9 @@ constexpr uint32_t ax_wave_bytes() {
 #define SPEQ_AX_WPB 4
 #endif
 constexpr uint32_t AX_WPB = SPEQ_AX_WPB, AX_THREADS = 64 * SPEQ_AX_WPB;
-#ifndef SPEQ_AX_SU  // staging: stream instructions per load batch (A/B knob)
-#define SPEQ_AX_SU 2
-#endif
-#ifndef SPEQ_AX_MIN_WAVES  // minimum waves per SIMD the register allocator must allow, k <= 32 (A/B knob): 5 (96
-#define SPEQ_AX_MIN_WAVES 5   // VGPRs, no spills; LDS fits 5 blocks) is 16 % faster than 4 (profiles/r03/ax_variants_w5)
-#endif
-#ifndef SPEQ_AX_MIN_WAVES4  // the same for 33 <= k <= 64
-#define SPEQ_AX_MIN_WAVES4 5
-#endif
-#ifndef SPEQ_AX_MIN_WAVES5  // 65 <= k <= 96
-#define SPEQ_AX_MIN_WAVES5 5
-#endif
-#ifndef SPEQ_AX_MIN_WAVES6  // and 97 <= k <= 128
-#define SPEQ_AX_MIN_WAVES6 4  // (at 5: 8-24 B of spills per lane)
-#endif
+#ifndef SPEQ_AX_MIN_WAVES  // minimum waves per SIMD the register allocator must allow, global mode, k <= 96 (A/B knob):
+#define SPEQ_AX_MIN_WAVES 5   // 5 (96 VGPRs, no spills; LDS fits 5 blocks) is 16 % faster than 4 (r03/ax_variants_w5);
+#endif                        // 97 <= k <= 128 stays at most 4 (at 5: 8-24 B of spills per lane)
 #ifndef SPEQ_AX_MIN_WAVES_LOCAL  // local (Phred-weighted) mode, every k: 4 (<= 128 VGPRs, no spills; its LDS fits 4
 #define SPEQ_AX_MIN_WAVES_LOCAL 4   // blocks per CU up to 77 groups); the instrumented twin 3
 #endif
@@ -651,68 +518,25 @@ constexpr uint32_t AX_WPB = SPEQ_AX_WPB, AX_THREADS = 64 * SPEQ_AX_WPB;
 #ifndef SPEQ_AX_BLOCKED  // idle lanes waiting for their deferred windows that trigger the deferred-window pass
 #define SPEQ_AX_BLOCKED 16
 #endif
-#ifndef SPEQ_AX_MICRO  // 1: the run's compare is not masked per dword (its first mismatch is clamped to the compared
-#define SPEQ_AX_MICRO 1   // length instead) and the deferred-list length is read only when phase 2 may run (A/B knob)
-#endif
-#ifndef SPEQ_AX_LAZYNV  // 1: a lane looking a window up advances to its next valid window only in lookup iterations
-#define SPEQ_AX_LAZYNV 1   // (0: at the top of every iteration, run iterations included). A/B knob
-#endif
-#ifndef SPEQ_AX_SPECRW  // 1: with LAZYNV, a lookup reads its window's code words together with the valid bits
-#define SPEQ_AX_SPECRW 1
-#endif
-#ifndef SPEQ_AX_REFILL_SYNC  // 1: the refill ends with wave-level LDS fences after the valid-window bits (A/B knob;
-#define SPEQ_AX_REFILL_SYNC 0   // 0: none — every lane writes and then reads only its own column of them)
-#endif
 #ifndef SPEQ_AX_SPEC_HW  // speculative left runs after an absent lookup whose mismatch is unknown, for HW >= this
 #define SPEQ_AX_SPEC_HW 3  // (k > 64 by default; 8 = off), Phred-weighted scans only (A/B knob): k = 70 local -5 % at
 #endif                     // 0.1 % errors, -14 % at 0.5 %; global mode +6 % (8 B of spills; profiles/r04/ab_*)
-#ifndef SPEQ_AX_SPEC_GLOBAL  // 1: speculative left runs in global mode too
-#define SPEQ_AX_SPEC_GLOBAL 0
-#endif
-#ifndef SPEQ_AX_OFFPF  // 1: single-end refills take the new reads' offsets from a window prefetched during the previous
-#define SPEQ_AX_OFFPF 0   // refill (one dependent round trip less per refill, but 12 B of spills at k <= 32: config 2
-#endif                    // 0.2243 vs 0.2162 ms, profiles/r04/ab_*); 0 (default): load them when needed (A/B knob)
-#ifndef SPEQ_AX_TAIL  // percent of a launch's units handed out at run time, SPEQ_AX_GRAB at a time, to the waves that
-#define SPEQ_AX_TAIL 0  // have finished their static pools (0: every unit in the static pools). A/B knob
-#endif
-#ifndef SPEQ_AX_GRAB
-#define SPEQ_AX_GRAB 32u
-#endif
-constexpr uint32_t AX_TAIL_XCD = 8;  // tail shares (one per XCD of an MI355X)
 #ifndef SPEQ_AX_PRIO  // 1: waves set their issue priority by the share of their pool still to do (A/B knob)
 #define SPEQ_AX_PRIO 1
 #endif
-#ifndef SPEQ_AX_GENW  // pools weighted by dispatch generation where PRIO is off (0: equal pools). A/B knob
-#define SPEQ_AX_GENW 0
-#endif
-#ifndef SPEQ_AX_FMIN  // 1: minimizer-keyed Bloom filter for k = 24..32 when it is at least SPEQ_AX_FMIN_BYTES (A/B knob:
-#define SPEQ_AX_FMIN 0   // config 5 -3.1 % in the probe, but neutral in the bench and +7 % in local mode; forced on
-#endif                   // L2-sized filters it loses 14-36 %: profiles/r04/ab_fmin.jsonl, bench_default_s5.log)
-#ifndef SPEQ_AX_FMIN_BYTES
-#define SPEQ_AX_FMIN_BYTES (8u << 20)
-#endif
-#ifndef SPEQ_AX_PRIO_LEVELS  // priority levels used (2..4: the pool split into that many parts, the last at 0)
-#define SPEQ_AX_PRIO_LEVELS 4u
-#endif
-#ifndef SPEQ_AX_PRIO_MIN
+#ifndef SPEQ_AX_PRIO_MIN  // ... for static pools of at least this many units (and always for k > 64)
 #define SPEQ_AX_PRIO_MIN 384u
 #endif
 #ifndef SPEQ_AX_P2_MARGIN  // the deferred-window pass also runs when fewer than this many list entries are free
 #define SPEQ_AX_P2_MARGIN 256u  // (A/B knob; a deferral that finds the list full waits for the pass: lane state 3)
-#endif
-#ifndef SPEQ_AX_PROBE  // timing probes (wrong counts; make axvariant only): 1 staging only, 2 no deferred-window pass,
-                       // 3 staging loads only (no decode), 5 as 3 without the valid-window bits, 6 / 7 as 3 without the
-                       // doubling steps / the bad-bit reads
-#define SPEQ_AX_PROBE 0
 #endif
 // EM scans and the instrumented twin hold more live state: 4 waves (no spills)
 template <int MODE, int HW, bool EM, bool STATS>
 constexpr int ax_min_waves() {
     return MODE == KM_LOCAL ? (STATS ? 3 : SPEQ_AX_MIN_WAVES_LOCAL)
                             : ((EM || STATS) ? 4
-                                             : (HW >= 4 ? SPEQ_AX_MIN_WAVES6
-                                                        : (HW == 3 ? SPEQ_AX_MIN_WAVES5
-                                                                   : (HW >= 2 ? SPEQ_AX_MIN_WAVES4 : SPEQ_AX_MIN_WAVES))));
+                                             : (HW >= 4 ? (SPEQ_AX_MIN_WAVES < 4 ? SPEQ_AX_MIN_WAVES : 4)
+                                                        : SPEQ_AX_MIN_WAVES));
 }
 
 __device__ __forceinline__ uint32_t alignbit(uint32_t hi, uint32_t lo, uint32_t s) {  // ({hi, lo} >> (s & 31))[31:0]
@@ -789,8 +613,7 @@ __global__ __launch_bounds__(AX_THREADS, (ax_min_waves<MODE, HW, EM, STATS>())) 
     const __amdgpu_buffer_rsrc_t rs_gran =
         __builtin_amdgcn_make_buffer_rsrc((void*)A.gran, (short)0, (int)(uint32_t)A.gran_bytes, 0x00020000);
     const __amdgpu_buffer_rsrc_t rs_atab =
-        __builtin_amdgcn_make_buffer_rsrc((void*)A.atab, (short)0, (int)(uint32_t)(A.nb * (SPEQ_AX_CUCKOO ? 32u : 64u)),
-                                          0x00020000);
+        __builtin_amdgcn_make_buffer_rsrc((void*)A.atab, (short)0, (int)(uint32_t)(A.nb * 64u), 0x00020000);
     const __amdgpu_buffer_rsrc_t rs_filt =
         __builtin_amdgcn_make_buffer_rsrc((void*)A.filt, (short)0, (int)(uint32_t)(A.nf * 8u), 0x00020000);
     const uint64_t NWV = (uint64_t)gridDim.x * AX_WPB;
@@ -956,33 +779,12 @@ __global__ __launch_bounds__(AX_THREADS, (ax_min_waves<MODE, HW, EM, STATS>())) 
     // reads (coalesced staging), and every wave gets the same number of units so the waves finish together (a
     // launch-wide counter handing out groups was slower: one contended atomic address; so were groups of 64-256 units
     // dealt round robin, profiles/r03/ax_variants_owner_group.jsonl)
-    // (TAIL) the static pools cover the units before A.tail_base; the rest go, SPEQ_AX_GRAB at a time, to whichever
-    // wave has run out (the waves of a SIMD progress at different rates: issue goes to the oldest first)
-    const uint64_t nst = SPEQ_AX_TAIL ? A.tail_base : nu;
-    uint64_t cur = (nst * gw) / NWV;  // next unit
-    uint64_t cur_end = (nst * (gw + 1)) / NWV;
-    bool tail_done = SPEQ_AX_TAIL == 0;
-    const uint64_t pool_n = cur_end - cur;  // (PRIO) units of the static pool
+    uint64_t cur = (nu * gw) / NWV;  // next unit
+    const uint64_t cur_end = (nu * (gw + 1)) / NWV;
+    const uint64_t pool_n = cur_end - cur;  // (PRIO) units of the pool
     // (PRIO) on for pools of SPEQ_AX_PRIO_MIN units or more (a priority step every few refills) and for k > 64; off for
     // the small pools of light scans, which it slows (config 2 k = 21 +3.5 %: their refills then come in step)
-    const bool prio_on = pool_n >= SPEQ_AX_PRIO_MIN || HW >= 3;
-    if (SPEQ_AX_GENW && !prio_on) {
-        // (GENW) pools weighted by dispatch generation (blocks 0-255 first, ...: the older waves of a SIMD, which the
-        // arbiter favours, take more units): weight 10 + GENW per generation younger than the last, in tenths
-        const uint32_t ng = (gridDim.x + 255u) / 256u;
-        auto pre = [&](uint64_t w) -> uint64_t {  // summed weights of the waves before wave w
-            const uint64_t g = w / (256u * AX_WPB), in = w - g * 256u * AX_WPB;
-            // generations before g are full (256 blocks); weight of generation x: 10 + GENW (ng - 1 - x)
-            const uint64_t full = 256u * AX_WPB * (10u * g + (uint64_t)SPEQ_AX_GENW * (g * (ng - 1u) - g * (g - 1u) / 2u));
-            return full + in * (10u + (uint64_t)SPEQ_AX_GENW * (ng - 1u - g));
-        };
-        const uint64_t wt = pre(NWV);
-        cur = (nst * pre(gw)) / wt;
-        cur_end = (nst * pre(gw + 1u)) / wt;
-    }
-    const uint32_t nxq = min(AX_TAIL_XCD, gridDim.x);  // tail shares (every share has blocks)
-    const uint32_t xq = blockIdx.x % nxq;                // the XCD share of the tail: [tq0, tq1)
-    const uint64_t tq0 = nst + ((nu - nst) * xq) / nxq, tq1 = nst + ((nu - nst) * (xq + 1u)) / nxq;
+    const bool prio_on = pool_n >= (uint64_t)SPEQ_AX_PRIO_MIN || HW >= 3;
     // ---- phase-1 state of the current piece
     uint32_t wend = 0;         // windows of the piece
     uint32_t off0 = 0;         // first base of the piece in the slot
@@ -1005,7 +807,7 @@ __global__ __launch_bounds__(AX_THREADS, (ax_min_waves<MODE, HW, EM, STATS>())) 
     // error, which lies in the window before sp) defers only the windows [sp, sp + e] that hold it, and the rest
     // goes on as a run whose first k bases are still to be compared (ps = AX_PS_FRESH). A speculative run must stay in
     // its anchor's text: an END window among the pending ones defers them instead.
-    constexpr bool SPEC = HW >= SPEQ_AX_SPEC_HW && !EM && (MODE == KM_LOCAL || SPEQ_AX_SPEC_GLOBAL);
+    constexpr bool SPEC = HW >= SPEQ_AX_SPEC_HW && !EM && MODE == KM_LOCAL;
     constexpr uint32_t AX_PS_SPEC = 16u, AX_PS_FRESH = 17u;
     uint32_t sp = 0;  // pending windows [sp, sp + k - 2] of the piece; 0: none
     // defers the valid windows of [lo, hi] (hi - lo <= 127; hi < lo: none) of this lane's piece; when the list has
@@ -1029,7 +831,7 @@ __global__ __launch_bounds__(AX_THREADS, (ax_min_waves<MODE, HW, EM, STATS>())) 
         for (uint64_t t = dm0; t; t &= t - 1) defl[sl++] = (uint16_t)(lane | ((lo + (uint32_t)__builtin_ctzll(t)) << 6));
         for (uint64_t t = dm1; t; t &= t - 1)
             defl[sl++] = (uint16_t)(lane | ((lo + 64u + (uint32_t)__builtin_ctzll(t)) << 6));
-        hasdef = SPEQ_AX_PROBE != 2;
+        hasdef = true;
         if (STATS) s_def += cnt;
         return true;
     };
@@ -1043,26 +845,18 @@ __global__ __launch_bounds__(AX_THREADS, (ax_min_waves<MODE, HW, EM, STATS>())) 
         seg = 0;
     };
     auto start_read = [&](uint64_t r) { start_read_at(r, src.off[r], src.off[r + 1]); };
-    // (OFFPF) the prefetched window of read offsets, relative to the wave's first read (a wave whose reads span
-    // 4 GiB or more loads its offsets directly: pf_ok false)
-    constexpr bool OFFPF = SPEQ_AX_OFFPF && !PAIRED;
-    static_assert(!(SPEQ_AX_OFFPF && SPEQ_AX_TAIL), "the offset window assumes one contiguous pool");
-    const uint64_t wbase = OFFPF ? src.off[cur] : 0;
-    const bool pf_ok = OFFPF && src.off[cur_end] - wbase < (1ull << 32);
-    uint32_t pf = (pf_ok && cur + lane <= nu) ? (uint32_t)(src.off[cur + lane] - wbase) : 0u;
-
     for (;;) {
         // ================= housekeeping (wave-uniform decisions) =================
         const unsigned long long idle = __ballot(st == 2u);
         const unsigned long long blk = __ballot(st >= 2u && hasdef);
         const unsigned long long busy = ~idle;
-        if (SPEQ_AX_PROBE == 2 && lane == 0) defn[0] = 0u;  // probe: deferred windows are dropped
-        // (a lane whose deferral found the list full waits for this pass and then looks its window up again)
         // (a lane whose deferral found the list full, st 3, counts as blocked: the list then holds more than AX_DEF
         // entries, so this pass runs, and the lane looks its window up again afterwards)
         const bool p2 = blk != 0 && ((uint32_t)__popcll(blk) >= SPEQ_AX_BLOCKED || busy == 0 ||
-                                     __builtin_amdgcn_readfirstlane(defn[0]) + SPEQ_AX_P2_MARGIN > AX_DEF);
-        const uint32_t n_def = (SPEQ_AX_MICRO && !p2) ? 0u : __builtin_amdgcn_readfirstlane(defn[0]);
+                                     (uint32_t)__builtin_amdgcn_readfirstlane(defn[0]) + (uint32_t)SPEQ_AX_P2_MARGIN > AX_DEF);
+        // (the list length is read only when the pass runs: an LDS round trip on every iteration's critical path
+        // cost 8-10 %, profiles/r03/ax_variants_micro_interleaved_s3.jsonl)
+        const uint32_t n_def = p2 ? __builtin_amdgcn_readfirstlane(defn[0]) : 0u;
         if (STATS) c_s = clock64();
         if (p2) {
             // ---- phase 2: the deferred windows of the wave. (a) the Bloom filter, AX_F windows per lane per round
@@ -1076,7 +870,6 @@ __global__ __launch_bounds__(AX_THREADS, (ax_min_waves<MODE, HW, EM, STATS>())) 
                 uint32_t ent[AX_F];
                 uint64_t hh[AX_F];
                 uint64_t fw[AX_F];
-                uint64_t kw[AX_F];  // (minimizer-keyed filter) the entries' first code words
                 // in stages over the AX_F entries (entries, then their slot offsets, then their bases), so each stage's
                 // LDS reads are in flight together instead of one dependent chain per entry
                 uint32_t so[AX_F];
@@ -1093,13 +886,10 @@ __global__ __launch_bounds__(AX_THREADS, (ax_min_waves<MODE, HW, EM, STATS>())) 
                     uint64_t ra[HW];
                     read_words(ent[t] & 63u, so[t], ra);
                     hh[t] = ax_hash<HW>(ra, k);
-                    kw[t] = SPEQ_AX_FMIN ? ra[0] : 0ull;
                 }
 #pragma unroll
                 for (uint32_t t = 0; t < AX_F; ++t) {
-                    const uint32_t fwi = (SPEQ_AX_FMIN && HW == 1 && A.fmin)
-                                             ? ax_fword_min(hh[t], kw[t], k, A.fmin, A.nf) : ax_fword(hh[t], A.nf);
-                    const uint32_t foff = ent[t] != AX_EMPTY ? fwi * 8u : AX_OOB;
+                    const uint32_t foff = ent[t] != AX_EMPTY ? ax_fword(hh[t], A.nf) * 8u : AX_OOB;
                     const u32x2 v = __builtin_amdgcn_raw_buffer_load_b64(rs_filt, foff, 0, 0);
                     fw[t] = (uint64_t)v[0] | ((uint64_t)v[1] << 32);
                 }
@@ -1132,13 +922,11 @@ __global__ __launch_bounds__(AX_THREADS, (ax_min_waves<MODE, HW, EM, STATS>())) 
                 const uint64_t h = ax_hash<HW>(ra, k);
                 const uint32_t fp = ax_fp(h);
                 uint32_t b = act ? ax_bucket(h, A.nb) : 0u, sl = 0, pp = 0, pg = 0;
-                const uint32_t b2 = SPEQ_AX_CUCKOO ? ax_bucket2(h, A.nb) : 0u;
                 bool pend = act, found = false;
                 uint32_t cl = AX_SENT;
                 while (__ballot(pend) != 0) {
                     if (STATS) s_p2r += lane == 0 ? 1u : 0u;
-                    const bool c = SPEQ_AX_CUCKOO ? ax_probe_ck(rs_atab, fp, b, b2, sl, pp, pg, pend, s_p2)
-                                                  : ax_probe(A, rs_atab, fp, b, sl, pp, pg, pend, s_p2);
+                    const bool c = ax_probe(A, rs_atab, fp, b, sl, pp, pg, pend, s_p2);
                     const bool cand = pend && c;
                     if (STATS) s_p2v += cand ? 1u : 0u;
                     u32x4 gv[HW + 1];
@@ -1201,19 +989,6 @@ __global__ __launch_bounds__(AX_THREADS, (ax_min_waves<MODE, HW, EM, STATS>())) 
         // lanes that can start a piece now: idle, no deferred windows pending, and a next piece of their unit or
         // a unit left in the pool
         const bool ready = st == 2u && !hasdef;
-        if (SPEQ_AX_TAIL && cur >= cur_end && !tail_done && __ballot(ready && !(has_unit && !last_piece)) != 0) {
-            // the next units of the tail (one atomic per SPEQ_AX_GRAB units; at the end of the launch only), from the
-            // share of the wave's XCD (blocks go to the XCDs in turn): one counter per XCD, on its own cache line
-            unsigned long long t0 = 0;
-            if (lane == 0) t0 = atomicAdd(&A.tail[16u * xq], (unsigned long long)SPEQ_AX_GRAB);
-            const uint64_t g0 = tq0 + (uint64_t)__shfl((long long)t0, 0);
-            if (g0 < tq1) {
-                cur = g0;
-                cur_end = min(g0 + (uint64_t)SPEQ_AX_GRAB, tq1);
-            } else {
-                tail_done = true;
-            }
-        }
         const bool more_pool = cur < cur_end;
         const bool wants = ready && ((has_unit && !last_piece) || more_pool);
         const unsigned long long want = __ballot(wants);
@@ -1235,25 +1010,12 @@ __global__ __launch_bounds__(AX_THREADS, (ax_min_waves<MODE, HW, EM, STATS>())) 
             const uint32_t rank = lanes_below(tk);
             const uint64_t taken = (uint64_t)__popcll(tk);
             if (wants && !has_unit && cur + rank < cur_end) newu = cur + rank;
-            // (OFFPF, single-end) the new units' bounds come from the wave's prefetched window of read offsets (lane
-            // i: off[cur + i] - wbase, loaded during the previous refill's staging), so the staging loads below do not
-            // wait behind a round trip for the offsets; the window then moves on by `taken` units, its top lanes
-            // loading the next offsets (consumed at the next refill)
-            uint32_t pf_s = 0, pf_e = 0;
-            const bool pf_use = OFFPF && pf_ok && taken < 64u;
-            if (OFFPF && pf_ok) {
-                pf_s = (uint32_t)__shfl((int)pf, (int)min(rank, 63u));
-                pf_e = (uint32_t)__shfl((int)pf, (int)min(rank + 1u, 63u));
-                const uint32_t shifted = (uint32_t)__shfl((int)pf, (int)((lane + (uint32_t)taken) & 63u));
-                const uint64_t idx = cur + taken + lane;
-                pf = lane + taken < 64u ? shifted : (idx <= nu ? (uint32_t)(src.off[idx] - wbase) : 0u);
-            }
             cur = min(cur + taken, cur_end);
             if (SPEQ_AX_PRIO && prio_on) {
                 // issue priority by the share of the pool still to do: the SIMD's arbiter favours the oldest wave at
                 // equal priority, so without this the waves dispatched first finish in a third of the time of the
                 // last ones and the SIMD runs the end of the launch with few waves (profiles/r04/stats_gen.jsonl)
-                const uint32_t q = (uint32_t)(((cur_end - cur) * SPEQ_AX_PRIO_LEVELS) / (pool_n + 1u));
+                const uint32_t q = (uint32_t)(((cur_end - cur) * 4u) / (pool_n + 1u));
                 if (q >= 3u) __builtin_amdgcn_s_setprio(3);
                 else if (q == 2u) __builtin_amdgcn_s_setprio(2);
                 else if (q == 1u) __builtin_amdgcn_s_setprio(1);
@@ -1265,8 +1027,7 @@ __global__ __launch_bounds__(AX_THREADS, (ax_min_waves<MODE, HW, EM, STATS>())) 
                     if (newu < nu) {
                         has_unit = true;
                         mate = 0;
-                        if (pf_use) start_read_at(newu, wbase + pf_s, wbase + pf_e);
-                        else start_read(PAIRED ? 2 * newu : newu);
+                        start_read(PAIRED ? 2 * newu : newu);
                         stg = true;
                     }
                 } else if (seg + 1u < nseg) {
@@ -1349,12 +1110,6 @@ __global__ __launch_bounds__(AX_THREADS, (ax_min_waves<MODE, HW, EM, STATS>())) 
 #pragma unroll
                 for (uint32_t u = 0; u < SU; ++u) {
                     const uint32_t c = c0 + 64u * u + lane;
-                    if (SPEQ_AX_PROBE == 3 || SPEQ_AX_PROBE >= 5) {  // probe: the loads only
-                        if (c < nch_tot)
-                            codes[ci[u] * 64u + own[u]] = sv[u].x ^ sv[u].y ^ sv[u].z ^ sv[u].w ^ qv[u].x ^ qv[u].y ^
-                                                          qv[u].z ^ qv[u].w;
-                        continue;
-                    }
                     const uint32_t sd[4] = {sv[u].x, sv[u].y, sv[u].z, sv[u].w};
                     const uint32_t qd[4] = {qv[u].x, qv[u].y, qv[u].z, qv[u].w};
                     uint32_t cw = 0, bad = 0, chb = 0;
@@ -1402,9 +1157,7 @@ __global__ __launch_bounds__(AX_THREADS, (ax_min_waves<MODE, HW, EM, STATS>())) 
             }
             wave_sync();
             if (STATS) c_rstg += clock64() - c_b;
-            if (SPEQ_AX_PROBE == 5 && stg) {  // probe: no valid-window bits either
-                st = 2u;
-            } else if (stg) {
+            if (stg) {
                 // this lane's good-base bits, 16 per chunk from a16 (chunks past its piece are bad), as 8 dwords
                 uint32_t ok[8];
                 {
@@ -1413,14 +1166,14 @@ __global__ __launch_bounds__(AX_THREADS, (ax_min_waves<MODE, HW, EM, STATS>())) 
 #pragma unroll
                     for (uint32_t d = 0; d < 8u; ++d) {
                         const uint32_t b0 = 32u * d;  // dword d: chunks 2d, 2d + 1 (word d / 2 of the lane's column)
-                        uint32_t v = SPEQ_AX_PROBE == 7 ? 0u : vw32[((d >> 1) * 64u + lane) * 2u + (d & 1u)];
+                        uint32_t v = vw32[((d >> 1) * 64u + lane) * 2u + (d & 1u)];
                         v |= nb <= b0 ? ~0u : (nb < b0 + 32u ? ~0u << (nb - b0) : 0u);
                         ok[d] = ~v;
                     }
                 }
                 // valid windows: AND of k consecutive good bits (doubling: shifts of at most 64 bits, one funnel
                 // shift per dword), then aligned to the piece's first base
-                for (uint32_t len = SPEQ_AX_PROBE == 6 ? k : 1u; len < k;) {
+                for (uint32_t len = 1u; len < k;) {
                     const uint32_t sft = min(len, k - len);  // 1 .. 64
                     const uint32_t dw = sft >> 5, bs = sft & 31u;
                     if (dw == 0u) {
@@ -1438,7 +1191,7 @@ __global__ __launch_bounds__(AX_THREADS, (ax_min_waves<MODE, HW, EM, STATS>())) 
                 }
                 // valid-window bits of the piece (window j at bit j): the good-window dwords from slot position
                 // off0 (< 16, so dword d + {0, 1}), none past wend
-                if (SPEQ_AX_REFILL_SYNC) wave_sync();  // (own column: the lane's reads precede its writes anyway)
+                // (no fence: every lane writes and then reads only its own column of the valid-window bits)
                 {
                     uint32_t* vw32 = reinterpret_cast<uint32_t*>(vw);
                     uint32_t tc = 0;  // T (fm_scanner.cpp:164): the piece's passing windows
@@ -1454,16 +1207,13 @@ __global__ __launch_bounds__(AX_THREADS, (ax_min_waves<MODE, HW, EM, STATS>())) 
                 }
                 j = 0;
                 if (SPEC) sp = 0;
-                st = (wend > 0 && SPEQ_AX_PROBE != 1 && SPEQ_AX_PROBE != 3 && SPEQ_AX_PROBE < 6) ? 0u : 2u;
+                st = wend > 0 ? 0u : 2u;
                 verify = false;
                 resume = false;
                 last_mm = -1;
-            } else if (SPEQ_AX_REFILL_SYNC) {
-                wave_sync();
             }
             // the slots' code words were fenced after the decode (phase 2 reads other lanes' slots); the valid-window
             // bits are read by their own lane only
-            if (SPEQ_AX_REFILL_SYNC) wave_sync();
             if (STATS) c_ref += clock64() - c_s;
             continue;  // re-evaluate (lanes whose piece has no window are idle again)
         }
@@ -1475,12 +1225,8 @@ __global__ __launch_bounds__(AX_THREADS, (ax_min_waves<MODE, HW, EM, STATS>())) 
         // of work per iteration, alternating (a lookup is followed by a run and a run by a lookup, so a lane rarely
         // waits): the wave executes the lookup code or the run code, not both under exec masks (the kernel is bound
         // by VALU issue, profiles/r03), and a kind no lane needs is skipped.
-        // (LAZYNV) the next valid window of a lane waiting to look one up is found in the lookup iteration itself, so
-        // a run iteration does not wait for those lanes' LDS reads; such a lane may count as busy one iteration longer
-        if (!SPEQ_AX_LAZYNV && st == 0u) {
-            j = next_valid(lane, j, wend);
-            if (j >= wend) st = 2u;
-        }
+        // the next valid window of a lane waiting to look one up is found in the lookup iteration itself, so a run
+        // iteration does not wait for those lanes' LDS reads; such a lane may count as busy one iteration longer
         const unsigned long long busy1 = __ballot(st != 2u);
         if (busy1 == 0) continue;
         if (STATS && lane == 0) {
@@ -1492,12 +1238,12 @@ __global__ __launch_bounds__(AX_THREADS, (ax_min_waves<MODE, HW, EM, STATS>())) 
         }
         const bool want_lk = __ballot(st == 0u) != 0, want_rn = __ballot(st == 1u) != 0;
         run_phase = run_phase ? !want_lk : want_rn;
-        // (LAZYNV) lookup iterations: the window's code words are read together with its valid bits (the same
+        // lookup iterations: the window's code words are read together with its valid bits (the same
         // window unless it is not valid, then read again), one LDS round trip before the bucket load instead of two
         // (single-end k <= 32 only: elsewhere the words held across the valid-bit search spill)
-        constexpr bool SPEC_RW = SPEQ_AX_SPECRW && HW == 1 && !PAIRED;
+        constexpr bool SPEC_RW = HW == 1 && !PAIRED;
         uint64_t ra[HW];
-        if (SPEQ_AX_LAZYNV && !run_phase && st == 0u) {
+        if (!run_phase && st == 0u) {
             const uint32_t j0 = j;
             if (SPEC_RW) read_words(lane, off0 + j0, ra);
             j = next_valid(lane, j0, wend);
@@ -1516,25 +1262,23 @@ __global__ __launch_bounds__(AX_THREADS, (ax_min_waves<MODE, HW, EM, STATS>())) 
         }
         if (!run_phase) {
             // ---- lookup: hash window j -> bucket (8 slots {pos, fp | group}); resolve
-            if (!SPEQ_AX_LAZYNV || !SPEC_RW) read_words(lane, off0 + j, ra);
+            if (!SPEC_RW) read_words(lane, off0 + j, ra);
             const uint64_t h = ax_hash<HW>(ra, k);
             const uint32_t fp = ax_fp(h);
             if (lk && !resume) {
-                if (!SPEQ_AX_CUCKOO) pb = ax_bucket(h, A.nb);
+                pb = ax_bucket(h, A.nb);
                 ps = 0;
             }
-            // cuckoo: the key's two 32-B buckets (recomputed from the hash each time: no bucket state to keep);
-            // linear probing: the 64-B bucket pb of the probe chain
-            const uint32_t boff = lk ? (SPEQ_AX_CUCKOO ? ax_bucket(h, A.nb) * 32u : pb * 64u) : AX_OOB;
-            const uint32_t boff2 = SPEQ_AX_CUCKOO ? (lk ? ax_bucket2(h, A.nb) * 32u : AX_OOB) : boff + 32u;
+            // the 64-B bucket pb of the probe chain
+            const uint32_t boff = lk ? pb * 64u : AX_OOB;
+            const uint32_t boff2 = boff + 32u;
             const u32x4 q0 = __builtin_amdgcn_raw_buffer_load_b128(rs_atab, boff, 0, 0);
             const u32x4 q1 = __builtin_amdgcn_raw_buffer_load_b128(rs_atab, boff + 16u, 0, 0);
             const u32x4 q2 = __builtin_amdgcn_raw_buffer_load_b128(rs_atab, boff2, 0, 0);
             const u32x4 q3 = __builtin_amdgcn_raw_buffer_load_b128(rs_atab, boff2 + 16u, 0, 0);
             if (lk) {
                 uint32_t slot = 0, cp = 0, cg = 0;
-                const uint32_t res = SPEQ_AX_CUCKOO ? ax_resolve_ck(q0, q1, q2, q3, fp, ps, slot, cp, cg)
-                                                    : ax_resolve(q0, q1, q2, q3, fp, ps, slot, cp, cg);
+                const uint32_t res = ax_resolve(q0, q1, q2, q3, fp, ps, slot, cp, cg);
                 if (res == 1u) {  // candidate: compared with the text in the next iteration
                     p = cp;
                     gt = cg;
@@ -1627,15 +1371,11 @@ __global__ __launch_bounds__(AX_THREADS, (ax_min_waves<MODE, HW, EM, STATS>())) 
                     const uint32_t rdw = alignbit(rw[i + 1], rw[i], rsh);
                     uint32_t x = td ^ rdw;
                     const uint32_t b0 = 16u * (uint32_t)i;
-                    if (!SPEQ_AX_MICRO) {
-                        const uint32_t nb = cl > b0 ? min(cl - b0, 16u) : 0u;  // bases of this dword in the compare
-                        x &= nb >= 16u ? ~0u : ((1u << (2u * nb)) - 1u);
-                    }
                     e = x ? b0 + ((uint32_t)__builtin_ctz(x) >> 1) : e;
                 }
-                // (MICRO) bases past cl compare whatever lies there (zeros past the staged chunks and the loaded
+                // bases past cl compare whatever lies there (zeros past the staged chunks and the loaded
                 // granules): a mismatch among them only matters as "none before cl"
-                if (SPEQ_AX_MICRO) e = min(e, cl);
+                e = min(e, cl);
                 // (SPEC) a speculative run must stay in its anchor's text: an END window (a text end) among the pending
                 // windows [0, pb) defers them, and the anchored window is compared from its own position next
                 bool sep = false;
@@ -1794,7 +1534,7 @@ __global__ __launch_bounds__(AX_THREADS, (ax_min_waves<MODE, HW, EM, STATS>())) 
                             const uint32_t slot = atomicAdd(&defn[0], 1u);
                             if (slot < AX_DEF) {
                                 defl[slot] = (uint16_t)(lane | ((j + d0) << 6));
-                                hasdef = SPEQ_AX_PROBE != 2;
+                                hasdef = true;
                                 if (STATS) s_def += 1u;
                                 j += d0 + 1u;
                                 p += d0 + 1u;
@@ -1876,14 +1616,6 @@ __global__ __launch_bounds__(AX_THREADS, (ax_min_waves<MODE, HW, EM, STATS>())) 
         }
     }
     const uint64_t c_tot = STATS ? clock64() - c_t0 : 0ull;
-    if (SPEQ_AX_TAIL && lane == 0) {  // the XCD share's last wave out resets its counters for the next launch
-        const uint64_t nwx = (uint64_t)AX_WPB * ((gridDim.x - xq + nxq - 1u) / nxq);
-        __threadfence();
-        if (atomicAdd(&A.tail[16u * xq + 1u], 1ull) == nwx - 1) {
-            atomicExch(&A.tail[16u * xq], 0ull);
-            atomicExch(&A.tail[16u * xq + 1u], 0ull);
-        }
-    }
     if (has_unit && ad) atomicAdd(&wsum[1], 1ull);  // the wave's last units
     wave_sync();
     const unsigned long long tsum = wsum[0], asum = wsum[1];
@@ -1979,13 +1711,18 @@ void ax_launch_mode(bool lds_hist, uint32_t k, const AxView& A, const UnitSrc& s
 
 namespace speq {
 
+uint32_t ax_effective_load(const speq_device_index* d) { return d->ax_load ? d->ax_load : 35u; }
+
 // Builds the per-k anchor structures of replica d (blocking, on its stream). Returns a table with ok == false when
 // k, the group count or the index is outside what the scan supports (a structural limit: `transient` false), or
 // the structures would not fit the free HBM at this moment (`transient` true: ensure_ax tries again next time).
-uint32_t ax_effective_load(const speq_device_index* d) {
-    return d->ax_load ? d->ax_load : (SPEQ_AX_CUCKOO ? 88u : 35u);
-}
-
+//
+// The representatives come from the replica's suffix array (k_ax_classify: the median of each k-mer's interval),
+// sorted on the GPU by the index build's prefix doubling into a buffer of this build's own and freed with the other
+// temporaries: it is read only here (about 52 B per symbol of temporaries while it is sorted, 4 B per symbol while
+// the classes are computed). When it does not fit, or the sort fails, the first thread to claim an interval
+// represents it (same classes and counts; only the runs per read differ). SPEQ_INJECT_SA_SORT_FAILURE=1 (tests)
+// makes the sort fail after its buffer was allocated.
 AxTable build_ax(speq_device_index* d, uint32_t k) {
     DeviceGuard g(d->device);
     const auto t0 = std::chrono::steady_clock::now();
@@ -2005,16 +1742,16 @@ AxTable build_ax(speq_device_index* d, uint32_t k) {
     }
     uint32_t* owner = nullptr;
     uint8_t* codes = nullptr;
+    uint32_t* sa = nullptr;
     unsigned long long* d_cnt = nullptr;
     std::vector<void*> mine;  // this table's allocations (tracked by the replica once the table is complete)
     auto cleanup = [&] {
         (void)hipStreamSynchronize(d->stream);
-        if (owner) (void)hipFree(owner);
-        if (codes) (void)hipFree(codes);
-        if (d_cnt) (void)hipFree(d_cnt);
-        owner = nullptr;
-        codes = nullptr;
-        d_cnt = nullptr;
+        for (void** q : {reinterpret_cast<void**>(&owner), reinterpret_cast<void**>(&codes),
+                         reinterpret_cast<void**>(&sa), reinterpret_cast<void**>(&d_cnt)}) {
+            if (*q) (void)hipFree(*q);
+            *q = nullptr;
+        }
     };
     auto alloc = [&](void** pp, uint64_t bytes) {
         HIP_OK(hipMalloc(pp, bytes));
@@ -2031,28 +1768,32 @@ AxTable build_ax(speq_device_index* d, uint32_t k) {
                                nw64);
             HIP_OK(hipGetLastError());
         }
+        HIP_OK(hipMemGetInfo(&free_b, &total_b));
+        if (n * 60 + need < free_b / 10 * 9) {
+            HIP_OK(hipMalloc(&sa, n * 4));
+            try {
+                HIP_OK(hipStreamSynchronize(d->stream));
+                const char* inj = std::getenv("SPEQ_INJECT_SA_SORT_FAILURE");
+                if (inj && inj[0] == '1') throw DeviceError("build_ax: injected suffix-sort failure");
+                gpu_suffix_sort(d->d_text, (uint32_t)n, sa, d->stream, false);
+                HIP_OK(hipStreamSynchronize(d->stream));
+            } catch (const std::exception&) {
+                (void)hipStreamSynchronize(d->stream);
+                (void)hipGetLastError();
+                (void)hipFree(sa);
+                sa = nullptr;  // first claimants represent their k-mers
+            }
+        }
         alloc(&ax.gran, gran_bytes);
         HIP_OK(hipMalloc(&owner, (n + 1) * 4));
         HIP_OK(hipMalloc(&codes, n + 64));
         HIP_OK(hipMalloc(&d_cnt, 8));
         HIP_OK(hipMemsetAsync(owner, 0xFF, (n + 1) * 4, d->stream));
         HIP_OK(hipMemsetAsync(d_cnt, 0, 8, d->stream));
-        if (SPEQ_AX_REP == 2 && !d->d_sa) {
-            // the replica's suffix array (median representatives), once: the GPU prefix-doubling sort of the index
-            // build (build_gpu.hip), about 52 B per symbol of temporary memory; skipped (first claimant) if short
-            HIP_OK(hipMemGetInfo(&free_b, &total_b));
-            if (n * 60 < free_b / 10 * 9) {
-                HIP_OK(hipMalloc(&d->d_sa, n * 4));
-                d->track(d->d_sa);
-                HIP_OK(hipStreamSynchronize(d->stream));
-                gpu_suffix_sort(d->d_text, (uint32_t)n, d->d_sa, d->stream, false);
-                HIP_OK(hipStreamSynchronize(d->stream));
-            }
-        }
         const DevView v = search_view(d, k);
         const uint32_t grid = (uint32_t)std::min<uint64_t>((n + 255) / 256, 16384);
         hipLaunchKernelGGL(k_ax_classify, dim3(grid), dim3(256), 0, d->stream, v, d->d_text, d->d_tbad, n, k, codes,
-                           owner, SPEQ_AX_REP == 2 ? d->d_sa : nullptr, d_cnt);
+                           owner, sa, d_cnt);
         HIP_OK(hipGetLastError());
         const uint32_t pgrid = (uint32_t)std::min<uint64_t>((n_gran + 255) / 256, 16384);
         hipLaunchKernelGGL(k_ax_pack, dim3(pgrid), dim3(256), 0, d->stream, d->d_text2, 2 * nw64, codes, n,
@@ -2061,56 +1802,40 @@ AxTable build_ax(speq_device_index* d, uint32_t k) {
         unsigned long long distinct = 0;
         HIP_OK(hipMemcpyAsync(&distinct, d_cnt, 8, hipMemcpyDeviceToHost, d->stream));
         HIP_OK(hipStreamSynchronize(d->stream));
+        if (sa) {  // read by k_ax_classify only
+            (void)hipFree(sa);
+            sa = nullptr;
+        }
         ax.distinct = distinct;
-        constexpr uint32_t SLOTS = SPEQ_AX_CUCKOO ? 4u : 8u, BUCKET_B = 8u * SLOTS;
-        // minimizer-keyed filter (ax_fword_min) for k = 24..32 when the filter outgrows an XCD's L2 share
-        // (SPEQ_AX_FMIN; the cuckoo form keeps the plain filter)
-        ax.fmin = (SPEQ_AX_FMIN && !SPEQ_AX_CUCKOO && k >= 24u && k <= 32u &&
-                   distinct * AX_FILTER_BITS / 8 >= (uint64_t)SPEQ_AX_FMIN_BYTES) ? 16u : 0u;
+        const uint32_t load = ax_effective_load(d);
         ax.nf = std::max<uint64_t>(1, distinct * AX_FILTER_BITS / 64);
-        if (ax.fmin) ax.nf = (ax.nf + 15u) & ~(uint64_t)15u;
+        ax.nb = std::max<uint64_t>(1, (uint64_t)((double)distinct * 100.0 / (8.0 * load)) + 1);
+        if (ax.nb * 64u >= (1ull << 32) - 64 || ax.nf * 8 >= (1ull << 32) - 64) {
+            // the scan addresses the tables with 32-bit buffer offsets: leave this k to the other kernels
+            cleanup();
+            for (void* q : mine) (void)hipFree(q);
+            return AxTable{};
+        }
+        HIP_OK(hipMemGetInfo(&free_b, &total_b));
+        if (ax.nb * 64u + ax.nf * 8 > free_b / 10 * 9) {  // the table and filter do not fit now: try again later
+            cleanup();
+            for (void* q : mine) (void)hipFree(q);
+            AxTable t;
+            t.transient = true;
+            return t;
+        }
         alloc(&ax.filt, ax.nf * 8);
         HIP_OK(hipMemsetAsync(ax.filt, 0, ax.nf * 8, d->stream));
-        // cuckoo: a build that leaves a key out (eviction walk too long) is redone at a lower load factor
-        for (uint32_t load = ax_effective_load(d);; load = load > 60u ? load - 8u : load / 2u) {
-            ax.nb = std::max<uint64_t>(SPEQ_AX_CUCKOO ? 2 : 1,
-                                       (uint64_t)((double)distinct * 100.0 / ((double)SLOTS * load)) + 1);
-            if (ax.nb * BUCKET_B >= (1ull << 32) - 64 || ax.nf * 8 >= (1ull << 32) - 64) {
-                // the scan addresses the tables with 32-bit buffer offsets: leave this k to the other kernels
-                cleanup();
-                for (void* q : mine) (void)hipFree(q);
-                return AxTable{};
-            }
-            alloc(&ax.atab, ax.nb * BUCKET_B);
-            HIP_OK(hipMemsetAsync(ax.atab, 0xFF, ax.nb * BUCKET_B, d->stream));
-            if (!SPEQ_AX_CUCKOO) {
-                hipLaunchKernelGGL(k_ax_insert, dim3(grid), dim3(256), 0, d->stream, owner, n, d->d_text2, k,
-                                   d->d_text_start, d->d_text_group, d->n_texts,
-                                   reinterpret_cast<unsigned long long*>(ax.atab), ax.nb,
-                                   reinterpret_cast<unsigned long long*>(ax.filt), ax.nf, ax.fmin);
-                HIP_OK(hipGetLastError());
-                HIP_OK(hipStreamSynchronize(d->stream));
-                ax.load = load;
-                break;
-            }
-            HIP_OK(hipMemsetAsync(d_cnt, 0, 8, d->stream));
-            hipLaunchKernelGGL(k_ax_insert_ck, dim3(grid), dim3(256), 0, d->stream, owner, n, d->d_text2, k,
-                               d->d_text_start, d->d_text_group, d->n_texts,
-                               reinterpret_cast<unsigned long long*>(ax.atab), ax.nb,
-                               reinterpret_cast<unsigned long long*>(ax.filt), ax.nf, 512u, d_cnt);
-            HIP_OK(hipGetLastError());
-            unsigned long long failed = 0;
-            HIP_OK(hipMemcpyAsync(&failed, d_cnt, 8, hipMemcpyDeviceToHost, d->stream));
-            HIP_OK(hipStreamSynchronize(d->stream));
-            ax.load = load;
-            if (failed == 0) break;
-            if (load <= 10u) throw DeviceError("build_ax: the cuckoo anchor table could not place every k-mer");
-            (void)hipFree(ax.atab);  // smaller load next: a new table
-            mine.erase(std::find(mine.begin(), mine.end(), ax.atab));
-            ax.atab = nullptr;
-        }
+        alloc(&ax.atab, ax.nb * 64u);
+        HIP_OK(hipMemsetAsync(ax.atab, 0xFF, ax.nb * 64u, d->stream));
+        hipLaunchKernelGGL(k_ax_insert, dim3(grid), dim3(256), 0, d->stream, owner, n, d->d_text2, k, d->d_text_start,
+                           d->d_text_group, d->n_texts, reinterpret_cast<unsigned long long*>(ax.atab), ax.nb,
+                           reinterpret_cast<unsigned long long*>(ax.filt), ax.nf);
+        HIP_OK(hipGetLastError());
+        HIP_OK(hipStreamSynchronize(d->stream));
+        ax.load = load;
         ax.gran_bytes = gran_bytes;
-        ax.bytes = ax.nb * BUCKET_B + ax.nf * 8 + gran_bytes;
+        ax.bytes = ax.nb * 64u + ax.nf * 8 + gran_bytes;
         ax.ok = true;
     } catch (...) {
         cleanup();
@@ -2170,19 +1895,6 @@ static bool ensure_ax_em(speq_device_index* d, AxTable* ax, uint32_t k) {
 // src.k; returns false when the caller must use another kernel. With src.ax_stats set (speq_scan_reads_device_stats:
 // a per-call buffer, so concurrent ordinary scans of the replica never see it), the diagnostic instantiation also adds
 // its work counters there.
-// The tail counters of the next launch: one of AX_TAIL_SLOTS sets of AX_TAIL_XCD {handed out, waves done} pairs
-// (128 B apart), in turn (launches on different streams may run together; each leaves its set at zero).
-constexpr uint32_t AX_TAIL_SLOTS = 256;
-unsigned long long* ax_tail_slot(speq_device_index* d) {
-    std::lock_guard<std::mutex> lk(d->ax_mu);
-    if (!d->d_ax_tail) {
-        HIP_OK(hipMalloc(&d->d_ax_tail, AX_TAIL_SLOTS * AX_TAIL_XCD * 128u));
-        d->track(d->d_ax_tail);
-        HIP_OK(hipMemset(d->d_ax_tail, 0, AX_TAIL_SLOTS * AX_TAIL_XCD * 128u));
-    }
-    return d->d_ax_tail + 16u * AX_TAIL_XCD * (d->ax_tail_next++ % AX_TAIL_SLOTS);
-}
-
 bool launch_ax(speq_device_index* d, int mode, bool paired, const UnitSrc& src, hipStream_t st, unsigned long long* a,
                double* w) {
     if (src.n_units >= (1ull << 32)) return false;  // 32-bit read indices in the kernel: the other kernels take it
@@ -2198,17 +1910,9 @@ bool launch_ax(speq_device_index* d, int mode, bool paired, const UnitSrc& src, 
     A.stats = src.ax_stats;
     A.nb = ax->nb;
     A.nf = ax->nf;
-    A.fmin = ax->fmin;
     A.n = d->view.n;
     A.gran_bytes = ax->gran_bytes;
     A.G = d->G;
-    A.tail = nullptr;
-    A.tail_base = 0;
-    if (SPEQ_AX_TAIL) {
-        const uint64_t units = paired ? src.n_units / 2 : src.n_units;
-        A.tail = ax_tail_slot(d);
-        A.tail_base = units - units * SPEQ_AX_TAIL / 100u;
-    }
     const bool lds_hist = d->G <= LDS_HIST_MAX_G;
     const uint32_t hist_words = lds_hist ? (mode == KM_GLOBAL ? d->G : 2u * d->G) : 0u;
     const size_t lds = ((hist_words * 8u + 15u) & ~15u) + (mode == KM_LOCAL ? QTAB_BYTES : 0u) +

@@ -20,9 +20,8 @@ struct AxTable {
     uint32_t* mhi = nullptr;   // on the first EM scan of k, ensure_ax_em) / its end, indexed by its interval start
     void* atab = nullptr;      // anchor table: 64-B buckets of 8 {representative position, fingerprint, group} slots
     void* filt = nullptr;      // blocked Bloom filter of the distinct k-mers (one 64-bit word per k-mer, 3 bits)
-    uint64_t nb = 0;           // buckets (cuckoo: 32 B, 4 slots; linear probing: 64 B, 8 slots)
+    uint64_t nb = 0;           // buckets (64 B, 8 slots, linear probing)
     uint32_t load = 0;         // load factor the table was built at (percent)
-    uint32_t fmin = 0;         // minimizer length of a minimizer-keyed filter (ax_scan.hip ax_fword_min), 0: plain
     uint64_t nf = 0;           // filter words
     uint64_t gran_bytes = 0;
     uint64_t distinct = 0;     // distinct k-mers of the texts
@@ -92,19 +91,14 @@ struct speq_device_index {
     // anchor-and-extend scan (ax_scan.hip)
     uint64_t* d_text2 = nullptr;    // 2-bit text, built with the first per-k structures
     uint64_t* d_tbad = nullptr;     // bitmap of non-ACGT text positions
-    uint32_t* d_sa = nullptr;       // suffix array (median anchor representatives), sorted on the GPU with the first
-                                    // per-k structures
     bool ax_scan = true;            // tuning "ax_scan": read scans of k <= 128 use k_scan_ax
-    uint32_t ax_load = 0;           // tuning "ax_load": anchor-table load factor, percent (0: the table form's
-                                    // default, ax_scan.hip: cuckoo 88, linear probing 35)
+    uint32_t ax_load = 0;           // tuning "ax_load": anchor-table load factor, percent (0: default 35)
     uint32_t grid_blocks_ax = 65535;  // tuning "grid_blocks_ax"
     uint32_t blocks_per_cu_ax = 0;  // tuning "blocks_per_cu_ax" (0: as many as registers/LDS allow)
     uint32_t ax_generations = 1;    // tuning "ax_generations": grid = this many times the resident blocks (1: one
                                     // persistent generation; more: smaller pools, freed slots refilled by new blocks)
     std::mutex ax_mu;
     std::map<uint32_t, speq::AxTable> axtabs;
-    unsigned long long* d_ax_tail = nullptr;  // k_scan_ax tail counters (ax_tail_slot), allocated on first use
-    uint32_t ax_tail_next = 0;
     std::mutex events_mu;  // launches may come from several host threads (pipelines, concurrent scans)
     std::vector<std::pair<hipEvent_t, hipEvent_t>> events;
     double timed_ms = 0.0;

@@ -1541,6 +1541,11 @@ static int scan_device_impl(speq_device_index* d, const uint8_t* d_seq, const ui
     const int kernel = launch_scan(d, mode, p->paired != 0, src, p->paired ? n_reads / 2 : n_reads, st,
                                    reinterpret_cast<unsigned long long*>(d_counts), nullptr, d_weights);
     if (d->timing) {
+        if (kernel < 0) {  // nothing was launched (ax_stats, the anchor kernel cannot take it): no interval to time
+            (void)hipEventDestroy(e0);
+            (void)hipEventDestroy(e1);
+            return kernel;
+        }
         HIP_OK(hipEventRecord(e1, st));
         std::lock_guard<std::mutex> lk(d->events_mu);
         d->events.emplace_back(e0, e1);

@@ -284,3 +284,22 @@ def test_varying_quality_weights_within_the_documented_bound(k, paired):
         tol = (3 * k + 2 * int(U[g]) + 2) * u * W[g]
         assert abs(got.weights[g] - W[g]) <= tol, (g, got.weights[g], W[g], tol)
     assert int(U.sum()) > 2000  # enough windows counted for the bound to mean something
+
+
+def test_suffix_sort_failure_leaves_a_working_replica(small, monkeypatch):
+    """The median representatives come from a suffix array that build_ax sorts into a buffer of its own and frees
+    after k_ax_classify (a failed sort used to leave a published, unsorted array that later builds read).
+    With the sort failing (injected after its buffer was allocated) the first claimant represents each k-mer: same
+    counts as the oracle; a later k on the same replica (sort succeeding) too."""
+    ref, idx = small
+    reads = synth.make_reads(ref, 3_000, err_rate=0.003, n_rate=0.001)
+    monkeypatch.setenv("SPEQ_INJECT_SA_SORT_FAILURE", "1")
+    dev = DeviceIndex(idx)
+    for k in (21, 70):
+        for local in (False, True):
+            check(dev, Oracle(ref.records, ref.groups, 4, k), reads.seq, reads.qual, reads.offsets, k, local=local)
+        assert dev.tuning("last_kernel") == 3
+    monkeypatch.delenv("SPEQ_INJECT_SA_SORT_FAILURE")
+    for k in (31, 64):
+        check(dev, Oracle(ref.records, ref.groups, 4, k), reads.seq, reads.qual, reads.offsets, k)
+        assert dev.tuning("last_kernel") == 3
