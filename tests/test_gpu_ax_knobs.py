@@ -30,7 +30,7 @@ KNOBS = {"SPEQ_AX_DEF_LOCAL", "SPEQ_AX_DEF_GLOBAL", "SPEQ_AX_WL", "SPEQ_AX_WPB",
 def test_variants_cover_every_knob():
     forced = {f.split("=")[0][2:] for v in VARIANTS.values() for f in v.split()}
     assert forced == KNOBS
-    src = open(os.path.join(ROOT, "speq_amd", "csrc", "ax_scan.hip")).read()
+    src = "".join(open(os.path.join(ROOT, "speq_amd", "csrc", f)).read() for f in ("ax_common.hpp", "ax_scan.hip"))
     import re
     defined = set(re.findall(r"#ifndef (SPEQ_AX_[A-Z0-9_]+)", src))
     assert defined == KNOBS, defined ^ KNOBS
