@@ -15,7 +15,7 @@ LIB      := speq_amd/libspeq_scan.so
 CLI      := bin/speq
 OBJDIR   := build/obj
 
-LIB_HIP  := speq_amd/csrc/scan_kernels.hip speq_amd/csrc/ax_scan.hip speq_amd/csrc/ax_stager.hip speq_amd/csrc/build_gpu.hip speq_amd/csrc/fastq_gpu.hip
+LIB_HIP  := speq_amd/csrc/scan_kernels.hip speq_amd/csrc/ax_scan.hip speq_amd/csrc/build_gpu.hip speq_amd/csrc/fastq_gpu.hip
 LIB_CPP  := speq_amd/csrc/sais.cpp speq_amd/csrc/fm_index.cpp speq_amd/csrc/capi.cpp speq_amd/csrc/comm.cpp \
             speq_amd/csrc/host_io.cpp speq_amd/csrc/em.cpp speq_amd/csrc/pipeline.cpp \
             speq_amd/csrc/fastq_stream.cpp

@@ -3,7 +3,7 @@
 index and reads once, then the variants take turns (`--rounds` times, 5 timed launches each, minimum kept), so box
 drift falls on every variant alike. Counts must agree across variants.
 
-Usage: python scripts/ab_tune.py --variants "base:;stg:ax_stager=1" --cases "2:21:0.001:s:g,3:31:0.001:s:g"
+Usage: python scripts/ab_tune.py --variants "base:;l50:ax_load=50" --cases "2:21:0.001:s:g,3:31:0.001:s:g"
   case = config:k:err:s|p (single-end / paired):g|l (global / local)[:reads]
 Prints one JSON line per case: {case, variants: {name: {ms, Gkmers_s}}, counts_equal}."""
 import argparse

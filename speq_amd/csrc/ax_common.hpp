@@ -1,5 +1,4 @@
-// Shared device code of the anchor-and-extend read scans (ax_scan.hip: k_scan_ax and the per-k structures;
-// ax_stager.hip: k_scan_axq, the staged variant): constants, compile-time knobs, hashing of k-mers into the anchor
+// Device code of the anchor-and-extend read scan (ax_scan.hip: k_scan_ax and the per-k structures): constants, compile-time knobs, hashing of k-mers into the anchor
 // table and the Bloom filter, the anchor-table slot resolution and probe chain, bit helpers. DESIGN.md §4e.
 #pragma once
 #include <hip/hip_runtime.h>

@@ -1624,7 +1624,6 @@ bool launch_ax(speq_device_index* d, int mode, bool paired, const UnitSrc& src, 
     A.n = d->view.n;
     A.gran_bytes = ax->gran_bytes;
     A.G = d->G;
-    if (mode == KM_GLOBAL && d->ax_stager && launch_axq(d, paired, A, src, st, a, w)) return true;
     const bool lds_hist = d->G <= LDS_HIST_MAX_G;
     const uint32_t hist_words = lds_hist ? (mode == KM_GLOBAL ? d->G : 2u * d->G) : 0u;
     const size_t lds = ((hist_words * 8u + 15u) & ~15u) + (mode == KM_LOCAL ? QTAB_BYTES : 0u) +

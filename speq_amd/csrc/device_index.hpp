@@ -96,7 +96,6 @@ struct speq_device_index {
     uint64_t* d_text2 = nullptr;    // 2-bit text, built with the first per-k structures
     uint64_t* d_tbad = nullptr;     // bitmap of non-ACGT text positions
     bool ax_scan = true;            // tuning "ax_scan": read scans of k <= 128 use k_scan_ax
-    bool ax_stager = false;         // tuning "ax_stager": global-mode anchor scans use k_scan_axq (a staging wave)
     uint32_t ax_load = 0;           // tuning "ax_load": anchor-table load factor, percent (0: default 35)
     uint32_t grid_blocks_ax = 65535;  // tuning "grid_blocks_ax"
     uint32_t blocks_per_cu_ax = 0;  // tuning "blocks_per_cu_ax" (0: as many as registers/LDS allow)
@@ -120,7 +119,4 @@ const AxTable* ensure_ax(speq_device_index* d, uint32_t k);
 uint32_t ax_effective_load(const speq_device_index* d);  // the anchor table's load factor (percent) builds use
 bool launch_ax(speq_device_index* d, int mode, bool paired, const speq_dev::UnitSrc& src, hipStream_t st,
                unsigned long long* a, double* w);
-// the staged variant k_scan_axq (ax_stager.hip): global-mode read scans; false when it cannot take the scan
-bool launch_axq(speq_device_index* d, bool paired, const speq_dev::AxView& A, const speq_dev::UnitSrc& src,
-                hipStream_t st, unsigned long long* a, double* w);
 }  // namespace speq

@@ -2048,9 +2048,6 @@ int speq_device_set_tuning(speq_device_index* d, const char* key, int64_t value)
         } else if (k == "ax_scan") {
             if (value != 0 && value != 1) throw std::invalid_argument("ax_scan must be 0 or 1");
             d->ax_scan = value != 0;
-        } else if (k == "ax_stager") {
-            if (value != 0 && value != 1) throw std::invalid_argument("ax_stager must be 0 or 1");
-            d->ax_stager = value != 0;
         } else if (k == "ax_load") {
             if (value < 10 || value > 90) throw std::invalid_argument("ax_load must be in [10, 90] (percent)");
             std::lock_guard<std::mutex> lk(d->ax_mu);
@@ -2103,7 +2100,6 @@ int speq_device_get_tuning(const speq_device_index* d, const char* key, int64_t*
         else if (k == "kt_compact") *value = d->kt_compact ? 1 : 0;
         else if (k == "kt_load8") *value = d->kt_load8;
         else if (k == "ax_scan") *value = d->ax_scan ? 1 : 0;
-        else if (k == "ax_stager") *value = d->ax_stager ? 1 : 0;
         else if (k == "last_kernel") *value = d->last_kernel;
         else if (k == "ax_load") *value = speq::ax_effective_load(d);
         else if (k == "grid_blocks_ax") *value = d->grid_blocks_ax;
