@@ -436,7 +436,7 @@ def run_workload(ctx: Ctx, cfg_no: int, k: int, n_reads: int, mode: str, steps: 
     cpu = None
     if with_cpu and ctx.rank == 0 and ctx.world == 1:
         cpu = cpu_baseline(prepared, reads, k, G, cpu_seconds, local, paired, extra_ports=cpu_extra_ports,
-                           timed=(counts, weights))
+                           timed_counts=(counts, weights))
 
     check = {"T": int(counts[0]), "ambiguous": int(counts[1]), "U_sha1": u_sha1(counts[2:]),
              **({"W_sum": float(weights.sum())} if weights is not None else {})}
@@ -740,14 +740,14 @@ def cli_e2e(prep: dict, k: int, check: dict) -> dict:
 _SEQAN_LIKE = {}
 
 
-def cpu_baseline(prep, reads, k, G, target_s, local, paired=False, extra_ports=False, timed=None):
+def cpu_baseline(prep, reads, k, G, target_s, local, paired=False, extra_ports=False, timed_counts=None):
     """CPU baseline on this host's cores over a bounded sample of the same reads (rank 0, N = 1 only).
 
     value: oracle/seqan_like.c — the reference's ALGORITHM restated (backward search on a wavelet structure, locate of
     every hit through SA samples every 16 rows, sorted hit lists, first-hit rule), the SURVEY.md 8(d) stand-in for
     the SeqAn3 binary, which cannot be built here (8(c)). Its counts on the sample are checked against the GPU scan of
     the same sample (`checked`); when the sample is the whole shard, also against the TIMED scan's own counters
-    (`timed` = (counts, weights) of speq_scan_reads_device: T, ambiguous, every U[g], W; `checked_timed`).
+    (`timed_counts` = (counts, weights) of speq_scan_reads_device: T, ambiguous, every U[g], W; `checked_timed`).
     extra_ports (headline): also oracle/kmer_oracle.c (hash map, no FM-index) and oracle/fm_cpu.c (this build's
     label-run search on host cores)."""
     from oracle.oracle import Oracle, SeqanLike
@@ -800,8 +800,8 @@ def cpu_baseline(prep, reads, k, G, target_s, local, paired=False, extra_ports=F
     if not checked:
         raise RuntimeError("CPU baseline (seqan_like) disagrees with the GPU scan on its sample")
     checked_timed = None
-    if timed is not None and n == units:
-        tc, tw = timed
+    if timed_counts is not None and n == units:
+        tc, tw = timed_counts
         checked_timed = (r[0], r[1], r[2].tolist()) == (int(tc[0]), int(tc[1]), [int(x) for x in tc[2:]])
         if checked_timed and local:
             checked_timed = bool(np.allclose(r[3], tw, rtol=1e-9, atol=0))
