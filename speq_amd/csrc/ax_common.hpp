@@ -14,13 +14,17 @@ struct AxView {
     const u32x4* gran;         // granules {2-bit text, class plane 0, class plane 1} per 32 text positions
     const uint32_t* mlo;       // SA interval start of the multi-group k-mer at a text position (EM)
     const uint32_t* mhi;       // its end, by interval start (EM)
-    const unsigned long long* atab;
+    const unsigned long long* atab;  // (followed, in the same allocation, by the m-mer filter: byte offset mf_off)
     const unsigned long long* filt;
     unsigned long long* stats; // STATS instantiation only: AXS_N counters
     uint64_t nb;               // buckets
     uint64_t nf;               // filter words
     uint64_t n;                // text length
     uint64_t gran_bytes;       // bytes of gran (incl. END padding)
+    uint64_t nmf;              // m-mer filter words (0: no m-mer absence proofs)
+    uint32_t mf_off;           // byte offset of the m-mer filter from atab (the anchor table's buffer descriptor
+                               // covers both, so a lookup iteration loads buckets and m-mer filter words alike)
+    uint32_t m;                // m of the m-mer filter (0: off)
     uint32_t G;
 };
 }  // namespace speq_dev
@@ -32,7 +36,7 @@ using namespace speq_dev;
 // Compile-time knobs (A/B only; every one is run through the parity tests forced to a non-default value by
 // tests/test_gpu_ax_knobs.py over `make axknobs` builds): SPEQ_AX_DEF_LOCAL, SPEQ_AX_DEF_GLOBAL, SPEQ_AX_WL,
 // SPEQ_AX_WPB, SPEQ_AX_SU, SPEQ_AX_MIN_WAVES, SPEQ_AX_MIN_WAVES_LOCAL, SPEQ_AX_REFILL, SPEQ_AX_BLOCKED,
-// SPEQ_AX_SPEC_HW, SPEQ_AX_PRIO, SPEQ_AX_PRIO_MIN, SPEQ_AX_P2_MARGIN. Measured losers of rounds 3-4 (a cuckoo anchor
+// SPEQ_AX_SPEC_HW, SPEQ_AX_PRIO, SPEQ_AX_PRIO_MIN, SPEQ_AX_P2_MARGIN, SPEQ_AX_MPROOF. Measured losers of rounds 3-4 (a cuckoo anchor
 // table, lowest / first-claimant representatives, a dynamic tail, generation-weighted pools, offset prefetch,
 // speculative runs in global mode, a minimizer-keyed filter) were removed; DESIGN.md §4f keeps their numbers.
 constexpr uint32_t AX_MAX_K = 128;    // longest k the scan takes (AX_CAP - k + 1 windows per segment)
@@ -63,6 +67,7 @@ constexpr uint16_t AX_VOID = 0xFFFFu;  // a deferred-list slot reserved by a lan
 constexpr unsigned long long AX_SLOT_EMPTY = ~0ull;
 constexpr uint32_t AX_OOB = 0xFFFFFFF0u;  // buffer offset past every array (n < 2^30)
 constexpr uint32_t AX_FILTER_BITS = 16;   // Bloom filter bits per distinct k-mer (3 bits set per k-mer, one 64-bit word)
+constexpr uint32_t AX_MP = 4;             // m-mer absence probes per lane per lookup iteration (one per bucket load)
 constexpr uint32_t AX_MAX_G = 0xFFFFu;    // groups a slot's 16-bit group field holds
 typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
 
@@ -288,6 +293,9 @@ constexpr uint32_t AX_WPB = SPEQ_AX_WPB, AX_THREADS = 64 * SPEQ_AX_WPB;
 #ifndef SPEQ_AX_PRIO_MIN  // ... for static pools of at least this many units (and always for k > 64)
 #define SPEQ_AX_PRIO_MIN 384u
 #endif
+#ifndef SPEQ_AX_MPROOF  // 1: the windows that share an absent window's known mismatch are proven absent by m-mer
+#define SPEQ_AX_MPROOF 1  // probes where the m-mer filter allows (lane state 4), not deferred (A/B knob; runtime:
+#endif                    // tuning ax_mproof)
 #ifndef SPEQ_AX_P2_MARGIN  // the deferred-window pass also runs when fewer than this many list entries are free
 #define SPEQ_AX_P2_MARGIN 256u  // (A/B knob; a deferral that finds the list full waits for the pass: lane state 3)
 #endif

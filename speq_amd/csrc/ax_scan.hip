@@ -253,6 +253,33 @@ __global__ void k_ax_insert(const uint32_t* __restrict__ owner, uint64_t n, cons
     }
 }
 
+// Pass D: the m-mer filter — a blocked Bloom filter of every m-mer of the texts that holds no non-ACGT symbol (both
+// strands: the texts are [fwd_r, rc_r]). A window that contains an m-mer whose bits are missing cannot occur in the
+// texts (every occurrence of the window would contain an occurrence of the m-mer), so the scan proves the windows
+// around a mismatch absent with a few m-mer probes instead of deferring each (k_scan_ax, lane state 4).
+__global__ void k_ax_mfilter(const uint64_t* __restrict__ t2, const uint64_t* __restrict__ tbad, uint64_t n,
+                             uint32_t m, unsigned long long* __restrict__ mf, uint64_t nmf) {
+    for (uint64_t pos = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; pos + m <= n;
+         pos += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t w = pos >> 6, sh = pos & 63u;
+        const uint64_t bad = sh + m <= 64u ? (tbad[w] >> sh) : ((tbad[w] >> sh) | (tbad[w + 1] << (64u - sh)));
+        if ((bad & ((m == 64u) ? ~0ull : ((1ull << m) - 1ull))) != 0) continue;
+        uint64_t x[1];
+        ax_text_words<1>(t2, pos, x);
+        const uint64_t h = ax_hash<1>(x, m);
+        atomicOr(&mf[ax_fword(h, nmf)], (unsigned long long)ax_fbits(h));
+    }
+}
+
+// m of the m-mer filter of a text of n symbols for k-mers: the smallest m >= 12 with 4^m >= 200 n (a random m-mer
+// then occurs in the text with probability <= 1 %, so an m-mer over a sequencing error is almost always absent),
+// and only when a probe covers at least 4 windows (k - m + 1 >= 4); 0 = no m-mer proofs
+static uint32_t ax_mproof_m(uint64_t n, uint32_t k) {
+    uint32_t m = 12;
+    while (m < 32u && (double)(1ull << (2u * m)) < 200.0 * (double)n) ++m;
+    return k >= m + 3u ? m : 0u;
+}
+
 // ---------------------------------------------------------------------------------------------------------------
 // The scan
 // ---------------------------------------------------------------------------------------------------------------
@@ -323,8 +350,9 @@ __global__ __launch_bounds__(AX_THREADS, (ax_min_waves<MODE, HW, EM, STATS>())) 
     // nothing to load gets an out-of-range offset, which issues no memory request
     const __amdgpu_buffer_rsrc_t rs_gran =
         __builtin_amdgcn_make_buffer_rsrc((void*)A.gran, (short)0, (int)(uint32_t)A.gran_bytes, 0x00020000);
-    const __amdgpu_buffer_rsrc_t rs_atab =
-        __builtin_amdgcn_make_buffer_rsrc((void*)A.atab, (short)0, (int)(uint32_t)(A.nb * 64u), 0x00020000);
+    // (the anchor table's descriptor also covers the m-mer filter after it: 16-B loads of its 8-B words)
+    const __amdgpu_buffer_rsrc_t rs_atab = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)A.atab, (short)0, (int)(uint32_t)(A.nb * 64u + (A.m != 0u ? A.nmf * 8u + 16u : 0u)), 0x00020000);
     const __amdgpu_buffer_rsrc_t rs_filt =
         __builtin_amdgcn_make_buffer_rsrc((void*)A.filt, (short)0, (int)(uint32_t)(A.nf * 8u), 0x00020000);
     const uint64_t NWV = (uint64_t)gridDim.x * AX_WPB;
@@ -502,7 +530,9 @@ __global__ __launch_bounds__(AX_THREADS, (ax_min_waves<MODE, HW, EM, STATS>())) 
     uint64_t ta = 0;           // first base of the piece in seq/qual (local mode; other lanes read it by a shuffle)
     uint32_t j = 0;
     uint32_t st = 2u;          // 0: look window j up, 1: extend from text position p, 2: idle, 3: wait for the
-                               // deferred-window pass (its deferral found the list full), then look window j up
+                               // deferred-window pass (its deferral found the list full), then look window j up,
+                               // 4: window j is absent and the windows [j + 1, last_mm] share its mismatch last_mm:
+                               // probe the m-mers over it, defer the windows no absent m-mer covers (MPROOF)
     bool verify = false;       // st 1: p came from the anchor table (window j itself not compared yet)
     uint32_t p = 0;            // text position of window j (st 1)
     uint32_t gt = 0;           // group of p's text (st 1)
@@ -523,10 +553,10 @@ __global__ __launch_bounds__(AX_THREADS, (ax_min_waves<MODE, HW, EM, STATS>())) 
     uint32_t sp = 0;  // pending windows [sp, sp + k - 2] of the piece; 0: none
     // defers the valid windows of [lo, hi] (hi - lo <= 127; hi < lo: none) of this lane's piece; when the list has
     // no room: the reserved slots are voided, the lane waits for the deferred-window pass (st 3) and false
-    auto defer_range = [&](uint32_t lo, uint32_t hi) -> bool {
-        if (hi + 1u <= lo) return true;
+    auto defer_except = [&](uint32_t lo, uint32_t hi, uint64_t x0, uint64_t x1) -> bool {  // (x: windows lo + i
+        if (hi + 1u <= lo) return true;                                                    // proven absent)
         const uint32_t span = hi + 1u - lo;
-        uint64_t dm0 = vbits(lane, lo), dm1 = span > 64u ? vbits(lane, lo + 64u) : 0ull;
+        uint64_t dm0 = vbits(lane, lo) & ~x0, dm1 = span > 64u ? (vbits(lane, lo + 64u) & ~x1) : 0ull;
         dm0 &= span >= 64u ? ~0ull : ((1ull << span) - 1ull);
         if (span > 64u) dm1 &= span - 64u >= 64u ? ~0ull : ((1ull << (span - 64u)) - 1ull);
         const uint32_t cnt = (uint32_t)__popcll(dm0) + (uint32_t)__popcll(dm1);
@@ -546,6 +576,7 @@ __global__ __launch_bounds__(AX_THREADS, (ax_min_waves<MODE, HW, EM, STATS>())) 
         if (STATS) s_def += cnt;
         return true;
     };
+    auto defer_range = [&](uint32_t lo, uint32_t hi) -> bool { return defer_except(lo, hi, 0ull, 0ull); };
 
     auto start_read_at = [&](uint64_t r, uint64_t b, uint64_t e) {  // read r spans [b, e) of seq / qual
         rd = (uint32_t)r;
@@ -559,7 +590,7 @@ __global__ __launch_bounds__(AX_THREADS, (ax_min_waves<MODE, HW, EM, STATS>())) 
     for (;;) {
         // ================= housekeeping (wave-uniform decisions) =================
         const unsigned long long idle = __ballot(st == 2u);
-        const unsigned long long blk = __ballot(st >= 2u && hasdef);
+        const unsigned long long blk = __ballot((st == 2u || st == 3u) && hasdef);
         const unsigned long long busy = ~idle;
         // (a lane whose deferral found the list full, st 3, counts as blocked: the list then holds more than AX_DEF
         // entries, so this pass runs, and the lane looks its window up again afterwards)
@@ -947,7 +978,7 @@ __global__ __launch_bounds__(AX_THREADS, (ax_min_waves<MODE, HW, EM, STATS>())) 
             s_b32 += (nb > 16u && nb <= 32u) ? 1u : 0u;
             s_b64 += nb > 32u ? 1u : 0u;
         }
-        const bool want_lk = __ballot(st == 0u) != 0, want_rn = __ballot(st == 1u) != 0;
+        const bool want_lk = __ballot(st == 0u || st == 4u) != 0, want_rn = __ballot(st == 1u) != 0;
         run_phase = run_phase ? !want_lk : want_rn;
         // lookup iterations: the window's code words are read together with its valid bits (the same
         // window unless it is not valid, then read again), one LDS round trip before the bucket load instead of two
@@ -982,11 +1013,65 @@ __global__ __launch_bounds__(AX_THREADS, (ax_min_waves<MODE, HW, EM, STATS>())) 
             }
             // the 64-B bucket pb of the probe chain
             const uint32_t boff = lk ? pb * 64u : AX_OOB;
-            const uint32_t boff2 = boff + 32u;
-            const u32x4 q0 = __builtin_amdgcn_raw_buffer_load_b128(rs_atab, boff, 0, 0);
-            const u32x4 q1 = __builtin_amdgcn_raw_buffer_load_b128(rs_atab, boff + 16u, 0, 0);
-            const u32x4 q2 = __builtin_amdgcn_raw_buffer_load_b128(rs_atab, boff2, 0, 0);
-            const u32x4 q3 = __builtin_amdgcn_raw_buffer_load_b128(rs_atab, boff2 + 16u, 0, 0);
+            uint32_t o0 = boff, o1 = lk ? boff + 16u : AX_OOB, o2 = lk ? boff + 32u : AX_OOB,
+                     o3 = lk ? boff + 48u : AX_OOB;
+            // (MPROOF, state 4) the windows lo .. hi (lo = j + 1, hi = min(e, wend - 1)) all contain the mismatch
+            // e = last_mm. Probe t tests the m-mer from read base a_t (a_0 = min(e, lo + k - m), then steps of
+            // k - m + 1, at most e: every probe's m-mer holds e); it lies inside the windows a_t - (k - m) .. a_t, so
+            // when its filter bits are missing those windows are absent. The probes' filter words are loaded by the
+            // same four instructions as a bucket (lanes in state 4 never load one); mb[t]: bit indices, bit 31 = used
+            const bool mk = SPEQ_AX_MPROOF && st == 4u;
+            const uint32_t km = k - A.m;
+            uint32_t mb[AX_MP] = {0u, 0u, 0u, 0u};
+            static_assert(AX_MP == 4, "one m-mer probe per bucket load");
+            if (SPEQ_AX_MPROOF && mk) {
+                const uint32_t e = (uint32_t)last_mm;
+                uint32_t a = min(e, j + 1u + km);
+#pragma unroll
+                for (uint32_t t = 0; t < AX_MP; ++t) {
+                    const uint64_t x[1] = {slot64(lane, off0 + a)};
+                    const uint64_t hm = ax_hash<1>(x, A.m);
+                    const uint32_t off = A.mf_off + ax_fword(hm, A.nmf) * 8u;
+                    mb[t] = 0x80000000u | ((uint32_t)hm & 0x3FFFFu) | (a << 18);
+                    if (t == 0u) o0 = off;
+                    else if (t == 1u) o1 = off;
+                    else if (t == 2u) o2 = off;
+                    else o3 = off;
+                    if (a == e) break;  // (the last probe: later ones stay unused)
+                    a = min(e, a + km + 1u);
+                }
+            }
+            const u32x4 q0 = __builtin_amdgcn_raw_buffer_load_b128(rs_atab, o0, 0, 0);
+            const u32x4 q1 = __builtin_amdgcn_raw_buffer_load_b128(rs_atab, o1, 0, 0);
+            const u32x4 q2 = __builtin_amdgcn_raw_buffer_load_b128(rs_atab, o2, 0, 0);
+            const u32x4 q3 = __builtin_amdgcn_raw_buffer_load_b128(rs_atab, o3, 0, 0);
+            if (SPEQ_AX_MPROOF && mk) {
+                // windows proven absent, relative to lo (at most k - 1 <= 127 of them): two 64-bit masks
+                const uint32_t lo = j + 1u, hi = min((uint32_t)last_mm, wend - 1u);
+                uint64_t x0 = 0, x1 = 0;
+                const u32x4 qv[AX_MP] = {q0, q1, q2, q3};
+#pragma unroll
+                for (uint32_t t = 0; t < AX_MP; ++t) {
+                    if (!(mb[t] >> 31)) continue;
+                    const uint64_t word = (uint64_t)qv[t][0] | ((uint64_t)qv[t][1] << 32);
+                    const uint64_t bits = ax_fbits((uint64_t)(mb[t] & 0x3FFFFu));
+                    if ((word & bits) == bits) continue;  // the m-mer may occur: its windows stay deferred
+                    const uint32_t a = (mb[t] >> 18) & 0x1FFFu;
+                    const uint32_t r0 = (a >= lo + km ? a - km : lo) - lo, r1 = min(a, hi) - lo;  // covered lo + r0 ..
+                    // bits r0 .. r1 of the 128-bit mask x1:x0
+                    const uint64_t m0 = r0 >= 64u ? 0ull : (~0ull << r0) & (r1 >= 63u ? ~0ull : ((2ull << r1) - 1ull));
+                    const uint64_t m1 = r1 < 64u ? 0ull
+                                                 : ((r0 <= 64u ? ~0ull : (~0ull << (r0 - 64u))) &
+                                                    (r1 - 64u >= 63u ? ~0ull : ((2ull << (r1 - 64u)) - 1ull)));
+                    x0 |= m0;
+                    x1 |= m1;
+                }
+                st = 0u;
+                if (defer_except(lo, hi, x0, x1)) {  // (no room: st 3, and window j is looked up again afterwards)
+                    j = hi + 1u;
+                    last_mm = -1;
+                }
+            }
             if (lk) {
                 uint32_t slot = 0, cp = 0, cg = 0;
                 const uint32_t res = ax_resolve(q0, q1, q2, q3, fp, ps, slot, cp, cg);
@@ -1026,7 +1111,9 @@ __global__ __launch_bounds__(AX_THREADS, (ax_min_waves<MODE, HW, EM, STATS>())) 
                         dend = min(dend, wend - 1u);
                         // (no room: the lane waits for the deferred-window pass, st 3, and looks window j up again
                         // afterwards — one wasted lookup instead of looking up all k - 1 windows one by one)
-                        if (defer_range(j + 1u, dend)) {
+                        if (SPEQ_AX_MPROOF && A.m != 0u && known && dend > j) {
+                            st = 4u;  // m-mer probes over the mismatch in the next lookup iteration
+                        } else if (defer_range(j + 1u, dend)) {
                             j = dend + 1u;
                             last_mm = -1;
                         }
@@ -1521,6 +1608,12 @@ AxTable build_ax(speq_device_index* d, uint32_t k) {
         const uint32_t load = ax_effective_load(d);
         ax.nf = std::max<uint64_t>(1, distinct * AX_FILTER_BITS / 64);
         ax.nb = std::max<uint64_t>(1, (uint64_t)((double)distinct * 100.0 / (8.0 * load)) + 1);
+        // the m-mer filter (k_ax_mfilter) after the buckets: 16 bits per m-mer, sized by the distinct k-mers plus
+        // the m-mers that start no valid k-mer window near a text end (k per text); an undersized filter only
+        // passes more m-mers (their windows are deferred as before), it never proves a present window absent
+        ax.m = ax_mproof_m(n, k);
+        ax.nmf = ax.m ? std::max<uint64_t>(1, (distinct + (uint64_t)d->n_texts * k) * AX_FILTER_BITS / 64) : 0;
+        if (ax.m && ax.nb * 64u + ax.nmf * 8u + 16u >= (1ull << 32) - 64) ax.m = 0, ax.nmf = 0;
         if (ax.nb * 64u >= (1ull << 32) - 64 || ax.nf * 8 >= (1ull << 32) - 64) {
             // the scan addresses the tables with 32-bit buffer offsets: leave this k to the other kernels
             cleanup();
@@ -1528,7 +1621,8 @@ AxTable build_ax(speq_device_index* d, uint32_t k) {
             return AxTable{};
         }
         HIP_OK(hipMemGetInfo(&free_b, &total_b));
-        if (ax.nb * 64u + ax.nf * 8 > free_b / 10 * 9) {  // the table and filter do not fit now: try again later
+        const uint64_t atab_bytes = ax.nb * 64u + (ax.m ? ax.nmf * 8u + 16u : 0u);
+        if (atab_bytes + ax.nf * 8 > free_b / 10 * 9) {  // the table and filters do not fit now: try again later
             cleanup();
             for (void* q : mine) (void)hipFree(q);
             AxTable t;
@@ -1537,8 +1631,15 @@ AxTable build_ax(speq_device_index* d, uint32_t k) {
         }
         alloc(&ax.filt, ax.nf * 8);
         HIP_OK(hipMemsetAsync(ax.filt, 0, ax.nf * 8, d->stream));
-        alloc(&ax.atab, ax.nb * 64u);
+        alloc(&ax.atab, atab_bytes);
         HIP_OK(hipMemsetAsync(ax.atab, 0xFF, ax.nb * 64u, d->stream));
+        if (ax.m) {
+            unsigned long long* mf = reinterpret_cast<unsigned long long*>(static_cast<char*>(ax.atab) + ax.nb * 64u);
+            HIP_OK(hipMemsetAsync(mf, 0, ax.nmf * 8u + 16u, d->stream));
+            hipLaunchKernelGGL(k_ax_mfilter, dim3(grid), dim3(256), 0, d->stream, d->d_text2, d->d_tbad, n, ax.m, mf,
+                               ax.nmf);
+            HIP_OK(hipGetLastError());
+        }
         hipLaunchKernelGGL(k_ax_insert, dim3(grid), dim3(256), 0, d->stream, owner, n, d->d_text2, k, d->d_text_start,
                            d->d_text_group, d->n_texts, reinterpret_cast<unsigned long long*>(ax.atab), ax.nb,
                            reinterpret_cast<unsigned long long*>(ax.filt), ax.nf);
@@ -1546,7 +1647,7 @@ AxTable build_ax(speq_device_index* d, uint32_t k) {
         HIP_OK(hipStreamSynchronize(d->stream));
         ax.load = load;
         ax.gran_bytes = gran_bytes;
-        ax.bytes = ax.nb * 64u + ax.nf * 8 + gran_bytes;
+        ax.bytes = atab_bytes + ax.nf * 8 + gran_bytes;
         ax.ok = true;
     } catch (...) {
         cleanup();
@@ -1623,6 +1724,9 @@ bool launch_ax(speq_device_index* d, int mode, bool paired, const UnitSrc& src, 
     A.nf = ax->nf;
     A.n = d->view.n;
     A.gran_bytes = ax->gran_bytes;
+    A.m = d->ax_mproof ? ax->m : 0u;
+    A.nmf = A.m ? ax->nmf : 0u;
+    A.mf_off = (uint32_t)(ax->nb * 64u);
     A.G = d->G;
     const bool lds_hist = d->G <= LDS_HIST_MAX_G;
     const uint32_t hist_words = lds_hist ? (mode == KM_GLOBAL ? d->G : 2u * d->G) : 0u;

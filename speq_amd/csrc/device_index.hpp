@@ -27,6 +27,8 @@ struct AxTable {
     uint64_t nb = 0;           // buckets (64 B, 8 slots, linear probing)
     uint32_t load = 0;         // load factor the table was built at (percent)
     uint64_t nf = 0;           // filter words
+    uint64_t nmf = 0;          // m-mer filter words (after the nb buckets in atab's allocation; 0: none)
+    uint32_t m = 0;            // m of the m-mer filter (0: none)
     uint64_t gran_bytes = 0;
     uint64_t distinct = 0;     // distinct k-mers of the texts
     uint64_t bytes = 0;        // device bytes of the structures
@@ -96,6 +98,7 @@ struct speq_device_index {
     uint64_t* d_text2 = nullptr;    // 2-bit text, built with the first per-k structures
     uint64_t* d_tbad = nullptr;     // bitmap of non-ACGT text positions
     bool ax_scan = true;            // tuning "ax_scan": read scans of k <= 128 use k_scan_ax
+    bool ax_mproof = true;          // tuning "ax_mproof": m-mer absence proofs for the windows around a mismatch
     uint32_t ax_load = 0;           // tuning "ax_load": anchor-table load factor, percent (0: default 35)
     uint32_t grid_blocks_ax = 65535;  // tuning "grid_blocks_ax"
     uint32_t blocks_per_cu_ax = 0;  // tuning "blocks_per_cu_ax" (0: as many as registers/LDS allow)
