@@ -532,7 +532,8 @@ __global__ __launch_bounds__(AX_THREADS, (ax_min_waves<MODE, HW, EM, STATS>())) 
     uint32_t st = 2u;          // 0: look window j up, 1: extend from text position p, 2: idle, 3: wait for the
                                // deferred-window pass (its deferral found the list full), then look window j up,
                                // 4: window j is absent and the windows [j + 1, last_mm] share its mismatch last_mm:
-                               // probe the m-mers over it, defer the windows no absent m-mer covers (MPROOF)
+                               // probe the m-mers over it, defer the windows no absent m-mer covers (MPROOF),
+                               // 5: the same for the windows [j, last_mm] of a speculative run, which then resumes
     bool verify = false;       // st 1: p came from the anchor table (window j itself not compared yet)
     uint32_t p = 0;            // text position of window j (st 1)
     uint32_t gt = 0;           // group of p's text (st 1)
@@ -978,7 +979,7 @@ __global__ __launch_bounds__(AX_THREADS, (ax_min_waves<MODE, HW, EM, STATS>())) 
             s_b32 += (nb > 16u && nb <= 32u) ? 1u : 0u;
             s_b64 += nb > 32u ? 1u : 0u;
         }
-        const bool want_lk = __ballot(st == 0u || st == 4u) != 0, want_rn = __ballot(st == 1u) != 0;
+        const bool want_lk = __ballot(st == 0u || st >= 4u) != 0, want_rn = __ballot(st == 1u) != 0;
         run_phase = run_phase ? !want_lk : want_rn;
         // lookup iterations: the window's code words are read together with its valid bits (the same
         // window unless it is not valid, then read again), one LDS round trip before the bucket load instead of two
@@ -1020,13 +1021,14 @@ __global__ __launch_bounds__(AX_THREADS, (ax_min_waves<MODE, HW, EM, STATS>())) 
             // k - m + 1, at most e: every probe's m-mer holds e); it lies inside the windows a_t - (k - m) .. a_t, so
             // when its filter bits are missing those windows are absent. The probes' filter words are loaded by the
             // same four instructions as a bucket (lanes in state 4 never load one); mb[t]: bit indices, bit 31 = used
-            const bool mk = SPEQ_AX_MPROOF && st == 4u;
+            // (state 5: the windows j .. e of a speculative run, lo = j, then the run resumes)
+            const bool mk = SPEQ_AX_MPROOF && st >= 4u;
             const uint32_t km = k - A.m;
             uint32_t mb[AX_MP] = {0u, 0u, 0u, 0u};
             static_assert(AX_MP == 4, "one m-mer probe per bucket load");
             if (SPEQ_AX_MPROOF && mk) {
                 const uint32_t e = (uint32_t)last_mm;
-                uint32_t a = min(e, j + 1u + km);
+                uint32_t a = min(e, j + (st == 4u ? 1u : 0u) + km);
 #pragma unroll
                 for (uint32_t t = 0; t < AX_MP; ++t) {
                     const uint64_t x[1] = {slot64(lane, off0 + a)};
@@ -1047,7 +1049,7 @@ __global__ __launch_bounds__(AX_THREADS, (ax_min_waves<MODE, HW, EM, STATS>())) 
             const u32x4 q3 = __builtin_amdgcn_raw_buffer_load_b128(rs_atab, o3, 0, 0);
             if (SPEQ_AX_MPROOF && mk) {
                 // windows proven absent, relative to lo (at most k - 1 <= 127 of them): two 64-bit masks
-                const uint32_t lo = j + 1u, hi = min((uint32_t)last_mm, wend - 1u);
+                const uint32_t lo = j + (st == 4u ? 1u : 0u), hi = min((uint32_t)last_mm, wend - 1u);
                 uint64_t x0 = 0, x1 = 0;
                 const u32x4 qv[AX_MP] = {q0, q1, q2, q3};
 #pragma unroll
@@ -1066,9 +1068,19 @@ __global__ __launch_bounds__(AX_THREADS, (ax_min_waves<MODE, HW, EM, STATS>())) 
                     x0 |= m0;
                     x1 |= m1;
                 }
+                const bool resume_run = st == 5u;
                 st = 0u;
                 if (defer_except(lo, hi, x0, x1)) {  // (no room: st 3, and window j is looked up again afterwards)
+                    if (SPEC && resume_run) {  // the speculative run goes on after the mismatch, fresh
+                        p += hi + 1u - j;
+                        ps = AX_PS_FRESH;
+                        st = hi + 1u < wend ? 1u : 2u;
+                    }
                     j = hi + 1u;
+                    last_mm = -1;
+                } else if (SPEC && resume_run) {  // (state 4 keeps last_mm: the retried lookup probes again)
+                    ps = 0;
+                    resume = false;
                     last_mm = -1;
                 }
             }
@@ -1199,17 +1211,23 @@ __global__ __launch_bounds__(AX_THREADS, (ax_min_waves<MODE, HW, EM, STATS>())) 
                     last_mm = -1;
                 } else if (SPEC && verify && e < k && ps == AX_PS_SPEC) {
                     // the windows [j, j + e] hold the speculative run's first mismatch (the read's error): deferred;
-                    // the run goes on after it, its first k bases still to be compared
-                    if (defer_range(j, j + e)) {
-                        j += e + 1u;
-                        p += e + 1u;
-                        ps = AX_PS_FRESH;
-                        st = j < wend ? 1u : 2u;
+                    // the run goes on after it, its first k bases still to be compared. (MPROOF: state 5 first proves
+                    // them absent by m-mer probes over base j + e where it can, then resumes this run)
+                    if (SPEQ_AX_MPROOF && A.m != 0u && j + e < wend) {
+                        last_mm = (int32_t)(j + e);
+                        st = 5u;
                     } else {
-                        ps = 0;
-                        resume = false;
+                        if (defer_range(j, j + e)) {
+                            j += e + 1u;
+                            p += e + 1u;
+                            ps = AX_PS_FRESH;
+                            st = j < wend ? 1u : 2u;
+                        } else {
+                            ps = 0;
+                            resume = false;
+                        }
+                        last_mm = -1;
                     }
-                    last_mm = -1;
                 } else if (SPEC && verify && e < k && ps == AX_PS_FRESH) {  // no match from here: look window j up
                     st = 0u;
                     resume = false;
