@@ -356,7 +356,9 @@ void speq_groupings_free(speq_groupings* g);
  * anchor-and-extend scans (k <= 128): "ax_scan" 1 (default) / 0 (other kernels), "ax_load" anchor-table load factor in
  *                  percent for tables built afterwards, "grid_blocks_ax" grid cap, "blocks_per_cu_ax" resident blocks
  *                  per CU (0: as registers/LDS allow), "ax_generations" grid = 1..16 times the resident blocks
- *                  (default 1: one persistent generation); "last_kernel" (read only) the kernel of the last scan. */
+ *                  (default 1: one persistent generation), "ax_mproof" m-mer absence proofs of the windows around a
+ *                  mismatch (1 default: known and unknown mismatches, 2: known ones only, 0: off; results are the
+ *                  same); "last_kernel" (read only) the kernel of the last scan. */
 int speq_device_set_tuning(speq_device_index* d, const char* key, int64_t value);
 int speq_device_get_tuning(const speq_device_index* d, const char* key, int64_t* value);
 

@@ -25,6 +25,7 @@ struct AxView {
     uint32_t mf_off;           // byte offset of the m-mer filter from atab (the anchor table's buffer descriptor
                                // covers both, so a lookup iteration loads buckets and m-mer filter words alike)
     uint32_t m;                // m of the m-mer filter (0: off)
+    uint32_t mtiles;           // 1: also probe windows whose mismatch is unknown (lane state 6)
     uint32_t G;
 };
 }  // namespace speq_dev
@@ -296,6 +297,9 @@ constexpr uint32_t AX_WPB = SPEQ_AX_WPB, AX_THREADS = 64 * SPEQ_AX_WPB;
 #ifndef SPEQ_AX_MPROOF  // 1: the windows that share an absent window's known mismatch are proven absent by m-mer
 #define SPEQ_AX_MPROOF 1  // probes where the m-mer filter allows (lane state 4), not deferred (A/B knob; runtime:
 #endif                    // tuning ax_mproof)
+#ifndef SPEQ_AX_MTILES  // 1: ... and for an absent window whose mismatch is unknown (lane state 6; A/B knob)
+#define SPEQ_AX_MTILES 1
+#endif
 #ifndef SPEQ_AX_P2_MARGIN  // the deferred-window pass also runs when fewer than this many list entries are free
 #define SPEQ_AX_P2_MARGIN 256u  // (A/B knob; a deferral that finds the list full waits for the pass: lane state 3)
 #endif

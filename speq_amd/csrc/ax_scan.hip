@@ -273,11 +273,14 @@ __global__ void k_ax_mfilter(const uint64_t* __restrict__ t2, const uint64_t* __
 
 // m of the m-mer filter of a text of n symbols for k-mers: the smallest m >= 12 with 4^m >= 200 n (a random m-mer
 // then occurs in the text with probability <= 1 %, so an m-mer over a sequencing error is almost always absent),
-// and only when a probe covers at least 4 windows (k - m + 1 >= 4); 0 = no m-mer proofs
+// and only when one probe covers at least AX_MP_COVER windows (k - m + 1): a probe iteration delays its lane by one
+// round trip, which the deferred windows it saves repay from about 12 on (config 2, k = 21, m = 14: 8 windows per
+// probe, 1-3 % slower with the proofs; k = 31, m = 16-18 and k = 70 win: profiles/r05/ab_mproof*.jsonl); 0 = none
+constexpr uint32_t AX_MP_COVER = 12;
 static uint32_t ax_mproof_m(uint64_t n, uint32_t k) {
     uint32_t m = 12;
     while (m < 32u && (double)(1ull << (2u * m)) < 200.0 * (double)n) ++m;
-    return k >= m + 3u ? m : 0u;
+    return k + 1u >= m + AX_MP_COVER ? m : 0u;
 }
 
 // ---------------------------------------------------------------------------------------------------------------
@@ -533,7 +536,8 @@ __global__ __launch_bounds__(AX_THREADS, (ax_min_waves<MODE, HW, EM, STATS>())) 
                                // deferred-window pass (its deferral found the list full), then look window j up,
                                // 4: window j is absent and the windows [j + 1, last_mm] share its mismatch last_mm:
                                // probe the m-mers over it, defer the windows no absent m-mer covers (MPROOF),
-                               // 5: the same for the windows [j, last_mm] of a speculative run, which then resumes
+                               // 5: the same for the windows [j, last_mm] of a speculative run, which then resumes,
+                               // 6: window j is absent, its mismatch unknown: m-mer probes spread over window j
     bool verify = false;       // st 1: p came from the anchor table (window j itself not compared yet)
     uint32_t p = 0;            // text position of window j (st 1)
     uint32_t gt = 0;           // group of p's text (st 1)
@@ -551,6 +555,9 @@ __global__ __launch_bounds__(AX_THREADS, (ax_min_waves<MODE, HW, EM, STATS>())) 
     // its anchor's text: an END window among the pending ones defers them instead.
     constexpr bool SPEC = HW >= SPEQ_AX_SPEC_HW && !EM && MODE == KM_LOCAL;
     constexpr uint32_t AX_PS_SPEC = 16u, AX_PS_FRESH = 17u;
+    // (state 6, unknown mismatches, where no speculative run finds them: compiled into those instantiations only —
+    // in the speculative ones its code alone cost k = 70 local 31 %, profiles/r05/ab_mtiles_codegen.jsonl)
+    constexpr bool MTILES = SPEQ_AX_MTILES && !SPEC;
     uint32_t sp = 0;  // pending windows [sp, sp + k - 2] of the piece; 0: none
     // defers the valid windows of [lo, hi] (hi - lo <= 127; hi < lo: none) of this lane's piece; when the list has
     // no room: the reserved slots are voided, the lane waits for the deferred-window pass (st 3) and false
@@ -1026,11 +1033,20 @@ __global__ __launch_bounds__(AX_THREADS, (ax_min_waves<MODE, HW, EM, STATS>())) 
             const uint32_t km = k - A.m;
             uint32_t mb[AX_MP] = {0u, 0u, 0u, 0u};
             static_assert(AX_MP == 4, "one m-mer probe per bucket load");
+            // (state 6: window j is absent with no known mismatch: np m-mers spread evenly over window j's bases
+            // locate the error: the last absent one, at a_R, proves the windows that contain it and the windows up to
+            // a_R + m - 1 are deferred, the later ones looked up as usual)
+            const bool tiles = MTILES && st == 6u;
             if (SPEQ_AX_MPROOF && mk) {
-                const uint32_t e = (uint32_t)last_mm;
-                uint32_t a = min(e, j + (st == 4u ? 1u : 0u) + km);
+                const uint32_t e = tiles ? 0u : (uint32_t)last_mm;
+                const uint32_t np = tiles ? min(AX_MP, (k + A.m - 1u) / A.m) : AX_MP;  // (tiles: >= 2, k > m)
+                uint32_t a = tiles ? j : min(e, j + (st == 4u ? 1u : 0u) + km);
 #pragma unroll
                 for (uint32_t t = 0; t < AX_MP; ++t) {
+                    if (tiles) {
+                        if (t >= np) break;
+                        a = j + (t * km) / (np - 1u);
+                    }
                     const uint64_t x[1] = {slot64(lane, off0 + a)};
                     const uint64_t hm = ax_hash<1>(x, A.m);
                     const uint32_t off = A.mf_off + ax_fword(hm, A.nmf) * 8u;
@@ -1039,8 +1055,10 @@ __global__ __launch_bounds__(AX_THREADS, (ax_min_waves<MODE, HW, EM, STATS>())) 
                     else if (t == 1u) o1 = off;
                     else if (t == 2u) o2 = off;
                     else o3 = off;
-                    if (a == e) break;  // (the last probe: later ones stay unused)
-                    a = min(e, a + km + 1u);
+                    if (!tiles) {
+                        if (a == e) break;  // (the last probe: later ones stay unused)
+                        a = min(e, a + km + 1u);
+                    }
                 }
             }
             const u32x4 q0 = __builtin_amdgcn_raw_buffer_load_b128(rs_atab, o0, 0, 0);
@@ -1049,8 +1067,11 @@ __global__ __launch_bounds__(AX_THREADS, (ax_min_waves<MODE, HW, EM, STATS>())) 
             const u32x4 q3 = __builtin_amdgcn_raw_buffer_load_b128(rs_atab, o3, 0, 0);
             if (SPEQ_AX_MPROOF && mk) {
                 // windows proven absent, relative to lo (at most k - 1 <= 127 of them): two 64-bit masks
-                const uint32_t lo = j + (st == 4u ? 1u : 0u), hi = min((uint32_t)last_mm, wend - 1u);
+                const uint32_t lo = j + (st == 5u ? 0u : 1u);
+                uint32_t hi = min(tiles ? j + k - 1u : (uint32_t)last_mm, wend - 1u);
                 uint64_t x0 = 0, x1 = 0;
+                uint32_t aR = 0;  // (tiles) 1 + the last absent m-mer's start
+
                 const u32x4 qv[AX_MP] = {q0, q1, q2, q3};
 #pragma unroll
                 for (uint32_t t = 0; t < AX_MP; ++t) {
@@ -1059,6 +1080,8 @@ __global__ __launch_bounds__(AX_THREADS, (ax_min_waves<MODE, HW, EM, STATS>())) 
                     const uint64_t bits = ax_fbits((uint64_t)(mb[t] & 0x3FFFFu));
                     if ((word & bits) == bits) continue;  // the m-mer may occur: its windows stay deferred
                     const uint32_t a = (mb[t] >> 18) & 0x1FFFu;
+                    aR = max(aR, a + 1u);
+                    if (a < lo) continue;  // (tile 0 at window j: it only locates the error)
                     const uint32_t r0 = (a >= lo + km ? a - km : lo) - lo, r1 = min(a, hi) - lo;  // covered lo + r0 ..
                     // bits r0 .. r1 of the 128-bit mask x1:x0
                     const uint64_t m0 = r0 >= 64u ? 0ull : (~0ull << r0) & (r1 >= 63u ? ~0ull : ((2ull << r1) - 1ull));
@@ -1068,6 +1091,7 @@ __global__ __launch_bounds__(AX_THREADS, (ax_min_waves<MODE, HW, EM, STATS>())) 
                     x0 |= m0;
                     x1 |= m1;
                 }
+                if (tiles && aR != 0u) hi = min(aR - 1u + A.m - 1u, hi);  // later windows: looked up as usual
                 const bool resume_run = st == 5u;
                 st = 0u;
                 if (defer_except(lo, hi, x0, x1)) {  // (no room: st 3, and window j is looked up again afterwards)
@@ -1123,8 +1147,12 @@ __global__ __launch_bounds__(AX_THREADS, (ax_min_waves<MODE, HW, EM, STATS>())) 
                         dend = min(dend, wend - 1u);
                         // (no room: the lane waits for the deferred-window pass, st 3, and looks window j up again
                         // afterwards — one wasted lookup instead of looking up all k - 1 windows one by one)
-                        if (SPEQ_AX_MPROOF && A.m != 0u && known && dend > j) {
-                            st = 4u;  // m-mer probes over the mismatch in the next lookup iteration
+                        if (SPEQ_AX_MPROOF && A.m != 0u && dend > j) {
+                            st = known ? 4u : ((MTILES && A.mtiles) ? 6u : 0u);  // probes next lookup
+                            if (st == 0u && defer_range(j + 1u, dend)) {
+                                j = dend + 1u;
+                                last_mm = -1;
+                            }
                         } else if (defer_range(j + 1u, dend)) {
                             j = dend + 1u;
                             last_mm = -1;
@@ -1743,6 +1771,7 @@ bool launch_ax(speq_device_index* d, int mode, bool paired, const UnitSrc& src, 
     A.n = d->view.n;
     A.gran_bytes = ax->gran_bytes;
     A.m = d->ax_mproof ? ax->m : 0u;
+    A.mtiles = d->ax_mproof == 1u ? 1u : 0u;
     A.nmf = A.m ? ax->nmf : 0u;
     A.mf_off = (uint32_t)(ax->nb * 64u);
     A.G = d->G;

@@ -98,7 +98,8 @@ struct speq_device_index {
     uint64_t* d_text2 = nullptr;    // 2-bit text, built with the first per-k structures
     uint64_t* d_tbad = nullptr;     // bitmap of non-ACGT text positions
     bool ax_scan = true;            // tuning "ax_scan": read scans of k <= 128 use k_scan_ax
-    bool ax_mproof = true;          // tuning "ax_mproof": m-mer absence proofs for the windows around a mismatch
+    uint32_t ax_mproof = 1;         // tuning "ax_mproof": m-mer absence proofs for the windows around a mismatch
+                                    // (1: known and unknown mismatches, 2: known ones only, 0: off)
     uint32_t ax_load = 0;           // tuning "ax_load": anchor-table load factor, percent (0: default 35)
     uint32_t grid_blocks_ax = 65535;  // tuning "grid_blocks_ax"
     uint32_t blocks_per_cu_ax = 0;  // tuning "blocks_per_cu_ax" (0: as many as registers/LDS allow)

@@ -2049,8 +2049,8 @@ int speq_device_set_tuning(speq_device_index* d, const char* key, int64_t value)
             if (value != 0 && value != 1) throw std::invalid_argument("ax_scan must be 0 or 1");
             d->ax_scan = value != 0;
         } else if (k == "ax_mproof") {
-            if (value != 0 && value != 1) throw std::invalid_argument("ax_mproof must be 0 or 1");
-            d->ax_mproof = value != 0;
+            if (value < 0 || value > 2) throw std::invalid_argument("ax_mproof must be 0, 1 or 2");
+            d->ax_mproof = (uint32_t)value;
         } else if (k == "ax_load") {
             if (value < 10 || value > 90) throw std::invalid_argument("ax_load must be in [10, 90] (percent)");
             std::lock_guard<std::mutex> lk(d->ax_mu);
@@ -2104,7 +2104,7 @@ int speq_device_get_tuning(const speq_device_index* d, const char* key, int64_t*
         else if (k == "kt_load8") *value = d->kt_load8;
         else if (k == "ax_scan") *value = d->ax_scan ? 1 : 0;
         else if (k == "last_kernel") *value = d->last_kernel;
-        else if (k == "ax_mproof") *value = d->ax_mproof ? 1 : 0;
+        else if (k == "ax_mproof") *value = d->ax_mproof;
         else if (k == "ax_load") *value = speq::ax_effective_load(d);
         else if (k == "grid_blocks_ax") *value = d->grid_blocks_ax;
         else if (k == "blocks_per_cu_ax") *value = d->blocks_per_cu_ax;
