@@ -35,11 +35,12 @@ namespace {
 using namespace speq_dev;
 
 // Compile-time knobs (A/B only; every one is run through the parity tests forced to a non-default value by
-// tests/test_gpu_ax_knobs.py over `make axknobs` builds): SPEQ_AX_DEF_LOCAL, SPEQ_AX_DEF_GLOBAL, SPEQ_AX_WL,
+// tests/test_gpu_ax_knobs.py over `make axknobs` builds), fifteen: SPEQ_AX_DEF_LOCAL, SPEQ_AX_DEF_GLOBAL, SPEQ_AX_WL,
 // SPEQ_AX_WPB, SPEQ_AX_SU, SPEQ_AX_MIN_WAVES, SPEQ_AX_MIN_WAVES_LOCAL, SPEQ_AX_REFILL, SPEQ_AX_BLOCKED,
-// SPEQ_AX_SPEC_HW, SPEQ_AX_PRIO, SPEQ_AX_PRIO_MIN, SPEQ_AX_P2_MARGIN, SPEQ_AX_MPROOF. Measured losers of rounds 3-4 (a cuckoo anchor
-// table, lowest / first-claimant representatives, a dynamic tail, generation-weighted pools, offset prefetch,
-// speculative runs in global mode, a minimizer-keyed filter) were removed; DESIGN.md §4f keeps their numbers.
+// SPEQ_AX_SPEC_HW, SPEQ_AX_PRIO, SPEQ_AX_PRIO_MIN, SPEQ_AX_P2_MARGIN, SPEQ_AX_MPROOF, SPEQ_AX_MTILES. Measured losers
+// of rounds 3-5 (a cuckoo anchor table, lowest / first-claimant representatives, a dynamic tail, generation-weighted
+// pools, offset prefetch, speculative runs in global mode, a minimizer-keyed filter, workgroup-shared pools) were
+// removed; DESIGN.md §4f-§4g keep their numbers.
 constexpr uint32_t AX_MAX_K = 128;    // longest k the scan takes (AX_CAP - k + 1 windows per segment)
 constexpr uint32_t AX_CAP = 192;      // bases of a read a lane stages at once (longer reads: segments of AX_CAP bases)
 constexpr uint32_t AX_STREAM = AX_CAP + 16;  // staged bases incl. the 16-B alignment slack before the read
