@@ -595,6 +595,9 @@ __global__ __launch_bounds__(AX_THREADS, (ax_min_waves<MODE, HW, EM, STATS>())) 
         seg = 0;
     };
     auto start_read = [&](uint64_t r) { start_read_at(r, src.off[r], src.off[r + 1]); };
+    // (PAIRED) the second mate's length, loaded with the first mate's offsets: the second mate then starts at the
+    // first's end without another offsets round trip in its refill
+    uint32_t L2m = 0;
     for (;;) {
         // ================= housekeeping (wave-uniform decisions) =================
         const unsigned long long idle = __ballot(st == 2u);
@@ -777,7 +780,13 @@ __global__ __launch_bounds__(AX_THREADS, (ax_min_waves<MODE, HW, EM, STATS>())) 
                     if (newu < nu) {
                         has_unit = true;
                         mate = 0;
-                        start_read(PAIRED ? 2 * newu : newu);
+                        if (PAIRED) {
+                            const uint64_t r0 = 2 * newu, o0 = src.off[r0], o1 = src.off[r0 + 1], o2 = src.off[r0 + 2];
+                            start_read_at(r0, o0, o1);
+                            L2m = (uint32_t)(o2 - o1);
+                        } else {
+                            start_read(newu);
+                        }
                         stg = true;
                     }
                 } else if (seg + 1u < nseg) {
@@ -785,7 +794,7 @@ __global__ __launch_bounds__(AX_THREADS, (ax_min_waves<MODE, HW, EM, STATS>())) 
                     stg = true;
                 } else {  // PAIRED: the second mate
                     mate = 1;
-                    start_read(rd + 1);
+                    start_read_at(rd + 1, rb + L, rb + L + L2m);
                     stg = true;
                 }
             }
