@@ -437,15 +437,37 @@ __global__ __launch_bounds__(AX_THREADS, (ax_min_waves<MODE, HW, EM, STATS>())) 
             if (STATS) s_qb += 1u;
             return wtab[qof((wp[0] >> (8u * sh)) & 0xFFu)];
         }
+        // (k > 32: the dwords four at a time, as weight8's middle product)
         const uint32_t nd = (sh + k + 3u) >> 2;
         double x = 1.0;
-        for (uint32_t t = 0; t < nd; ++t) {
-            const uint32_t w = wp[t];
+        if constexpr (HW >= 2) {
+            for (uint32_t t = 0; t < nd; t += 4u) {
+                uint32_t w[4];
 #pragma unroll
-            for (uint32_t b = 0; b < 4u; ++b) {
-                const uint32_t idx = 4u * t + b;  // the window's base idx - sh
-                const double f = qtab[qof((w >> (8u * b)) & 0xFFu)].y;
-                x = (idx >= sh && idx < sh + k) ? x * f : x;
+                for (uint32_t i = 0; i < 4u; ++i) w[i] = t + i < nd ? wp[t + i] : 0u;
+                double pw[4];
+#pragma unroll
+                for (uint32_t i = 0; i < 4u; ++i) {
+                    double f[4];
+#pragma unroll
+                    for (uint32_t b = 0; b < 4u; ++b) {
+                        const uint32_t idx = 4u * (t + i) + b;  // the window's base idx - sh
+                        const double y = qtab[qof((w[i] >> (8u * b)) & 0xFFu)].y;
+                        f[b] = (t + i < nd && idx >= sh && idx < sh + k) ? y : 1.0;
+                    }
+                    pw[i] = (f[0] * f[1]) * (f[2] * f[3]);
+                }
+                x *= (pw[0] * pw[1]) * (pw[2] * pw[3]);
+            }
+        } else {
+            for (uint32_t t = 0; t < nd; ++t) {
+                const uint32_t w = wp[t];
+#pragma unroll
+                for (uint32_t b = 0; b < 4u; ++b) {
+                    const uint32_t idx = 4u * t + b;  // the window's base idx - sh
+                    const double f = qtab[qof((w >> (8u * b)) & 0xFFu)].y;
+                    x = (idx >= sh && idx < sh + k) ? x * f : x;
+                }
             }
         }
         if (STATS) s_qb += k;
@@ -471,25 +493,63 @@ __global__ __launch_bounds__(AX_THREADS, (ax_min_waves<MODE, HW, EM, STATS>())) 
         const uint32_t* rp = wp + (rs >> 2);
         const uint32_t c0 = tmax >= 1u ? rp[0] : 0u, c1 = rlast > 4u ? rp[1] : 0u, c2 = rlast > 8u ? rp[2] : 0u;
         const uint32_t r03 = __builtin_amdgcn_alignbyte(c1, c0, rsh), r47 = __builtin_amdgcn_alignbyte(c2, c1, rsh);
+        // k > 32: the middle bytes' dwords four at a time (their loads issued together), each group's factors as a
+        // product tree (a factor outside the window is 1.0, whose product is exact), and the right bytes' products
+        // R[t] as a chain of their own beside M's (window t = L[t] (M R[t])): short dependent chains instead of one
+        // of k + 7 products with a load wait per dword (k = 70 varying qualities -5 %; at k <= 32 the 4-dword groups
+        // evaluate more masked factors than they save: +5 %, so the one chain stays; profiles/r05/ab_weight_trees.jsonl)
         double M = 1.0;
-        for (uint32_t t = (sh + 7u) >> 2; t <= (sh + k - 1u) >> 2; ++t) {
-            const uint32_t w = wp[t];
+        const uint32_t t0 = (sh + 7u) >> 2, t1 = (sh + k - 1u) >> 2;
+        if constexpr (HW >= 2) {
+            for (uint32_t t = t0; t <= t1; t += 4u) {
+                uint32_t w[4];
 #pragma unroll
-            for (uint32_t b = 0; b < 4u; ++b) {
-                const uint32_t idx = 4u * t + b;
-                const double f = qinv(w >> (8u * b));
-                M = (idx >= sh + 7u && idx < sh + k) ? M * f : M;
+                for (uint32_t i = 0; i < 4u; ++i) w[i] = t + i <= t1 ? wp[t + i] : 0u;
+                double pw[4];
+#pragma unroll
+                for (uint32_t i = 0; i < 4u; ++i) {
+                    double f[4];
+#pragma unroll
+                    for (uint32_t b = 0; b < 4u; ++b) {
+                        const uint32_t idx = 4u * (t + i) + b;
+                        const double x = qinv(w[i] >> (8u * b));
+                        f[b] = (t + i <= t1 && idx >= sh + 7u && idx < sh + k) ? x : 1.0;
+                    }
+                    pw[i] = (f[0] * f[1]) * (f[2] * f[3]);
+                }
+                M *= (pw[0] * pw[1]) * (pw[2] * pw[3]);
+            }
+        } else {
+            for (uint32_t t = t0; t <= t1; ++t) {
+                const uint32_t w = wp[t];
+#pragma unroll
+                for (uint32_t b = 0; b < 4u; ++b) {
+                    const uint32_t idx = 4u * t + b;
+                    const double f = qinv(w >> (8u * b));
+                    M = (idx >= sh + 7u && idx < sh + k) ? M * f : M;
+                }
             }
         }
         double L[8];
         L[7] = 1.0;
 #pragma unroll
         for (int t = 6; t >= 0; --t) L[t] = qinv((t < 4 ? l03 : l47) >> (8 * (t & 3))) * L[t + 1];
-        double MR = M, sum = 0.0;
+        double sum = 0.0;
+        if constexpr (HW >= 2) {
+            double R[8];
+            R[0] = 1.0;
 #pragma unroll
-        for (uint32_t t = 0; t < 8u; ++t) {
-            sum += ((mask >> t) & 1u) ? L[t] * MR : 0.0;
-            if (t < 7u) MR *= qinv((t < 4u ? r03 : r47) >> (8u * (t & 3u)));
+            for (uint32_t t = 1; t < 8u; ++t)
+                R[t] = R[t - 1] * qinv((t - 1u < 4u ? r03 : r47) >> (8u * ((t - 1u) & 3u)));
+#pragma unroll
+            for (uint32_t t = 0; t < 8u; ++t) sum += ((mask >> t) & 1u) ? L[t] * (M * R[t]) : 0.0;
+        } else {
+            double MR = M;
+#pragma unroll
+            for (uint32_t t = 0; t < 8u; ++t) {
+                sum += ((mask >> t) & 1u) ? L[t] * MR : 0.0;
+                if (t < 7u) MR *= qinv((t < 4u ? r03 : r47) >> (8u * (t & 3u)));
+            }
         }
         if (STATS) s_qb += k + tmax;
         return sum;
