@@ -1532,7 +1532,10 @@ __global__ __launch_bounds__(AX_THREADS, (ax_min_waves<MODE, HW, EM, STATS>())) 
     if (has_unit && ad) atomicAdd(&wsum[1], 1ull);  // the wave's last units
     wave_sync();
     const unsigned long long tsum = wsum[0], asum = wsum[1];
-    if (lane == 0) {
+    // T and the ambiguous units go out with the workgroup's histogram (LDS_HIST: one atomic instruction per workgroup
+    // for all G + 2 counters, after the barrier). One atomic per wave on the counters' cache line, 5,120 of them per
+    // launch at config 2 on the same line, cost 35 µs of a 0.22 ms launch (profiles/r05/ab_final_atomics.jsonl).
+    if (!LDS_HIST && lane == 0) {
         if (tsum) atomicAdd(&out_a[0], tsum);
         if (asum) atomicAdd(&out_a[1], asum);
     }
@@ -1554,9 +1557,21 @@ __global__ __launch_bounds__(AX_THREADS, (ax_min_waves<MODE, HW, EM, STATS>())) 
     }
     if (LDS_HIST) {
         __syncthreads();
-        for (uint32_t g = threadIdx.x; g < G; g += AX_THREADS) {
-            const unsigned long long x = hA[g];
-            if (x) atomicAdd(&gU[g], x);
+        // out_a = {T, ambiguous, U[0 .. G)}: thread 0 and 1 sum the waves' T and ambiguous units, thread 2 + g adds U[g]
+        for (uint32_t i = threadIdx.x; i < G + 2u; i += AX_THREADS) {
+            unsigned long long x = 0;
+            if (i < 2u) {
+#pragma unroll
+                for (uint32_t w = 0; w < AX_WPB; ++w)
+                    x += reinterpret_cast<const unsigned long long*>(
+                        smem + hist_bytes + qtab_bytes + w * WAVE_BYTES +
+                        (reinterpret_cast<const unsigned char*>(wsum) - wb))[i];
+            } else {
+                x = hA[i - 2u];
+            }
+            if (x) atomicAdd(&out_a[i], x);
+        }
+        for (uint32_t g = threadIdx.x; g < (MODE == KM_LOCAL ? G : 0u); g += AX_THREADS) {
             if (MODE == KM_LOCAL) {
                 const double y = hW[g];
                 if (y != 0.0) atomicAdd(&out_w[g], y);
