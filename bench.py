@@ -345,25 +345,30 @@ def run_workload(ctx: Ctx, cfg_no: int, k: int, n_reads: int, mode: str, steps: 
             if local:
                 ctx.comm.allreduce_f64(d_w.data_ptr(), G, stream)
 
-    def timed_run(n_steps, n_warm):
+    def timed_run(n_steps, n_warm, events=True):
         for _ in range(n_warm):
             step()
         torch.cuda.synchronize()
         ctx.barrier()
         torch.cuda.synchronize()
-        dev.timing(True)
-        dev.timing_read()  # reset
+        dev.timing(events)
+        if events:
+            dev.timing_read()  # reset
         t0 = time.perf_counter()
         for _ in range(n_steps):
             step()
         torch.cuda.synchronize()
         ctx.barrier()
         elapsed = time.perf_counter() - t0
-        kernel_ms, launches = dev.timing_read()
+        kernel_ms, launches = dev.timing_read() if events else (0.0, 0)
         dev.timing(False)
         return ctx.allreduce_max(elapsed), kernel_ms, launches
 
-    elapsed, kernel_ms, launches = timed_run(steps, warmup)
+    # `value`: the K steps as a job runs them. The scan's HIP timing events (two per launch) cost 6-10 µs per step
+    # (scripts/step_overhead.py: 0.177 ms per step without them, 0.185-0.188 with), so the roofline's per-launch kernel
+    # time comes from the same K steps timed once more with the events on (ms_per_step_with_events)
+    elapsed, _, _ = timed_run(steps, warmup, events=False)
+    elapsed_ev, kernel_ms, launches = timed_run(steps, 0, events=True)
     counts = d_counts.cpu().numpy()
     weights = d_w.cpu().numpy() if local else None
     table_on = bool(ktab["table_bytes"])
@@ -441,7 +446,8 @@ def run_workload(ctx: Ctx, cfg_no: int, k: int, n_reads: int, mode: str, steps: 
     check = {"T": int(counts[0]), "ambiguous": int(counts[1]), "U_sha1": u_sha1(counts[2:]),
              **({"W_sum": float(weights.sum())} if weights is not None else {})}
     out = {
-        "value": value, "ms_per_step": elapsed / steps * 1e3, "avg_kernel_ms": avg_kernel_s * 1e3, "k": k,
+        "value": value, "ms_per_step": elapsed / steps * 1e3, "avg_kernel_ms": avg_kernel_s * 1e3,
+        "ms_per_step_with_events": elapsed_ev / steps * 1e3, "k": k,
         "mode": mode,
         "workload": f"BASELINE config {cfg_no}: {c['n_variants']} variants x {c['n_isolates']} isolates x "
                     f"{c['length']} bp, {n_reads} x 150 bp {'pairs' if paired else 'reads'} per GPU, k={k}, {mode}"
@@ -494,6 +500,9 @@ def compact_result(head: dict, lines: dict, meta: dict) -> dict:
     out = {
         "metric": meta["metric"], "value": head["value"], "unit": "k-mers/s", "n_gpus": meta["n_gpus"],
         "steps": meta["steps"], "warmup": meta["warmup"], "ms_per_step": head["ms_per_step"],
+        "ms_per_step_with_events": head.get("ms_per_step_with_events"),
+        "timing": "value: K steps without per-launch events; roofline.avg_kernel_ms: the same K steps again with HIP "
+                  "events around every launch on its stream",
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u32",
         "data": "synthetic (splitmix64 references/reads, SURVEY.md §8(d))",
         "config": meta["config"],
