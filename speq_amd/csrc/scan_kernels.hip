@@ -190,9 +190,11 @@ __global__ __launch_bounds__(BLOCK_THREADS, (KT && NWIN == 1 && MODE == KM_GLOBA
     // branches on them are uniform (no exec-mask bookkeeping)
     const uint32_t wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t G = I.G, k = src.k;
-    const uint32_t hist_words = LDS_HIST ? ((MODE == KM_GLOBAL) ? G : 2u * G) : 0u;
+    // (+ 2 words: the workgroup's T and ambiguous units, flushed with the histogram: ax_scan.hip §4i)
+    const uint32_t hist_words = LDS_HIST ? ((MODE == KM_GLOBAL) ? G : 2u * G) + 2u : 0u;
     const uint32_t hist_bytes = (hist_words * 8u + 15u) & ~15u;
     unsigned long long* hA = reinterpret_cast<unsigned long long*>(smem);
+    unsigned long long* hT = hA + (hist_words >= 2u ? hist_words - 2u : 0u);  // LDS_HIST: {T, ambiguous}
     unsigned long long* hB = hA + G;              // KM_REF: Tot_ref
     double* hW = reinterpret_cast<double*>(hA + G);  // KM_LOCAL: W
     const uint32_t buf = src.buf_bytes;
@@ -480,12 +482,17 @@ __global__ __launch_bounds__(BLOCK_THREADS, (KT && NWIN == 1 && MODE == KM_GLOBA
         if (cunit != ~0ull) amb += (cmax >= 0 && cmin != cmax) ? 1u : 0u;
         const unsigned long long tsum = wave_sum<unsigned long long>((unsigned long long)t_cnt);
         if (lane == 0) {
-            if (tsum) atomicAdd(&out_a[0], tsum);
-            if (amb) atomicAdd(&out_a[1], (unsigned long long)amb);
+            unsigned long long* tgt = LDS_HIST ? hT : out_a;
+            if (tsum) atomicAdd(&tgt[0], tsum);
+            if (amb) atomicAdd(&tgt[1], (unsigned long long)amb);
         }
     }
     if (LDS_HIST) {
         __syncthreads();
+        if (MODE != KM_REF && threadIdx.x < 2u) {
+            const unsigned long long x = hT[threadIdx.x];
+            if (x) atomicAdd(&out_a[threadIdx.x], x);
+        }
         for (uint32_t g = threadIdx.x; g < G; g += BLOCK_THREADS) {
             const unsigned long long a = hA[g];
             if (a) atomicAdd(&gU[g], a);
@@ -692,9 +699,11 @@ void k_scan_kt(DevView I, UnitSrc src, unsigned long long* __restrict__ out_a, d
     // branches on them are uniform (no exec-mask bookkeeping)
     const uint32_t wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t G = I.G, k = src.k;
-    const uint32_t hist_words = LDS_HIST ? ((MODE == KM_GLOBAL) ? G : 2u * G) : 0u;
+    // (+ 2 words: the workgroup's T and ambiguous units, flushed with the histogram: ax_scan.hip §4i)
+    const uint32_t hist_words = LDS_HIST ? ((MODE == KM_GLOBAL) ? G : 2u * G) + 2u : 0u;
     const uint32_t hist_bytes = (hist_words * 8u + 15u) & ~15u;
     unsigned long long* hA = reinterpret_cast<unsigned long long*>(smem);
+    unsigned long long* hT = hA + (hist_words >= 2u ? hist_words - 2u : 0u);  // LDS_HIST: {T, ambiguous}
     double* hW = reinterpret_cast<double*>(hA + G);  // KM_LOCAL: W
     const uint32_t buf = src.buf_bytes;
     double2* qtab = reinterpret_cast<double2*>(smem + hist_bytes);  // KM_LOCAL only
@@ -1006,11 +1015,16 @@ void k_scan_kt(DevView I, UnitSrc src, unsigned long long* __restrict__ out_a, d
     if (cunit != ~0ull) amb += (uint32_t)cmax;
     const unsigned long long tsum = wave_sum<unsigned long long>((unsigned long long)t_cnt);
     if (lane == 0) {
-        if (tsum) atomicAdd(&out_a[0], tsum);
-        if (amb) atomicAdd(&out_a[1], (unsigned long long)amb);
+        unsigned long long* tgt = LDS_HIST ? hT : out_a;
+        if (tsum) atomicAdd(&tgt[0], tsum);
+        if (amb) atomicAdd(&tgt[1], (unsigned long long)amb);
     }
     if (LDS_HIST) {
         __syncthreads();
+        if (threadIdx.x < 2u) {
+            const unsigned long long x = hT[threadIdx.x];
+            if (x) atomicAdd(&out_a[threadIdx.x], x);
+        }
         for (uint32_t g = threadIdx.x; g < G; g += BLOCK_THREADS) {
             const unsigned long long a = hA[g];
             if (a) atomicAdd(&gU[g], a);
@@ -1469,7 +1483,7 @@ int launch_scan(speq_device_index* d, int mode, bool paired, const UnitSrc& src,
     if (src.ax_stats) return -1;  // the diagnostic twin exists for k_scan_ax only: launch nothing
     const speq_device_index::KmerTable* kt = ensure_ktab(d, src.k);
     const bool lds_hist = d->G <= LDS_HIST_MAX_G;
-    const uint32_t hist_words = lds_hist ? ((mode == KM_GLOBAL) ? d->G : 2u * d->G) : 0u;
+    const uint32_t hist_words = lds_hist ? ((mode == KM_GLOBAL) ? d->G : 2u * d->G) + 2u : 0u;
     const size_t lds = ((hist_words * 8u + 15u) & ~15u) + (mode == KM_LOCAL ? QTAB_BYTES : 0u) +
                        (size_t)WAVES_PER_BLOCK * wave_lds_bytes(src.buf_bytes, mode == KM_LOCAL);
     // >= 4 units (or 256 windows) per wave; grid capped (default 4096 = 2x the 8 resident blocks x 256 CUs).
