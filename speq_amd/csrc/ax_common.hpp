@@ -254,11 +254,15 @@ __device__ __forceinline__ bool ax_probe(const AxView& A, const __amdgpu_buffer_
 //   defl   u16 [ax_def]         deferred windows (lane | window << 6), defn u32[4] counters, ambf/ambd i32[64]
 //   wl     u32 [AX_WL]          (local) weight work list: 8-window blocks of runs with varying qualities
 //                               (lane | block << 6 | window mask << 11); wlm u32 [64] the lane's run (group | j << 16)
-#ifndef SPEQ_AX_WL  // weight work-list entries per wave (A/B knob): 64 lanes x AX_WL / 64 blocks per pass
+// local mode's factor table in LDS (k_scan_ax): ftab[AX_FTAB] indexed by min(quality byte, 75), entry AX_FONE = 1.0,
+// then wtab[QLUT_LEN], within the QTAB_BYTES the launch reserves
+constexpr uint32_t AX_FONE = 76u, AX_FTAB = AX_FONE + 1u;
+static_assert(8u * (AX_FTAB + QLUT_LEN) <= QTAB_BYTES && AX_FONE - 1u == 33u + 41u + 1u, "ftab + wtab in QTAB_BYTES");
+#ifndef SPEQ_AX_WL  // weight work-list entries per wave (A/B knob): the blocks of one round of the weighing pass
 #define SPEQ_AX_WL 128
 #endif
-constexpr uint32_t AX_WL = SPEQ_AX_WL, AX_WL_TAKE = AX_WL / 64u;
-static_assert(AX_WL % 64u == 0 && AX_WL_TAKE >= 1u && AX_WL_TAKE <= 7u, "work list: 1-7 blocks per lane per pass");
+constexpr uint32_t AX_WL = SPEQ_AX_WL;
+static_assert(AX_WL % 64u == 0 && AX_WL >= 64u && AX_WL <= 512u, "work list: 1-8 sub-batches of 64 blocks per round");
 #ifndef SPEQ_AX_SU  // staging: stream instructions per load batch (A/B knob; 3 at 5 waves spills 20-36 B per lane)
 #define SPEQ_AX_SU 2
 #endif

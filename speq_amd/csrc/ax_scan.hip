@@ -310,8 +310,10 @@ __global__ __launch_bounds__(AX_THREADS, (ax_min_waves<MODE, HW, EM, STATS>())) 
     const uint32_t hist_bytes = (hist_words * 8u + 15u) & ~15u;
     unsigned long long* hA = reinterpret_cast<unsigned long long*>(smem);
     double* hW = reinterpret_cast<double*>(hA + G);
-    double2* qtab = reinterpret_cast<double2*>(smem + hist_bytes);  // KM_LOCAL
-    double* wtab = reinterpret_cast<double*>(qtab + QLUT_LEN);
+    // KM_LOCAL: ftab[min(byte, 75)] = fl(1 / lut[q]) of the quality byte's rank q (bytes <= 33 rank 0, >= 74 rank 41;
+    // entry 76 = 1.0, the factor of a byte outside a product), wtab[q] = the weight of a window of k bytes of rank q
+    double* ftab = reinterpret_cast<double*>(smem + hist_bytes);
+    double* wtab = ftab + AX_FTAB;
     const uint32_t qtab_bytes = MODE == KM_LOCAL ? QTAB_BYTES : 0u;
     constexpr uint32_t WAVE_BYTES = ax_wave_bytes<MODE>();
     unsigned char* wb = smem + hist_bytes + qtab_bytes + wid * WAVE_BYTES;
@@ -333,12 +335,15 @@ __global__ __launch_bounds__(AX_THREADS, (ax_min_waves<MODE, HW, EM, STATS>())) 
     uint8_t* ownb = reinterpret_cast<uint8_t*>(MODE == KM_LOCAL ? wlm + 64 : wl);  // [AX_OWNB] staging owner map
 
     if (MODE == KM_LOCAL)
-        for (uint32_t i = threadIdx.x; i < QLUT_LEN; i += AX_THREADS) {
-            const double lut = src.qlut[2 * i], inv = src.qlut[2 * i + 1];
-            qtab[i] = make_double2(lut, inv);
-            double x = 1.0;  // fm_scanner.cpp:454, k bases of quality i
-            for (uint32_t j = 0; j < k; ++j) x = div_rn(x, lut, inv);
-            wtab[i] = x;
+        for (uint32_t i = threadIdx.x; i < AX_FTAB; i += AX_THREADS) {
+            const int q = (int)i - 33;
+            ftab[i] = i == AX_FONE ? 1.0 : src.qlut[2 * (q < 0 ? 0 : (q > 41 ? 41 : q)) + 1];
+            if (i < QLUT_LEN) {
+                const double lut = src.qlut[2 * i], inv = src.qlut[2 * i + 1];
+                double x = 1.0;  // fm_scanner.cpp:454, k bases of quality i
+                for (uint32_t j = 0; j < k; ++j) x = div_rn(x, lut, inv);
+                wtab[i] = x;
+            }
         }
     if (LDS_HIST)
         for (uint32_t i = threadIdx.x; i < hist_words; i += AX_THREADS) hA[i] = 0ull;
@@ -421,138 +426,91 @@ __global__ __launch_bounds__(AX_THREADS, (ax_min_waves<MODE, HW, EM, STATS>())) 
         }
         return end;
     };
-    // Phred weight of the window whose first quality byte is src.qual[qo]. fm_scanner.cpp:454 divides 1 by the lut
-    // values of its k qualities in turn: a window of one quality takes that quotient from wtab (bit-exact); any
-    // other window is the product of the k reciprocals qtab[q].y = fl(1 / lut[q]), within 3 k 2^-53 of the
-    // reference's quotient (relative). Qualities are read as the aligned dwords that hold them.
-    auto weight = [&](uint64_t qo, bool uniform) -> double {
-        const uintptr_t ad = reinterpret_cast<uintptr_t>(src.qual + qo);
-        const uint32_t* wp = reinterpret_cast<const uint32_t*>(ad & ~(uintptr_t)3);
-        const uint32_t sh = (uint32_t)ad & 3u;
-        auto qof = [](uint32_t byte) -> uint32_t {
-            const int q = (int)byte - 33;
-            return q < 0 ? 0u : (q > 41 ? 41u : (uint32_t)q);
-        };
-        if (uniform) {
-            if (STATS) s_qb += 1u;
-            return wtab[qof((wp[0] >> (8u * sh)) & 0xFFu)];
-        }
-        // (k > 32: the dwords four at a time, as weight8's middle product)
-        const uint32_t nd = (sh + k + 3u) >> 2;
-        double x = 1.0;
-        if constexpr (HW >= 2) {
-            for (uint32_t t = 0; t < nd; t += 4u) {
-                uint32_t w[4];
-#pragma unroll
-                for (uint32_t i = 0; i < 4u; ++i) w[i] = t + i < nd ? wp[t + i] : 0u;
-                double pw[4];
-#pragma unroll
-                for (uint32_t i = 0; i < 4u; ++i) {
-                    double f[4];
-#pragma unroll
-                    for (uint32_t b = 0; b < 4u; ++b) {
-                        const uint32_t idx = 4u * (t + i) + b;  // the window's base idx - sh
-                        const double y = qtab[qof((w[i] >> (8u * b)) & 0xFFu)].y;
-                        f[b] = (t + i < nd && idx >= sh && idx < sh + k) ? y : 1.0;
-                    }
-                    pw[i] = (f[0] * f[1]) * (f[2] * f[3]);
-                }
-                x *= (pw[0] * pw[1]) * (pw[2] * pw[3]);
-            }
-        } else {
-            for (uint32_t t = 0; t < nd; ++t) {
-                const uint32_t w = wp[t];
-#pragma unroll
-                for (uint32_t b = 0; b < 4u; ++b) {
-                    const uint32_t idx = 4u * t + b;  // the window's base idx - sh
-                    const double f = qtab[qof((w >> (8u * b)) & 0xFFu)].y;
-                    x = (idx >= sh && idx < sh + k) ? x * f : x;
-                }
-            }
-        }
-        if (STATS) s_qb += k;
-        return x;
-    };
+    // the factor of quality byte x (its low 8 bits): fl(1 / lut[q]) for its rank q (phred42: bytes below '!' rank 0,
+    // above 'J' rank 41)
+    auto fac = [&](uint32_t x) -> double { return ftab[min(x & 0xFFu, AX_FONE - 1u)]; };
     // the summed weights of the windows t (bits of mask, t < 8) of a block whose first window's first quality byte is
-    // src.qual[qo] (k >= 8): every window t is L_t M R_t with M the product of the reciprocals of bytes 7 .. k - 1
-    // (shared by the 8 windows), L_t of bytes t .. 6 and R_t of bytes k .. k + t - 1, so k + 21 products weigh 8
-    // windows instead of 8 k. Any product tree over k factors rounds k - 1 times: the bound of weight() holds.
-    // Only the dwords that hold a byte of a window in the mask are read (none past the read's last quality byte).
+    // src.qual[qo] (k >= 8). fm_scanner.cpp:454 divides 1 by the lut values of a window's k qualities in turn; here
+    // window t (bytes t .. t + k - 1 of the block) is S[t] P[t], S[t] the product of the reciprocals ftab of bytes
+    // t .. 7 (a chain from byte 7 down), P[t] that of bytes 8 .. k + t - 1 (the middle product M of bytes 8 .. k - 1,
+    // then one byte more per window): a product tree over the window's k factors, k - 1 roundings, within 3 k 2^-53 of
+    // the reference's quotient (relative), and added to the block's sum by one fma (exact product).
+    // Every quality dword of the block is loaded before the first product (one round trip; the middle product's next
+    // 16 bytes are loaded while the current 16 are multiplied, k > 24), and the factors' LDS reads issue in groups
+    // rather than one wait per factor. Dwords past the last byte of the last window in the mask are not read (their
+    // indices clamp to it; nothing past the read's end), and the middle product's bytes past k - 1 read ftab's 1.0.
     auto weight8 = [&](uint64_t qo, uint32_t mask) -> double {
         const uintptr_t ad = reinterpret_cast<uintptr_t>(src.qual + qo);
         const uint32_t* wp = reinterpret_cast<const uint32_t*>(ad & ~(uintptr_t)3);
         const uint32_t sh = (uint32_t)ad & 3u;
-        auto qinv = [&](uint32_t byte) -> double {
-            const int q = (int)(byte & 0xFFu) - 33;
-            return qtab[q < 0 ? 0 : (q > 41 ? 41 : q)].y;
-        };
         const uint32_t tmax = 31u - (uint32_t)__builtin_clz(mask);  // the last window of the block to weigh
-        const uint32_t a0 = wp[0], a1 = wp[1], a2 = sh >= 2u ? wp[2] : 0u;
+        const uint32_t dl = (sh + k + tmax - 1u) >> 2;                 // the dword of its last byte
+        auto ld = [&](uint32_t i) -> uint32_t { return wp[min(i, dl)]; };
+        const uint32_t a0 = ld(0), a1 = ld(1), a2 = ld(2);  // bytes 0 .. 7
+        const uint32_t rs = sh + k, rd = rs >> 2, rsh = rs & 3u;
+        const uint32_t c0 = ld(rd), c1 = ld(rd + 1u), c2 = ld(rd + 2u);  // bytes k .. k + 6
+        uint32_t w[5];  // the middle product's first 16 bytes (8 .. 23)
+#pragma unroll
+        for (uint32_t i = 0; i < 5u; ++i) w[i] = ld(2u + i);
         const uint32_t l03 = __builtin_amdgcn_alignbyte(a1, a0, sh), l47 = __builtin_amdgcn_alignbyte(a2, a1, sh);
-        const uint32_t rs = sh + k, rsh = rs & 3u, rlast = rsh + tmax;  // right bytes k .. k + tmax - 1
-        const uint32_t* rp = wp + (rs >> 2);
-        const uint32_t c0 = tmax >= 1u ? rp[0] : 0u, c1 = rlast > 4u ? rp[1] : 0u, c2 = rlast > 8u ? rp[2] : 0u;
         const uint32_t r03 = __builtin_amdgcn_alignbyte(c1, c0, rsh), r47 = __builtin_amdgcn_alignbyte(c2, c1, rsh);
-        // k > 32: the middle bytes' dwords four at a time (their loads issued together), each group's factors as a
-        // product tree (a factor outside the window is 1.0, whose product is exact), and the right bytes' products
-        // R[t] as a chain of their own beside M's (window t = L[t] (M R[t])): short dependent chains instead of one
-        // of k + 7 products with a load wait per dword (k = 70 varying qualities -5 %; at k <= 32 the 4-dword groups
-        // evaluate more masked factors than they save: +5 %, so the one chain stays; profiles/r05/ab_weight_trees.jsonl)
+        double S[8];
+        S[7] = fac(l47 >> 24);
+#pragma unroll
+        for (int t = 6; t >= 0; --t) S[t] = fac((t < 4 ? l03 : l47) >> (8 * (t & 3))) * S[t + 1];
         double M = 1.0;
-        const uint32_t t0 = (sh + 7u) >> 2, t1 = (sh + k - 1u) >> 2;
-        if constexpr (HW >= 2) {
-            for (uint32_t t = t0; t <= t1; t += 4u) {
-                uint32_t w[4];
+        const uint32_t nbat = (k + 7u) >> 4;  // 16-byte batches of bytes 8 .. k - 1 (uniform)
+        auto batch = [&](uint32_t j) {
+            uint32_t e[4];
 #pragma unroll
-                for (uint32_t i = 0; i < 4u; ++i) w[i] = t + i <= t1 ? wp[t + i] : 0u;
-                double pw[4];
+            for (uint32_t i = 0; i < 4u; ++i) e[i] = __builtin_amdgcn_alignbyte(w[i + 1], w[i], sh);
+            if (j + 1u < nbat) {  // the next 16 bytes' dwords, before this batch's factors
+                w[0] = w[4];
 #pragma unroll
-                for (uint32_t i = 0; i < 4u; ++i) {
-                    double f[4];
-#pragma unroll
-                    for (uint32_t b = 0; b < 4u; ++b) {
-                        const uint32_t idx = 4u * (t + i) + b;
-                        const double x = qinv(w[i] >> (8u * b));
-                        f[b] = (t + i <= t1 && idx >= sh + 7u && idx < sh + k) ? x : 1.0;
-                    }
-                    pw[i] = (f[0] * f[1]) * (f[2] * f[3]);
-                }
-                M *= (pw[0] * pw[1]) * (pw[2] * pw[3]);
+                for (uint32_t i = 1; i < 5u; ++i) w[i] = ld(6u + 4u * j + i);
             }
+            double f[16];
+#pragma unroll
+            for (uint32_t i = 0; i < 16u; ++i) {
+                const uint32_t b = 8u + 16u * j + i;  // (b < k: uniform)
+                f[i] = ftab[b < k ? min((e[i >> 2] >> (8u * (i & 3u))) & 0xFFu, AX_FONE - 1u) : AX_FONE];
+            }
+#pragma unroll
+            for (uint32_t h = 8; h >= 1u; h >>= 1)
+#pragma unroll
+                for (uint32_t i = 0; i < h; ++i) f[i] = f[i] * f[i + h];
+            M *= f[0];
+        };
+        if constexpr (HW == 1) {  // (k <= 32: at most 2 batches, unrolled)
+            if (nbat > 0u) batch(0);
+            if (nbat > 1u) batch(1);
         } else {
-            for (uint32_t t = t0; t <= t1; ++t) {
-                const uint32_t w = wp[t];
-#pragma unroll
-                for (uint32_t b = 0; b < 4u; ++b) {
-                    const uint32_t idx = 4u * t + b;
-                    const double f = qinv(w >> (8u * b));
-                    M = (idx >= sh + 7u && idx < sh + k) ? M * f : M;
-                }
-            }
+            for (uint32_t j = 0; j < nbat; ++j) batch(j);
         }
-        double L[8];
-        L[7] = 1.0;
+        double sum = 0.0, P = M;
 #pragma unroll
-        for (int t = 6; t >= 0; --t) L[t] = qinv((t < 4 ? l03 : l47) >> (8 * (t & 3))) * L[t + 1];
-        double sum = 0.0;
-        if constexpr (HW >= 2) {
-            double R[8];
-            R[0] = 1.0;
-#pragma unroll
-            for (uint32_t t = 1; t < 8u; ++t)
-                R[t] = R[t - 1] * qinv((t - 1u < 4u ? r03 : r47) >> (8u * ((t - 1u) & 3u)));
-#pragma unroll
-            for (uint32_t t = 0; t < 8u; ++t) sum += ((mask >> t) & 1u) ? L[t] * (M * R[t]) : 0.0;
-        } else {
-            double MR = M;
-#pragma unroll
-            for (uint32_t t = 0; t < 8u; ++t) {
-                sum += ((mask >> t) & 1u) ? L[t] * MR : 0.0;
-                if (t < 7u) MR *= qinv((t < 4u ? r03 : r47) >> (8u * (t & 3u)));
-            }
+        for (uint32_t t = 0; t < 8u; ++t) {
+            if (t > 0u) P *= fac((t - 1u < 4u ? r03 : r47) >> (8u * ((t - 1u) & 3u)));
+            const double x = fma(S[t], P, sum);  // (a window outside the mask may hold rank 0: inf)
+            sum = ((mask >> t) & 1u) ? x : sum;
         }
         if (STATS) s_qb += k + tmax;
         return sum;
+    };
+    // Phred weight of the window whose first quality byte is src.qual[qo]: a window of one quality takes
+    // fm_scanner.cpp:454's quotient from wtab (bit-exact); any other window (k >= 8) is weight8's block of one window,
+    // for k < 8 the product of its k reciprocals in order.
+    auto weight = [&](uint64_t qo, bool uniform) -> double {
+        if (uniform) {
+            if (STATS) s_qb += 1u;
+            const uint32_t x = src.qual[qo];
+            return wtab[x < 33u ? 0u : min(x - 33u, 41u)];
+        }
+        if (k >= 8u) return weight8(qo, 1u);
+        double x = 1.0;
+        for (uint32_t i = 0; i < k; ++i) x *= fac(src.qual[qo + i]);
+        if (STATS) s_qb += k;
+        return x;
     };
     // quality-change bits of slot o over slot positions [x, x + len) all zero (local mode)
     auto chg_zero = [&](uint32_t o, uint32_t x, uint32_t len) -> bool {
@@ -1472,7 +1430,11 @@ __global__ __launch_bounds__(AX_THREADS, (ax_min_waves<MODE, HW, EM, STATS>())) 
             }
             if (MODE == KM_LOCAL && __ballot(wl_pend) != 0) {
                 // runs with varying qualities: their own windows in 8-window blocks (20 per run), weighed by the
-                // whole wave, at most 4 blocks of every lane per pass (a lane sums a block's windows, one atomic)
+                // whole wave, every lane's blocks at once: each lane writes its blocks' entries at its prefix of the
+                // wave's block counts, AX_WL entries per round, and the wave weighs them 64 at a time (a lane sums a
+                // block's windows, one atomic). Rounds: usually one (AX_WL = 128, ~100 blocks per pass at config 2
+                // with varying qualities); at most 2 blocks of every lane per pass cost 2-5 passes, each with its
+                // own sub-batches of 64 (mostly idle lanes) and wave synchronisations.
                 uint32_t nzb = 0;
                 if (wl_pend) {
 #pragma unroll
@@ -1482,23 +1444,25 @@ __global__ __launch_bounds__(AX_THREADS, (ax_min_waves<MODE, HW, EM, STATS>())) 
                             nzb |= (((ownc[c] >> (8u * b)) & 0xFFu) != 0u ? 1u : 0u) << (4u * c + b);
                     wlm[lane] = wl_g | (wl_j << 16);
                 }
-                while (__ballot(nzb != 0u) != 0) {
-                    const uint32_t take = min((uint32_t)__popc(nzb), AX_WL_TAKE);
-                    uint32_t pre = 0, tot = 0;
+                const uint32_t cnt = (uint32_t)__popc(nzb);  // <= 20
+                uint32_t pre = 0, all = 0;
 #pragma unroll
-                    for (uint32_t b = 0; b < 3u; ++b) {
-                        const unsigned long long m = __ballot(((take >> b) & 1u) != 0u);
-                        pre += lanes_below(m) << b;
-                        tot += (uint32_t)__popcll(m) << b;
-                    }
-                    for (uint32_t t = 0; t < take; ++t) {
+                for (uint32_t b = 0; b < 5u; ++b) {
+                    const unsigned long long m = __ballot(((cnt >> b) & 1u) != 0u);
+                    pre += lanes_below(m) << b;
+                    all += (uint32_t)__popcll(m) << b;
+                }
+                for (uint32_t r0 = 0; r0 < all; r0 += AX_WL) {
+                    while (nzb != 0u && pre < r0 + AX_WL) {  // this lane's entries in [r0, r0 + AX_WL)
                         const uint32_t blk = (uint32_t)__builtin_ctz(nzb);
                         nzb &= nzb - 1u;
                         const uint32_t c = blk >> 2;
                         const uint32_t oc = c == 0u ? ownc[0] : (c == 1u ? ownc[1] : (c == 2u ? ownc[2] : (c == 3u ? ownc[3] : ownc[4])));
-                        wl[pre + t] = lane | (blk << 6) | (((oc >> (8u * (blk & 3u))) & 0xFFu) << 11);
+                        wl[pre - r0] = lane | (blk << 6) | (((oc >> (8u * (blk & 3u))) & 0xFFu) << 11);
+                        ++pre;
                     }
                     wave_sync();
+                    const uint32_t tot = min(all - r0, AX_WL);
                     for (uint32_t b0 = 0; b0 < tot; b0 += 64u) {
                         // the entry's lane o and the first base of o's piece (a full-wave shuffle, before the branch)
                         const uint32_t en = wl[min(b0 + lane, AX_WL - 1u)];

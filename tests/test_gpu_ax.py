@@ -256,7 +256,7 @@ def test_grid_generations_give_identical_counts(small):
         dev.tune(ax_generations=0)
 
 
-@pytest.mark.parametrize("k", [12, 21, 31, 70])
+@pytest.mark.parametrize("k", [5, 8, 9, 12, 21, 24, 25, 31, 32, 33, 40, 70, 97, 128])  # weight8's batch edges
 @pytest.mark.parametrize("paired", [False, True])
 def test_varying_quality_weights_within_the_documented_bound(k, paired):
     """Phred-weighted scans of reads whose qualities vary base by base (the anchor kernel's non-uniform path: k
@@ -283,7 +283,7 @@ def test_varying_quality_weights_within_the_documented_bound(k, paired):
     for g in range(24):
         tol = (3 * k + 2 * int(U[g]) + 2) * u * W[g]
         assert abs(got.weights[g] - W[g]) <= tol, (g, got.weights[g], W[g], tol)
-    assert int(U.sum()) > 2000  # enough windows counted for the bound to mean something
+    assert int(U.sum()) > (2000 if k <= 70 else 200)  # enough windows counted for the bound to mean something
 
 
 def test_suffix_sort_failure_leaves_a_working_replica(small, monkeypatch):
