@@ -256,7 +256,7 @@ def test_grid_generations_give_identical_counts(small):
         dev.tune(ax_generations=0)
 
 
-@pytest.mark.parametrize("k", [5, 8, 9, 12, 21, 24, 25, 31, 32, 33, 40, 70, 97, 128])  # weight8's batch edges
+@pytest.mark.parametrize("k", [12, 21, 24, 25, 31, 32, 33, 40, 70, 97, 128])  # weight8's batch edges
 @pytest.mark.parametrize("paired", [False, True])
 def test_varying_quality_weights_within_the_documented_bound(k, paired):
     """Phred-weighted scans of reads whose qualities vary base by base (the anchor kernel's non-uniform path: k
@@ -284,6 +284,40 @@ def test_varying_quality_weights_within_the_documented_bound(k, paired):
         tol = (3 * k + 2 * int(U[g]) + 2) * u * W[g]
         assert abs(got.weights[g] - W[g]) <= tol, (g, got.weights[g], W[g], tol)
     assert int(U.sum()) > (2000 if k <= 70 else 200)  # enough windows counted for the bound to mean something
+
+
+@pytest.mark.parametrize("k", [1, 3, 5, 7, 8, 9, 10])
+def test_varying_quality_weights_short_k(k):
+    """The same bound for k < 12, where windows are unique only if the groups share no k-mer: group 0's texts are
+    A/T only and group 1's C/G only (both alphabets closed under reverse complement), so every window of a read is
+    unique to its group. k < 8 weighs windows one by one (k reciprocal products in order), k = 8 is weight8 without a
+    middle product, 9-10 with one partial batch."""
+    rng = np.random.default_rng(100 + k)
+    recs = [bytes(rng.choice(np.frombuffer(a, dtype=np.uint8), size=1_500)) for a in (b"AT", b"AT", b"CG", b"CG")]
+    groups = [0, 0, 1, 1]
+    idx = FmIndex.build(recs, groups, 2, prefix_q=6, pair_steps=True, triple_steps=True)
+    dev = DeviceIndex(idx)
+    orc = Oracle(recs, groups, 2, k)
+    seqs = []
+    for _ in range(150):
+        r = recs[int(rng.integers(0, 4))]
+        a = int(rng.integers(0, len(r) - 150))
+        x = r[a:a + 150]
+        seqs.append(x.translate(COMP)[::-1] if rng.random() < 0.5 else x)
+    seq = np.frombuffer(b"".join(seqs), dtype=np.uint8)
+    off = np.arange(0, 150 * len(seqs) + 1, 150, dtype=np.uint64)
+    q = rng.integers(31, 42, size=len(seq)).astype(np.uint8)
+    q[rng.random(len(q)) < 0.01] = 20
+    qual = (q + 33).astype(np.uint8)
+    got = dev.scan(seq.tobytes(), qual.tobytes(), off, k=k, local=True)
+    T, amb, U, W = orc.scan(seq, qual, off, local=True)
+    assert (got.total, got.ambiguous, got.unique.tolist()) == (T, amb, U.tolist())
+    assert dev.tuning("last_kernel") == 3
+    u = 2.0 ** -53
+    for g in range(2):
+        tol = (3 * k + 2 * int(U[g]) + 2) * u * W[g]
+        assert abs(got.weights[g] - W[g]) <= tol, (g, got.weights[g], W[g], tol)
+    assert int(U.sum()) > 10_000
 
 
 def test_suffix_sort_failure_leaves_a_working_replica(small, monkeypatch):
