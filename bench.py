@@ -71,6 +71,10 @@ def parse_args(argv=None):
                    help="extra launch tuning key=value (speq_device_set_tuning), e.g. ilp_kt=2; repeatable")
     p.add_argument("--no-lf-compare", action="store_true",
                    help="skip timing the LF-step kernel beside the table kernel")
+    p.add_argument("--streams", type=int, default=2,
+                   help="HIP streams the timed steps alternate between (each with its own counters): consecutive "
+                        "batches overlap, the next scan's workgroups taking the CUs the previous one's drain leaves "
+                        "(default 2; 1 = every step on one stream, each waiting for the one before)")
     p.add_argument("--no-extra", action="store_true", help="skip the secondary lines")
     p.add_argument("--only", default="", help="comma-separated secondary lines to run (default: all)")
     p.add_argument("--k31-reads", type=int, default=0, help="reads per GPU of the k=31 line (0 = config 3/4)")
@@ -156,6 +160,9 @@ def relaunch_cmd(gpus: int, argv: list, port: int) -> list:
     arguments; WORLD_SIZE then equals --gpus in every rank."""
     return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={gpus}",
             "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + list(argv)
+
+
+_PIPE_STREAMS = {}  # device -> the bench's extra HIP streams (see run())
 
 
 class Ctx:
@@ -333,22 +340,77 @@ def run_workload(ctx: Ctx, cfg_no: int, k: int, n_reads: int, mode: str, steps: 
     d_w = torch.zeros(G, dtype=torch.float64, device=ctx.dev_t)
     local = mode == "local"
     stream = torch.cuda.current_stream(ctx.dev_t).cuda_stream
+    # --streams S: step i runs on stream i % S, each stream with its own batch of reads (stream 0: `reads`; stream
+    # s > 0: the reads after every rank's batch 0, so no batch's reads are another's) and its own counters, so the
+    # scans of consecutive batches overlap: the next scan's workgroups take the CUs the previous one's drain leaves
+    # (a pipeline of S batches in flight). With more ranks each step's counters are all-reduced on one
+    # communication stream, in step order on every rank, after that step's scan (events). Every stream's counters
+    # of its last timed step are checked against its batch scanned again on one stream; the per-launch kernel time
+    # (events) is taken with S = 1.
+    n_str = max(1, int(getattr(a, "streams", 1)))
+    xkey = (qual_profile, err, n_reads, n_str)
+    if prepared.get("x_key") != xkey:
+        xb = []
+        for si in range(1, n_str):
+            r = synth.make_reads(prepared["ref"], n_reads, start_index=(si * ctx.world + ctx.rank) * n_reads,
+                                 paired=paired, err_rate=err)
+            r = synth.apply_quality_profile(r, qual_profile)
+            xb.append(dict(reads=r, seq=torch.from_numpy(r.seq).to(ctx.dev_t),
+                           qual=torch.from_numpy(r.qual).to(ctx.dev_t),
+                           off=torch.from_numpy(r.offsets.astype(np.int64)).to(ctx.dev_t),
+                           kmers=int(np.maximum(np.diff(r.offsets).astype(np.int64) - k + 1, 0).sum())))
+        prepared.update(x_key=xkey, x_batches=xb)
+    # The extra streams (and the communication stream) are created once per process, before any other: HIP maps a
+    # new stream to a hardware queue of its own until GPU_MAX_HW_QUEUES (4) are in use, then shares the least used
+    # one — a stream created per line would sooner or later share the current stream's queue, and the two batches
+    # would run one after the other (scripts/overlap_probe.py).
+    ps = _PIPE_STREAMS.setdefault(ctx.device, [])
+    while len(ps) < n_str - 1 + (ctx.comm is not None):
+        ps.append(torch.cuda.Stream(ctx.dev_t))
+    bufs = [dict(seq=d_seq, qual=d_qual, off=d_off, n=reads.n, kmers=kmers_per_step, cnt=d_counts, w=d_w,
+                 stream=torch.cuda.current_stream(ctx.dev_t))]
+    for si, b in enumerate(prepared["x_batches"]):
+        bufs.append(dict(seq=b["seq"], qual=b["qual"], off=b["off"], n=b["reads"].n, kmers=b["kmers"],
+                         cnt=torch.zeros(G + 2, dtype=torch.int64, device=ctx.dev_t),
+                         w=torch.zeros(G, dtype=torch.float64, device=ctx.dev_t), stream=ps[si]))
+    comm_stream = ps[n_str - 1] if ctx.comm is not None and n_str > 1 else None
+    ev_scan = [torch.cuda.Event() for _ in bufs]
+    ev_comm = [torch.cuda.Event() for _ in bufs]
+    rot = {"i": 0, "n": 1, "kmers": 0}
+
+    def allreduce(b, st):
+        ctx.comm.allreduce_u64(b["cnt"].data_ptr(), G + 2, st)  # RCCL all-reduce of the G+2 counters over xGMI
+        if local:
+            ctx.comm.allreduce_f64(b["w"].data_ptr(), G, st)
 
     def step():
-        d_counts.zero_()
-        if local:
-            d_w.zero_()
-        dev.scan_device(d_seq.data_ptr(), d_qual.data_ptr(), d_off.data_ptr(), reads.n, k, d_counts.data_ptr(),
-                        d_w.data_ptr(), paired=paired, local=local, stream=stream)
-        if ctx.comm is not None:  # one RCCL all-reduce of the G+2 counters over xGMI (speq_allreduce_u64)
-            ctx.comm.allreduce_u64(d_counts.data_ptr(), G + 2, stream)
+        i = rot["i"] % rot["n"]
+        rot["i"] += 1
+        b, s = bufs[i], bufs[i]["stream"]
+        rot["kmers"] += b["kmers"]
+        with torch.cuda.stream(s):
+            b["cnt"].zero_()
             if local:
-                ctx.comm.allreduce_f64(d_w.data_ptr(), G, stream)
+                b["w"].zero_()
+            dev.scan_device(b["seq"].data_ptr(), b["qual"].data_ptr(), b["off"].data_ptr(), b["n"], k,
+                            b["cnt"].data_ptr(), b["w"].data_ptr(), paired=paired, local=local,
+                            stream=s.cuda_stream)
+        if ctx.comm is not None:
+            if rot["n"] == 1:  # one stream: the all-reduce follows the scan on it
+                allreduce(b, s.cuda_stream)
+            else:
+                ev_scan[i].record(s)
+                comm_stream.wait_event(ev_scan[i])
+                allreduce(b, comm_stream.cuda_stream)
+                ev_comm[i].record(comm_stream)
+                s.wait_event(ev_comm[i])  # the stream's next step zeroes these counters after their all-reduce
 
     def timed_run(n_steps, n_warm, events=True):
+        rot["i"], rot["n"] = 0, 1 if events else n_str
         for _ in range(n_warm):
             step()
         torch.cuda.synchronize()
+        rot["kmers"] = 0  # k-mers of the timed steps only
         ctx.barrier()
         torch.cuda.synchronize()
         dev.timing(events)
@@ -368,6 +430,18 @@ def run_workload(ctx: Ctx, cfg_no: int, k: int, n_reads: int, mode: str, steps: 
     # (scripts/step_overhead.py: 0.177 ms per step without them, 0.185-0.188 with), so the roofline's per-launch kernel
     # time comes from the same K steps timed once more with the events on (ms_per_step_with_events)
     elapsed, _, _ = timed_run(steps, warmup, events=False)
+    timed_kmers = rot["kmers"]
+    for b in bufs[1:]:  # the other streams' last scans against their batches scanned again on one stream
+        rb = dict(b, cnt=torch.zeros(G + 2, dtype=torch.int64, device=ctx.dev_t),
+                  w=torch.zeros(G, dtype=torch.float64, device=ctx.dev_t))
+        dev.scan_device(rb["seq"].data_ptr(), rb["qual"].data_ptr(), rb["off"].data_ptr(), rb["n"], k,
+                        rb["cnt"].data_ptr(), rb["w"].data_ptr(), paired=paired, local=local, stream=stream)
+        if ctx.comm is not None:
+            allreduce(rb, stream)
+        torch.cuda.synchronize()
+        if not np.array_equal(b["cnt"].cpu().numpy(), rb["cnt"].cpu().numpy()) or (
+                local and not np.allclose(b["w"].cpu().numpy(), rb["w"].cpu().numpy(), rtol=1e-12, atol=0)):
+            raise RuntimeError("a pipelined scan disagrees with the same batch scanned on one stream")
     elapsed_ev, kernel_ms, launches = timed_run(steps, 0, events=True)
     counts = d_counts.cpu().numpy()
     weights = d_w.cpu().numpy() if local else None
@@ -397,7 +471,7 @@ def run_workload(ctx: Ctx, cfg_no: int, k: int, n_reads: int, mode: str, steps: 
               "avg_kernel_ms": lf_ms / max(1, lf_n),
               "path": "k_scan<..., KT = false>: q-mer table + three-base LF steps + label-run classification"}
 
-    total_kmers = kmers_per_step * ctx.world * steps
+    total_kmers = timed_kmers * ctx.world
     value = total_kmers / elapsed
     avg_kernel_s = (kernel_ms / 1e3) / max(1, launches)
     ax_stats = req = None
@@ -447,7 +521,7 @@ def run_workload(ctx: Ctx, cfg_no: int, k: int, n_reads: int, mode: str, steps: 
              **({"W_sum": float(weights.sum())} if weights is not None else {})}
     out = {
         "value": value, "ms_per_step": elapsed / steps * 1e3, "avg_kernel_ms": avg_kernel_s * 1e3,
-        "ms_per_step_with_events": elapsed_ev / steps * 1e3, "k": k,
+        "ms_per_step_with_events": elapsed_ev / steps * 1e3, "k": k, "streams": n_str,
         "mode": mode,
         "workload": f"BASELINE config {cfg_no}: {c['n_variants']} variants x {c['n_isolates']} isolates x "
                     f"{c['length']} bp, {n_reads} x 150 bp {'pairs' if paired else 'reads'} per GPU, k={k}, {mode}"
@@ -501,8 +575,11 @@ def compact_result(head: dict, lines: dict, meta: dict) -> dict:
         "metric": meta["metric"], "value": head["value"], "unit": "k-mers/s", "n_gpus": meta["n_gpus"],
         "steps": meta["steps"], "warmup": meta["warmup"], "ms_per_step": head["ms_per_step"],
         "ms_per_step_with_events": head.get("ms_per_step_with_events"),
-        "timing": "value: K steps without per-launch events; roofline.avg_kernel_ms: the same K steps again with HIP "
-                  "events around every launch on its stream",
+        "streams": head.get("streams", 1),
+        "timing": "value: K steps without per-launch events" + (
+            f", step i on HIP stream i % {head.get('streams')} (consecutive batches overlap)"
+            if head.get("streams", 1) > 1 else "") + "; roofline.avg_kernel_ms: the same K steps again on one "
+                  "stream with HIP events around every launch",
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u32",
         "data": "synthetic (splitmix64 references/reads, SURVEY.md §8(d))",
         "config": meta["config"],
@@ -533,6 +610,9 @@ def main(argv=None):
         # nothing has touched a GPU in this process: start the N ranks as a child and exit with its status
         sys.exit(subprocess.call(relaunch_cmd(a.gpus, argv, free_port())))
     ctx = Ctx(a)
+    # the pipeline's streams first, so they get hardware queues of their own (run())
+    _PIPE_STREAMS[ctx.device] = [ctx.torch.cuda.Stream(ctx.dev_t)
+                                 for _ in range(max(0, a.streams - 1) + (ctx.comm is not None))]
     from speq_amd import synth
 
     c = dict(synth.CONFIGS[a.config])

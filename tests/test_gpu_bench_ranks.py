@@ -25,9 +25,14 @@ import bench  # noqa: E402
 READS = 100_000
 
 
-def test_bench_two_ranks_on_one_gpu(tmp_path):
+@pytest.mark.parametrize("streams", [1, 2])
+def test_bench_two_ranks_on_one_gpu(tmp_path, streams):
+    """streams = 2: each rank pipelines two batches on two HIP streams, the counters all-reduced on a third (the
+    communication stream) in step order; the line's check is stream 0's batch, the other stream's is checked by the
+    bench itself against its batch scanned again on one stream."""
     detail = tmp_path / "detail.json"
-    cmd = [sys.executable, "-u", os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "3", "--warmup", "1",
+    cmd = [sys.executable, "-u", os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "4", "--warmup", "2",
+           "--streams", str(streams),
            "--reads", str(READS), "--no-extra", "--no-cpu-baseline", "--no-pcie", "--no-lf-compare",
            "--detail", str(detail)]
     env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
@@ -57,4 +62,5 @@ def test_bench_two_ranks_on_one_gpu(tmp_path):
     assert out["check"]["U_sha1"] == bench.u_sha1(r.unique)
     kmers = int(np.maximum(np.diff(reads.offsets).astype(np.int64) - 21 + 1, 0).sum())
     # value = all ranks' k-mers / max-over-ranks time
-    assert out["value"] == pytest.approx(kmers * 3 / (out["ms_per_step"] * 3 / 1e3), rel=1e-6)
+    assert out["streams"] == streams
+    assert out["value"] == pytest.approx(kmers * 4 / (out["ms_per_step"] * 4 / 1e3), rel=1e-6)
