@@ -634,7 +634,7 @@ def main(argv=None):
                                                      with_pcie=False, with_cpu=False, cpu_seconds=0, prepared=prep)
         if want("k31") or want("cli_e2e"):
             n31 = a.k31_reads or (10_000_000 if ctx.world == 1 else synth.CONFIGS[4]["n_reads"] // 8)
-            lines["k31"], p31 = run_workload(ctx, 3, 31, n31, "global", max(10, a.steps // 2), max(3, a.warmup),
+            lines["k31"], p31 = run_workload(ctx, 3, 31, n31, "global", max(20, a.steps), max(3, a.warmup),
                                              with_lf=False, with_pcie=False, with_cpu=cpu_on, cpu_seconds=short_cpu)
             lines["k31"]["note"] = ("config 3 (10 M reads on one GPU); with 8 ranks each scans config 4's 12.5 M-read "
                                     "shard of the same index")
@@ -661,13 +661,13 @@ def main(argv=None):
                                                  err=0.005)
         if a.cfg5_pairs and (want("cfg5_paired") or want("cfg5_paired_local")):
             # BASELINE config 5 (the north_star's scaling config): paired, k = 31, on a per-GPU sample of its pairs
-            lines["cfg5_paired"], p5 = run_workload(ctx, 5, 31, a.cfg5_pairs, "global", max(10, a.steps // 2),
+            lines["cfg5_paired"], p5 = run_workload(ctx, 5, 31, a.cfg5_pairs, "global", max(20, a.steps),
                                                     max(3, a.warmup), with_lf=False, with_pcie=False,
                                                     with_cpu=cpu_on, cpu_seconds=short_cpu)
             lines["cfg5_paired"]["note"] = (f"config 5 lists 500 M pairs (a node's job); each GPU scans a "
                                             f"{a.cfg5_pairs}-pair shard of the same deterministic pair stream")
             if want("cfg5_paired_local"):
-                lines["cfg5_paired_local"], _ = run_workload(ctx, 5, 31, a.cfg5_pairs, "local", max(10, a.steps // 2),
+                lines["cfg5_paired_local"], _ = run_workload(ctx, 5, 31, a.cfg5_pairs, "local", max(20, a.steps),
                                                              max(3, a.warmup), with_lf=False, with_pcie=False,
                                                              with_cpu=False, cpu_seconds=0, prepared=p5)
             p5["dev"].close()
