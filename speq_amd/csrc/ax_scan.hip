@@ -469,17 +469,22 @@ __global__ __launch_bounds__(AX_THREADS, (ax_min_waves<MODE, HW, EM, STATS>())) 
 #pragma unroll
                 for (uint32_t i = 1; i < 5u; ++i) w[i] = ld(6u + 4u * j + i);
             }
-            double f[16];
+            // 16 factors (HW = 4, whose other state holds more registers: two groups of 8, no spills)
+            constexpr uint32_t NF = HW >= 4 ? 8u : 16u;
 #pragma unroll
-            for (uint32_t i = 0; i < 16u; ++i) {
-                const uint32_t b = 8u + 16u * j + i;  // (b < k: uniform)
-                f[i] = ftab[b < k ? min((e[i >> 2] >> (8u * (i & 3u))) & 0xFFu, AX_FONE - 1u) : AX_FONE];
+            for (uint32_t g = 0; g < 16u; g += NF) {
+                double f[NF];
+#pragma unroll
+                for (uint32_t i = 0; i < NF; ++i) {
+                    const uint32_t b = 8u + 16u * j + g + i;  // (b < k: uniform)
+                    f[i] = ftab[b < k ? min((e[(g + i) >> 2] >> (8u * (i & 3u))) & 0xFFu, AX_FONE - 1u) : AX_FONE];
+                }
+#pragma unroll
+                for (uint32_t h = NF / 2u; h >= 1u; h >>= 1)
+#pragma unroll
+                    for (uint32_t i = 0; i < h; ++i) f[i] = f[i] * f[i + h];
+                M *= f[0];
             }
-#pragma unroll
-            for (uint32_t h = 8; h >= 1u; h >>= 1)
-#pragma unroll
-                for (uint32_t i = 0; i < h; ++i) f[i] = f[i] * f[i + h];
-            M *= f[0];
         };
         if constexpr (HW == 1) {  // (k <= 32: at most 2 batches, unrolled)
             if (nbat > 0u) batch(0);
