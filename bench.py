@@ -75,6 +75,9 @@ def parse_args(argv=None):
                    help="HIP streams the timed steps alternate between (each with its own counters): consecutive "
                         "batches overlap, the next scan's workgroups taking the CUs the previous one's drain leaves "
                         "(default 2; 1 = every step on one stream, each waiting for the one before)")
+    p.add_argument("--regions", type=int, default=5,
+                   help="timed regions of K steps per line (SURVEY §8(d): the median of 5 after warm-up); each region "
+                        "times the pipelined steps, the same steps on one stream, and one stream with per-launch events")
     p.add_argument("--no-extra", action="store_true", help="skip the secondary lines")
     p.add_argument("--only", default="", help="comma-separated secondary lines to run (default: all)")
     p.add_argument("--k31-reads", type=int, default=0, help="reads per GPU of the k=31 line (0 = config 3/4)")
@@ -142,7 +145,9 @@ def pick_transport(requested: str, world: int, n_devices: int) -> str:
     if requested not in ("auto", "rccl", "host"):
         raise LaunchError(f"--transport {requested}: auto, rccl or host")
     if world <= 1:
-        return "none"
+        # one rank: no collective, unless RCCL is asked for explicitly (a one-member communicator: the N > 1 code
+        # path — process group, RCCL streams, per-step all-reduce on the communication stream — on one GPU)
+        return "rccl" if requested == "rccl" and n_devices >= 1 else "none"
     if requested == "auto":
         return "rccl" if n_devices >= world else "host"
     return requested
@@ -162,7 +167,7 @@ def relaunch_cmd(gpus: int, argv: list, port: int) -> list:
             "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + list(argv)
 
 
-_PIPE_STREAMS = {}  # device -> the bench's extra HIP streams (see run())
+_PIPE_STREAMS = {}  # device -> the bench's extra HIP streams (created first, in Ctx; used by run_workload)
 
 
 class Ctx:
@@ -177,12 +182,24 @@ class Ctx:
         self.transport = pick_transport(a.transport, self.world, n_dev)
         # ranks beyond the visible GPUs share them round-robin (host transport only: RCCL needs one GPU per rank)
         self.device = self.local_rank % max(1, n_dev)
+        torch.cuda.set_device(self.device)
+        self.dev_t = torch.device(f"cuda:{self.device}")
+        # The pipeline's HIP streams (run_workload) are created FIRST, before torch's NCCL process group and the
+        # product's RCCL communicator create theirs: HIP gives a new stream a hardware queue of its own until
+        # GPU_MAX_HW_QUEUES (4) are in use and then shares the least used one, so streams created after RCCL's could
+        # share a queue with each other and the batches would run one after the other. The one-stream
+        # vs pipelined ratio of every line ("overlap") shows whether they did.
+        n_extra = max(0, int(getattr(a, "streams", 1)) - 1) + (1 if self.transport in ("rccl", "host") else 0)
+        _PIPE_STREAMS[self.device] = [torch.cuda.Stream(self.dev_t) for _ in range(n_extra)]
         if self.transport == "rccl":
+            if self.world == 1:  # forced at one rank (tests): a one-member group over the loopback rendezvous
+                os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+                os.environ.setdefault("MASTER_PORT", str(free_port()))
+                os.environ.setdefault("RANK", "0")
+                os.environ.setdefault("WORLD_SIZE", "1")
             dist.init_process_group("nccl", device_id=torch.device(f"cuda:{self.device}"))
         elif self.transport == "host":
             dist.init_process_group("gloo")
-        torch.cuda.set_device(self.device)
-        self.dev_t = torch.device(f"cuda:{self.device}")
         self.comm = None
         from speq_amd import Comm
         if self.transport == "rccl":
@@ -357,26 +374,29 @@ def run_workload(ctx: Ctx, cfg_no: int, k: int, n_reads: int, mode: str, steps: 
             r = synth.apply_quality_profile(r, qual_profile)
             xb.append(dict(reads=r, seq=torch.from_numpy(r.seq).to(ctx.dev_t),
                            qual=torch.from_numpy(r.qual).to(ctx.dev_t),
-                           off=torch.from_numpy(r.offsets.astype(np.int64)).to(ctx.dev_t),
-                           kmers=int(np.maximum(np.diff(r.offsets).astype(np.int64) - k + 1, 0).sum())))
+                           off=torch.from_numpy(r.offsets.astype(np.int64)).to(ctx.dev_t)))
         prepared.update(x_key=xkey, x_batches=xb)
-    # The extra streams (and the communication stream) are created once per process, before any other: HIP maps a
-    # new stream to a hardware queue of its own until GPU_MAX_HW_QUEUES (4) are in use, then shares the least used
-    # one — a stream created per line would sooner or later share the current stream's queue, and the two batches
-    # would run one after the other (scripts/overlap_probe.py).
+    # The extra streams (and the communication stream) were created once per process, before any other (Ctx): HIP
+    # maps a new stream to a hardware queue of its own until GPU_MAX_HW_QUEUES (4) are in use, then shares the least
+    # used one — a stream created per line (or after RCCL's) would sooner or later share another's queue, and the
+    # batches would run one after the other (scripts/overlap_probe.py).
     ps = _PIPE_STREAMS.setdefault(ctx.device, [])
     while len(ps) < n_str - 1 + (ctx.comm is not None):
         ps.append(torch.cuda.Stream(ctx.dev_t))
+
+    def kmers_at_k(offsets) -> int:  # windows of every read at THIS call's k (never cached across k)
+        return int(np.maximum(np.diff(offsets).astype(np.int64) - k + 1, 0).sum())
+
     bufs = [dict(seq=d_seq, qual=d_qual, off=d_off, n=reads.n, kmers=kmers_per_step, cnt=d_counts, w=d_w,
                  stream=torch.cuda.current_stream(ctx.dev_t))]
     for si, b in enumerate(prepared["x_batches"]):
-        bufs.append(dict(seq=b["seq"], qual=b["qual"], off=b["off"], n=b["reads"].n, kmers=b["kmers"],
+        bufs.append(dict(seq=b["seq"], qual=b["qual"], off=b["off"], n=b["reads"].n, kmers=kmers_at_k(b["reads"].offsets),
                          cnt=torch.zeros(G + 2, dtype=torch.int64, device=ctx.dev_t),
                          w=torch.zeros(G, dtype=torch.float64, device=ctx.dev_t), stream=ps[si]))
     comm_stream = ps[n_str - 1] if ctx.comm is not None and n_str > 1 else None
     ev_scan = [torch.cuda.Event() for _ in bufs]
     ev_comm = [torch.cuda.Event() for _ in bufs]
-    rot = {"i": 0, "n": 1, "kmers": 0}
+    rot = {"i": 0, "n": 1, "kmers": 0, "ran": set()}
 
     def allreduce(b, st):
         ctx.comm.allreduce_u64(b["cnt"].data_ptr(), G + 2, st)  # RCCL all-reduce of the G+2 counters over xGMI
@@ -388,6 +408,7 @@ def run_workload(ctx: Ctx, cfg_no: int, k: int, n_reads: int, mode: str, steps: 
         rot["i"] += 1
         b, s = bufs[i], bufs[i]["stream"]
         rot["kmers"] += b["kmers"]
+        rot["ran"].add(i)
         with torch.cuda.stream(s):
             b["cnt"].zero_()
             if local:
@@ -405,12 +426,13 @@ def run_workload(ctx: Ctx, cfg_no: int, k: int, n_reads: int, mode: str, steps: 
                 ev_comm[i].record(comm_stream)
                 s.wait_event(ev_comm[i])  # the stream's next step zeroes these counters after their all-reduce
 
-    def timed_run(n_steps, n_warm, events=True):
-        rot["i"], rot["n"] = 0, 1 if events else n_str
+    def timed_run(n_steps, n_warm, events=True, pipelined=False):
+        rot["i"], rot["n"] = 0, n_str if pipelined else 1
         for _ in range(n_warm):
             step()
         torch.cuda.synchronize()
         rot["kmers"] = 0  # k-mers of the timed steps only
+        rot["ran"] = set()
         ctx.barrier()
         torch.cuda.synchronize()
         dev.timing(events)
@@ -424,14 +446,51 @@ def run_workload(ctx: Ctx, cfg_no: int, k: int, n_reads: int, mode: str, steps: 
         elapsed = time.perf_counter() - t0
         kernel_ms, launches = dev.timing_read() if events else (0.0, 0)
         dev.timing(False)
+        expect = sum(bufs[i % rot["n"]]["kmers"] for i in range(n_steps))
+        if rot["kmers"] != expect:  # the timed k-mers are the steps' batches' windows at this k
+            raise RuntimeError(f"timed k-mers {rot['kmers']} != {expect} of the {n_steps} steps' batches at k={k}")
         return ctx.allreduce_max(elapsed), kernel_ms, launches
 
-    # `value`: the K steps as a job runs them. The scan's HIP timing events (two per launch) cost 6-10 µs per step
-    # (scripts/step_overhead.py: 0.177 ms per step without them, 0.185-0.188 with), so the roofline's per-launch kernel
-    # time comes from the same K steps timed once more with the events on (ms_per_step_with_events)
-    elapsed, _, _ = timed_run(steps, warmup, events=False)
-    timed_kmers = rot["kmers"]
-    for b in bufs[1:]:  # the other streams' last scans against their batches scanned again on one stream
+    def counters(b):
+        return b["cnt"].cpu().numpy().copy(), (b["w"].cpu().numpy().copy() if local else None)
+
+    def same(x, y) -> bool:
+        return np.array_equal(x[0], y[0]) and (not local or np.allclose(x[1], y[1], rtol=1e-12, atol=0))
+
+    # the median of `regions` timed regions of K steps after one warm-up. Each region times
+    #   (p) the K steps as a job runs them (step i on stream i % S): `value`;
+    #   (1) the same K steps on one stream, each waiting for the one before: `one_stream` and the overlap ratio
+    #       (1) / (p) — below 1.1 the streams ran one after the other (e.g. shared hardware queues at N = 8);
+    #   (e) (1) again with HIP events around every launch: the per-launch kernel time of the roofline (the events
+    #       cost 6-10 µs per step, scripts/step_overhead.py, so (p) and (1) run without them).
+    n_reg = max(1, int(getattr(a, "regions", 5)))
+    el_p, el_1, el_e, kms = [], [], [], []
+    ran_p = set()
+    snap_p = None
+    for r_i in range(n_reg):
+        e, _, _ = timed_run(steps, warmup if r_i == 0 else 0, events=False, pipelined=True)
+        el_p.append(e)
+        timed_kmers = rot["kmers"]
+        ran_p = set(rot["ran"])
+        if r_i == n_reg - 1:
+            snap_p = [counters(b) for b in bufs]  # every stream's last pipelined scan (checked below)
+        if n_str > 1:
+            el_1.append(timed_run(steps, 0, events=False)[0])
+            kmers_1 = rot["kmers"]
+        e, kmsum, launches = timed_run(steps, 0, events=True)
+        el_e.append(e)
+        kms.append(kmsum / max(1, launches))
+    elapsed = float(np.median(el_p))
+    elapsed_ev = float(np.median(el_e))
+    kernel_med = float(np.median(kms))
+    # the last pipelined scan of every stream that ran one against its batch scanned again on one stream; stream 0's
+    # against the events run's last scan (the same batch on one stream), whose counters the CPU baseline checks
+    one = counters(bufs[0])
+    if 0 in ran_p and not same(snap_p[0], one):
+        raise RuntimeError("the pipelined scan of stream 0 disagrees with the same batch scanned on one stream")
+    for si, b in enumerate(bufs[1:], start=1):
+        if si not in ran_p:
+            continue  # (fewer timed steps than streams: this stream's batch never ran)
         rb = dict(b, cnt=torch.zeros(G + 2, dtype=torch.int64, device=ctx.dev_t),
                   w=torch.zeros(G, dtype=torch.float64, device=ctx.dev_t))
         dev.scan_device(rb["seq"].data_ptr(), rb["qual"].data_ptr(), rb["off"].data_ptr(), rb["n"], k,
@@ -439,10 +498,24 @@ def run_workload(ctx: Ctx, cfg_no: int, k: int, n_reads: int, mode: str, steps: 
         if ctx.comm is not None:
             allreduce(rb, stream)
         torch.cuda.synchronize()
-        if not np.array_equal(b["cnt"].cpu().numpy(), rb["cnt"].cpu().numpy()) or (
-                local and not np.allclose(b["w"].cpu().numpy(), rb["w"].cpu().numpy(), rtol=1e-12, atol=0)):
+        if not same(snap_p[si], counters(rb)):
             raise RuntimeError("a pipelined scan disagrees with the same batch scanned on one stream")
-    elapsed_ev, kernel_ms, launches = timed_run(steps, 0, events=True)
+    timing = {
+        "regions": n_reg, "steps_per_region": steps,
+        "value_median": timed_kmers * ctx.world / elapsed,
+        "value_min": timed_kmers * ctx.world / max(el_p), "value_max": timed_kmers * ctx.world / min(el_p),
+        "ms_per_step": [round(x / steps * 1e3, 5) for x in el_p],
+        "avg_kernel_ms": [round(x, 5) for x in kms],
+        "avg_kernel_ms_median": kernel_med, "avg_kernel_ms_min": min(kms), "avg_kernel_ms_max": max(kms),
+    }
+    if el_1:
+        e1 = float(np.median(el_1))
+        timing["one_stream"] = {"value": kmers_1 * ctx.world / e1, "ms_per_step": e1 / steps * 1e3,
+                                "ms_per_step_all": [round(x / steps * 1e3, 5) for x in el_1]}
+        # k-mers/s pipelined over k-mers/s on one stream (equal-length reads: one-stream ms per step / pipelined)
+        timing["overlap"] = (timed_kmers / elapsed) / (kmers_1 / e1)
+    launches = steps
+    kernel_ms = kernel_med * launches
     counts = d_counts.cpu().numpy()
     weights = d_w.cpu().numpy() if local else None
     table_on = bool(ktab["table_bytes"])
@@ -513,9 +586,12 @@ def run_workload(ctx: Ctx, cfg_no: int, k: int, n_reads: int, mode: str, steps: 
                 "host_GB_per_s": 2 * len(seq_b) / best / 1e9}
 
     cpu = None
-    if with_cpu and ctx.rank == 0 and ctx.world == 1:
+    if with_cpu and ctx.rank == 0:
+        # rank 0 only, at any N (the other ranks wait at the next barrier); at N > 1 the timed counters are the
+        # all-reduced sums of every rank's shard, so only the sample check (`checked`) applies there
         cpu = cpu_baseline(prepared, reads, k, G, cpu_seconds, local, paired, extra_ports=cpu_extra_ports,
-                           timed_counts=(counts, weights))
+                           timed_counts=(counts, weights) if ctx.world == 1 else None)
+        cpu["ranks_waiting"] = ctx.world - 1
 
     check = {"T": int(counts[0]), "ambiguous": int(counts[1]), "U_sha1": u_sha1(counts[2:]),
              **({"W_sum": float(weights.sum())} if weights is not None else {})}
@@ -532,7 +608,7 @@ def run_workload(ctx: Ctx, cfg_no: int, k: int, n_reads: int, mode: str, steps: 
         "kmer_table": {"on": table_on, "distinct_kmers": ktab["distinct_kmers"], "bytes": ktab["table_bytes"],
                        "build_s": round(ktab["build_ms"] / 1e3, 4)},
         "roofline": roofline, "traffic_key": key, "cpu_baseline": cpu, "lf_steps": lf, "kmer_table_kernel": prev,
-        "pcie_inclusive": pcie, "check": check,
+        "pcie_inclusive": pcie, "check": check, "timing": timing,
         "detail": {"U": [int(x) for x in counts[2:]], "W": weights.tolist() if weights is not None else None,
                    "ax_work": ax_stats, "request_bytes_by_kind": req["parts"] if req else None},
     }
@@ -552,6 +628,12 @@ def compact_line(r: dict) -> dict:
     for key in ("ms_per_step", "avg_kernel_ms", "seconds", "unit"):
         if key in r:
             out[key] = r[key]
+    tm = r.get("timing") or {}
+    if tm:
+        out["value_min"], out["value_max"] = tm["value_min"], tm["value_max"]
+        if "one_stream" in tm:
+            out["one_stream_value"] = tm["one_stream"]["value"]
+            out["overlap"] = round(tm["overlap"], 4)
     if rf:
         out.update(frac=rf.get("frac"), traffic_frac=rf.get("traffic_frac"), l2_request_frac=rf.get("l2_request_frac"),
                    frac_basis=rf.get("frac_basis"))
@@ -567,6 +649,7 @@ def compact_result(head: dict, lines: dict, meta: dict) -> dict:
     """The ONE stdout JSON line (BASELINE keys + roofline + cpu_baseline + compact secondary lines), < LINE_LIMIT
     bytes; everything else goes to the detail file."""
     rf = dict(head["roofline"])
+    tm = head["timing"]
     roof = {k: rf.get(k) for k in ("bound", "achieved", "peak", "unit", "frac", "traffic", "traffic_frac",
                                    "frac_basis", "avg_kernel_ms", "traffic_source", "traffic_rocprof_kernel_ms",
                                    "l2_hit_rate", "l2_request_frac", "compulsory_frac", "survey_model_frac",
@@ -576,10 +659,15 @@ def compact_result(head: dict, lines: dict, meta: dict) -> dict:
         "steps": meta["steps"], "warmup": meta["warmup"], "ms_per_step": head["ms_per_step"],
         "ms_per_step_with_events": head.get("ms_per_step_with_events"),
         "streams": head.get("streams", 1),
-        "timing": "value: K steps without per-launch events" + (
-            f", step i on HIP stream i % {head.get('streams')} (consecutive batches overlap)"
-            if head.get("streams", 1) > 1 else "") + "; roofline.avg_kernel_ms: the same K steps again on one "
-                  "stream with HIP events around every launch",
+        "timing": f"value: the median of {tm['regions']} timed regions of K steps without per-launch events" + (
+            f", step i on HIP stream i % {head.get('streams')} (consecutive batches overlap); one_stream: the same "
+            "steps on one stream in each region (overlap = value / one_stream.value)"
+            if head.get("streams", 1) > 1 else "") + "; roofline.avg_kernel_ms: the median over the regions of "
+                  "the same K steps on one stream with HIP events around every launch",
+        "value_min": tm["value_min"], "value_max": tm["value_max"],
+        "one_stream": {k2: tm["one_stream"][k2] for k2 in ("value", "ms_per_step")} if "one_stream" in tm else None,
+        "overlap": tm.get("overlap"),
+        "avg_kernel_ms_min_max": [tm["avg_kernel_ms_min"], tm["avg_kernel_ms_max"]],
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u32",
         "data": "synthetic (splitmix64 references/reads, SURVEY.md §8(d))",
         "config": meta["config"],
@@ -609,10 +697,7 @@ def main(argv=None):
     if plan == "relaunch":
         # nothing has touched a GPU in this process: start the N ranks as a child and exit with its status
         sys.exit(subprocess.call(relaunch_cmd(a.gpus, argv, free_port())))
-    ctx = Ctx(a)
-    # the pipeline's streams first, so they get hardware queues of their own (run())
-    _PIPE_STREAMS[ctx.device] = [ctx.torch.cuda.Stream(ctx.dev_t)
-                                 for _ in range(max(0, a.streams - 1) + (ctx.comm is not None))]
+    ctx = Ctx(a)  # (creates the pipeline's streams before any collective's: Ctx.__init__)
     from speq_amd import synth
 
     c = dict(synth.CONFIGS[a.config])

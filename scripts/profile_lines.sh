@@ -16,7 +16,7 @@ declare -A ARGS=(
 NAMES=${*:-"cfg2 local k31 k70local k70err05 varq cfg5 cfg5local"}
 for n in $NAMES; do
   rm -rf gpurun_out/prof_$n
-  if [ $n = cfg2 ]; then P="trace req fetch write tcc sq sq2 ta"; else P="trace req"; fi
+  if [ $n = cfg2 ]; then P="trace req fetch write tcc sq sq2 ta"; else P="trace req tcc"; fi
   PASSES="$P" OUT=gpurun_out/prof_$n bash scripts/profile.sh ${ARGS[$n]} 2> gpurun_out/profile_$n.err || { echo "profile $n failed"; exit 1; }
   echo "profiled $n"
 done

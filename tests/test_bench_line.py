@@ -24,7 +24,13 @@ def _line(G=200, local=True):
     cpu = {"value": 1.1e7, "unit": "k-mers/s", "cores": 16, "kind": "port", "checked": True,
            "sample": "x" * 180, "host": {"cpu_model": "AMD EPYC 9575F 64-Core Processor", "rule": "y" * 80},
            "hash_port": {"value": 3.3e8, "sample": "z" * 150}, "label_run_port": {"value": 1e9, "sample": "w" * 150}}
+    timing = {"regions": 5, "steps_per_region": 20, "value_median": 5.1e11, "value_min": 5.012345e11,
+              "value_max": 5.212345e11, "ms_per_step": [0.2561234] * 5, "avg_kernel_ms": [0.2481234] * 5,
+              "avg_kernel_ms_median": 0.2481234, "avg_kernel_ms_min": 0.2461234, "avg_kernel_ms_max": 0.2501234,
+              "one_stream": {"value": 4.1234567e11, "ms_per_step": 0.3161234, "ms_per_step_all": [0.3161234] * 5},
+              "overlap": 1.2345678}
     return {"value": 5.1e11, "ms_per_step": 0.2561234, "avg_kernel_ms": 0.2481234, "k": 21, "mode": "local",
+            "timing": timing,
             "workload": "w" * 160, "roofline": rf, "cpu_baseline": cpu,
             "check": {"T": 130000000, "ambiguous": 3633, "U_sha1": "0123456789abcdef", "W_sum": 1.23456789e8},
             "detail": {"U": [10 ** 8] * G, "W": [1.234567891234e7] * G if local else None, "ax_work": ax}}
@@ -50,8 +56,11 @@ def test_compact_line_is_small_and_complete():
     assert {"achieved", "peak", "unit", "frac", "traffic", "avg_kernel_ms", "traffic_source"} <= set(out["roofline"])
     assert out["cpu_baseline"]["cores"] == 16 and out["cpu_baseline"]["kind"] == "port"
     assert "ax_work" not in s and "hash_port" not in s  # detail only
+    assert out["overlap"] == pytest.approx(1.2345678) and out["one_stream"]["value"] == pytest.approx(4.1234567e11)
+    assert out["value_min"] <= out["value"] <= out["value_max"]
+    assert "median of 5 timed regions" in out["timing"]
     for r in out["lines"].values():
-        assert {"value", "avg_kernel_ms", "frac", "traffic_frac", "check"} <= set(r)
+        assert {"value", "avg_kernel_ms", "frac", "traffic_frac", "check", "overlap"} <= set(r)
         assert "U" not in r["check"]
 
 
@@ -111,6 +120,9 @@ def test_launch_plan():
 
 def test_pick_transport():
     assert bench.pick_transport("auto", 1, 1) == "none"
+    assert bench.pick_transport("rccl", 1, 1) == "rccl"   # forced: a one-member RCCL communicator (GPU test)
+    assert bench.pick_transport("rccl", 1, 0) == "none"
+    assert bench.pick_transport("host", 1, 1) == "none"
     assert bench.pick_transport("auto", 8, 8) == "rccl"   # the driver's 8-GPU node: one rank per GPU
     assert bench.pick_transport("auto", 2, 1) == "host"   # two ranks on the one-GPU box
     assert bench.pick_transport("host", 8, 8) == "host"
