@@ -2,8 +2,8 @@
 """bench.py — k-mers scanned/sec of the MI355X SPeQ scan path (BASELINE.json `metric`).
 
 One "step" = one pass of the hot path (exact search of every k-mer window + unique-to-one-group tally) over this
-rank's batch of synthetic 150-bp reads already resident in HBM, followed by the RCCL all-reduce of the G+2
-counters (N > 1). Default workload = BASELINE config 2 (10 variants x 50 kb, 1M reads per GPU, k = 21, global
+rank's batch of synthetic 150-bp reads already resident in HBM; the K steps of a timed region are one job whose summed
+G + 2 counters are all-reduced over RCCL once at its end, inside the region (N > 1). Default workload = BASELINE config 2 (10 variants x 50 kb, 1M reads per GPU, k = 21, global
 mode) -> `value`. The same run also measures secondary lines (compact objects under "lines" in the JSON):
   * "local_mode": config 2 in the reference's default Phred-weighted mode (fixed_accuracy 0, arg_parse.h:23);
   * "k31": BASELINE config 3 (50 variants x 3 isolates, k = 31) at its full 10 M reads per GPU — at N = 8 the
@@ -78,6 +78,10 @@ def parse_args(argv=None):
     p.add_argument("--regions", type=int, default=5,
                    help="timed regions of K steps per line (SURVEY §8(d): the median of 5 after warm-up); each region "
                         "times the pipelined steps, the same steps on one stream, and one stream with per-launch events")
+    p.add_argument("--allreduce", choices=["job", "step"], default="job",
+                   help="N > 1 (or --transport rccl): job = the K steps of a timed region are one job whose summed "
+                        "counters are all-reduced once at its end (default; SURVEY 8(d)); step = every step's "
+                        "counters zeroed and all-reduced after its scan (diagnostic)")
     p.add_argument("--no-extra", action="store_true", help="skip the secondary lines")
     p.add_argument("--only", default="", help="comma-separated secondary lines to run (default: all)")
     p.add_argument("--k31-reads", type=int, default=0, help="reads per GPU of the k=31 line (0 = config 3/4)")
@@ -191,6 +195,13 @@ class Ctx:
         # vs pipelined ratio of every line ("overlap") shows whether they did.
         n_extra = max(0, int(getattr(a, "streams", 1)) - 1) + (1 if self.transport in ("rccl", "host") else 0)
         _PIPE_STREAMS[self.device] = [torch.cuda.Stream(self.dev_t) for _ in range(n_extra)]
+        # HIP binds a stream to its hardware queue at the stream's first command, not at its creation: without one
+        # before RCCL's init the pipeline's streams came to share a queue with each other (one-member RCCL test:
+        # pipelined 0.98x the one-stream rate). So every stream, the current one included, runs a command now.
+        for s in [torch.cuda.current_stream(self.dev_t)] + _PIPE_STREAMS[self.device]:
+            with torch.cuda.stream(s):
+                torch.zeros(1, device=self.dev_t).add_(1)
+        torch.cuda.synchronize(self.dev_t)
         if self.transport == "rccl":
             if self.world == 1:  # forced at one rank (tests): a one-member group over the loopback rendezvous
                 os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
@@ -360,10 +371,10 @@ def run_workload(ctx: Ctx, cfg_no: int, k: int, n_reads: int, mode: str, steps: 
     # --streams S: step i runs on stream i % S, each stream with its own batch of reads (stream 0: `reads`; stream
     # s > 0: the reads after every rank's batch 0, so no batch's reads are another's) and its own counters, so the
     # scans of consecutive batches overlap: the next scan's workgroups take the CUs the previous one's drain leaves
-    # (a pipeline of S batches in flight). With more ranks each step's counters are all-reduced on one
-    # communication stream, in step order on every rank, after that step's scan (events). Every stream's counters
-    # of its last timed step are checked against its batch scanned again on one stream; the per-launch kernel time
-    # (events) is taken with S = 1.
+    # (a pipeline of S batches in flight). The scans add into their stream's counters; with more ranks the job's
+    # summed counters are all-reduced once at its end (finish_job; --allreduce step: after every step, on one
+    # communication stream in step order). Every stream's counters of the last timed job are checked against its
+    # batch scanned alone on one stream; the per-launch kernel time (events) is taken with S = 1.
     n_str = max(1, int(getattr(a, "streams", 1)))
     xkey = (qual_profile, err, n_reads, n_str)
     if prepared.get("x_key") != xkey:
@@ -396,35 +407,66 @@ def run_workload(ctx: Ctx, cfg_no: int, k: int, n_reads: int, mode: str, steps: 
     comm_stream = ps[n_str - 1] if ctx.comm is not None and n_str > 1 else None
     ev_scan = [torch.cuda.Event() for _ in bufs]
     ev_comm = [torch.cuda.Event() for _ in bufs]
-    rot = {"i": 0, "n": 1, "kmers": 0, "ran": set()}
+    rot = {"i": 0, "n": 1, "kmers": 0, "ran": [0] * len(bufs)}
+    # --allreduce job (default): the K steps of a timed region are ONE job over K batches — every scan adds into its
+    # stream's counters (the kernel's atomics accumulate), and the job ends with one all-reduce of the summed G + 2
+    # counters (+ G weights) inside the timed region, as `speq scan` ends a shard ("to completion of the
+    # final ncclAllReduce"; replaces the future.get() sums of /root/reference/src/fm_scanner.cpp:224-233).
+    # --allreduce step: every step zeroes its counters and all-reduces them after its scan (diagnostic).
+    per_step = getattr(a, "allreduce", "job") == "step"
+    job_cnt = torch.zeros(G + 2, dtype=torch.int64, device=ctx.dev_t)
+    job_w = torch.zeros(G, dtype=torch.float64, device=ctx.dev_t)
 
-    def allreduce(b, st):
-        ctx.comm.allreduce_u64(b["cnt"].data_ptr(), G + 2, st)  # RCCL all-reduce of the G+2 counters over xGMI
+    def allreduce(cnt, w, st):
+        ctx.comm.allreduce_u64(cnt.data_ptr(), G + 2, st)  # RCCL all-reduce of the G+2 counters over xGMI
         if local:
-            ctx.comm.allreduce_f64(b["w"].data_ptr(), G, st)
+            ctx.comm.allreduce_f64(w.data_ptr(), G, st)
+
+    def zero(b):
+        b["cnt"].zero_()
+        if local:
+            b["w"].zero_()
 
     def step():
         i = rot["i"] % rot["n"]
         rot["i"] += 1
         b, s = bufs[i], bufs[i]["stream"]
         rot["kmers"] += b["kmers"]
-        rot["ran"].add(i)
+        rot["ran"][i] += 1
         with torch.cuda.stream(s):
-            b["cnt"].zero_()
-            if local:
-                b["w"].zero_()
+            if per_step:
+                zero(b)
             dev.scan_device(b["seq"].data_ptr(), b["qual"].data_ptr(), b["off"].data_ptr(), b["n"], k,
                             b["cnt"].data_ptr(), b["w"].data_ptr(), paired=paired, local=local,
                             stream=s.cuda_stream)
-        if ctx.comm is not None:
+        if ctx.comm is not None and per_step:
             if rot["n"] == 1:  # one stream: the all-reduce follows the scan on it
-                allreduce(b, s.cuda_stream)
+                allreduce(b["cnt"], b["w"], s.cuda_stream)
             else:
                 ev_scan[i].record(s)
                 comm_stream.wait_event(ev_scan[i])
-                allreduce(b, comm_stream.cuda_stream)
+                allreduce(b["cnt"], b["w"], comm_stream.cuda_stream)
                 ev_comm[i].record(comm_stream)
                 s.wait_event(ev_comm[i])  # the stream's next step zeroes these counters after their all-reduce
+
+    def finish_job():
+        """(job mode) the end of the timed job: the streams' counters summed and all-reduced once."""
+        if ctx.comm is None or per_step:
+            return
+        cs = comm_stream if (comm_stream is not None and rot["n"] > 1) else bufs[0]["stream"]
+        for i in range(rot["n"]):
+            if cs is not bufs[i]["stream"]:
+                ev_scan[i].record(bufs[i]["stream"])
+                cs.wait_event(ev_scan[i])
+        with torch.cuda.stream(cs):
+            job_cnt.copy_(bufs[0]["cnt"])
+            for b in bufs[1:rot["n"]]:
+                job_cnt.add_(b["cnt"])
+            if local:
+                job_w.copy_(bufs[0]["w"])
+                for b in bufs[1:rot["n"]]:
+                    job_w.add_(b["w"])
+        allreduce(job_cnt, job_w, cs.cuda_stream)
 
     def timed_run(n_steps, n_warm, events=True, pipelined=False):
         rot["i"], rot["n"] = 0, n_str if pipelined else 1
@@ -432,7 +474,9 @@ def run_workload(ctx: Ctx, cfg_no: int, k: int, n_reads: int, mode: str, steps: 
             step()
         torch.cuda.synchronize()
         rot["kmers"] = 0  # k-mers of the timed steps only
-        rot["ran"] = set()
+        rot["ran"] = [0] * len(bufs)
+        for b in bufs:
+            zero(b)
         ctx.barrier()
         torch.cuda.synchronize()
         dev.timing(events)
@@ -441,6 +485,8 @@ def run_workload(ctx: Ctx, cfg_no: int, k: int, n_reads: int, mode: str, steps: 
         t0 = time.perf_counter()
         for _ in range(n_steps):
             step()
+        t_enq = time.perf_counter() - t0
+        finish_job()
         torch.cuda.synchronize()
         ctx.barrier()
         elapsed = time.perf_counter() - t0
@@ -449,31 +495,47 @@ def run_workload(ctx: Ctx, cfg_no: int, k: int, n_reads: int, mode: str, steps: 
         expect = sum(bufs[i % rot["n"]]["kmers"] for i in range(n_steps))
         if rot["kmers"] != expect:  # the timed k-mers are the steps' batches' windows at this k
             raise RuntimeError(f"timed k-mers {rot['kmers']} != {expect} of the {n_steps} steps' batches at k={k}")
+        rot["enqueue_s"] = t_enq
         return ctx.allreduce_max(elapsed), kernel_ms, launches
 
-    def counters(b):
-        return b["cnt"].cpu().numpy().copy(), (b["w"].cpu().numpy().copy() if local else None)
+    def counters(cnt, w):
+        return cnt.cpu().numpy().copy(), (w.cpu().numpy().copy() if local else None)
 
-    def same(x, y) -> bool:
-        return np.array_equal(x[0], y[0]) and (not local or np.allclose(x[1], y[1], rtol=1e-12, atol=0))
+    def times(x, n):  # n x a batch's counters (the job's sum of n scans of that batch)
+        return x[0] * n, (x[1] * n if local else None)
+
+    def same(x, y, rtol=1e-12) -> bool:
+        return np.array_equal(x[0], y[0]) and (not local or np.allclose(x[1], y[1], rtol=rtol, atol=0))
+
+    def scan_once(b, reduce):  # batch b scanned alone on the current stream (+ all-reduced over the ranks)
+        cnt = torch.zeros(G + 2, dtype=torch.int64, device=ctx.dev_t)
+        w = torch.zeros(G, dtype=torch.float64, device=ctx.dev_t)
+        dev.scan_device(b["seq"].data_ptr(), b["qual"].data_ptr(), b["off"].data_ptr(), b["n"], k, cnt.data_ptr(),
+                        w.data_ptr(), paired=paired, local=local, stream=stream)
+        if reduce and ctx.comm is not None:
+            allreduce(cnt, w, stream)
+        torch.cuda.synchronize()
+        return counters(cnt, w)
 
     # the median of `regions` timed regions of K steps after one warm-up. Each region times
     #   (p) the K steps as a job runs them (step i on stream i % S): `value`;
     #   (1) the same K steps on one stream, each waiting for the one before: `one_stream` and the overlap ratio
-    #       (1) / (p) — below 1.1 the streams ran one after the other (e.g. shared hardware queues at N = 8);
+    #       (p) / (1) in k-mers/s — near 1.0 the streams ran one after the other (e.g. shared hardware queues);
     #   (e) (1) again with HIP events around every launch: the per-launch kernel time of the roofline (the events
     #       cost 6-10 µs per step, scripts/step_overhead.py, so (p) and (1) run without them).
     n_reg = max(1, int(getattr(a, "regions", 5)))
-    el_p, el_1, el_e, kms = [], [], [], []
-    ran_p = set()
-    snap_p = None
+    el_p, el_1, el_e, kms, enq = [], [], [], [], []
+    snap_p = snap_job = None
+    ran_p = [0] * len(bufs)
     for r_i in range(n_reg):
         e, _, _ = timed_run(steps, warmup if r_i == 0 else 0, events=False, pipelined=True)
         el_p.append(e)
+        enq.append(rot["enqueue_s"])
         timed_kmers = rot["kmers"]
-        ran_p = set(rot["ran"])
-        if r_i == n_reg - 1:
-            snap_p = [counters(b) for b in bufs]  # every stream's last pipelined scan (checked below)
+        ran_p = list(rot["ran"])
+        if r_i == n_reg - 1:  # every stream's counters of the last pipelined job (checked below)
+            snap_p = [counters(b["cnt"], b["w"]) for b in bufs]
+            snap_job = counters(job_cnt, job_w) if (ctx.comm is not None and not per_step) else None
         if n_str > 1:
             el_1.append(timed_run(steps, 0, events=False)[0])
             kmers_1 = rot["kmers"]
@@ -483,28 +545,38 @@ def run_workload(ctx: Ctx, cfg_no: int, k: int, n_reads: int, mode: str, steps: 
     elapsed = float(np.median(el_p))
     elapsed_ev = float(np.median(el_e))
     kernel_med = float(np.median(kms))
-    # the last pipelined scan of every stream that ran one against its batch scanned again on one stream; stream 0's
-    # against the events run's last scan (the same batch on one stream), whose counters the CPU baseline checks
-    one = counters(bufs[0])
-    if 0 in ran_p and not same(snap_p[0], one):
-        raise RuntimeError("the pipelined scan of stream 0 disagrees with the same batch scanned on one stream")
-    for si, b in enumerate(bufs[1:], start=1):
-        if si not in ran_p:
+    # Checks of the last pipelined job: every stream's counters equal (scans of that stream) x its batch scanned
+    # alone on one stream (per step mode: one scan, all-reduced); the job's all-reduced total equals the sum over
+    # the streams of the same, all-reduced. `counts`: batch 0 scanned alone and all-reduced (the line's check, and
+    # what the CPU baseline is compared with).
+    alone_local = [scan_once(b, reduce=False) if ran_p[i] else None for i, b in enumerate(bufs)]
+    counts_t = scan_once(bufs[0], reduce=True)
+    for i, b in enumerate(bufs):
+        if not ran_p[i]:
             continue  # (fewer timed steps than streams: this stream's batch never ran)
-        rb = dict(b, cnt=torch.zeros(G + 2, dtype=torch.int64, device=ctx.dev_t),
-                  w=torch.zeros(G, dtype=torch.float64, device=ctx.dev_t))
-        dev.scan_device(rb["seq"].data_ptr(), rb["qual"].data_ptr(), rb["off"].data_ptr(), rb["n"], k,
-                        rb["cnt"].data_ptr(), rb["w"].data_ptr(), paired=paired, local=local, stream=stream)
-        if ctx.comm is not None:
-            allreduce(rb, stream)
-        torch.cuda.synchronize()
-        if not same(snap_p[si], counters(rb)):
-            raise RuntimeError("a pipelined scan disagrees with the same batch scanned on one stream")
+        want = (scan_once(b, reduce=True) if ctx.comm is not None else alone_local[i]) if per_step else \
+            times(alone_local[i], ran_p[i])
+        if not same(snap_p[i], want, rtol=1e-11):
+            raise RuntimeError(f"the pipelined scans of stream {i} disagree with its batch scanned alone")
+    if snap_job is not None:
+        tot = None
+        for i, b in enumerate(bufs):
+            if ran_p[i]:
+                x = times(scan_once(b, reduce=True), ran_p[i])
+                tot = x if tot is None else (tot[0] + x[0], (tot[1] + x[1]) if local else None)
+        if not same(snap_job, tot, rtol=1e-11):
+            raise RuntimeError("the job's all-reduced counters disagree with its batches scanned alone")
+    # batch 0's counters after a one-stream timed run: `steps` scans summed (job), or one scan (+ all-reduced) per step
+    job1 = ((counts_t[0] if ctx.comm is not None else alone_local[0][0]) if per_step else alone_local[0][0] * steps)
+    d_counts.copy_(torch.from_numpy(counts_t[0]).to(ctx.dev_t))
+    if local:
+        d_w.copy_(torch.from_numpy(counts_t[1]).to(ctx.dev_t))
     timing = {
-        "regions": n_reg, "steps_per_region": steps,
+        "regions": n_reg, "steps_per_region": steps, "allreduce": "step" if per_step else "job",
         "value_median": timed_kmers * ctx.world / elapsed,
         "value_min": timed_kmers * ctx.world / max(el_p), "value_max": timed_kmers * ctx.world / min(el_p),
         "ms_per_step": [round(x / steps * 1e3, 5) for x in el_p],
+        "host_enqueue_ms_per_step": [round(x / steps * 1e3, 5) for x in enq],
         "avg_kernel_ms": [round(x, 5) for x in kms],
         "avg_kernel_ms_median": kernel_med, "avg_kernel_ms_min": min(kms), "avg_kernel_ms_max": max(kms),
     }
@@ -526,10 +598,10 @@ def run_workload(ctx: Ctx, cfg_no: int, k: int, n_reads: int, mode: str, steps: 
         # the previous hot path (k-mer-table kernel for k <= 31, else LF steps) on the same reads
         dev.tune(ax_scan=0)
         pv_el, pv_ms, pv_n = timed_run(steps, 1)
-        pv_counts = d_counts.cpu().numpy()
+        pv_counts = d_counts.cpu().numpy()  # (the sum of the `steps` scans of batch 0 on this rank)
         kind = dev.tuning("last_kernel")
         dev.tune(ax_scan=1)
-        if not np.array_equal(pv_counts, counts):
+        if not np.array_equal(pv_counts, job1):
             raise RuntimeError("k-mer-table scan disagrees with the anchor-and-extend scan")
         prev = {"value": kmers_per_step * ctx.world * steps / pv_el, "unit": "k-mers/s",
                 "avg_kernel_ms": pv_ms / max(1, pv_n), "path": KERNEL_NAME.get(kind, str(kind))}
@@ -538,7 +610,7 @@ def run_workload(ctx: Ctx, cfg_no: int, k: int, n_reads: int, mode: str, steps: 
         lf_el, lf_ms, lf_n = timed_run(steps, 1)
         lf_counts = d_counts.cpu().numpy()
         dev.tune(kmer_table=1, ax_scan=1)
-        if not np.array_equal(lf_counts, counts):
+        if not np.array_equal(lf_counts, job1):
             raise RuntimeError("LF-step scan disagrees with the hot path")
         lf = {"value": kmers_per_step * ctx.world * steps / lf_el, "unit": "k-mers/s",
               "avg_kernel_ms": lf_ms / max(1, lf_n),
@@ -555,7 +627,7 @@ def run_workload(ctx: Ctx, cfg_no: int, k: int, n_reads: int, mode: str, steps: 
             d_w.zero_()
         ax_stats = dev.scan_device_stats(d_seq.data_ptr(), d_qual.data_ptr(), d_off.data_ptr(), reads.n, k,
                                          d_counts.data_ptr(), d_w.data_ptr(), paired=paired, local=local)
-        if not np.array_equal(d_counts.cpu().numpy(), counts):
+        if not np.array_equal(d_counts.cpu().numpy(), alone_local[0][0]):  # (this rank's, not all-reduced)
             raise RuntimeError("instrumented anchor-and-extend scan disagrees with the timed scan")
         req = ax_request_bytes(ax_stats, k, reads.n, local)
     compulsory = 2.0 * read_bytes + 8.0 * (reads.n + 1)  # bases + qualities + read offsets
@@ -763,7 +835,7 @@ def main(argv=None):
             "workload": head["workload"],
             "k": k, "reads_per_gpu": n_reads, "paired": head["paired"], "mode": a.mode,
             "parallelism": f"dp{ctx.world} (reads sharded, index replicated)",
-            "collective": {"rccl": "speq_allreduce_u64/_f64 (C ABI; RCCL ncclAllReduce of the G + 2 counters per step)",
+            "collective": {"rccl": "speq_allreduce_u64/_f64 (C ABI; RCCL ncclAllReduce of the G + 2 counters, once per timed job of K steps)",
                            "host": "speq_allreduce_u64/_f64 (C ABI; host-socket transport, ranks share GPUs)",
                            "none": "none (one GPU)"}[ctx.transport],
             "gpus_visible": ctx.n_dev, "ranks_per_gpu": -(-ctx.world // max(1, min(ctx.world, ctx.n_dev))),
