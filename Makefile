@@ -79,7 +79,7 @@ axvariant: $(filter-out $(OBJDIR)/ax_scan.o,$(LIB_OBJS))
 
 # Every compile-time knob of k_scan_ax forced off its default, three builds (tests/test_gpu_ax_knobs.py runs the
 # parity suite tests/ax_knob_suite.py against each): make axknobs -> build/axknobs/<name>/libspeq_scan.so
-AXKNOB_kv1 := -DSPEQ_AX_SU=1 -DSPEQ_AX_REFILL=8 -DSPEQ_AX_BLOCKED=32 -DSPEQ_AX_P2_MARGIN=64 -DSPEQ_AX_PRIO_MIN=0 -DSPEQ_AX_WL=64 -DSPEQ_AX_MTILES=0
+AXKNOB_kv1 := -DSPEQ_AX_SU=1 -DSPEQ_AX_SU_LOCAL=2 -DSPEQ_AX_REFILL=8 -DSPEQ_AX_BLOCKED=32 -DSPEQ_AX_P2_MARGIN=64 -DSPEQ_AX_PRIO_MIN=0 -DSPEQ_AX_WL=64 -DSPEQ_AX_MTILES=0
 AXKNOB_kv2 := -DSPEQ_AX_WPB=2 -DSPEQ_AX_MIN_WAVES=4 -DSPEQ_AX_MIN_WAVES_LOCAL=3 -DSPEQ_AX_DEF_GLOBAL=192 -DSPEQ_AX_DEF_LOCAL=128
 AXKNOB_kv3 := -DSPEQ_AX_SPEC_HW=1 -DSPEQ_AX_PRIO=0 -DSPEQ_AX_MPROOF=0
 AXKNOBS    := kv1 kv2 kv3

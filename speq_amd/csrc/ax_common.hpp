@@ -35,8 +35,8 @@ namespace {
 using namespace speq_dev;
 
 // Compile-time knobs (A/B only; every one is run through the parity tests forced to a non-default value by
-// tests/test_gpu_ax_knobs.py over `make axknobs` builds), fifteen: SPEQ_AX_DEF_LOCAL, SPEQ_AX_DEF_GLOBAL, SPEQ_AX_WL,
-// SPEQ_AX_WPB, SPEQ_AX_SU, SPEQ_AX_MIN_WAVES, SPEQ_AX_MIN_WAVES_LOCAL, SPEQ_AX_REFILL, SPEQ_AX_BLOCKED,
+// tests/test_gpu_ax_knobs.py over `make axknobs` builds), sixteen: SPEQ_AX_DEF_LOCAL, SPEQ_AX_DEF_GLOBAL, SPEQ_AX_WL,
+// SPEQ_AX_WPB, SPEQ_AX_SU, SPEQ_AX_SU_LOCAL, SPEQ_AX_MIN_WAVES, SPEQ_AX_MIN_WAVES_LOCAL, SPEQ_AX_REFILL, SPEQ_AX_BLOCKED,
 // SPEQ_AX_SPEC_HW, SPEQ_AX_PRIO, SPEQ_AX_PRIO_MIN, SPEQ_AX_P2_MARGIN, SPEQ_AX_MPROOF, SPEQ_AX_MTILES. Measured losers
 // of rounds 3-5 (a cuckoo anchor table, lowest / first-claimant representatives, a dynamic tail, generation-weighted
 // pools, offset prefetch, speculative runs in global mode, a minimizer-keyed filter, workgroup-shared pools) were
@@ -51,13 +51,15 @@ constexpr uint32_t AX_NGR = AX_CMPW + 1;         // granules that cover AX_CMP b
 constexpr uint32_t AX_CHK = 3;                   // 64-window class chunks of one run (<= AX_CMP - k + 1 windows)
 constexpr uint32_t AX_VWW = 4;        // valid-window words per lane (>= AX_CAP - k + 1 windows; 16 B per staged chunk)
 #ifndef SPEQ_AX_DEF_LOCAL  // deferred-window entries per wave in local mode (A/B knob)
-#define SPEQ_AX_DEF_LOCAL 448
+#define SPEQ_AX_DEF_LOCAL 416
 #endif
 #ifndef SPEQ_AX_DEF_GLOBAL  // the same in global mode (A/B knob; a multiple of 4)
-#define SPEQ_AX_DEF_GLOBAL 896
+#define SPEQ_AX_DEF_GLOBAL 864
 #endif
-// deferred-window entries per wave (u16: lane | window << 6): global mode 896 (7.9 KB per wave: 5 blocks of 4 waves
-// per CU); local mode 448, so that its 9.7 KB per wave fit 4 blocks per CU (up to 77 groups)
+// deferred-window entries per wave (u16: lane | window << 6): global mode 864 (7.9 KB per wave: 5 blocks of 4 waves
+// per CU); local mode 416, so that its 9.7 KB per wave fit 4 blocks per CU (up to 77 groups). (896 / 448 until round
+// 6: 32 entries each gave their 64 B to the owner map's third row, SPEQ_AX_SU = 3, so a workgroup's LDS stayed the same
+// — with both, config 3's 50-group workgroups no longer fitted 5 per CU: k = 31 1.44 -> 1.91 ms.)
 template <int MODE>
 constexpr uint32_t ax_def() {
     return MODE == KM_LOCAL ? SPEQ_AX_DEF_LOCAL : SPEQ_AX_DEF_GLOBAL;
@@ -263,15 +265,27 @@ static_assert(8u * (AX_FTAB + QLUT_LEN) <= QTAB_BYTES && AX_FONE - 1u == 33u + 4
 #endif
 constexpr uint32_t AX_WL = SPEQ_AX_WL;
 static_assert(AX_WL % 64u == 0 && AX_WL >= 64u && AX_WL <= 512u, "work list: 1-8 sub-batches of 64 blocks per round");
-#ifndef SPEQ_AX_SU  // staging: stream instructions per load batch (A/B knob; 3 at 5 waves spills 20-36 B per lane)
-#define SPEQ_AX_SU 2
+#ifndef SPEQ_AX_SU  // staging: stream instructions per load batch, global mode (A/B knob). 3 since round 6: the
+#define SPEQ_AX_SU 3   // staging code hoisted out of the refill branch left the registers for it at 5 waves/SIMD
+#endif                 // (round 4's 3 spilled 20-36 B per lane); k 65-96 and paired k 33-64 keep 2 (3 spills there)
+#ifndef SPEQ_AX_SU_LOCAL  // the same, Phred-weighted mode (4 waves/SIMD, 128 VGPRs; A/B knob)
+#define SPEQ_AX_SU_LOCAL 3
 #endif
-constexpr uint32_t AX_OWNB = 64u * SPEQ_AX_SU;  // bytes of the staging owner map (64 x SPEQ_AX_SU)
+template <int MODE, bool PAIRED, int HW>
+constexpr uint32_t ax_su() {
+    return MODE == KM_LOCAL ? SPEQ_AX_SU_LOCAL
+                            : ((HW == 3 || (PAIRED && HW == 2)) && SPEQ_AX_SU > 2 ? 2u : SPEQ_AX_SU);
+}
+template <int MODE>
+constexpr uint32_t ax_ownb() {  // bytes of the staging owner map (64 per stream instruction of a batch)
+    return 64u * (MODE == KM_LOCAL ? SPEQ_AX_SU_LOCAL : SPEQ_AX_SU);
+}
 template <int MODE>
 constexpr uint32_t ax_wave_bytes() {
     static_assert(8u * AX_VWW >= 2u * AX_CHUNKS, "the bad-base bits of a staged piece live in its valid-window words");
     return 4u * AX_CHUNKS * 64u + 8u * AX_VWW * 64u + (MODE == KM_LOCAL ? 2u * AX_CHUNKS * 64u : 0u) +
-           64u + 2u * ax_def<MODE>() + 24u + 8u * 64u + (MODE == KM_LOCAL ? 4u * AX_WL + 4u * 64u : 0u) + AX_OWNB;
+           64u + 2u * ax_def<MODE>() + 24u + 8u * 64u + (MODE == KM_LOCAL ? 4u * AX_WL + 4u * 64u : 0u) +
+           ax_ownb<MODE>();
 }
 
 #ifndef SPEQ_AX_WPB  // waves per workgroup of k_scan_ax (A/B knob)

@@ -332,7 +332,7 @@ __global__ __launch_bounds__(AX_THREADS, (ax_min_waves<MODE, HW, EM, STATS>())) 
     int32_t* ambd = ambf + 64;                                               // [64] another group seen
     uint32_t* wl = reinterpret_cast<uint32_t*>(ambd + 64);                   // [AX_WL] (local)
     uint32_t* wlm = wl + AX_WL;                                              // [64] (local)
-    uint8_t* ownb = reinterpret_cast<uint8_t*>(MODE == KM_LOCAL ? wlm + 64 : wl);  // [AX_OWNB] staging owner map
+    uint8_t* ownb = reinterpret_cast<uint8_t*>(MODE == KM_LOCAL ? wlm + 64 : wl);  // [ax_ownb] staging owner map
 
     if (MODE == KM_LOCAL)
         for (uint32_t i = threadIdx.x; i < AX_FTAB; i += AX_THREADS) {
@@ -621,6 +621,146 @@ __global__ __launch_bounds__(AX_THREADS, (ax_min_waves<MODE, HW, EM, STATS>())) 
     // (PAIRED) the second mate's length, loaded with the first mate's offsets: the second mate then starts at the
     // first's end without another offsets round trip in its refill
     uint32_t L2m = 0;
+
+    // ---- staging of a refill group: the refilling lanes' pieces laid end to end as one stream of 16-base chunks
+    // (lane o's at [stg_pre_o, stg_pre_o + stg_nch_o)); every lane of the wave loads and decodes whole chunks, SU x 64
+    // chunks per batch, into the owners' slots, one round trip per batch while the wave waits. (Round 6 tried the
+    // batches beside the following phase-1 iterations' loads instead: 37 % slower)
+    constexpr uint32_t SU = ax_su<MODE, PAIRED, HW>();  // stream instructions of one batch
+    static_assert(64u * SU <= ax_ownb<MODE>(), "owner map of one batch");
+    static_assert(AX_CHUNKS < 16, "chunk counts in four bits");
+    uint32_t stg_tot = 0;      // (wave-uniform) the group's chunks
+    uint32_t stg_ocarry = 0;   // (wave-uniform) owner mark of the last chunk of the previous 64
+    uint32_t stg_qcarry = 0;   // (wave-uniform, local) last quality dword of the previous instruction's lane 63
+    uint32_t stg_pre = 0, stg_nch = 0;  // this lane's piece: first chunk in the group's stream, chunks (0: none)
+    // owners and loads of the batch from chunk c0: every refilling lane marks the first chunk of its range in a byte
+    // map (lane + 1); a prefix max over the lanes (DPP; owners grow with the chunk index) spreads the mark over the
+    // range, and the last owner carries into the next 64 chunks. dst[u] = the owner's slot word (ci * 64 + owner).
+    auto stage_issue = [&](uint32_t c0, uint4(&sv)[SU], uint4(&qv)[SU], uint32_t(&dst)[SU]) {
+#pragma unroll
+        for (uint32_t u = 0; u < SU; ++u) ownb[64u * u + lane] = 0;
+        if (stg_nch != 0u && stg_pre >= c0 && stg_pre < c0 + 64u * SU) ownb[stg_pre - c0] = (uint8_t)(lane + 1u);
+        wave_sync();
+        uint32_t mk[SU];
+#pragma unroll
+        for (uint32_t u = 0; u < SU; ++u) mk[u] = ownb[64u * u + lane];
+#pragma unroll
+        for (uint32_t u = 0; u < SU; ++u) {
+            const uint32_t c = min(c0 + 64u * u + lane, stg_tot - 1u);
+            uint32_t m = mk[u];
+            m = max(m, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)m, 0x111, 0xF, 0xF, false));  // row_shr:1
+            m = max(m, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)m, 0x112, 0xF, 0xF, false));  // row_shr:2
+            m = max(m, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)m, 0x114, 0xF, 0xF, false));  // row_shr:4
+            m = max(m, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)m, 0x118, 0xF, 0xF, false));  // row_shr:8
+            m = max(m, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)m, 0x142, 0xA, 0xF, false));  // row_bcast:15
+            m = max(m, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)m, 0x143, 0xC, 0xF, false));  // row_bcast:31
+            m = max(m, stg_ocarry);
+            stg_ocarry = (uint32_t)__builtin_amdgcn_readlane((int)m, 63);
+            const uint32_t o = m - 1u;
+            const uint32_t ci = c - (uint32_t)__shfl((int)stg_pre, (int)o);
+            dst[u] = ci * 64u + o;
+            // the owner's piece starts at ta (its first base); its slot position 0 is ta's 16-B-aligned base
+            const uint64_t go = ((uint64_t)__shfl((long long)ta, (int)o) & ~15ull) + 16ull * ci;
+            sv[u] = *reinterpret_cast<const uint4*>(src.seq + go);
+            qv[u] = *reinterpret_cast<const uint4*>(src.qual + go);
+        }
+    };
+    // decodes the batch from chunk c0 into the owners' slots: 2-bit codes, bad-base bits, quality changes
+    auto stage_decode = [&](uint32_t c0, const uint4(&sv)[SU], const uint4(&qv)[SU], const uint32_t(&dst)[SU]) {
+#pragma unroll
+        for (uint32_t u = 0; u < SU; ++u) {
+            const uint32_t c = c0 + 64u * u + lane;
+            const uint32_t sd[4] = {sv[u].x, sv[u].y, sv[u].z, sv[u].w};
+            const uint32_t qd[4] = {qv[u].x, qv[u].y, qv[u].z, qv[u].w};
+            uint32_t cw = 0, bad = 0, chb = 0;
+            // local mode: the quality byte before the chunk (a chunk's change bit 0 compares with it; the piece's
+            // first base never reads its change bit)
+            uint32_t qprev = 0;
+            if (MODE == KM_LOCAL) {  // the previous chunk's last quality (the previous lane's, or the carry)
+                const uint32_t up = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)qv[u].w, 0x138, 0xF, 0xF, false);
+                qprev = lane == 0 ? stg_qcarry : up;
+                stg_qcarry = __builtin_amdgcn_readlane(qv[u].w, 63);
+            }
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const uint32_t x = sd[i] | 0x20202020u;  // lower case
+                const uint32_t c4 = ((x >> 1) ^ (x >> 2)) & 0x03030303u;  // a c g t/u -> 0 1 2 3
+                cw |= ((c4 | (c4 >> 6) | (c4 >> 12) | (c4 >> 18)) & 0xFFu) << (8 * i);
+                const uint32_t canon = __builtin_amdgcn_perm(0u, 0x74676361u, c4);  // the letter of that code
+                const uint32_t okb = zero_bytes(x ^ canon) | zero_bytes(x ^ 0x75757575u);  // ACGT or U
+                const uint32_t y = qd[i];
+                const uint32_t badq = (((0x80808080u | qt4) - (y & 0x7F7F7F7Fu)) & ~y & 0x80808080u) | allbad;
+                bad |= flags4((~okb & 0x80808080u) | badq) << (4 * i);
+                if (MODE == KM_LOCAL) {
+                    const uint32_t prev = (y << 8) | (qprev >> 24);
+                    chb |= flags4(~zero_bytes(y ^ prev) & 0x80808080u) << (4 * i);
+                    qprev = y;
+                }
+            }
+            if (c < stg_tot) {
+                const uint32_t ci = dst[u] >> 6, o = dst[u] & 63u;
+                codes[dst[u]] = cw;
+                bad16[((ci >> 2) * 64u + o) * 4u + (ci & 3u)] = (uint16_t)bad;
+                if (MODE == KM_LOCAL) chg[dst[u]] = (uint16_t)chb;
+            }
+        }
+    };
+    // a staged lane's piece becomes workable: its valid-window bits (from the bad-base bits the decode left in its
+    // valid-window words), T, and phase-1 state (the slots' code words were fenced after the decode)
+    auto finish_piece = [&](uint32_t nch) {
+        // this lane's good-base bits, 16 per chunk from a16 (chunks past its piece are bad), as 8 dwords
+        uint32_t ok[8];
+        {
+            const uint32_t* vw32 = reinterpret_cast<const uint32_t*>(vw);
+            const uint32_t nb = 16u * nch;
+#pragma unroll
+            for (uint32_t d = 0; d < 8u; ++d) {
+                const uint32_t b0 = 32u * d;  // dword d: chunks 2d, 2d + 1 (word d / 2 of the lane's column)
+                uint32_t v = vw32[((d >> 1) * 64u + lane) * 2u + (d & 1u)];
+                v |= nb <= b0 ? ~0u : (nb < b0 + 32u ? ~0u << (nb - b0) : 0u);
+                ok[d] = ~v;
+            }
+        }
+        // valid windows: AND of k consecutive good bits (doubling: shifts of at most 64 bits, one funnel shift per
+        // dword), then aligned to the piece's first base
+        for (uint32_t len = 1u; len < k;) {
+            const uint32_t sft = min(len, k - len);  // 1 .. 64
+            const uint32_t dw = sft >> 5, bs = sft & 31u;
+            if (dw == 0u) {
+#pragma unroll
+                for (uint32_t d = 0; d < 8u; ++d) ok[d] &= alignbit(d + 1u < 8u ? ok[d + 1] : 0u, ok[d], bs);
+            } else if (dw == 1u) {
+#pragma unroll
+                for (uint32_t d = 0; d < 8u; ++d)
+                    ok[d] &= alignbit(d + 2u < 8u ? ok[d + 2] : 0u, d + 1u < 8u ? ok[d + 1] : 0u, bs);
+            } else {  // sft == 64
+#pragma unroll
+                for (uint32_t d = 0; d < 8u; ++d) ok[d] &= d + 2u < 8u ? ok[d + 2] : 0u;
+            }
+            len += sft;
+        }
+        // valid-window bits of the piece (window j at bit j): the good-window dwords from slot position off0 (< 16,
+        // so dword d + {0, 1}), none past wend (no fence: every lane writes and then reads only its own column)
+        {
+            uint32_t* vw32 = reinterpret_cast<uint32_t*>(vw);
+            uint32_t tc = 0;  // T (fm_scanner.cpp:164): the piece's passing windows
+#pragma unroll
+            for (uint32_t d = 0; d < 2u * AX_VWW; ++d) {
+                uint32_t v = alignbit(d + 1u < 8u ? ok[d + 1] : 0u, ok[d], off0);
+                const uint32_t bit0 = 32u * d;
+                v = wend <= bit0 ? 0u : (wend < bit0 + 32u ? v & ((1u << (wend - bit0)) - 1u) : v);
+                tc += (uint32_t)__popc(v);
+                vw32[((d >> 1) * 64u + lane) * 2u + (d & 1u)] = v;
+            }
+            if (tc) atomicAdd(&wsum[0], (unsigned long long)tc);
+        }
+        j = 0;
+        if (SPEC) sp = 0;
+        st = wend > 0 ? 0u : 2u;
+        verify = false;
+        resume = false;
+        last_mm = -1;
+    };
     for (;;) {
         // ================= housekeeping (wave-uniform decisions) =================
         const unsigned long long idle = __ballot(st == 2u);
@@ -840,10 +980,7 @@ __global__ __launch_bounds__(AX_THREADS, (ax_min_waves<MODE, HW, EM, STATS>())) 
                     s_seg += 1u;
                 }
             }
-            // ---- coalesced staging: the refilling lanes' chunks laid end to end (lane o's at [pre_o, pre_o + nch_o));
-            // every lane of the wave decodes whole chunks, SU x 64 chunks per batch (software-pipelining the batches,
-            // the next one's loads in flight while one is decoded, spilled 128 B per lane and was slower)
-            static_assert(AX_CHUNKS < 16, "chunk counts in four bits");
+            // ---- the group's chunk stream: lane o's chunks at [pre_o, pre_o + nch_o)
             uint32_t pre = 0, nch_tot = 0;
 #pragma unroll
             for (uint32_t bb = 0; bb < 4; ++bb) {
@@ -851,81 +988,11 @@ __global__ __launch_bounds__(AX_THREADS, (ax_min_waves<MODE, HW, EM, STATS>())) 
                 pre += lanes_below(m) << bb;
                 nch_tot += (uint32_t)__popcll(m) << bb;
             }
-            uint32_t qcarry = 0;  // local: last quality dword of the previous instruction's lane 63
-            uint32_t ocarry = 0;  // owner mark of the last chunk of the previous 64
-            constexpr uint32_t SU = SPEQ_AX_SU;  // stream instructions of one batch
-            static_assert(64u * SU <= AX_OWNB, "owner map of one batch");
-            // owners and loads of the batch from chunk c0: every refilling lane marks the first chunk of its range in
-            // a byte map (lane + 1); a prefix max over the lanes (DPP; owners grow with the chunk index) spreads the
-            // mark over the range, and the last owner carries into the next 64 chunks
-            auto issue = [&](uint32_t c0, uint4(&sv)[SU], uint4(&qv)[SU], uint32_t(&own)[SU], uint32_t(&ci)[SU]) {
-#pragma unroll
-                for (uint32_t u = 0; u < SU; ++u) ownb[64u * u + lane] = 0;
-                if (nch != 0u && pre >= c0 && pre < c0 + 64u * SU) ownb[pre - c0] = (uint8_t)(lane + 1u);
-                wave_sync();
-                uint32_t mk[SU];
-#pragma unroll
-                for (uint32_t u = 0; u < SU; ++u) mk[u] = ownb[64u * u + lane];
-#pragma unroll
-                for (uint32_t u = 0; u < SU; ++u) {
-                    const uint32_t c = min(c0 + 64u * u + lane, nch_tot - 1u);
-                    uint32_t m = mk[u];
-                    m = max(m, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)m, 0x111, 0xF, 0xF, false));  // row_shr:1
-                    m = max(m, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)m, 0x112, 0xF, 0xF, false));  // row_shr:2
-                    m = max(m, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)m, 0x114, 0xF, 0xF, false));  // row_shr:4
-                    m = max(m, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)m, 0x118, 0xF, 0xF, false));  // row_shr:8
-                    m = max(m, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)m, 0x142, 0xA, 0xF, false));  // row_bcast:15
-                    m = max(m, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)m, 0x143, 0xC, 0xF, false));  // row_bcast:31
-                    m = max(m, ocarry);
-                    ocarry = (uint32_t)__builtin_amdgcn_readlane((int)m, 63);
-                    const uint32_t o = m - 1u;
-                    own[u] = o;
-                    ci[u] = c - (uint32_t)__shfl((int)pre, (int)o);
-                    const uint64_t go = (uint64_t)__shfl((long long)a16, (int)o) + 16ull * ci[u];
-                    sv[u] = *reinterpret_cast<const uint4*>(src.seq + go);
-                    qv[u] = *reinterpret_cast<const uint4*>(src.qual + go);
-                }
-            };
-            // decodes the batch from chunk c0 into the owners' slots: 2-bit codes, bad-base bits, quality changes
-            auto decode = [&](uint32_t c0, const uint4(&sv)[SU], const uint4(&qv)[SU], const uint32_t(&own)[SU],
-                              const uint32_t(&ci)[SU]) {
-#pragma unroll
-                for (uint32_t u = 0; u < SU; ++u) {
-                    const uint32_t c = c0 + 64u * u + lane;
-                    const uint32_t sd[4] = {sv[u].x, sv[u].y, sv[u].z, sv[u].w};
-                    const uint32_t qd[4] = {qv[u].x, qv[u].y, qv[u].z, qv[u].w};
-                    uint32_t cw = 0, bad = 0, chb = 0;
-                    // local mode: the quality byte before the chunk (a chunk's change bit 0 compares with it; the
-                    // piece's first base never reads its change bit)
-                    uint32_t qprev = 0;
-                    if (MODE == KM_LOCAL) {  // the previous chunk's last quality (the previous lane's, or the carry)
-                        const uint32_t up = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)qv[u].w, 0x138, 0xF, 0xF, false);
-                        qprev = lane == 0 ? qcarry : up;
-                        qcarry = __builtin_amdgcn_readlane(qv[u].w, 63);
-                    }
-#pragma unroll
-                    for (int i = 0; i < 4; ++i) {
-                        const uint32_t x = sd[i] | 0x20202020u;  // lower case
-                        const uint32_t c4 = ((x >> 1) ^ (x >> 2)) & 0x03030303u;  // a c g t/u -> 0 1 2 3
-                        cw |= ((c4 | (c4 >> 6) | (c4 >> 12) | (c4 >> 18)) & 0xFFu) << (8 * i);
-                        const uint32_t canon = __builtin_amdgcn_perm(0u, 0x74676361u, c4);  // the letter of that code
-                        const uint32_t okb = zero_bytes(x ^ canon) | zero_bytes(x ^ 0x75757575u);  // ACGT or U
-                        const uint32_t y = qd[i];
-                        const uint32_t badq = (((0x80808080u | qt4) - (y & 0x7F7F7F7Fu)) & ~y & 0x80808080u) | allbad;
-                        bad |= flags4((~okb & 0x80808080u) | badq) << (4 * i);
-                        if (MODE == KM_LOCAL) {
-                            const uint32_t prev = (y << 8) | (qprev >> 24);
-                            chb |= flags4(~zero_bytes(y ^ prev) & 0x80808080u) << (4 * i);
-                            qprev = y;
-                        }
-                    }
-                    if (c < nch_tot) {
-                        codes[ci[u] * 64u + own[u]] = cw;
-                        bad16[((ci[u] >> 2) * 64u + own[u]) * 4u + (ci[u] & 3u)] = (uint16_t)bad;
-                        if (MODE == KM_LOCAL) chg[ci[u] * 64u + own[u]] = (uint16_t)chb;
-                    }
-                }
-            };
+            stg_pre = pre;
+            stg_nch = stg ? nch : 0u;
+            stg_tot = nch_tot;
+            stg_ocarry = 0;
+            stg_qcarry = 0;
             uint64_t c_b = 0;
             if (STATS) {
                 c_b = clock64();
@@ -933,67 +1000,13 @@ __global__ __launch_bounds__(AX_THREADS, (ax_min_waves<MODE, HW, EM, STATS>())) 
             }
             for (uint32_t c0 = 0; c0 < nch_tot; c0 += 64u * SU) {
                 uint4 sv[SU], qv[SU];
-                uint32_t own[SU], ci[SU];
-                issue(c0, sv, qv, own, ci);
-                decode(c0, sv, qv, own, ci);
+                uint32_t dst[SU];
+                stage_issue(c0, sv, qv, dst);
+                stage_decode(c0, sv, qv, dst);
             }
             wave_sync();
             if (STATS) c_rstg += clock64() - c_b;
-            if (stg) {
-                // this lane's good-base bits, 16 per chunk from a16 (chunks past its piece are bad), as 8 dwords
-                uint32_t ok[8];
-                {
-                    const uint32_t* vw32 = reinterpret_cast<const uint32_t*>(vw);
-                    const uint32_t nb = 16u * nch;
-#pragma unroll
-                    for (uint32_t d = 0; d < 8u; ++d) {
-                        const uint32_t b0 = 32u * d;  // dword d: chunks 2d, 2d + 1 (word d / 2 of the lane's column)
-                        uint32_t v = vw32[((d >> 1) * 64u + lane) * 2u + (d & 1u)];
-                        v |= nb <= b0 ? ~0u : (nb < b0 + 32u ? ~0u << (nb - b0) : 0u);
-                        ok[d] = ~v;
-                    }
-                }
-                // valid windows: AND of k consecutive good bits (doubling: shifts of at most 64 bits, one funnel
-                // shift per dword), then aligned to the piece's first base
-                for (uint32_t len = 1u; len < k;) {
-                    const uint32_t sft = min(len, k - len);  // 1 .. 64
-                    const uint32_t dw = sft >> 5, bs = sft & 31u;
-                    if (dw == 0u) {
-#pragma unroll
-                        for (uint32_t d = 0; d < 8u; ++d) ok[d] &= alignbit(d + 1u < 8u ? ok[d + 1] : 0u, ok[d], bs);
-                    } else if (dw == 1u) {
-#pragma unroll
-                        for (uint32_t d = 0; d < 8u; ++d)
-                            ok[d] &= alignbit(d + 2u < 8u ? ok[d + 2] : 0u, d + 1u < 8u ? ok[d + 1] : 0u, bs);
-                    } else {  // sft == 64
-#pragma unroll
-                        for (uint32_t d = 0; d < 8u; ++d) ok[d] &= d + 2u < 8u ? ok[d + 2] : 0u;
-                    }
-                    len += sft;
-                }
-                // valid-window bits of the piece (window j at bit j): the good-window dwords from slot position
-                // off0 (< 16, so dword d + {0, 1}), none past wend
-                // (no fence: every lane writes and then reads only its own column of the valid-window bits)
-                {
-                    uint32_t* vw32 = reinterpret_cast<uint32_t*>(vw);
-                    uint32_t tc = 0;  // T (fm_scanner.cpp:164): the piece's passing windows
-#pragma unroll
-                    for (uint32_t d = 0; d < 2u * AX_VWW; ++d) {
-                        uint32_t v = alignbit(d + 1u < 8u ? ok[d + 1] : 0u, ok[d], off0);
-                        const uint32_t bit0 = 32u * d;
-                        v = wend <= bit0 ? 0u : (wend < bit0 + 32u ? v & ((1u << (wend - bit0)) - 1u) : v);
-                        tc += (uint32_t)__popc(v);
-                        vw32[((d >> 1) * 64u + lane) * 2u + (d & 1u)] = v;
-                    }
-                    if (tc) atomicAdd(&wsum[0], (unsigned long long)tc);
-                }
-                j = 0;
-                if (SPEC) sp = 0;
-                st = wend > 0 ? 0u : 2u;
-                verify = false;
-                resume = false;
-                last_mm = -1;
-            }
+            if (stg) finish_piece(nch);
             // the slots' code words were fenced after the decode (phase 2 reads other lanes' slots); the valid-window
             // bits are read by their own lane only
             if (STATS) c_ref += clock64() - c_s;
@@ -1097,6 +1110,7 @@ __global__ __launch_bounds__(AX_THREADS, (ax_min_waves<MODE, HW, EM, STATS>())) 
             const u32x4 q1 = __builtin_amdgcn_raw_buffer_load_b128(rs_atab, o1, 0, 0);
             const u32x4 q2 = __builtin_amdgcn_raw_buffer_load_b128(rs_atab, o2, 0, 0);
             const u32x4 q3 = __builtin_amdgcn_raw_buffer_load_b128(rs_atab, o3, 0, 0);
+
             if (SPEQ_AX_MPROOF && mk) {
                 // windows proven absent, relative to lo (at most k - 1 <= 127 of them): two 64-bit masks
                 const uint32_t lo = j + (st == 5u ? 0u : 1u);
@@ -1207,6 +1221,7 @@ __global__ __launch_bounds__(AX_THREADS, (ax_min_waves<MODE, HW, EM, STATS>())) 
 #pragma unroll
             for (uint32_t i = 0; i < AX_NGR; ++i)
                 gr[i] = __builtin_amdgcn_raw_buffer_load_b128(rs_gran, i < ng ? goff + 16u * i : AX_OOB, 0, 0);
+
             if (STATS) s_rg += ng;
             uint32_t qj = 0;
             if (MODE == KM_LOCAL) {

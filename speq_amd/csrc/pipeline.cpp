@@ -185,6 +185,14 @@ int speq_pipeline_create(speq_device_index* d, const speq_scan_params* params, s
         hip_ok(hipMemsetAsync(pl->d_err, 0, 16, pl->compute), "hipMemset");
         hip_ok(hipMalloc(reinterpret_cast<void**>(&pl->d_bases), 8), "hipMalloc");
         hip_ok(hipMemsetAsync(pl->d_bases, 0, 8, pl->compute), "hipMemset");
+        // HIP binds a stream to a hardware queue at its first command: every lane and the copy stream get one now,
+        // so that streams created later (an RCCL communicator's) cannot take the queues first and leave the lanes
+        // sharing one (bench.py measured two scan streams serialised that way: DESIGN.md §7)
+        for (hipStream_t l : pl->lanes)
+            if (l != pl->compute) hip_ok(hipMemsetAsync(pl->d_bases, 0, 8, l), "hipMemset");
+        hip_ok(hipMemsetAsync(pl->d_bases, 0, 8, pl->copy), "hipMemset");
+        for (hipStream_t l : pl->lanes) hip_ok(hipStreamSynchronize(l), "hipStreamSynchronize");
+        hip_ok(hipStreamSynchronize(pl->copy), "hipStreamSynchronize");
         hip_ok(hipMalloc(reinterpret_cast<void**>(&pl->d_w), std::max<uint32_t>(pl->G, 1) * 8), "hipMalloc");
         hip_ok(hipMemsetAsync(pl->d_w, 0, std::max<uint32_t>(pl->G, 1) * 8, pl->compute), "hipMemset");
         pl->slots.resize(n_slots);

@@ -16,13 +16,14 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 # name -> the knobs it forces (kept in step with AXKNOB_* in the Makefile; checked below)
 VARIANTS = {
-    "kv1": "-DSPEQ_AX_SU=1 -DSPEQ_AX_REFILL=8 -DSPEQ_AX_BLOCKED=32 -DSPEQ_AX_P2_MARGIN=64 -DSPEQ_AX_PRIO_MIN=0 "
+    "kv1": "-DSPEQ_AX_SU=1 -DSPEQ_AX_SU_LOCAL=2 -DSPEQ_AX_REFILL=8 -DSPEQ_AX_BLOCKED=32 -DSPEQ_AX_P2_MARGIN=64 -DSPEQ_AX_PRIO_MIN=0 "
            "-DSPEQ_AX_WL=64 -DSPEQ_AX_MTILES=0",
     "kv2": "-DSPEQ_AX_WPB=2 -DSPEQ_AX_MIN_WAVES=4 -DSPEQ_AX_MIN_WAVES_LOCAL=3 -DSPEQ_AX_DEF_GLOBAL=192 "
            "-DSPEQ_AX_DEF_LOCAL=128",
     "kv3": "-DSPEQ_AX_SPEC_HW=1 -DSPEQ_AX_PRIO=0 -DSPEQ_AX_MPROOF=0",
 }
-KNOBS = {"SPEQ_AX_DEF_LOCAL", "SPEQ_AX_DEF_GLOBAL", "SPEQ_AX_WL", "SPEQ_AX_WPB", "SPEQ_AX_SU", "SPEQ_AX_MIN_WAVES",
+KNOBS = {"SPEQ_AX_DEF_LOCAL", "SPEQ_AX_DEF_GLOBAL", "SPEQ_AX_WL", "SPEQ_AX_WPB", "SPEQ_AX_SU", "SPEQ_AX_SU_LOCAL",
+         "SPEQ_AX_MIN_WAVES",
          "SPEQ_AX_MIN_WAVES_LOCAL", "SPEQ_AX_REFILL", "SPEQ_AX_BLOCKED", "SPEQ_AX_SPEC_HW", "SPEQ_AX_PRIO",
          "SPEQ_AX_PRIO_MIN", "SPEQ_AX_P2_MARGIN", "SPEQ_AX_MPROOF", "SPEQ_AX_MTILES"}
 
