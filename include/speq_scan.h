@@ -127,6 +127,11 @@ int speq_index_get_info(const speq_index* idx, speq_index_info* info);
 int speq_index_array(const speq_index* idx, const char* name, const void** ptr, uint64_t* bytes);
 
 /* ---- device replica ---- */
+/* Optional, before the index is even loaded (any thread): prepares GPU `device` for this process's first scan — its
+ * context, the library's GPU code (otherwise loaded at the first use of each kernel file: 30-55 ms inside the first
+ * scan) and `streams` (0-16) ready streams that speq_device_open and the FASTQ pipelines then take instead of creating
+ * them (3-10 ms each). New in the MI355X build: the reference loads a host index (fm_scanner.cpp:45-58). */
+int speq_device_warmup(int device, uint32_t streams);
 int speq_device_open(const speq_index* idx, int device, speq_device_index** out);
 int speq_device_close(speq_device_index* d);
 
@@ -262,6 +267,10 @@ typedef struct {
 } speq_stream_stats;
 int speq_scan_fastq(speq_device_index* d, const char* path1, const char* path2, const speq_scan_params* params,
                     speq_em* em, uint32_t threads, uint64_t* counts, double* weights, speq_stream_stats* stats);
+/* Optional, ahead of speq_scan_fastq on GPU `device` with `threads` parsers (e.g. while the index loads): allocates
+ * the stream's pinned and device slot buffers now (otherwise the parser threads' first slots allocate them: up to
+ * 66 ms of page-locking at the start of a `speq scan` run); the next stream's slots of that device take them. */
+int speq_stream_reserve(int device, uint32_t threads, uint32_t paired);
 /* The same reader and parsers without a device (host only; for tests and tools): record and base counts, and an
  * order-independent digest = sum over records of mix64(FNV-1a-64 over (len, (base << 8 | qual) per position)). */
 int speq_fastq_checksum(const char* path1, const char* path2, uint32_t threads, uint64_t* records, uint64_t* bases,

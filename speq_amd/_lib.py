@@ -67,6 +67,8 @@ SIGNATURES = {
     "speq_free": (None, [_P]),
     "speq_index_get_info": (C.c_int, [_P, C.POINTER(IndexInfo)]),
     "speq_index_array": (C.c_int, [_P, C.c_char_p, C.POINTER(_P), C.POINTER(C.c_uint64)]),
+    "speq_device_warmup": (C.c_int, [C.c_int, C.c_uint32]),
+    "speq_stream_reserve": (C.c_int, [C.c_int, C.c_uint32, C.c_uint32]),
     "speq_device_open": (C.c_int, [_P, C.c_int, C.POINTER(_P)]),
     "speq_device_close": (C.c_int, [_P]),
     "speq_scan_reads_device": (C.c_int, [_P, _P, _P, _P, C.c_uint64, C.POINTER(ScanParams), _P, _P, _P]),

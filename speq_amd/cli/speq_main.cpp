@@ -401,6 +401,14 @@ struct PhaseClock {
     PhaseClock() {
         const char* v = std::getenv("SPEQ_CLI_TIMING");
         on = v && *v && *v != '0';
+        since_launch("launch -> main");
+    }
+    // SPEQ_T0 (ns since the epoch, set by a timing harness just before it starts the process): process start-up cost
+    void since_launch(const char* what) const {
+        const char* t0 = std::getenv("SPEQ_T0");
+        if (!on || !t0 || !*t0) return;
+        const double now = std::chrono::duration<double>(std::chrono::system_clock::now().time_since_epoch()).count();
+        std::fprintf(stderr, "speq: %-22s %.4f s\n", what, now - std::strtod(t0, nullptr) * 1e-9);
     }
     void operator()(const char* what) {
         const auto now = std::chrono::steady_clock::now();
@@ -482,26 +490,6 @@ int run_scan(CmdArguments& a) {
         dist_connect(dd);
         phase("rendezvous");
     }
-    // HIP runtime start-up (device enumeration, ~0.1 s) overlaps the index read
-    std::thread hip_init([] { (void)speq_device_count(); });
-    struct Joiner {
-        std::thread& t;
-        ~Joiner() {
-            if (t.joinable()) t.join();
-        }
-    } join_init{hip_init};
-    fs::path idx_path = a.io_file_index;
-    idx_path.replace_extension(".idx");
-    speq_index* idx = nullptr;
-    void* hdr_data = nullptr;
-    uint64_t hdr_len = 0;
-    ok(speq_index_load(idx_path.c_str(), &idx, &hdr_data, &hdr_len), "loading the index");
-    hip_init.join();
-    IndexHeader h = decode_header(hdr_data, hdr_len);
-    speq_free(hdr_data);
-    const size_t G = h.names.size();
-    phase("index load");
-
     // GPUs: --devices list, --gpus N (0..N-1), or one (--device, $LOCAL_RANK, 0). Reads shard across them in-process
     // (SURVEY 8(e)): one replica of the index per GPU, the counters summed at the end.
     std::vector<int> devs = a.devices;
@@ -522,6 +510,35 @@ int run_scan(CmdArguments& a) {
         devs.push_back(dev);
     }
     const uint32_t n_dev = (uint32_t)devs.size();
+    const bool paired = !a.in_file_reads_path_2.empty();
+    // While the index loads: the HIP runtime, each GPU's context, the library's GPU code and ready streams
+    // (speq_device_warmup), and with one GPU per process the FASTQ stream's pinned and device slot buffers
+    // (speq_stream_reserve) — all of it had been on the critical path after the load (~0.2 s of a config-3 scan,
+    // profiles/r06/cli_trace_*). Failures here are left to speq_device_open / the stream to report.
+    std::vector<std::thread> warm;
+    for (int dv : devs)
+        warm.emplace_back([dv, n_dev, paired, threads = a.threads] {
+            if (speq_device_warmup(dv, 5) == SPEQ_OK && n_dev == 1) (void)speq_stream_reserve(dv, threads, paired);
+        });
+    struct Joiner {
+        std::vector<std::thread>& ts;
+        ~Joiner() {
+            for (auto& t : ts)
+                if (t.joinable()) t.join();
+        }
+    } join_warm{warm};
+    fs::path idx_path = a.io_file_index;
+    idx_path.replace_extension(".idx");
+    speq_index* idx = nullptr;
+    void* hdr_data = nullptr;
+    uint64_t hdr_len = 0;
+    ok(speq_index_load(idx_path.c_str(), &idx, &hdr_data, &hdr_len), "loading the index");
+    IndexHeader h = decode_header(hdr_data, hdr_len);
+    speq_free(hdr_data);
+    const size_t G = h.names.size();
+    phase("index load");
+    for (auto& t : warm) t.join();
+    phase("GPU warm-up (rest)");
     std::vector<speq_device_index*> ds(n_dev, nullptr);
     {  // replicas are uploaded concurrently (one host thread per GPU)
         std::vector<int> rcs(n_dev, SPEQ_OK);
@@ -565,7 +582,6 @@ int run_scan(CmdArguments& a) {
     }
     phase(".dat");
 
-    const bool paired = !a.in_file_reads_path_2.empty();
     const bool local = a.fixed_accuracy == 0.0;
     speq_scan_params prm{a.kmer, a.phred_cutoff, paired ? 1u : 0u, local ? (uint32_t)SPEQ_MODE_LOCAL : (uint32_t)SPEQ_MODE_GLOBAL};
     std::vector<uint64_t> counts(G + 2, 0);
@@ -691,6 +707,7 @@ int run_scan(CmdArguments& a) {
     (void)d;
     (void)idx;
     phase("output");
+    phase.since_launch("launch -> done");
     return 1;  // the reference's scan returns 1 (fm_scanner.cpp:280); main ignores it
 }
 

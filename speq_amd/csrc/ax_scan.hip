@@ -1869,3 +1869,12 @@ bool launch_ax(speq_device_index* d, int mode, bool paired, const UnitSrc& src, 
 }
 
 }  // namespace speq
+
+namespace speq {
+// Loads this translation unit's code object onto the current device (HIP loads a code object at the first use of
+// one of its kernels: 30-55 ms for the scan kernels' on the first launch of a `speq scan` run; speq_device_warmup).
+void warm_module_ax_scan() {
+    hipFuncAttributes a;
+    (void)hipFuncGetAttributes(&a, reinterpret_cast<const void*>(&k_ax_pack));
+}
+}  // namespace speq

@@ -443,3 +443,12 @@ void fm_build_arrays_gpu(FmIndex& idx, int device, bool pair_steps, bool triple_
 }
 
 }  // namespace speq
+
+namespace speq {
+// Loads this translation unit's code object onto the current device (HIP loads a code object at the first use of
+// one of its kernels: 30-55 ms for the scan kernels' on the first launch of a `speq scan` run; speq_device_warmup).
+void warm_module_build_gpu() {
+    hipFuncAttributes a;
+    (void)hipFuncGetAttributes(&a, reinterpret_cast<const void*>(&k_init_keys));
+}
+}  // namespace speq

@@ -384,3 +384,12 @@ void launch_fastq_parse(const uint8_t* d_raw, uint64_t len1, uint64_t len2, uint
 }
 
 }  // namespace speq
+
+namespace speq {
+// Loads this translation unit's code object onto the current device (HIP loads a code object at the first use of
+// one of its kernels: 30-55 ms for the scan kernels' on the first launch of a `speq scan` run; speq_device_warmup).
+void warm_module_fastq_gpu() {
+    hipFuncAttributes a;
+    (void)hipFuncGetAttributes(&a, reinterpret_cast<const void*>(&k_count_nl));
+}
+}  // namespace speq

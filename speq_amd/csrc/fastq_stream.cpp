@@ -827,6 +827,13 @@ struct ChecksumSink final : Sink {
 // Pinned slot size of speq_scan_fastq's pipeline: a block pair of up to 12 MiB per file plus one record usually
 // fits (larger blocks grow their slot once: speq_pipeline_reserve).
 constexpr uint64_t SLOT_BYTES = 16ull << 20;
+// One replica's slot count of a FASTQ stream with `threads` parsers (scan_fastq_impl, n_dev == 1)
+uint32_t stream_slots(uint32_t threads) {
+    const uint32_t n_parsers = std::max<uint32_t>(1, std::min<uint32_t>(threads ? threads : 1, 64));
+    const char* sm = std::getenv("SPEQ_STREAM_SLOTS_MAX");
+    const uint32_t slots_max = sm && *sm ? (uint32_t)std::max(3l, std::min(64l, std::atol(sm))) : 18u;
+    return std::min<uint32_t>(n_parsers + 2, slots_max);
+}
 
 struct StreamTotals {
     uint64_t records = 0, bases = 0, batches = 0;
@@ -1265,13 +1272,10 @@ void scan_fastq_impl(speq_device_index* const* ds, speq_em* const* ems, uint32_t
             throw std::invalid_argument("speq_scan_fastq_multi: replicas of different indexes");
     const uint32_t G = speq::device_groups(ds[0]);
     const auto t0 = std::chrono::steady_clock::now();
-    const uint32_t n_parsers = std::max<uint32_t>(1, std::min<uint32_t>(threads ? threads : 1, 64));
     // one replica: parsers + 2 slots (up to SPEQ_STREAM_SLOTS_MAX, default 18: 9.5 -> 8.6 ms at cfg 2 with 16 parsers,
     // profiles/r02/stream_slots.jsonl); several: the same total spread over
     // them, at least 3 each
-    const char* sm = std::getenv("SPEQ_STREAM_SLOTS_MAX");
-    const uint32_t slots_max = sm && *sm ? (uint32_t)std::max(3l, std::min(64l, std::atol(sm))) : 18u;
-    const uint32_t want = std::min<uint32_t>(n_parsers + 2, slots_max);
+    const uint32_t want = stream_slots(threads);
     const uint32_t n_slots = n_dev == 1 ? want : std::max<uint32_t>(3, (want + n_dev - 1) / n_dev + 1);
     std::vector<std::unique_ptr<speq_pipeline, void (*)(speq_pipeline*)>> guards;
     std::vector<speq_pipeline*> pls;
@@ -1351,6 +1355,14 @@ void scan_fastq_impl(speq_device_index* const* ds, speq_em* const* ems, uint32_t
 }
 
 }  // namespace
+
+extern "C" int speq_stream_reserve(int device, uint32_t threads, uint32_t paired) {
+    return speq::guarded([&] {
+        if (device < 0) throw std::invalid_argument("speq_stream_reserve: bad device ordinal");
+        speq::reserve_slot_buffers(device, stream_slots(threads), paired ? 2 * SLOT_BYTES : SLOT_BYTES,
+                                   paired ? 2u << 15 : 1u << 15, paired != 0);
+    });
+}
 
 extern "C" int speq_scan_fastq(speq_device_index* d, const char* path1, const char* path2,
                                const speq_scan_params* params, speq_em* em, uint32_t threads, uint64_t* counts,

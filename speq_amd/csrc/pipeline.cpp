@@ -86,6 +86,56 @@ void free_buffers(Slot& s) {
     s.cap_bytes = s.cap_records = 0;
 }
 
+// Slot buffer sets allocated ahead of a FASTQ stream (speq_stream_reserve, from the CLI's start-up thread while the
+// index loads): pinned host text + offsets, device text + offsets, and the GPU parse buffers sized for the slot. At
+// the start of a `speq scan` run the 16 parser threads' first slots allocated these on the critical path (up to 66 ms
+// of pinned allocation per thread, profiles/r06/cli_trace_*).
+struct PooledSlot {
+    int device = 0;
+    uint64_t bytes = 0, records = 0;
+    uint8_t* h_seq = nullptr;
+    uint64_t* h_off = nullptr;
+    uint8_t* d_seq = nullptr;
+    uint64_t* d_off = nullptr;
+    uint8_t* d_pseq = nullptr;
+    uint8_t* d_pqual = nullptr;
+    uint64_t* d_poff = nullptr;
+    void* d_scratch = nullptr;
+    size_t scratch_bytes = 0;
+};
+std::mutex g_slot_mu;
+auto* g_slot_pool = new std::vector<PooledSlot>();
+
+// A fresh slot takes a pooled set of the current device with room for (bytes, records), if there is one.
+bool take_pooled(Slot& s, uint64_t bytes, uint64_t records) {
+    int dev = -1;
+    if (hipGetDevice(&dev) != hipSuccess) return false;
+    PooledSlot e;
+    {
+        std::lock_guard<std::mutex> lk(g_slot_mu);
+        auto it = std::find_if(g_slot_pool->begin(), g_slot_pool->end(), [&](const PooledSlot& x) {
+            return x.device == dev && x.bytes >= bytes && x.records >= records;
+        });
+        if (it == g_slot_pool->end()) return false;
+        e = *it;
+        g_slot_pool->erase(it);
+    }
+    s.h_seq = e.h_seq;
+    s.h_off = e.h_off;
+    s.d_seq = e.d_seq;
+    s.d_off = e.d_off;
+    s.cap_bytes = e.bytes;
+    s.cap_records = e.records;
+    s.d_pseq = e.d_pseq;
+    s.d_pqual = e.d_pqual;
+    s.d_poff = e.d_poff;
+    s.d_scratch = e.d_scratch;
+    s.parse_bytes = e.bytes;
+    s.parse_slots = e.records;
+    s.scratch_bytes = e.scratch_bytes;
+    return true;
+}
+
 // Grows the slot to at least (bytes, records); qualities (host + device) only when asked for or already there:
 // raw-text submits (GPU FASTQ parsing) use the base buffer alone, which halves the pinned memory of a FASTQ stream.
 void ensure_buffers(Slot& s, uint64_t bytes, uint64_t records, bool qual) {
@@ -95,14 +145,17 @@ void ensure_buffers(Slot& s, uint64_t bytes, uint64_t records, bool qual) {
         bytes = std::max(bytes, s.cap_bytes);
         records = std::max(records, s.cap_records);
         qual = qual || s.h_qual;
+        const bool fresh = s.cap_bytes == 0 && !s.d_pseq;
         free_buffers(s);
-        hip_ok(hipHostMalloc(reinterpret_cast<void**>(&s.h_seq), bytes, hipHostMallocDefault), "hipHostMalloc");
-        hip_ok(hipHostMalloc(reinterpret_cast<void**>(&s.h_off), (records + 1) * 8, hipHostMallocDefault),
-               "hipHostMalloc");
-        hip_ok(hipMalloc(reinterpret_cast<void**>(&s.d_seq), bytes + 64), "hipMalloc");  // GPU parse: 16-B windows
-        hip_ok(hipMalloc(reinterpret_cast<void**>(&s.d_off), (records + 1) * 8), "hipMalloc");
-        s.cap_bytes = bytes;
-        s.cap_records = records;
+        if (!(fresh && take_pooled(s, bytes, records))) {
+            hip_ok(hipHostMalloc(reinterpret_cast<void**>(&s.h_seq), bytes, hipHostMallocDefault), "hipHostMalloc");
+            hip_ok(hipHostMalloc(reinterpret_cast<void**>(&s.h_off), (records + 1) * 8, hipHostMallocDefault),
+                   "hipHostMalloc");
+            hip_ok(hipMalloc(reinterpret_cast<void**>(&s.d_seq), bytes + 64), "hipMalloc");  // GPU parse: 16-B windows
+            hip_ok(hipMalloc(reinterpret_cast<void**>(&s.d_off), (records + 1) * 8), "hipMalloc");
+            s.cap_bytes = bytes;
+            s.cap_records = records;
+        }
     }
     if (qual && !s.h_qual) {
         hip_ok(hipHostMalloc(reinterpret_cast<void**>(&s.h_qual), s.cap_bytes, hipHostMallocDefault), "hipHostMalloc");
@@ -175,9 +228,9 @@ int speq_pipeline_create(speq_device_index* d, const speq_scan_params* params, s
         pl->device = speq::device_ordinal(d);
         pl->G = speq::device_groups(d);
         DevScope g(pl->device);
-        hip_ok(hipStreamCreateWithFlags(&pl->copy, hipStreamNonBlocking), "hipStreamCreate");
+        pl->copy = static_cast<hipStream_t>(speq::pooled_stream(pl->device));
         pl->lanes.resize(std::max<uint32_t>(1, speq::device_stream_lanes(d)), nullptr);
-        for (hipStream_t& l : pl->lanes) hip_ok(hipStreamCreateWithFlags(&l, hipStreamNonBlocking), "hipStreamCreate");
+        for (hipStream_t& l : pl->lanes) l = static_cast<hipStream_t>(speq::pooled_stream(pl->device));
         pl->compute = pl->lanes[0];
         hip_ok(hipMalloc(reinterpret_cast<void**>(&pl->d_counts), SPEQ_COUNTS_LEN(pl->G) * 8), "hipMalloc");
         hip_ok(hipMemsetAsync(pl->d_counts, 0, SPEQ_COUNTS_LEN(pl->G) * 8, pl->compute), "hipMemset");
@@ -185,14 +238,6 @@ int speq_pipeline_create(speq_device_index* d, const speq_scan_params* params, s
         hip_ok(hipMemsetAsync(pl->d_err, 0, 16, pl->compute), "hipMemset");
         hip_ok(hipMalloc(reinterpret_cast<void**>(&pl->d_bases), 8), "hipMalloc");
         hip_ok(hipMemsetAsync(pl->d_bases, 0, 8, pl->compute), "hipMemset");
-        // HIP binds a stream to a hardware queue at its first command: every lane and the copy stream get one now,
-        // so that streams created later (an RCCL communicator's) cannot take the queues first and leave the lanes
-        // sharing one (bench.py measured two scan streams serialised that way: DESIGN.md §7)
-        for (hipStream_t l : pl->lanes)
-            if (l != pl->compute) hip_ok(hipMemsetAsync(pl->d_bases, 0, 8, l), "hipMemset");
-        hip_ok(hipMemsetAsync(pl->d_bases, 0, 8, pl->copy), "hipMemset");
-        for (hipStream_t l : pl->lanes) hip_ok(hipStreamSynchronize(l), "hipStreamSynchronize");
-        hip_ok(hipStreamSynchronize(pl->copy), "hipStreamSynchronize");
         hip_ok(hipMalloc(reinterpret_cast<void**>(&pl->d_w), std::max<uint32_t>(pl->G, 1) * 8), "hipMalloc");
         hip_ok(hipMemsetAsync(pl->d_w, 0, std::max<uint32_t>(pl->G, 1) * 8, pl->compute), "hipMemset");
         pl->slots.resize(n_slots);
@@ -709,6 +754,114 @@ void speq_pipeline_free(speq_pipeline* pl) { delete pl; }
 // ---- host-buffer scans (speq_scan_reads / speq_em_scan_reads) over the pipeline ----
 // Whole units are cut into batches of <= 16 MiB of bases; up to four filler threads copy batches into pinned slots
 // (pageable -> pinned memcpy) and submit them, so the PCIe copy and the kernel of different batches overlap.
+namespace {
+// Streams created ahead of use (speq_device_warmup): hipStreamCreate takes 3-10 ms per stream at the start of a
+// process (5 of them were 36 ms of a `speq scan` run on the critical path: profiles/r06/cli_trace_*).
+std::mutex g_stream_mu;
+auto* g_streams = new std::multimap<int, hipStream_t>();
+void* g_stream_scratch[64] = {};  // per device: 8 B that a stream's binding command writes
+
+hipStream_t new_bound_stream(int device) {
+    hipStream_t st = nullptr;
+    hip_ok(hipStreamCreateWithFlags(&st, hipStreamNonBlocking), "hipStreamCreate");
+    void* scratch = nullptr;
+    {
+        std::lock_guard<std::mutex> lk(g_stream_mu);
+        if (device >= 0 && device < 64) {
+            if (!g_stream_scratch[device]) hip_ok(hipMalloc(&g_stream_scratch[device], 8), "hipMalloc");
+            scratch = g_stream_scratch[device];
+        }
+    }
+    // HIP binds a stream to its hardware queue at its first command: one now (see speq_pipeline_create)
+    if (scratch) hip_ok(hipMemsetAsync(scratch, 0, 8, st), "hipMemset");
+    hip_ok(hipStreamSynchronize(st), "hipStreamSynchronize");
+    return st;
+}
+}  // namespace
+
+namespace speq {
+void reserve_slot_buffers(int device, uint32_t n, uint64_t bytes, uint64_t records, bool paired) {
+    bytes = std::max<uint64_t>(bytes, 64);
+    records = std::max<uint64_t>(records, 2);
+    const size_t sb = fastq_gpu_scratch_bytes(bytes / (paired ? 2 : 1), records / (paired ? 2 : 1), paired);
+    std::vector<PooledSlot> got(n);
+    std::vector<std::string> err(n);
+    std::vector<std::thread> ts;
+    for (uint32_t i = 0; i < n; ++i)  // (pinned allocation is page-locking: one thread per set)
+        ts.emplace_back([&, i] {
+            try {
+                DevScope g(device);
+                PooledSlot& e = got[i];
+                e.device = device;
+                e.bytes = bytes;
+                e.records = records;
+                e.scratch_bytes = sb;
+                hip_ok(hipHostMalloc(reinterpret_cast<void**>(&e.h_seq), bytes, hipHostMallocDefault), "hipHostMalloc");
+                hip_ok(hipHostMalloc(reinterpret_cast<void**>(&e.h_off), (records + 1) * 8, hipHostMallocDefault),
+                       "hipHostMalloc");
+                hip_ok(hipMalloc(reinterpret_cast<void**>(&e.d_seq), bytes + 64), "hipMalloc");
+                hip_ok(hipMalloc(reinterpret_cast<void**>(&e.d_off), (records + 1) * 8), "hipMalloc");
+                hip_ok(hipMalloc(reinterpret_cast<void**>(&e.d_pseq), bytes), "hipMalloc");
+                hip_ok(hipMalloc(reinterpret_cast<void**>(&e.d_pqual), bytes), "hipMalloc");
+                hip_ok(hipMalloc(reinterpret_cast<void**>(&e.d_poff), (records + 1) * 8), "hipMalloc");
+                hip_ok(hipMalloc(&e.d_scratch, sb), "hipMalloc");
+            } catch (const std::exception& x) {
+                err[i] = x.what();
+            }
+        });
+    for (auto& t : ts) t.join();
+    std::lock_guard<std::mutex> lk(g_slot_mu);
+    for (uint32_t i = 0; i < n; ++i) {
+        PooledSlot& e = got[i];
+        if (err[i].empty()) {
+            g_slot_pool->push_back(e);
+            continue;
+        }
+        // (a set that failed part-way is released; the stream allocates its own slots as before)
+        if (e.h_seq) (void)hipHostFree(e.h_seq);
+        if (e.h_off) (void)hipHostFree(e.h_off);
+        for (void* q : {(void*)e.d_seq, (void*)e.d_off, (void*)e.d_pseq, (void*)e.d_pqual, (void*)e.d_poff, e.d_scratch})
+            if (q) (void)hipFree(q);
+    }
+    for (const std::string& x : err)
+        if (!x.empty()) throw DeviceError("speq_stream_reserve: " + x);
+}
+
+void* pooled_stream(int device) {
+    {
+        std::lock_guard<std::mutex> lk(g_stream_mu);
+        auto it = g_streams->find(device);
+        if (it != g_streams->end()) {
+            hipStream_t st = it->second;
+            g_streams->erase(it);
+            return st;
+        }
+    }
+    return new_bound_stream(device);
+}
+}  // namespace speq
+
+extern "C" int speq_device_warmup(int device, uint32_t streams) {
+    return speq::guarded([&] {
+        int ndev = 0;
+        if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0)
+            throw speq::DeviceError("no GPU visible (the scan path has no CPU fallback)");
+        if (device < 0 || device >= ndev) throw std::invalid_argument("speq_device_warmup: bad device ordinal");
+        if (streams > 16) throw std::invalid_argument("speq_device_warmup: at most 16 streams");
+        DevScope g(device);
+        hip_ok(hipFree(nullptr), "hipFree");  // the device's context
+        speq::warm_module_scan_kernels();
+        speq::warm_module_ax_scan();
+        speq::warm_module_build_gpu();
+        speq::warm_module_fastq_gpu();
+        for (uint32_t i = 0; i < streams; ++i) {
+            hipStream_t st = new_bound_stream(device);
+            std::lock_guard<std::mutex> lk(g_stream_mu);
+            g_streams->emplace(device, st);
+        }
+    });
+}
+
 namespace {
 // Idle host-scan pipelines per device (pinned allocation costs more than a typical scan); never destroyed at exit.
 std::mutex g_cache_mu;

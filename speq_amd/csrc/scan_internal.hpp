@@ -68,6 +68,17 @@ void em_clear(speq_em* em);
 bool device_fastq_gpu(const speq_device_index* d);
 uint32_t device_stream_lanes(const speq_device_index* d);
 int device_ordinal(const speq_device_index* d);
+// Code-object warm-up hooks, one per HIP translation unit (speq_device_warmup)
+void warm_module_scan_kernels();
+void warm_module_ax_scan();
+void warm_module_build_gpu();
+void warm_module_fastq_gpu();
+// A non-blocking stream (hipStream_t) on `device` (the current device), from the pool speq_device_warmup filled, else a
+// new one; bound to its hardware queue (a command has run on it). Its user destroys it with hipStreamDestroy.
+void* pooled_stream(int device);
+// Allocates n slot buffer sets of a FASTQ stream on `device` ahead of use (speq_stream_reserve): a fresh pipeline
+// slot of at most (bytes, records) then takes one instead of allocating (pipeline.cpp).
+void reserve_slot_buffers(int device, uint32_t n, uint64_t bytes, uint64_t records, bool paired);
 uint32_t device_groups(const speq_device_index* d);
 uint64_t device_text_len(const speq_device_index* d);  // FM text length n of the replica's index
 }  // namespace speq

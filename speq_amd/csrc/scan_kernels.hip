@@ -1653,7 +1653,7 @@ int speq_device_open(const speq_index* idx, int device, speq_device_index** out)
             lut[2 * q + 1] = 1.0 / lut[2 * q];  // q = 0: inf, never used (a passing window has every q > cutoff >= 0)
         }
         d->d_qlut = d->track(dev_upload(lut));
-        HIP_OK(hipStreamCreateWithFlags(&d->stream, hipStreamNonBlocking));
+        d->stream = static_cast<hipStream_t>(speq::pooled_stream(device));
         hipDeviceProp_t prop;
         HIP_OK(hipGetDeviceProperties(&prop, device));
         d->n_cus = (uint32_t)prop.multiProcessorCount;
@@ -2180,4 +2180,13 @@ bool device_fastq_gpu(const speq_device_index* d) { return d->fastq_gpu; }
 uint32_t device_stream_lanes(const speq_device_index* d) { return d->stream_lanes; }
 uint32_t device_groups(const speq_device_index* d) { return d->G; }
 uint64_t device_text_len(const speq_device_index* d) { return d->view.n; }
+}  // namespace speq
+
+namespace speq {
+// Loads this translation unit's code object onto the current device (HIP loads a code object at the first use of
+// one of its kernels: 30-55 ms for the scan kernels' on the first launch of a `speq scan` run; speq_device_warmup).
+void warm_module_scan_kernels() {
+    hipFuncAttributes a;
+    (void)hipFuncGetAttributes(&a, reinterpret_cast<const void*>(&k_ktab_keys));
+}
 }  // namespace speq
