@@ -19,7 +19,7 @@ mode) -> `value`. The same run also measures secondary lines (compact objects un
 Weak scaling: every rank scans its own shard of the deterministic read stream.
 
 stdout: ONE compact JSON line on rank 0 (< 8 KB; `compact_result`); the full per-line detail (work counters, U
-vectors, paths) goes to --detail (default profiles/r05/bench_detail_n<N>.json).
+vectors, paths) goes to --detail (default profiles/r06/bench_detail_n<N>.json).
 Launch: python bench.py [--gpus N --steps K --warmup W]. N > 1 under torch.distributed.run (WORLD_SIZE must equal N),
 or without a launcher: bench.py then starts torch.distributed.run over N local ranks itself (launch_plan).
 """
@@ -90,7 +90,7 @@ def parse_args(argv=None):
     p.add_argument("--cpu-seconds", type=float, default=15.0, help="target CPU-baseline sample duration (headline)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-pcie", action="store_true", help="skip the PCIe-inclusive host-buffer measurement")
-    p.add_argument("--detail", default="", help="full-detail JSON path (default profiles/r05/bench_detail_n<N>.json)")
+    p.add_argument("--detail", default="", help="full-detail JSON path (default profiles/r06/bench_detail_n<N>.json)")
     return p.parse_args(argv)
 
 
@@ -830,7 +830,7 @@ def main(argv=None):
             p5["dev"].close()
 
     if ctx.rank == 0:
-        detail_path = a.detail or os.path.join(ROOT, "profiles", "r05", f"bench_detail_n{ctx.world}.json")
+        detail_path = a.detail or os.path.join(ROOT, "profiles", "r06", f"bench_detail_n{ctx.world}.json")
         config = {
             "workload": head["workload"],
             "k": k, "reads_per_gpu": n_reads, "paired": head["paired"], "mode": a.mode,

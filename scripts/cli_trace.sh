@@ -23,7 +23,7 @@ cd $W
 export SPEQ_CLI_TIMING=1
 timeout -k 10 120 $GRAFT_REPO_ROOT/bin/speq index -r refs.fa -g groups.txt -x ref -t 16 > $OUT/index.log 2>&1 || exit 1
 timeout -k 10 120 $GRAFT_REPO_ROOT/bin/speq scan -1 r1.fq -x ref -k 31 -t 16 -o o1.txt > $OUT/scan1.log 2>&1 || exit 1
-for i in 1 2 3; do timeout -k 10 120 python -c "import os, subprocess, sys, time; t = time.time(); r = subprocess.call(sys.argv[1:], env=dict(os.environ, SPEQ_T0=str(time.time_ns()))); print('wall %.3f s' % (time.time() - t), file=sys.stderr); sys.exit(r)" $GRAFT_REPO_ROOT/bin/speq scan -1 r1.fq -x ref -k 31 -t 16 -o o2_$i.txt > $OUT/scan2_$i.log 2>&1 || exit 1; done
+for i in ${CLI_REPS:-1 2 3}; do timeout -k 10 120 python -c "import os, subprocess, sys, time; t = time.time(); r = subprocess.call(sys.argv[1:], env=dict(os.environ, SPEQ_T0=str(time.time_ns()))); print('wall %.3f s' % (time.time() - t), file=sys.stderr); sys.exit(r)" $GRAFT_REPO_ROOT/bin/speq scan -1 r1.fq -x ref -k 31 -t 16 -o o2_$i.txt > $OUT/scan2_$i.log 2>&1 || exit 1; done
 timeout -k 10 300 rocprofv3 --hip-trace --kernel-trace --stats -d $OUT/prof -o scan --output-format csv -- $GRAFT_REPO_ROOT/bin/speq scan -1 r1.fq -x ref -k 31 -t 16 -o o3.txt > $OUT/scan3.log 2>&1; rc=$?
 cd /; rm -rf $W
 grep -h "speq: \|wall" $OUT/scan2_*.log

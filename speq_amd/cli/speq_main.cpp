@@ -515,11 +515,12 @@ int run_scan(CmdArguments& a) {
     // (speq_device_warmup), and with one GPU per process the FASTQ stream's pinned and device slot buffers
     // (speq_stream_reserve) — all of it had been on the critical path after the load (~0.2 s of a config-3 scan,
     // profiles/r06/cli_trace_*). Failures here are left to speq_device_open / the stream to report.
+    // (device open needs only the runtime: it runs beside what is left of the warm-up, joined before the stream)
     std::vector<std::thread> warm;
-    for (int dv : devs)
-        warm.emplace_back([dv, n_dev, paired, threads = a.threads] {
-            if (speq_device_warmup(dv, 5) == SPEQ_OK && n_dev == 1) (void)speq_stream_reserve(dv, threads, paired);
-        });
+    for (int dv : devs) {
+        warm.emplace_back([dv] { (void)speq_device_warmup(dv, 5); });
+        if (n_dev == 1) warm.emplace_back([dv, paired, threads = a.threads] { (void)speq_stream_reserve(dv, threads, paired); });
+    }
     struct Joiner {
         std::vector<std::thread>& ts;
         ~Joiner() {
@@ -537,8 +538,6 @@ int run_scan(CmdArguments& a) {
     speq_free(hdr_data);
     const size_t G = h.names.size();
     phase("index load");
-    for (auto& t : warm) t.join();
-    phase("GPU warm-up (rest)");
     std::vector<speq_device_index*> ds(n_dev, nullptr);
     {  // replicas are uploaded concurrently (one host thread per GPU)
         std::vector<int> rcs(n_dev, SPEQ_OK);
@@ -555,6 +554,8 @@ int run_scan(CmdArguments& a) {
     }
     speq_device_index* d = ds[0];
     phase("device open");
+    for (auto& t : warm) t.join();
+    phase("GPU warm-up (rest)");
 
     // Reference uniqueness per group, cached in <stem>_<k>mer.dat keyed by the index mtime.
     const int64_t idx_mtime = mtime_ns(idx_path);
@@ -732,7 +733,19 @@ int main(int argc, char** argv) {
         dist_clear_stale(dd);
         const bool other_rank = dd.rank != 0;
         if (a.is_indexer && !other_rank) run_index(a);
-        if (a.is_scanner) run_scan(a);
+        if (a.is_scanner) {
+            run_scan(a);
+            // Everything is written and the GPU idle: leave without the runtime's teardown (unpinning the stream's
+            // slots, freeing the replica: ~0.2 s of a config-3 scan, profiles/r06/cli_trace_*), which process exit
+            // does in the kernel anyway. SPEQ_FULL_EXIT=1 keeps the ordinary exit.
+            const char* fe = std::getenv("SPEQ_FULL_EXIT");
+            if (!(fe && fe[0] == '1')) {
+                std::cout.flush();
+                std::cerr.flush();
+                std::fflush(nullptr);
+                std::_Exit(0);
+            }
+        }
     } catch (const std::exception& e) {
         std::cerr << "speq: error: " << e.what() << "\n";
         return 2;

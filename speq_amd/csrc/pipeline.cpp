@@ -848,17 +848,42 @@ extern "C" int speq_device_warmup(int device, uint32_t streams) {
             throw speq::DeviceError("no GPU visible (the scan path has no CPU fallback)");
         if (device < 0 || device >= ndev) throw std::invalid_argument("speq_device_warmup: bad device ordinal");
         if (streams > 16) throw std::invalid_argument("speq_device_warmup: at most 16 streams");
-        DevScope g(device);
-        hip_ok(hipFree(nullptr), "hipFree");  // the device's context
-        speq::warm_module_scan_kernels();
-        speq::warm_module_ax_scan();
-        speq::warm_module_build_gpu();
-        speq::warm_module_fastq_gpu();
-        for (uint32_t i = 0; i < streams; ++i) {
-            hipStream_t st = new_bound_stream(device);
-            std::lock_guard<std::mutex> lk(g_stream_mu);
-            g_streams->emplace(device, st);
+        {
+            DevScope g(device);
+            hip_ok(hipFree(nullptr), "hipFree");  // the device's context
         }
+        // the four code objects (10-42 ms each) and the streams (~8 ms each) on threads of their own
+        std::vector<std::thread> ts;
+        std::vector<std::string> err(5);
+        auto run = [&](int i, void (*f)()) {
+            ts.emplace_back([&, i, f] {
+                try {
+                    DevScope g(device);
+                    f();
+                } catch (const std::exception& x) {
+                    err[i] = x.what();
+                }
+            });
+        };
+        run(0, speq::warm_module_scan_kernels);
+        run(1, speq::warm_module_ax_scan);
+        run(2, speq::warm_module_build_gpu);
+        run(3, speq::warm_module_fastq_gpu);
+        ts.emplace_back([&] {
+            try {
+                DevScope g(device);
+                for (uint32_t i = 0; i < streams; ++i) {
+                    hipStream_t st = new_bound_stream(device);
+                    std::lock_guard<std::mutex> lk(g_stream_mu);
+                    g_streams->emplace(device, st);
+                }
+            } catch (const std::exception& x) {
+                err[4] = x.what();
+            }
+        });
+        for (auto& t : ts) t.join();
+        for (const std::string& x : err)
+            if (!x.empty()) throw speq::DeviceError("speq_device_warmup: " + x);
     });
 }
 
