@@ -12,7 +12,7 @@ export SPEQ_BENCH_NO_STATS=1  # no instrumented k_scan_ax launch among the profi
 OUT=${OUT:-gpurun_out/prof}
 PASSES=${PASSES:-"trace req fetch write tcc sq sq2 ta"}
 mkdir -p $OUT
-BENCH="bench.py --steps 5 --warmup 1 --no-cpu-baseline --no-pcie --no-lf-compare --no-extra --detail $OUT/detail.json $*"
+BENCH="bench.py --steps 5 --warmup 1 --streams 1 --regions 1 --no-cpu-baseline --no-pcie --no-lf-compare --no-extra --detail $OUT/detail.json $*"
 run() {  # name, rocprof args...
     local name=$1; shift
     echo "== $name" >&2
