@@ -13,29 +13,29 @@ constexpr uint64_t EM_CHUNKS = 64;  // fixed row partition of speq_em_step (dete
 
 namespace speq {
 
-void em_build_rows(speq_em& em, const std::vector<uint32_t>& mult, const std::vector<uint32_t>& hi, uint32_t threads) {
+void em_build_rows(speq_em& em, const std::vector<uint32_t>& lo, const std::vector<uint32_t>& mult,
+                          const std::vector<uint32_t>& hi, uint32_t threads) {
     const FmIndex& fm = em.idx->fm;
-    const uint64_t n = em.n;
+    const uint64_t m = lo.size();
     if (threads == 0) threads = std::max(1u, std::thread::hardware_concurrency());
-    threads = std::max<uint32_t>(1, std::min<uint64_t>(threads, n / 65536 + 1));
+    threads = std::max<uint32_t>(1, std::min<uint64_t>(threads, m / 4096 + 1));
     struct Part {
         std::vector<uint64_t> mult, nnz;
         std::vector<uint32_t> grp, cnt;
     };
     std::vector<Part> parts(threads);
     std::vector<std::thread> pool;
-    const uint64_t chunk = (n + threads - 1) / threads;
+    const uint64_t chunk = (m + threads - 1) / threads;
     for (uint32_t t = 0; t < threads; ++t) {
         pool.emplace_back([&, t] {
             Part& P = parts[t];
             std::vector<uint32_t> dense(em.G, 0);
             std::vector<uint32_t> touched;
-            const uint64_t b = t * chunk, e = std::min(n, b + chunk);
-            for (uint64_t lo = b; lo < e; ++lo) {
-                if (!mult[lo]) continue;
-                const uint64_t h = hi[lo];
+            const uint64_t b = t * chunk, e = std::min(m, b + chunk);
+            for (uint64_t r = b; r < e; ++r) {
+                const uint64_t h = hi[r];
                 // per-group occurrence counts c_g = overlap of [lo, h) with the label runs of group g
-                for (uint64_t i = lo; i < h;) {
+                for (uint64_t i = lo[r]; i < h;) {
                     const uint64_t j = std::min<uint64_t>(fm.run_end(i), h);
                     const uint16_t g = fm.label_at(i);
                     if (!dense[g]) touched.push_back(g);
@@ -43,7 +43,7 @@ void em_build_rows(speq_em& em, const std::vector<uint32_t>& mult, const std::ve
                     i = j;
                 }
                 std::sort(touched.begin(), touched.end());  // the reference sums groups in index order
-                P.mult.push_back(mult[lo]);
+                P.mult.push_back(mult[r]);
                 P.nnz.push_back(touched.size());
                 for (uint32_t g : touched) {
                     P.grp.push_back(g);

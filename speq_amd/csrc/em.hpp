@@ -30,6 +30,8 @@ struct speq_em {
 };
 
 namespace speq {
-// Builds the CSR rows from the downloaded per-position arrays (host, multi-threaded).
-void em_build_rows(speq_em& em, const std::vector<uint32_t>& mult, const std::vector<uint32_t>& hi, uint32_t threads);
+// Builds the CSR rows (host, multi-threaded) from the positions that start a recorded interval, ascending, with their
+// multiplicities and interval ends (compacted on the GPU by speq_em_finalize): one row per interval, in position order.
+void em_build_rows(speq_em& em, const std::vector<uint32_t>& lo, const std::vector<uint32_t>& mult,
+                   const std::vector<uint32_t>& hi, uint32_t threads);
 }  // namespace speq

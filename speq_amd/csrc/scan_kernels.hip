@@ -1570,6 +1570,80 @@ static int scan_device_impl(speq_device_index* d, const uint8_t* d_seq, const ui
 
 // dst += src for the EM interval histogram; an interval's end is a function of its start, so a start that src
 // recorded takes src's end (dst's is either the same or unset). Grid-stride loop.
+// EM finalize: the positions that start a recorded interval, compacted in position order (the CSR rows keep the
+// order the host built before, so the EM step's sums are unchanged). Block b covers EM_TILE positions; pass 1 counts
+// them, an exclusive scan of the counts (one workgroup) gives every block its offset, pass 2 writes (lo, mult, hi).
+constexpr uint32_t EM_TILE = 4096;
+__global__ __launch_bounds__(256) void k_em_count(const uint32_t* __restrict__ mult, uint64_t n,
+                                                  uint32_t* __restrict__ counts) {
+    __shared__ uint32_t part[4];
+    const uint64_t b0 = (uint64_t)blockIdx.x * EM_TILE;
+    uint32_t c = 0;
+    for (uint32_t i = threadIdx.x; i < EM_TILE; i += 256) {
+        const uint64_t pos = b0 + i;
+        c += (pos < n && mult[pos] != 0u) ? 1u : 0u;
+    }
+    for (int o = 32; o > 0; o >>= 1) c += __shfl_down(c, o);
+    if ((threadIdx.x & 63u) == 0) part[threadIdx.x >> 6] = c;
+    __syncthreads();
+    if (threadIdx.x == 0) counts[blockIdx.x] = part[0] + part[1] + part[2] + part[3];
+}
+// exclusive scan of nb block counts in place, one workgroup of 1024 threads; total at counts[nb]
+__global__ __launch_bounds__(1024) void k_em_scan(uint32_t* __restrict__ counts, uint32_t nb) {
+    __shared__ uint32_t wsum[16];
+    __shared__ uint32_t carry;
+    if (threadIdx.x == 0) carry = 0;
+    __syncthreads();
+    for (uint32_t base = 0; base < nb; base += 1024) {
+        const uint32_t i = base + threadIdx.x;
+        const uint32_t v = i < nb ? counts[i] : 0u;
+        uint32_t x = v;  // inclusive scan within the wave
+        const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
+        for (uint32_t o = 1; o < 64; o <<= 1) {
+            const uint32_t y = __shfl_up(x, o);
+            if (lane >= o) x += y;
+        }
+        if (lane == 63) wsum[w] = x;
+        __syncthreads();
+        uint32_t before = carry;
+        for (uint32_t q = 0; q < w; ++q) before += wsum[q];
+        if (i < nb) counts[i] = before + x - v;
+        __syncthreads();
+        if (threadIdx.x == 1023) carry = before + x;
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) counts[nb] = carry;
+}
+__global__ __launch_bounds__(256) void k_em_compact(const uint32_t* __restrict__ mult, const uint32_t* __restrict__ hi,
+                                                    uint64_t n, const uint32_t* __restrict__ offs,
+                                                    uint32_t* __restrict__ out_lo, uint32_t* __restrict__ out_mult,
+                                                    uint32_t* __restrict__ out_hi) {
+    __shared__ uint32_t wtot[4];
+    __shared__ uint32_t run;
+    const uint64_t b0 = (uint64_t)blockIdx.x * EM_TILE;
+    if (threadIdx.x == 0) run = offs[blockIdx.x];
+    __syncthreads();
+    const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
+    for (uint32_t i = 0; i < EM_TILE; i += 256) {  // 256 consecutive positions per round, in order
+        const uint64_t pos = b0 + i + threadIdx.x;
+        const uint32_t m = pos < n ? mult[pos] : 0u;
+        const unsigned long long bal = __ballot(m != 0u);
+        if (lane == 0) wtot[w] = (uint32_t)__popcll(bal);
+        __syncthreads();
+        uint32_t at = run;
+        for (uint32_t q = 0; q < w; ++q) at += wtot[q];
+        if (m != 0u) {
+            at += __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
+            out_lo[at] = (uint32_t)pos;
+            out_mult[at] = m;
+            out_hi[at] = hi[pos];
+        }
+        __syncthreads();
+        if (threadIdx.x == 0) run += wtot[0] + wtot[1] + wtot[2] + wtot[3];
+        __syncthreads();
+    }
+}
+
 __global__ void k_em_merge(uint32_t* __restrict__ dmult, uint32_t* __restrict__ dhi, const uint32_t* __restrict__ smult,
                            const uint32_t* __restrict__ shi, uint64_t n) {
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
@@ -1786,10 +1860,45 @@ int speq_em_finalize(speq_em* em, uint32_t threads) {
         if (em->finalized) return;
         DeviceGuard g(em->dev->device);
         HIP_OK(hipDeviceSynchronize());
-        std::vector<uint32_t> mult(em->n), hi(em->n);
-        HIP_OK(hipMemcpy(mult.data(), em->d_mult, em->n * 4, hipMemcpyDeviceToHost));
-        HIP_OK(hipMemcpy(hi.data(), em->d_hi, em->n * 4, hipMemcpyDeviceToHost));
-        speq::em_build_rows(*em, mult, hi, threads);
+        // only the positions that start a recorded interval come to the host, in position order (round 6: the two
+        // whole per-position arrays were 80 MB at config 3, most of the CLI's 54 ms EM finalize)
+        const uint64_t n = em->n;
+        const uint32_t nb = (uint32_t)((n + EM_TILE - 1) / EM_TILE);
+        hipStream_t st = em->dev->stream;
+        uint32_t* d_cnt = nullptr;
+        uint32_t* d_out = nullptr;
+        HIP_OK(hipMalloc(&d_cnt, ((uint64_t)nb + 1) * 4));
+        uint32_t nnz = 0;
+        try {
+            if (nb) {
+                hipLaunchKernelGGL(k_em_count, dim3(nb), dim3(256), 0, st, em->d_mult, n, d_cnt);
+                HIP_OK(hipGetLastError());
+            }
+            hipLaunchKernelGGL(k_em_scan, dim3(1), dim3(1024), 0, st, d_cnt, nb);
+            HIP_OK(hipGetLastError());
+            HIP_OK(hipMemcpyAsync(&nnz, d_cnt + nb, 4, hipMemcpyDeviceToHost, st));
+            HIP_OK(hipStreamSynchronize(st));
+            std::vector<uint32_t> lo(nnz), mult(nnz), hi(nnz);
+            if (nnz) {
+                HIP_OK(hipMalloc(&d_out, (uint64_t)nnz * 12));
+                hipLaunchKernelGGL(k_em_compact, dim3(nb), dim3(256), 0, st, em->d_mult, em->d_hi, n, d_cnt, d_out,
+                                   d_out + nnz, d_out + 2ull * nnz);
+                HIP_OK(hipGetLastError());
+                HIP_OK(hipMemcpyAsync(lo.data(), d_out, (uint64_t)nnz * 4, hipMemcpyDeviceToHost, st));
+                HIP_OK(hipMemcpyAsync(mult.data(), d_out + nnz, (uint64_t)nnz * 4, hipMemcpyDeviceToHost, st));
+                HIP_OK(hipMemcpyAsync(hi.data(), d_out + 2ull * nnz, (uint64_t)nnz * 4, hipMemcpyDeviceToHost, st));
+                HIP_OK(hipStreamSynchronize(st));
+            }
+            (void)hipFree(d_cnt);
+            if (d_out) (void)hipFree(d_out);
+            d_cnt = d_out = nullptr;
+            speq::em_build_rows(*em, lo, mult, hi, threads);
+        } catch (...) {
+            (void)hipStreamSynchronize(st);
+            if (d_cnt) (void)hipFree(d_cnt);
+            if (d_out) (void)hipFree(d_out);
+            throw;
+        }
         (void)hipFree(em->d_mult);
         (void)hipFree(em->d_hi);
         em->d_mult = em->d_hi = nullptr;
