@@ -128,8 +128,8 @@ int speq_index_array(const speq_index* idx, const char* name, const void** ptr, 
 
 /* ---- device replica ---- */
 /* Optional, before the index is even loaded (any thread): prepares GPU `device` for this process's first scan — its
- * context, the library's GPU code (otherwise loaded at the first use of each kernel file: 30-55 ms inside the first
- * scan) and `streams` (0-16) ready streams that speq_device_open and the FASTQ pipelines then take instead of creating
+ * context, the scan's GPU code (otherwise loaded at the first use of each kernel file, inside the first scan; the
+ * GPU index builder's code is left to its first use) and `streams` (0-16) ready streams that speq_device_open and the FASTQ pipelines then take instead of creating
  * them (3-10 ms each). New in the MI355X build: the reference loads a host index (fm_scanner.cpp:45-58). */
 int speq_device_warmup(int device, uint32_t streams);
 int speq_device_open(const speq_index* idx, int device, speq_device_index** out);

@@ -1771,6 +1771,7 @@ AxTable build_ax(speq_device_index* d, uint32_t k) {
     cleanup();
     for (void* q : mine) d->track(q);
     ax.build_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    startup_trace("per-k structures built");
     return ax;
 }
 

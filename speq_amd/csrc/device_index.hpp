@@ -66,6 +66,9 @@ struct speq_device_index {
     const uint4* sparse_rank[3] = {nullptr, nullptr, nullptr};    // their sparse forms (see prefix_lookup)
     const uint2* sparse_iv[3] = {nullptr, nullptr, nullptr};
     uint64_t present[3] = {0, 0, 0};                              // distinct q-mers per level
+    uint64_t prefix_words[3] = {0, 0, 0};                         // u32 words of the dense tables
+    std::mutex sparse_mu;                                         // the sparse forms are built on first use
+    bool sparse_built = false;
     bool fastq_gpu = true;        // tuning "fastq_gpu_parse": parse simple four-line FASTQ blocks on the GPU
     uint32_t stream_lanes = 3;    // tuning "stream_lanes": compute streams per pipeline (batches scanned concurrently)
     int sparse_choice = 0;        // tuning "sparse_prefix": 0 dense (default), 1 sparse, -1 sparse when < 1/8 of

@@ -761,6 +761,8 @@ struct PipelineSink final : Sink {
     }
     void submit_raw(const speq_slot& s, uint64_t len1, uint64_t len2, uint64_t n, bool paired, const char* host1,
                     const char* host2) override {
+        static std::atomic<bool> first{true};
+        if (first.exchange(false)) speq::startup_trace("stream: first block submitted");
         speq::pipeline_submit_raw(of(s.slot), local(s.slot), len1, len2, n, paired,
                                   reinterpret_cast<const uint8_t*>(host1), reinterpret_cast<const uint8_t*>(host2));
     }

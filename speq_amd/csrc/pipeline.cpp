@@ -10,7 +10,9 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <condition_variable>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <deque>
@@ -62,6 +64,28 @@ struct Slot {
     size_t scratch_bytes = 0;
 };
 
+// Pinned host memory of the slots: an aligned allocation, touched, then page-locked with hipHostRegister — 300 MB in
+// 16 threads take 9-11 ms this way against 64-69 ms of hipHostMalloc (tools/upload_probe.cpp alloc,
+// profiles/r06/cli/), and the copies from it run at the same DMA rate.
+void* pinned_alloc(size_t bytes) {
+    const size_t n = (std::max<size_t>(bytes, 1) + 4095) & ~size_t(4095);
+    void* p = std::aligned_alloc(4096, n);
+    if (!p) throw std::bad_alloc();
+    std::memset(p, 0, n);
+    const hipError_t e = hipHostRegister(p, n, hipHostRegisterDefault);
+    if (e != hipSuccess) {
+        std::free(p);
+        hip_ok(e, "hipHostRegister");
+    }
+    return p;
+}
+
+void pinned_free(void* p) {
+    if (!p) return;
+    (void)hipHostUnregister(p);
+    std::free(p);
+}
+
 void free_parse(Slot& s) {
     if (s.d_pseq) (void)hipFree(s.d_pseq);
     if (s.d_pqual) (void)hipFree(s.d_pqual);
@@ -75,9 +99,9 @@ void free_parse(Slot& s) {
 }
 
 void free_buffers(Slot& s) {
-    if (s.h_seq) (void)hipHostFree(s.h_seq);
-    if (s.h_qual) (void)hipHostFree(s.h_qual);
-    if (s.h_off) (void)hipHostFree(s.h_off);
+    pinned_free(s.h_seq);
+    pinned_free(s.h_qual);
+    pinned_free(s.h_off);
     if (s.d_seq) (void)hipFree(s.d_seq);
     if (s.d_qual) (void)hipFree(s.d_qual);
     if (s.d_off) (void)hipFree(s.d_off);
@@ -148,9 +172,8 @@ void ensure_buffers(Slot& s, uint64_t bytes, uint64_t records, bool qual) {
         const bool fresh = s.cap_bytes == 0 && !s.d_pseq;
         free_buffers(s);
         if (!(fresh && take_pooled(s, bytes, records))) {
-            hip_ok(hipHostMalloc(reinterpret_cast<void**>(&s.h_seq), bytes, hipHostMallocDefault), "hipHostMalloc");
-            hip_ok(hipHostMalloc(reinterpret_cast<void**>(&s.h_off), (records + 1) * 8, hipHostMallocDefault),
-                   "hipHostMalloc");
+            s.h_seq = static_cast<uint8_t*>(pinned_alloc(bytes));
+            s.h_off = static_cast<uint64_t*>(pinned_alloc((records + 1) * 8));
             hip_ok(hipMalloc(reinterpret_cast<void**>(&s.d_seq), bytes + 64), "hipMalloc");  // GPU parse: 16-B windows
             hip_ok(hipMalloc(reinterpret_cast<void**>(&s.d_off), (records + 1) * 8), "hipMalloc");
             s.cap_bytes = bytes;
@@ -158,7 +181,7 @@ void ensure_buffers(Slot& s, uint64_t bytes, uint64_t records, bool qual) {
         }
     }
     if (qual && !s.h_qual) {
-        hip_ok(hipHostMalloc(reinterpret_cast<void**>(&s.h_qual), s.cap_bytes, hipHostMallocDefault), "hipHostMalloc");
+        s.h_qual = static_cast<uint8_t*>(pinned_alloc(s.cap_bytes));
         hip_ok(hipMalloc(reinterpret_cast<void**>(&s.d_qual), s.cap_bytes), "hipMalloc");
     }
 }
@@ -780,6 +803,21 @@ hipStream_t new_bound_stream(int device) {
 }  // namespace
 
 namespace speq {
+void startup_trace(const char* what) {
+    static const bool on = [] {
+        const char* v = std::getenv("SPEQ_STARTUP_TRACE");
+        return v && *v && *v != '0';
+    }();
+    if (!on) return;
+    static const double t0 = [] {
+        const char* v = std::getenv("SPEQ_T0");
+        if (v && *v) return std::strtod(v, nullptr) * 1e-9;
+        return std::chrono::duration<double>(std::chrono::system_clock::now().time_since_epoch()).count();
+    }();
+    const double now = std::chrono::duration<double>(std::chrono::system_clock::now().time_since_epoch()).count();
+    std::fprintf(stderr, "speq-trace: %-34s %.4f s\n", what, now - t0);
+}
+
 void reserve_slot_buffers(int device, uint32_t n, uint64_t bytes, uint64_t records, bool paired) {
     bytes = std::max<uint64_t>(bytes, 64);
     records = std::max<uint64_t>(records, 2);
@@ -796,9 +834,8 @@ void reserve_slot_buffers(int device, uint32_t n, uint64_t bytes, uint64_t recor
                 e.bytes = bytes;
                 e.records = records;
                 e.scratch_bytes = sb;
-                hip_ok(hipHostMalloc(reinterpret_cast<void**>(&e.h_seq), bytes, hipHostMallocDefault), "hipHostMalloc");
-                hip_ok(hipHostMalloc(reinterpret_cast<void**>(&e.h_off), (records + 1) * 8, hipHostMallocDefault),
-                       "hipHostMalloc");
+                e.h_seq = static_cast<uint8_t*>(pinned_alloc(bytes));
+                e.h_off = static_cast<uint64_t*>(pinned_alloc((records + 1) * 8));
                 hip_ok(hipMalloc(reinterpret_cast<void**>(&e.d_seq), bytes + 64), "hipMalloc");
                 hip_ok(hipMalloc(reinterpret_cast<void**>(&e.d_off), (records + 1) * 8), "hipMalloc");
                 hip_ok(hipMalloc(reinterpret_cast<void**>(&e.d_pseq), bytes), "hipMalloc");
@@ -810,6 +847,7 @@ void reserve_slot_buffers(int device, uint32_t n, uint64_t bytes, uint64_t recor
             }
         });
     for (auto& t : ts) t.join();
+    startup_trace("slot buffers reserved");
     std::lock_guard<std::mutex> lk(g_slot_mu);
     for (uint32_t i = 0; i < n; ++i) {
         PooledSlot& e = got[i];
@@ -818,8 +856,8 @@ void reserve_slot_buffers(int device, uint32_t n, uint64_t bytes, uint64_t recor
             continue;
         }
         // (a set that failed part-way is released; the stream allocates its own slots as before)
-        if (e.h_seq) (void)hipHostFree(e.h_seq);
-        if (e.h_off) (void)hipHostFree(e.h_off);
+        pinned_free(e.h_seq);
+        pinned_free(e.h_off);
         for (void* q : {(void*)e.d_seq, (void*)e.d_off, (void*)e.d_pseq, (void*)e.d_pqual, (void*)e.d_poff, e.d_scratch})
             if (q) (void)hipFree(q);
     }
@@ -850,9 +888,11 @@ extern "C" int speq_device_warmup(int device, uint32_t streams) {
         if (streams > 16) throw std::invalid_argument("speq_device_warmup: at most 16 streams");
         {
             DevScope g(device);
+            speq::startup_trace("warm-up: runtime up");
             hip_ok(hipFree(nullptr), "hipFree");  // the device's context
+            speq::startup_trace("warm-up: context");
         }
-        // the four code objects (10-42 ms each) and the streams (~8 ms each) on threads of their own
+        // the scan's three code objects (3-10 ms each alone) and the streams (~8 ms each) on threads of their own
         std::vector<std::thread> ts;
         std::vector<std::string> err(5);
         auto run = [&](int i, void (*f)()) {
@@ -860,6 +900,9 @@ extern "C" int speq_device_warmup(int device, uint32_t streams) {
                 try {
                     DevScope g(device);
                     f();
+                    static const char* names[4] = {"warm-up: scan_kernels code", "warm-up: ax_scan code",
+                                                   "warm-up: build_gpu code", "warm-up: fastq_gpu code"};
+                    speq::startup_trace(names[i]);
                 } catch (const std::exception& x) {
                     err[i] = x.what();
                 }
@@ -867,8 +910,7 @@ extern "C" int speq_device_warmup(int device, uint32_t streams) {
         };
         run(0, speq::warm_module_scan_kernels);
         run(1, speq::warm_module_ax_scan);
-        run(2, speq::warm_module_build_gpu);
-        run(3, speq::warm_module_fastq_gpu);
+        run(3, speq::warm_module_fastq_gpu);  // (not the index builder's: a scan never runs it)
         ts.emplace_back([&] {
             try {
                 DevScope g(device);
@@ -877,6 +919,7 @@ extern "C" int speq_device_warmup(int device, uint32_t streams) {
                     std::lock_guard<std::mutex> lk(g_stream_mu);
                     g_streams->emplace(device, st);
                 }
+                speq::startup_trace("warm-up: streams");
             } catch (const std::exception& x) {
                 err[4] = x.what();
             }

@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -407,12 +408,31 @@ __device__ __forceinline__ void search_packed_n(const DevView& I, const Rsrc& R,
             throw speq::DeviceError(std::string(#expr) + ": " + hipGetErrorString(_e));                      \
     } while (0)
 
+// Host -> device copy of a pageable array. Large arrays are page-locked for the copy (hipHostRegister, ~3 ms for a
+// 377 MB index) and copied by DMA at the link rate: the runtime's staged pageable copy ran at 2-10 GB/s, 0.24 s of a
+// `speq scan` start-up (tools/upload_probe.cpp, profiles/r06/cli/). One registration at a time in the process (two
+// replicas uploading the same host arrays must not unregister under each other's copy).
+inline void upload_bytes(void* dst, const void* src, size_t bytes) {
+    static std::mutex mu;
+    if (bytes >= (4u << 20)) {
+        std::lock_guard<std::mutex> lk(mu);
+        if (hipHostRegister(const_cast<void*>(src), bytes, hipHostRegisterDefault) == hipSuccess) {
+            const hipError_t e = hipMemcpy(dst, src, bytes, hipMemcpyHostToDevice);
+            (void)hipHostUnregister(const_cast<void*>(src));
+            HIP_OK(e);
+            return;
+        }
+        (void)hipGetLastError();  // (not registered: the staged copy below)
+    }
+    HIP_OK(hipMemcpy(dst, src, bytes, hipMemcpyHostToDevice));
+}
+
 template <typename T>
 T* dev_upload(const std::vector<T>& v) {
     if (v.empty()) return nullptr;
     void* p = nullptr;
     HIP_OK(hipMalloc(&p, v.size() * sizeof(T)));
-    HIP_OK(hipMemcpy(p, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice));
+    upload_bytes(p, v.data(), v.size() * sizeof(T));
     return static_cast<T*>(p);
 }
 

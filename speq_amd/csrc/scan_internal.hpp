@@ -79,6 +79,9 @@ void* pooled_stream(int device);
 // Allocates n slot buffer sets of a FASTQ stream on `device` ahead of use (speq_stream_reserve): a fresh pipeline
 // slot of at most (bytes, records) then takes one instead of allocating (pipeline.cpp).
 void reserve_slot_buffers(int device, uint32_t n, uint64_t bytes, uint64_t records, bool paired);
+// SPEQ_STARTUP_TRACE=1 (performance investigation only): "speq-trace: <what> <seconds>" on stderr, seconds since
+// $SPEQ_T0 (ns since the epoch, set by a timing harness) or since the library was loaded
+void startup_trace(const char* what);
 uint32_t device_groups(const speq_device_index* d);
 uint64_t device_text_len(const speq_device_index* d);  // FM text length n of the replica's index
 }  // namespace speq

@@ -1222,6 +1222,40 @@ void allow_big_lds_all() {
 // The q-mer table level for a scan of k-mers: the longest of q, q-1, q-2 that leaves a number of symbols divisible
 // by the widest LF step (3 with occ3, 2 with occ2), so the search needs no leftover single/pair step; any level
 // gives the same intervals (tests/test_gpu_parity.py runs each).
+// The sparse forms of the q-mer tables (tuning "sparse_prefix" 1 or -1): per level a rank directory of 96 codes per
+// entry over the codes that occur, and their intervals. Built from the dense tables on the first tuning that asks for
+// them (a host pass over 4^q codes, 50 ms at q = 12, that every device open paid until round 6; the default dense
+// lookups never read them).
+void build_sparse(speq_device_index* d) {
+    std::lock_guard<std::mutex> lk(d->sparse_mu);
+    if (d->sparse_built) return;
+    DeviceGuard g(d->device);
+    for (int lvl = 0; lvl < 3; ++lvl) {
+        if (d->prefix_level[lvl] == nullptr || d->prefix_words[lvl] == 0) continue;
+        std::vector<uint32_t> t(d->prefix_words[lvl]);
+        HIP_OK(hipMemcpy(t.data(), d->prefix_level[lvl], t.size() * 4, hipMemcpyDeviceToHost));
+        const uint64_t Q = t.size() / 2, nbk = Q / 96 + 1;
+        std::vector<speq::OccEntry> rk(nbk, speq::OccEntry{});
+        std::vector<uint32_t> iv;
+        uint32_t cnt = 0;
+        for (uint64_t c = 0; c < Q; ++c) {
+            if (c % 96 == 0) rk[c / 96].count = cnt;
+            if (t[2 * c] < t[2 * c + 1]) {
+                rk[c / 96].bits[(c % 96) / 32] |= 1u << (c % 32);
+                iv.push_back(t[2 * c]);
+                iv.push_back(t[2 * c + 1]);
+                ++cnt;
+            }
+        }
+        if (Q % 96 == 0) rk[nbk - 1].count = cnt;
+        d->present[lvl] = cnt;
+        if (iv.empty()) iv.assign(2, 0u);
+        d->sparse_rank[lvl] = reinterpret_cast<const uint4*>(d->track(dev_upload(rk)));
+        d->sparse_iv[lvl] = reinterpret_cast<const uint2*>(d->track(dev_upload(iv)));
+    }
+    d->sparse_built = true;
+}
+
 void use_sparse(const speq_device_index* d, uint32_t lvl, DevView& v) {
     v.pfx_rank = nullptr;
     v.pfx_iv = nullptr;
@@ -1671,6 +1705,7 @@ int speq_device_open(const speq_index* idx, int device, speq_device_index** out)
         if (ndev <= 0) throw speq::DeviceError("no GPU visible (the scan path has no CPU fallback)");
         if (device < 0 || device >= ndev) throw std::invalid_argument("speq_device_open: bad device ordinal");
         DeviceGuard g(device);
+        speq::startup_trace("device open: start");
         const speq::FmIndex& fm = idx->fm;
         auto d = std::make_unique<speq_device_index>();
         d->device = device;
@@ -1689,31 +1724,9 @@ int speq_device_open(const speq_index* idx, int device, speq_device_index** out)
         d->prefix_level[0] = v.prefix;
         d->prefix_level[1] = reinterpret_cast<const uint2*>(d->track(dev_upload(fm.prefix1)));
         d->prefix_level[2] = reinterpret_cast<const uint2*>(d->track(dev_upload(fm.prefix2)));
-        {
-            const std::vector<uint32_t>* tabs[3] = {&fm.prefix, &fm.prefix1, &fm.prefix2};
-            for (int lvl = 0; lvl < 3; ++lvl) {
-                const std::vector<uint32_t>& t = *tabs[lvl];
-                if (t.empty()) continue;
-                const uint64_t Q = t.size() / 2, nbk = Q / 96 + 1;
-                std::vector<speq::OccEntry> rk(nbk, speq::OccEntry{});
-                std::vector<uint32_t> iv;
-                uint32_t cnt = 0;
-                for (uint64_t c = 0; c < Q; ++c) {
-                    if (c % 96 == 0) rk[c / 96].count = cnt;
-                    if (t[2 * c] < t[2 * c + 1]) {
-                        rk[c / 96].bits[(c % 96) / 32] |= 1u << (c % 32);
-                        iv.push_back(t[2 * c]);
-                        iv.push_back(t[2 * c + 1]);
-                        ++cnt;
-                    }
-                }
-                if (Q % 96 == 0) rk[nbk - 1].count = cnt;
-                d->present[lvl] = cnt;
-                if (iv.empty()) iv.assign(2, 0u);
-                d->sparse_rank[lvl] = reinterpret_cast<const uint4*>(d->track(dev_upload(rk)));
-                d->sparse_iv[lvl] = reinterpret_cast<const uint2*>(d->track(dev_upload(iv)));
-            }
-        }
+        for (int lvl = 0; lvl < 3; ++lvl)  // (the sparse forms are built on first use: build_sparse)
+            d->prefix_words[lvl] = (lvl == 0 ? fm.prefix : lvl == 1 ? fm.prefix1 : fm.prefix2).size();
+        speq::startup_trace("device open: FM arrays");
         v.n = (uint32_t)fm.n;
         v.q = fm.prefix_q;
         d->base_q = fm.prefix_q;
@@ -1727,6 +1740,7 @@ int speq_device_open(const speq_index* idx, int device, speq_device_index** out)
             lut[2 * q + 1] = 1.0 / lut[2 * q];  // q = 0: inf, never used (a passing window has every q > cutoff >= 0)
         }
         d->d_qlut = d->track(dev_upload(lut));
+        speq::startup_trace("device open: uploads");
         d->stream = static_cast<hipStream_t>(speq::pooled_stream(device));
         hipDeviceProp_t prop;
         HIP_OK(hipGetDeviceProperties(&prop, device));
@@ -1750,6 +1764,7 @@ int speq_device_open(const speq_index* idx, int device, speq_device_index** out)
         // sweep_triples.jsonl
         d->ilp = fm.n < (4ull << 20) ? 2u : 1u;
         allow_big_lds_all();
+        speq::startup_trace("device open: end");
         *out = d.release();
     });
 }
@@ -2145,6 +2160,7 @@ int speq_device_set_tuning(speq_device_index* d, const char* key, int64_t value)
             d->stream_lanes = (uint32_t)value;
         } else if (k == "sparse_prefix") {
             if (value < -1 || value > 1) throw std::invalid_argument("sparse_prefix must be -1 (auto), 0 or 1");
+            if (value != 0) build_sparse(d);
             d->sparse_choice = (int)value;
         } else if (k == "grid_blocks_kt") {
             if (value < 1 || value > (1 << 20)) throw std::invalid_argument("grid_blocks_kt must be in [1, 2^20]");
