@@ -4,11 +4,70 @@
 #include <algorithm>
 #include <atomic>
 #include <cmath>
+#include <condition_variable>
+#include <functional>
 #include <limits>
+#include <mutex>
 #include <thread>
 
 namespace {
 constexpr uint64_t EM_CHUNKS = 64;  // fixed row partition of speq_em_step (deterministic across machines)
+
+// Workers of speq_em_step, started once per process: a step takes 1-2 ms, and starting 16 threads for every one of
+// a run's 20-30 steps cost about as much as the sweep. run(n, f) calls f(0..n-1) on the workers and the caller.
+class StepPool {
+public:
+    explicit StepPool(uint32_t n) : workers_(n) {
+        for (uint32_t i = 0; i < n; ++i)
+            ws_.emplace_back([this] {
+                uint64_t seen = 0;
+                for (;;) {
+                    {
+                        std::unique_lock<std::mutex> lk(mu_);
+                        cv_.wait(lk, [&] { return gen_ != seen; });
+                        seen = gen_;
+                    }
+                    drain();
+                    std::lock_guard<std::mutex> lk(mu_);
+                    if (--pending_ == 0) done_.notify_all();
+                }
+            });
+    }
+    // every worker takes part in every run (so none can still be in this one when the next begins)
+    void run(uint64_t n, const std::function<void(uint64_t)>& f) {
+        std::lock_guard<std::mutex> one(run_mu_);  // (one step at a time in the process)
+        {
+            std::lock_guard<std::mutex> lk(mu_);
+            job_ = &f;
+            n_ = n;
+            next_ = 0;
+            pending_ = workers_;
+            ++gen_;
+        }
+        cv_.notify_all();
+        drain();
+        std::unique_lock<std::mutex> lk(mu_);
+        done_.wait(lk, [&] { return pending_ == 0; });
+    }
+
+private:
+    void drain() {
+        for (uint64_t i; (i = next_.fetch_add(1)) < n_;) (*job_)(i);
+    }
+    const uint32_t workers_;
+    std::vector<std::thread> ws_;  // (never joined: the pool lives until the process ends)
+    std::mutex mu_, run_mu_;
+    std::condition_variable cv_, done_;
+    const std::function<void(uint64_t)>* job_ = nullptr;
+    std::atomic<uint64_t> next_{0};
+    uint64_t n_ = 0, gen_ = 0;
+    uint32_t pending_ = 0;
+};
+
+StepPool& step_pool() {
+    static StepPool* p = new StepPool(std::min(std::max(1u, std::thread::hardware_concurrency()), 16u) - 1u);
+    return *p;
+}
 }  // namespace
 
 namespace speq {
@@ -131,18 +190,10 @@ int speq_em_step(const speq_em* em, const double* percent, const int32_t* group_
                     }
                 }
             };
-            const uint32_t hw = std::max(1u, std::thread::hardware_concurrency());
-            const uint32_t n_threads = (uint32_t)std::min<uint64_t>(std::min<uint32_t>(hw, 16u), n_chunks);
-            if (n_threads <= 1) {
-                for (uint64_t ci = 0; ci < n_chunks; ++ci) run_chunk(ci);
+            if (n_chunks <= 1) {
+                run_chunk(0);
             } else {
-                std::atomic<uint64_t> next_chunk{0};
-                std::vector<std::thread> pool;
-                for (uint32_t t = 0; t < n_threads; ++t)
-                    pool.emplace_back([&] {
-                        for (uint64_t ci; (ci = next_chunk++) < n_chunks;) run_chunk(ci);
-                    });
-                for (auto& t : pool) t.join();
+                step_pool().run(n_chunks, run_chunk);
             }
             for (uint64_t ci = 0; ci < n_chunks; ++ci)
                 for (uint32_t g = 0; g < G; ++g) next[g] += part[ci * G + g];
