@@ -4,18 +4,18 @@ import subprocess
 import sys
 import time
 
-CASES = [(0, 0, 1), (1024, 0, 1), (1024, 0, 64), (4096, 0, 16), (0, 300, 1), (1024, 300, 64)]
+CASES = [(0, 0, 1, 0), (0, 0, 1, 4), (0, 0, 1, 8), (1024, 0, 64, 0), (2048, 300, 128, 0), (2048, 300, 128, 6)]
 
 
-def once(vram, pinned, nbuf):
+def once(vram, pinned, nbuf, streams):
     t_start = time.time()
-    p = subprocess.Popen(["tools/build/exit_probe", str(vram), str(pinned), str(nbuf)], stdout=subprocess.PIPE,
-                         text=True)
+    p = subprocess.Popen(["tools/build/exit_probe", str(vram), str(pinned), str(nbuf), str(streams)],
+                         stdout=subprocess.PIPE, text=True)
     line = p.stdout.readline()
     rc = p.wait()
     t_end = time.time()
     if rc != 0 or not line.strip():
-        raise SystemExit(f"exit_probe {vram} {pinned} {nbuf}: rc {rc}")
+        raise SystemExit(f"exit_probe {vram} {pinned} {nbuf} {streams}: rc {rc}")
     t_print = int(line) * 1e-9
     return t_print - t_start, t_end - t_print
 
@@ -25,8 +25,9 @@ def main():
     for rep in range(reps):
         for c in CASES:
             run, tail = once(*c)
-            print(f"vram {c[0]:5d} MiB in {c[2]:3d} buffers, pinned {c[1]:4d} MiB: start-to-print {run * 1e3:7.1f} ms, "
-                  f"exit {tail * 1e3:7.1f} ms", flush=True)
+            print(f"vram {c[0]:5d} MiB in {c[2]:3d} buffers, pinned {c[1]:4d} MiB, {c[3]} streams: start-to-print "
+                  f"{run * 1e3:7.1f} ms, exit {tail * 1e3:7.1f} ms", flush=True)
+            time.sleep(1.0)
 
 
 if __name__ == "__main__":
