@@ -19,7 +19,7 @@ open(os.path.join(w, "groups.txt"), "w").write(ref.groupings_text())
 reads = synth.make_reads(ref, int(os.environ.get("CLI_READS", "10000000")))
 bench.write_fastq(os.path.join(w, "r1.fq"), reads)
 PY
-OUT=$GRAFT_REPO_ROOT/gpurun_out/cli_trace; mkdir -p $OUT
+OUT=${CLI_OUT:-$GRAFT_REPO_ROOT/gpurun_out/cli_trace}; mkdir -p $OUT
 cd $W
 export SPEQ_CLI_TIMING=1 SPEQ_STARTUP_TRACE=1
 timeout -k 10 120 $GRAFT_REPO_ROOT/bin/speq index -r refs.fa -g groups.txt -x ref -t 16 > $OUT/index.log 2>&1 || exit 1

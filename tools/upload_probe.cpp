@@ -30,6 +30,31 @@ int main(int argc, char** argv) {
     auto t0 = clk::now();
     OK(hipFree(nullptr));
     std::printf("runtime %.1f ms\n", ms(t0, clk::now()));
+    if (argc > 3 && std::strcmp(argv[3], "first") == 0) {
+        // the process's first host -> device copy, registered, of `mib` MiB; with argv[4] == "tiny", after one
+        // 64-byte pageable copy (does the first copy pay a one-time set-up?)
+        const bool tiny = argc > 4 && std::strcmp(argv[4], "tiny") == 0;
+        std::vector<unsigned char> h(n);
+        for (size_t i = 0; i < n; i += 4096) h[i] = (unsigned char)i;
+        void* d = nullptr;
+        OK(hipMalloc(&d, n));
+        if (tiny) {
+            auto a = clk::now();
+            OK(hipMemcpy(d, h.data(), 64, hipMemcpyHostToDevice));
+            std::printf("tiny pageable copy %.1f ms\n", ms(a, clk::now()));
+        }
+        for (int rep = 0; rep < 2; ++rep) {
+            auto a = clk::now();
+            OK(hipHostRegister(h.data(), n, hipHostRegisterDefault));
+            auto r = clk::now();
+            OK(hipMemcpy(d, h.data(), n, hipMemcpyHostToDevice));
+            auto c = clk::now();
+            OK(hipHostUnregister(h.data()));
+            std::printf("registered copy %d: register %.1f ms, copy %.1f ms (%.1f GB/s)\n", rep, ms(a, r), ms(r, c),
+                        n / 1e6 / ms(r, c));
+        }
+        return 0;
+    }
     if (argc > 3 && std::strcmp(argv[3], "alloc") == 0) {
         // pinned host memory of `mib` MiB in T threads (one buffer each): hipHostMalloc, or an aligned allocation
         // touched and then registered
