@@ -673,6 +673,12 @@ int run_scan(CmdArguments& a) {
     }
     ok(speq_em_finalize(em, a.threads), "building the EM histogram");
     phase("EM finalize");
+    if (phase.on) {
+        uint64_t rows = 0, ents = 0, wins = 0;
+        if (speq_em_info(em, &rows, &ents, &wins) == SPEQ_OK)
+            std::fprintf(stderr, "speq: EM histogram: %llu intervals, %llu (group, count) entries, %llu windows\n",
+                         (unsigned long long)rows, (unsigned long long)ents, (unsigned long long)wins);
+    }
     std::vector<uint64_t> unique(counts.begin() + 2, counts.end());
     std::vector<double> diff(G, 1.0), next(G);
     for (unsigned it = 0; G > 0 && *std::max_element(diff.begin(), diff.end()) > a.precision; ++it) {

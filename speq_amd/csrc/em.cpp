@@ -72,52 +72,71 @@ StepPool& step_pool() {
 
 namespace speq {
 
-void em_build_rows(speq_em& em, const std::vector<uint32_t>& lo, const std::vector<uint32_t>& mult,
-                          const std::vector<uint32_t>& hi, uint32_t threads) {
+void em_build_rows(speq_em& em, const uint32_t* lo, const uint32_t* mult, const uint32_t* hi, uint64_t m) {
     const FmIndex& fm = em.idx->fm;
-    const uint64_t m = lo.size();
-    if (threads == 0) threads = std::max(1u, std::thread::hardware_concurrency());
-    threads = std::max<uint32_t>(1, std::min<uint64_t>(threads, m / 4096 + 1));
+    // contiguous chunks of intervals, built on the step pool's workers and appended in chunk order (rows in lo order)
+    const uint64_t n_chunks = std::min<uint64_t>(EM_CHUNKS, std::max<uint64_t>(1, m / 2048));
     struct Part {
         std::vector<uint64_t> mult, nnz;
         std::vector<uint32_t> grp, cnt;
     };
-    std::vector<Part> parts(threads);
-    std::vector<std::thread> pool;
-    const uint64_t chunk = (m + threads - 1) / threads;
-    for (uint32_t t = 0; t < threads; ++t) {
-        pool.emplace_back([&, t] {
-            Part& P = parts[t];
-            std::vector<uint32_t> dense(em.G, 0);
-            std::vector<uint32_t> touched;
-            const uint64_t b = t * chunk, e = std::min(m, b + chunk);
-            for (uint64_t r = b; r < e; ++r) {
-                const uint64_t h = hi[r];
-                // per-group occurrence counts c_g = overlap of [lo, h) with the label runs of group g
-                for (uint64_t i = lo[r]; i < h;) {
-                    const uint64_t j = std::min<uint64_t>(fm.run_end(i), h);
-                    const uint16_t g = fm.label_at(i);
-                    if (!dense[g]) touched.push_back(g);
-                    dense[g] += (uint32_t)(j - i);
-                    i = j;
+    std::vector<Part> parts(n_chunks);
+    const bool lab = !fm.lab.empty();
+    auto build = [&](uint64_t ci) {
+        Part& P = parts[ci];
+        std::vector<uint32_t> dense(em.G, 0);
+        std::vector<uint32_t> touched;
+        const uint64_t b = m * ci / n_chunks, e = m * (ci + 1) / n_chunks;
+        P.mult.reserve(e - b);
+        P.nnz.reserve(e - b);
+        for (uint64_t r = b; r < e; ++r) {
+            const uint64_t h = hi[r];
+            // per-group occurrence counts c_g = overlap of [lo, h) with the label runs of group g; the label table
+            // gives a run's group and its distance to the run's end in one load (saturated distances: the rank path)
+            for (uint64_t i = lo[r]; i < h;) {
+                uint64_t j;
+                uint16_t g;
+                const uint32_t x = lab ? fm.lab[i] : 0u;
+                if (lab && (x >> 16) != 0xFFFFu) {
+                    g = (uint16_t)(x & 0xFFFFu);
+                    j = std::min<uint64_t>(i + (x >> 16), h);
+                } else {
+                    g = fm.label_at(i);
+                    j = std::min<uint64_t>(fm.run_end(i), h);
                 }
-                std::sort(touched.begin(), touched.end());  // the reference sums groups in index order
-                P.mult.push_back(mult[r]);
-                P.nnz.push_back(touched.size());
-                for (uint32_t g : touched) {
-                    P.grp.push_back(g);
-                    P.cnt.push_back(dense[g]);
-                    dense[g] = 0;
-                }
-                touched.clear();
+                if (!dense[g]) touched.push_back(g);
+                dense[g] += (uint32_t)(j - i);
+                i = j;
             }
-        });
+            std::sort(touched.begin(), touched.end());  // the reference sums groups in index order
+            P.mult.push_back(mult[r]);
+            P.nnz.push_back(touched.size());
+            for (uint32_t g : touched) {
+                P.grp.push_back(g);
+                P.cnt.push_back(dense[g]);
+                dense[g] = 0;
+            }
+            touched.clear();
+        }
+    };
+    if (n_chunks <= 1) {
+        build(0);
+    } else {
+        step_pool().run(n_chunks, build);
     }
-    for (auto& th : pool) th.join();
+    uint64_t rows = 0, ents = 0;
+    for (const Part& P : parts) {
+        rows += P.mult.size();
+        ents += P.grp.size();
+    }
     em.row_mult.clear();
+    em.row_mult.reserve(rows);
     em.row_ptr.assign(1, 0);
+    em.row_ptr.reserve(rows + 1);
     em.col_group.clear();
+    em.col_group.reserve(ents);
     em.col_count.clear();
+    em.col_count.reserve(ents);
     for (auto& P : parts) {
         em.row_mult.insert(em.row_mult.end(), P.mult.begin(), P.mult.end());
         for (uint64_t z : P.nnz) em.row_ptr.push_back(em.row_ptr.back() + z);

@@ -32,6 +32,5 @@ struct speq_em {
 namespace speq {
 // Builds the CSR rows (host, multi-threaded) from the positions that start a recorded interval, ascending, with their
 // multiplicities and interval ends (compacted on the GPU by speq_em_finalize): one row per interval, in position order.
-void em_build_rows(speq_em& em, const std::vector<uint32_t>& lo, const std::vector<uint32_t>& mult,
-                   const std::vector<uint32_t>& hi, uint32_t threads);
+void em_build_rows(speq_em& em, const uint32_t* lo, const uint32_t* mult, const uint32_t* hi, uint64_t m);
 }  // namespace speq
