@@ -39,13 +39,14 @@ def test_em_trajectory_matches_golden(name, mode):
     np.testing.assert_allclose(traj[-1][0], g["em"][-1]["percent"], rtol=1e-7)
 
 
-@pytest.mark.parametrize("paired", [False, True])
-def test_em_step_matches_oracle_larger(paired):
+@pytest.mark.parametrize("paired,label_table", [(False, True), (True, True), (False, False)])
+def test_em_step_matches_oracle_larger(paired, label_table):
+    # (label_table: the rows walk the label table, one load per label run; without it, the run bitvector's rank path)
     ref = synth.make_reference(5, 3, 6_000, ref_n_rate=0.001)
     reads = synth.make_reads(ref, 2_000, read_len=100, paired=paired, n_rate=0.002, lowq_rate=0.01)
     G, k, cutoff = 5, 21, 30
     counts = [3, 3, 2, 3, 1]
-    dev = DeviceIndex(FmIndex.build(ref.records, ref.groups, G, prefix_q=9, pair_steps=True, label_table=True))
+    dev = DeviceIndex(FmIndex.build(ref.records, ref.groups, G, prefix_q=9, pair_steps=True, label_table=label_table))
     em = EmHistogram(dev)
     r = em.scan(reads.seq.tobytes(), reads.qual.tobytes(), reads.offsets, k=k, phred_cutoff=cutoff, paired=paired,
                 local=True)
