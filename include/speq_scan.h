@@ -215,9 +215,11 @@ int speq_em_scan_reads(speq_em* em, const uint8_t* seq, const uint8_t* qual, con
 int speq_em_scan_reads_device(speq_em* em, const uint8_t* d_seq, const uint8_t* d_qual, const uint64_t* d_offsets,
                               uint64_t n_reads, const speq_scan_params* params, uint64_t* d_counts,
                               double* d_weights, void* stream);
-/* Downloads the histogram and builds one row per distinct interval {multiplicity, (group, count)...}. `threads` is
- * kept for the ABI: the rows are built on the library's worker pool (at most 16 threads), as the EM steps are. */
+/* Downloads the histogram and builds one row per distinct interval {multiplicity, (group, count)...}; rows of equal
+ * content are then merged (multiplicities summed). `threads` is kept for the ABI: the rows are built on the
+ * library's worker pool (at most 16 threads), as the EM steps are. */
 int speq_em_finalize(speq_em* em, uint32_t threads);
+/* Distinct intervals recorded, their (group, count) entries, and the windows (sum of multiplicities); before merging. */
 int speq_em_info(const speq_em* em, uint64_t* n_intervals, uint64_t* n_entries, uint64_t* n_windows);
 /* next[g] = sum over passing windows with hits of (c_g p_g / n_g) / sum_j (c_j p_j / n_j) (windows with a
  * non-positive sum skipped), given percent[G], group_counts[G] (the "(count)" of each groupings line) and

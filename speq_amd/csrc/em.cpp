@@ -5,10 +5,14 @@
 #include <atomic>
 #include <cmath>
 #include <condition_variable>
+#include <cstdio>
+#include <cstdlib>
 #include <functional>
 #include <limits>
 #include <mutex>
 #include <thread>
+
+#include "scan_internal.hpp"
 
 namespace {
 constexpr uint64_t EM_CHUNKS = 64;  // fixed row partition of speq_em_step (deterministic across machines)
@@ -71,6 +75,94 @@ StepPool& step_pool() {
 }  // namespace
 
 namespace speq {
+
+// Rows with the same (group, count) entries — k-mers whose occurrences lie in the same texts — contribute the same
+// function of the step's percentages times their multiplicity, so they are merged into the first of them with the
+// multiplicities summed (the sums then differ from row-by-row ones by fp64 re-association only). Row order: first
+// occurrence. SPEQ_EM_MERGE_ROWS=0 keeps every interval's row (A/B).
+void merge_equal_rows(speq_em& em) {
+    const char* e = std::getenv("SPEQ_EM_MERGE_ROWS");
+    const uint64_t R = em.row_mult.size();
+    if ((e && e[0] == '0') || R < 2) return;
+    std::vector<uint64_t> h(R);
+    const uint64_t n_chunks = std::min<uint64_t>(EM_CHUNKS, std::max<uint64_t>(1, R / 2048));
+    auto hash_rows = [&](uint64_t ci) {
+        for (uint64_t r = R * ci / n_chunks; r < R * (ci + 1) / n_chunks; ++r) {
+            uint64_t x = 0x9E3779B97F4A7C15ull ^ (em.row_ptr[r + 1] - em.row_ptr[r]);
+            for (uint64_t i = em.row_ptr[r]; i < em.row_ptr[r + 1]; ++i) {
+                x ^= ((uint64_t)em.col_group[i] << 32) | em.col_count[i];
+                x *= 0xFF51AFD7ED558CCDull;
+                x ^= x >> 29;
+            }
+            h[r] = x;
+        }
+    };
+    if (n_chunks <= 1) hash_rows(0);
+    else step_pool().run(n_chunks, hash_rows);
+    auto same = [&](uint64_t a, uint64_t b) {
+        const uint64_t na = em.row_ptr[a + 1] - em.row_ptr[a];
+        if (na != em.row_ptr[b + 1] - em.row_ptr[b]) return false;
+        return std::equal(em.col_group.begin() + em.row_ptr[a], em.col_group.begin() + em.row_ptr[a + 1],
+                          em.col_group.begin() + em.row_ptr[b]) &&
+               std::equal(em.col_count.begin() + em.row_ptr[a], em.col_count.begin() + em.row_ptr[a + 1],
+                          em.col_count.begin() + em.row_ptr[b]);
+    };
+    // open addressing over the hashes: slot -> 1 + the first row with that content. First by hash alone, each row's
+    // representative then checked entry by entry (in parallel); a hash collision between different contents (never
+    // seen) redoes the assignment comparing entries.
+    uint64_t cap = 1;
+    while (cap < 2 * R) cap <<= 1;
+    std::vector<uint64_t> rep(R);
+    uint64_t distinct = 0;
+    auto assign = [&](bool exact) {
+        std::vector<uint64_t> slot(cap, 0);
+        distinct = 0;
+        for (uint64_t r = 0; r < R; ++r) {
+            for (uint64_t s = h[r] & (cap - 1);; s = (s + 1) & (cap - 1)) {
+                if (slot[s] == 0) {
+                    slot[s] = r + 1;
+                    rep[r] = r;
+                    ++distinct;
+                    break;
+                }
+                const uint64_t q = slot[s] - 1;
+                if (h[q] == h[r] && (!exact || same(q, r))) {
+                    rep[r] = q;
+                    break;
+                }
+            }
+        }
+    };
+    assign(false);
+    std::atomic<bool> collided{false};
+    auto verify = [&](uint64_t ci) {
+        for (uint64_t r = R * ci / n_chunks; r < R * (ci + 1) / n_chunks; ++r)
+            if (rep[r] != r && !same(rep[r], r)) collided = true;
+    };
+    if (n_chunks <= 1) verify(0);
+    else step_pool().run(n_chunks, verify);
+    if (collided) assign(true);
+    if (distinct == R) return;
+    std::vector<uint64_t> at(R), mult, ptr(1, 0);
+    std::vector<uint32_t> grp, cnt;
+    mult.reserve(distinct);
+    ptr.reserve(distinct + 1);
+    for (uint64_t r = 0; r < R; ++r) {
+        if (rep[r] != r) {
+            mult[at[rep[r]]] += em.row_mult[r];
+            continue;
+        }
+        at[r] = mult.size();
+        mult.push_back(em.row_mult[r]);
+        grp.insert(grp.end(), em.col_group.begin() + em.row_ptr[r], em.col_group.begin() + em.row_ptr[r + 1]);
+        cnt.insert(cnt.end(), em.col_count.begin() + em.row_ptr[r], em.col_count.begin() + em.row_ptr[r + 1]);
+        ptr.push_back(grp.size());
+    }
+    em.row_mult.swap(mult);
+    em.row_ptr.swap(ptr);
+    em.col_group.swap(grp);
+    em.col_count.swap(cnt);
+}
 
 void em_build_rows(speq_em& em, const uint32_t* lo, const uint32_t* mult, const uint32_t* hi, uint64_t m) {
     const FmIndex& fm = em.idx->fm;
@@ -143,6 +235,13 @@ void em_build_rows(speq_em& em, const uint32_t* lo, const uint32_t* mult, const 
         em.col_group.insert(em.col_group.end(), P.grp.begin(), P.grp.end());
         em.col_count.insert(em.col_count.end(), P.cnt.begin(), P.cnt.end());
     }
+    em.n_intervals = em.row_mult.size();
+    em.n_entries = em.col_group.size();
+    merge_equal_rows(em);
+    char msg[96];
+    std::snprintf(msg, sizeof msg, "em rows: %llu intervals -> %llu rows",
+                  (unsigned long long)em.n_intervals, (unsigned long long)em.row_mult.size());
+    startup_trace(msg);
     em.finalized = true;
 }
 
@@ -153,8 +252,8 @@ extern "C" {
 int speq_em_info(const speq_em* em, uint64_t* n_intervals, uint64_t* n_entries, uint64_t* n_windows) {
     return speq::guarded([&] {
         if (!em || !em->finalized) throw std::invalid_argument("speq_em_info: histogram not finalized");
-        if (n_intervals) *n_intervals = em->row_mult.size();
-        if (n_entries) *n_entries = em->col_group.size();
+        if (n_intervals) *n_intervals = em->n_intervals;
+        if (n_entries) *n_entries = em->n_entries;
         if (n_windows) {
             uint64_t s = 0;
             for (uint64_t m : em->row_mult) s += m;
@@ -188,7 +287,7 @@ int speq_em_step(const speq_em* em, const double* percent, const int32_t* group_
             // Rows are split into a FIXED number of contiguous chunks (independent of the machine's thread count),
             // each summed into its own vector, and the chunk vectors are added in chunk order: the result is
             // deterministic, and differs from a serial sweep only by fp64 re-association (tests: rtol 1e-9).
-            const uint64_t n_chunks = std::min<uint64_t>(EM_CHUNKS, std::max<uint64_t>(1, R / 4096));
+            const uint64_t n_chunks = std::min<uint64_t>(EM_CHUNKS, std::max<uint64_t>(1, em->col_group.size() / 16384));
             std::vector<double> part(n_chunks * G, 0.0);
             auto run_chunk = [&](uint64_t ci) {
                 const uint64_t r0 = R * ci / n_chunks, r1 = R * (ci + 1) / n_chunks;

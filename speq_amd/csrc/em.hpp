@@ -22,7 +22,10 @@ struct speq_em {
     uint32_t* d_mult = nullptr;  // device: per SA position, # multi-group windows whose interval starts there
     uint32_t* d_hi = nullptr;    // device: end of that interval
     bool finalized = false;
-    // CSR rows, one per distinct multi-group interval: multiplicity, then (group, count) entries by group id
+    uint64_t n_intervals = 0;  // distinct multi-group intervals recorded (rows before equal rows are merged)
+    uint64_t n_entries = 0;    // their (group, count) entries
+    // CSR rows, one per distinct (group, count) content of the intervals (equal rows merged, multiplicities summed):
+    // multiplicity, then (group, count) entries by group id
     std::vector<uint64_t> row_mult;
     std::vector<uint64_t> row_ptr;
     std::vector<uint32_t> col_group;
@@ -33,4 +36,6 @@ namespace speq {
 // Builds the CSR rows (host, multi-threaded) from the positions that start a recorded interval, ascending, with their
 // multiplicities and interval ends (compacted on the GPU by speq_em_finalize): one row per interval, in position order.
 void em_build_rows(speq_em& em, const uint32_t* lo, const uint32_t* mult, const uint32_t* hi, uint64_t m);
+// Merges rows of equal content (em.cpp); em_build_rows calls it
+void merge_equal_rows(speq_em& em);
 }  // namespace speq
