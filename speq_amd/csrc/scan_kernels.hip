@@ -1902,13 +1902,14 @@ int speq_em_finalize(speq_em* em, uint32_t threads) {
                 hipLaunchKernelGGL(k_em_compact, dim3(nb), dim3(256), 0, st, em->d_mult, em->d_hi, n, d_cnt, d_out,
                                    d_out + nnz, d_out + 2ull * nnz);
                 HIP_OK(hipGetLastError());
+                // (the compaction first, then a synchronous copy: an asynchronous device-to-host copy on the
+                // replica's stream paid about 8 ms of first-use cost in a `speq scan` process, this one 0.1 ms)
+                HIP_OK(hipStreamSynchronize(st));
                 const bool reg = hipHostRegister(tri.get(), (uint64_t)nnz * 12, hipHostRegisterDefault) == hipSuccess;
                 if (!reg) (void)hipGetLastError();
-                const hipError_t ce = hipMemcpyAsync(tri.get(), d_out, (uint64_t)nnz * 12, hipMemcpyDeviceToHost, st);
-                const hipError_t se = hipStreamSynchronize(st);
+                const hipError_t ce = hipMemcpy(tri.get(), d_out, (uint64_t)nnz * 12, hipMemcpyDeviceToHost);
                 if (reg) (void)hipHostUnregister(tri.get());
                 HIP_OK(ce);
-                HIP_OK(se);
             }
             (void)hipFree(d_cnt);
             if (d_out) (void)hipFree(d_out);

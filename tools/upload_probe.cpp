@@ -8,6 +8,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <memory>
 #include <thread>
 #include <vector>
 
@@ -30,6 +31,25 @@ int main(int argc, char** argv) {
     auto t0 = clk::now();
     OK(hipFree(nullptr));
     std::printf("runtime %.1f ms\n", ms(t0, clk::now()));
+    if (argc > 3 && std::strcmp(argv[3], "d2h") == 0) {
+        // the process's first device -> host copies of `mib` MiB into registered memory (after one host -> device
+        // copy, as in a scan), three in a row
+        std::vector<unsigned char> h(n);
+        void* d = nullptr;
+        OK(hipMalloc(&d, n));
+        OK(hipMemcpy(d, h.data(), n, hipMemcpyHostToDevice));
+        for (int rep = 0; rep < 3; ++rep) {
+            std::unique_ptr<unsigned char[]> o(new unsigned char[n]);
+            auto a = clk::now();
+            OK(hipHostRegister(o.get(), n, hipHostRegisterDefault));
+            auto r = clk::now();
+            OK(hipMemcpy(o.get(), d, n, hipMemcpyDeviceToHost));
+            auto c = clk::now();
+            OK(hipHostUnregister(o.get()));
+            std::printf("d2h %d: register %.2f ms, copy %.2f ms\n", rep, ms(a, r), ms(r, c));
+        }
+        return 0;
+    }
     if (argc > 3 && std::strcmp(argv[3], "first") == 0) {
         // the process's first host -> device copy, registered, of `mib` MiB; with argv[4] == "tiny", after one
         // 64-byte pageable copy (does the first copy pay a one-time set-up?)
