@@ -19,6 +19,7 @@
 #include <map>
 #include <memory>
 #include <mutex>
+#include <set>
 #include <string>
 #include <thread>
 #include <vector>
@@ -67,21 +68,39 @@ struct Slot {
 // Pinned host memory of the slots: an aligned allocation, touched, then page-locked with hipHostRegister — 300 MB in
 // 16 threads take 9-11 ms this way against 64-69 ms of hipHostMalloc (tools/upload_probe.cpp alloc,
 // profiles/r06/cli/), and the copies from it run at the same DMA rate.
+// Where registration is refused (a host whose page-locking limits differ from the GPU box's), hipHostMalloc;
+// SPEQ_PINNED=hostmalloc takes that path always (tests).
+std::mutex g_pinned_mu;
+auto* g_host_malloced = new std::set<void*>();
+
 void* pinned_alloc(size_t bytes) {
     const size_t n = (std::max<size_t>(bytes, 1) + 4095) & ~size_t(4095);
-    void* p = std::aligned_alloc(4096, n);
-    if (!p) throw std::bad_alloc();
-    std::memset(p, 0, n);
-    const hipError_t e = hipHostRegister(p, n, hipHostRegisterDefault);
-    if (e != hipSuccess) {
+    const char* mode = std::getenv("SPEQ_PINNED");
+    void* p = nullptr;
+    if (!(mode && std::strcmp(mode, "hostmalloc") == 0)) {
+        p = std::aligned_alloc(4096, n);
+        if (!p) throw std::bad_alloc();
+        std::memset(p, 0, n);
+        if (hipHostRegister(p, n, hipHostRegisterDefault) == hipSuccess) return p;
+        (void)hipGetLastError();
         std::free(p);
-        hip_ok(e, "hipHostRegister");
+        p = nullptr;
     }
+    hip_ok(hipHostMalloc(&p, n, hipHostMallocDefault), "hipHostMalloc");
+    std::lock_guard<std::mutex> lk(g_pinned_mu);
+    g_host_malloced->insert(p);
     return p;
 }
 
 void pinned_free(void* p) {
     if (!p) return;
+    {
+        std::lock_guard<std::mutex> lk(g_pinned_mu);
+        if (g_host_malloced->erase(p)) {
+            (void)hipHostFree(p);
+            return;
+        }
+    }
     (void)hipHostUnregister(p);
     std::free(p);
 }

@@ -70,6 +70,23 @@ def test_scan_fastq_matches_golden(tmp_path, name, gz):
             assert st["records"] == len(c.offsets) - 1
 
 
+@pytest.mark.parametrize("pinned", ["register", "hostmalloc"])
+def test_slot_memory_registered_or_host_malloced(tmp_path, monkeypatch, pinned):
+    """The slots' page-locked host memory (registered aligned allocations, or hipHostMalloc where registration is
+    refused: SPEQ_PINNED=hostmalloc) gives the in-memory scan's counters."""
+    monkeypatch.setenv("SPEQ_PINNED", pinned)
+    ref = synth.make_reference(3, 2, 15_000)
+    reads = synth.make_reads(ref, 60_000, n_rate=0.001, lowq_rate=0.005)
+    dev = DeviceIndex(FmIndex.build(ref.records, ref.groups, 3, prefix_q=9))  # (a new replica: new slots)
+    seqs, quals = split(reads)
+    write_fastq(tmp_path / "r1.fq", seqs, quals)
+    for local in (False, True):
+        exp = dev.scan(reads.seq.tobytes(), reads.qual.tobytes(), reads.offsets, k=21, local=local)
+        got, st = dev.scan_fastq(str(tmp_path / "r1.fq"), None, k=21, local=local, threads=4)
+        same(got, exp, local)
+        assert st["records"] == reads.n
+
+
 @pytest.mark.parametrize("fmt", [dict(), dict(wrap=37, crlf=True, blank=True), dict(gz=True, wrap=60),
                                  dict(crlf=True), dict(gz=True)])
 @pytest.mark.parametrize("paired", [False, True])
