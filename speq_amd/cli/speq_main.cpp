@@ -517,8 +517,9 @@ int run_scan(CmdArguments& a) {
     // profiles/r06/cli_trace_*). Failures here are left to speq_device_open / the stream to report.
     // (device open needs only the runtime: it runs beside what is left of the warm-up, joined before the stream)
     std::vector<std::thread> warm;
+    // (7 streams: the replica's, the FASTQ stream's copy stream and its 5 compute lanes, set below)
     for (int dv : devs) {
-        warm.emplace_back([dv] { (void)speq_device_warmup(dv, 5); });
+        warm.emplace_back([dv] { (void)speq_device_warmup(dv, 7); });
         if (n_dev == 1) warm.emplace_back([dv, paired, threads = a.threads] { (void)speq_stream_reserve(dv, threads, paired); });
     }
     struct Joiner {
@@ -553,6 +554,25 @@ int run_scan(CmdArguments& a) {
             if (rcs[i] != SPEQ_OK) throw CApiError("opening GPU " + std::to_string(devs[i]) + ": " + msgs[i]);
     }
     speq_device_index* d = ds[0];
+    // A whole FASTQ file keeps more blocks in flight than the library default's 3 compute lanes carry: config 3's
+    // 3.16 GB stream takes 0.127-0.134 s with 4-5 lanes against 0.145-0.147 s with 3 (profiles/r06/cli/lanes.txt;
+    // the bench's 316 MB fastq_e2e is within noise of 3 either way)
+    for (speq_device_index* x : ds) ok(speq_device_set_tuning(x, "stream_lanes", 5), "setting the stream lanes");
+    // SPEQ_TUNE="key=value,..." (performance investigation only): launch tunings of every replica
+    // (speq_device_set_tuning; results never depend on them)
+    if (const char* tv = std::getenv("SPEQ_TUNE"); tv && *tv) {
+        std::string spec(tv);
+        size_t at = 0;
+        while (at < spec.size()) {
+            const size_t end = std::min(spec.find(',', at), spec.size());
+            const std::string kv = spec.substr(at, end - at);
+            const size_t eq = kv.find('=');
+            if (eq == std::string::npos) throw CApiError("SPEQ_TUNE: expected key=value, got '" + kv + "'");
+            for (speq_device_index* x : ds)
+                ok(speq_device_set_tuning(x, kv.substr(0, eq).c_str(), std::stoll(kv.substr(eq + 1))), "SPEQ_TUNE");
+            at = end + 1;
+        }
+    }
     phase("device open");
     for (auto& t : warm) t.join();
     phase("GPU warm-up (rest)");
