@@ -10,10 +10,6 @@
 // Replaces the per-record split of seqan3::sequence_file_input (/root/reference/src/fm_scanner.cpp:138-141).
 #include <hip/hip_runtime.h>
 
-#include <cstring>  // rocprim/iterator/texture_cache_iterator.hpp uses ::memset
-
-#include <rocprim/rocprim.hpp>
-
 #include <algorithm>
 #include <cstdint>
 #include <string>
@@ -199,6 +195,87 @@ __global__ void k_add_total(const uint64_t* __restrict__ off_end, unsigned long 
     atomicAdd(total, (unsigned long long)*off_end);
 }
 
+// Exclusive scan of n items (the newline counts of a block's 4 KiB spans; the record lengths), out of place, in two
+// launches: each 2,048-item tile's sum, then every tile scanned after adding the sums of the tiles before it (a block
+// adds those itself: a FASTQ block has at most a few dozen tiles). Until round 6 rocPRIM's scan: its 480 kernel
+// instantiations made this file's code object load 3-5 ms (and up to 12 ms more under the start-up's contention)
+// where the scan needs two kernels.
+constexpr uint32_t SCAN_THREADS = 256, SCAN_ITEMS = 8, SCAN_TILE = SCAN_THREADS * SCAN_ITEMS;
+
+template <typename T>
+__global__ __launch_bounds__(SCAN_THREADS) void k_tile_sums(const T* __restrict__ in, uint64_t n, T* __restrict__ sums) {
+    __shared__ T part[SCAN_THREADS / 64];
+    const uint64_t t0 = (uint64_t)blockIdx.x * SCAN_TILE;
+    T x = 0;
+    for (uint32_t i = threadIdx.x; i < SCAN_TILE; i += SCAN_THREADS) x += t0 + i < n ? in[t0 + i] : T(0);
+    for (int o = 32; o > 0; o >>= 1) x += __shfl_down(x, o);
+    if ((threadIdx.x & 63u) == 0) part[threadIdx.x >> 6] = x;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        T t = 0;
+        for (uint32_t w = 0; w < SCAN_THREADS / 64; ++w) t += part[w];
+        sums[blockIdx.x] = t;
+    }
+}
+
+template <typename T>
+__global__ __launch_bounds__(SCAN_THREADS) void k_tile_scan(const T* __restrict__ in, T* __restrict__ out, uint64_t n,
+                                                            const T* __restrict__ sums) {
+    __shared__ T part[SCAN_THREADS / 64];
+    __shared__ T base;
+    const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
+    // the sums of the tiles before this one
+    T b = 0;
+    for (uint32_t i = threadIdx.x; i < blockIdx.x; i += SCAN_THREADS) b += sums[i];
+    for (int o = 32; o > 0; o >>= 1) b += __shfl_down(b, o);
+    if (lane == 0) part[w] = b;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        T t = 0;
+        for (uint32_t q = 0; q < SCAN_THREADS / 64; ++q) t += part[q];
+        base = t;
+    }
+    __syncthreads();
+    // this thread's SCAN_ITEMS consecutive items
+    const uint64_t i0 = (uint64_t)blockIdx.x * SCAN_TILE + (uint64_t)threadIdx.x * SCAN_ITEMS;
+    T v[SCAN_ITEMS];
+    T tot = 0;
+#pragma unroll
+    for (uint32_t j = 0; j < SCAN_ITEMS; ++j) {
+        v[j] = i0 + j < n ? in[i0 + j] : T(0);
+        tot += v[j];
+    }
+    // exclusive prefix of the thread totals: within the wave, then over the waves
+    T x = tot;
+    for (uint32_t o = 1; o < 64; o <<= 1) {
+        const T y = __shfl_up(x, o);
+        if (lane >= o) x += y;
+    }
+    __syncthreads();  // (part is reused)
+    if (lane == 63) part[w] = x;
+    __syncthreads();
+    T run = base + x - tot;
+    for (uint32_t q = 0; q < w; ++q) run += part[q];
+#pragma unroll
+    for (uint32_t j = 0; j < SCAN_ITEMS; ++j) {
+        if (i0 + j < n) out[i0 + j] = run;
+        run += v[j];
+    }
+}
+
+inline uint64_t scan_tiles(uint64_t n) { return (n + SCAN_TILE - 1) / SCAN_TILE; }
+
+// out[i] = in[0] + ... + in[i - 1]; `sums` holds scan_tiles(n) items
+template <typename T>
+void exclusive_scan(const T* in, T* out, uint64_t n, T* sums, hipStream_t st) {
+    if (n == 0) return;
+    const uint32_t tiles = (uint32_t)scan_tiles(n);
+    k_tile_sums<T><<<tiles, SCAN_THREADS, 0, st>>>(in, n, sums);
+    FHIP(hipGetLastError());
+    k_tile_scan<T><<<tiles, SCAN_THREADS, 0, st>>>(in, out, n, sums);
+    FHIP(hipGetLastError());
+}
+
 inline uint32_t grid(uint64_t n, uint32_t bs = 256) { return (uint32_t)((n + bs - 1) / bs); }
 inline uint64_t align16(uint64_t x) { return (x + 15) & ~uint64_t(15); }
 
@@ -224,14 +301,10 @@ Layout layout(uint64_t raw_bytes, uint64_t n_slots, uint64_t n_lines, size_t tem
     return L;
 }
 
+// the scans' tile sums (8 B each: the record-length scan's are u64)
 size_t temp_need(uint64_t raw_bytes, uint64_t n_slots) {
-    size_t a = 0, b = 0;
     const uint64_t chunks = nl_groups(raw_bytes) + 2;
-    (void)rocprim::exclusive_scan(nullptr, a, (uint32_t*)nullptr, (uint32_t*)nullptr, 0u, (size_t)chunks,
-                                  rocprim::plus<uint32_t>());
-    (void)rocprim::exclusive_scan(nullptr, b, (uint64_t*)nullptr, (uint64_t*)nullptr, uint64_t(0),
-                                  (size_t)(n_slots + 1), rocprim::plus<uint64_t>());
-    return std::max(a, b);
+    return (size_t)std::max(scan_tiles(chunks), scan_tiles(n_slots + 1)) * 8;
 }
 
 }  // namespace
@@ -359,10 +432,9 @@ void launch_fastq_parse(const uint8_t* d_raw, uint64_t len1, uint64_t len2, uint
         const uint32_t groups = (uint32_t)((end - a0 + NL_SPAN - 1) / NL_SPAN + (end == a0));
         k_count_nl<<<groups, NL_THREADS, 0, st>>>(d_raw, a0, begin, end, counts);
         FHIP(hipGetLastError());
-        size_t need = tn;
         // groups + 1 entries: the last exclusive sum is the total newline count
         FHIP(hipMemsetAsync(counts + groups, 0, 4, st));
-        FHIP(rocprim::exclusive_scan(temp, need, counts, offs, 0u, (size_t)groups + 1, rocprim::plus<uint32_t>(), st));
+        exclusive_scan<uint32_t>(counts, offs, (uint64_t)groups + 1, static_cast<uint32_t*>(temp), st);
         FHIP(hipMemcpyAsync(n_nl, offs + groups, 4, hipMemcpyDeviceToDevice, st));
         k_write_nl<<<groups, NL_THREADS, 0, st>>>(d_raw, a0, begin, end, offs, nl, (uint32_t)(4 * n + 1));
         FHIP(hipGetLastError());
@@ -371,10 +443,8 @@ void launch_fastq_parse(const uint8_t* d_raw, uint64_t len1, uint64_t len2, uint
                                                  paired ? 2u : 1u, rec, lens, d_err);
         FHIP(hipGetLastError());
     }
-    size_t need = tn;
     FHIP(hipMemsetAsync(lens + n_slots, 0, 8, st));
-    FHIP(rocprim::exclusive_scan(temp, need, lens, d_off, uint64_t(0), (size_t)(n_slots + 1),
-                                 rocprim::plus<uint64_t>(), st));
+    exclusive_scan<uint64_t>(lens, d_off, n_slots + 1, static_cast<uint64_t*>(temp), st);
     k_copy<<<grid(n_slots * 64u), 256, 0, st>>>(d_raw, rec, d_off, (uint32_t)n_slots, d_seq, d_qual);
     FHIP(hipGetLastError());
     if (d_total_bases) {
